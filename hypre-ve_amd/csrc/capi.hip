@@ -1,0 +1,961 @@
+// extern "C" entry points of libhypreve.so (declared in include/hypreve.h).
+// Each function keeps the reference's name, argument meaning and return
+// convention (hypre_error_flag: 0 on success, error bits otherwise).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/hypreve.h"
+#include "device/runtime.hpp"
+#include "host/hve_host.hpp"
+#include "host/layout.hpp"
+
+using namespace hve;
+
+// ---------------------------------------------------------------------------
+// object layouts
+// ---------------------------------------------------------------------------
+struct hypreve_comm_struct {
+  int rank = 0, size = 1;
+  void* nccl = nullptr;
+};
+
+struct hypre_ParVector_struct {
+  HYPRE_Comm comm = nullptr;
+  HYPRE_BigInt global_size = 0, first = 0;
+  int n = 0;
+  double* d = nullptr;
+  bool owns = true;
+};
+
+struct hypre_ParCSRMatrix_struct {
+  HYPRE_Comm comm = nullptr;
+  HYPRE_BigInt global_rows = 0, first_row = 0, global_cols = 0, first_col = 0;
+  int n = 0;
+  CSR diag;         // host local block, local columns, diagonal first
+  DevSell dA;       // device copy (SELL-64) used by Matvec
+  bool dev = false;
+  void ensure_device() {
+    if (!dev) { dA.upload(diag); dev = true; }
+  }
+};
+
+struct hypre_IJMatrix_struct {
+  HYPRE_Comm comm = nullptr;
+  HYPRE_BigInt ilower = 0, iupper = -1, jlower = 0, jupper = -1;
+  std::vector<std::vector<std::pair<int, double>>> rows;
+  HYPRE_ParCSRMatrix par = nullptr;
+};
+
+struct hypre_IJVector_struct {
+  HYPRE_Comm comm = nullptr;
+  HYPRE_BigInt jlower = 0, jupper = -1;
+  std::vector<double> h;
+  HYPRE_ParVector par = nullptr;
+};
+
+enum SolverKind { KIND_AMG = 1, KIND_PCG = 2 };
+
+struct hypre_Solver_struct {
+  int kind = 0;
+  // AMG
+  AMGParams prm;
+  Hierarchy H;
+  std::unique_ptr<DevAMG> dev;
+  int iters = 0;
+  double rel_res = 0.0;
+  bool use_graph = true;
+  bool user_num_blocks = false;
+  // PCG
+  PCGParams pcg;
+  HYPRE_Solver precond = nullptr;
+  HYPRE_PtrToParSolverFcn precond_solve = nullptr, precond_setup = nullptr;
+  std::unique_ptr<DevAMG> ws;
+};
+
+// ---------------------------------------------------------------------------
+// error state (utilities/hypre_error.c semantics)
+// ---------------------------------------------------------------------------
+static thread_local int g_error = 0;
+static thread_local std::string g_msg;
+static int g_memloc = HYPRE_MEMORY_HOST;
+static hipStream_t g_stream = nullptr;
+
+static hipStream_t lib_stream() {
+  if (!g_stream) HVE_HIP(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
+  return g_stream;
+}
+static int set_err(int code, const std::string& m) {
+  g_error |= code;
+  g_msg = m;
+  return g_error;
+}
+#define API_BEGIN try {
+#define API_END                                              \
+  }                                                          \
+  catch (const std::exception& e) {                          \
+    return set_err(HYPRE_ERROR_GENERIC, e.what());           \
+  }                                                          \
+  catch (...) {                                              \
+    return set_err(HYPRE_ERROR_GENERIC, "unknown exception"); \
+  }                                                          \
+  return g_error;
+#define CHECK_ARG(c, i) \
+  if (!(c)) return set_err(HYPRE_ERROR_ARG | ((i) << 3), "invalid argument " #i);
+
+template <typename T>
+static std::vector<T> host_copy(const T* p, size_t n) {
+  std::vector<T> v(n);
+  if (!n) return v;
+  if (g_memloc == HYPRE_MEMORY_DEVICE) HVE_HIP(hipMemcpy(v.data(), p, n * sizeof(T), hipMemcpyDeviceToHost));
+  else std::memcpy(v.data(), p, n * sizeof(T));
+  return v;
+}
+
+extern "C" {
+
+// ---------------------------------------------------------------------------
+// utilities
+// ---------------------------------------------------------------------------
+HYPRE_Int HYPRE_Init(void) {
+  API_BEGIN
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    return set_err(HYPRE_ERROR_GENERIC, "no HIP device: the hypre-ve_amd solve path runs only on the GPU");
+  lib_stream();
+  API_END
+}
+HYPRE_Int HYPRE_Finalize(void) {
+  if (g_stream) { hipStreamDestroy(g_stream); g_stream = nullptr; }
+  return 0;
+}
+HYPRE_Int HYPRE_SetMemoryLocation(HYPRE_Int loc) {
+  CHECK_ARG(loc == HYPRE_MEMORY_HOST || loc == HYPRE_MEMORY_DEVICE, 1);
+  g_memloc = loc;
+  return 0;
+}
+HYPRE_Int HYPRE_GetError(void) { return g_error; }
+HYPRE_Int HYPRE_ClearAllErrors(void) { g_error = 0; g_msg.clear(); return 0; }
+HYPRE_Int HYPRE_CheckError(HYPRE_Int ierr, HYPRE_Int code) { return ierr & code; }
+const char* hypreve_LastErrorMessage(void) { return g_msg.c_str(); }
+const char* hypreve_BuildInfo(void) {
+  return "hypre-ve_amd: BoomerAMG solve path for gfx950 (SELL-64 lane-per-row operators, f64, "
+         "no FMA contraction; host setup PMIS/ext+i/RAP)";
+}
+HYPRE_Int hypreve_DeviceSynchronize(void) {
+  API_BEGIN
+  HVE_HIP(hipDeviceSynchronize());
+  API_END
+}
+
+// ---------------------------------------------------------------------------
+// communicators (RCCL wiring lives in comm.hip; single-GPU here)
+// ---------------------------------------------------------------------------
+HYPRE_Int hypreve_CommDestroy(HYPRE_Comm comm) {
+  delete comm;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// ParVector
+// ---------------------------------------------------------------------------
+static HYPRE_ParVector new_vector(HYPRE_Comm comm, HYPRE_BigInt global, HYPRE_BigInt first, int n) {
+  auto* v = new hypre_ParVector_struct;
+  v->comm = comm;
+  v->global_size = global;
+  v->first = first;
+  v->n = n;
+  return v;
+}
+static void vec_alloc(HYPRE_ParVector v) {
+  if (!v->d) {
+    HVE_HIP(hipMalloc((void**)&v->d, sizeof(double) * std::max(1, v->n)));
+    HVE_HIP(hipMemset(v->d, 0, sizeof(double) * std::max(1, v->n)));
+  }
+}
+
+HYPRE_Int HYPRE_ParVectorCreate(HYPRE_Comm comm, HYPRE_BigInt global_size, HYPRE_BigInt* partitioning,
+                                HYPRE_ParVector* vector) {
+  CHECK_ARG(vector, 4);
+  HYPRE_BigInt first = 0, last = global_size;
+  if (partitioning) { first = partitioning[0]; last = partitioning[1]; }
+  *vector = new_vector(comm, global_size, first, (int)(last - first));
+  return 0;
+}
+HYPRE_Int HYPRE_ParVectorInitialize(HYPRE_ParVector v) {
+  CHECK_ARG(v, 1);
+  API_BEGIN
+  vec_alloc(v);
+  API_END
+}
+HYPRE_Int HYPRE_ParVectorDestroy(HYPRE_ParVector v) {
+  if (!v) return 0;
+  if (v->d && v->owns) hipFree(v->d);
+  delete v;
+  return 0;
+}
+HYPRE_Int HYPRE_ParVectorSetConstantValues(HYPRE_ParVector v, HYPRE_Complex value) {
+  CHECK_ARG(v, 1);
+  API_BEGIN
+  vec_alloc(v);
+  HVE_HIP(launch_set(v->n, value, v->d, lib_stream()));
+  HVE_HIP(hipStreamSynchronize(lib_stream()));
+  API_END
+}
+HYPRE_Int HYPRE_ParVectorCopy(HYPRE_ParVector x, HYPRE_ParVector y) {
+  CHECK_ARG(x && y && x->n == y->n, 1);
+  API_BEGIN
+  vec_alloc(y);
+  HVE_HIP(launch_copy(x->n, x->d, y->d, lib_stream()));
+  HVE_HIP(hipStreamSynchronize(lib_stream()));
+  API_END
+}
+HYPRE_Int HYPRE_ParVectorScale(HYPRE_Complex value, HYPRE_ParVector x) {
+  CHECK_ARG(x, 2);
+  API_BEGIN
+  HVE_HIP(launch_scale(x->n, nullptr, value, x->d, lib_stream()));
+  HVE_HIP(hipStreamSynchronize(lib_stream()));
+  API_END
+}
+HYPRE_Int HYPRE_ParVectorAxpy(HYPRE_Complex alpha, HYPRE_ParVector x, HYPRE_ParVector y) {
+  CHECK_ARG(x && y && x->n == y->n, 2);
+  API_BEGIN
+  HVE_HIP(launch_axpy(x->n, nullptr, alpha, 1.0, x->d, y->d, lib_stream()));
+  HVE_HIP(hipStreamSynchronize(lib_stream()));
+  API_END
+}
+
+static double* g_dot_part = nullptr;
+static double* g_dot_out = nullptr;
+HYPRE_Int HYPRE_ParVectorInnerProd(HYPRE_ParVector x, HYPRE_ParVector y, HYPRE_Real* prod) {
+  CHECK_ARG(x && y && x->n == y->n, 1);
+  CHECK_ARG(prod, 3);
+  API_BEGIN
+  if (!g_dot_part) {
+    HVE_HIP(hipMalloc((void**)&g_dot_part, 1024 * sizeof(double)));
+    HVE_HIP(hipMalloc((void**)&g_dot_out, sizeof(double)));
+  }
+  HVE_HIP(launch_dot(x->n, x->d, y->d, g_dot_part, g_dot_out, lib_stream()));
+  HVE_HIP(hipMemcpyAsync(prod, g_dot_out, sizeof(double), hipMemcpyDeviceToHost, lib_stream()));
+  HVE_HIP(hipStreamSynchronize(lib_stream()));
+  API_END
+}
+HYPRE_Real* hypreve_ParVectorDeviceData(HYPRE_ParVector v) {
+  if (!v) return nullptr;
+  try { vec_alloc(v); } catch (...) { return nullptr; }
+  return v->d;
+}
+HYPRE_Int hypreve_ParVectorLocalSize(HYPRE_ParVector v) { return v ? v->n : 0; }
+HYPRE_Int hypreve_ParVectorCopyToHost(HYPRE_ParVector v, HYPRE_Real* host) {
+  CHECK_ARG(v && host, 1);
+  API_BEGIN
+  HVE_HIP(hipMemcpy(host, v->d, sizeof(double) * v->n, hipMemcpyDeviceToHost));
+  API_END
+}
+HYPRE_Int hypreve_ParVectorCopyFromHost(HYPRE_ParVector v, const HYPRE_Real* host) {
+  CHECK_ARG(v && host, 1);
+  API_BEGIN
+  vec_alloc(v);
+  HVE_HIP(hipMemcpy(v->d, host, sizeof(double) * v->n, hipMemcpyHostToDevice));
+  API_END
+}
+// par_vector.c:328 + vector.c:286: SeedRand(seed*(rank+1)); x_i = 2*Rand()-1
+HYPRE_Int hypreve_ParVectorSetRandomValues(HYPRE_ParVector v, HYPRE_Int seed) {
+  CHECK_ARG(v, 1);
+  API_BEGIN
+  const int rank = v->comm ? v->comm->rank : 0;
+  const int s = seed * (rank + 1);
+  std::vector<double> h(v->n);
+  for (int i = 0; i < v->n; ++i) h[i] = 2.0 * hypre_rand_at(i, s) - 1.0;
+  vec_alloc(v);
+  HVE_HIP(hipMemcpy(v->d, h.data(), sizeof(double) * v->n, hipMemcpyHostToDevice));
+  API_END
+}
+
+// ---------------------------------------------------------------------------
+// ParCSR matrix
+// ---------------------------------------------------------------------------
+static HYPRE_ParCSRMatrix wrap_matrix(HYPRE_Comm comm, CSR&& A, HYPRE_BigInt first, HYPRE_BigInt global) {
+  auto* M = new hypre_ParCSRMatrix_struct;
+  M->comm = comm;
+  M->first_row = M->first_col = first;
+  M->global_rows = M->global_cols = global;
+  M->n = A.nrows;
+  M->diag = std::move(A);
+  return M;
+}
+
+HYPRE_Int HYPRE_ParCSRMatrixDestroy(HYPRE_ParCSRMatrix M) {
+  if (!M) return 0;
+  M->dA.release();
+  delete M;
+  return 0;
+}
+HYPRE_Int HYPRE_ParCSRMatrixGetLocalRange(HYPRE_ParCSRMatrix M, HYPRE_BigInt* rs, HYPRE_BigInt* re,
+                                          HYPRE_BigInt* cs, HYPRE_BigInt* ce) {
+  CHECK_ARG(M, 1);
+  *rs = M->first_row; *re = M->first_row + M->n - 1;
+  *cs = M->first_col; *ce = M->first_col + M->n - 1;
+  return 0;
+}
+
+static int matvec_general(HYPRE_Complex alpha, HYPRE_ParCSRMatrix A, HYPRE_ParVector x, HYPRE_Complex beta,
+                          HYPRE_ParVector b, HYPRE_ParVector y) {
+  A->ensure_device();
+  vec_alloc(y);
+  hipStream_t s = lib_stream();
+  if (alpha == 0.0) {
+    // y = beta*b
+    if (b != y) HVE_HIP(launch_copy(A->n, b->d, y->d, s));
+    HVE_HIP(launch_scale(A->n, nullptr, beta, y->d, s));
+  } else if (x == y) {
+    double* tmp = nullptr;
+    HVE_HIP(hipMalloc((void**)&tmp, sizeof(double) * A->n));
+    HVE_HIP(launch_copy(A->n, x->d, tmp, s));
+    HVE_HIP(launch_sell(K_GENERAL, A->dA.view(), tmp, b->d, nullptr, nullptr, 0, y->d, alpha, beta / alpha, s));
+    HVE_HIP(hipStreamSynchronize(s));
+    hipFree(tmp);
+  } else {
+    HVE_HIP(launch_sell(K_GENERAL, A->dA.view(), x->d, b->d, nullptr, nullptr, 0, y->d, alpha, beta / alpha, s));
+  }
+  HVE_HIP(hipStreamSynchronize(s));
+  return 0;
+}
+
+HYPRE_Int HYPRE_ParCSRMatrixMatvec(HYPRE_Complex alpha, HYPRE_ParCSRMatrix A, HYPRE_ParVector x, HYPRE_Complex beta,
+                                   HYPRE_ParVector y) {
+  CHECK_ARG(A, 2);
+  CHECK_ARG(x && x->n == A->n, 3);
+  CHECK_ARG(y && y->n == A->n, 5);
+  API_BEGIN
+  matvec_general(alpha, A, x, beta, y, y);
+  API_END
+}
+HYPRE_Int HYPRE_ParCSRMatrixMatvecOutOfPlace(HYPRE_Complex alpha, HYPRE_ParCSRMatrix A, HYPRE_ParVector x,
+                                             HYPRE_Complex beta, HYPRE_ParVector b, HYPRE_ParVector y) {
+  CHECK_ARG(A, 2);
+  CHECK_ARG(x && x->n == A->n, 3);
+  CHECK_ARG(b && b->n == A->n, 5);
+  CHECK_ARG(y && y->n == A->n, 6);
+  API_BEGIN
+  matvec_general(alpha, A, x, beta, b, y);
+  API_END
+}
+HYPRE_Int HYPRE_ParCSRMatrixMatvecT(HYPRE_Complex alpha, HYPRE_ParCSRMatrix A, HYPRE_ParVector x,
+                                    HYPRE_Complex beta, HYPRE_ParVector y) {
+  CHECK_ARG(A, 2);
+  API_BEGIN
+  // y = alpha*A^T*x + beta*y via an explicit transpose (csr_matvec.c:424 order)
+  CSR AT;
+  transpose(A->diag, AT);
+  DevSell dT;
+  dT.upload(AT);
+  hipStream_t s = lib_stream();
+  double* tmp = nullptr;
+  HVE_HIP(hipMalloc((void**)&tmp, sizeof(double) * y->n));
+  HVE_HIP(launch_sell(K_RESTRICT, dT.view(), x->d, nullptr, nullptr, nullptr, 0, tmp, 1.0, 0.0, s));
+  // y = beta*y + alpha*tmp  (beta/alpha scaling as in the reference)
+  if (beta == 0.0) HVE_HIP(launch_set(y->n, 0.0, y->d, s));
+  else HVE_HIP(launch_scale(y->n, nullptr, beta, y->d, s));
+  HVE_HIP(launch_axpy(y->n, nullptr, alpha, 1.0, tmp, y->d, s));
+  HVE_HIP(hipStreamSynchronize(s));
+  hipFree(tmp);
+  dT.release();
+  API_END
+}
+
+HYPRE_Int hypreve_ParCSRMatrixCreateFromCSR(HYPRE_Comm comm, HYPRE_BigInt first_row, HYPRE_Int local_rows,
+                                            HYPRE_BigInt global_rows, const HYPRE_Int* row_ptr,
+                                            const HYPRE_BigInt* cols, const HYPRE_Real* vals, HYPRE_ParCSRMatrix* A) {
+  CHECK_ARG(row_ptr && cols && vals && A, 5);
+  API_BEGIN
+  if (comm && comm->size > 1) throw std::runtime_error("multi-rank matrices: use GenerateLaplacian or IJ per rank");
+  CSR M;
+  M.resize_rows(local_rows, (int)global_rows);
+  for (int r = 0; r <= local_rows; ++r) M.i[r] = row_ptr[r] - row_ptr[0];
+  M.j.resize(M.i[local_rows]);
+  M.a.resize(M.i[local_rows]);
+  for (int r = 0; r < local_rows; ++r) {
+    // diagonal first (hypre ParCSR convention), others in given order
+    int o = M.i[r];
+    const int b = row_ptr[r] - row_ptr[0], e = row_ptr[r + 1] - row_ptr[0];
+    int dpos = -1;
+    for (int k = b; k < e; ++k)
+      if (cols[k] - first_row == r) { dpos = k; break; }
+    if (dpos >= 0) { M.j[o] = r; M.a[o++] = vals[dpos]; }
+    for (int k = b; k < e; ++k) {
+      if (k == dpos) continue;
+      M.j[o] = (int)(cols[k] - first_row);
+      M.a[o++] = vals[k];
+    }
+  }
+  *A = wrap_matrix(comm, std::move(M), first_row, global_rows);
+  API_END
+}
+
+// par_laplace.c:15 (P=Q=R=1 in this build; multi-rank grids in comm.hip)
+HYPRE_ParCSRMatrix GenerateLaplacian(HYPRE_Comm comm, HYPRE_BigInt nx, HYPRE_BigInt ny, HYPRE_BigInt nz,
+                                     HYPRE_Int P, HYPRE_Int Q, HYPRE_Int R, HYPRE_Int p, HYPRE_Int q, HYPRE_Int r,
+                                     HYPRE_Real* value) {
+  try {
+    if (P * Q * R != 1) throw std::runtime_error("GenerateLaplacian: multi-rank partition not built in");
+    CSR A;
+    const double cx = -value[1], cy = -value[2], cz = -value[3];
+    generate_laplacian_7pt((int)nx, (int)ny, (int)nz, cx, cy, cz, A);
+    // the reference takes value[0] verbatim
+    for (int i = 0; i < A.nrows; ++i) A.a[A.i[i]] = value[0];
+    return wrap_matrix(comm, std::move(A), 0, (HYPRE_BigInt)nx * ny * nz);
+  } catch (const std::exception& e) {
+    set_err(HYPRE_ERROR_GENERIC, e.what());
+    return nullptr;
+  }
+}
+HYPRE_ParCSRMatrix GenerateLaplacian27pt(HYPRE_Comm comm, HYPRE_BigInt nx, HYPRE_BigInt ny, HYPRE_BigInt nz,
+                                         HYPRE_Int P, HYPRE_Int Q, HYPRE_Int R, HYPRE_Int p, HYPRE_Int q,
+                                         HYPRE_Int r, HYPRE_Real* value) {
+  try {
+    if (P * Q * R != 1) throw std::runtime_error("GenerateLaplacian27pt: multi-rank partition not built in");
+    CSR A;
+    generate_laplacian_27pt((int)nx, (int)ny, (int)nz, A);
+    for (int i = 0; i < A.nrows; ++i) {
+      A.a[A.i[i]] = value[0];
+      for (int k = A.i[i] + 1; k < A.i[i + 1]; ++k) A.a[k] = value[1];
+    }
+    return wrap_matrix(comm, std::move(A), 0, (HYPRE_BigInt)nx * ny * nz);
+  } catch (const std::exception& e) {
+    set_err(HYPRE_ERROR_GENERIC, e.what());
+    return nullptr;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// IJ interface
+// ---------------------------------------------------------------------------
+HYPRE_Int HYPRE_IJMatrixCreate(HYPRE_Comm comm, HYPRE_BigInt ilower, HYPRE_BigInt iupper, HYPRE_BigInt jlower,
+                               HYPRE_BigInt jupper, HYPRE_IJMatrix* matrix) {
+  CHECK_ARG(matrix, 6);
+  CHECK_ARG(iupper >= ilower - 1, 3);
+  auto* M = new hypre_IJMatrix_struct;
+  M->comm = comm;
+  M->ilower = ilower; M->iupper = iupper; M->jlower = jlower; M->jupper = jupper;
+  *matrix = M;
+  return 0;
+}
+HYPRE_Int HYPRE_IJMatrixDestroy(HYPRE_IJMatrix M) {
+  if (!M) return 0;
+  if (M->par) HYPRE_ParCSRMatrixDestroy(M->par);
+  delete M;
+  return 0;
+}
+HYPRE_Int HYPRE_IJMatrixSetObjectType(HYPRE_IJMatrix M, HYPRE_Int type) {
+  CHECK_ARG(M, 1);
+  CHECK_ARG(type == HYPRE_PARCSR, 2);
+  return 0;
+}
+HYPRE_Int HYPRE_IJMatrixInitialize(HYPRE_IJMatrix M) {
+  CHECK_ARG(M, 1);
+  M->rows.assign((size_t)(M->iupper - M->ilower + 1), {});
+  return 0;
+}
+static int ij_set(HYPRE_IJMatrix M, HYPRE_Int nrows, HYPRE_Int* ncols, const HYPRE_BigInt* rows,
+                  const HYPRE_BigInt* cols, const HYPRE_Complex* values, bool add) {
+  if (M->rows.empty() && M->iupper >= M->ilower) HYPRE_IJMatrixInitialize(M);
+  auto nc = host_copy(ncols, nrows);
+  size_t tot = 0;
+  for (int r = 0; r < nrows; ++r) tot += (size_t)nc[r];
+  auto rw = host_copy(rows, nrows);
+  auto cl = host_copy(cols, tot);
+  auto vl = host_copy(values, tot);
+  size_t k = 0;
+  for (int r = 0; r < nrows; ++r) {
+    const HYPRE_BigInt row = rw[r];
+    if (row < M->ilower || row > M->iupper) throw std::runtime_error("IJMatrixSetValues: off-process row");
+    auto& R = M->rows[row - M->ilower];
+    for (int q = 0; q < nc[r]; ++q, ++k) {
+      const int c = (int)cl[k];
+      auto it = std::find_if(R.begin(), R.end(), [&](const std::pair<int, double>& e) { return e.first == c; });
+      if (it == R.end()) R.emplace_back(c, vl[k]);
+      else if (add) it->second += vl[k];
+      else it->second = vl[k];
+    }
+  }
+  return 0;
+}
+HYPRE_Int HYPRE_IJMatrixSetValues(HYPRE_IJMatrix M, HYPRE_Int nrows, HYPRE_Int* ncols, const HYPRE_BigInt* rows,
+                                  const HYPRE_BigInt* cols, const HYPRE_Complex* values) {
+  CHECK_ARG(M, 1);
+  API_BEGIN
+  ij_set(M, nrows, ncols, rows, cols, values, false);
+  API_END
+}
+HYPRE_Int HYPRE_IJMatrixAddToValues(HYPRE_IJMatrix M, HYPRE_Int nrows, HYPRE_Int* ncols, const HYPRE_BigInt* rows,
+                                    const HYPRE_BigInt* cols, const HYPRE_Complex* values) {
+  CHECK_ARG(M, 1);
+  API_BEGIN
+  ij_set(M, nrows, ncols, rows, cols, values, true);
+  API_END
+}
+HYPRE_Int HYPRE_IJMatrixAssemble(HYPRE_IJMatrix M) {
+  CHECK_ARG(M, 1);
+  API_BEGIN
+  if (M->comm && M->comm->size > 1) throw std::runtime_error("IJ assembly across ranks: use per-rank blocks");
+  const int n = (int)(M->iupper - M->ilower + 1);
+  CSR A;
+  A.resize_rows(n, (int)(M->jupper - M->jlower + 1));
+  for (int r = 0; r < n; ++r) A.i[r + 1] = A.i[r] + (int)M->rows[r].size();
+  A.j.resize(A.i[n]);
+  A.a.resize(A.i[n]);
+  for (int r = 0; r < n; ++r) {
+    int o = A.i[r];
+    const auto& R = M->rows[r];
+    const int drow = (int)(r + M->ilower - M->jlower);
+    for (const auto& e : R)
+      if (e.first - (int)M->jlower == drow) { A.j[o] = drow; A.a[o++] = e.second; }
+    for (const auto& e : R)
+      if (e.first - (int)M->jlower != drow) { A.j[o] = e.first - (int)M->jlower; A.a[o++] = e.second; }
+  }
+  if (M->par) HYPRE_ParCSRMatrixDestroy(M->par);
+  M->par = wrap_matrix(M->comm, std::move(A), M->ilower, M->iupper + 1);
+  API_END
+}
+HYPRE_Int HYPRE_IJMatrixGetObject(HYPRE_IJMatrix M, void** object) {
+  CHECK_ARG(M && M->par, 1);
+  *object = (void*)M->par;
+  return 0;
+}
+
+HYPRE_Int HYPRE_IJVectorCreate(HYPRE_Comm comm, HYPRE_BigInt jlower, HYPRE_BigInt jupper, HYPRE_IJVector* vector) {
+  CHECK_ARG(vector, 4);
+  auto* V = new hypre_IJVector_struct;
+  V->comm = comm;
+  V->jlower = jlower;
+  V->jupper = jupper;
+  *vector = V;
+  return 0;
+}
+HYPRE_Int HYPRE_IJVectorDestroy(HYPRE_IJVector V) {
+  if (!V) return 0;
+  if (V->par) HYPRE_ParVectorDestroy(V->par);
+  delete V;
+  return 0;
+}
+HYPRE_Int HYPRE_IJVectorSetObjectType(HYPRE_IJVector V, HYPRE_Int type) {
+  CHECK_ARG(V, 1);
+  CHECK_ARG(type == HYPRE_PARCSR, 2);
+  return 0;
+}
+HYPRE_Int HYPRE_IJVectorInitialize(HYPRE_IJVector V) {
+  CHECK_ARG(V, 1);
+  V->h.assign((size_t)(V->jupper - V->jlower + 1), 0.0);
+  return 0;
+}
+HYPRE_Int HYPRE_IJVectorSetValues(HYPRE_IJVector V, HYPRE_Int nvalues, const HYPRE_BigInt* indices,
+                                  const HYPRE_Complex* values) {
+  CHECK_ARG(V, 1);
+  API_BEGIN
+  if (V->h.empty()) HYPRE_IJVectorInitialize(V);
+  auto vl = host_copy(values, nvalues);
+  if (indices) {
+    auto ix = host_copy(indices, nvalues);
+    for (int k = 0; k < nvalues; ++k) V->h.at(ix[k] - V->jlower) = vl[k];
+  } else {
+    for (int k = 0; k < nvalues; ++k) V->h.at(k) = vl[k];
+  }
+  if (V->par) {  // after assembly: write through to the device vector
+    HVE_HIP(hipMemcpy(V->par->d, V->h.data(), sizeof(double) * V->h.size(), hipMemcpyHostToDevice));
+  }
+  API_END
+}
+HYPRE_Int HYPRE_IJVectorAssemble(HYPRE_IJVector V) {
+  CHECK_ARG(V, 1);
+  API_BEGIN
+  if (V->h.empty()) HYPRE_IJVectorInitialize(V);
+  if (!V->par) {
+    V->par = new_vector(V->comm, V->jupper + 1, V->jlower, (int)V->h.size());
+    vec_alloc(V->par);
+  }
+  HVE_HIP(hipMemcpy(V->par->d, V->h.data(), sizeof(double) * V->h.size(), hipMemcpyHostToDevice));
+  API_END
+}
+HYPRE_Int HYPRE_IJVectorGetObject(HYPRE_IJVector V, void** object) {
+  CHECK_ARG(V && V->par, 1);
+  *object = (void*)V->par;
+  return 0;
+}
+HYPRE_Int HYPRE_IJVectorGetValues(HYPRE_IJVector V, HYPRE_Int nvalues, const HYPRE_BigInt* indices,
+                                  HYPRE_Complex* values) {
+  CHECK_ARG(V && V->par, 1);
+  API_BEGIN
+  std::vector<double> h(V->par->n);
+  HVE_HIP(hipMemcpy(h.data(), V->par->d, sizeof(double) * h.size(), hipMemcpyDeviceToHost));
+  std::vector<double> out(nvalues);
+  if (indices) {
+    auto ix = host_copy(indices, nvalues);
+    for (int k = 0; k < nvalues; ++k) out[k] = h.at(ix[k] - V->jlower);
+  } else {
+    for (int k = 0; k < nvalues; ++k) out[k] = h.at(k);
+  }
+  if (g_memloc == HYPRE_MEMORY_DEVICE) HVE_HIP(hipMemcpy(values, out.data(), sizeof(double) * nvalues, hipMemcpyHostToDevice));
+  else std::memcpy(values, out.data(), sizeof(double) * nvalues);
+  API_END
+}
+
+// ---------------------------------------------------------------------------
+// BoomerAMG
+// ---------------------------------------------------------------------------
+#define AMG_SET(name, field, type)                          \
+  HYPRE_Int HYPRE_BoomerAMGSet##name(HYPRE_Solver s, type v) { \
+    CHECK_ARG(s && s->kind == KIND_AMG, 1);                   \
+    s->prm.field = v;                                         \
+    return 0;                                                 \
+  }
+
+HYPRE_Int HYPRE_BoomerAMGCreate(HYPRE_Solver* solver) {
+  CHECK_ARG(solver, 1);
+  auto* s = new hypre_Solver_struct;
+  s->kind = KIND_AMG;
+  *solver = s;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGDestroy(HYPRE_Solver s) {
+  if (!s) return 0;
+  delete s;
+  return 0;
+}
+AMG_SET(ConvergeType, converge_type, HYPRE_Int)
+AMG_SET(Tol, tol, HYPRE_Real)
+AMG_SET(MaxIter, max_iter, HYPRE_Int)
+AMG_SET(MinIter, min_iter, HYPRE_Int)
+AMG_SET(MaxCoarseSize, max_coarse_size, HYPRE_Int)
+AMG_SET(MinCoarseSize, min_coarse_size, HYPRE_Int)
+AMG_SET(MaxLevels, max_levels, HYPRE_Int)
+AMG_SET(StrongThreshold, strong_threshold, HYPRE_Real)
+AMG_SET(MaxRowSum, max_row_sum, HYPRE_Real)
+AMG_SET(CoarsenType, coarsen_type, HYPRE_Int)
+AMG_SET(MeasureType, measure_type, HYPRE_Int)
+AMG_SET(AggNumLevels, agg_num_levels, HYPRE_Int)
+AMG_SET(InterpType, interp_type, HYPRE_Int)
+AMG_SET(TruncFactor, trunc_factor, HYPRE_Real)
+AMG_SET(PMaxElmts, P_max_elmts, HYPRE_Int)
+AMG_SET(CycleType, cycle_type, HYPRE_Int)
+AMG_SET(RelaxOrder, relax_order, HYPRE_Int)
+AMG_SET(RelaxWt, relax_weight, HYPRE_Real)
+AMG_SET(OuterWt, outer_weight, HYPRE_Real)
+AMG_SET(PrintLevel, print_level, HYPRE_Int)
+AMG_SET(Logging, logging, HYPRE_Int)
+
+// par_amg.c:1962 SetNumSweeps: all of [0..2] (coarsest keeps 1), :2084 SetRelaxType
+HYPRE_Int HYPRE_BoomerAMGSetNumSweeps(HYPRE_Solver s, HYPRE_Int num_sweeps) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(num_sweeps >= 1, 2);
+  for (int i = 0; i < 3; ++i) s->prm.num_sweeps[i] = num_sweeps;
+  s->prm.num_sweeps[3] = 1;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGSetCycleNumSweeps(HYPRE_Solver s, HYPRE_Int num_sweeps, HYPRE_Int k) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(num_sweeps >= 0, 2);
+  CHECK_ARG(k >= 1 && k <= 3, 3);
+  s->prm.num_sweeps[k] = num_sweeps;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGSetRelaxType(HYPRE_Solver s, HYPRE_Int relax_type) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(relax_type >= 0, 2);
+  for (int i = 0; i < 3; ++i) s->prm.relax_type[i] = relax_type;
+  s->prm.relax_type[3] = 9;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGSetCycleRelaxType(HYPRE_Solver s, HYPRE_Int relax_type, HYPRE_Int k) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(k >= 1 && k <= 3, 3);
+  CHECK_ARG(relax_type >= 0, 2);
+  s->prm.relax_type[k] = relax_type;
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver s, HYPRE_Int nb) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  s->prm.num_blocks = nb < 1 ? 1 : nb;
+  s->user_num_blocks = nb >= 1;
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGSetUseGraph(HYPRE_Solver s, HYPRE_Int g) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  s->use_graph = g != 0;
+  if (s->dev) s->dev->set_use_graph(s->use_graph);
+  return 0;
+}
+
+HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(A, 2);
+  API_BEGIN
+  amg_setup(A->diag, s->prm, s->H);
+  API_END
+}
+
+HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVector b, HYPRE_ParVector x) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(A, 2);
+  API_BEGIN
+  amg_setup(A->diag, s->prm, s->H);
+  if (!s->dev) s->dev.reset(new DevAMG);
+  s->dev->build(s->H);
+  s->dev->set_use_graph(s->use_graph);
+  API_END
+}
+
+HYPRE_Int HYPRE_BoomerAMGSolve(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVector b, HYPRE_ParVector x) {
+  CHECK_ARG(s && s->kind == KIND_AMG && s->dev && s->dev->built(), 1);
+  CHECK_ARG(A, 2);
+  CHECK_ARG(b && b->n == s->dev->n0(), 3);
+  CHECK_ARG(x && x->n == s->dev->n0(), 4);
+  API_BEGIN
+  vec_alloc(x);
+  s->dev->prm.tol = s->prm.tol;
+  s->dev->prm.max_iter = s->prm.max_iter;
+  s->dev->prm.min_iter = s->prm.min_iter;
+  s->dev->prm.converge_type = s->prm.converge_type;
+  s->dev->prm.print_level = s->prm.print_level;
+  const int rc = s->dev->solve(b->d, x->d, s->dev->stream(), &s->iters, &s->rel_res);
+  HVE_HIP(hipStreamSynchronize(s->dev->stream()));
+  if (rc) g_error |= rc;
+  API_END
+}
+HYPRE_Int hypreve_BoomerAMGCycle(HYPRE_Solver s, HYPRE_ParVector f, HYPRE_ParVector u) {
+  CHECK_ARG(s && s->kind == KIND_AMG && s->dev && s->dev->built(), 1);
+  CHECK_ARG(f && u && f->n == s->dev->n0() && u->n == s->dev->n0(), 2);
+  API_BEGIN
+  s->dev->cycle(f->d, u->d, s->dev->stream());
+  HVE_HIP(hipStreamSynchronize(s->dev->stream()));
+  API_END
+}
+HYPRE_Int HYPRE_BoomerAMGGetNumIterations(HYPRE_Solver s, HYPRE_Int* it) {
+  CHECK_ARG(s && it, 1);
+  *it = s->iters;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGGetFinalRelativeResidualNorm(HYPRE_Solver s, HYPRE_Real* r) {
+  CHECK_ARG(s && r, 1);
+  *r = s->rel_res;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGGetNumLevels(HYPRE_Solver s, HYPRE_Int* nl) {
+  CHECK_ARG(s && nl, 1);
+  *nl = (int)s->H.lev.size();
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGGetComplexities(HYPRE_Solver s, HYPRE_Real* grid, HYPRE_Real* oper, HYPRE_Real* cycle) {
+  CHECK_ARG(s, 1);
+  if (grid) *grid = s->H.grid_complexity;
+  if (oper) *oper = s->H.operator_complexity;
+  if (cycle) {
+    // par_cycle.c op count: one smoothing sweep costs nnz(A_l)
+    double ops = 0;
+    const int nl = (int)s->H.lev.size();
+    for (int l = 0; l < nl; ++l) {
+      const double nz = (double)s->H.lev[l].A.nnz();
+      if (nl == 1) ops += nz;
+      else if (l < nl - 1) ops += nz * (s->H.prm.num_sweeps[1] + s->H.prm.num_sweeps[2]);
+      else ops += nz * s->H.prm.num_sweeps[3];
+    }
+    *cycle = nl ? ops / (double)s->H.lev[0].A.nnz() : 0.0;
+  }
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGGetLevelInfo(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int* rows, int64_t* nnz_A,
+                                        int64_t* nnz_P) {
+  CHECK_ARG(s && level >= 0 && level < (int)s->H.lev.size(), 2);
+  const Level& L = s->H.lev[level];
+  if (rows) *rows = L.A.nrows;
+  if (nnz_A) *nnz_A = L.A.nnz();
+  if (nnz_P) *nnz_P = L.P.nnz();
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGGetLevelMatrix(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int* nrows,
+                                          HYPRE_Int* ncols, int64_t* nnz, HYPRE_Int* row_ptr, HYPRE_Int* cols,
+                                          HYPRE_Real* vals) {
+  CHECK_ARG(s && level >= 0 && level < (int)s->H.lev.size(), 2);
+  const Level& L = s->H.lev[level];
+  const CSR& M = which == 0 ? L.A : L.P;
+  if (nrows) *nrows = M.nrows;
+  if (ncols) *ncols = M.ncols;
+  if (nnz) *nnz = M.nnz();
+  if (row_ptr && !M.i.empty()) std::memcpy(row_ptr, M.i.data(), sizeof(int) * M.i.size());
+  if (cols && M.nnz()) std::memcpy(cols, M.j.data(), sizeof(int) * M.nnz());
+  if (vals && M.nnz()) std::memcpy(vals, M.a.data(), sizeof(double) * M.nnz());
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGGetLevelVector(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int* n,
+                                          void* data) {
+  CHECK_ARG(s && level >= 0 && level < (int)s->H.lev.size(), 2);
+  const Level& L = s->H.lev[level];
+  if (which == 0) {
+    if (n) *n = (int)L.cf.size();
+    if (data && !L.cf.empty()) std::memcpy(data, L.cf.data(), sizeof(int) * L.cf.size());
+  } else {
+    if (n) *n = (int)L.l1.size();
+    if (data && !L.l1.empty()) std::memcpy(data, L.l1.data(), sizeof(double) * L.l1.size());
+  }
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGGetCoarseMatrix(HYPRE_Solver s, HYPRE_Int* n, HYPRE_Real* dense) {
+  CHECK_ARG(s, 1);
+  if (n) *n = s->H.coarse_n;
+  if (dense && !s->H.coarse_dense.empty())
+    std::memcpy(dense, s->H.coarse_dense.data(), sizeof(double) * s->H.coarse_dense.size());
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGGetRelaxInfo(HYPRE_Solver s, HYPRE_Int* rt, HYPRE_Int* ns, HYPRE_Real* w, HYPRE_Int* misc) {
+  CHECK_ARG(s, 1);
+  const AMGParams& p = s->H.lev.empty() ? s->prm : s->H.prm;
+  for (int i = 0; i < 4; ++i) { if (rt) rt[i] = p.relax_type[i]; if (ns) ns[i] = p.num_sweeps[i]; }
+  if (w) { w[0] = p.relax_weight; w[1] = p.outer_weight; }
+  if (misc) { misc[0] = p.relax_order; misc[1] = p.cycle_type; misc[2] = p.num_blocks; }
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGGetKernelStats(HYPRE_Solver s, HYPRE_Real* stats, HYPRE_Int n) {
+  CHECK_ARG(s && stats, 1);
+  for (int i = 0; i < n; ++i) stats[i] = 0.0;
+  if (n > 0 && s->dev) stats[0] = s->dev->cycle_op_count();
+  return 0;
+}
+
+// Finest-level residual SpMV timed with HIP events on the solver's stream.
+// Algorithmic bytes per launch: nnz*(8 val + 4 col) + n*(8 x + 8 b + 8 y)
+// + slice pointers (4 per 64 rows).
+HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver s, HYPRE_Int reps, HYPRE_Real* avg_ms, HYPRE_Real* bytes) {
+  CHECK_ARG(s && s->dev && s->dev->built(), 1);
+  API_BEGIN
+  DevAMG& D = *s->dev;
+  const DevSell& A = D.fineA();
+  hipStream_t st = D.stream();
+  double* x = D.scratch(0);
+  double* b = D.scratch(1);
+  double* y = D.scratch(2);
+  HVE_HIP(launch_set(A.nrows, 1.0, x, st));
+  HVE_HIP(launch_set(A.nrows, 0.5, b, st));
+  for (int w = 0; w < 3; ++w)
+    HVE_HIP(launch_sell(K_RESID, A.view(), x, b, nullptr, nullptr, 0, y, -1.0, 0.0, st));
+  hipEvent_t e0, e1;
+  HVE_HIP(hipEventCreate(&e0));
+  HVE_HIP(hipEventCreate(&e1));
+  HVE_HIP(hipEventRecord(e0, st));
+  for (int r = 0; r < reps; ++r)
+    HVE_HIP(launch_sell(K_RESID, A.view(), x, b, nullptr, nullptr, 0, y, -1.0, 0.0, st));
+  HVE_HIP(hipEventRecord(e1, st));
+  HVE_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HVE_HIP(hipEventElapsedTime(&ms, e0, e1));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (avg_ms) *avg_ms = ms / reps;
+  if (bytes) *bytes = (double)A.nnz * 12.0 + (double)A.nrows * 24.0 + (double)(A.nslices + 1) * 4.0;
+  API_END
+}
+
+// ---------------------------------------------------------------------------
+// PCG
+// ---------------------------------------------------------------------------
+HYPRE_Int HYPRE_ParCSRPCGCreate(HYPRE_Comm comm, HYPRE_Solver* solver) {
+  CHECK_ARG(solver, 2);
+  auto* s = new hypre_Solver_struct;
+  s->kind = KIND_PCG;
+  *solver = s;
+  return 0;
+}
+HYPRE_Int HYPRE_ParCSRPCGDestroy(HYPRE_Solver s) {
+  if (!s) return 0;
+  delete s;
+  return 0;
+}
+HYPRE_Int HYPRE_ParCSRPCGSetTol(HYPRE_Solver s, HYPRE_Real tol) { CHECK_ARG(s, 1); s->pcg.tol = tol; return 0; }
+HYPRE_Int HYPRE_ParCSRPCGSetMaxIter(HYPRE_Solver s, HYPRE_Int m) { CHECK_ARG(s, 1); s->pcg.max_iter = m; return 0; }
+HYPRE_Int HYPRE_ParCSRPCGSetTwoNorm(HYPRE_Solver s, HYPRE_Int t) { CHECK_ARG(s, 1); s->pcg.two_norm = t; return 0; }
+HYPRE_Int HYPRE_ParCSRPCGSetPrintLevel(HYPRE_Solver s, HYPRE_Int l) { CHECK_ARG(s, 1); s->pcg.print_level = l; return 0; }
+HYPRE_Int HYPRE_ParCSRPCGSetPrecond(HYPRE_Solver s, HYPRE_PtrToParSolverFcn precond,
+                                    HYPRE_PtrToParSolverFcn precond_setup, HYPRE_Solver precond_solver) {
+  CHECK_ARG(s && s->kind == KIND_PCG, 1);
+  s->precond_solve = precond;
+  s->precond_setup = precond_setup;
+  s->precond = precond_solver;
+  return 0;
+}
+HYPRE_Int HYPRE_ParCSRPCGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVector b, HYPRE_ParVector x) {
+  CHECK_ARG(s && s->kind == KIND_PCG, 1);
+  CHECK_ARG(A, 2);
+  API_BEGIN
+  A->ensure_device();
+  if (s->precond_setup && s->precond) {
+    int rc = s->precond_setup(s->precond, A, b, x);
+    if (rc) return rc;
+  }
+  if (!(s->precond && s->precond->kind == KIND_AMG && s->precond->dev)) {
+    s->ws.reset(new DevAMG);
+    s->ws->init_workspace(A->n);
+  }
+  API_END
+}
+HYPRE_Int HYPRE_ParCSRPCGSolve(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVector b, HYPRE_ParVector x) {
+  CHECK_ARG(s && s->kind == KIND_PCG, 1);
+  CHECK_ARG(A, 2);
+  CHECK_ARG(b && b->n == A->n, 3);
+  CHECK_ARG(x && x->n == A->n, 4);
+  API_BEGIN
+  A->ensure_device();
+  vec_alloc(x);
+  DevAMG* amg = (s->precond && s->precond->kind == KIND_AMG && s->precond->dev) ? s->precond->dev.get() : nullptr;
+  DevAMG* ws = amg ? amg : s->ws.get();
+  if (!ws) throw std::runtime_error("PCGSolve called before PCGSetup");
+  hipStream_t st = ws->stream();
+  Precond pre;
+  if (amg && s->precond_solve == (HYPRE_PtrToParSolverFcn)HYPRE_BoomerAMGSolve) {
+    // HYPRE_BoomerAMGSolve(precond, A, r, z) on device buffers, honoring the
+    // preconditioner's tol / max_iter (tol 0, max_iter 1 = one cycle)
+    hypre_Solver_struct* P = s->precond;
+    pre = [amg, P, st](const double* r, double* z) {
+      amg->prm.tol = P->prm.tol;
+      amg->prm.max_iter = P->prm.max_iter;
+      amg->prm.min_iter = P->prm.min_iter;
+      amg->prm.converge_type = P->prm.converge_type;
+      amg->prm.print_level = 0;
+      if (P->prm.tol == 0.0 && P->prm.max_iter == 1) amg->cycle(r, z, st);
+      else amg->solve(r, z, st, &P->iters, &P->rel_res);
+    };
+  } else if (s->precond_solve && s->precond) {
+    const int n = A->n;
+    hypre_Solver_struct* P = s->precond;
+    auto fn = s->precond_solve;
+    pre = [fn, P, A, n, st](const double* r, double* z) {
+      HVE_HIP(hipStreamSynchronize(st));
+      hypre_ParVector_struct rv, zv;
+      rv.n = zv.n = n; rv.d = const_cast<double*>(r); zv.d = z; rv.owns = zv.owns = false;
+      fn(P, A, &rv, &zv);
+    };
+  } else {
+    const int n = A->n;
+    pre = [n, st](const double* r, double* z) { HVE_HIP(launch_copy(n, r, z, st)); };
+  }
+  const int rc = pcg_solve(ws, A->dA, s->pcg, pre, b->d, x->d, st, &s->iters, &s->rel_res);
+  if (rc) g_error |= rc;
+  API_END
+}
+HYPRE_Int HYPRE_ParCSRPCGGetNumIterations(HYPRE_Solver s, HYPRE_Int* it) {
+  CHECK_ARG(s && it, 1);
+  *it = s->iters;
+  return 0;
+}
+HYPRE_Int HYPRE_ParCSRPCGGetFinalRelativeResidualNorm(HYPRE_Solver s, HYPRE_Real* r) {
+  CHECK_ARG(s && r, 1);
+  *r = s->rel_res;
+  return 0;
+}
+
+}  // extern "C"

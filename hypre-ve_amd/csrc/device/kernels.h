@@ -1,0 +1,45 @@
+// Launch interface of the hot-path kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace hve {
+
+// Device view of one SELL-64 operator (see kernels.hip header comment).
+struct SellView {
+  const int* slice_ptr = nullptr;  // nslices + 1 offsets (in entries)
+  const int* col = nullptr;        // padded; -1 marks padding
+  const double* val = nullptr;
+  int nrows = 0;
+  int ncols = 0;
+};
+
+enum : int {
+  K_RESID = 0, K_MATVEC = 1, K_L1JAC = 2, K_L1JAC_W = 3, K_JAC = 4,
+  K_PROLONG = 5, K_RESTRICT = 6, K_GENERAL = 7,
+};
+
+hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
+                       const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s);
+// op: 0 l1-Jacobi w=1, 1 l1-Jacobi weighted, 2 Jacobi (s = diagonal)
+hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u,
+                             hipStream_t st);
+hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,
+                       hipStream_t st);
+hipError_t launch_scale(int n, const double* alpha_p, double alpha, double* y, hipStream_t st);
+hipError_t launch_set(int n, double v, double* y, hipStream_t st);
+hipError_t launch_copy(int n, const double* x, double* y, hipStream_t st);
+hipError_t launch_pcg_p(int n, const double* beta_p, const double* s, double* p, hipStream_t st);
+int dot_num_parts(int n);
+hipError_t launch_dot(int n, const double* x, const double* y, double* part, double* out, hipStream_t st);
+hipError_t launch_pcg_alpha(double* sc, hipStream_t st);
+hipError_t launch_pcg_beta(double* sc, hipStream_t st);
+hipError_t launch_coarse(int n, const double* Lf, const unsigned char* Lmask, const double* U,
+                         const double* f, double* u, hipStream_t st);
+
+// Hybrid Gauss-Seidel (block-Jacobi across row blocks, exact GS inside a block).
+struct GSPlan;  // defined in relax_gs.hip
+hipError_t launch_hybrid_gs(const GSPlan& plan, const double* f, const double* l1, const int* cf,
+                            int relax_points, double* u, double* tmp, int fwd, int bwd, int use_l1,
+                            hipStream_t st);
+
+}  // namespace hve

@@ -1,0 +1,367 @@
+// HIP kernels for the BoomerAMG solve path on MI355X (gfx950).
+//
+// Layout in HBM.  Every operator of the hierarchy (A_l, P_l, R_l = P_l^T) is
+// stored in SELL-64: rows are cut into slices of 64 consecutive rows (one
+// wavefront), a slice is padded to its longest row, and entry k of lane r of
+// slice s sits at slice_ptr[s] + 64*k + r.  One lane owns one row and walks its
+// entries in the order the reference stores them, so every row sum is formed
+// in the reference's order (seq_mv/csr_matvec.c:187 for A and P,
+// csr_matvec.c:585 for the transpose) while all 64 lanes of a wave read one
+// contiguous 512-B (values) / 256-B (columns) segment per entry.  Padding
+// entries carry column -1 and are skipped.  No FMA contraction: the device code
+// is compiled with -ffp-contract=off, so each a*x is rounded before it is
+// added, exactly as the reference's C loops do.
+//
+// Grid mapping is XCD-aware: hardware dispatches workgroup b to XCD b % 8, so
+// the logical slice range is re-mapped so that each XCD streams one contiguous
+// eighth of the rows and its private 4 MiB L2 keeps the x-vector window that
+// neighbouring rows share (the z-neighbours of a 3-D stencil are nx*ny rows away).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "kernels.h"
+
+namespace hve {
+
+static constexpr int kWave = 64;
+
+__device__ __forceinline__ int xcd_logical_block(int b, int nblocks_pad) {
+  // nblocks_pad is a multiple of 8; block b runs on XCD b%8; give each XCD a
+  // contiguous range of logical blocks.
+  const int per_xcd = nblocks_pad >> 3;
+  return (b & 7) * per_xcd + (b >> 3);
+}
+
+// ---------------------------------------------------------------------------
+// Generic SELL row loop.  OP selects the row epilogue.
+// ---------------------------------------------------------------------------
+enum SpOp : int {
+  OP_RESID = 0,       // y = b - A x                 (hypre alpha=-1, beta=1)
+  OP_MATVEC = 1,      // y = A x                     (alpha=1, beta=0)
+  OP_L1JAC = 2,       // u_out = u + (f - A u)/l1    (relax 18/7, weight 1)
+  OP_L1JAC_W = 3,     // u_out = u + (-w)*(-f + A u)/l1 (relax 18/7, weight w)
+  OP_JAC = 4,         // u_out = (1-w) u + w (f - sum_{j!=i} a_ij u_j)/a_ii (relax 0)
+  OP_PROLONG = 5,     // u += P uc                   (alpha=1, beta=1)
+  OP_RESTRICT = 6,    // fc = R v                    (MatvecT, alpha=1, beta=0)
+  OP_GENERAL = 7,     // y = alpha*A*x + beta*b, hypre's branch structure
+};
+
+struct SpArgs {
+  const int* __restrict__ slice_ptr;
+  const int* __restrict__ col;
+  const double* __restrict__ val;
+  int nrows;
+  int nblocks_pad;
+  const double* __restrict__ x;   // vector multiplied by the matrix
+  const double* __restrict__ b;   // rhs / additive term (f or b)
+  const double* __restrict__ l1;  // l1 norms (or diag) for smoothers
+  const int* __restrict__ cf;     // CF marker (relax_points != 0 only)
+  double* __restrict__ y;         // output
+  double w;                       // relax weight / alpha
+  double temp;                    // beta/alpha for OP_GENERAL
+  int relax_points;
+};
+
+template <int OP, bool CFSEL>
+__global__ void __launch_bounds__(256) k_sell(SpArgs p) {
+  const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  const int row = lb * 256 + threadIdx.x;
+  if (row >= p.nrows) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int slice = row >> 6;
+  const int beg = p.slice_ptr[slice];
+  const int width = (p.slice_ptr[slice + 1] - beg) >> 6;
+  const int* __restrict__ cp = p.col + beg + lane;
+  const double* __restrict__ vp = p.val + beg + lane;
+
+  if (CFSEL) {
+    if (p.cf[row] != p.relax_points) {
+      if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) p.y[row] = p.x[row];
+      return;
+    }
+  }
+
+  if (OP == OP_RESID || OP == OP_L1JAC) {
+    double t = p.b[row];
+    for (int k = 0; k < width; ++k) {
+      const int c = cp[k * kWave];
+      const double a = vp[k * kWave];
+      if (c >= 0) t -= a * p.x[c];
+    }
+    if (OP == OP_RESID) p.y[row] = t;
+    else p.y[row] = p.x[row] + t / p.l1[row];
+  } else if (OP == OP_L1JAC_W) {
+    double t = -p.b[row];
+    for (int k = 0; k < width; ++k) {
+      const int c = cp[k * kWave];
+      const double a = vp[k * kWave];
+      if (c >= 0) t += a * p.x[c];
+    }
+    const double v = (-p.w) * t;
+    p.y[row] = p.x[row] + v / p.l1[row];
+  } else if (OP == OP_MATVEC || OP == OP_RESTRICT) {
+    double t = 0.0;
+    for (int k = 0; k < width; ++k) {
+      const int c = cp[k * kWave];
+      const double a = vp[k * kWave];
+      if (c >= 0) t += a * p.x[c];
+    }
+    p.y[row] = t;
+  } else if (OP == OP_PROLONG) {
+    double t = p.y[row];
+    for (int k = 0; k < width; ++k) {
+      const int c = cp[k * kWave];
+      const double a = vp[k * kWave];
+      if (c >= 0) t += a * p.x[c];
+    }
+    p.y[row] = t;
+  } else if (OP == OP_JAC) {
+    const double d = vp[0];  // diagonal stored first
+    const double uo = p.x[row];
+    if (d == 0.0) { p.y[row] = uo; return; }
+    double t = p.b[row];
+    for (int k = 1; k < width; ++k) {
+      const int c = cp[k * kWave];
+      const double a = vp[k * kWave];
+      if (c >= 0) t -= a * p.x[c];
+    }
+    double u = uo * (1.0 - p.w);
+    u += p.w * t / d;
+    p.y[row] = u;
+  } else if (OP == OP_GENERAL) {
+    // seq_mv/csr_matvec.c:187-330 branch structure; alpha = p.w, temp = beta/alpha
+    const double alpha = p.w, temp = p.temp;
+    double t;
+    const bool neg = (alpha == -1.0);
+    if (temp == 0.0) t = 0.0;
+    else if (temp == -1.0) t = neg ? p.b[row] : -p.b[row];
+    else if (temp == 1.0) t = neg ? -p.b[row] : p.b[row];
+    else t = neg ? -p.b[row] * temp : p.b[row] * temp;
+    for (int k = 0; k < width; ++k) {
+      const int c = cp[k * kWave];
+      const double a = vp[k * kWave];
+      if (c >= 0) {
+        if (neg) t -= a * p.x[c];
+        else t += a * p.x[c];
+      }
+    }
+    p.y[row] = (alpha == 1.0 || neg) ? t : alpha * t;
+  }
+}
+
+// Zero-initial-guess smoothers (coarse levels right after U_c = 0): A*0 is
+// exactly zero, so the reference's arithmetic reduces to elementwise forms.
+//   l1-Jacobi, w = 1: u = 0 + f/l1       ams.c:96 (v = f - A*0; u += v/l1)
+//   l1-Jacobi, w:     u = 0 + (-w*(-f))/l1
+//   Jacobi:           u = 0*(1-w) + w*f/d
+__global__ void __launch_bounds__(256) k_zero_guess(int n, int op, double w, const double* __restrict__ f,
+                                                    const double* __restrict__ s, double* __restrict__ u) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double r;
+  if (op == 0) r = 0.0 + f[i] / s[i];
+  else if (op == 1) r = 0.0 + ((-w) * (-f[i])) / s[i];
+  else {
+    const double d = s[i];
+    if (d == 0.0) r = 0.0;
+    else { r = 0.0 * (1.0 - w); r += w * f[i] / d; }
+  }
+  u[i] = r;
+}
+
+// ---------------------------------------------------------------------------
+// BLAS-1 (parcsr_mv/par_vector.c semantics)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_axpy(int n, const double* __restrict__ alpha_p, double alpha,
+                                              double sgn, const double* __restrict__ x, double* __restrict__ y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double a = alpha_p ? sgn * (*alpha_p) : alpha;
+  y[i] += a * x[i];
+}
+__global__ void __launch_bounds__(256) k_scale(int n, const double* __restrict__ alpha_p, double alpha,
+                                               double* __restrict__ y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const double a = alpha_p ? *alpha_p : alpha;
+  y[i] *= a;
+}
+__global__ void __launch_bounds__(256) k_set(int n, double v, double* __restrict__ y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = v;
+}
+__global__ void __launch_bounds__(256) k_copy(int n, const double* __restrict__ x, double* __restrict__ y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = x[i];
+}
+// p = s + beta*p  done as hypre does it: p *= beta; p += 1.0*s
+__global__ void __launch_bounds__(256) k_pcg_p(int n, const double* __restrict__ beta_p, const double* __restrict__ s,
+                                               double* __restrict__ p) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double v = p[i] * (*beta_p);
+  v += 1.0 * s[i];
+  p[i] = v;
+}
+
+// Deterministic two-stage dot product: stage 1 writes one partial per block.
+__global__ void __launch_bounds__(256) k_dot_partial(int n, const double* __restrict__ x, const double* __restrict__ y,
+                                                     double* __restrict__ part) {
+  __shared__ double sh[4];
+  double s = 0.0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += x[i] * y[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+__global__ void __launch_bounds__(256) k_dot_final(int nparts, const double* __restrict__ part, double* __restrict__ out) {
+  __shared__ double sh[4];
+  double s = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += part[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+// PCG scalar updates on device (krylov/pcg.c:522 alpha = gamma/<s,p>,
+// :730 beta = gamma/gamma_old).  sc[]: 0 gamma, 1 gamma_old, 2 sdotp, 3 alpha,
+// 4 beta, 5 i_prod, 6 flag (1 = stop)
+__global__ void k_pcg_alpha(double* sc) {
+  const double sdotp = sc[2];
+  sc[1] = sc[0];
+  if (sdotp == 0.0) { sc[6] = 2.0; sc[3] = 0.0; return; }
+  const double a = sc[0] / sdotp;
+  if (!(a > 2.2250738585072014e-308)) { sc[6] = 3.0; sc[3] = 0.0; return; }
+  sc[3] = a;
+}
+__global__ void k_pcg_beta(double* sc) { sc[4] = sc[0] / sc[1]; }
+
+// ---------------------------------------------------------------------------
+// Coarsest-level direct solve: hypre_gselim (sstruct_ls/gselim.h) applied to
+// f.  The elimination of the matrix does not depend on f, so the setup stores
+// the multipliers (L, with a skip flag where the reference skips) and the
+// eliminated upper triangle (U); here the same x-updates run in the same
+// order, parallel only across independent rows of one elimination step.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_coarse_gselim(int n, const double* __restrict__ Lf,
+                                                       const unsigned char* __restrict__ Lmask,
+                                                       const double* __restrict__ U, const double* __restrict__ f,
+                                                       double* __restrict__ u) {
+  extern __shared__ double xs[];
+  for (int i = threadIdx.x; i < n; i += blockDim.x) xs[i] = f[i];
+  __syncthreads();
+  if (n == 1) {
+    if (threadIdx.x == 0 && U[0] != 0.0) xs[0] = xs[0] / U[0];
+  } else {
+    for (int k = 0; k < n - 1; ++k) {
+      if (U[k * n + k] != 0.0) {  // pivot nonzero at step k (unchanged afterwards)
+        const double xk = xs[k];
+        for (int j = k + 1 + threadIdx.x; j < n; j += blockDim.x)
+          if (Lmask[j * n + k]) xs[j] -= Lf[j * n + k] * xk;
+      }
+      __syncthreads();
+    }
+    for (int k = n - 1; k > 0; --k) {
+      const double ukk = U[k * n + k];
+      if (ukk != 0.0) {
+        if (threadIdx.x == 0) xs[k] /= ukk;
+        __syncthreads();
+        const double xk = xs[k];
+        for (int j = threadIdx.x; j < k; j += blockDim.x)
+          if (U[j * n + k] != 0.0) xs[j] -= xk * U[j * n + k];
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0 && U[0] != 0.0) xs[0] /= U[0];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) u[i] = xs[i];
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launch helpers
+// ---------------------------------------------------------------------------
+static inline int blocks_for(int n) { return (n + 255) / 256; }
+static inline int blocks_pad8(int n) { int b = blocks_for(n); return ((b + 7) / 8) * 8; }
+
+hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
+                       const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s) {
+  if (M.nrows <= 0) return hipSuccess;
+  SpArgs a;
+  a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
+  a.nblocks_pad = blocks_pad8(M.nrows);
+  a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.w = w; a.temp = temp; a.relax_points = relax_points;
+  dim3 grid(a.nblocks_pad), block(256);
+  const bool cfsel = (relax_points != 0 && cf != nullptr);
+#define HVE_L(OPV)                                                                       \
+  case OPV:                                                                              \
+    if (cfsel) hipLaunchKernelGGL((k_sell<OPV, true>), grid, block, 0, s, a);           \
+    else hipLaunchKernelGGL((k_sell<OPV, false>), grid, block, 0, s, a);                \
+    break;
+  switch (op) {
+    HVE_L(OP_RESID) HVE_L(OP_MATVEC) HVE_L(OP_L1JAC) HVE_L(OP_L1JAC_W) HVE_L(OP_JAC)
+    HVE_L(OP_PROLONG) HVE_L(OP_RESTRICT) HVE_L(OP_GENERAL)
+    default: return hipErrorInvalidValue;
+  }
+#undef HVE_L
+  return hipGetLastError();
+}
+
+hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_zero_guess, dim3(blocks_for(n)), dim3(256), 0, st, n, op, w, f, s, u);
+  return hipGetLastError();
+}
+hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_axpy, dim3(blocks_for(n)), dim3(256), 0, st, n, alpha_p, alpha, sgn, x, y);
+  return hipGetLastError();
+}
+hipError_t launch_scale(int n, const double* alpha_p, double alpha, double* y, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_scale, dim3(blocks_for(n)), dim3(256), 0, st, n, alpha_p, alpha, y);
+  return hipGetLastError();
+}
+hipError_t launch_set(int n, double v, double* y, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_set, dim3(blocks_for(n)), dim3(256), 0, st, n, v, y);
+  return hipGetLastError();
+}
+hipError_t launch_copy(int n, const double* x, double* y, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_copy, dim3(blocks_for(n)), dim3(256), 0, st, n, x, y);
+  return hipGetLastError();
+}
+hipError_t launch_pcg_p(int n, const double* beta_p, const double* s, double* p, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pcg_p, dim3(blocks_for(n)), dim3(256), 0, st, n, beta_p, s, p);
+  return hipGetLastError();
+}
+int dot_num_parts(int n) {
+  int b = blocks_for(n);
+  return b < 1024 ? (b < 1 ? 1 : b) : 1024;
+}
+hipError_t launch_dot(int n, const double* x, const double* y, double* part, double* out, hipStream_t st) {
+  const int np = dot_num_parts(n);
+  hipLaunchKernelGGL(k_dot_partial, dim3(np), dim3(256), 0, st, n, x, y, part);
+  hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, st, np, part, out);
+  return hipGetLastError();
+}
+hipError_t launch_pcg_alpha(double* sc, hipStream_t st) {
+  hipLaunchKernelGGL(k_pcg_alpha, dim3(1), dim3(1), 0, st, sc);
+  return hipGetLastError();
+}
+hipError_t launch_pcg_beta(double* sc, hipStream_t st) {
+  hipLaunchKernelGGL(k_pcg_beta, dim3(1), dim3(1), 0, st, sc);
+  return hipGetLastError();
+}
+hipError_t launch_coarse(int n, const double* Lf, const unsigned char* Lmask, const double* U, const double* f,
+                         double* u, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_coarse_gselim, dim3(1), dim3(256), (size_t)n * sizeof(double), st, n, Lf, Lmask, U, f, u);
+  return hipGetLastError();
+}
+
+}  // namespace hve

@@ -1,0 +1,129 @@
+// Host-side data structures and BoomerAMG setup for hypre-ve_amd.
+//
+// The setup phase (strength, coarsening, interpolation, Galerkin product) runs
+// on the host in C++ exactly as hypre's single-process CPU path does, so that
+// the hierarchy handed to the GPU solve is the reference's hierarchy.  The solve
+// phase (the hot path) lives in ../device and never falls back to the host.
+//
+// Reference anchors (SX-Aurora/hypre-ve, src/):
+//   parcsr_ls/par_amg.c:141-229        hypre_BoomerAMGCreate defaults
+//   parcsr_ls/par_amg_setup.c:889-2880 coarsening loop
+//   parcsr_ls/par_strength.c:80        hypre_BoomerAMGCreateSHost
+//   parcsr_ls/par_coarsen.c:2031       hypre_BoomerAMGCoarsenPMISHost
+//   parcsr_ls/par_indepset.c:25        hypre_BoomerAMGIndepSetInit
+//   parcsr_ls/par_lr_interp.c:1041     hypre_BoomerAMGBuildExtPIInterpHost
+//   parcsr_mv/par_csr_matrix.c:2671    hypre_ParCSRMatrixTruncate
+//   parcsr_ls/par_rap.c:27             hypre_BoomerAMGBuildCoarseOperatorKT
+//   parcsr_ls/ams.c:571,3398           hypre_ParCSRComputeL1Norms(Threads)
+#pragma once
+#include <cstdint>
+#include <string>
+#include <utility>
+#include <vector>
+
+namespace hve {
+
+// CSR matrix, 0-based, hypre convention: in square operators the diagonal
+// entry is stored first in its row (parcsr_mv relies on A_diag_i[i] == diag).
+struct CSR {
+  int nrows = 0, ncols = 0;
+  std::vector<int> i;     // nrows + 1
+  std::vector<int> j;     // nnz
+  std::vector<double> a;  // nnz
+  int64_t nnz() const { return i.empty() ? 0 : (int64_t)i[nrows]; }
+  void resize_rows(int nr, int nc) { nrows = nr; ncols = nc; i.assign(nr + 1, 0); }
+  void swap(CSR& o) {
+    std::swap(nrows, o.nrows); std::swap(ncols, o.ncols);
+    i.swap(o.i); j.swap(o.j); a.swap(o.a);
+  }
+};
+
+// Strength pattern (hypre S): column indices only, no diagonal.
+struct Pattern {
+  int n = 0;
+  std::vector<int> i, j;
+};
+
+// Point types (hypre: C_PT 1, F_PT -1, Z_PT -2, SF_PT -3).
+enum { C_PT = 1, F_PT = -1, Z_PT = -2, SF_PT = -3 };
+
+// Relaxation types supported by this build (hypre numbering, par_relax.c:120).
+//   0  weighted Jacobi           18 l1-Jacobi
+//   3  hybrid GS forward         4  hybrid GS backward   6 hybrid symmetric GS
+//   13 hybrid l1-GS forward      14 hybrid l1-GS backward 8 hybrid l1 symmetric GS
+//   7  Jacobi via matvec         9  Gaussian elimination (coarsest level)
+struct AMGParams {
+  int max_levels = 25;
+  int max_coarse_size = 9;
+  int min_coarse_size = 0;
+  double strong_threshold = 0.25;
+  double max_row_sum = 0.9;
+  int coarsen_type = 10;          // 8 PMIS, 9 PMIS(seq rand), 10 HMIS
+  int measure_type = 0;
+  int interp_type = 6;            // 6 ext+i, 3 direct
+  int P_max_elmts = 4;
+  double trunc_factor = 0.0;
+  int relax_type[4] = {13, 13, 14, 9};   // [0]=all, [1]=down, [2]=up, [3]=coarsest
+  int num_sweeps[4] = {1, 1, 1, 1};
+  double relax_weight = 1.0;
+  double outer_weight = 1.0;
+  int relax_order = 0;            // 1 = C/F relaxation
+  int cycle_type = 1;             // 1 V, 2 W
+  int max_iter = 20;
+  int min_iter = 0;
+  double tol = 1e-6;
+  int converge_type = 0;
+  int print_level = 0;
+  int logging = 0;
+  // Number of contiguous row blocks for the hybrid (block-Jacobi / in-block GS)
+  // smoothers; hypre's CPU path uses num_threads for this (par_relax.c:4387).
+  int num_blocks = 1;
+  int agg_num_levels = 0;
+};
+
+struct Level {
+  CSR A;                        // operator on this level
+  CSR P;                        // interpolation to this level from level+1 (nrows = A.nrows)
+  CSR R;                        // R = P^T (kept explicitly for the GPU restriction)
+  std::vector<int> cf;          // CF marker (C_PT / F_PT), empty on coarsest
+  std::vector<double> l1;       // row norms for the l1 smoothers (may be empty)
+  std::vector<double> dinv;     // unused slot (Jacobi uses A's diagonal directly)
+};
+
+struct Hierarchy {
+  AMGParams prm;
+  std::vector<Level> lev;
+  // Dense coarsest operator for relax type 9 (row-major, par_gauss_elim.c:84).
+  int coarse_n = 0;
+  std::vector<double> coarse_dense;
+  double grid_complexity = 0, operator_complexity = 0;
+  std::string log;
+};
+
+// ---- generators (parcsr_ls/par_laplace.c:15, par_laplace_27pt.c) ----
+// 7-point Laplacian on nx*ny*nz with coefficients (cx,cy,cz), single partition,
+// same row/entry ordering as GenerateLaplacian with P=Q=R=1.
+void generate_laplacian_7pt(int nx, int ny, int nz, double cx, double cy, double cz, CSR& A);
+void generate_laplacian_27pt(int nx, int ny, int nz, CSR& A);
+
+// ---- setup building blocks ----
+void create_strength(const CSR& A, double thr, double max_row_sum, Pattern& S);
+void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf);
+void coarsen_hmis(const Pattern& S, int measure_type, std::vector<int>& cf);
+void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
+                        double trunc_factor, int max_elmts, CSR& P);
+void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
+                         double trunc_factor, int max_elmts, CSR& P);
+void truncate_rows(CSR& P, double tol, int max_elmts);
+void transpose(const CSR& A, CSR& AT);
+void rap(const CSR& P, const CSR& A, CSR& RAP);
+void compute_l1_norms(const CSR& A, int option, const int* cf, int num_blocks,
+                      std::vector<double>& l1);
+
+// Full setup; returns 0 on success.
+int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H);
+
+// Park-Miller generator used by hypre_Rand (utilities/random.c:40-71).
+double hypre_rand_at(int64_t k, int seed);  // value of the (k+1)-th draw after SeedRand(seed)
+
+}  // namespace hve

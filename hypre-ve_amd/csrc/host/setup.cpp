@@ -1,0 +1,755 @@
+// BoomerAMG setup phase on the host: strength, PMIS coarsening, extended+i
+// interpolation, truncation and the Galerkin product.  Every routine follows the
+// single-process (num_procs == 1) branch of the cited hypre routine statement for
+// statement, including entry order inside rows and the floating-point
+// accumulation order, so that the resulting hierarchy (and therefore the
+// complexities and convergence the reference reports) is reproduced exactly.
+#include "hve_host.hpp"
+#include "layout.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+namespace hve {
+
+// ---------------------------------------------------------------------------
+// Problem generators
+// ---------------------------------------------------------------------------
+
+// parcsr_ls/par_laplace.c:15 GenerateLaplacian with P=Q=R=1, values from
+// test/ij.c:7790 (values[0] = 2cx+2cy+2cz for dims > 1, off-diag -c).
+void generate_laplacian_7pt(int nx, int ny, int nz, double cx, double cy, double cz, CSR& A) {
+  const int64_t n64 = (int64_t)nx * ny * nz;
+  if (n64 > 0x7fffffff) throw std::runtime_error("grid too large for 32-bit rows");
+  const int n = (int)n64;
+  double v0 = 0.0;
+  if (nx > 1) v0 += 2.0 * cx;
+  if (ny > 1) v0 += 2.0 * cy;
+  if (nz > 1) v0 += 2.0 * cz;
+  const double v1 = -cx, v2 = -cy, v3 = -cz;
+  A.resize_rows(n, n);
+  // first pass: row lengths (boundary-dependent), computed per row in parallel
+  const int64_t nxny = (int64_t)nx * ny;
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < n; ++r) {
+    int ix = r % nx, iy = (r / nx) % ny, iz = (int)(r / nxny);
+    int c = 1 + (iz > 0) + (iy > 0) + (ix > 0) + (ix + 1 < nx) + (iy + 1 < ny) + (iz + 1 < nz);
+    A.i[r + 1] = c;
+  }
+  for (int r = 0; r < n; ++r) A.i[r + 1] += A.i[r];
+  if ((int64_t)A.i[n] < 0) throw std::runtime_error("nnz overflow");
+  A.j.resize(A.i[n]);
+  A.a.resize(A.i[n]);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < n; ++r) {
+    int ix = r % nx, iy = (r / nx) % ny, iz = (int)(r / nxny);
+    int k = A.i[r];
+    A.j[k] = r; A.a[k++] = v0;
+    if (iz > 0) { A.j[k] = r - (int)nxny; A.a[k++] = v3; }
+    if (iy > 0) { A.j[k] = r - nx; A.a[k++] = v2; }
+    if (ix > 0) { A.j[k] = r - 1; A.a[k++] = v1; }
+    if (ix + 1 < nx) { A.j[k] = r + 1; A.a[k++] = v1; }
+    if (iy + 1 < ny) { A.j[k] = r + nx; A.a[k++] = v2; }
+    if (iz + 1 < nz) { A.j[k] = r + (int)nxny; A.a[k++] = v3; }
+  }
+}
+
+// parcsr_ls/par_laplace_27pt.c GenerateLaplacian27pt (P=Q=R=1): diagonal 26,
+// every neighbour in the 3x3x3 box -1, neighbours visited z-major, then y, then x.
+void generate_laplacian_27pt(int nx, int ny, int nz, CSR& A) {
+  const int64_t n64 = (int64_t)nx * ny * nz;
+  if (n64 > 0x7fffffff) throw std::runtime_error("grid too large for 32-bit rows");
+  const int n = (int)n64;
+  const int64_t nxny = (int64_t)nx * ny;
+  A.resize_rows(n, n);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < n; ++r) {
+    int ix = r % nx, iy = (r / nx) % ny, iz = (int)(r / nxny);
+    int c = 0;
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          int x = ix + dx, y = iy + dy, z = iz + dz;
+          if (x >= 0 && x < nx && y >= 0 && y < ny && z >= 0 && z < nz) ++c;
+        }
+    A.i[r + 1] = c;
+  }
+  for (int r = 0; r < n; ++r) A.i[r + 1] += A.i[r];
+  if (A.i[n] < 0) throw std::runtime_error("nnz overflow (use more GPUs)");
+  A.j.resize(A.i[n]);
+  A.a.resize(A.i[n]);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < n; ++r) {
+    int ix = r % nx, iy = (r / nx) % ny, iz = (int)(r / nxny);
+    int k = A.i[r];
+    A.j[k] = r; A.a[k++] = 26.0;
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (!dx && !dy && !dz) continue;
+          int x = ix + dx, y = iy + dy, z = iz + dz;
+          if (x >= 0 && x < nx && y >= 0 && y < ny && z >= 0 && z < nz) {
+            A.j[k] = (int)(((int64_t)z * ny + y) * nx + x);
+            A.a[k++] = -1.0;
+          }
+        }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// hypre_Rand: Park-Miller minimal standard, a = 16807, m = 2^31-1.
+// utilities/random.c:40 (SeedRand), :56 (RandI via Schrage), :71 (Rand = RandI/m).
+// The k-th draw after SeedRand(s) is a^(k+1) * s mod m; jump-ahead lets the
+// measure initialisation run in parallel while producing the identical stream.
+// ---------------------------------------------------------------------------
+static const uint64_t kRandA = 16807ULL, kRandM = 2147483647ULL;
+static uint64_t powmod(uint64_t b, uint64_t e, uint64_t m) {
+  uint64_t r = 1 % m;
+  b %= m;
+  while (e) {
+    if (e & 1) r = (r * b) % m;
+    b = (b * b) % m;
+    e >>= 1;
+  }
+  return r;
+}
+double hypre_rand_at(int64_t k, int seed) {
+  uint64_t s = (uint64_t)seed;
+  if (seed < 1) s = 1; else if (s >= kRandM) s = kRandM - 1;
+  uint64_t v = (powmod(kRandA, (uint64_t)k + 1, kRandM) * s) % kRandM;
+  return (double)v / (double)kRandM;
+}
+
+// ---------------------------------------------------------------------------
+// Strength of connection: par_strength.c:80 hypre_BoomerAMGCreateSHost,
+// num_functions == 1, no offd part.  The first stored entry of each row is
+// the diagonal and is never in S.
+// ---------------------------------------------------------------------------
+void create_strength(const CSR& A, double thr, double max_row_sum, Pattern& S) {
+  const int n = A.nrows;
+  S.n = n;
+  S.i.assign(n + 1, 0);
+  std::vector<int> cnt(n, 0);
+  // first pass: count (row-parallel; the per-row decisions are independent)
+  std::vector<unsigned char> keep(A.nnz(), 0);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < n; ++r) {
+    const int b = A.i[r], e = A.i[r + 1];
+    const double diag = A.a[b];
+    double row_scale = 0.0, row_sum = diag;
+    if (diag < 0) {
+      for (int k = b + 1; k < e; ++k) { row_scale = std::max(row_scale, A.a[k]); row_sum += A.a[k]; }
+    } else {
+      for (int k = b + 1; k < e; ++k) { row_scale = std::min(row_scale, A.a[k]); row_sum += A.a[k]; }
+    }
+    int c = 0;
+    if ((std::fabs(row_sum) > std::fabs(diag) * max_row_sum) && (max_row_sum < 1.0)) {
+      // all dependencies weak
+    } else if (diag < 0) {
+      for (int k = b + 1; k < e; ++k)
+        if (!(A.a[k] <= thr * row_scale)) { keep[k] = 1; ++c; }
+    } else {
+      for (int k = b + 1; k < e; ++k)
+        if (!(A.a[k] >= thr * row_scale)) { keep[k] = 1; ++c; }
+    }
+    cnt[r] = c;
+  }
+  for (int r = 0; r < n; ++r) S.i[r + 1] = S.i[r] + cnt[r];
+  S.j.resize(S.i[n]);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < n; ++r) {
+    int o = S.i[r];
+    for (int k = A.i[r] + 1; k < A.i[r + 1]; ++k)
+      if (keep[k]) S.j[o++] = A.j[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// PMIS coarsening: par_coarsen.c:2031 hypre_BoomerAMGCoarsenPMISHost, one
+// process.  cf_init 0 (coarsen_type 8), 2 (type 9, sequential random stream),
+// 1 (HMIS second stage: cf holds the first-pass C points).
+// ---------------------------------------------------------------------------
+void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
+  const int n = S.n;
+  std::vector<double> measure(n, 0.0);
+  // column counts of S (number of points each point influences)
+  {
+    std::vector<int> mcount(n, 0);
+    for (int64_t k = 0; k < (int64_t)S.j.size(); ++k) mcount[S.j[k]]++;
+#pragma omp parallel for schedule(static)
+    for (int r = 0; r < n; ++r) measure[r] = (double)mcount[r];
+  }
+  // hypre_BoomerAMGIndepSetInit (par_indepset.c:25): seed 2747 + my_id (0),
+  // one hypre_Rand() per local row in row order (first_row_index = 0).
+  {
+    const int seed = 2747;
+#pragma omp parallel
+    {
+#ifdef _OPENMP
+      int t = omp_get_thread_num(), nt = omp_get_num_threads();
+#else
+      int t = 0, nt = 1;
+#endif
+      int64_t chunk = (n + nt - 1) / nt;
+      int64_t b = std::min<int64_t>((int64_t)t * chunk, n), e = std::min<int64_t>(b + chunk, n);
+      if (b < e) {
+        uint64_t s = (powmod(kRandA, (uint64_t)b + 1, kRandM) * (uint64_t)seed) % kRandM;
+        for (int64_t r = b; r < e; ++r) {
+          measure[r] += (double)s / (double)kRandM;
+          s = (s * kRandA) % kRandM;
+        }
+      }
+    }
+  }
+  std::vector<int> graph;
+  graph.reserve(n);
+  if (cf_init == 1) {
+    // CF from the first (Ruge) pass: C points keep 1, others reset to 0/F.
+    for (int r = 0; r < n; ++r) {
+      if (cf[r] != SF_PT) {
+        if (cf[r] == -1) cf[r] = 0;  // no offd in a single process
+        if (cf[r] == Z_PT) {
+          if (measure[r] >= 1.0 || S.i[r + 1] - S.i[r] > 0) { cf[r] = 0; graph.push_back(r); }
+          else cf[r] = F_PT;
+        } else {
+          graph.push_back(r);
+        }
+      } else {
+        measure[r] = 0;
+      }
+    }
+  } else {
+    cf.assign(n, 0);
+    for (int r = 0; r < n; ++r) {
+      if (S.i[r + 1] - S.i[r] == 0) {
+        cf[r] = SF_PT;
+        measure[r] = 0;
+      } else {
+        graph.push_back(r);
+      }
+    }
+  }
+  std::vector<int> graph2;
+  graph2.reserve(n);
+  int iter = 0;
+  while (!graph.empty()) {
+    const int gs = (int)graph.size();
+    if (!cf_init || iter) {
+#pragma omp parallel for schedule(static)
+      for (int ig = 0; ig < gs; ++ig) {
+        int i = graph[ig];
+        if (measure[i] > 1) cf[i] = 1;
+      }
+      // remove nodes from the initial independent set (only writes 0: order-free)
+#pragma omp parallel for schedule(static)
+      for (int ig = 0; ig < gs; ++ig) {
+        int i = graph[ig];
+        if (measure[i] > 1) {
+          for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
+            int j = S.j[k];
+            if (measure[j] > 1) {
+              if (measure[i] > measure[j]) {
+#pragma omp atomic write
+                cf[j] = 0;
+              } else if (measure[j] > measure[i]) {
+#pragma omp atomic write
+                cf[i] = 0;
+              }
+            }
+          }
+        }
+      }
+    }
+    ++iter;
+    // set C and F points
+#pragma omp parallel for schedule(static)
+    for (int ig = 0; ig < gs; ++ig) {
+      int i = graph[ig];
+      if (measure[i] < 1) cf[i] = F_PT;
+      if (cf[i] > 0) {
+        cf[i] = C_PT;
+      } else {
+        for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
+          int j = S.j[k];
+          if (cf[j] > 0) { cf[i] = F_PT; break; }
+        }
+      }
+    }
+    graph2.clear();
+    for (int ig = 0; ig < gs; ++ig) {
+      int i = graph[ig];
+      if (cf[i] != 0) measure[i] = 0;
+      else graph2.push_back(i);
+    }
+    graph.swap(graph2);
+  }
+}
+
+void coarsen_hmis(const Pattern& /*S*/, int /*measure_type*/, std::vector<int>& /*cf*/) {
+  throw std::runtime_error("coarsen_type 10 (HMIS) is not available yet: use 8 (PMIS) or 9");
+}
+
+// ---------------------------------------------------------------------------
+// Truncation: parcsr_mv/par_csr_matrix.c:2671 hypre_ParCSRMatrixTruncate with
+// rescale = 1, nrm_type = 0 (inf-norm), one thread, no offd.
+// hypre_qsort2_abs (utilities/hypre_qsort.c:367) is reproduced exactly because
+// the kept entries among equal magnitudes depend on its pivoting.
+// ---------------------------------------------------------------------------
+static void qsort2_abs(int* v, double* w, int left, int right) {
+  if (left >= right) return;
+  auto swap2 = [&](int a, int b) { std::swap(v[a], v[b]); std::swap(w[a], w[b]); };
+  swap2(left, (left + right) / 2);
+  int last = left;
+  for (int i = left + 1; i <= right; ++i)
+    if (std::fabs(w[i]) > std::fabs(w[left])) swap2(++last, i);
+  swap2(left, last);
+  qsort2_abs(v, w, left, last - 1);
+  qsort2_abs(v, w, last + 1, right);
+}
+
+void truncate_rows(CSR& P, double tol, int max_elmts) {
+  if (tol <= 0.0 && max_elmts == 0) return;
+  const int n = P.nrows;
+  std::vector<int> ni(n + 1, 0);
+  std::vector<int> nj;
+  std::vector<double> na;
+  nj.reserve(P.j.size());
+  na.reserve(P.a.size());
+  std::vector<int> rj;
+  std::vector<double> ra;
+  for (int r = 0; r < n; ++r) {
+    rj.assign(P.j.begin() + P.i[r], P.j.begin() + P.i[r + 1]);
+    ra.assign(P.a.begin() + P.i[r], P.a.begin() + P.i[r + 1]);
+    if (tol > 0) {
+      double row_nrm = 0;
+      for (double x : ra) row_nrm = (row_nrm < std::fabs(x)) ? std::fabs(x) : row_nrm;
+      const double drop = tol * row_nrm;
+      double row_sum = 0, scale = 0;
+      std::vector<int> kj;
+      std::vector<double> ka;
+      for (size_t k = 0; k < ra.size(); ++k) {
+        row_sum += ra[k];
+        if (!(std::fabs(ra[k]) < drop)) { scale += ra[k]; kj.push_back(rj[k]); ka.push_back(ra[k]); }
+      }
+      if (scale != 0. && scale != row_sum) {
+        scale = row_sum / scale;
+        for (double& x : ka) x *= scale;
+      }
+      rj.swap(kj);
+      ra.swap(ka);
+    }
+    if (max_elmts > 0 && (int)ra.size() > max_elmts) {
+      double row_sum = 0;
+      for (double x : ra) row_sum += x;
+      qsort2_abs(rj.data(), ra.data(), 0, (int)ra.size() - 1);
+      double scale = 0;
+      for (int k = 0; k < max_elmts; ++k) scale += ra[k];
+      rj.resize(max_elmts);
+      ra.resize(max_elmts);
+      if (scale != 0. && scale != row_sum) {
+        scale = row_sum / scale;
+        for (double& x : ra) x *= scale;
+      }
+    }
+    nj.insert(nj.end(), rj.begin(), rj.end());
+    na.insert(na.end(), ra.begin(), ra.end());
+    ni[r + 1] = (int)nj.size();
+  }
+  P.i.swap(ni);
+  P.j.swap(nj);
+  P.a.swap(na);
+}
+
+// ---------------------------------------------------------------------------
+// Extended+i interpolation: par_lr_interp.c:1041
+// hypre_BoomerAMGBuildExtPIInterpHost, single process, one thread.
+// ---------------------------------------------------------------------------
+void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
+                        double trunc_factor, int max_elmts, CSR& P) {
+  const int n = A.nrows;
+  std::vector<int> fine_to_coarse(n, -1);
+  std::vector<int> P_marker(n, -1);
+  P.resize_rows(n, 0);
+  // first pass: size of P and fine_to_coarse
+  int jj_counter = 0, coarse_counter = 0;
+  for (int i = 0; i < n; ++i) {
+    P.i[i] = jj_counter;
+    if (cf[i] >= 0) {
+      jj_counter++;
+      fine_to_coarse[i] = coarse_counter++;
+    } else if (cf[i] != SF_PT) {
+      for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+        int i1 = S.j[jj];
+        if (cf[i1] >= 0) {
+          if (P_marker[i1] < P.i[i]) { P_marker[i1] = jj_counter; jj_counter++; }
+        } else if (cf[i1] != SF_PT) {
+          for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+            int k1 = S.j[kk];
+            if (cf[k1] >= 0 && P_marker[k1] < P.i[i]) { P_marker[k1] = jj_counter; jj_counter++; }
+          }
+        }
+      }
+    }
+  }
+  P.i[n] = jj_counter;
+  P.ncols = coarse_counter;
+  P.j.assign(jj_counter, 0);
+  P.a.assign(jj_counter, 0.0);
+  std::fill(P_marker.begin(), P_marker.end(), -1);
+  int strong_f_marker = -2;
+  for (int i = 0; i < n; ++i) {
+    const int jj_begin_row = P.i[i];
+    int jc = jj_begin_row;
+    if (cf[i] >= 0) {
+      P.j[jc] = fine_to_coarse[i];
+      P.a[jc] = 1.0;
+      jc++;
+    } else if (cf[i] != SF_PT) {
+      strong_f_marker--;
+      for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+        int i1 = S.j[jj];
+        if (cf[i1] >= 0) {
+          if (P_marker[i1] < jj_begin_row) {
+            P_marker[i1] = jc; P.j[jc] = fine_to_coarse[i1]; P.a[jc] = 0.0; jc++;
+          }
+        } else if (cf[i1] != SF_PT) {
+          P_marker[i1] = strong_f_marker;
+          for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+            int k1 = S.j[kk];
+            if (cf[k1] >= 0 && P_marker[k1] < jj_begin_row) {
+              P_marker[k1] = jc; P.j[jc] = fine_to_coarse[k1]; P.a[jc] = 0.0; jc++;
+            }
+          }
+        }
+      }
+      const int jj_end_row = jc;
+      double diagonal = A.a[A.i[i]];
+      for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
+        int i1 = A.j[jj];
+        if (P_marker[i1] >= jj_begin_row) {
+          P.a[P_marker[i1]] += A.a[jj];
+        } else if (P_marker[i1] == strong_f_marker) {
+          double sum = 0.0;
+          int sgn = 1;
+          if (A.a[A.i[i1]] < 0) sgn = -1;
+          for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
+            int i2 = A.j[jj1];
+            if ((P_marker[i2] >= jj_begin_row || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
+          }
+          if (sum != 0) {
+            double distribute = A.a[jj] / sum;
+            for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
+              int i2 = A.j[jj1];
+              if (P_marker[i2] >= jj_begin_row && (sgn * A.a[jj1]) < 0) P.a[P_marker[i2]] += distribute * A.a[jj1];
+              if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
+            }
+          } else {
+            diagonal += A.a[jj];
+          }
+        } else if (cf[i1] != SF_PT) {
+          diagonal += A.a[jj];
+        }
+      }
+      if (diagonal) {
+        for (int jj = jj_begin_row; jj < jj_end_row; ++jj) P.a[jj] /= -diagonal;
+      }
+    }
+    strong_f_marker--;
+  }
+  if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+  for (int i = 0; i < n; ++i)
+    if (cf[i] == SF_PT) cf[i] = F_PT;
+}
+
+// Direct interpolation (interp_type 3): par_interp.c hypre_BoomerAMGBuildDirInterp
+// host path, one process.  Weights from strong C neighbours, positive and
+// negative off-diagonals distributed separately.
+void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
+                         double trunc_factor, int max_elmts, CSR& P) {
+  const int n = A.nrows;
+  std::vector<int> fine_to_coarse(n, -1);
+  P.resize_rows(n, 0);
+  int cc = 0;
+  for (int i = 0; i < n; ++i) {
+    int c = 0;
+    if (cf[i] >= 0) { c = 1; fine_to_coarse[i] = cc++; }
+    else for (int k = S.i[i]; k < S.i[i + 1]; ++k) if (cf[S.j[k]] >= 0) ++c;
+    P.i[i + 1] = P.i[i] + c;
+  }
+  P.ncols = cc;
+  P.j.assign(P.i[n], 0);
+  P.a.assign(P.i[n], 0.0);
+  std::vector<int> P_marker(n, -1);
+  // par_interp.c:2008: alfa/beta are initialised once and carried across rows
+  // whose strong-C sums vanish (single-thread semantics).
+  double alfa = 1.0, beta = 1.0;
+  for (int i = 0; i < n; ++i) {
+    int jc = P.i[i];
+    if (cf[i] >= 0) { P.j[jc] = fine_to_coarse[i]; P.a[jc] = 1.0; continue; }
+    const int begin = jc;
+    for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
+      int i1 = S.j[k];
+      if (cf[i1] >= 0) { P_marker[i1] = jc; P.j[jc] = fine_to_coarse[i1]; P.a[jc] = 0.0; ++jc; }
+    }
+    const int end = jc;
+    const double diagonal = A.a[A.i[i]];
+    double sum_N_pos = 0, sum_N_neg = 0, sum_P_pos = 0, sum_P_neg = 0;
+    for (int k = A.i[i] + 1; k < A.i[i + 1]; ++k) {
+      int i1 = A.j[k];
+      double v = A.a[k];
+      if (v > 0) sum_N_pos += v; else sum_N_neg += v;
+      if (P_marker[i1] >= begin) {
+        P.a[P_marker[i1]] += v;
+        if (v > 0) sum_P_pos += v; else sum_P_neg += v;
+      }
+    }
+    if (sum_P_neg) alfa = sum_N_neg / sum_P_neg / diagonal;
+    if (sum_P_pos) beta = sum_N_pos / sum_P_pos / diagonal;
+    for (int k = begin; k < end; ++k) {
+      if (P.a[k] > 0) P.a[k] *= -beta; else P.a[k] *= -alfa;
+    }
+  }
+  if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+  for (int i = 0; i < n; ++i)
+    if (cf[i] == SF_PT) cf[i] = F_PT;
+}
+
+// ---------------------------------------------------------------------------
+// Transpose: seq_mv/csr_matop.c:578 (counting sort; rows of A^T list the
+// original row indices in ascending order).
+// ---------------------------------------------------------------------------
+void transpose(const CSR& A, CSR& AT) {
+  AT.resize_rows(A.ncols, A.nrows);
+  for (int64_t k = 0; k < A.nnz(); ++k) AT.i[A.j[k] + 1]++;
+  for (int r = 0; r < A.ncols; ++r) AT.i[r + 1] += AT.i[r];
+  AT.j.resize(A.nnz());
+  AT.a.resize(A.nnz());
+  std::vector<int> pos(AT.i.begin(), AT.i.end() - 1);
+  for (int r = 0; r < A.nrows; ++r)
+    for (int k = A.i[r]; k < A.i[r + 1]; ++k) {
+      int c = A.j[k];
+      AT.j[pos[c]] = r;
+      AT.a[pos[c]] = A.a[k];
+      pos[c]++;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Galerkin product RAP = P^T A P: par_rap.c:27 hypre_BoomerAMGBuildCoarseOperatorKT,
+// single process (the RA row is formed first, then RA*P, each with first-touch
+// column order and the diagonal placed first).  Parallel over coarse rows with
+// the row structure computed in a first pass.
+// ---------------------------------------------------------------------------
+void rap(const CSR& P, const CSR& A, CSR& C) {
+  CSR R;
+  transpose(P, R);
+  const int nc = P.ncols;
+  C.resize_rows(nc, nc);
+  std::vector<int> rowlen(nc, 0);
+  // Each thread keeps its own markers.  Two passes: sizes, then values.
+  for (int pass = 0; pass < 2; ++pass) {
+    if (pass == 1) {
+      for (int r = 0; r < nc; ++r) C.i[r + 1] = C.i[r] + rowlen[r];
+      C.j.assign(C.i[nc], 0);
+      C.a.assign(C.i[nc], 0.0);
+    }
+#pragma omp parallel
+    {
+      std::vector<int> A_marker(A.ncols, -1), P_marker(nc, -1);
+      std::vector<int> ra_j;
+      std::vector<double> ra_a;
+      ra_j.reserve(4096);
+      ra_a.reserve(4096);
+      std::vector<int> tj;
+      std::vector<double> ta;
+#pragma omp for schedule(dynamic, 256)
+      for (int ic = 0; ic < nc; ++ic) {
+        ra_j.clear();
+        ra_a.clear();
+        for (int jj1 = R.i[ic]; jj1 < R.i[ic + 1]; ++jj1) {
+          const int i1 = R.j[jj1];
+          const double r_entry = R.a[jj1];
+          for (int jj2 = A.i[i1]; jj2 < A.i[i1 + 1]; ++jj2) {
+            const int i2 = A.j[jj2];
+            const int marker = A_marker[i2];
+            if (marker < 0) {
+              A_marker[i2] = (int)ra_j.size();
+              ra_j.push_back(i2);
+              ra_a.push_back(r_entry * A.a[jj2]);
+            } else {
+              ra_a[marker] += r_entry * A.a[jj2];
+            }
+          }
+        }
+        for (int i2 : ra_j) A_marker[i2] = -1;
+        tj.clear();
+        ta.clear();
+        P_marker[ic] = 0;
+        tj.push_back(ic);
+        ta.push_back(0.0);
+        for (size_t q = 0; q < ra_j.size(); ++q) {
+          const int i1 = ra_j[q];
+          const double rap_ = ra_a[q];
+          for (int jj2 = P.i[i1]; jj2 < P.i[i1 + 1]; ++jj2) {
+            const int i2 = P.j[jj2];
+            const int marker = P_marker[i2];
+            if (marker < 0) {
+              P_marker[i2] = (int)tj.size();
+              tj.push_back(i2);
+              ta.push_back(rap_ * P.a[jj2]);
+            } else {
+              ta[marker] += rap_ * P.a[jj2];
+            }
+          }
+        }
+        for (int c : tj) P_marker[c] = -1;
+        if (pass == 0) {
+          rowlen[ic] = (int)tj.size();
+        } else {
+          std::copy(tj.begin(), tj.end(), C.j.begin() + C.i[ic]);
+          std::copy(ta.begin(), ta.end(), C.a.begin() + C.i[ic]);
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// l1 norms: ams.c:571 (one thread) and ams.c:3398 (num_threads blocks).
+// option 1: full row l1 norm; option 4: |a_ii| + 0.5 * sum over off-block
+// entries, truncated to |a_ii| when <= 4/3 |a_ii|.  Negative-diagonal rows
+// get a negative norm (ams.c:760).
+// ---------------------------------------------------------------------------
+void compute_l1_norms(const CSR& A, int option, const int* cf, int num_blocks, std::vector<double>& l1) {
+  const int n = A.nrows;
+  l1.assign(n, 0.0);
+  const int nb = std::max(1, num_blocks);
+#pragma omp parallel for schedule(static)
+  for (int k = 0; k < nb; ++k) {
+    int size = n / nb, rest = n - size * nb;
+    int ns, ne;
+    if (k < rest) { ns = k * size + k; ne = (k + 1) * size + k + 1; }
+    else { ns = k * size + rest; ne = (k + 1) * size + rest; }
+    for (int i = ns; i < ne; ++i) {
+      double s = 0.0;
+      if (option == 1) {
+        for (int q = A.i[i]; q < A.i[i + 1]; ++q)
+          if (!cf || cf[i] == cf[A.j[q]]) s += std::fabs(A.a[q]);
+      } else if (option == 4) {
+        double diag = 0.0;
+        for (int q = A.i[i]; q < A.i[i + 1]; ++q) {
+          int c = A.j[q];
+          if ((c == i || c < ns || c >= ne) && (!cf || cf[i] == cf[c])) {
+            if (c == i) { diag = std::fabs(A.a[q]); s += std::fabs(A.a[q]); }
+            else s += 0.5 * std::fabs(A.a[q]);
+          }
+        }
+        if (s <= 4.0 / 3.0 * diag) s = diag;
+      }
+      l1[i] = s;
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    if (A.a[A.i[i]] < 0.0) l1[i] = -l1[i];
+}
+
+// ---------------------------------------------------------------------------
+// Setup driver: par_amg_setup.c:889-2880 (coarsening loop), :2990-3120 (l1 norms).
+// ---------------------------------------------------------------------------
+static bool uses_l1_gs(int t) { return t == 8 || t == 13 || t == 14; }
+
+int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
+  H = Hierarchy();
+  H.prm = prm_in;
+  AMGParams& prm = H.prm;
+  int coarsen_type = prm.coarsen_type;
+  H.lev.emplace_back();
+  H.lev[0].A = A0;
+  char buf[256];
+  int level = 0;
+  bool finished = prm.max_levels <= 1;
+  while (!finished) {
+    Level& L = H.lev[level];
+    const int fine_size = L.A.nrows;
+    Pattern S;
+    create_strength(L.A, prm.strong_threshold, prm.max_row_sum, S);
+    std::vector<int> cf;
+    if (coarsen_type == 8) coarsen_pmis(S, 0, cf);
+    else if (coarsen_type == 9) coarsen_pmis(S, 2, cf);
+    else if (coarsen_type == 10) coarsen_hmis(S, prm.measure_type, cf);
+    else throw std::runtime_error("unsupported coarsen_type " + std::to_string(coarsen_type));
+    int coarse_size = 0;
+    for (int v : cf) coarse_size += (v == 1);
+    if (coarse_size == 0 || coarse_size == fine_size) {
+      if (prm.relax_type[3] == 9 || prm.relax_type[3] == 99 || prm.relax_type[3] == 19 || prm.relax_type[3] == 98) {
+        prm.relax_type[3] = prm.relax_type[0];
+        prm.num_sweeps[3] = 1;
+      }
+      break;
+    }
+    if (coarse_size < prm.min_coarse_size) break;
+    CSR P;
+    if (prm.interp_type == 6) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
+    else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
+    else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));
+    CSR Ac;
+    rap(P, L.A, Ac);
+    L.cf.swap(cf);
+    L.P.swap(P);
+    transpose(L.P, L.R);
+    snprintf(buf, sizeof buf, "level %d: rows %d nnz %lld -> coarse %d (P nnz %lld)\n", level, fine_size,
+             (long long)L.A.nnz(), coarse_size, (long long)L.P.nnz());
+    H.log += buf;
+    H.lev.emplace_back();
+    H.lev[level + 1].A.swap(Ac);
+    ++level;
+    if (coarsen_type > 0 && coarse_size >= (int)(fine_size * 0.75)) {
+      // par_amg_setup.c:2858 switches to CLJP; not available in this build.
+      throw std::runtime_error("slow coarsening (coarse >= 0.75 fine) would switch to CLJP: unsupported");
+    }
+    if (level == prm.max_levels - 1 || coarse_size <= prm.max_coarse_size) finished = true;
+  }
+  const int nl = (int)H.lev.size();
+  // l1 norms for the smoothers that need them
+  for (int j = 0; j < nl; ++j) {
+    Level& L = H.lev[j];
+    const int* cfp = (prm.relax_order && !L.cf.empty()) ? L.cf.data() : nullptr;
+    if (j < nl - 1 && (uses_l1_gs(prm.relax_type[1]) || uses_l1_gs(prm.relax_type[2])))
+      compute_l1_norms(L.A, 4, cfp, prm.num_blocks, L.l1);
+    else if (j == nl - 1 && uses_l1_gs(prm.relax_type[3]))
+      compute_l1_norms(L.A, 4, nullptr, prm.num_blocks, L.l1);
+    if (j < nl - 1 && (prm.relax_type[1] == 18 || prm.relax_type[2] == 18))
+      compute_l1_norms(L.A, 1, cfp, 1, L.l1);
+    else if (j == nl - 1 && prm.relax_type[3] == 18)
+      compute_l1_norms(L.A, 1, nullptr, 1, L.l1);
+    // par_amg_setup.c:3122: relax type 7 scales by the diagonal (ams.c option 5)
+    if (prm.relax_type[1] == 7 || prm.relax_type[2] == 7 || (prm.relax_type[3] == 7 && j == nl - 1)) {
+      L.l1.resize(L.A.nrows);
+      for (int r = 0; r < L.A.nrows; ++r) {
+        double d = L.A.a[L.A.i[r]];
+        L.l1[r] = (d == 0.0) ? 1.0 : d;
+      }
+    }
+  }
+  // coarsest-level direct solve
+  if (nl > 1 && (prm.relax_type[3] == 9 || prm.relax_type[3] == 99 || prm.relax_type[3] == 19 ||
+                 prm.relax_type[3] == 98)) {
+    const CSR& Ac = H.lev[nl - 1].A;
+    if (Ac.nrows > 8192) throw std::runtime_error("coarsest level too large for the dense direct solve");
+    H.coarse_n = Ac.nrows;
+    csr_to_dense(Ac, H.coarse_dense);
+  }
+  double tot_rows = 0, tot_nnz = 0;
+  for (auto& L : H.lev) { tot_rows += L.A.nrows; tot_nnz += (double)L.A.nnz(); }
+  H.grid_complexity = tot_rows / H.lev[0].A.nrows;
+  H.operator_complexity = tot_nnz / (double)H.lev[0].A.nnz();
+  return 0;
+}
+
+}  // namespace hve

@@ -1,0 +1,455 @@
+"""Python binding of libhypreve.so (the C ABI in include/hypreve.h).
+
+This mirrors the reference's C interface one-to-one (HYPRE_IJ*, HYPRE_ParCSR*,
+HYPRE_BoomerAMG*, HYPRE_ParCSRPCG*, GenerateLaplacian) so tests and the bench
+drive the product exactly as a hypre user's C code would.  It adds no compute
+of its own: every solve-path operation runs in the HIP kernels of the library.
+The library refuses to run a solve without a GPU (HYPRE_Init fails), there is
+no CPU fallback.
+
+Reference: src/parcsr_ls/HYPRE_parcsr_ls.h, src/IJ_mv/HYPRE_IJ_mv.h,
+src/krylov/HYPRE_krylov.h (SX-Aurora/hypre-ve).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libhypreve.so")
+
+HYPRE_PARCSR = 5555
+HYPRE_MEMORY_HOST = 0
+HYPRE_MEMORY_DEVICE = 1
+HYPRE_ERROR_GENERIC = 1
+HYPRE_ERROR_ARG = 4
+HYPRE_ERROR_CONV = 256
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libhypreve.so in-tree (hipcc --offload-arch=gfx950)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-j8"], cwd=PKG_ROOT, check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: run `make -C hypre-ve_amd` (no fallback path exists)")
+        _lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        _declare(_lib)
+    return _lib
+
+
+_p = C.c_void_p
+_i = C.c_int
+_d = C.c_double
+_pi = C.POINTER(C.c_int)
+_pd = C.POINTER(C.c_double)
+_pi64 = C.POINTER(C.c_int64)
+
+SOLVER_FCN = C.CFUNCTYPE(_i, _p, _p, _p, _p)
+
+# (name, restype, argtypes) for every symbol include/hypreve.h declares
+SIGNATURES = [
+    ("HYPRE_Init", _i, []),
+    ("HYPRE_Finalize", _i, []),
+    ("HYPRE_SetMemoryLocation", _i, [_i]),
+    ("HYPRE_GetError", _i, []),
+    ("HYPRE_ClearAllErrors", _i, []),
+    ("HYPRE_CheckError", _i, [_i, _i]),
+    ("HYPRE_IJMatrixCreate", _i, [_p, _i, _i, _i, _i, C.POINTER(_p)]),
+    ("HYPRE_IJMatrixDestroy", _i, [_p]),
+    ("HYPRE_IJMatrixInitialize", _i, [_p]),
+    ("HYPRE_IJMatrixSetObjectType", _i, [_p, _i]),
+    ("HYPRE_IJMatrixSetValues", _i, [_p, _i, _pi, _pi, _pi, _pd]),
+    ("HYPRE_IJMatrixAddToValues", _i, [_p, _i, _pi, _pi, _pi, _pd]),
+    ("HYPRE_IJMatrixAssemble", _i, [_p]),
+    ("HYPRE_IJMatrixGetObject", _i, [_p, C.POINTER(_p)]),
+    ("HYPRE_IJVectorCreate", _i, [_p, _i, _i, C.POINTER(_p)]),
+    ("HYPRE_IJVectorDestroy", _i, [_p]),
+    ("HYPRE_IJVectorInitialize", _i, [_p]),
+    ("HYPRE_IJVectorSetObjectType", _i, [_p, _i]),
+    ("HYPRE_IJVectorSetValues", _i, [_p, _i, _pi, _pd]),
+    ("HYPRE_IJVectorGetValues", _i, [_p, _i, _pi, _pd]),
+    ("HYPRE_IJVectorAssemble", _i, [_p]),
+    ("HYPRE_IJVectorGetObject", _i, [_p, C.POINTER(_p)]),
+    ("HYPRE_ParCSRMatrixDestroy", _i, [_p]),
+    ("HYPRE_ParCSRMatrixGetLocalRange", _i, [_p, _pi, _pi, _pi, _pi]),
+    ("HYPRE_ParCSRMatrixMatvec", _i, [_d, _p, _p, _d, _p]),
+    ("HYPRE_ParCSRMatrixMatvecOutOfPlace", _i, [_d, _p, _p, _d, _p, _p]),
+    ("HYPRE_ParCSRMatrixMatvecT", _i, [_d, _p, _p, _d, _p]),
+    ("HYPRE_ParVectorCreate", _i, [_p, _i, _pi, C.POINTER(_p)]),
+    ("HYPRE_ParVectorInitialize", _i, [_p]),
+    ("HYPRE_ParVectorDestroy", _i, [_p]),
+    ("HYPRE_ParVectorSetConstantValues", _i, [_p, _d]),
+    ("HYPRE_ParVectorCopy", _i, [_p, _p]),
+    ("HYPRE_ParVectorScale", _i, [_d, _p]),
+    ("HYPRE_ParVectorAxpy", _i, [_d, _p, _p]),
+    ("HYPRE_ParVectorInnerProd", _i, [_p, _p, _pd]),
+    ("GenerateLaplacian", _p, [_p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _pd]),
+    ("GenerateLaplacian27pt", _p, [_p, _i, _i, _i, _i, _i, _i, _i, _i, _i, _pd]),
+    ("HYPRE_BoomerAMGCreate", _i, [C.POINTER(_p)]),
+    ("HYPRE_BoomerAMGDestroy", _i, [_p]),
+    ("HYPRE_BoomerAMGSetup", _i, [_p, _p, _p, _p]),
+    ("HYPRE_BoomerAMGSolve", _i, [_p, _p, _p, _p]),
+    ("HYPRE_BoomerAMGGetNumIterations", _i, [_p, _pi]),
+    ("HYPRE_BoomerAMGGetFinalRelativeResidualNorm", _i, [_p, _pd]),
+    ("HYPRE_BoomerAMGSetConvergeType", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetTol", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetMaxIter", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetMinIter", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetMaxCoarseSize", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetMinCoarseSize", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetMaxLevels", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetStrongThreshold", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetMaxRowSum", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetCoarsenType", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetMeasureType", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetAggNumLevels", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetInterpType", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetTruncFactor", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetPMaxElmts", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetCycleType", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetNumSweeps", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetCycleNumSweeps", _i, [_p, _i, _i]),
+    ("HYPRE_BoomerAMGSetRelaxType", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetCycleRelaxType", _i, [_p, _i, _i]),
+    ("HYPRE_BoomerAMGSetRelaxOrder", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetRelaxWt", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetOuterWt", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetPrintLevel", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetLogging", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGGetNumLevels", _i, [_p, _pi]),
+    ("HYPRE_ParCSRPCGCreate", _i, [_p, C.POINTER(_p)]),
+    ("HYPRE_ParCSRPCGDestroy", _i, [_p]),
+    ("HYPRE_ParCSRPCGSetup", _i, [_p, _p, _p, _p]),
+    ("HYPRE_ParCSRPCGSolve", _i, [_p, _p, _p, _p]),
+    ("HYPRE_ParCSRPCGSetTol", _i, [_p, _d]),
+    ("HYPRE_ParCSRPCGSetMaxIter", _i, [_p, _i]),
+    ("HYPRE_ParCSRPCGSetTwoNorm", _i, [_p, _i]),
+    ("HYPRE_ParCSRPCGSetPrecond", _i, [_p, _p, _p, _p]),
+    ("HYPRE_ParCSRPCGSetPrintLevel", _i, [_p, _i]),
+    ("HYPRE_ParCSRPCGGetNumIterations", _i, [_p, _pi]),
+    ("HYPRE_ParCSRPCGGetFinalRelativeResidualNorm", _i, [_p, _pd]),
+    ("hypreve_CommGetUniqueId", _i, [_p]),
+    ("hypreve_CommCreate", _i, [_i, _i, _p, C.POINTER(_p)]),
+    ("hypreve_CommDestroy", _i, [_p]),
+    ("hypreve_ParCSRMatrixCreateFromCSR", _i, [_p, _i, _i, _i, _pi, _pi, _pd, C.POINTER(_p)]),
+    ("hypreve_ParVectorDeviceData", _p, [_p]),
+    ("hypreve_ParVectorLocalSize", _i, [_p]),
+    ("hypreve_ParVectorCopyToHost", _i, [_p, _pd]),
+    ("hypreve_ParVectorCopyFromHost", _i, [_p, _pd]),
+    ("hypreve_ParVectorSetRandomValues", _i, [_p, _i]),
+    ("hypreve_BoomerAMGSetNumBlocks", _i, [_p, _i]),
+    ("hypreve_BoomerAMGSetUseGraph", _i, [_p, _i]),
+    ("hypreve_BoomerAMGGetComplexities", _i, [_p, _pd, _pd, _pd]),
+    ("hypreve_BoomerAMGGetLevelInfo", _i, [_p, _i, _pi, _pi64, _pi64]),
+    ("hypreve_BoomerAMGGetLevelMatrix", _i, [_p, _i, _i, _pi, _pi, _pi64, _pi, _pi, _pd]),
+    ("hypreve_BoomerAMGGetLevelVector", _i, [_p, _i, _i, _pi, _p]),
+    ("hypreve_BoomerAMGGetCoarseMatrix", _i, [_p, _pi, _pd]),
+    ("hypreve_BoomerAMGGetRelaxInfo", _i, [_p, _pi, _pi, _pd, _pi]),
+    ("hypreve_BoomerAMGSetupHost", _i, [_p, _p]),
+    ("hypreve_BoomerAMGCycle", _i, [_p, _p, _p]),
+    ("hypreve_BoomerAMGGetKernelStats", _i, [_p, _pd, _i]),
+    ("hypreve_BenchFineSpMV", _i, [_p, _i, _pd, _pd]),
+    ("hypreve_DeviceSynchronize", _i, []),
+    ("hypreve_BuildInfo", C.c_char_p, []),
+    ("hypreve_LastErrorMessage", C.c_char_p, []),
+]
+
+
+def _declare(L):
+    for name, res, args in SIGNATURES:
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+class HypreError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str = ""):
+    if rc:
+        msg = lib().hypreve_LastErrorMessage().decode()
+        lib().HYPRE_ClearAllErrors()
+        raise HypreError(f"{what} failed (hypre error {rc}): {msg}")
+
+
+def _ptr(a, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+# ---------------------------------------------------------------------------
+# thin object layer
+# ---------------------------------------------------------------------------
+class ParCSRMatrix:
+    def __init__(self, handle, n):
+        self.h = handle
+        self.n = n
+
+    @classmethod
+    def laplacian(cls, nx, ny, nz, cx=1.0, cy=1.0, cz=1.0):
+        """GenerateLaplacian as test/ij.c:7790 BuildParLaplacian calls it."""
+        v0 = (2.0 * cx if nx > 1 else 0.0) + (2.0 * cy if ny > 1 else 0.0) + (2.0 * cz if nz > 1 else 0.0)
+        vals = np.array([v0, -cx, -cy, -cz], dtype=np.float64)
+        h = lib().GenerateLaplacian(None, nx, ny, nz, 1, 1, 1, 0, 0, 0, _ptr(vals, C.c_double))
+        if not h:
+            check(lib().HYPRE_GetError() or 1, "GenerateLaplacian")
+        return cls(h, nx * ny * nz)
+
+    @classmethod
+    def laplacian27(cls, nx, ny, nz):
+        vals = np.array([26.0, -1.0], dtype=np.float64)
+        h = lib().GenerateLaplacian27pt(None, nx, ny, nz, 1, 1, 1, 0, 0, 0, _ptr(vals, C.c_double))
+        if not h:
+            check(lib().HYPRE_GetError() or 1, "GenerateLaplacian27pt")
+        return cls(h, nx * ny * nz)
+
+    @classmethod
+    def from_scipy(cls, A):
+        A = A.tocsr()
+        n = A.shape[0]
+        ip = np.ascontiguousarray(A.indptr, dtype=np.int32)
+        jj = np.ascontiguousarray(A.indices, dtype=np.int32)
+        vv = np.ascontiguousarray(A.data, dtype=np.float64)
+        h = _p()
+        check(lib().hypreve_ParCSRMatrixCreateFromCSR(None, 0, n, n, _ptr(ip, C.c_int), _ptr(jj, C.c_int),
+                                                      _ptr(vv, C.c_double), C.byref(h)), "CreateFromCSR")
+        return cls(h, n)
+
+    def matvec(self, alpha, x, beta, y):
+        check(lib().HYPRE_ParCSRMatrixMatvec(alpha, self.h, x.h, beta, y.h), "Matvec")
+
+    def destroy(self):
+        if self.h:
+            lib().HYPRE_ParCSRMatrixDestroy(self.h)
+            self.h = None
+
+
+class ParVector:
+    def __init__(self, n, data=None):
+        self.n = n
+        h = _p()
+        part = np.array([0, n], dtype=np.int32)
+        check(lib().HYPRE_ParVectorCreate(None, n, _ptr(part, C.c_int), C.byref(h)), "ParVectorCreate")
+        self.h = h
+        check(lib().HYPRE_ParVectorInitialize(h), "ParVectorInitialize")
+        if data is not None:
+            self.set(data)
+
+    def set(self, data):
+        a = np.ascontiguousarray(data, dtype=np.float64)
+        assert a.size == self.n
+        check(lib().hypreve_ParVectorCopyFromHost(self.h, _ptr(a, C.c_double)), "CopyFromHost")
+
+    def get(self):
+        out = np.empty(self.n, dtype=np.float64)
+        check(lib().hypreve_ParVectorCopyToHost(self.h, _ptr(out, C.c_double)), "CopyToHost")
+        return out
+
+    def fill(self, v):
+        check(lib().HYPRE_ParVectorSetConstantValues(self.h, v), "SetConstantValues")
+
+    def dot(self, other):
+        r = C.c_double()
+        check(lib().HYPRE_ParVectorInnerProd(self.h, other.h, C.byref(r)), "InnerProd")
+        return r.value
+
+    def destroy(self):
+        if self.h:
+            lib().HYPRE_ParVectorDestroy(self.h)
+            self.h = None
+
+
+class BoomerAMG:
+    """HYPRE_BoomerAMG* with keyword settings named like the Set* calls."""
+
+    _setters = {
+        "tol": ("HYPRE_BoomerAMGSetTol", float), "max_iter": ("HYPRE_BoomerAMGSetMaxIter", int),
+        "min_iter": ("HYPRE_BoomerAMGSetMinIter", int),
+        "max_coarse_size": ("HYPRE_BoomerAMGSetMaxCoarseSize", int),
+        "min_coarse_size": ("HYPRE_BoomerAMGSetMinCoarseSize", int),
+        "max_levels": ("HYPRE_BoomerAMGSetMaxLevels", int),
+        "strong_threshold": ("HYPRE_BoomerAMGSetStrongThreshold", float),
+        "max_row_sum": ("HYPRE_BoomerAMGSetMaxRowSum", float),
+        "coarsen_type": ("HYPRE_BoomerAMGSetCoarsenType", int),
+        "interp_type": ("HYPRE_BoomerAMGSetInterpType", int),
+        "trunc_factor": ("HYPRE_BoomerAMGSetTruncFactor", float),
+        "P_max_elmts": ("HYPRE_BoomerAMGSetPMaxElmts", int),
+        "cycle_type": ("HYPRE_BoomerAMGSetCycleType", int),
+        "num_sweeps": ("HYPRE_BoomerAMGSetNumSweeps", int),
+        "relax_type": ("HYPRE_BoomerAMGSetRelaxType", int),
+        "relax_order": ("HYPRE_BoomerAMGSetRelaxOrder", int),
+        "relax_wt": ("HYPRE_BoomerAMGSetRelaxWt", float), "outer_wt": ("HYPRE_BoomerAMGSetOuterWt", float),
+        "print_level": ("HYPRE_BoomerAMGSetPrintLevel", int), "converge_type": ("HYPRE_BoomerAMGSetConvergeType", int),
+        "num_blocks": ("hypreve_BoomerAMGSetNumBlocks", int), "use_graph": ("hypreve_BoomerAMGSetUseGraph", int),
+    }
+
+    def __init__(self, **kw):
+        h = _p()
+        check(lib().HYPRE_BoomerAMGCreate(C.byref(h)), "BoomerAMGCreate")
+        self.h = h
+        self.set(**kw)
+
+    def set(self, **kw):
+        for k, v in kw.items():
+            if k == "cycle_relax_type":
+                for kk, t in v.items():
+                    check(lib().HYPRE_BoomerAMGSetCycleRelaxType(self.h, int(t), int(kk)), k)
+                continue
+            if k == "cycle_num_sweeps":
+                for kk, t in v.items():
+                    check(lib().HYPRE_BoomerAMGSetCycleNumSweeps(self.h, int(t), int(kk)), k)
+                continue
+            fn, ty = self._setters[k]
+            check(getattr(lib(), fn)(self.h, ty(v)), fn)
+
+    def setup(self, A, b=None, x=None):
+        check(lib().HYPRE_BoomerAMGSetup(self.h, A.h, b.h if b else None, x.h if x else None), "BoomerAMGSetup")
+
+    def setup_host(self, A):
+        check(lib().hypreve_BoomerAMGSetupHost(self.h, A.h), "BoomerAMGSetupHost")
+
+    def solve(self, A, b, x, allow_conv_error=True):
+        rc = lib().HYPRE_BoomerAMGSolve(self.h, A.h, b.h, x.h)
+        if rc and not (allow_conv_error and rc == HYPRE_ERROR_CONV):
+            check(rc, "BoomerAMGSolve")
+        lib().HYPRE_ClearAllErrors()
+        return self.num_iterations(), self.final_rel_res()
+
+    def cycle(self, f, u):
+        check(lib().hypreve_BoomerAMGCycle(self.h, f.h, u.h), "BoomerAMGCycle")
+
+    def num_iterations(self):
+        v = C.c_int()
+        lib().HYPRE_BoomerAMGGetNumIterations(self.h, C.byref(v))
+        return v.value
+
+    def final_rel_res(self):
+        v = C.c_double()
+        lib().HYPRE_BoomerAMGGetFinalRelativeResidualNorm(self.h, C.byref(v))
+        return v.value
+
+    def num_levels(self):
+        v = C.c_int()
+        lib().HYPRE_BoomerAMGGetNumLevels(self.h, C.byref(v))
+        return v.value
+
+    def complexities(self):
+        g, o, c = C.c_double(), C.c_double(), C.c_double()
+        lib().hypreve_BoomerAMGGetComplexities(self.h, C.byref(g), C.byref(o), C.byref(c))
+        return g.value, o.value, c.value
+
+    def level_info(self, l):
+        r, a, p = C.c_int(), C.c_int64(), C.c_int64()
+        check(lib().hypreve_BoomerAMGGetLevelInfo(self.h, l, C.byref(r), C.byref(a), C.byref(p)), "GetLevelInfo")
+        return r.value, a.value, p.value
+
+    def level_matrix(self, l, which=0):
+        """(indptr, indices, data, shape) of A_l (which=0) or P_l (which=1)."""
+        nr, nc, nz = C.c_int(), C.c_int(), C.c_int64()
+        L = lib()
+        check(L.hypreve_BoomerAMGGetLevelMatrix(self.h, l, which, C.byref(nr), C.byref(nc), C.byref(nz),
+                                                None, None, None), "GetLevelMatrix")
+        ip = np.zeros(nr.value + 1, dtype=np.int32)
+        jj = np.zeros(max(1, nz.value), dtype=np.int32)
+        vv = np.zeros(max(1, nz.value), dtype=np.float64)
+        check(L.hypreve_BoomerAMGGetLevelMatrix(self.h, l, which, None, None, None, _ptr(ip, C.c_int),
+                                                _ptr(jj, C.c_int), _ptr(vv, C.c_double)), "GetLevelMatrix")
+        return ip, jj[: nz.value], vv[: nz.value], (nr.value, nc.value)
+
+    def level_vector(self, l, which):
+        n = C.c_int()
+        check(lib().hypreve_BoomerAMGGetLevelVector(self.h, l, which, C.byref(n), None), "GetLevelVector")
+        out = np.zeros(n.value, dtype=np.int32 if which == 0 else np.float64)
+        if n.value:
+            lib().hypreve_BoomerAMGGetLevelVector(self.h, l, which, None, out.ctypes.data_as(C.c_void_p))
+        return out
+
+    def coarse_matrix(self):
+        n = C.c_int()
+        lib().hypreve_BoomerAMGGetCoarseMatrix(self.h, C.byref(n), None)
+        out = np.zeros(n.value * n.value, dtype=np.float64)
+        if n.value:
+            lib().hypreve_BoomerAMGGetCoarseMatrix(self.h, None, _ptr(out, C.c_double))
+        return out.reshape(n.value, n.value) if n.value else out
+
+    def relax_info(self):
+        rt = np.zeros(4, dtype=np.int32)
+        ns = np.zeros(4, dtype=np.int32)
+        w = np.zeros(2, dtype=np.float64)
+        misc = np.zeros(3, dtype=np.int32)
+        lib().hypreve_BoomerAMGGetRelaxInfo(self.h, _ptr(rt, C.c_int), _ptr(ns, C.c_int), _ptr(w, C.c_double),
+                                            _ptr(misc, C.c_int))
+        return dict(relax_type=rt.tolist(), num_sweeps=ns.tolist(), relax_weight=float(w[0]), omega=float(w[1]),
+                    relax_order=int(misc[0]), cycle_type=int(misc[1]), num_blocks=int(misc[2]))
+
+    def bench_fine_spmv(self, reps=20):
+        ms, by = C.c_double(), C.c_double()
+        check(lib().hypreve_BenchFineSpMV(self.h, reps, C.byref(ms), C.byref(by)), "BenchFineSpMV")
+        return ms.value, by.value
+
+    def destroy(self):
+        if self.h:
+            lib().HYPRE_BoomerAMGDestroy(self.h)
+            self.h = None
+
+
+class PCG:
+    def __init__(self, tol=1e-8, max_iter=1000, two_norm=1, print_level=0):
+        h = _p()
+        check(lib().HYPRE_ParCSRPCGCreate(None, C.byref(h)), "PCGCreate")
+        self.h = h
+        lib().HYPRE_ParCSRPCGSetTol(h, tol)
+        lib().HYPRE_ParCSRPCGSetMaxIter(h, max_iter)
+        lib().HYPRE_ParCSRPCGSetTwoNorm(h, two_norm)
+        lib().HYPRE_ParCSRPCGSetPrintLevel(h, print_level)
+        self.precond = None
+
+    def set_precond_amg(self, amg: BoomerAMG):
+        L = lib()
+        solve = C.cast(L.HYPRE_BoomerAMGSolve, C.c_void_p)
+        setup = C.cast(L.HYPRE_BoomerAMGSetup, C.c_void_p)
+        check(L.HYPRE_ParCSRPCGSetPrecond(self.h, solve, setup, amg.h), "PCGSetPrecond")
+        self.precond = amg
+
+    def setup(self, A, b, x):
+        check(lib().HYPRE_ParCSRPCGSetup(self.h, A.h, b.h, x.h), "PCGSetup")
+
+    def solve(self, A, b, x, allow_conv_error=True):
+        rc = lib().HYPRE_ParCSRPCGSolve(self.h, A.h, b.h, x.h)
+        if rc and not (allow_conv_error and rc == HYPRE_ERROR_CONV):
+            check(rc, "PCGSolve")
+        lib().HYPRE_ClearAllErrors()
+        it, r = C.c_int(), C.c_double()
+        lib().HYPRE_ParCSRPCGGetNumIterations(self.h, C.byref(it))
+        lib().HYPRE_ParCSRPCGGetFinalRelativeResidualNorm(self.h, C.byref(r))
+        return it.value, r.value
+
+    def destroy(self):
+        if self.h:
+            lib().HYPRE_ParCSRPCGDestroy(self.h)
+            self.h = None
+
+
+def init():
+    check(lib().HYPRE_Init(), "HYPRE_Init")
+
+
+def ij_amg_defaults(solver_id=0):
+    """BoomerAMG settings test/ij.c applies before its command-line options
+    (ij.c:1181-1199, 3365-3540): max_row_sum 1.0, tol 1e-8 (solver 0),
+    P_max_elmts 4, coarsen HMIS (10), ext+i (6), print level 3."""
+    return dict(max_row_sum=1.0, tol=1e-8 if solver_id == 0 else 0.0, max_iter=100 if solver_id == 0 else 1,
+                strong_threshold=0.25, trunc_factor=0.0, P_max_elmts=4, max_coarse_size=9, max_levels=25,
+                cycle_type=1, relax_wt=1.0, outer_wt=1.0)

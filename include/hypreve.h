@@ -1,0 +1,243 @@
+/*
+ * hypre-ve_amd: MI355X-native BoomerAMG solve path behind hypre's C interface.
+ *
+ * Drop-in boundary: every entry point below has the name, argument meaning and
+ * error behaviour of the reference's public function it replaces; the comment
+ * on each cites the reference declaration (SX-Aurora/hypre-ve, src/...:line).
+ * Plain C ABI: pointers and sizes only, no C++ or torch types.
+ *
+ * Memory model: HYPRE_ParVector / HYPRE_ParCSRMatrix data live in HBM
+ * (HYPRE_MEMORY_DEVICE).  IJ set/get-values arrays are host arrays unless
+ * HYPRE_SetMemoryLocation(HYPRE_MEMORY_DEVICE) was called, in which case they
+ * are device pointers (reference: utilities/HYPRE_utilities.h, HYPRE_SetMemoryLocation).
+ *
+ * Communicator: the reference takes an MPI_Comm.  This build has no MPI; an
+ * HYPRE_Comm is either HYPRE_COMM_SELF (one GPU) or a communicator created
+ * by hypreve_CommCreate() over RCCL (one process per GPU).
+ */
+#ifndef HYPREVE_H
+#define HYPREVE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* utilities/HYPRE_utilities.h: 32-bit ints, double reals (default build) */
+typedef int HYPRE_Int;
+typedef int HYPRE_BigInt;
+typedef double HYPRE_Real;
+typedef double HYPRE_Complex;
+
+typedef struct hypreve_comm_struct *HYPRE_Comm;
+#define HYPRE_COMM_SELF ((HYPRE_Comm)0)
+
+typedef struct hypre_Solver_struct *HYPRE_Solver;
+typedef struct hypre_ParCSRMatrix_struct *HYPRE_ParCSRMatrix;
+typedef struct hypre_ParVector_struct *HYPRE_ParVector;
+typedef struct hypre_IJMatrix_struct *HYPRE_IJMatrix;
+typedef struct hypre_IJVector_struct *HYPRE_IJVector;
+
+/* krylov/HYPRE_krylov.h:70 */
+typedef HYPRE_Int (*HYPRE_PtrToParSolverFcn)(HYPRE_Solver, HYPRE_ParCSRMatrix, HYPRE_ParVector,
+                                             HYPRE_ParVector);
+
+#define HYPRE_PARCSR 5555          /* IJ_mv/HYPRE_IJ_mv.h object type */
+#define HYPRE_MEMORY_HOST 0
+#define HYPRE_MEMORY_DEVICE 1
+
+/* error codes: utilities/HYPRE_utilities.h:80-86 */
+#define HYPRE_ERROR_GENERIC 1
+#define HYPRE_ERROR_MEMORY 2
+#define HYPRE_ERROR_ARG 4
+#define HYPRE_ERROR_CONV 256
+
+/* ---------------- utilities (utilities/HYPRE_utilities.h) ---------------- */
+HYPRE_Int HYPRE_Init(void);                                   /* HYPRE_utilities.h: HYPRE_Init */
+HYPRE_Int HYPRE_Finalize(void);                               /* HYPRE_utilities.h: HYPRE_Finalize */
+HYPRE_Int HYPRE_SetMemoryLocation(HYPRE_Int memory_location); /* HYPRE_utilities.h */
+HYPRE_Int HYPRE_GetError(void);                               /* HYPRE_utilities.h: HYPRE_GetError */
+HYPRE_Int HYPRE_ClearAllErrors(void);
+HYPRE_Int HYPRE_CheckError(HYPRE_Int hypre_ierr, HYPRE_Int hypre_error_code);
+
+/* ---------------- IJ interface (IJ_mv/HYPRE_IJ_mv.h) ---------------- */
+HYPRE_Int HYPRE_IJMatrixCreate(HYPRE_Comm comm, HYPRE_BigInt ilower, HYPRE_BigInt iupper,
+                               HYPRE_BigInt jlower, HYPRE_BigInt jupper,
+                               HYPRE_IJMatrix *matrix);                       /* :68 */
+HYPRE_Int HYPRE_IJMatrixDestroy(HYPRE_IJMatrix matrix);                       /* :80 */
+HYPRE_Int HYPRE_IJMatrixInitialize(HYPRE_IJMatrix matrix);                    /* :90 */
+HYPRE_Int HYPRE_IJMatrixSetObjectType(HYPRE_IJMatrix matrix, HYPRE_Int type); /* :235 */
+HYPRE_Int HYPRE_IJMatrixSetValues(HYPRE_IJMatrix matrix, HYPRE_Int nrows, HYPRE_Int *ncols,
+                                  const HYPRE_BigInt *rows, const HYPRE_BigInt *cols,
+                                  const HYPRE_Complex *values);               /* :127 */
+HYPRE_Int HYPRE_IJMatrixAddToValues(HYPRE_IJMatrix matrix, HYPRE_Int nrows, HYPRE_Int *ncols,
+                                    const HYPRE_BigInt *rows, const HYPRE_BigInt *cols,
+                                    const HYPRE_Complex *values);             /* :180 */
+HYPRE_Int HYPRE_IJMatrixAssemble(HYPRE_IJMatrix matrix);                      /* :200 */
+HYPRE_Int HYPRE_IJMatrixGetObject(HYPRE_IJMatrix matrix, void **object);      /* :259 */
+
+HYPRE_Int HYPRE_IJVectorCreate(HYPRE_Comm comm, HYPRE_BigInt jlower, HYPRE_BigInt jupper,
+                               HYPRE_IJVector *vector);                       /* :368 */
+HYPRE_Int HYPRE_IJVectorDestroy(HYPRE_IJVector vector);                       /* :378 */
+HYPRE_Int HYPRE_IJVectorInitialize(HYPRE_IJVector vector);                    /* :386 */
+HYPRE_Int HYPRE_IJVectorSetObjectType(HYPRE_IJVector vector, HYPRE_Int type);
+HYPRE_Int HYPRE_IJVectorSetValues(HYPRE_IJVector vector, HYPRE_Int nvalues,
+                                  const HYPRE_BigInt *indices,
+                                  const HYPRE_Complex *values);               /* :423 */
+HYPRE_Int HYPRE_IJVectorGetValues(HYPRE_IJVector vector, HYPRE_Int nvalues,
+                                  const HYPRE_BigInt *indices, HYPRE_Complex *values); /* :453 */
+HYPRE_Int HYPRE_IJVectorAssemble(HYPRE_IJVector vector);
+HYPRE_Int HYPRE_IJVectorGetObject(HYPRE_IJVector vector, void **object);
+
+/* ---------------- ParCSR (parcsr_mv/HYPRE_parcsr_mv.h) ---------------- */
+HYPRE_Int HYPRE_ParCSRMatrixDestroy(HYPRE_ParCSRMatrix matrix);
+HYPRE_Int HYPRE_ParCSRMatrixGetLocalRange(HYPRE_ParCSRMatrix matrix, HYPRE_BigInt *row_start,
+                                          HYPRE_BigInt *row_end, HYPRE_BigInt *col_start,
+                                          HYPRE_BigInt *col_end);
+/* :51  y = alpha*A*x + beta*y, on the GPU */
+HYPRE_Int HYPRE_ParCSRMatrixMatvec(HYPRE_Complex alpha, HYPRE_ParCSRMatrix A, HYPRE_ParVector x,
+                                   HYPRE_Complex beta, HYPRE_ParVector y);
+/* parcsr_mv/protos: hypre_ParCSRMatrixMatvecOutOfPlace  y = alpha*A*x + beta*b */
+HYPRE_Int HYPRE_ParCSRMatrixMatvecOutOfPlace(HYPRE_Complex alpha, HYPRE_ParCSRMatrix A,
+                                             HYPRE_ParVector x, HYPRE_Complex beta,
+                                             HYPRE_ParVector b, HYPRE_ParVector y);
+HYPRE_Int HYPRE_ParCSRMatrixMatvecT(HYPRE_Complex alpha, HYPRE_ParCSRMatrix A, HYPRE_ParVector x,
+                                    HYPRE_Complex beta, HYPRE_ParVector y);
+HYPRE_Int HYPRE_ParVectorCreate(HYPRE_Comm comm, HYPRE_BigInt global_size,
+                                HYPRE_BigInt *partitioning, HYPRE_ParVector *vector);
+HYPRE_Int HYPRE_ParVectorInitialize(HYPRE_ParVector vector);
+HYPRE_Int HYPRE_ParVectorDestroy(HYPRE_ParVector vector);
+HYPRE_Int HYPRE_ParVectorSetConstantValues(HYPRE_ParVector vector, HYPRE_Complex value);
+HYPRE_Int HYPRE_ParVectorCopy(HYPRE_ParVector x, HYPRE_ParVector y);
+HYPRE_Int HYPRE_ParVectorScale(HYPRE_Complex value, HYPRE_ParVector x);
+HYPRE_Int HYPRE_ParVectorAxpy(HYPRE_Complex alpha, HYPRE_ParVector x, HYPRE_ParVector y);
+HYPRE_Int HYPRE_ParVectorInnerProd(HYPRE_ParVector x, HYPRE_ParVector y, HYPRE_Real *prod); /* :64 */
+
+/* ---------------- generators (parcsr_ls/HYPRE_parcsr_ls.h) ---------------- */
+/* :4168 GenerateLaplacian (value[0..3] = diag, -cx, -cy, -cz); this rank owns
+ * grid block (p,q,r) of a P x Q x R process grid. */
+HYPRE_ParCSRMatrix GenerateLaplacian(HYPRE_Comm comm, HYPRE_BigInt nx, HYPRE_BigInt ny,
+                                     HYPRE_BigInt nz, HYPRE_Int P, HYPRE_Int Q, HYPRE_Int R,
+                                     HYPRE_Int p, HYPRE_Int q, HYPRE_Int r, HYPRE_Real *value);
+/* :4180 GenerateLaplacian27pt */
+HYPRE_ParCSRMatrix GenerateLaplacian27pt(HYPRE_Comm comm, HYPRE_BigInt nx, HYPRE_BigInt ny,
+                                         HYPRE_BigInt nz, HYPRE_Int P, HYPRE_Int Q, HYPRE_Int R,
+                                         HYPRE_Int p, HYPRE_Int q, HYPRE_Int r, HYPRE_Real *value);
+
+/* ---------------- BoomerAMG (parcsr_ls/HYPRE_parcsr_ls.h) ---------------- */
+HYPRE_Int HYPRE_BoomerAMGCreate(HYPRE_Solver *solver);                          /* :83 */
+HYPRE_Int HYPRE_BoomerAMGDestroy(HYPRE_Solver solver);                          /* :89 */
+HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver solver, HYPRE_ParCSRMatrix A, HYPRE_ParVector b,
+                               HYPRE_ParVector x);                              /* :100 */
+HYPRE_Int HYPRE_BoomerAMGSolve(HYPRE_Solver solver, HYPRE_ParCSRMatrix A, HYPRE_ParVector b,
+                               HYPRE_ParVector x);                              /* :115 */
+HYPRE_Int HYPRE_BoomerAMGGetNumIterations(HYPRE_Solver solver, HYPRE_Int *num_iterations); /* :155 */
+HYPRE_Int HYPRE_BoomerAMGGetFinalRelativeResidualNorm(HYPRE_Solver solver, HYPRE_Real *rel_resid_norm); /* :161 */
+HYPRE_Int HYPRE_BoomerAMGSetConvergeType(HYPRE_Solver solver, HYPRE_Int type);  /* :184 */
+HYPRE_Int HYPRE_BoomerAMGSetTol(HYPRE_Solver solver, HYPRE_Real tol);           /* :192 */
+HYPRE_Int HYPRE_BoomerAMGSetMaxIter(HYPRE_Solver solver, HYPRE_Int max_iter);   /* :200 */
+HYPRE_Int HYPRE_BoomerAMGSetMinIter(HYPRE_Solver solver, HYPRE_Int min_iter);   /* :206 */
+HYPRE_Int HYPRE_BoomerAMGSetMaxCoarseSize(HYPRE_Solver solver, HYPRE_Int max_coarse_size); /* :213 */
+HYPRE_Int HYPRE_BoomerAMGSetMinCoarseSize(HYPRE_Solver solver, HYPRE_Int min_coarse_size); /* :220 */
+HYPRE_Int HYPRE_BoomerAMGSetMaxLevels(HYPRE_Solver solver, HYPRE_Int max_levels);  /* :227 */
+HYPRE_Int HYPRE_BoomerAMGSetStrongThreshold(HYPRE_Solver solver, HYPRE_Real strong_threshold); /* :246 */
+HYPRE_Int HYPRE_BoomerAMGSetMaxRowSum(HYPRE_Solver solver, HYPRE_Real max_row_sum); /* :283 */
+HYPRE_Int HYPRE_BoomerAMGSetCoarsenType(HYPRE_Solver solver, HYPRE_Int coarsen_type); /* :310 */
+HYPRE_Int HYPRE_BoomerAMGSetMeasureType(HYPRE_Solver solver, HYPRE_Int measure_type); /* :362 */
+HYPRE_Int HYPRE_BoomerAMGSetAggNumLevels(HYPRE_Solver solver, HYPRE_Int agg_num_levels); /* :369 */
+HYPRE_Int HYPRE_BoomerAMGSetInterpType(HYPRE_Solver solver, HYPRE_Int interp_type); /* :442 */
+HYPRE_Int HYPRE_BoomerAMGSetTruncFactor(HYPRE_Solver solver, HYPRE_Real trunc_factor); /* :448 */
+HYPRE_Int HYPRE_BoomerAMGSetPMaxElmts(HYPRE_Solver solver, HYPRE_Int P_max_elmts); /* :455 */
+HYPRE_Int HYPRE_BoomerAMGSetCycleType(HYPRE_Solver solver, HYPRE_Int cycle_type); /* :572 */
+HYPRE_Int HYPRE_BoomerAMGSetNumSweeps(HYPRE_Solver solver, HYPRE_Int num_sweeps); /* :691 */
+HYPRE_Int HYPRE_BoomerAMGSetCycleNumSweeps(HYPRE_Solver solver, HYPRE_Int num_sweeps, HYPRE_Int k); /* :702 */
+HYPRE_Int HYPRE_BoomerAMGSetRelaxType(HYPRE_Solver solver, HYPRE_Int relax_type); /* :741 */
+HYPRE_Int HYPRE_BoomerAMGSetCycleRelaxType(HYPRE_Solver solver, HYPRE_Int relax_type, HYPRE_Int k); /* :753 */
+HYPRE_Int HYPRE_BoomerAMGSetRelaxOrder(HYPRE_Solver solver, HYPRE_Int relax_order); /* :770 */
+HYPRE_Int HYPRE_BoomerAMGSetRelaxWt(HYPRE_Solver solver, HYPRE_Real relax_weight); /* :805 */
+HYPRE_Int HYPRE_BoomerAMGSetOuterWt(HYPRE_Solver solver, HYPRE_Real omega);       /* :839 */
+HYPRE_Int HYPRE_BoomerAMGSetPrintLevel(HYPRE_Solver solver, HYPRE_Int print_level); /* :1103 */
+HYPRE_Int HYPRE_BoomerAMGSetLogging(HYPRE_Solver solver, HYPRE_Int logging);
+HYPRE_Int HYPRE_BoomerAMGGetNumLevels(HYPRE_Solver solver, HYPRE_Int *num_levels);
+
+/* ---------------- PCG (parcsr_ls/HYPRE_parcsr_ls.h, krylov/HYPRE_krylov.h) ------- */
+HYPRE_Int HYPRE_ParCSRPCGCreate(HYPRE_Comm comm, HYPRE_Solver *solver);        /* :2403 */
+HYPRE_Int HYPRE_ParCSRPCGDestroy(HYPRE_Solver solver);                          /* :2409 */
+HYPRE_Int HYPRE_ParCSRPCGSetup(HYPRE_Solver solver, HYPRE_ParCSRMatrix A, HYPRE_ParVector b,
+                               HYPRE_ParVector x);                              /* :2411 */
+HYPRE_Int HYPRE_ParCSRPCGSolve(HYPRE_Solver solver, HYPRE_ParCSRMatrix A, HYPRE_ParVector b,
+                               HYPRE_ParVector x);                              /* :2416 */
+HYPRE_Int HYPRE_ParCSRPCGSetTol(HYPRE_Solver solver, HYPRE_Real tol);           /* :2421 */
+HYPRE_Int HYPRE_ParCSRPCGSetMaxIter(HYPRE_Solver solver, HYPRE_Int max_iter);   /* :2427 */
+HYPRE_Int HYPRE_ParCSRPCGSetTwoNorm(HYPRE_Solver solver, HYPRE_Int two_norm);   /* :2436 */
+HYPRE_Int HYPRE_ParCSRPCGSetPrecond(HYPRE_Solver solver, HYPRE_PtrToParSolverFcn precond,
+                                    HYPRE_PtrToParSolverFcn precond_setup,
+                                    HYPRE_Solver precond_solver);               /* :2442 */
+HYPRE_Int HYPRE_ParCSRPCGSetPrintLevel(HYPRE_Solver solver, HYPRE_Int level);  /* :2453 */
+HYPRE_Int HYPRE_ParCSRPCGGetNumIterations(HYPRE_Solver solver, HYPRE_Int *num_iterations); /* :2456 */
+HYPRE_Int HYPRE_ParCSRPCGGetFinalRelativeResidualNorm(HYPRE_Solver solver, HYPRE_Real *norm); /* :2459 */
+
+/* ---------------- hypre-ve_amd extensions (no reference counterpart) ------------ */
+/* Communicator over RCCL: rank/size of this process, nccl_id = 128-byte
+ * ncclUniqueId produced on rank 0 by hypreve_CommGetUniqueId and broadcast by
+ * the caller (torch.distributed, MPI, a file...). */
+HYPRE_Int hypreve_CommGetUniqueId(void *nccl_id_128);
+HYPRE_Int hypreve_CommCreate(HYPRE_Int rank, HYPRE_Int size, const void *nccl_id_128,
+                             HYPRE_Comm *comm);
+HYPRE_Int hypreve_CommDestroy(HYPRE_Comm comm);
+
+/* Direct construction of a local ParCSR block from host CSR arrays (global
+ * column indices), equivalent to IJ create/set/assemble in one call. */
+HYPRE_Int hypreve_ParCSRMatrixCreateFromCSR(HYPRE_Comm comm, HYPRE_BigInt first_row,
+                                            HYPRE_Int local_rows, HYPRE_BigInt global_rows,
+                                            const HYPRE_Int *row_ptr, const HYPRE_BigInt *cols,
+                                            const HYPRE_Real *vals, HYPRE_ParCSRMatrix *A);
+/* Device pointer / length of a vector's local part (for zero-copy use). */
+HYPRE_Real *hypreve_ParVectorDeviceData(HYPRE_ParVector v);
+HYPRE_Int hypreve_ParVectorLocalSize(HYPRE_ParVector v);
+HYPRE_Int hypreve_ParVectorCopyToHost(HYPRE_ParVector v, HYPRE_Real *host);
+HYPRE_Int hypreve_ParVectorCopyFromHost(HYPRE_ParVector v, const HYPRE_Real *host);
+HYPRE_Int hypreve_ParVectorSetRandomValues(HYPRE_ParVector v, HYPRE_Int seed); /* HYPRE_ParVectorSetRandomValues */
+
+/* Number of contiguous row blocks used by the hybrid Gauss-Seidel smoothers
+ * (reference: OMP_NUM_THREADS on the CPU path). 0 = automatic. */
+HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_blocks);
+/* Whole-cycle hipGraph capture on/off (default on). */
+HYPRE_Int hypreve_BoomerAMGSetUseGraph(HYPRE_Solver solver, HYPRE_Int use_graph);
+/* Statistics after Setup: levels, complexities, per-level rows/nnz. */
+HYPRE_Int hypreve_BoomerAMGGetComplexities(HYPRE_Solver solver, HYPRE_Real *grid,
+                                           HYPRE_Real *oper, HYPRE_Real *cycle);
+HYPRE_Int hypreve_BoomerAMGGetLevelInfo(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int *rows,
+                                        int64_t *nnz_A, int64_t *nnz_P);
+/* Export one level of the (host-side) hierarchy for inspection/testing.
+ * which: 0 = A, 1 = P.  Pass NULL arrays to query sizes. */
+HYPRE_Int hypreve_BoomerAMGGetLevelMatrix(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,
+                                          HYPRE_Int *nrows, HYPRE_Int *ncols, int64_t *nnz,
+                                          HYPRE_Int *row_ptr, HYPRE_Int *cols, HYPRE_Real *vals);
+HYPRE_Int hypreve_BoomerAMGGetLevelVector(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,
+                                          HYPRE_Int *n, void *data); /* 0 cf (int), 1 l1 (double) */
+HYPRE_Int hypreve_BoomerAMGGetCoarseMatrix(HYPRE_Solver solver, HYPRE_Int *n, HYPRE_Real *dense);
+HYPRE_Int hypreve_BoomerAMGGetRelaxInfo(HYPRE_Solver solver, HYPRE_Int *relax_type4,
+                                        HYPRE_Int *num_sweeps4, HYPRE_Real *weights2,
+                                        HYPRE_Int *misc3); /* misc: relax_order, cycle_type, num_blocks */
+/* Host-only setup (no device upload): lets the CPU test suite check the
+ * hierarchy against the reference fixtures on a machine without a GPU. */
+HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver solver, HYPRE_ParCSRMatrix A);
+/* Run exactly one cycle (hypre_BoomerAMGCycle) on device vectors f, u. */
+HYPRE_Int hypreve_BoomerAMGCycle(HYPRE_Solver solver, HYPRE_ParVector f, HYPRE_ParVector u);
+/* Device timing of the last Solve, per kernel class (ms), for bench/profiling. */
+HYPRE_Int hypreve_BoomerAMGGetKernelStats(HYPRE_Solver solver, HYPRE_Real *stats, HYPRE_Int n);
+/* Time `reps` launches of the finest-level residual SpMV r = b - A x with HIP
+ * events on the solver's stream; returns avg ms and the algorithmic bytes. */
+HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver solver, HYPRE_Int reps, HYPRE_Real *avg_ms,
+                                HYPRE_Real *bytes);
+HYPRE_Int hypreve_DeviceSynchronize(void);
+const char *hypreve_BuildInfo(void);
+const char *hypreve_LastErrorMessage(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HYPREVE_H */

@@ -1,0 +1,404 @@
+/* CPU ORACLE for hypre-ve_amd -- TEST INFRASTRUCTURE ONLY (see oracle.h).
+ *
+ * Restates, statement for statement, the single-process (num_procs == 1)
+ * branches of the reference's solve-phase routines.  Block-parallel
+ * ("hybrid") smoothers take the reference's OpenMP thread partition as the
+ * explicit parameter num_blocks (par_relax.c: size = n/num_threads, rest = ...).
+ * Compiled with -ffp-contract=off so every a*b+c rounds twice, as the
+ * reference's generic C path does on a host without FMA contraction.
+ */
+#include "oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include <float.h>
+
+double orc_dot(int n, const double *x, const double *y) {
+  double s = 0.0;
+  for (int i = 0; i < n; i++) s += x[i] * y[i];
+  return s;
+}
+
+/* ---- seq_mv/csr_matvec.c:24-330 (generic, non-rownnz path) ---- */
+void orc_matvec(double alpha, const orc_csr *A, const double *x, double beta,
+                const double *b, double *y) {
+  const int n = A->nrows;
+  const int *Ai = A->i, *Aj = A->j;
+  const double *Aa = A->a;
+  double *xcopy = NULL;
+  if (alpha == 0.0) {
+    for (int i = 0; i < n; i++) y[i] = beta * b[i];
+    return;
+  }
+  if (x == y) {
+    xcopy = (double *)malloc(sizeof(double) * (size_t)A->ncols);
+    memcpy(xcopy, x, sizeof(double) * (size_t)A->ncols);
+    x = xcopy;
+  }
+  const double temp = beta / alpha;
+  for (int i = 0; i < n; i++) {
+    double t;
+    if (temp == 0.0) {
+      t = 0.0;
+      if (alpha == -1.0) { for (int k = Ai[i]; k < Ai[i + 1]; k++) t -= Aa[k] * x[Aj[k]]; y[i] = t; }
+      else { for (int k = Ai[i]; k < Ai[i + 1]; k++) t += Aa[k] * x[Aj[k]]; y[i] = (alpha == 1.0) ? t : alpha * t; }
+    } else if (temp == -1.0) {
+      if (alpha == 1.0) { t = -b[i]; for (int k = Ai[i]; k < Ai[i + 1]; k++) t += Aa[k] * x[Aj[k]]; y[i] = t; }
+      else if (alpha == -1.0) { t = b[i]; for (int k = Ai[i]; k < Ai[i + 1]; k++) t -= Aa[k] * x[Aj[k]]; y[i] = t; }
+      else { t = -b[i]; for (int k = Ai[i]; k < Ai[i + 1]; k++) t += Aa[k] * x[Aj[k]]; y[i] = alpha * t; }
+    } else if (temp == 1.0) {
+      if (alpha == 1.0) { t = b[i]; for (int k = Ai[i]; k < Ai[i + 1]; k++) t += Aa[k] * x[Aj[k]]; y[i] = t; }
+      else if (alpha == -1.0) { t = -b[i]; for (int k = Ai[i]; k < Ai[i + 1]; k++) t -= Aa[k] * x[Aj[k]]; y[i] = t; }
+      else { t = b[i]; for (int k = Ai[i]; k < Ai[i + 1]; k++) t += Aa[k] * x[Aj[k]]; y[i] = alpha * t; }
+    } else {
+      if (alpha == 1.0) { t = b[i] * temp; for (int k = Ai[i]; k < Ai[i + 1]; k++) t += Aa[k] * x[Aj[k]]; y[i] = t; }
+      else if (alpha == -1.0) { t = -b[i] * temp; for (int k = Ai[i]; k < Ai[i + 1]; k++) t -= Aa[k] * x[Aj[k]]; y[i] = t; }
+      else { t = b[i] * temp; for (int k = Ai[i]; k < Ai[i + 1]; k++) t += Aa[k] * x[Aj[k]]; y[i] = alpha * t; }
+    }
+  }
+  free(xcopy);
+}
+
+/* ---- seq_mv/csr_matvec.c:424 (one thread) ---- */
+void orc_matvecT(double alpha, const orc_csr *A, const double *x, double beta, double *y) {
+  const int nc = A->ncols;
+  if (alpha == 0.0) { for (int i = 0; i < nc; i++) y[i] *= beta; return; }
+  const double temp = beta / alpha;
+  if (temp != 1.0) {
+    if (temp == 0.0) for (int i = 0; i < nc; i++) y[i] = 0.0;
+    else for (int i = 0; i < nc; i++) y[i] *= temp;
+  }
+  for (int i = 0; i < A->nrows; i++)
+    for (int k = A->i[i]; k < A->i[i + 1]; k++) y[A->j[k]] += A->a[k] * x[i];
+  if (alpha != 1.0) for (int i = 0; i < nc; i++) y[i] *= alpha;
+}
+
+static void block_range(int n, int nb, int k, int *ns, int *ne) {
+  int size = n / nb, rest = n - size * nb;
+  if (k < rest) { *ns = k * size + k; *ne = (k + 1) * size + k + 1; }
+  else { *ns = k * size + rest; *ne = (k + 1) * size + rest; }
+}
+
+/* hybrid GS (3 fwd, 4 bwd, 6 sym) and l1 hybrid GS (13, 14, 8), weights 1.
+ * par_relax.c:354 (3), :1875 (4), :2266 (6), :3492 (8), :4340 (13), :4732 (14). */
+static void hybrid_gs(const orc_csr *A, const double *f, const int *cf, int relax_points,
+                      const double *l1, int nb, int fwd, int bwd, int use_l1,
+                      double *u, double *tmp) {
+  const int n = A->nrows;
+  const int *Ai = A->i, *Aj = A->j;
+  const double *Aa = A->a;
+  if (nb < 1) nb = 1;
+  if (nb > 1) memcpy(tmp, u, sizeof(double) * (size_t)n);
+  for (int b = 0; b < nb; b++) {
+    int ns, ne;
+    block_range(n, nb, b, &ns, &ne);
+    if (nb == 1) { ns = 0; ne = n; }
+    for (int pass = 0; pass < 2; pass++) {
+      if ((pass == 0 && !fwd) || (pass == 1 && !bwd)) continue;
+      for (int q = 0; q < ne - ns; q++) {
+        const int i = pass == 0 ? ns + q : ne - 1 - q;
+        if (relax_points != 0 && cf[i] != relax_points) continue;
+        if (use_l1) {
+          if (l1[i] == 0.0) continue;
+          double res = f[i];
+          for (int k = Ai[i]; k < Ai[i + 1]; k++) {
+            const int c = Aj[k];
+            if (nb == 1 || (c >= ns && c < ne)) res -= Aa[k] * u[c];
+            else res -= Aa[k] * tmp[c];
+          }
+          u[i] += res / l1[i];
+        } else {
+          const double d = Aa[Ai[i]];
+          if (d == 0.0) continue;
+          double res = f[i];
+          for (int k = Ai[i] + 1; k < Ai[i + 1]; k++) {
+            const int c = Aj[k];
+            if (nb == 1 || (c >= ns && c < ne)) res -= Aa[k] * u[c];
+            else res -= Aa[k] * tmp[c];
+          }
+          u[i] = res / d;
+        }
+      }
+    }
+  }
+}
+
+int orc_relax(const orc_csr *A, const double *f, const int *cf, int relax_type,
+              int relax_points, double relax_weight, double omega, const double *l1,
+              int num_blocks, double *u, double *vtemp, double *ztemp) {
+  const int n = A->nrows;
+  const int *Ai = A->i, *Aj = A->j;
+  const double *Aa = A->a;
+  switch (relax_type) {
+    case 0: { /* par_relax.c:139 weighted Jacobi */
+      const double omw = 1.0 - relax_weight;
+      memcpy(vtemp, u, sizeof(double) * (size_t)n);
+      for (int i = 0; i < n; i++) {
+        if (relax_points != 0 && cf[i] != relax_points) continue;
+        const double d = Aa[Ai[i]];
+        if (d == 0.0) continue;
+        double res = f[i];
+        for (int k = Ai[i] + 1; k < Ai[i + 1]; k++) res -= Aa[k] * vtemp[Aj[k]];
+        u[i] *= omw;
+        u[i] += relax_weight * res / d;
+      }
+      return 0;
+    }
+    case 7:   /* par_relax.c:3463 Jacobi through the matvec (l1 = diag) */
+    case 18: { /* ams.c:41 hypre_ParCSRRelax type 1 (l1-scaled Jacobi) */
+      if (relax_points != 0) return 1; /* CF l1-Jacobi not restated */
+      memcpy(vtemp, f, sizeof(double) * (size_t)n);
+      orc_matvec(-relax_weight, A, u, relax_weight, vtemp, vtemp);
+      for (int i = 0; i < n; i++) u[i] += vtemp[i] / l1[i];
+      return 0;
+    }
+    case 3: case 4: case 6: case 8: case 13: case 14: {
+      if (relax_weight != 1.0 || omega != 1.0) return 2; /* weighted variants not restated */
+      const int fwd = (relax_type == 3 || relax_type == 6 || relax_type == 8 || relax_type == 13);
+      const int bwd = (relax_type == 4 || relax_type == 6 || relax_type == 8 || relax_type == 14);
+      const int use_l1 = (relax_type == 8 || relax_type == 13 || relax_type == 14);
+      hybrid_gs(A, f, cf, relax_points, l1, num_blocks, fwd, bwd, use_l1, u, ztemp);
+      return 0;
+    }
+    default:
+      return 3;
+  }
+}
+
+/* hypre_gselim (sstruct_ls/gselim.h) on a copy of the dense coarsest matrix,
+ * as hypre_GaussElimSolve (par_gauss_elim.c:202) does for relax type 9. */
+static void gauss_elim_solve(int n, const double *Amat, const double *f, double *u) {
+  double *A = (double *)malloc(sizeof(double) * (size_t)n * n);
+  double *x = (double *)malloc(sizeof(double) * (size_t)n);
+  memcpy(A, Amat, sizeof(double) * (size_t)n * n);
+  memcpy(x, f, sizeof(double) * (size_t)n);
+  if (n == 1) {
+    if (A[0] != 0.0) x[0] = x[0] / A[0];
+  } else {
+    for (int k = 0; k < n - 1; k++) {
+      if (A[k * n + k] != 0.0) {
+        double divA = 1.0 / A[k * n + k];
+        for (int j = k + 1; j < n; j++) {
+          if (A[j * n + k] != 0.0) {
+            double factor = A[j * n + k] * divA;
+            for (int m = k + 1; m < n; m++) A[j * n + m] -= factor * A[k * n + m];
+            x[j] -= factor * x[k];
+          }
+        }
+      }
+    }
+    for (int k = n - 1; k > 0; --k) {
+      if (A[k * n + k] != 0.0) {
+        x[k] /= A[k * n + k];
+        for (int j = 0; j < k; j++)
+          if (A[j * n + k] != 0.0) x[j] -= x[k] * A[j * n + k];
+      }
+    }
+    if (A[0] != 0.0) x[0] /= A[0];
+  }
+  memcpy(u, x, sizeof(double) * (size_t)n);
+  free(A);
+  free(x);
+}
+
+/* ---- parcsr_ls/par_cycle.c:22 hypre_BoomerAMGCycle (smooth_num_levels = 0,
+ * no grid_relax_points, no block mode) ---- */
+int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
+  const int nl = amg->num_levels;
+  int lev_counter[ORC_MAX_LEVELS];
+  int nmax = 0;
+  for (int l = 0; l < nl; l++) if (amg->A[l].nrows > nmax) nmax = amg->A[l].nrows;
+  double *vtemp = (double *)calloc((size_t)nmax, sizeof(double));
+  double *ztemp = (double *)calloc((size_t)nmax, sizeof(double));
+  double ops = op_count ? *op_count : 0.0;
+  int err = 0;
+  lev_counter[0] = 1;
+  for (int k = 1; k < nl; k++) lev_counter[k] = amg->cycle_type;
+  int level = 0, cycle_param = 1, not_finished = 1;
+  while (not_finished) {
+    int num_sweep, relax_type;
+    if (nl > 1) {
+      num_sweep = amg->num_sweeps[cycle_param];
+      relax_type = amg->relax_type[cycle_param];
+    } else {
+      num_sweep = 1;
+      relax_type = amg->relax_type[0] >= 0 ? amg->relax_type[0] : 6;
+    }
+    for (int j = 0; j < num_sweep; j++) {
+      ops += (double)amg->A[level].i[amg->A[level].nrows];
+      if (relax_type == 9 || relax_type == 99 || relax_type == 199) {
+        gauss_elim_solve(amg->coarse_n, amg->coarse_A, F[level], U[level]);
+      } else if (relax_type == 18 || relax_type == 7) {
+        err = orc_relax(&amg->A[level], F[level], amg->cf[level], relax_type, 0,
+                        amg->relax_weight, amg->omega, amg->l1[level], amg->num_blocks,
+                        U[level], vtemp, ztemp);
+      } else {
+        /* hypre_BoomerAMGRelaxIF (par_relax_interface.c:19) */
+        if (amg->relax_order == 1 && cycle_param < 3) {
+          int pts[2];
+          if (cycle_param < 2) { pts[0] = 1; pts[1] = -1; } else { pts[0] = -1; pts[1] = 1; }
+          for (int q = 0; q < 2 && !err; q++)
+            err = orc_relax(&amg->A[level], F[level], amg->cf[level], relax_type, pts[q],
+                            amg->relax_weight, amg->omega, amg->l1[level], amg->num_blocks,
+                            U[level], vtemp, ztemp);
+        } else {
+          err = orc_relax(&amg->A[level], F[level], amg->cf[level], relax_type, 0,
+                          amg->relax_weight, amg->omega, amg->l1[level], amg->num_blocks,
+                          U[level], vtemp, ztemp);
+        }
+      }
+      if (err) goto done;
+    }
+    --lev_counter[level];
+    if (lev_counter[level] >= 0 && level != nl - 1) {
+      const int fine = level, coarse = level + 1;
+      memset(U[coarse], 0, sizeof(double) * (size_t)amg->A[coarse].nrows);
+      orc_matvec(-1.0, &amg->A[fine], U[fine], 1.0, F[fine], vtemp);
+      orc_matvecT(1.0, &amg->P[fine], vtemp, 0.0, F[coarse]);
+      ++level;
+      lev_counter[level] = lev_counter[level] > amg->cycle_type ? lev_counter[level] : amg->cycle_type;
+      cycle_param = (level == nl - 1) ? 3 : 1;
+    } else if (level != 0) {
+      const int fine = level - 1, coarse = level;
+      orc_matvec(1.0, &amg->P[fine], U[coarse], 1.0, U[fine], U[fine]);
+      --level;
+      cycle_param = 2;
+    } else {
+      not_finished = 0;
+    }
+  }
+done:
+  free(vtemp);
+  free(ztemp);
+  if (op_count) *op_count = ops;
+  return err;
+}
+
+/* ---- parcsr_ls/par_amg_solve.c:22 ---- */
+int orc_amg_solve(const orc_amg *amg, const double *f, double *u, double tol,
+                  int min_iter, int max_iter, int converge_type, double *stats) {
+  const int nl = amg->num_levels;
+  const int n = amg->A[0].nrows;
+  double *F[ORC_MAX_LEVELS], *U[ORC_MAX_LEVELS];
+  F[0] = (double *)f;
+  U[0] = u;
+  for (int l = 1; l < nl; l++) {
+    F[l] = (double *)calloc((size_t)amg->A[l].nrows, sizeof(double));
+    U[l] = (double *)calloc((size_t)amg->A[l].nrows, sizeof(double));
+  }
+  double *vtemp = (double *)malloc(sizeof(double) * (size_t)n);
+  double resid_nrm = 1.0, resid_nrm_init = 0.0, rhs_norm = 0.0, relative_resid = 1.0;
+  double op_count = 0.0;
+  int cycle_count = 0, err = 0;
+  if (tol > 0.) {
+    memcpy(vtemp, f, sizeof(double) * (size_t)n);
+    orc_matvec(1.0, &amg->A[0], u, -1.0, vtemp, vtemp);
+    resid_nrm = sqrt(orc_dot(n, vtemp, vtemp));
+    resid_nrm_init = resid_nrm;
+    if (converge_type == 0) {
+      rhs_norm = sqrt(orc_dot(n, f, f));
+      relative_resid = rhs_norm ? resid_nrm_init / rhs_norm : resid_nrm_init;
+    } else {
+      relative_resid = 1.0;
+    }
+  }
+  while ((relative_resid >= tol || cycle_count < min_iter) && cycle_count < max_iter) {
+    op_count = 0.0;
+    err = orc_cycle(amg, F, U, &op_count);
+    if (err) break;
+    if (tol > 0.) {
+      double old_resid = resid_nrm;
+      (void)old_resid;
+      orc_matvec(-1.0, &amg->A[0], u, 1.0, f, vtemp);
+      resid_nrm = sqrt(orc_dot(n, vtemp, vtemp));
+      if (converge_type == 0) relative_resid = rhs_norm ? resid_nrm / rhs_norm : resid_nrm;
+      else relative_resid = resid_nrm / resid_nrm_init;
+    }
+    ++cycle_count;
+  }
+  double conv_factor = 1.0;
+  if (cycle_count > 0 && resid_nrm_init) conv_factor = pow(resid_nrm / resid_nrm_init, 1.0 / (double)cycle_count);
+  if (stats) {
+    stats[0] = cycle_count;
+    stats[1] = relative_resid;
+    stats[2] = conv_factor;
+    stats[3] = op_count / (double)amg->A[0].i[n];
+    stats[4] = resid_nrm_init;
+  }
+  for (int l = 1; l < nl; l++) { free(F[l]); free(U[l]); }
+  free(vtemp);
+  return err;
+}
+
+/* ---- krylov/pcg.c:262 hypre_PCGSolve (stop_crit 0, rel_change 0, no
+ * recompute, cf_tol 0) with BoomerAMG preconditioning: HYPRE_BoomerAMGSolve
+ * with tol 0 and max_iter 1 performs exactly one cycle on a cleared vector. ---- */
+int orc_pcg_amg(const orc_amg *amg, const double *b, double *x, double tol,
+                int max_iter, int two_norm, double *stats) {
+  const int n = amg->A[0].nrows;
+  const orc_csr *A = &amg->A[0];
+  double *r = (double *)malloc(sizeof(double) * (size_t)n);
+  double *p = (double *)malloc(sizeof(double) * (size_t)n);
+  double *s = (double *)malloc(sizeof(double) * (size_t)n);
+  double bi_prod, eps, gamma, gamma_old, alpha, beta, sdotp;
+  double i_prod = 0.0, i_prod_0 = 0.0;
+  int i = 0, err = 0;
+  double *F[ORC_MAX_LEVELS], *U[ORC_MAX_LEVELS];
+  for (int l = 1; l < amg->num_levels; l++) {
+    F[l] = (double *)calloc((size_t)amg->A[l].nrows, sizeof(double));
+    U[l] = (double *)calloc((size_t)amg->A[l].nrows, sizeof(double));
+  }
+#define PRECOND(rr, zz)                                    \
+  do {                                                     \
+    memset((zz), 0, sizeof(double) * (size_t)n);           \
+    F[0] = (double *)(rr); U[0] = (zz);                    \
+    if (orc_cycle(amg, F, U, NULL)) { err = 4; goto done; } \
+  } while (0)
+
+  if (two_norm) {
+    bi_prod = orc_dot(n, b, b);
+  } else {
+    PRECOND(b, p);
+    bi_prod = orc_dot(n, p, b);
+  }
+  eps = tol * tol;
+  if (!(bi_prod > 0.0)) {
+    memcpy(x, b, sizeof(double) * (size_t)n);
+    if (stats) { stats[0] = 0; stats[1] = 0; }
+    goto done;
+  }
+  memcpy(r, b, sizeof(double) * (size_t)n);
+  orc_matvec(-1.0, A, x, 1.0, r, r);
+  PRECOND(r, p);
+  gamma = orc_dot(n, r, p);
+  i_prod_0 = two_norm ? orc_dot(n, r, r) : gamma;
+  while ((i + 1) <= max_iter) {
+    i++;
+    orc_matvec(1.0, A, p, 0.0, s, s);
+    sdotp = orc_dot(n, s, p);
+    if (sdotp == 0.0) { if (i == 1) i_prod = i_prod_0; break; }
+    alpha = gamma / sdotp;
+    if (!(alpha > DBL_MIN)) { if (i == 1) i_prod = i_prod_0; break; }
+    gamma_old = gamma;
+    for (int q = 0; q < n; q++) x[q] += alpha * p[q];
+    for (int q = 0; q < n; q++) r[q] += -alpha * s[q];
+    PRECOND(r, s);
+    gamma = orc_dot(n, r, s);
+    i_prod = two_norm ? orc_dot(n, r, r) : gamma;
+    if (i_prod / bi_prod < eps) break;
+    if (!(gamma > DBL_MIN)) break;
+    beta = gamma / gamma_old;
+    for (int q = 0; q < n; q++) p[q] *= beta;
+    for (int q = 0; q < n; q++) p[q] += 1.0 * s[q];
+  }
+  if (stats) {
+    stats[0] = i;
+    stats[1] = sqrt(i_prod / bi_prod);
+  }
+#undef PRECOND
+done:
+  for (int l = 1; l < amg->num_levels; l++) { free(F[l]); free(U[l]); }
+  free(r); free(p); free(s);
+  return err;
+}
