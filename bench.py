@@ -1,0 +1,152 @@
+"""BoomerAMG V-cycle throughput on MI355X (BASELINE.json metric).
+
+Workload (configs[1]): 3-D 7-point Laplacian, 256^3 rows per GPU, BoomerAMG
+with PMIS coarsening, extended+i interpolation (P_max_elmts 4), l1-Jacobi
+down/up smoothing, Gaussian elimination on the coarsest level.
+A step = one BoomerAMG solve iteration (hypre_BoomerAMGSolve loop body): one
+V-cycle plus the fine-grid residual and its norm.  Inputs are resident in HBM
+before the timed region; the host setup phase is not timed.
+
+Multi-GPU: one process per GPU (torch.distributed.run); weak scaling with
+256^3 rows per GPU (global grid 256 x 256 x 256*N, row blocks by z-slab).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hypre-ve_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=256, help="grid edge per GPU (n^3 rows per GPU)")
+    ap.add_argument("--cpu-cycles", type=int, default=3, help="oracle V-cycles for the CPU baseline (0 = skip)")
+    ap.add_argument("--spmv-reps", type=int, default=50)
+    args = ap.parse_args()
+
+    import torch  # loads the HIP runtime the library then shares
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo")
+    else:
+        torch.cuda.set_device(0)
+
+    import hypreve as hv
+
+    hv.init()
+    n = args.n
+    t0 = time.time()
+    if world > 1:
+        raise SystemExit("multi-GPU run requested but the distributed path is not built into this bench yet")
+    A = hv.ParCSRMatrix.laplacian(n, n, n)
+    nrows = A.n
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-300, max_iter=args.warmup,
+              min_iter=0)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup(A)
+    t_setup = time.time() - t0
+    g, o, c = amg.complexities()
+    log(f"[bench] n={n}^3 rows={nrows} levels={amg.num_levels()} grid={g:.4f} op={o:.4f} setup={t_setup:.1f}s")
+    b = hv.ParVector(nrows, np.ones(nrows))
+    x = hv.ParVector(nrows, np.zeros(nrows))
+
+    # warmup (also instantiates the cycle hipGraph)
+    if args.warmup > 0:
+        amg.set(max_iter=args.warmup)
+        amg.solve(A, b, x)
+    x.fill(0.0)
+    amg.set(max_iter=args.steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t_start = time.perf_counter()
+    it, rr = amg.solve(A, b, x)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    assert it == args.steps, (it, args.steps)
+    ms_per_step = elapsed / args.steps * 1e3
+    value = nrows * world * args.steps / elapsed
+    log(f"[bench] {args.steps} steps in {elapsed*1e3:.2f} ms -> {ms_per_step:.3f} ms/step, rel.res {rr:.3e}")
+
+    # roofline: finest-level SpMV (the dominant kernel), HIP events on the solver stream
+    spmv_ms, spmv_bytes = amg.bench_fine_spmv(args.spmv_reps)
+    achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "kernel": "k_sell<OP_RESID> finest level (r = b - A x)", "avg_ms": round(spmv_ms, 4),
+            "bytes_per_launch": spmv_bytes}
+    log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {spmv_bytes/1e9:.3f} GB -> {achieved:.1f} GB/s")
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_cycles > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle_py
+
+        O = oracle_py.OracleAMG(amg)
+        bh = np.ones(nrows)
+        u = np.zeros(nrows)
+        tc = time.perf_counter()
+        st = O.solve(bh, u, 1e-300, args.cpu_cycles)
+        tcpu = time.perf_counter() - tc
+        cpu = {"value": round(nrows * st["iterations"] / tcpu, 1), "unit": "DOF/s", "cores": 1, "kind": "port",
+               "sample": f"{st['iterations']} solve iterations (V-cycle + residual norm) of the same {n}^3 "
+                         f"hierarchy by the C oracle (oracle/oracle.c), 1 thread, {tcpu:.1f}s"}
+        log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({tcpu:.1f}s)")
+
+    if rank == 0:
+        out = {
+            "metric": "BoomerAMG V-cycle DOF/s + finest-level SpMV GB/s vs HBM peak, 1/2/4/8 GPU",
+            "value": round(value, 1),
+            "unit": "DOF/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (GenerateLaplacian 7-point, rhs = ones)",
+            "config": {"workload": f"3D 7-point Laplacian {n}^3 per GPU, BoomerAMG V-cycle, PMIS + ext+i (Pmx 4), "
+                                   f"l1-Jacobi (relax 18) down/up, Gaussian elimination coarsest",
+                       "rows_per_gpu": nrows, "levels": amg.num_levels(), "grid_complexity": round(g, 6),
+                       "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
+                       "parallelism": f"rows{world}"},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,31 @@
+#!/bin/bash
+# One gpurun call: GPU tests, smoke, bench, rocprof profiles.  Every GPU step has
+# its own time limit; after a fault / abort / timeout nothing further runs.
+set -u
+mkdir -p gpurun_out
+OUT=gpurun_out
+export TMPDIR=/tmp
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -5 "$OUT/$name.log"
+  case $rc in
+    0|1|2|5) return 0 ;;   # pass / test failures / usage: keep going
+    *) echo "=== stopping after $name (rc=$rc)"; exit $rc ;;
+  esac
+}
+WHAT=${1:-all}
+if [[ $WHAT == all || $WHAT == tests ]]; then
+  step pytest_gpu 900 python -m pytest tests -m gpu -x -q
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+fi
+if [[ $WHAT == all || $WHAT == bench ]]; then
+  step bench 900 python bench.py --steps 10 --warmup 2
+fi
+if [[ $WHAT == all || $WHAT == prof ]]; then
+  step rocprof_stats 900 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --cpu-cycles 0
+fi
+echo "=== done"

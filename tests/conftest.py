@@ -1,0 +1,32 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "hypre-ve_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+
+
+@pytest.fixture(scope="session")
+def hv():
+    import hypreve
+    hypreve.lib()
+    return hypreve
+
+
+@pytest.fixture(scope="session")
+def orc():
+    import oracle_py
+    oracle_py.lib()
+    return oracle_py
+
+
+@pytest.fixture(scope="session")
+def gpu(hv):
+    hv.init()
+    return hv
