@@ -16,6 +16,8 @@
 #include "device/runtime.hpp"
 #include "host/hve_host.hpp"
 #include "host/layout.hpp"
+#include "host/partition.hpp"
+#include <rccl/rccl.h>
 
 using namespace hve;
 
@@ -39,10 +41,12 @@ struct hypre_ParCSRMatrix_struct {
   HYPRE_Comm comm = nullptr;
   HYPRE_BigInt global_rows = 0, first_row = 0, global_cols = 0, first_col = 0;
   int n = 0;
-  CSR diag;         // host local block, local columns, diagonal first
-  DevSell dA;       // device copy (SELL-64) used by Matvec
+  CSR diag;         // host: owned rows, GLOBAL column indices, diagonal first
+  DevSell dA;       // device copy (SELL-64) used by Matvec (one rank)
   bool dev = false;
+  bool multi() const { return comm && comm->size > 1; }
   void ensure_device() {
+    if (multi()) throw std::runtime_error("ParCSR matvec across ranks needs a BoomerAMG setup on this matrix");
     if (!dev) { dA.upload(diag); dev = true; }
   }
 };
@@ -67,7 +71,9 @@ struct hypre_Solver_struct {
   int kind = 0;
   // AMG
   AMGParams prm;
-  Hierarchy H;
+  Hierarchy H;        // global hierarchy (one rank, or rank 0 of a multi-rank setup)
+  RankHierarchy RH;   // this rank's part
+  HYPRE_Comm comm = nullptr;
   std::unique_ptr<DevAMG> dev;
   int iters = 0;
   double rel_res = 0.0;
@@ -405,8 +411,13 @@ HYPRE_ParCSRMatrix GenerateLaplacian(HYPRE_Comm comm, HYPRE_BigInt nx, HYPRE_Big
                                      HYPRE_Int P, HYPRE_Int Q, HYPRE_Int R, HYPRE_Int p, HYPRE_Int q, HYPRE_Int r,
                                      HYPRE_Real* value) {
   try {
-    if (P * Q * R != 1) throw std::runtime_error("GenerateLaplacian: multi-rank partition not built in");
     CSR A;
+    if (P * Q * R != 1) {
+      if (!comm || comm->size != P * Q * R) throw std::runtime_error("GenerateLaplacian: P*Q*R != communicator size");
+      int64_t first = 0;
+      generate_laplacian_7pt_block((int)nx, (int)ny, (int)nz, P, Q, R, p, q, r, value, A, first);
+      return wrap_matrix(comm, std::move(A), (HYPRE_BigInt)first, (HYPRE_BigInt)nx * ny * nz);
+    }
     const double cx = -value[1], cy = -value[2], cz = -value[3];
     generate_laplacian_7pt((int)nx, (int)ny, (int)nz, cx, cy, cz, A);
     // the reference takes value[0] verbatim
@@ -701,14 +712,148 @@ HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   API_END
 }
 
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// Multi-rank setup.  hypre's BoomerAMGSetup is itself distributed; this build
+// runs the (bit-identical) single-process setup on rank 0 over the gathered
+// global matrix and ships every rank its part of each level (RCCL, device
+// staging), so an N-GPU solve reproduces the 1-GPU iterates exactly.
+// ---------------------------------------------------------------------------
+static void nck(ncclResult_t r, const char* w) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r) + " in " + w);
+}
+template <typename T>
+static T* dev_copy(const T* h, size_t n) {
+  T* d = nullptr;
+  HVE_HIP(hipMalloc((void**)&d, std::max<size_t>(1, n) * sizeof(T)));
+  if (n) HVE_HIP(hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
+  return d;
+}
+static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
+  HYPRE_Comm c = A->comm;
+  ncclComm_t comm = (ncclComm_t)c->nccl;
+  const int rank = c->rank, size = c->size;
+  hipStream_t st = lib_stream();
+  // 1. sizes
+  int64_t mine[3] = {A->n, A->diag.nnz(), A->first_row};
+  int64_t* d_all = nullptr;
+  HVE_HIP(hipMalloc((void**)&d_all, sizeof(int64_t) * 3 * size));
+  int64_t* d_mine = dev_copy(mine, 3);
+  nck(ncclAllGather(d_mine, d_all, 3, ncclInt64, comm, st), "ncclAllGather(sizes)");
+  std::vector<int64_t> all(3 * size);
+  HVE_HIP(hipMemcpyAsync(all.data(), d_all, sizeof(int64_t) * 3 * size, hipMemcpyDeviceToHost, st));
+  HVE_HIP(hipStreamSynchronize(st));
+  (void)hipFree(d_all);
+  (void)hipFree(d_mine);
+  std::vector<int> starts0(size + 1, 0);
+  for (int r = 0; r < size; ++r) {
+    if (all[3 * r + 2] != starts0[r]) throw std::runtime_error("ParCSR row blocks must be contiguous in rank order");
+    starts0[r + 1] = starts0[r] + (int)all[3 * r];
+  }
+  // 2. gather the rows on rank 0
+  int* d_i = dev_copy(A->diag.i.data(), A->diag.i.size());
+  int* d_j = dev_copy(A->diag.j.data(), A->diag.j.size());
+  double* d_a = dev_copy(A->diag.a.data(), A->diag.a.size());
+  std::vector<int*> ri(size, nullptr), rj(size, nullptr);
+  std::vector<double*> ra(size, nullptr);
+  nck(ncclGroupStart(), "group");
+  if (rank == 0) {
+    for (int r = 1; r < size; ++r) {
+      HVE_HIP(hipMalloc((void**)&ri[r], sizeof(int) * (all[3 * r] + 1)));
+      HVE_HIP(hipMalloc((void**)&rj[r], sizeof(int) * std::max<int64_t>(1, all[3 * r + 1])));
+      HVE_HIP(hipMalloc((void**)&ra[r], sizeof(double) * std::max<int64_t>(1, all[3 * r + 1])));
+      nck(ncclRecv(ri[r], all[3 * r] + 1, ncclInt32, r, comm, st), "recv i");
+      nck(ncclRecv(rj[r], all[3 * r + 1], ncclInt32, r, comm, st), "recv j");
+      nck(ncclRecv(ra[r], all[3 * r + 1], ncclDouble, r, comm, st), "recv a");
+    }
+  } else {
+    nck(ncclSend(d_i, A->n + 1, ncclInt32, 0, comm, st), "send i");
+    nck(ncclSend(d_j, A->diag.nnz(), ncclInt32, 0, comm, st), "send j");
+    nck(ncclSend(d_a, A->diag.nnz(), ncclDouble, 0, comm, st), "send a");
+  }
+  nck(ncclGroupEnd(), "group end");
+  HVE_HIP(hipStreamSynchronize(st));
+  std::vector<std::vector<char>> bufs;
+  if (rank == 0) {
+    CSR G;
+    G.resize_rows(starts0[size], starts0[size]);
+    std::vector<int64_t> nnzoff(size + 1, 0);
+    for (int r = 0; r < size; ++r) nnzoff[r + 1] = nnzoff[r] + all[3 * r + 1];
+    if (nnzoff[size] > 0x7fffffffLL) throw std::runtime_error("global matrix exceeds 2^31 nonzeros");
+    G.j.resize(nnzoff[size]);
+    G.a.resize(nnzoff[size]);
+    for (int r = 0; r < size; ++r) {
+      std::vector<int> li(all[3 * r] + 1);
+      if (r == 0) {
+        li = A->diag.i;
+        std::copy(A->diag.j.begin(), A->diag.j.end(), G.j.begin());
+        std::copy(A->diag.a.begin(), A->diag.a.end(), G.a.begin());
+      } else {
+        HVE_HIP(hipMemcpy(li.data(), ri[r], sizeof(int) * li.size(), hipMemcpyDeviceToHost));
+        HVE_HIP(hipMemcpy(G.j.data() + nnzoff[r], rj[r], sizeof(int) * all[3 * r + 1], hipMemcpyDeviceToHost));
+        HVE_HIP(hipMemcpy(G.a.data() + nnzoff[r], ra[r], sizeof(double) * all[3 * r + 1], hipMemcpyDeviceToHost));
+        (void)hipFree(ri[r]); (void)hipFree(rj[r]); (void)hipFree(ra[r]);
+      }
+      for (int q = 0; q < (int)all[3 * r]; ++q) G.i[starts0[r] + q + 1] = (int)(nnzoff[r] + li[q + 1]);
+    }
+    amg_setup(G, s->prm, s->H);
+    bufs.resize(size);
+    for (int r = 0; r < size; ++r) {
+      RankHierarchy RR;
+      partition_hierarchy(s->H, starts0, r, size, RR);
+      serialize(RR, bufs[r]);
+    }
+  }
+  (void)hipFree(d_i); (void)hipFree(d_j); (void)hipFree(d_a);
+  // 3. scatter the serialized parts
+  std::vector<int64_t> lens(size, 0);
+  if (rank == 0) for (int r = 0; r < size; ++r) lens[r] = (int64_t)bufs[r].size();
+  int64_t* d_lens = dev_copy(lens.data(), size);
+  nck(ncclBroadcast(d_lens, d_lens, size, ncclInt64, 0, comm, st), "bcast lens");
+  HVE_HIP(hipMemcpyAsync(lens.data(), d_lens, sizeof(int64_t) * size, hipMemcpyDeviceToHost, st));
+  HVE_HIP(hipStreamSynchronize(st));
+  (void)hipFree(d_lens);
+  std::vector<char> mybuf;
+  if (rank == 0) {
+    std::vector<char*> dsend(size, nullptr);
+    nck(ncclGroupStart(), "group");
+    for (int r = 1; r < size; ++r) {
+      dsend[r] = dev_copy(bufs[r].data(), bufs[r].size());
+      nck(ncclSend(dsend[r], lens[r], ncclUint8, r, comm, st), "send part");
+    }
+    nck(ncclGroupEnd(), "group end");
+    HVE_HIP(hipStreamSynchronize(st));
+    for (int r = 1; r < size; ++r) (void)hipFree(dsend[r]);
+    mybuf.swap(bufs[0]);
+  } else {
+    char* drecv = nullptr;
+    HVE_HIP(hipMalloc((void**)&drecv, std::max<int64_t>(1, lens[rank])));
+    nck(ncclRecv(drecv, lens[rank], ncclUint8, 0, comm, st), "recv part");
+    HVE_HIP(hipStreamSynchronize(st));
+    mybuf.resize(lens[rank]);
+    HVE_HIP(hipMemcpy(mybuf.data(), drecv, lens[rank], hipMemcpyDeviceToHost));
+    (void)hipFree(drecv);
+  }
+  deserialize(mybuf, s->RH);
+}
+
+extern "C" {
+
 HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVector b, HYPRE_ParVector x) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(A, 2);
   API_BEGIN
-  amg_setup(A->diag, s->prm, s->H);
+  s->comm = A->comm;
+  if (A->multi()) {
+    setup_multi(s, A);
+  } else {
+    amg_setup(A->diag, s->prm, s->H);
+    single_rank_hierarchy(s->H, s->RH);
+  }
   if (!s->dev) s->dev.reset(new DevAMG);
-  s->dev->build(s->H);
-  s->dev->set_use_graph(s->use_graph);
+  s->dev->build(s->RH, A->multi() ? A->comm->nccl : nullptr);
+  s->dev->set_use_graph(s->use_graph && !A->multi());
   API_END
 }
 
@@ -749,13 +894,13 @@ HYPRE_Int HYPRE_BoomerAMGGetFinalRelativeResidualNorm(HYPRE_Solver s, HYPRE_Real
 }
 HYPRE_Int HYPRE_BoomerAMGGetNumLevels(HYPRE_Solver s, HYPRE_Int* nl) {
   CHECK_ARG(s && nl, 1);
-  *nl = (int)s->H.lev.size();
+  *nl = s->H.lev.empty() ? (int)s->RH.lev.size() : (int)s->H.lev.size();
   return 0;
 }
 HYPRE_Int hypreve_BoomerAMGGetComplexities(HYPRE_Solver s, HYPRE_Real* grid, HYPRE_Real* oper, HYPRE_Real* cycle) {
   CHECK_ARG(s, 1);
-  if (grid) *grid = s->H.grid_complexity;
-  if (oper) *oper = s->H.operator_complexity;
+  if (grid) *grid = s->H.lev.empty() ? s->RH.grid_complexity : s->H.grid_complexity;
+  if (oper) *oper = s->H.lev.empty() ? s->RH.operator_complexity : s->H.operator_complexity;
   if (cycle) {
     // par_cycle.c op count: one smoothing sweep costs nnz(A_l)
     double ops = 0;
@@ -835,7 +980,7 @@ HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver s, HYPRE_Int reps, HYPRE_Real* avg_
   CHECK_ARG(s && s->dev && s->dev->built(), 1);
   API_BEGIN
   DevAMG& D = *s->dev;
-  const DevSell& A = D.fineA();
+  const DevSell& A = D.level(0).A.in;
   hipStream_t st = D.stream();
   double* x = D.scratch(0);
   double* b = D.scratch(1);
@@ -892,14 +1037,14 @@ HYPRE_Int HYPRE_ParCSRPCGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
   CHECK_ARG(s && s->kind == KIND_PCG, 1);
   CHECK_ARG(A, 2);
   API_BEGIN
-  A->ensure_device();
   if (s->precond_setup && s->precond) {
     int rc = s->precond_setup(s->precond, A, b, x);
     if (rc) return rc;
   }
   if (!(s->precond && s->precond->kind == KIND_AMG && s->precond->dev)) {
+    A->ensure_device();
     s->ws.reset(new DevAMG);
-    s->ws->init_workspace(A->n);
+    s->ws->init_workspace(A->n, nullptr);
   }
   API_END
 }
@@ -909,7 +1054,6 @@ HYPRE_Int HYPRE_ParCSRPCGSolve(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
   CHECK_ARG(b && b->n == A->n, 3);
   CHECK_ARG(x && x->n == A->n, 4);
   API_BEGIN
-  A->ensure_device();
   vec_alloc(x);
   DevAMG* amg = (s->precond && s->precond->kind == KIND_AMG && s->precond->dev) ? s->precond->dev.get() : nullptr;
   DevAMG* ws = amg ? amg : s->ws.get();
@@ -943,7 +1087,19 @@ HYPRE_Int HYPRE_ParCSRPCGSolve(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
     const int n = A->n;
     pre = [n, st](const double* r, double* z) { HVE_HIP(launch_copy(n, r, z, st)); };
   }
-  const int rc = pcg_solve(ws, A->dA, s->pcg, pre, b->d, x->d, st, &s->iters, &s->rel_res);
+  MatvecFn Aop;
+  if (amg) {
+    Aop = [amg, st](int op, const double* xx, const double* bb, double* yy) {
+      amg->fine_apply(op, xx, bb, yy, op == K_RESID ? -1.0 : 1.0, 0.0, st);
+    };
+  } else {
+    A->ensure_device();
+    DevSell* dA = &A->dA;
+    Aop = [dA, st](int op, const double* xx, const double* bb, double* yy) {
+      HVE_HIP(launch_sell(op, dA->view(), xx, bb, nullptr, nullptr, 0, yy, op == K_RESID ? -1.0 : 1.0, 0.0, st));
+    };
+  }
+  const int rc = pcg_solve(ws, A->n, Aop, s->pcg, pre, b->d, x->d, st, &s->iters, &s->rel_res);
   if (rc) g_error |= rc;
   API_END
 }

@@ -9,6 +9,7 @@ struct SellView {
   const int* slice_ptr = nullptr;  // nslices + 1 offsets (in entries)
   const int* col = nullptr;        // padded; -1 marks padding
   const double* val = nullptr;
+  const int* rowmap = nullptr;     // subset row -> local row, nullptr = identity
   int nrows = 0;
   int ncols = 0;
 };
@@ -23,6 +24,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 // op: 0 l1-Jacobi w=1, 1 l1-Jacobi weighted, 2 Jacobi (s = diagonal)
 hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u,
                              hipStream_t st);
+hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st);
 hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,
                        hipStream_t st);
 hipError_t launch_scale(int n, const double* alpha_p, double alpha, double* y, hipStream_t st);

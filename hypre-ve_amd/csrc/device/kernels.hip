@@ -56,6 +56,7 @@ struct SpArgs {
   const double* __restrict__ b;   // rhs / additive term (f or b)
   const double* __restrict__ l1;  // l1 norms (or diag) for smoothers
   const int* __restrict__ cf;     // CF marker (relax_points != 0 only)
+  const int* __restrict__ rowmap; // subset row -> local row (nullptr: identity)
   double* __restrict__ y;         // output
   double w;                       // relax weight / alpha
   double temp;                    // beta/alpha for OP_GENERAL
@@ -69,36 +70,37 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
   if (row >= p.nrows) return;
   const int lane = threadIdx.x & (kWave - 1);
   const int slice = row >> 6;
+  const int g = p.rowmap ? p.rowmap[row] : row;  // row of the local vectors
   const int beg = p.slice_ptr[slice];
   const int width = (p.slice_ptr[slice + 1] - beg) >> 6;
   const int* __restrict__ cp = p.col + beg + lane;
   const double* __restrict__ vp = p.val + beg + lane;
 
   if (CFSEL) {
-    if (p.cf[row] != p.relax_points) {
-      if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) p.y[row] = p.x[row];
+    if (p.cf[g] != p.relax_points) {
+      if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) p.y[g] = p.x[g];
       return;
     }
   }
 
   if (OP == OP_RESID || OP == OP_L1JAC) {
-    double t = p.b[row];
+    double t = p.b[g];
     for (int k = 0; k < width; ++k) {
       const int c = cp[k * kWave];
       const double a = vp[k * kWave];
       if (c >= 0) t -= a * p.x[c];
     }
-    if (OP == OP_RESID) p.y[row] = t;
-    else p.y[row] = p.x[row] + t / p.l1[row];
+    if (OP == OP_RESID) p.y[g] = t;
+    else p.y[g] = p.x[g] + t / p.l1[g];
   } else if (OP == OP_L1JAC_W) {
-    double t = -p.b[row];
+    double t = -p.b[g];
     for (int k = 0; k < width; ++k) {
       const int c = cp[k * kWave];
       const double a = vp[k * kWave];
       if (c >= 0) t += a * p.x[c];
     }
     const double v = (-p.w) * t;
-    p.y[row] = p.x[row] + v / p.l1[row];
+    p.y[g] = p.x[g] + v / p.l1[g];
   } else if (OP == OP_MATVEC || OP == OP_RESTRICT) {
     double t = 0.0;
     for (int k = 0; k < width; ++k) {
@@ -106,20 +108,20 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
       const double a = vp[k * kWave];
       if (c >= 0) t += a * p.x[c];
     }
-    p.y[row] = t;
+    p.y[g] = t;
   } else if (OP == OP_PROLONG) {
-    double t = p.y[row];
+    double t = p.y[g];
     for (int k = 0; k < width; ++k) {
       const int c = cp[k * kWave];
       const double a = vp[k * kWave];
       if (c >= 0) t += a * p.x[c];
     }
-    p.y[row] = t;
+    p.y[g] = t;
   } else if (OP == OP_JAC) {
     const double d = vp[0];  // diagonal stored first
-    const double uo = p.x[row];
-    if (d == 0.0) { p.y[row] = uo; return; }
-    double t = p.b[row];
+    const double uo = p.x[g];
+    if (d == 0.0) { p.y[g] = uo; return; }
+    double t = p.b[g];
     for (int k = 1; k < width; ++k) {
       const int c = cp[k * kWave];
       const double a = vp[k * kWave];
@@ -127,16 +129,16 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     }
     double u = uo * (1.0 - p.w);
     u += p.w * t / d;
-    p.y[row] = u;
+    p.y[g] = u;
   } else if (OP == OP_GENERAL) {
     // seq_mv/csr_matvec.c:187-330 branch structure; alpha = p.w, temp = beta/alpha
     const double alpha = p.w, temp = p.temp;
     double t;
     const bool neg = (alpha == -1.0);
     if (temp == 0.0) t = 0.0;
-    else if (temp == -1.0) t = neg ? p.b[row] : -p.b[row];
-    else if (temp == 1.0) t = neg ? -p.b[row] : p.b[row];
-    else t = neg ? -p.b[row] * temp : p.b[row] * temp;
+    else if (temp == -1.0) t = neg ? p.b[g] : -p.b[g];
+    else if (temp == 1.0) t = neg ? -p.b[g] : p.b[g];
+    else t = neg ? -p.b[g] * temp : p.b[g] * temp;
     for (int k = 0; k < width; ++k) {
       const int c = cp[k * kWave];
       const double a = vp[k * kWave];
@@ -145,7 +147,7 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
         else t += a * p.x[c];
       }
     }
-    p.y[row] = (alpha == 1.0 || neg) ? t : alpha * t;
+    p.y[g] = (alpha == 1.0 || neg) ? t : alpha * t;
   }
 }
 
@@ -290,6 +292,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
                        const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s) {
   if (M.nrows <= 0) return hipSuccess;
   SpArgs a;
+  a.rowmap = M.rowmap;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
   a.nblocks_pad = blocks_pad8(M.nrows);
   a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.w = w; a.temp = temp; a.relax_points = relax_points;
@@ -306,6 +309,22 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     default: return hipErrorInvalidValue;
   }
 #undef HVE_L
+  return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) k_gather(int n, const int* __restrict__ idx, const double* __restrict__ x,
+                                                double* __restrict__ out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = x[idx[i]];
+}
+__global__ void __launch_bounds__(256) k_copy_offset(int n, const double* __restrict__ x, double* __restrict__ y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) y[i] = x[i];
+}
+
+hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather, dim3(blocks_for(n)), dim3(256), 0, st, n, idx, x, out);
   return hipGetLastError();
 }
 

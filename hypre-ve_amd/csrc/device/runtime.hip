@@ -9,6 +9,8 @@
 #include <stdexcept>
 #include <string>
 
+#include <rccl/rccl.h>
+
 #include "../host/layout.hpp"
 #include "runtime.hpp"
 
@@ -34,7 +36,7 @@ static T* dupload(const T* h, size_t n) {
   return p;
 }
 
-void DevSell::upload(const CSR& A) {
+void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h) {
   release();
   std::vector<int> sp, col;
   std::vector<double> val;
@@ -47,91 +49,98 @@ void DevSell::upload(const CSR& A) {
   slice_ptr = dupload(sp.data(), sp.size());
   this->col = dupload(col.data(), col.size());
   this->val = dupload(val.data(), val.size());
+  bool ident = true;
+  for (size_t i = 0; i < rowmap_h.size() && ident; ++i) ident = rowmap_h[i] == (int)i;
+  if (!rowmap_h.empty() && !ident) rowmap = dupload(rowmap_h.data(), rowmap_h.size());
 }
 void DevSell::release() {
-  if (slice_ptr) hipFree(slice_ptr);
-  if (col) hipFree(col);
-  if (val) hipFree(val);
-  slice_ptr = nullptr; col = nullptr; val = nullptr;
+  if (slice_ptr) (void)hipFree(slice_ptr);
+  if (col) (void)hipFree(col);
+  if (val) (void)hipFree(val);
+  if (rowmap) (void)hipFree(rowmap);
+  slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0;
+}
+
+void DevOp::upload(const RankOp& op) {
+  in.upload(op.interior, op.map_int);
+  bd.upload(op.boundary, op.map_bnd);
+  nrows_local = op.nrows_local;
+}
+
+void DevHalo::upload(const RankHalo& h) {
+  release();
+  n_loc = h.n_loc;
+  n_halo = h.n_halo;
+  peers = h.peers;
+  recv_cnt = h.recv_cnt;
+  send_cnt = h.send_cnt;
+  recv_off.assign(peers.size(), 0);
+  send_off.assign(peers.size(), 0);
+  int ro = 0, so = 0;
+  for (size_t p = 0; p < peers.size(); ++p) {
+    recv_off[p] = ro; ro += recv_cnt[p];
+    send_off[p] = so; so += send_cnt[p];
+  }
+  n_send = so;
+  if (n_send) {
+    d_send_idx = dupload(h.send_idx.data(), h.send_idx.size());
+    d_sendbuf = dalloc<double>(n_send);
+  }
+}
+void DevHalo::release() {
+  if (d_send_idx) (void)hipFree(d_send_idx);
+  if (d_sendbuf) (void)hipFree(d_sendbuf);
+  d_send_idx = nullptr; d_sendbuf = nullptr;
+  peers.clear(); recv_cnt.clear(); recv_off.clear(); send_cnt.clear(); send_off.clear();
+  n_loc = n_halo = n_send = 0;
+}
+
+static void nccl_check(ncclResult_t r, const char* what) {
+  if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL error '") + ncclGetErrorString(r) + "' in " + what);
 }
 
 DevAMG::~DevAMG() { release(); }
 
 void DevAMG::release() {
-  for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+  for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   graphs_.clear();
   for (auto& L : lev_) {
     L.A.release(); L.P.release(); L.R.release();
-    if (L.l1) hipFree(L.l1);
-    if (L.cf) hipFree(L.cf);
-    if (L.F) hipFree(L.F);
-    if (L.U[0]) hipFree(L.U[0]);
-    if (L.U[1]) hipFree(L.U[1]);
-    if (L.V) hipFree(L.V);
-    if (L.Z) hipFree(L.Z);
+    L.hu.release(); L.hv.release();
+    for (void* p : {(void*)L.l1, (void*)L.cf, (void*)L.F, (void*)L.U[0], (void*)L.U[1], (void*)L.V})
+      if (p) (void)hipFree(p);
   }
   lev_.clear();
-  if (coarse_L_) hipFree(coarse_L_);
-  if (coarse_mask_) hipFree(coarse_mask_);
-  if (coarse_U_) hipFree(coarse_U_);
-  coarse_L_ = nullptr; coarse_mask_ = nullptr; coarse_U_ = nullptr;
-  if (dot_part_) hipFree(dot_part_);
-  if (dscal_) hipFree(dscal_);
-  if (hscal_) hipHostFree(hscal_);
-  for (auto& s : scratch_) { if (s) hipFree(s); s = nullptr; }
-  dot_part_ = nullptr; dscal_ = nullptr; hscal_ = nullptr;
-  if (stream_) hipStreamDestroy(stream_);
-  stream_ = nullptr;
+  for (void* p : {(void*)coarse_L_, (void*)coarse_mask_, (void*)coarse_U_, (void*)coarse_f_, (void*)coarse_u_,
+                  (void*)u0_buf_[0], (void*)u0_buf_[1], (void*)x0_buf_, (void*)dot_part_, (void*)dscal_})
+    if (p) (void)hipFree(p);
+  coarse_L_ = nullptr; coarse_mask_ = nullptr; coarse_U_ = nullptr; coarse_f_ = nullptr; coarse_u_ = nullptr;
+  u0_buf_[0] = u0_buf_[1] = nullptr; x0_buf_ = nullptr; dot_part_ = nullptr; dscal_ = nullptr;
+  if (hscal_) (void)hipHostFree(hscal_);
+  hscal_ = nullptr;
+  for (auto& s : scratch_) { if (s) (void)hipFree(s); s = nullptr; }
+  if (ev_packed_) (void)hipEventDestroy(ev_packed_);
+  if (ev_halo_) (void)hipEventDestroy(ev_halo_);
+  ev_packed_ = ev_halo_ = nullptr;
+  if (stream_) (void)hipStreamDestroy(stream_);
+  if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
+  stream_ = comm_stream_ = nullptr;
+  nccl_ = nullptr;
+  ws_n_ = 0;
 }
 
-void DevAMG::build(const Hierarchy& H) {
-  release();
-  prm = H.prm;
-  HVE_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  const int nl = (int)H.lev.size();
-  lev_.resize(nl);
-  for (int l = 0; l < nl; ++l) {
-    const Level& L = H.lev[l];
-    DevLevel& D = lev_[l];
-    D.n = L.A.nrows;
-    D.A.upload(L.A);
-    if (l < nl - 1) {
-      D.P.upload(L.P);
-      D.R.upload(L.R);
-    }
-    if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
-    if (!L.cf.empty()) D.cf = dupload(L.cf.data(), L.cf.size());
-    D.F = dalloc<double>(D.n);
-    D.U[0] = dalloc<double>(D.n);
-    D.U[1] = dalloc<double>(D.n);
-    D.V = dalloc<double>(D.n);
-    D.Z = dalloc<double>(D.n);
-    HVE_HIP(hipMemset(D.F, 0, sizeof(double) * D.n));
-    HVE_HIP(hipMemset(D.U[0], 0, sizeof(double) * D.n));
-    HVE_HIP(hipMemset(D.U[1], 0, sizeof(double) * D.n));
-  }
-  coarse_n_ = H.coarse_n;
-  if (coarse_n_ > 0) {
-    std::vector<double> Lf, U;
-    std::vector<unsigned char> mask;
-    gselim_factor(coarse_n_, H.coarse_dense, Lf, mask, U);
-    coarse_L_ = dupload(Lf.data(), Lf.size());
-    coarse_mask_ = dupload(mask.data(), mask.size());
-    coarse_U_ = dupload(U.data(), U.size());
-  }
-  dot_part_ = dalloc<double>(1024);
-  dscal_ = dalloc<double>(16);
-  HVE_HIP(hipMemset(dscal_, 0, 16 * sizeof(double)));
-  HVE_HIP(hipHostMalloc((void**)&hscal_, 16 * sizeof(double), hipHostMallocDefault));
-  for (auto& s : scratch_) s = dalloc<double>(lev_[0].n);
-  ws_n_ = lev_[0].n;
-  HVE_HIP(hipDeviceSynchronize());
+static void init_common(hipStream_t* s, hipStream_t* cs, hipEvent_t* e1, hipEvent_t* e2) {
+  HVE_HIP(hipStreamCreateWithFlags(s, hipStreamNonBlocking));
+  HVE_HIP(hipStreamCreateWithFlags(cs, hipStreamNonBlocking));
+  HVE_HIP(hipEventCreateWithFlags(e1, hipEventDisableTiming));
+  HVE_HIP(hipEventCreateWithFlags(e2, hipEventDisableTiming));
 }
 
-void DevAMG::init_workspace(int n) {
+void DevAMG::init_workspace(int n, void* nccl_comm) {
   release();
-  HVE_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  nccl_ = nccl_comm;
+  init_common(&stream_, &comm_stream_, &ev_packed_, &ev_halo_);
   dot_part_ = dalloc<double>(1024);
   dscal_ = dalloc<double>(16);
   HVE_HIP(hipMemset(dscal_, 0, 16 * sizeof(double)));
@@ -140,14 +149,126 @@ void DevAMG::init_workspace(int n) {
   ws_n_ = n;
 }
 
+void DevAMG::build(const RankHierarchy& R, void* nccl_comm) {
+  const int n0 = R.lev.empty() ? 0 : R.lev[0].n_loc;
+  init_workspace(n0, nccl_comm);
+  prm = R.prm;
+  const int nl = (int)R.lev.size();
+  lev_.resize(nl);
+  for (int l = 0; l < nl; ++l) {
+    const RankLevel& L = R.lev[l];
+    DevLevel& D = lev_[l];
+    D.n = L.n_loc;
+    D.first = L.first;
+    D.n_glob = L.n_glob;
+    D.A.upload(L.A);
+    D.hu.upload(L.hu);
+    if (l < nl - 1) {
+      D.P.upload(L.P);
+      D.R.upload(L.R);
+      D.hv.upload(L.hv);
+    }
+    if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
+    if (!L.cf.empty()) D.cf = dupload(L.cf.data(), L.cf.size());
+    D.F = dalloc<double>(D.n);
+    D.U[0] = dalloc<double>(D.n + D.hu.n_halo);
+    D.U[1] = dalloc<double>(D.n + D.hu.n_halo);
+    D.V = dalloc<double>(D.n + D.hv.n_halo);
+    HVE_HIP(hipMemset(D.F, 0, sizeof(double) * std::max(1, D.n)));
+    HVE_HIP(hipMemset(D.U[0], 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
+    HVE_HIP(hipMemset(D.U[1], 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
+    HVE_HIP(hipMemset(D.V, 0, sizeof(double) * std::max(1, D.n + D.hv.n_halo)));
+  }
+  coarse_n_ = R.coarse_n;
+  if (coarse_n_ > 0) {
+    std::vector<double> Lf, U;
+    std::vector<unsigned char> mask;
+    gselim_factor(coarse_n_, R.coarse_dense, Lf, mask, U);
+    coarse_L_ = dupload(Lf.data(), Lf.size());
+    coarse_mask_ = dupload(mask.data(), mask.size());
+    coarse_U_ = dupload(U.data(), U.size());
+    coarse_f_ = dalloc<double>(coarse_n_);
+    coarse_u_ = dalloc<double>(coarse_n_);
+  }
+  if (nl > 0 && lev_[0].hu.n_halo > 0) {
+    const int m = lev_[0].n + lev_[0].hu.n_halo;
+    u0_buf_[0] = dalloc<double>(m);
+    u0_buf_[1] = dalloc<double>(m);
+    x0_buf_ = dalloc<double>(m);
+    HVE_HIP(hipMemset(u0_buf_[0], 0, sizeof(double) * m));
+    HVE_HIP(hipMemset(u0_buf_[1], 0, sizeof(double) * m));
+    HVE_HIP(hipMemset(x0_buf_, 0, sizeof(double) * m));
+  }
+  if (nccl_) use_graph_ = false;  // RCCL calls stay outside graph capture in this build
+  HVE_HIP(hipDeviceSynchronize());
+}
+
 void DevAMG::dot(int n, const double* x, const double* y, double* out, hipStream_t s) {
   HVE_HIP(launch_dot(n, x, y, dot_part_, out, s));
+  if (nccl_) nccl_check(ncclAllReduce(out, out, 1, ncclDouble, ncclSum, (ncclComm_t)nccl_, s), "ncclAllReduce(dot)");
 }
 double DevAMG::dot_host(int n, const double* x, const double* y, hipStream_t s) {
   dot(n, x, y, dscal_ + 15, s);
   HVE_HIP(hipMemcpyAsync(hscal_ + 15, dscal_ + 15, sizeof(double), hipMemcpyDeviceToHost, s));
   HVE_HIP(hipStreamSynchronize(s));
   return hscal_[15];
+}
+
+// ParCSR halo exchange (par_csr_communication.c hypre_ParCSRCommHandleCreate,
+// job 1) as gather -> grouped RCCL send/recv on the side stream.
+void DevAMG::halo_start(const DevHalo& h, double* x, hipStream_t s) {
+  HVE_HIP(launch_gather(h.n_send, h.d_send_idx, x, h.d_sendbuf, s));
+  HVE_HIP(hipEventRecord(ev_packed_, s));
+  HVE_HIP(hipStreamWaitEvent(comm_stream_, ev_packed_, 0));
+  ncclComm_t comm = (ncclComm_t)nccl_;
+  nccl_check(ncclGroupStart(), "ncclGroupStart");
+  for (size_t p = 0; p < h.peers.size(); ++p) {
+    if (h.send_cnt[p])
+      nccl_check(ncclSend(h.d_sendbuf + h.send_off[p], h.send_cnt[p], ncclDouble, h.peers[p], comm, comm_stream_),
+                 "ncclSend");
+    if (h.recv_cnt[p])
+      nccl_check(ncclRecv(x + h.n_loc + h.recv_off[p], h.recv_cnt[p], ncclDouble, h.peers[p], comm, comm_stream_),
+                 "ncclRecv");
+  }
+  nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  HVE_HIP(hipEventRecord(ev_halo_, comm_stream_));
+}
+void DevAMG::halo_finish(hipStream_t s) { HVE_HIP(hipStreamWaitEvent(s, ev_halo_, 0)); }
+
+void DevAMG::apply(const DevOp& M, const DevHalo* hx, int op, double* x, const double* b, const double* l1,
+                   const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s) {
+  const bool ex = hx && hx->active() && nccl_;
+  if (ex) halo_start(*hx, x, s);
+  HVE_HIP(launch_sell(op, M.in.view(), x, b, l1, cf, relax_points, y, w, temp, s));
+  if (ex) halo_finish(s);
+  if (M.bd.nrows > 0) HVE_HIP(launch_sell(op, M.bd.view(), x, b, l1, cf, relax_points, y, w, temp, s));
+}
+
+void DevAMG::fine_apply(int op, const double* x, const double* b, double* y, double alpha, double temp,
+                        hipStream_t s) {
+  DevLevel& L = lev_[0];
+  double* xin = const_cast<double*>(x);
+  if (x0_buf_) {
+    HVE_HIP(launch_copy(L.n, x, x0_buf_, s));
+    xin = x0_buf_;
+  }
+  apply(L.A, &L.hu, op, xin, b, nullptr, nullptr, 0, y, alpha, temp, s);
+}
+
+void DevAMG::coarse_solve(int level, const double* f, double* u, hipStream_t s) {
+  DevLevel& L = lev_[level];
+  if (coarse_n_ != L.n_glob) throw std::runtime_error("coarse solve size mismatch");
+  if (!nccl_) {
+    HVE_HIP(launch_coarse(coarse_n_, coarse_L_, coarse_mask_, coarse_U_, f, u, s));
+    return;
+  }
+  // hypre_GaussElimSolve gathers f on every rank and solves redundantly
+  HVE_HIP(launch_set(coarse_n_, 0.0, coarse_f_, s));
+  HVE_HIP(launch_copy(L.n, f, coarse_f_ + L.first, s));
+  nccl_check(ncclAllReduce(coarse_f_, coarse_f_, coarse_n_, ncclDouble, ncclSum, (ncclComm_t)nccl_, s),
+             "ncclAllReduce(coarse)");
+  HVE_HIP(launch_coarse(coarse_n_, coarse_L_, coarse_mask_, coarse_U_, coarse_f_, coarse_u_, s));
+  HVE_HIP(launch_copy(L.n, coarse_u_ + L.first, u, s));
 }
 
 // One smoothing step on `level` (par_cycle.c:333-505 dispatch).  u_cur holds the
@@ -169,15 +290,14 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       if (zero_guess) {
         HVE_HIP(launch_zero_guess(n, w == 1.0 ? 0 : 1, w, f, L.l1, u_cur, s));
       } else {
-        HVE_HIP(launch_sell(w == 1.0 ? K_L1JAC : K_L1JAC_W, L.A.view(), u_cur, f, L.l1, nullptr, 0, u_alt, w,
-                            0.0, s));
+        apply(L.A, &L.hu, w == 1.0 ? K_L1JAC : K_L1JAC_W, u_cur, f, L.l1, nullptr, 0, u_alt, w, 0.0, s);
         std::swap(u_cur, u_alt);
       }
       break;
     }
     case 0: {
       if (zero_guess) HVE_HIP(launch_set(n, 0.0, u_cur, s));
-      HVE_HIP(launch_sell(K_JAC, L.A.view(), u_cur, f, nullptr, L.cf, relax_points, u_alt, w, 0.0, s));
+      apply(L.A, &L.hu, K_JAC, u_cur, f, nullptr, L.cf, relax_points, u_alt, w, 0.0, s);
       std::swap(u_cur, u_alt);
       break;
     }
@@ -195,8 +315,14 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s) {
   std::vector<const double*> fl(nl);
   std::vector<char> zero(nl, 0);
   lev_counter[0] = 1;
-  ucur[0] = u0;
-  ualt[0] = lev_[0].U[0];
+  if (u0_buf_[0]) {
+    HVE_HIP(launch_copy(lev_[0].n, u0, u0_buf_[0], s));
+    ucur[0] = u0_buf_[0];
+    ualt[0] = u0_buf_[1];
+  } else {
+    ucur[0] = u0;
+    ualt[0] = lev_[0].U[0];
+  }
   fl[0] = f0;
   for (int l = 1; l < nl; ++l) {
     ucur[l] = lev_[l].U[0];
@@ -216,10 +342,9 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s) {
       relax_type = prm.relax_type[0] >= 0 ? prm.relax_type[0] : 6;
     }
     for (int j = 0; j < num_sweep; ++j) {
-      ops += (double)lev_[level].A.nnz;
+      ops += (double)lev_[level].A.nnz();
       if (relax_type == 9 || relax_type == 99 || relax_type == 19 || relax_type == 98) {
-        if (coarse_n_ != lev_[level].n) throw std::runtime_error("coarse solve size mismatch");
-        HVE_HIP(launch_coarse(coarse_n_, coarse_L_, coarse_mask_, coarse_U_, fl[level], ucur[level], s));
+        coarse_solve(level, fl[level], ucur[level], s);
         zero[level] = 0;
       } else if (relax_type == 18 || relax_type == 7) {
         relax(level, relax_type, 0, fl[level], ucur[level], ualt[level], zero[level], s);
@@ -243,9 +368,8 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s) {
       const int fine = level, coarse = level + 1;
       DevLevel& Lf = lev_[fine];
       // Vtemp = f - A u  (csr_matvec.c, alpha=-1 beta=1);  F_c = P^T Vtemp
-      HVE_HIP(launch_sell(K_RESID, Lf.A.view(), ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s));
-      HVE_HIP(launch_sell(K_RESTRICT, Lf.R.view(), Lf.V, nullptr, nullptr, nullptr, 0, lev_[coarse].F, 1.0, 0.0,
-                          s));
+      apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);
+      apply(Lf.R, &Lf.hv, K_RESTRICT, Lf.V, nullptr, nullptr, nullptr, 0, lev_[coarse].F, 1.0, 0.0, s);
       ++level;
       lev_counter[level] = std::max(lev_counter[level], prm.cycle_type);
       cycle_param = (level == nl - 1) ? 3 : 1;
@@ -255,8 +379,8 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s) {
       if (zero[coarse]) HVE_HIP(launch_set(lev_[coarse].n, 0.0, ucur[coarse], s));
       zero[coarse] = 0;
       // u_f = u_f + P u_c  (alpha=1, beta=1)
-      HVE_HIP(launch_sell(K_PROLONG, lev_[fine].P.view(), ucur[coarse], nullptr, nullptr, nullptr, 0, ucur[fine],
-                          1.0, 0.0, s));
+      apply(lev_[fine].P, &lev_[coarse].hu, K_PROLONG, ucur[coarse], nullptr, nullptr, nullptr, 0, ucur[fine], 1.0,
+            0.0, s);
       --level;
       cycle_param = 2;
     } else {
@@ -280,9 +404,9 @@ void DevAMG::cycle(const double* f, double* u, hipStream_t s) {
     try {
       emit_cycle(f, u, s);
     } catch (...) {
-      hipGraph_t tmp;
-      hipStreamEndCapture(s, &tmp);
-      if (tmp) hipGraphDestroy(tmp);
+      hipGraph_t tmp = nullptr;
+      (void)hipStreamEndCapture(s, &tmp);
+      if (tmp) (void)hipGraphDestroy(tmp);
       throw;
     }
     HVE_HIP(hipStreamEndCapture(s, &g));
@@ -290,7 +414,7 @@ void DevAMG::cycle(const double* f, double* u, hipStream_t s) {
     HVE_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     HVE_HIP(hipGraphDestroy(g));
     if (graphs_.size() > 16) {
-      for (auto& kv : graphs_) hipGraphExecDestroy(kv.second);
+      for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
       graphs_.clear();
     }
     it = graphs_.emplace(key, ge).first;
@@ -307,7 +431,7 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
   int cycle_count = 0;
   if (tol > 0.) {
     // Vtemp = A u - f  (hypre copies f then Matvec(1, A, u, -1, Vtemp))
-    HVE_HIP(launch_sell(K_GENERAL, lev_[0].A.view(), u, f, nullptr, nullptr, 0, V, 1.0, -1.0, s));
+    fine_apply(K_GENERAL, u, f, V, 1.0, -1.0, s);
     resid_nrm = std::sqrt(dot_host(n, V, V, s));
     if (resid_nrm != 0.) {
       double ieee = resid_nrm / resid_nrm;
@@ -322,7 +446,7 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
   while ((relative_resid >= tol || cycle_count < prm.min_iter) && cycle_count < prm.max_iter) {
     cycle(f, u, s);
     if (tol > 0.) {
-      HVE_HIP(launch_sell(K_RESID, lev_[0].A.view(), u, f, nullptr, nullptr, 0, V, -1.0, 0.0, s));
+      fine_apply(K_RESID, u, f, V, -1.0, 0.0, s);
       resid_nrm = std::sqrt(dot_host(n, V, V, s));
       if (prm.converge_type == 0) relative_resid = rhs_norm ? resid_nrm / rhs_norm : resid_nrm;
       else relative_resid = resid_nrm / resid_nrm_init;
@@ -341,9 +465,8 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
 // off; no recompute) with one BoomerAMG cycle on a cleared vector as the
 // preconditioner (HYPRE_BoomerAMGSolve with tol 0, max_iter 1).  Scalars stay
 // on the device; one host read per iteration for the convergence test.
-int pcg_solve(DevAMG* amg, const DevSell& A, const PCGParams& prm, const Precond& user_precond, const double* b,
-              double* x, hipStream_t s, int* iters, double* rel_res) {
-  const int n = A.nrows;
+int pcg_solve(DevAMG* amg, int n, const MatvecFn& Aop, const PCGParams& prm, const Precond& user_precond,
+              const double* b, double* x, hipStream_t s, int* iters, double* rel_res) {
   double* r = amg->scratch(0);
   double* p = amg->scratch(1);
   double* sv = amg->scratch(2);
@@ -383,7 +506,7 @@ int pcg_solve(DevAMG* amg, const DevSell& A, const PCGParams& prm, const Precond
     return 0;
   }
   // r = b - A x
-  HVE_HIP(launch_sell(K_RESID, A.view(), x, b, nullptr, nullptr, 0, r, -1.0, 0.0, s));
+  Aop(K_RESID, x, b, r);
   precond(r, p);
   amg->dot(n, r, p, sc + 0, s);  // gamma
   if (prm.two_norm) amg->dot(n, r, r, sc + 5, s);
@@ -391,7 +514,7 @@ int pcg_solve(DevAMG* amg, const DevSell& A, const PCGParams& prm, const Precond
   i_prod_0 = prm.two_norm ? hs[5] : hs[0];
   while (i + 1 <= prm.max_iter) {
     ++i;
-    HVE_HIP(launch_sell(K_MATVEC, A.view(), p, nullptr, nullptr, nullptr, 0, sv, 1.0, 0.0, s));
+    Aop(K_MATVEC, p, nullptr, sv);
     amg->dot(n, sv, p, sc + 2, s);
     HVE_HIP(launch_pcg_alpha(sc, s));
     HVE_HIP(launch_axpy(n, sc + 3, 0.0, 1.0, p, x, s));    // x += alpha p

@@ -1,6 +1,7 @@
 // Device-side runtime for the BoomerAMG solve path: operators resident in HBM,
 // the cycle driver (hypre_BoomerAMGCycle control flow) launching HIP kernels on
-// one stream, whole-cycle hipGraph capture, and the BoomerAMG / PCG loops.
+// one stream, halo exchange over RCCL on a side stream, whole-cycle hipGraph
+// capture, and the BoomerAMG / PCG loops.
 #pragma once
 #include <hip/hip_runtime.h>
 
@@ -8,10 +9,12 @@
 #include <functional>
 #include <map>
 #include <string>
+#include <tuple>
 #include <utility>
 #include <vector>
 
 #include "../host/hve_host.hpp"
+#include "../host/partition.hpp"
 #include "kernels.h"
 
 namespace hve {
@@ -27,90 +30,125 @@ struct DevSell {
   int* slice_ptr = nullptr;
   int* col = nullptr;
   double* val = nullptr;
+  int* rowmap = nullptr;
   SellView view() const {
     SellView v;
-    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.nrows = nrows; v.ncols = ncols;
+    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.nrows = nrows; v.ncols = ncols;
     return v;
   }
-  void upload(const CSR& A);
+  // rowmap: subset row -> local row; empty or identity -> no map
+  void upload(const CSR& A, const std::vector<int>& rowmap = {});
   void release();
-  size_t bytes() const { return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * 12; }
+  size_t bytes() const { return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * 12 + (rowmap ? (size_t)nrows * 4 : 0); }
+};
+
+// Rows of one operator a rank applies, split by whether they read halo values.
+struct DevOp {
+  DevSell in, bd;
+  int nrows_local = 0;
+  int64_t nnz() const { return in.nnz + bd.nnz; }
+  void upload(const RankOp& op);
+  void release() { in.release(); bd.release(); }
+};
+
+struct DevHalo {
+  int n_loc = 0, n_halo = 0, n_send = 0;
+  std::vector<int> peers, recv_cnt, recv_off, send_cnt, send_off;
+  int* d_send_idx = nullptr;
+  double* d_sendbuf = nullptr;
+  bool active() const { return !peers.empty(); }
+  void upload(const RankHalo& h);
+  void release();
 };
 
 struct DevLevel {
-  int n = 0;
-  DevSell A, P, R;        // P: n x n_{l+1}; R = P^T: n_{l+1} x n
-  double* l1 = nullptr;   // smoother scaling (l1 norms or diagonal)
+  int n = 0;               // owned rows
+  int first = 0, n_glob = 0;
+  DevOp A, P, R;
+  DevHalo hu, hv;
+  double* l1 = nullptr;
   int* cf = nullptr;
-  double* F = nullptr;    // rhs of this level (level 0: internal copy slot unused)
-  double* U[2] = {nullptr, nullptr};
-  double* V = nullptr;    // Vtemp
-  double* Z = nullptr;    // Ztemp (hybrid GS off-block copy)
-};
-
-struct KernelStats {
-  double ms[8] = {0};
+  double* F = nullptr;
+  double* U[2] = {nullptr, nullptr};  // n + hu.n_halo each
+  double* V = nullptr;                // n + hv.n_halo
 };
 
 class DevAMG {
  public:
   DevAMG() = default;
   ~DevAMG();
-  void build(const Hierarchy& H);
+  // Build from a (rank-local) hierarchy; nccl_comm = ncclComm_t or nullptr.
+  void build(const RankHierarchy& R, void* nccl_comm);
   // Scratch/dot workspace only (PCG without an AMG preconditioner).
-  void init_workspace(int n);
+  void init_workspace(int n, void* nccl_comm);
   void release();
   bool built() const { return !lev_.empty(); }
 
-  // One hypre_BoomerAMGCycle on device vectors f, u (natural order, length n0).
+  // One hypre_BoomerAMGCycle on device vectors f, u (owned rows, length n0).
   void cycle(const double* f, double* u, hipStream_t s);
-  // hypre_BoomerAMGSolve.  Returns 0 or HYPRE_ERROR_CONV-style flag.
   int solve(const double* f, double* u, hipStream_t s, int* iters, double* rel_res);
-  // device dot product into a device scalar
-  void dot(int n, const double* x, const double* y, double* out, hipStream_t s);
+  // y = op(A_0) x on owned rows (halo exchanged through an internal buffer)
+  void fine_apply(int op, const double* x, const double* b, double* y, double alpha, double temp, hipStream_t s);
+  void dot(int n, const double* x, const double* y, double* out, hipStream_t s);  // global (allreduce)
   double dot_host(int n, const double* x, const double* y, hipStream_t s);
-  int n0() const { return lev_.empty() ? 0 : lev_[0].n; }
+  int n0() const { return lev_.empty() ? ws_n_ : lev_[0].n; }
   int ws_n() const { return ws_n_; }
   int num_levels() const { return (int)lev_.size(); }
   const DevLevel& level(int l) const { return lev_[l]; }
-  const DevSell& fineA() const { return lev_[0].A; }
   hipStream_t stream() const { return stream_; }
   double* scratch(int i) { return scratch_[i]; }
   void set_use_graph(bool g) { use_graph_ = g; }
   double cycle_op_count() const { return cycle_ops_; }
+  bool multi_rank() const { return nccl_ != nullptr; }
 
   AMGParams prm;
 
  private:
-  void emit_cycle(const double* f, double* u, hipStream_t s);
+  void emit_cycle(const double* f0, double* u0, hipStream_t s);
   void relax(int level, int relax_type, int relax_points, const double* f, double*& u_cur, double*& u_alt,
              bool zero_guess, hipStream_t s);
+  // y = op(M) x with the halo of x exchanged first (interior rows overlap it)
+  void apply(const DevOp& M, const DevHalo* hx, int op, double* x, const double* b, const double* l1,
+             const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s);
+  void halo_start(const DevHalo& h, double* x, hipStream_t s);
+  void halo_finish(hipStream_t s);
+  void coarse_solve(int level, const double* f, double* u, hipStream_t s);
+
   std::vector<DevLevel> lev_;
   int coarse_n_ = 0;
   double* coarse_L_ = nullptr;
   unsigned char* coarse_mask_ = nullptr;
   double* coarse_U_ = nullptr;
+  double* coarse_f_ = nullptr;  // replicated rhs / solution of the coarsest level
+  double* coarse_u_ = nullptr;
+  double* u0_buf_[2] = {nullptr, nullptr};  // level-0 iterate with halo space (multi-rank)
+  double* x0_buf_ = nullptr;                // fine_apply input with halo space
   double* dot_part_ = nullptr;
   double* dscal_ = nullptr;  // device scalars
   double* hscal_ = nullptr;  // pinned host scalars
   double* scratch_[4] = {nullptr, nullptr, nullptr, nullptr};
   hipStream_t stream_ = nullptr;
+  hipStream_t comm_stream_ = nullptr;
+  hipEvent_t ev_packed_ = nullptr, ev_halo_ = nullptr;
+  void* nccl_ = nullptr;
   bool use_graph_ = true;
   double cycle_ops_ = 0;
   int ws_n_ = 0;
   std::map<std::pair<const void*, const void*>, hipGraphExec_t> graphs_;
 };
 
-// PCG (krylov/pcg.c:262) with a BoomerAMG V-cycle as preconditioner.
+// PCG (krylov/pcg.c:262).
 struct PCGParams {
   double tol = 1e-6, atol = 0.0;
   int max_iter = 1000;
   int two_norm = 0;
   int print_level = 0;
 };
-// precond(r, z): z = M^{-1} r on stream s (z need not be cleared by the caller).
+// precond(r, z): z = M^{-1} r on stream s.
 using Precond = std::function<void(const double* r, double* z)>;
-int pcg_solve(DevAMG* ws, const DevSell& A, const PCGParams& prm, const Precond& precond, const double* b, double* x,
-              hipStream_t s, int* iters, double* rel_res);
+// apply(op, x, b, y): op K_MATVEC (y = A x) or K_RESID (y = b - A x)
+using MatvecFn = std::function<void(int op, const double* x, const double* b, double* y)>;
+int pcg_solve(DevAMG* ws, int n, const MatvecFn& A, const PCGParams& prm, const Precond& precond, const double* b,
+              double* x, hipStream_t s, int* iters, double* rel_res);
 
 }  // namespace hve

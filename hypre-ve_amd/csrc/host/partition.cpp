@@ -1,0 +1,270 @@
+// Row partition of the hierarchy (see partition.hpp).
+#include "partition.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+namespace hve {
+
+namespace {
+
+int owner_of(const std::vector<int>& starts, int g) {
+  // starts: size+1 ascending; returns r with starts[r] <= g < starts[r+1]
+  auto it = std::upper_bound(starts.begin(), starts.end(), g);
+  return (int)(it - starts.begin()) - 1;
+}
+
+// Collect the sorted, unique global columns outside [a,b) referenced by rows
+// [r0,r1) of M.
+void halo_cols(const CSR& M, int r0, int r1, int a, int b, std::vector<int>& out) {
+  for (int r = r0; r < r1; ++r)
+    for (int k = M.i[r]; k < M.i[r + 1]; ++k) {
+      const int c = M.j[k];
+      if (c < a || c >= b) out.push_back(c);
+    }
+}
+void sort_unique(std::vector<int>& v) {
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+}
+
+// Build the local operator for rows [r0,r1) of M whose input vector is owned
+// on [a,b) with halo list `halo` (sorted global indices).
+void make_op(const CSR& M, int r0, int r1, int a, int b, const std::vector<int>& halo, RankOp& op) {
+  const int nloc_in = b - a;
+  const int nrows = r1 - r0;
+  op.nrows_local = nrows;
+  std::vector<char> bnd(nrows, 0);
+  for (int r = r0; r < r1; ++r)
+    for (int k = M.i[r]; k < M.i[r + 1]; ++k) {
+      const int c = M.j[k];
+      if (c < a || c >= b) { bnd[r - r0] = 1; break; }
+    }
+  auto build = [&](bool want_bnd, CSR& out, std::vector<int>& map) {
+    map.clear();
+    for (int r = 0; r < nrows; ++r)
+      if ((bool)bnd[r] == want_bnd) map.push_back(r);
+    const int m = (int)map.size();
+    out.resize_rows(m, nloc_in + (int)halo.size());
+    for (int q = 0; q < m; ++q) {
+      const int r = map[q] + r0;
+      out.i[q + 1] = out.i[q] + (M.i[r + 1] - M.i[r]);
+    }
+    out.j.resize(out.i[m]);
+    out.a.resize(out.i[m]);
+    for (int q = 0; q < m; ++q) {
+      const int r = map[q] + r0;
+      int o = out.i[q];
+      for (int k = M.i[r]; k < M.i[r + 1]; ++k, ++o) {
+        const int c = M.j[k];
+        int lc;
+        if (c >= a && c < b) lc = c - a;
+        else lc = nloc_in + (int)(std::lower_bound(halo.begin(), halo.end(), c) - halo.begin());
+        out.j[o] = lc;
+        out.a[o] = M.a[k];
+      }
+    }
+  };
+  build(false, op.interior, op.map_int);
+  build(true, op.boundary, op.map_bnd);
+}
+
+}  // namespace
+
+static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, int size,
+                          std::vector<RankHierarchy>& out) {
+  const int nl = (int)H.lev.size();
+  if ((int)starts0.size() != size + 1 || starts0[size] != H.lev[0].A.nrows)
+    throw std::runtime_error("partition: level-0 row starts do not cover the matrix");
+  std::vector<std::vector<int>> starts(nl, std::vector<int>(size + 1, 0));
+  starts[0] = starts0;
+  for (int l = 0; l + 1 < nl; ++l) {
+    const std::vector<int>& cf = H.lev[l].cf;
+    std::vector<int> pref(cf.size() + 1, 0);
+    for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] == 1);
+    for (int r = 0; r <= size; ++r) starts[l + 1][r] = pref[starts[l][r]];
+  }
+  out.assign(size, RankHierarchy());
+  for (int r = 0; r < size; ++r) {
+    RankHierarchy& R = out[r];
+    R.rank = r;
+    R.size = size;
+    R.prm = H.prm;
+    R.lev.resize(nl);
+    R.coarse_n = H.coarse_n;
+    R.coarse_dense = H.coarse_dense;
+    R.grid_complexity = H.grid_complexity;
+    R.operator_complexity = H.operator_complexity;
+    for (int l = 0; l < nl; ++l) {
+      R.nnz_A.push_back(H.lev[l].A.nnz());
+      R.rows.push_back(H.lev[l].A.nrows);
+    }
+  }
+  // halo sets per rank per level: u_l (A_l and P_{l-1}) and V_l (R_l)
+  std::vector<std::vector<std::vector<int>>> hu(nl, std::vector<std::vector<int>>(size)),
+      hv(nl, std::vector<std::vector<int>>(size));
+  for (int l = 0; l < nl; ++l) {
+    const Level& L = H.lev[l];
+#pragma omp parallel for schedule(dynamic)
+    for (int r = 0; r < size; ++r) {
+      const int a = starts[l][r], b = starts[l][r + 1];
+      std::vector<int> u;
+      halo_cols(L.A, a, b, a, b, u);
+      if (l > 0) halo_cols(H.lev[l - 1].P, starts[l - 1][r], starts[l - 1][r + 1], a, b, u);
+      sort_unique(u);
+      hu[l][r].swap(u);
+      if (l + 1 < nl) {
+        std::vector<int> v;
+        halo_cols(L.R, starts[l + 1][r], starts[l + 1][r + 1], a, b, v);
+        sort_unique(v);
+        hv[l][r].swap(v);
+      }
+    }
+  }
+  for (int l = 0; l < nl; ++l) {
+    const Level& L = H.lev[l];
+#pragma omp parallel for schedule(dynamic)
+    for (int r = 0; r < size; ++r) {
+      RankLevel& RL = out[r].lev[l];
+      const int a = starts[l][r], b = starts[l][r + 1];
+      RL.n_loc = b - a;
+      RL.first = a;
+      RL.n_glob = L.A.nrows;
+      make_op(L.A, a, b, a, b, hu[l][r], RL.A);
+      if (l + 1 < nl) {
+        const int ca = starts[l + 1][r], cb = starts[l + 1][r + 1];
+        make_op(L.P, a, b, ca, cb, hu[l + 1][r], RL.P);
+        make_op(L.R, ca, cb, a, b, hv[l][r], RL.R);
+      }
+      if (!L.l1.empty()) RL.l1.assign(L.l1.begin() + a, L.l1.begin() + b);
+      if (!L.cf.empty()) RL.cf.assign(L.cf.begin() + a, L.cf.begin() + b);
+      // halo plans
+      for (int which = 0; which < 2; ++which) {
+        if (which == 1 && l + 1 >= nl) break;
+        RankHalo& h = which == 0 ? RL.hu : RL.hv;
+        const std::vector<int>& mine = which == 0 ? hu[l][r] : hv[l][r];
+        h.n_loc = b - a;
+        h.n_halo = (int)mine.size();
+        h.halo_glob = mine;
+        // receive side: group my halo by owner
+        std::vector<int> rc(size, 0), sc(size, 0);
+        for (int g : mine) rc[owner_of(starts[l], g)]++;
+        // send side: every peer's halo entries that I own
+        std::vector<std::vector<int>> sidx(size);
+        for (int p = 0; p < size; ++p) {
+          if (p == r) continue;
+          const std::vector<int>& theirs = which == 0 ? hu[l][p] : hv[l][p];
+          auto lo = std::lower_bound(theirs.begin(), theirs.end(), a);
+          auto hi = std::lower_bound(theirs.begin(), theirs.end(), b);
+          for (auto it = lo; it != hi; ++it) sidx[p].push_back(*it - a);
+          sc[p] = (int)sidx[p].size();
+        }
+        for (int p = 0; p < size; ++p) {
+          if (p == r || (rc[p] == 0 && sc[p] == 0)) continue;
+          h.peers.push_back(p);
+          h.recv_cnt.push_back(rc[p]);
+          h.send_cnt.push_back(sc[p]);
+          h.send_idx.insert(h.send_idx.end(), sidx[p].begin(), sidx[p].end());
+        }
+      }
+    }
+  }
+}
+
+void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, int rank, int size,
+                         RankHierarchy& out) {
+  std::vector<RankHierarchy> all;
+  partition_all(H, starts0, size, all);
+  out = std::move(all[rank]);
+}
+
+void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out) {
+  std::vector<int> s0 = {0, H.lev[0].A.nrows};
+  partition_hierarchy(H, s0, 0, 1, out);
+}
+
+// ---------------------------------------------------------------------------
+// serialization (flat little-endian bytes; both ends are this library)
+// ---------------------------------------------------------------------------
+namespace {
+struct W {
+  std::vector<char>& b;
+  template <typename T> void pod(const T& v) {
+    const char* p = (const char*)&v;
+    b.insert(b.end(), p, p + sizeof(T));
+  }
+  template <typename T> void vec(const std::vector<T>& v) {
+    pod<int64_t>((int64_t)v.size());
+    const char* p = (const char*)v.data();
+    b.insert(b.end(), p, p + v.size() * sizeof(T));
+  }
+  void csr(const CSR& m) { pod(m.nrows); pod(m.ncols); vec(m.i); vec(m.j); vec(m.a); }
+  void op(const RankOp& o) { csr(o.interior); csr(o.boundary); vec(o.map_int); vec(o.map_bnd); pod(o.nrows_local); }
+  void halo(const RankHalo& h) {
+    pod(h.n_loc); pod(h.n_halo); vec(h.peers); vec(h.recv_cnt); vec(h.send_cnt); vec(h.send_idx); vec(h.halo_glob);
+  }
+};
+struct Rd {
+  const std::vector<char>& b;
+  size_t o = 0;
+  template <typename T> void pod(T& v) {
+    if (o + sizeof(T) > b.size()) throw std::runtime_error("deserialize: truncated buffer");
+    std::memcpy(&v, b.data() + o, sizeof(T));
+    o += sizeof(T);
+  }
+  template <typename T> void vec(std::vector<T>& v) {
+    int64_t n;
+    pod(n);
+    if (n < 0 || o + (size_t)n * sizeof(T) > b.size()) throw std::runtime_error("deserialize: bad length");
+    v.resize(n);
+    std::memcpy(v.data(), b.data() + o, n * sizeof(T));
+    o += n * sizeof(T);
+  }
+  void csr(CSR& m) { pod(m.nrows); pod(m.ncols); vec(m.i); vec(m.j); vec(m.a); }
+  void op(RankOp& x) { csr(x.interior); csr(x.boundary); vec(x.map_int); vec(x.map_bnd); pod(x.nrows_local); }
+  void halo(RankHalo& h) {
+    pod(h.n_loc); pod(h.n_halo); vec(h.peers); vec(h.recv_cnt); vec(h.send_cnt); vec(h.send_idx); vec(h.halo_glob);
+  }
+};
+const int64_t kMagic = 0x48564531414d47LL;  // "HVE1AMG"
+}  // namespace
+
+void serialize(const RankHierarchy& R, std::vector<char>& buf) {
+  buf.clear();
+  W w{buf};
+  w.pod(kMagic);
+  w.pod(R.rank); w.pod(R.size); w.pod(R.prm);
+  w.pod((int)R.lev.size());
+  for (const RankLevel& L : R.lev) {
+    w.pod(L.n_loc); w.pod(L.first); w.pod(L.n_glob);
+    w.op(L.A); w.op(L.P); w.op(L.R);
+    w.halo(L.hu); w.halo(L.hv);
+    w.vec(L.l1); w.vec(L.cf);
+  }
+  w.pod(R.coarse_n); w.vec(R.coarse_dense);
+  w.pod(R.grid_complexity); w.pod(R.operator_complexity);
+  w.vec(R.nnz_A); w.vec(R.rows);
+}
+
+void deserialize(const std::vector<char>& buf, RankHierarchy& R) {
+  Rd r{buf};
+  int64_t magic;
+  r.pod(magic);
+  if (magic != kMagic) throw std::runtime_error("deserialize: bad magic");
+  r.pod(R.rank); r.pod(R.size); r.pod(R.prm);
+  int nl;
+  r.pod(nl);
+  R.lev.assign(nl, RankLevel());
+  for (RankLevel& L : R.lev) {
+    r.pod(L.n_loc); r.pod(L.first); r.pod(L.n_glob);
+    r.op(L.A); r.op(L.P); r.op(L.R);
+    r.halo(L.hu); r.halo(L.hv);
+    r.vec(L.l1); r.vec(L.cf);
+  }
+  r.pod(R.coarse_n); r.vec(R.coarse_dense);
+  r.pod(R.grid_complexity); r.pod(R.operator_complexity);
+  r.vec(R.nnz_A); r.vec(R.rows);
+}
+
+}  // namespace hve

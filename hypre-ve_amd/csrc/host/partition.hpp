@@ -1,0 +1,70 @@
+// Row partition of a BoomerAMG hierarchy over ranks (one GPU per rank).
+//
+// Level 0 rows are owned in the caller's contiguous blocks (the ParCSR row
+// partition the user assembled, hypre's row_starts).  On every coarser level a
+// rank owns the C points of its fine rows (hypre_BoomerAMGCoarseParms), which
+// are again contiguous because fine_to_coarse is monotone.
+//
+// Each operator a rank applies is stored with columns in a [local | halo]
+// index space of the input vector (the reference's diag/offd pair with
+// col_map_offd, par_csr_matrix.h, folded into one column space), and its rows
+// are split into interior rows (no halo column: computed while the halo is in
+// flight) and boundary rows.  Entries keep their global row order, so every
+// row sum equals the single-GPU one bit for bit.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "hve_host.hpp"
+
+namespace hve {
+
+struct RankOp {
+  CSR interior, boundary;            // rows: subsets of the owned rows
+  std::vector<int> map_int, map_bnd; // subset row -> local row
+  int nrows_local = 0;               // owned rows of the output vector
+};
+
+// Halo of one vector: values this rank receives (placed after its n_loc owned
+// entries, grouped by peer in ascending global index) and sends.
+struct RankHalo {
+  int n_loc = 0, n_halo = 0;
+  std::vector<int> peers;      // ranks exchanged with (sorted)
+  std::vector<int> recv_cnt;   // per peer, contiguous at n_loc + recv_off
+  std::vector<int> send_cnt;   // per peer
+  std::vector<int> send_idx;   // local indices, concatenated per peer
+  std::vector<int> halo_glob;  // global indices of the halo entries (debug / tests)
+};
+
+struct RankLevel {
+  int n_loc = 0, first = 0, n_glob = 0;
+  RankOp A;          // A_l local rows; cols in u_l space
+  RankOp P;          // P_l local fine rows; cols in u_{l+1} space (not on coarsest)
+  RankOp R;          // R_l = P_l^T local coarse rows (level l+1); cols in V_l space
+  RankHalo hu;       // halo of u_l (union of A_l and P_{l-1} needs)
+  RankHalo hv;       // halo of V_l (R_l needs)
+  std::vector<double> l1;
+  std::vector<int> cf;
+};
+
+struct RankHierarchy {
+  int rank = 0, size = 1;
+  AMGParams prm;
+  std::vector<RankLevel> lev;
+  int coarse_n = 0;
+  std::vector<double> coarse_dense;  // replicated coarsest operator
+  double grid_complexity = 0, operator_complexity = 0;
+  std::vector<int64_t> nnz_A, rows;  // global per-level statistics
+};
+
+// starts0: level-0 row starts (size+1 entries).
+void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, int rank, int size,
+                         RankHierarchy& out);
+// Whole hierarchy as one rank (no halo), used for the single-GPU path.
+void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out);
+
+void serialize(const RankHierarchy& R, std::vector<char>& buf);
+void deserialize(const std::vector<char>& buf, RankHierarchy& R);
+
+}  // namespace hve

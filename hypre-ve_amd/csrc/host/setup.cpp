@@ -11,6 +11,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <chrono>
 #include <stdexcept>
 #ifdef _OPENMP
 #include <omp.h>
@@ -57,6 +58,61 @@ void generate_laplacian_7pt(int nx, int ny, int nz, double cx, double cy, double
     if (ix + 1 < nx) { A.j[k] = r + 1; A.a[k++] = v1; }
     if (iy + 1 < ny) { A.j[k] = r + nx; A.a[k++] = v2; }
     if (iz + 1 < nz) { A.j[k] = r + (int)nxny; A.a[k++] = v3; }
+  }
+}
+
+// Process-grid block (p,q,r) of GenerateLaplacian (par_laplace.c:15) with
+// hypre_GeneratePartitioning (seq_mv/genpart.c:18) and the global numbering of
+// hypre_map (par_laplace.c:363).  Rows come out with GLOBAL column indices,
+// each row's entries in the serial order (diag, z-, y-, x-, x+, y+, z+), so
+// the gathered matrix equals the one-process matrix for a z-slab partition.
+static std::vector<int64_t> gen_part(int64_t len, int np) {
+  std::vector<int64_t> part(np + 1, 0);
+  const int64_t size = len / np, rest = len - size * np;
+  for (int i = 0; i < np; ++i) part[i + 1] = part[i] + size + (i < rest ? 1 : 0);
+  return part;
+}
+void generate_laplacian_7pt_block(int nx, int ny, int nz, int P, int Q, int R, int p, int q, int r,
+                                  const double* value, CSR& A, int64_t& first_row) {
+  const auto xp = gen_part(nx, P), yp = gen_part(ny, Q), zp = gen_part(nz, R);
+  auto map = [&](int64_t ix, int64_t iy, int64_t iz, int pp, int qq, int rr) -> int64_t {
+    const int64_t nxl = xp[pp + 1] - xp[pp], nyl = yp[qq + 1] - yp[qq], nzl = zp[rr + 1] - zp[rr];
+    int64_t g = zp[rr] * nx * ny + yp[qq] * nx * nzl + xp[pp] * (nyl * nzl);
+    g += ((iz - zp[rr]) * nyl + (iy - yp[qq])) * nxl + (ix - xp[pp]);
+    return g;
+  };
+  const int nxl = (int)(xp[p + 1] - xp[p]), nyl = (int)(yp[q + 1] - yp[q]), nzl = (int)(zp[r + 1] - zp[r]);
+  const int64_t nloc = (int64_t)nxl * nyl * nzl;
+  if ((int64_t)nx * ny * nz > 0x7fffffffLL) throw std::runtime_error("global grid exceeds 2^31 rows");
+  first_row = map(xp[p], yp[q], zp[r], p, q, r);
+  A.resize_rows((int)nloc, (int)((int64_t)nx * ny * nz));
+  std::vector<int> len(nloc);
+#pragma omp parallel for schedule(static)
+  for (int64_t t = 0; t < nloc; ++t) {
+    const int64_t ix = xp[p] + t % nxl, iy = yp[q] + (t / nxl) % nyl, iz = zp[r] + t / ((int64_t)nxl * nyl);
+    len[t] = 1 + (iz > 0) + (iy > 0) + (ix > 0) + (ix + 1 < nx) + (iy + 1 < ny) + (iz + 1 < nz);
+  }
+  for (int64_t t = 0; t < nloc; ++t) A.i[t + 1] = A.i[t] + len[t];
+  A.j.resize(A.i[nloc]);
+  A.a.resize(A.i[nloc]);
+  auto owner = [](const std::vector<int64_t>& part, int64_t c) {
+    return (int)(std::upper_bound(part.begin(), part.end(), c) - part.begin()) - 1;
+  };
+#pragma omp parallel for schedule(static)
+  for (int64_t t = 0; t < nloc; ++t) {
+    const int64_t ix = xp[p] + t % nxl, iy = yp[q] + (t / nxl) % nyl, iz = zp[r] + t / ((int64_t)nxl * nyl);
+    int k = A.i[t];
+    auto put = [&](int64_t x, int64_t y, int64_t z, double v) {
+      A.j[k] = (int)map(x, y, z, owner(xp, x), owner(yp, y), owner(zp, z));
+      A.a[k++] = v;
+    };
+    put(ix, iy, iz, value[0]);
+    if (iz > 0) put(ix, iy, iz - 1, value[3]);
+    if (iy > 0) put(ix, iy - 1, iz, value[2]);
+    if (ix > 0) put(ix - 1, iy, iz, value[1]);
+    if (ix + 1 < nx) put(ix + 1, iy, iz, value[1]);
+    if (iy + 1 < ny) put(ix, iy + 1, iz, value[2]);
+    if (iz + 1 < nz) put(ix, iy, iz + 1, value[3]);
   }
 }
 
@@ -316,50 +372,60 @@ static void qsort2_abs(int* v, double* w, int left, int right) {
 void truncate_rows(CSR& P, double tol, int max_elmts) {
   if (tol <= 0.0 && max_elmts == 0) return;
   const int n = P.nrows;
+  std::vector<int> newlen(n, 0);
+  // each row is truncated in place inside its own slots (rows are independent)
+#pragma omp parallel
+  {
+    std::vector<int> rj;
+    std::vector<double> ra;
+#pragma omp for schedule(static)
+    for (int r = 0; r < n; ++r) {
+      const int b = P.i[r], e = P.i[r + 1];
+      rj.assign(P.j.begin() + b, P.j.begin() + e);
+      ra.assign(P.a.begin() + b, P.a.begin() + e);
+      if (tol > 0) {
+        double row_nrm = 0;
+        for (double x : ra) row_nrm = (row_nrm < std::fabs(x)) ? std::fabs(x) : row_nrm;
+        const double drop = tol * row_nrm;
+        double row_sum = 0, scale = 0;
+        size_t o = 0;
+        for (size_t k = 0; k < ra.size(); ++k) {
+          row_sum += ra[k];
+          if (!(std::fabs(ra[k]) < drop)) { scale += ra[k]; rj[o] = rj[k]; ra[o] = ra[k]; ++o; }
+        }
+        rj.resize(o);
+        ra.resize(o);
+        if (scale != 0. && scale != row_sum) {
+          scale = row_sum / scale;
+          for (double& x : ra) x *= scale;
+        }
+      }
+      if (max_elmts > 0 && (int)ra.size() > max_elmts) {
+        double row_sum = 0;
+        for (double x : ra) row_sum += x;
+        qsort2_abs(rj.data(), ra.data(), 0, (int)ra.size() - 1);
+        double scale = 0;
+        for (int k = 0; k < max_elmts; ++k) scale += ra[k];
+        rj.resize(max_elmts);
+        ra.resize(max_elmts);
+        if (scale != 0. && scale != row_sum) {
+          scale = row_sum / scale;
+          for (double& x : ra) x *= scale;
+        }
+      }
+      std::copy(rj.begin(), rj.end(), P.j.begin() + b);
+      std::copy(ra.begin(), ra.end(), P.a.begin() + b);
+      newlen[r] = (int)ra.size();
+    }
+  }
   std::vector<int> ni(n + 1, 0);
-  std::vector<int> nj;
-  std::vector<double> na;
-  nj.reserve(P.j.size());
-  na.reserve(P.a.size());
-  std::vector<int> rj;
-  std::vector<double> ra;
+  for (int r = 0; r < n; ++r) ni[r + 1] = ni[r] + newlen[r];
+  std::vector<int> nj(ni[n]);
+  std::vector<double> na(ni[n]);
+#pragma omp parallel for schedule(static)
   for (int r = 0; r < n; ++r) {
-    rj.assign(P.j.begin() + P.i[r], P.j.begin() + P.i[r + 1]);
-    ra.assign(P.a.begin() + P.i[r], P.a.begin() + P.i[r + 1]);
-    if (tol > 0) {
-      double row_nrm = 0;
-      for (double x : ra) row_nrm = (row_nrm < std::fabs(x)) ? std::fabs(x) : row_nrm;
-      const double drop = tol * row_nrm;
-      double row_sum = 0, scale = 0;
-      std::vector<int> kj;
-      std::vector<double> ka;
-      for (size_t k = 0; k < ra.size(); ++k) {
-        row_sum += ra[k];
-        if (!(std::fabs(ra[k]) < drop)) { scale += ra[k]; kj.push_back(rj[k]); ka.push_back(ra[k]); }
-      }
-      if (scale != 0. && scale != row_sum) {
-        scale = row_sum / scale;
-        for (double& x : ka) x *= scale;
-      }
-      rj.swap(kj);
-      ra.swap(ka);
-    }
-    if (max_elmts > 0 && (int)ra.size() > max_elmts) {
-      double row_sum = 0;
-      for (double x : ra) row_sum += x;
-      qsort2_abs(rj.data(), ra.data(), 0, (int)ra.size() - 1);
-      double scale = 0;
-      for (int k = 0; k < max_elmts; ++k) scale += ra[k];
-      rj.resize(max_elmts);
-      ra.resize(max_elmts);
-      if (scale != 0. && scale != row_sum) {
-        scale = row_sum / scale;
-        for (double& x : ra) x *= scale;
-      }
-    }
-    nj.insert(nj.end(), rj.begin(), rj.end());
-    na.insert(na.end(), ra.begin(), ra.end());
-    ni[r + 1] = (int)nj.size();
+    std::copy(P.j.begin() + P.i[r], P.j.begin() + P.i[r] + newlen[r], nj.begin() + ni[r]);
+    std::copy(P.a.begin() + P.i[r], P.a.begin() + P.i[r] + newlen[r], na.begin() + ni[r]);
   }
   P.i.swap(ni);
   P.j.swap(nj);
@@ -372,95 +438,112 @@ void truncate_rows(CSR& P, double tol, int max_elmts) {
 // ---------------------------------------------------------------------------
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P) {
+  // Row-parallel restatement.  Each row's P entries depend only on the
+  // markers set while processing that row (stale markers of earlier rows of
+  // the same thread are below jj_begin_row or are other negative stamps), so a
+  // thread-local P_marker processed in increasing row order reproduces the
+  // single-thread result entry for entry.
   const int n = A.nrows;
   std::vector<int> fine_to_coarse(n, -1);
-  std::vector<int> P_marker(n, -1);
-  P.resize_rows(n, 0);
-  // first pass: size of P and fine_to_coarse
-  int jj_counter = 0, coarse_counter = 0;
-  for (int i = 0; i < n; ++i) {
-    P.i[i] = jj_counter;
-    if (cf[i] >= 0) {
-      jj_counter++;
-      fine_to_coarse[i] = coarse_counter++;
-    } else if (cf[i] != SF_PT) {
-      for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
-        int i1 = S.j[jj];
-        if (cf[i1] >= 0) {
-          if (P_marker[i1] < P.i[i]) { P_marker[i1] = jj_counter; jj_counter++; }
-        } else if (cf[i1] != SF_PT) {
-          for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
-            int k1 = S.j[kk];
-            if (cf[k1] >= 0 && P_marker[k1] < P.i[i]) { P_marker[k1] = jj_counter; jj_counter++; }
+  int coarse_counter = 0;
+  for (int i = 0; i < n; ++i)
+    if (cf[i] >= 0) fine_to_coarse[i] = coarse_counter++;
+  P.resize_rows(n, coarse_counter);
+  std::vector<int> rowcnt(n, 0);
+#pragma omp parallel
+  {
+    std::vector<int> P_marker(n, -1);
+#pragma omp for schedule(static)
+    for (int i = 0; i < n; ++i) {
+      // first pass (par_lr_interp.c:1290-1370): |C-hat_i|, stamped by row id
+      int cnt = 0;
+      const int stamp = i;
+      if (cf[i] >= 0) {
+        cnt = 1;
+      } else if (cf[i] != SF_PT) {
+        for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+          int i1 = S.j[jj];
+          if (cf[i1] >= 0) {
+            if (P_marker[i1] != stamp) { P_marker[i1] = stamp; cnt++; }
+          } else if (cf[i1] != SF_PT) {
+            for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+              int k1 = S.j[kk];
+              if (cf[k1] >= 0 && P_marker[k1] != stamp) { P_marker[k1] = stamp; cnt++; }
+            }
           }
         }
       }
+      rowcnt[i] = cnt;
     }
   }
-  P.i[n] = jj_counter;
-  P.ncols = coarse_counter;
-  P.j.assign(jj_counter, 0);
-  P.a.assign(jj_counter, 0.0);
-  std::fill(P_marker.begin(), P_marker.end(), -1);
-  int strong_f_marker = -2;
-  for (int i = 0; i < n; ++i) {
-    const int jj_begin_row = P.i[i];
-    int jc = jj_begin_row;
-    if (cf[i] >= 0) {
-      P.j[jc] = fine_to_coarse[i];
-      P.a[jc] = 1.0;
-      jc++;
-    } else if (cf[i] != SF_PT) {
-      strong_f_marker--;
-      for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
-        int i1 = S.j[jj];
-        if (cf[i1] >= 0) {
-          if (P_marker[i1] < jj_begin_row) {
-            P_marker[i1] = jc; P.j[jc] = fine_to_coarse[i1]; P.a[jc] = 0.0; jc++;
-          }
-        } else if (cf[i1] != SF_PT) {
-          P_marker[i1] = strong_f_marker;
-          for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
-            int k1 = S.j[kk];
-            if (cf[k1] >= 0 && P_marker[k1] < jj_begin_row) {
-              P_marker[k1] = jc; P.j[jc] = fine_to_coarse[k1]; P.a[jc] = 0.0; jc++;
+  for (int i = 0; i < n; ++i) P.i[i + 1] = P.i[i] + rowcnt[i];
+  const int64_t nnzP = P.i[n];
+  P.j.assign(nnzP, 0);
+  P.a.assign(nnzP, 0.0);
+#pragma omp parallel
+  {
+    std::vector<int> P_marker(n, -1);
+    int strong_f_marker = -2;
+#pragma omp for schedule(static)
+    for (int i = 0; i < n; ++i) {
+      const int jj_begin_row = P.i[i];
+      int jc = jj_begin_row;
+      if (cf[i] >= 0) {
+        P.j[jc] = fine_to_coarse[i];
+        P.a[jc] = 1.0;
+        jc++;
+      } else if (cf[i] != SF_PT) {
+        strong_f_marker--;
+        for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+          int i1 = S.j[jj];
+          if (cf[i1] >= 0) {
+            if (P_marker[i1] < jj_begin_row) {
+              P_marker[i1] = jc; P.j[jc] = fine_to_coarse[i1]; P.a[jc] = 0.0; jc++;
+            }
+          } else if (cf[i1] != SF_PT) {
+            P_marker[i1] = strong_f_marker;
+            for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+              int k1 = S.j[kk];
+              if (cf[k1] >= 0 && P_marker[k1] < jj_begin_row) {
+                P_marker[k1] = jc; P.j[jc] = fine_to_coarse[k1]; P.a[jc] = 0.0; jc++;
+              }
             }
           }
         }
-      }
-      const int jj_end_row = jc;
-      double diagonal = A.a[A.i[i]];
-      for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
-        int i1 = A.j[jj];
-        if (P_marker[i1] >= jj_begin_row) {
-          P.a[P_marker[i1]] += A.a[jj];
-        } else if (P_marker[i1] == strong_f_marker) {
-          double sum = 0.0;
-          int sgn = 1;
-          if (A.a[A.i[i1]] < 0) sgn = -1;
-          for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
-            int i2 = A.j[jj1];
-            if ((P_marker[i2] >= jj_begin_row || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
-          }
-          if (sum != 0) {
-            double distribute = A.a[jj] / sum;
+        const int jj_end_row = jc;
+        double diagonal = A.a[A.i[i]];
+        for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
+          int i1 = A.j[jj];
+          if (P_marker[i1] >= jj_begin_row) {
+            P.a[P_marker[i1]] += A.a[jj];
+          } else if (P_marker[i1] == strong_f_marker) {
+            double sum = 0.0;
+            int sgn = 1;
+            if (A.a[A.i[i1]] < 0) sgn = -1;
             for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
               int i2 = A.j[jj1];
-              if (P_marker[i2] >= jj_begin_row && (sgn * A.a[jj1]) < 0) P.a[P_marker[i2]] += distribute * A.a[jj1];
-              if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
+              if ((P_marker[i2] >= jj_begin_row || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
             }
-          } else {
+            if (sum != 0) {
+              double distribute = A.a[jj] / sum;
+              for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
+                int i2 = A.j[jj1];
+                if (P_marker[i2] >= jj_begin_row && (sgn * A.a[jj1]) < 0) P.a[P_marker[i2]] += distribute * A.a[jj1];
+                if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
+              }
+            } else {
+              diagonal += A.a[jj];
+            }
+          } else if (cf[i1] != SF_PT) {
             diagonal += A.a[jj];
           }
-        } else if (cf[i1] != SF_PT) {
-          diagonal += A.a[jj];
+        }
+        if (diagonal) {
+          for (int jj = jj_begin_row; jj < jj_end_row; ++jj) P.a[jj] /= -diagonal;
         }
       }
-      if (diagonal) {
-        for (int jj = jj_begin_row; jj < jj_end_row; ++jj) P.a[jj] /= -diagonal;
-      }
+      strong_f_marker--;
     }
-    strong_f_marker--;
   }
   if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
   for (int i = 0; i < n; ++i)
@@ -674,16 +757,23 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
   char buf[256];
   int level = 0;
   bool finished = prm.max_levels <= 1;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double t_s = 0, t_c = 0, t_i = 0, t_r = 0, t_t = 0;
   while (!finished) {
     Level& L = H.lev[level];
     const int fine_size = L.A.nrows;
     Pattern S;
+    double t0 = now();
     create_strength(L.A, prm.strong_threshold, prm.max_row_sum, S);
+    double t1 = now();
+    t_s += t1 - t0;
     std::vector<int> cf;
     if (coarsen_type == 8) coarsen_pmis(S, 0, cf);
     else if (coarsen_type == 9) coarsen_pmis(S, 2, cf);
     else if (coarsen_type == 10) coarsen_hmis(S, prm.measure_type, cf);
     else throw std::runtime_error("unsupported coarsen_type " + std::to_string(coarsen_type));
+    double t2 = now();
+    t_c += t2 - t1;
     int coarse_size = 0;
     for (int v : cf) coarse_size += (v == 1);
     if (coarse_size == 0 || coarse_size == fine_size) {
@@ -698,11 +788,16 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     if (prm.interp_type == 6) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));
+    double t3 = now();
+    t_i += t3 - t2;
     CSR Ac;
     rap(P, L.A, Ac);
+    double t4 = now();
+    t_r += t4 - t3;
     L.cf.swap(cf);
     L.P.swap(P);
     transpose(L.P, L.R);
+    t_t += now() - t4;
     snprintf(buf, sizeof buf, "level %d: rows %d nnz %lld -> coarse %d (P nnz %lld)\n", level, fine_size,
              (long long)L.A.nnz(), coarse_size, (long long)L.P.nnz());
     H.log += buf;
@@ -715,6 +810,10 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     }
     if (level == prm.max_levels - 1 || coarse_size <= prm.max_coarse_size) finished = true;
   }
+  snprintf(buf, sizeof buf, "setup phases: strength %.3fs coarsen %.3fs interp %.3fs rap %.3fs transpose %.3fs\n",
+           t_s, t_c, t_i, t_r, t_t);
+  H.log += buf;
+  if (prm.print_level > 0) fputs(H.log.c_str(), stderr);
   const int nl = (int)H.lev.size();
   // l1 norms for the smoothers that need them
   for (int j = 0; j < nl; ++j) {

@@ -1,0 +1,68 @@
+"""Host setup logic: determinism across thread counts, structural invariants."""
+import hashlib
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_SCRIPT = r"""
+import sys, hashlib, numpy as np
+sys.path.insert(0, %r)
+import hypreve as hv
+A = hv.ParCSRMatrix.laplacian(24, 22, 20)
+amg = hv.BoomerAMG(**hv.ij_amg_defaults(0)); amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4)
+amg.setup_host(A)
+h = hashlib.sha256()
+for l in range(amg.num_levels()):
+    for w in (0, 1):
+        ip, jj, vv, shp = amg.level_matrix(l, w)
+        for a in (ip, jj, vv): h.update(np.ascontiguousarray(a).tobytes())
+    h.update(amg.level_vector(l, 0).tobytes()); h.update(amg.level_vector(l, 1).tobytes())
+print(h.hexdigest())
+""" % os.path.join(ROOT, "hypre-ve_amd")
+
+
+def _digest(threads):
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    out = subprocess.run([sys.executable, "-c", _SCRIPT], env=env, capture_output=True, text=True, check=True)
+    return out.stdout.strip()
+
+
+def test_setup_bitwise_independent_of_threads():
+    d1 = _digest(1)
+    assert d1 == _digest(3) == _digest(8)
+
+
+def test_hierarchy_invariants(hv):
+    A = hv.ParCSRMatrix.laplacian(16, 16, 16)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4)
+    amg.setup_host(A)
+    nl = amg.num_levels()
+    assert nl >= 3
+    import scipy.sparse as sp
+    for l in range(nl - 1):
+        ip, jj, vv, shp = amg.level_matrix(l, 0)
+        Al = sp.csr_matrix((vv, jj, ip), shape=shp)
+        # diagonal stored first in every row (hypre ParCSR convention)
+        assert np.all(jj[ip[:-1]] == np.arange(shp[0]))
+        ip, jj, vv, pshp = amg.level_matrix(l, 1)
+        P = sp.csr_matrix((vv, jj, ip), shape=pshp)
+        assert np.all(np.diff(ip) <= 4)  # P_max_elmts
+        cf = amg.level_vector(l, 0)
+        # C points interpolate by injection
+        c = np.where(cf == 1)[0]
+        assert np.allclose(P[c].toarray().max(axis=1), 1.0)
+        ip, jj, vv, cshp = amg.level_matrix(l + 1, 0)
+        Ac = sp.csr_matrix((vv, jj, ip), shape=cshp)
+        # Galerkin: A_c == P^T A P (values; order of summation may differ slightly)
+        G = (P.T @ Al @ P).tocsr()
+        assert abs(G - Ac).max() < 1e-12 * abs(Ac).max()
+        # symmetric
+        assert abs(Ac - Ac.T).max() < 1e-12 * abs(Ac).max()
+        # l1 norms (relax 18): row sums of |a|
+        l1 = amg.level_vector(l, 1)
+        assert np.allclose(l1, abs(Al).sum(axis=1).A1, rtol=1e-14)
