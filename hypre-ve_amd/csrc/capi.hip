@@ -704,6 +704,16 @@ HYPRE_Int hypreve_BoomerAMGSetUseGraph(HYPRE_Solver s, HYPRE_Int g) {
   return 0;
 }
 
+HYPRE_Int hypreve_BoomerAMGPartitionCheck(HYPRE_Solver s, HYPRE_Int size) {
+  CHECK_ARG(s && s->kind == KIND_AMG && !s->H.lev.empty(), 1);
+  CHECK_ARG(size >= 1, 2);
+  API_BEGIN
+  std::string msg;
+  const int errs = partition_self_check(s->H, size, msg);
+  if (errs) return set_err(HYPRE_ERROR_GENERIC, msg);
+  API_END
+}
+
 HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(A, 2);

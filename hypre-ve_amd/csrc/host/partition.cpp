@@ -172,6 +172,94 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
   }
 }
 
+// Self-check used by the CPU test-suite: reassembles every rank's operators,
+// checks halo plans pairwise and emulates the distributed apply (interior +
+// boundary rows over [local | halo] vectors) against the global operator.
+int partition_self_check(const Hierarchy& H, int size, std::string& msg) {
+  const int n0 = H.lev[0].A.nrows;
+  std::vector<int> s0(size + 1);
+  for (int r = 0; r <= size; ++r) s0[r] = (int)((int64_t)n0 * r / size);
+  std::vector<RankHierarchy> all;
+  partition_all(H, s0, size, all);
+  int errs = 0;
+  auto fail = [&](const std::string& m) { if (errs++ < 5) msg += m + "\n"; };
+  // serialization round trip
+  for (int r = 0; r < size; ++r) {
+    std::vector<char> b1, b2;
+    serialize(all[r], b1);
+    RankHierarchy back;
+    deserialize(b1, back);
+    serialize(back, b2);
+    if (b1 != b2) fail("serialize round trip differs on rank " + std::to_string(r));
+  }
+  const int nl = (int)H.lev.size();
+  uint64_t seed = 12345;
+  auto rnd = [&]() { seed = seed * 6364136223846793005ULL + 1442695040888963407ULL; return (double)(seed >> 11) / 9007199254740992.0 - 0.5; };
+  for (int l = 0; l < nl; ++l) {
+    for (int which = 0; which < 3; ++which) {  // A, P, R
+      if (which > 0 && l + 1 >= nl) continue;
+      const CSR& G = which == 0 ? H.lev[l].A : (which == 1 ? H.lev[l].P : H.lev[l].R);
+      std::vector<double> x(G.ncols), yg(G.nrows, 0.0), yd(G.nrows, 0.0);
+      for (auto& v : x) v = rnd();
+      for (int i = 0; i < G.nrows; ++i) {
+        double t = 0.0;
+        for (int k = G.i[i]; k < G.i[i + 1]; ++k) t += G.a[k] * x[G.j[k]];
+        yg[i] = t;
+      }
+      for (int r = 0; r < size; ++r) {
+        const RankLevel& L = all[r].lev[l];
+        // input vector ownership and halo for this operator
+        const RankLevel& Lin = which == 1 ? all[r].lev[l + 1] : L;
+        const RankHalo& h = which == 2 ? L.hv : Lin.hu;
+        const int in_first = Lin.first, in_loc = Lin.n_loc;
+        std::vector<double> xl(in_loc + h.n_halo);
+        for (int i = 0; i < in_loc; ++i) xl[i] = x[in_first + i];
+        for (int k = 0; k < h.n_halo; ++k) xl[in_loc + k] = x[h.halo_glob[k]];
+        const RankOp& op = which == 0 ? L.A : (which == 1 ? L.P : L.R);
+        const int out_first = which == 2 ? all[r].lev[l + 1].first : L.first;
+        for (int part = 0; part < 2; ++part) {
+          const CSR& M = part == 0 ? op.interior : op.boundary;
+          const std::vector<int>& mp = part == 0 ? op.map_int : op.map_bnd;
+          for (int q = 0; q < M.nrows; ++q) {
+            double t = 0.0;
+            for (int k = M.i[q]; k < M.i[q + 1]; ++k) {
+              if (part == 0 && M.j[k] >= in_loc) fail("interior row reads a halo column");
+              t += M.a[k] * xl[M.j[k]];
+            }
+            yd[out_first + mp[q]] = t;
+          }
+        }
+      }
+      for (int i = 0; i < G.nrows; ++i)
+        if (yg[i] != yd[i]) { fail("level " + std::to_string(l) + " op " + std::to_string(which) + " row " + std::to_string(i) + " differs"); break; }
+    }
+    // pairwise halo plans: what p sends to r == r's halo entries owned by p
+    for (int which = 0; which < 2; ++which) {
+      if (which == 1 && l + 1 >= nl) continue;
+      for (int r = 0; r < size; ++r) {
+        const RankHalo& hr = which == 0 ? all[r].lev[l].hu : all[r].lev[l].hv;
+        int roff = 0;
+        for (size_t q = 0; q < hr.peers.size(); ++q) {
+          const int p = hr.peers[q];
+          const RankHalo& hp = which == 0 ? all[p].lev[l].hu : all[p].lev[l].hv;
+          auto it = std::find(hp.peers.begin(), hp.peers.end(), r);
+          if (it == hp.peers.end()) { fail("asymmetric peer lists"); continue; }
+          const size_t pq = it - hp.peers.begin();
+          int soff = 0;
+          for (size_t z = 0; z < pq; ++z) soff += hp.send_cnt[z];
+          if (hp.send_cnt[pq] != hr.recv_cnt[q]) fail("send/recv count mismatch");
+          else
+            for (int k = 0; k < hr.recv_cnt[q]; ++k)
+              if (all[p].lev[l].first + hp.send_idx[soff + k] != hr.halo_glob[roff + k]) { fail("halo order mismatch"); break; }
+          roff += hr.recv_cnt[q];
+        }
+        if (roff != hr.n_halo) fail("halo not fully received");
+      }
+    }
+  }
+  return errs;
+}
+
 void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, int rank, int size,
                          RankHierarchy& out) {
   std::vector<RankHierarchy> all;

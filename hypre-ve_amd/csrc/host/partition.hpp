@@ -64,6 +64,8 @@ void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, in
 // Whole hierarchy as one rank (no halo), used for the single-GPU path.
 void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out);
 
+int partition_self_check(const Hierarchy& H, int size, std::string& msg);
+
 void serialize(const RankHierarchy& R, std::vector<char>& buf);
 void deserialize(const std::vector<char>& buf, RankHierarchy& R);
 

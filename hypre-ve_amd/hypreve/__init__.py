@@ -158,6 +158,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGGetCoarseMatrix", _i, [_p, _pi, _pd]),
     ("hypreve_BoomerAMGGetRelaxInfo", _i, [_p, _pi, _pi, _pd, _pi]),
     ("hypreve_BoomerAMGSetupHost", _i, [_p, _p]),
+    ("hypreve_BoomerAMGPartitionCheck", _i, [_p, _i]),
     ("hypreve_BoomerAMGCycle", _i, [_p, _p, _p]),
     ("hypreve_BoomerAMGGetKernelStats", _i, [_p, _pd, _i]),
     ("hypreve_BenchFineSpMV", _i, [_p, _i, _pd, _pd]),
@@ -316,6 +317,9 @@ class BoomerAMG:
 
     def setup(self, A, b=None, x=None):
         check(lib().HYPRE_BoomerAMGSetup(self.h, A.h, b.h if b else None, x.h if x else None), "BoomerAMGSetup")
+
+    def partition_check(self, size):
+        check(lib().hypreve_BoomerAMGPartitionCheck(self.h, size), "PartitionCheck")
 
     def setup_host(self, A):
         check(lib().hypreve_BoomerAMGSetupHost(self.h, A.h), "BoomerAMGSetupHost")

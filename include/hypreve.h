@@ -225,6 +225,9 @@ HYPRE_Int hypreve_BoomerAMGGetRelaxInfo(HYPRE_Solver solver, HYPRE_Int *relax_ty
 /* Host-only setup (no device upload): lets the CPU test suite check the
  * hierarchy against the reference fixtures on a machine without a GPU. */
 HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver solver, HYPRE_ParCSRMatrix A);
+/* CPU self-check of the row partition of the host hierarchy over `size`
+ * ranks: reassembly, pairwise halo plans, emulated distributed apply. */
+HYPRE_Int hypreve_BoomerAMGPartitionCheck(HYPRE_Solver solver, HYPRE_Int size);
 /* Run exactly one cycle (hypre_BoomerAMGCycle) on device vectors f, u. */
 HYPRE_Int hypreve_BoomerAMGCycle(HYPRE_Solver solver, HYPRE_ParVector f, HYPRE_ParVector u);
 /* Device timing of the last Solve, per kernel class (ms), for bench/profiling. */

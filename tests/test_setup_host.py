@@ -66,3 +66,15 @@ def test_hierarchy_invariants(hv):
         # l1 norms (relax 18): row sums of |a|
         l1 = amg.level_vector(l, 1)
         assert np.allclose(l1, abs(Al).sum(axis=1).A1, rtol=1e-14)
+
+
+def test_partition_self_check(hv):
+    """Row partition over N ranks: every rank's interior+boundary operators on
+    [local | halo] vectors reproduce the global operators row for row (bitwise),
+    and the pairwise halo send/recv plans agree."""
+    A = hv.ParCSRMatrix.laplacian(20, 18, 24)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4)
+    amg.setup_host(A)
+    for size in (1, 2, 3, 4, 7, 8):
+        amg.partition_check(size)
