@@ -63,8 +63,40 @@ struct SpArgs {
   int relax_points;
 };
 
+// Row accumulation in stored order, loads batched B entries at a time: the B
+// column and value loads of a batch are issued together, then the B gathers of
+// x, then the B dependent adds in order.  This keeps B independent memory
+// chains in flight per lane (a lane-per-row loop with one load pair per step is
+// latency-bound on the long rows of the Galerkin levels) without changing the
+// order or rounding of the row sum.
+template <bool SUB, int B>
+__device__ __forceinline__ double sell_row(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
+                                           int width, const double* __restrict__ x, double t) {
+  for (int k = k0; k < width; k += B) {
+    int c[B];
+    double a[B], xv[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const bool in = (k + q) < width;
+      c[q] = in ? cp[(k + q) * kWave] : -1;
+      a[q] = in ? vp[(k + q) * kWave] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) xv[q] = c[q] >= 0 ? x[c[q]] : 0.0;
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      if (c[q] >= 0) {
+        if (SUB) t -= a[q] * xv[q];
+        else t += a[q] * xv[q];
+      }
+    }
+  }
+  return t;
+}
+
 template <int OP, bool CFSEL>
 __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
+  constexpr int B = 8;
   const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
   const int row = lb * 256 + threadIdx.x;
   if (row >= p.nrows) return;
@@ -84,49 +116,22 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
   }
 
   if (OP == OP_RESID || OP == OP_L1JAC) {
-    double t = p.b[g];
-    for (int k = 0; k < width; ++k) {
-      const int c = cp[k * kWave];
-      const double a = vp[k * kWave];
-      if (c >= 0) t -= a * p.x[c];
-    }
+    const double t = sell_row<true, B>(cp, vp, 0, width, p.x, p.b[g]);
     if (OP == OP_RESID) p.y[g] = t;
     else p.y[g] = p.x[g] + t / p.l1[g];
   } else if (OP == OP_L1JAC_W) {
-    double t = -p.b[g];
-    for (int k = 0; k < width; ++k) {
-      const int c = cp[k * kWave];
-      const double a = vp[k * kWave];
-      if (c >= 0) t += a * p.x[c];
-    }
+    const double t = sell_row<false, B>(cp, vp, 0, width, p.x, -p.b[g]);
     const double v = (-p.w) * t;
     p.y[g] = p.x[g] + v / p.l1[g];
   } else if (OP == OP_MATVEC || OP == OP_RESTRICT) {
-    double t = 0.0;
-    for (int k = 0; k < width; ++k) {
-      const int c = cp[k * kWave];
-      const double a = vp[k * kWave];
-      if (c >= 0) t += a * p.x[c];
-    }
-    p.y[g] = t;
+    p.y[g] = sell_row<false, B>(cp, vp, 0, width, p.x, 0.0);
   } else if (OP == OP_PROLONG) {
-    double t = p.y[g];
-    for (int k = 0; k < width; ++k) {
-      const int c = cp[k * kWave];
-      const double a = vp[k * kWave];
-      if (c >= 0) t += a * p.x[c];
-    }
-    p.y[g] = t;
+    p.y[g] = sell_row<false, B>(cp, vp, 0, width, p.x, p.y[g]);
   } else if (OP == OP_JAC) {
     const double d = vp[0];  // diagonal stored first
     const double uo = p.x[g];
     if (d == 0.0) { p.y[g] = uo; return; }
-    double t = p.b[g];
-    for (int k = 1; k < width; ++k) {
-      const int c = cp[k * kWave];
-      const double a = vp[k * kWave];
-      if (c >= 0) t -= a * p.x[c];
-    }
+    const double t = sell_row<true, B>(cp, vp, 1, width, p.x, p.b[g]);
     double u = uo * (1.0 - p.w);
     u += p.w * t / d;
     p.y[g] = u;
@@ -139,14 +144,8 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     else if (temp == -1.0) t = neg ? p.b[g] : -p.b[g];
     else if (temp == 1.0) t = neg ? -p.b[g] : p.b[g];
     else t = neg ? -p.b[g] * temp : p.b[g] * temp;
-    for (int k = 0; k < width; ++k) {
-      const int c = cp[k * kWave];
-      const double a = vp[k * kWave];
-      if (c >= 0) {
-        if (neg) t -= a * p.x[c];
-        else t += a * p.x[c];
-      }
-    }
+    if (neg) t = sell_row<true, B>(cp, vp, 0, width, p.x, t);
+    else t = sell_row<false, B>(cp, vp, 0, width, p.x, t);
     p.y[g] = (alpha == 1.0 || neg) ? t : alpha * t;
   }
 }
