@@ -28,38 +28,17 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=256, help="grid edge per GPU (n^3 rows per GPU)")
-    ap.add_argument("--cpu-cycles", type=int, default=3, help="oracle V-cycles for the CPU baseline (0 = skip)")
-    ap.add_argument("--spmv-reps", type=int, default=50)
-    args = ap.parse_args()
+def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
+    """One rank's part of the bench; returns the JSON dict on rank 0."""
+    import torch
 
-    import torch  # loads the HIP runtime the library then shares
-
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("gloo")
-    else:
-        torch.cuda.set_device(0)
-
-    import hypreve as hv
-
-    hv.init()
     n = args.n
     t0 = time.time()
     if world > 1:
-        raise SystemExit("multi-GPU run requested but the distributed path is not built into this bench yet")
-    A = hv.ParCSRMatrix.laplacian(n, n, n)
+        # weak scaling: n x n x (n * world) grid, rank r owns z-slab r
+        A = hv.ParCSRMatrix.laplacian(n, n, n * world, comm=comm, P=1, Q=1, R=world, p=0, q=0, r=rank)
+    else:
+        A = hv.ParCSRMatrix.laplacian(n, n, n)
     nrows = A.n
     kw = hv.ij_amg_defaults(0)
     kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-300, max_iter=args.warmup,
@@ -68,9 +47,12 @@ def main():
     amg.setup(A)
     t_setup = time.time() - t0
     g, o, c = amg.complexities()
-    log(f"[bench] n={n}^3 rows={nrows} levels={amg.num_levels()} grid={g:.4f} op={o:.4f} setup={t_setup:.1f}s")
-    b = hv.ParVector(nrows, np.ones(nrows))
-    x = hv.ParVector(nrows, np.zeros(nrows))
+    if rank == 0:
+        log(f"[bench] ranks={world} n={n}^3/rank rows/rank={nrows} levels={amg.num_levels()} grid={g:.4f} "
+            f"op={o:.4f} setup={t_setup:.1f}s")
+    first = A.first if world > 1 else 0
+    b = hv.ParVector(nrows, np.ones(nrows), comm=comm, first=first, global_n=nrows * world)
+    x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=nrows * world)
 
     # warmup (also instantiates the cycle hipGraph)
     if args.warmup > 0:
@@ -79,22 +61,17 @@ def main():
     x.fill(0.0)
     amg.set(max_iter=args.steps)
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
+    barrier()
     t_start = time.perf_counter()
     it, rr = amg.solve(A, b, x)
     torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    barrier()
+    elapsed = max_over_ranks(time.perf_counter() - t_start)
     assert it == args.steps, (it, args.steps)
     ms_per_step = elapsed / args.steps * 1e3
     value = nrows * world * args.steps / elapsed
-    log(f"[bench] {args.steps} steps in {elapsed*1e3:.2f} ms -> {ms_per_step:.3f} ms/step, rel.res {rr:.3e}")
+    if rank == 0:
+        log(f"[bench] {args.steps} steps in {elapsed*1e3:.2f} ms -> {ms_per_step:.3f} ms/step, rel.res {rr:.3e}")
 
     # roofline: finest-level SpMV (the dominant kernel), HIP events on the solver stream
     spmv_ms, spmv_bytes = amg.bench_fine_spmv(args.spmv_reps)
@@ -103,7 +80,8 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
             "kernel": "k_sell<OP_RESID> finest level (r = b - A x)", "avg_ms": round(spmv_ms, 4),
             "bytes_per_launch": spmv_bytes}
-    log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {spmv_bytes/1e9:.3f} GB -> {achieved:.1f} GB/s")
+    if rank == 0:
+        log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {spmv_bytes/1e9:.3f} GB -> {achieved:.1f} GB/s")
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_cycles > 0:
@@ -120,29 +98,116 @@ def main():
                "sample": f"{st['iterations']} solve iterations (V-cycle + residual norm) of the same {n}^3 "
                          f"hierarchy by the C oracle (oracle/oracle.c), 1 thread, {tcpu:.1f}s"}
         log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({tcpu:.1f}s)")
+    if rank != 0:
+        return None
+    return {
+        "metric": "BoomerAMG V-cycle DOF/s + finest-level SpMV GB/s vs HBM peak, 1/2/4/8 GPU",
+        "value": round(value, 1),
+        "unit": "DOF/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (GenerateLaplacian 7-point, rhs = ones)",
+        "config": {"workload": f"3D 7-point Laplacian {n}^3 per GPU ({n}x{n}x{n * world} global, z-slab row "
+                               f"blocks), BoomerAMG V-cycle, PMIS + ext+i (Pmx 4), l1-Jacobi (relax 18) down/up, "
+                               f"Gaussian elimination coarsest",
+                   "rows_per_gpu": nrows, "levels": amg.num_levels(), "grid_complexity": round(g, 6),
+                   "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
+                   "parallelism": f"rows{world}"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
 
-    if rank == 0:
-        out = {
-            "metric": "BoomerAMG V-cycle DOF/s + finest-level SpMV GB/s vs HBM peak, 1/2/4/8 GPU",
-            "value": round(value, 1),
-            "unit": "DOF/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_per_step, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": "synthetic (GenerateLaplacian 7-point, rhs = ones)",
-            "config": {"workload": f"3D 7-point Laplacian {n}^3 per GPU, BoomerAMG V-cycle, PMIS + ext+i (Pmx 4), "
-                                   f"l1-Jacobi (relax 18) down/up, Gaussian elimination coarsest",
-                       "rows_per_gpu": nrows, "levels": amg.num_levels(), "grid_complexity": round(g, 6),
-                       "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
-                       "parallelism": f"rows{world}"},
-            "roofline": roof,
-            "cpu_baseline": cpu,
-        }
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=256, help="grid edge per GPU (n^3 rows per GPU)")
+    ap.add_argument("--cpu-cycles", type=int, default=3, help="oracle V-cycles for the CPU baseline (0 = skip)")
+    ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="rehearsal only: N virtual ranks (threads) sharing this process's GPU")
+    args = ap.parse_args()
+
+    import torch  # loads the HIP runtime the library then shares
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import hypreve as hv
+
+    if args.loopback > 1:
+        import threading
+
+        torch.cuda.set_device(0)
+        hv.init()
+        nv = args.loopback
+        comms = hv.Comm.loopback(nv)
+        bar = threading.Barrier(nv)
+        times = [0.0] * nv
+        results, errs = [None] * nv, [None] * nv
+
+        def worker(r):
+            def max_fn(t):
+                times[r] = t
+                bar.wait()
+                return max(times)
+            try:
+                results[r] = run_rank(hv, args, comms[r], r, nv, bar.wait, max_fn)
+            except BaseException as e:
+                errs[r] = e
+                bar.abort()
+
+        th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(nv)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        for e in errs:
+            if e is not None:
+                raise e
+        out = results[0]
+        out["data"] += f"; LOOPBACK REHEARSAL: {nv} virtual ranks on one GPU (not a multi-GPU measurement)"
+        print(json.dumps(out), flush=True)
+        return
+
+    dist = None
+    comm = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("gloo")
+        hv.init()
+        uid = hv.Comm.unique_id() if rank == 0 else bytes(128)
+        t = torch.tensor(list(uid), dtype=torch.uint8)
+        dist.broadcast(t, 0)
+        comm = hv.Comm.create(rank, world, bytes(t.tolist()))
+    else:
+        torch.cuda.set_device(0)
+        hv.init()
+
+    def barrier():
+        if dist:
+            dist.barrier()
+
+    def max_over_ranks(v):
+        if not dist:
+            return v
+        tt = torch.tensor([v], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    out = run_rank(hv, args, comm, rank, world, barrier, max_over_ranks)
+    if out is not None:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()

@@ -17,18 +17,12 @@
 #include "host/hve_host.hpp"
 #include "host/layout.hpp"
 #include "host/partition.hpp"
-#include <rccl/rccl.h>
 
 using namespace hve;
 
 // ---------------------------------------------------------------------------
 // object layouts
 // ---------------------------------------------------------------------------
-struct hypreve_comm_struct {
-  int rank = 0, size = 1;
-  void* nccl = nullptr;
-};
-
 struct hypre_ParVector_struct {
   HYPRE_Comm comm = nullptr;
   HYPRE_BigInt global_size = 0, first = 0;
@@ -92,7 +86,8 @@ struct hypre_Solver_struct {
 static thread_local int g_error = 0;
 static thread_local std::string g_msg;
 static int g_memloc = HYPRE_MEMORY_HOST;
-static hipStream_t g_stream = nullptr;
+// per host thread: a virtual rank of the loopback hub runs on its own thread
+static thread_local hipStream_t g_stream = nullptr;
 
 static hipStream_t lib_stream() {
   if (!g_stream) HVE_HIP(hipStreamCreateWithFlags(&g_stream, hipStreamNonBlocking));
@@ -162,12 +157,8 @@ HYPRE_Int hypreve_DeviceSynchronize(void) {
 }
 
 // ---------------------------------------------------------------------------
-// communicators (RCCL wiring lives in comm.hip; single-GPU here)
+// communicators: see comm.hip
 // ---------------------------------------------------------------------------
-HYPRE_Int hypreve_CommDestroy(HYPRE_Comm comm) {
-  delete comm;
-  return 0;
-}
 
 // ---------------------------------------------------------------------------
 // ParVector
@@ -238,8 +229,8 @@ HYPRE_Int HYPRE_ParVectorAxpy(HYPRE_Complex alpha, HYPRE_ParVector x, HYPRE_ParV
   API_END
 }
 
-static double* g_dot_part = nullptr;
-static double* g_dot_out = nullptr;
+static thread_local double* g_dot_part = nullptr;
+static thread_local double* g_dot_out = nullptr;
 HYPRE_Int HYPRE_ParVectorInnerProd(HYPRE_ParVector x, HYPRE_ParVector y, HYPRE_Real* prod) {
   CHECK_ARG(x && y && x->n == y->n, 1);
   CHECK_ARG(prod, 3);
@@ -249,6 +240,7 @@ HYPRE_Int HYPRE_ParVectorInnerProd(HYPRE_ParVector x, HYPRE_ParVector y, HYPRE_R
     HVE_HIP(hipMalloc((void**)&g_dot_out, sizeof(double)));
   }
   HVE_HIP(launch_dot(x->n, x->d, y->d, g_dot_part, g_dot_out, lib_stream()));
+  if (x->comm && x->comm->dc) x->comm->dc->allreduce_sum(g_dot_out, 1, lib_stream());
   HVE_HIP(hipMemcpyAsync(prod, g_dot_out, sizeof(double), hipMemcpyDeviceToHost, lib_stream()));
   HVE_HIP(hipStreamSynchronize(lib_stream()));
   API_END
@@ -730,9 +722,6 @@ HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
 // global matrix and ships every rank its part of each level (RCCL, device
 // staging), so an N-GPU solve reproduces the 1-GPU iterates exactly.
 // ---------------------------------------------------------------------------
-static void nck(ncclResult_t r, const char* w) {
-  if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r) + " in " + w);
-}
 template <typename T>
 static T* dev_copy(const T* h, size_t n) {
   T* d = nullptr;
@@ -742,7 +731,7 @@ static T* dev_copy(const T* h, size_t n) {
 }
 static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
   HYPRE_Comm c = A->comm;
-  ncclComm_t comm = (ncclComm_t)c->nccl;
+  DevComm& comm = *c->dc;
   const int rank = c->rank, size = c->size;
   hipStream_t st = lib_stream();
   // 1. sizes
@@ -750,7 +739,7 @@ static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
   int64_t* d_all = nullptr;
   HVE_HIP(hipMalloc((void**)&d_all, sizeof(int64_t) * 3 * size));
   int64_t* d_mine = dev_copy(mine, 3);
-  nck(ncclAllGather(d_mine, d_all, 3, ncclInt64, comm, st), "ncclAllGather(sizes)");
+  comm.allgather(d_mine, d_all, 3 * sizeof(int64_t), st);
   std::vector<int64_t> all(3 * size);
   HVE_HIP(hipMemcpyAsync(all.data(), d_all, sizeof(int64_t) * 3 * size, hipMemcpyDeviceToHost, st));
   HVE_HIP(hipStreamSynchronize(st));
@@ -767,22 +756,24 @@ static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
   double* d_a = dev_copy(A->diag.a.data(), A->diag.a.size());
   std::vector<int*> ri(size, nullptr), rj(size, nullptr);
   std::vector<double*> ra(size, nullptr);
-  nck(ncclGroupStart(), "group");
-  if (rank == 0) {
-    for (int r = 1; r < size; ++r) {
-      HVE_HIP(hipMalloc((void**)&ri[r], sizeof(int) * (all[3 * r] + 1)));
-      HVE_HIP(hipMalloc((void**)&rj[r], sizeof(int) * std::max<int64_t>(1, all[3 * r + 1])));
-      HVE_HIP(hipMalloc((void**)&ra[r], sizeof(double) * std::max<int64_t>(1, all[3 * r + 1])));
-      nck(ncclRecv(ri[r], all[3 * r] + 1, ncclInt32, r, comm, st), "recv i");
-      nck(ncclRecv(rj[r], all[3 * r + 1], ncclInt32, r, comm, st), "recv j");
-      nck(ncclRecv(ra[r], all[3 * r + 1], ncclDouble, r, comm, st), "recv a");
+  {
+    std::vector<P2PMsg> sends, recvs;
+    if (rank == 0) {
+      for (int r = 1; r < size; ++r) {
+        HVE_HIP(hipMalloc((void**)&ri[r], sizeof(int) * (all[3 * r] + 1)));
+        HVE_HIP(hipMalloc((void**)&rj[r], sizeof(int) * std::max<int64_t>(1, all[3 * r + 1])));
+        HVE_HIP(hipMalloc((void**)&ra[r], sizeof(double) * std::max<int64_t>(1, all[3 * r + 1])));
+        recvs.push_back({r, ri[r], sizeof(int) * (size_t)(all[3 * r] + 1)});
+        recvs.push_back({r, rj[r], sizeof(int) * (size_t)all[3 * r + 1]});
+        recvs.push_back({r, ra[r], sizeof(double) * (size_t)all[3 * r + 1]});
+      }
+    } else {
+      sends.push_back({0, d_i, sizeof(int) * (size_t)(A->n + 1)});
+      sends.push_back({0, d_j, sizeof(int) * (size_t)A->diag.nnz()});
+      sends.push_back({0, d_a, sizeof(double) * (size_t)A->diag.nnz()});
     }
-  } else {
-    nck(ncclSend(d_i, A->n + 1, ncclInt32, 0, comm, st), "send i");
-    nck(ncclSend(d_j, A->diag.nnz(), ncclInt32, 0, comm, st), "send j");
-    nck(ncclSend(d_a, A->diag.nnz(), ncclDouble, 0, comm, st), "send a");
+    comm.exchange(sends, recvs, st);
   }
-  nck(ncclGroupEnd(), "group end");
   HVE_HIP(hipStreamSynchronize(st));
   std::vector<std::vector<char>> bufs;
   if (rank == 0) {
@@ -820,26 +811,26 @@ static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
   std::vector<int64_t> lens(size, 0);
   if (rank == 0) for (int r = 0; r < size; ++r) lens[r] = (int64_t)bufs[r].size();
   int64_t* d_lens = dev_copy(lens.data(), size);
-  nck(ncclBroadcast(d_lens, d_lens, size, ncclInt64, 0, comm, st), "bcast lens");
+  comm.bcast(d_lens, sizeof(int64_t) * size, 0, st);
   HVE_HIP(hipMemcpyAsync(lens.data(), d_lens, sizeof(int64_t) * size, hipMemcpyDeviceToHost, st));
   HVE_HIP(hipStreamSynchronize(st));
   (void)hipFree(d_lens);
   std::vector<char> mybuf;
   if (rank == 0) {
     std::vector<char*> dsend(size, nullptr);
-    nck(ncclGroupStart(), "group");
+    std::vector<P2PMsg> sends;
     for (int r = 1; r < size; ++r) {
       dsend[r] = dev_copy(bufs[r].data(), bufs[r].size());
-      nck(ncclSend(dsend[r], lens[r], ncclUint8, r, comm, st), "send part");
+      sends.push_back({r, dsend[r], (size_t)lens[r]});
     }
-    nck(ncclGroupEnd(), "group end");
+    comm.exchange(sends, {}, st);
     HVE_HIP(hipStreamSynchronize(st));
     for (int r = 1; r < size; ++r) (void)hipFree(dsend[r]);
     mybuf.swap(bufs[0]);
   } else {
     char* drecv = nullptr;
     HVE_HIP(hipMalloc((void**)&drecv, std::max<int64_t>(1, lens[rank])));
-    nck(ncclRecv(drecv, lens[rank], ncclUint8, 0, comm, st), "recv part");
+    comm.exchange({}, {{0, drecv, (size_t)lens[rank]}}, st);
     HVE_HIP(hipStreamSynchronize(st));
     mybuf.resize(lens[rank]);
     HVE_HIP(hipMemcpy(mybuf.data(), drecv, lens[rank], hipMemcpyDeviceToHost));
@@ -862,7 +853,7 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
     single_rank_hierarchy(s->H, s->RH);
   }
   if (!s->dev) s->dev.reset(new DevAMG);
-  s->dev->build(s->RH, A->multi() ? A->comm->nccl : nullptr);
+  s->dev->build(s->RH, A->multi() ? A->comm->dc.get() : nullptr);
   s->dev->set_use_graph(s->use_graph && !A->multi());
   API_END
 }

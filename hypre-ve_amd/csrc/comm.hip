@@ -1,31 +1,23 @@
-// RCCL communicator plumbing (one process per GPU; the reference uses MPI_Comm).
+// Communicator handles of the C ABI (the reference passes an MPI_Comm; here a
+// HYPRE_Comm wraps a DevComm: RCCL over xGMI, one process per GPU, or the
+// in-process loopback hub used by the parity tests).
 #include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
 
 #include <cstring>
 #include <stdexcept>
 #include <string>
 
 #include "../../include/hypreve.h"
+#include "device/comm.hpp"
 
-struct hypreve_comm_struct {
-  int rank = 0, size = 1;
-  void* nccl = nullptr;
-};
-
-static void nccl_check(ncclResult_t r, const char* what) {
-  if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r) + " in " + what);
-}
+using namespace hve;
 
 extern "C" {
 
 HYPRE_Int hypreve_CommGetUniqueId(void* nccl_id_128) {
   if (!nccl_id_128) return HYPRE_ERROR_ARG;
-  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
   try {
-    ncclUniqueId id;
-    nccl_check(ncclGetUniqueId(&id), "ncclGetUniqueId");
-    std::memcpy(nccl_id_128, &id, sizeof(id));
+    rccl_unique_id(nccl_id_128);
   } catch (...) {
     return HYPRE_ERROR_GENERIC;
   }
@@ -33,23 +25,41 @@ HYPRE_Int hypreve_CommGetUniqueId(void* nccl_id_128) {
 }
 
 HYPRE_Int hypreve_CommCreate(HYPRE_Int rank, HYPRE_Int size, const void* nccl_id_128, HYPRE_Comm* comm) {
-  if (!comm || size < 1 || rank < 0 || rank >= size) return HYPRE_ERROR_ARG;
+  if (!comm || size < 1 || rank < 0 || rank >= size || (size > 1 && !nccl_id_128)) return HYPRE_ERROR_ARG;
   auto* c = new hypreve_comm_struct;
   c->rank = rank;
   c->size = size;
   if (size > 1) {
     try {
-      ncclUniqueId id;
-      std::memcpy(&id, nccl_id_128, sizeof(id));
-      ncclComm_t nc;
-      nccl_check(ncclCommInitRank(&nc, size, id, rank), "ncclCommInitRank");
-      c->nccl = (void*)nc;
+      c->dc = make_rccl_comm(rank, size, nccl_id_128);
     } catch (...) {
       delete c;
       return HYPRE_ERROR_GENERIC;
     }
   }
   *comm = c;
+  return 0;
+}
+
+HYPRE_Int hypreve_CommCreateLoopback(HYPRE_Int size, HYPRE_Comm* comms) {
+  if (!comms || size < 1) return HYPRE_ERROR_ARG;
+  try {
+    auto v = make_loopback_comms(size);
+    for (int r = 0; r < size; ++r) {
+      auto* c = new hypreve_comm_struct;
+      c->rank = r;
+      c->size = size;
+      if (size > 1) c->dc = std::move(v[r]);
+      comms[r] = c;
+    }
+  } catch (...) {
+    return HYPRE_ERROR_GENERIC;
+  }
+  return 0;
+}
+
+HYPRE_Int hypreve_CommDestroy(HYPRE_Comm comm) {
+  delete comm;
   return 0;
 }
 

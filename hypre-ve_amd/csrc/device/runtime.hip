@@ -9,7 +9,6 @@
 #include <stdexcept>
 #include <string>
 
-#include <rccl/rccl.h>
 
 #include "../host/layout.hpp"
 #include "runtime.hpp"
@@ -107,10 +106,6 @@ void DevHalo::release() {
   n_loc = n_halo = n_send = 0;
 }
 
-static void nccl_check(ncclResult_t r, const char* what) {
-  if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL error '") + ncclGetErrorString(r) + "' in " + what);
-}
-
 DevAMG::~DevAMG() { release(); }
 
 void DevAMG::release() {
@@ -137,7 +132,7 @@ void DevAMG::release() {
   if (stream_) (void)hipStreamDestroy(stream_);
   if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
   stream_ = comm_stream_ = nullptr;
-  nccl_ = nullptr;
+  comm_ = nullptr;
   ws_n_ = 0;
 }
 
@@ -148,9 +143,9 @@ static void init_common(hipStream_t* s, hipStream_t* cs, hipEvent_t* e1, hipEven
   HVE_HIP(hipEventCreateWithFlags(e2, hipEventDisableTiming));
 }
 
-void DevAMG::init_workspace(int n, void* nccl_comm) {
+void DevAMG::init_workspace(int n, DevComm* comm) {
   release();
-  nccl_ = nccl_comm;
+  comm_ = (comm && comm->size() > 1) ? comm : nullptr;
   init_common(&stream_, &comm_stream_, &ev_packed_, &ev_halo_);
   dot_part_ = dalloc<double>(1024);
   dscal_ = dalloc<double>(16);
@@ -160,9 +155,9 @@ void DevAMG::init_workspace(int n, void* nccl_comm) {
   ws_n_ = n;
 }
 
-void DevAMG::build(const RankHierarchy& R, void* nccl_comm) {
+void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   const int n0 = R.lev.empty() ? 0 : R.lev[0].n_loc;
-  init_workspace(n0, nccl_comm);
+  init_workspace(n0, comm);
   prm = R.prm;
   const int nl = (int)R.lev.size();
   lev_.resize(nl);
@@ -210,13 +205,13 @@ void DevAMG::build(const RankHierarchy& R, void* nccl_comm) {
     HVE_HIP(hipMemset(u0_buf_[1], 0, sizeof(double) * m));
     HVE_HIP(hipMemset(x0_buf_, 0, sizeof(double) * m));
   }
-  if (nccl_) use_graph_ = false;  // RCCL calls stay outside graph capture in this build
+  if (comm_) use_graph_ = false;  // communication stays outside graph capture in this build
   HVE_HIP(hipDeviceSynchronize());
 }
 
 void DevAMG::dot(int n, const double* x, const double* y, double* out, hipStream_t s) {
   HVE_HIP(launch_dot(n, x, y, dot_part_, out, s));
-  if (nccl_) nccl_check(ncclAllReduce(out, out, 1, ncclDouble, ncclSum, (ncclComm_t)nccl_, s), "ncclAllReduce(dot)");
+  if (comm_) comm_->allreduce_sum(out, 1, s);
 }
 double DevAMG::dot_host(int n, const double* x, const double* y, hipStream_t s) {
   dot(n, x, y, dscal_ + 15, s);
@@ -231,24 +226,19 @@ void DevAMG::halo_start(const DevHalo& h, double* x, hipStream_t s) {
   HVE_HIP(launch_gather(h.n_send, h.d_send_idx, x, h.d_sendbuf, s));
   HVE_HIP(hipEventRecord(ev_packed_, s));
   HVE_HIP(hipStreamWaitEvent(comm_stream_, ev_packed_, 0));
-  ncclComm_t comm = (ncclComm_t)nccl_;
-  nccl_check(ncclGroupStart(), "ncclGroupStart");
+  std::vector<P2PMsg> sends, recvs;
   for (size_t p = 0; p < h.peers.size(); ++p) {
-    if (h.send_cnt[p])
-      nccl_check(ncclSend(h.d_sendbuf + h.send_off[p], h.send_cnt[p], ncclDouble, h.peers[p], comm, comm_stream_),
-                 "ncclSend");
-    if (h.recv_cnt[p])
-      nccl_check(ncclRecv(x + h.n_loc + h.recv_off[p], h.recv_cnt[p], ncclDouble, h.peers[p], comm, comm_stream_),
-                 "ncclRecv");
+    if (h.send_cnt[p]) sends.push_back({h.peers[p], h.d_sendbuf + h.send_off[p], sizeof(double) * h.send_cnt[p]});
+    if (h.recv_cnt[p]) recvs.push_back({h.peers[p], x + h.n_loc + h.recv_off[p], sizeof(double) * h.recv_cnt[p]});
   }
-  nccl_check(ncclGroupEnd(), "ncclGroupEnd");
+  comm_->exchange(sends, recvs, comm_stream_);
   HVE_HIP(hipEventRecord(ev_halo_, comm_stream_));
 }
 void DevAMG::halo_finish(hipStream_t s) { HVE_HIP(hipStreamWaitEvent(s, ev_halo_, 0)); }
 
 void DevAMG::apply(const DevOp& M, const DevHalo* hx, int op, double* x, const double* b, const double* l1,
                    const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s) {
-  const bool ex = hx && hx->active() && nccl_;
+  const bool ex = hx && hx->active() && comm_;
   if (ex) halo_start(*hx, x, s);
   HVE_HIP(launch_sell(op, M.in.view(), x, b, l1, cf, relax_points, y, w, temp, s));
   if (ex) halo_finish(s);
@@ -269,15 +259,14 @@ void DevAMG::fine_apply(int op, const double* x, const double* b, double* y, dou
 void DevAMG::coarse_solve(int level, const double* f, double* u, hipStream_t s) {
   DevLevel& L = lev_[level];
   if (coarse_n_ != L.n_glob) throw std::runtime_error("coarse solve size mismatch");
-  if (!nccl_) {
+  if (!comm_) {
     HVE_HIP(launch_coarse(coarse_n_, coarse_L_, coarse_mask_, coarse_U_, f, u, s));
     return;
   }
   // hypre_GaussElimSolve gathers f on every rank and solves redundantly
   HVE_HIP(launch_set(coarse_n_, 0.0, coarse_f_, s));
   HVE_HIP(launch_copy(L.n, f, coarse_f_ + L.first, s));
-  nccl_check(ncclAllReduce(coarse_f_, coarse_f_, coarse_n_, ncclDouble, ncclSum, (ncclComm_t)nccl_, s),
-             "ncclAllReduce(coarse)");
+  comm_->allreduce_sum(coarse_f_, coarse_n_, s);
   HVE_HIP(launch_coarse(coarse_n_, coarse_L_, coarse_mask_, coarse_U_, coarse_f_, coarse_u_, s));
   HVE_HIP(launch_copy(L.n, coarse_u_ + L.first, u, s));
 }

@@ -15,6 +15,7 @@
 
 #include "../host/hve_host.hpp"
 #include "../host/partition.hpp"
+#include "comm.hpp"
 #include "kernels.h"
 
 namespace hve {
@@ -79,10 +80,10 @@ class DevAMG {
  public:
   DevAMG() = default;
   ~DevAMG();
-  // Build from a (rank-local) hierarchy; nccl_comm = ncclComm_t or nullptr.
-  void build(const RankHierarchy& R, void* nccl_comm);
+  // Build from a (rank-local) hierarchy; comm = nullptr for a single rank.
+  void build(const RankHierarchy& R, DevComm* comm);
   // Scratch/dot workspace only (PCG without an AMG preconditioner).
-  void init_workspace(int n, void* nccl_comm);
+  void init_workspace(int n, DevComm* comm);
   void release();
   bool built() const { return !lev_.empty(); }
 
@@ -101,7 +102,7 @@ class DevAMG {
   double* scratch(int i) { return scratch_[i]; }
   void set_use_graph(bool g) { use_graph_ = g; }
   double cycle_op_count() const { return cycle_ops_; }
-  bool multi_rank() const { return nccl_ != nullptr; }
+  bool multi_rank() const { return comm_ != nullptr; }
 
   AMGParams prm;
 
@@ -132,7 +133,7 @@ class DevAMG {
   hipStream_t stream_ = nullptr;
   hipStream_t comm_stream_ = nullptr;
   hipEvent_t ev_packed_ = nullptr, ev_halo_ = nullptr;
-  void* nccl_ = nullptr;
+  DevComm* comm_ = nullptr;  // not owned
   bool use_graph_ = true;
   double cycle_ops_ = 0;
   int ws_n_ = 0;

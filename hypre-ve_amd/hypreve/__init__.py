@@ -143,6 +143,7 @@ SIGNATURES = [
     ("hypreve_CommGetUniqueId", _i, [_p]),
     ("hypreve_CommCreate", _i, [_i, _i, _p, C.POINTER(_p)]),
     ("hypreve_CommDestroy", _i, [_p]),
+    ("hypreve_CommCreateLoopback", _i, [_i, C.POINTER(_p)]),
     ("hypreve_ParCSRMatrixCreateFromCSR", _i, [_p, _i, _i, _i, _pi, _pi, _pd, C.POINTER(_p)]),
     ("hypreve_ParVectorDeviceData", _p, [_p]),
     ("hypreve_ParVectorLocalSize", _i, [_p]),
@@ -190,6 +191,41 @@ def _ptr(a, ct):
     return a.ctypes.data_as(C.POINTER(ct))
 
 
+class Comm:
+    """Communicator over RCCL: one process per GPU (hypreve_CommCreate).  The
+    128-byte unique id comes from rank 0 (Comm.unique_id) and is broadcast by
+    the caller's own launcher (torch.distributed, MPI_Bcast, ...)."""
+
+    def __init__(self, h, rank, size):
+        self.h, self.rank, self.size = h, rank, size
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = C.create_string_buffer(128)
+        check(lib().hypreve_CommGetUniqueId(buf), "CommGetUniqueId")
+        return buf.raw
+
+    @classmethod
+    def create(cls, rank, size, uid: bytes):
+        assert len(uid) == 128
+        h = _p()
+        buf = C.create_string_buffer(uid, 128)
+        check(lib().hypreve_CommCreate(rank, size, buf, C.byref(h)), "CommCreate")
+        return cls(h, rank, size)
+
+    @classmethod
+    def loopback(cls, size):
+        """`size` virtual ranks on this process's GPU; drive each from its own thread."""
+        hs = (_p * size)()
+        check(lib().hypreve_CommCreateLoopback(size, hs), "CommCreateLoopback")
+        return [cls(_p(hs[r]), r, size) for r in range(size)]
+
+    def destroy(self):
+        if self.h:
+            lib().hypreve_CommDestroy(self.h)
+            self.h = None
+
+
 # ---------------------------------------------------------------------------
 # thin object layer
 # ---------------------------------------------------------------------------
@@ -199,14 +235,26 @@ class ParCSRMatrix:
         self.n = n
 
     @classmethod
-    def laplacian(cls, nx, ny, nz, cx=1.0, cy=1.0, cz=1.0):
-        """GenerateLaplacian as test/ij.c:7790 BuildParLaplacian calls it."""
+    def laplacian(cls, nx, ny, nz, cx=1.0, cy=1.0, cz=1.0, comm=None, P=1, Q=1, R=1, p=0, q=0, r=0):
+        """GenerateLaplacian as test/ij.c:7790 BuildParLaplacian calls it.  With a
+        Comm, this rank builds its block (p, q, r) of the P x Q x R processor grid."""
         v0 = (2.0 * cx if nx > 1 else 0.0) + (2.0 * cy if ny > 1 else 0.0) + (2.0 * cz if nz > 1 else 0.0)
         vals = np.array([v0, -cx, -cy, -cz], dtype=np.float64)
-        h = lib().GenerateLaplacian(None, nx, ny, nz, 1, 1, 1, 0, 0, 0, _ptr(vals, C.c_double))
+        h = lib().GenerateLaplacian(comm.h if comm else None, nx, ny, nz, P, Q, R, p, q, r, _ptr(vals, C.c_double))
         if not h:
             check(lib().HYPRE_GetError() or 1, "GenerateLaplacian")
-        return cls(h, nx * ny * nz)
+        M = cls(h, nx * ny * nz)
+        M.first, last = M.local_range()
+        M.n = last - M.first + 1
+        M.global_n = nx * ny * nz
+        return M
+
+    def local_range(self):
+        """(first_row, last_row) owned by this rank (HYPRE_ParCSRMatrixGetLocalRange)."""
+        r0, r1, c0, c1 = (C.c_int() for _ in range(4))
+        check(lib().HYPRE_ParCSRMatrixGetLocalRange(self.h, C.byref(r0), C.byref(r1), C.byref(c0), C.byref(c1)),
+              "GetLocalRange")
+        return r0.value, r1.value
 
     @classmethod
     def laplacian27(cls, nx, ny, nz):
@@ -238,11 +286,14 @@ class ParCSRMatrix:
 
 
 class ParVector:
-    def __init__(self, n, data=None):
+    def __init__(self, n, data=None, comm=None, first=0, global_n=None):
+        """n owned entries starting at global index first (HYPRE_ParVectorCreate)."""
         self.n = n
         h = _p()
-        part = np.array([0, n], dtype=np.int32)
-        check(lib().HYPRE_ParVectorCreate(None, n, _ptr(part, C.c_int), C.byref(h)), "ParVectorCreate")
+        part = np.array([first, first + n], dtype=np.int32)
+        gn = n if global_n is None else global_n
+        check(lib().HYPRE_ParVectorCreate(comm.h if comm else None, gn, _ptr(part, C.c_int), C.byref(h)),
+              "ParVectorCreate")
         self.h = h
         check(lib().HYPRE_ParVectorInitialize(h), "ParVectorInitialize")
         if data is not None:

@@ -187,6 +187,11 @@ HYPRE_Int hypreve_CommGetUniqueId(void *nccl_id_128);
 HYPRE_Int hypreve_CommCreate(HYPRE_Int rank, HYPRE_Int size, const void *nccl_id_128,
                              HYPRE_Comm *comm);
 HYPRE_Int hypreve_CommDestroy(HYPRE_Comm comm);
+/* `size` communicators of virtual ranks sharing one GPU inside this process
+ * (comms[0..size-1]); each rank must be driven from its own host thread.  Used
+ * to check the partitioned solve on a single GPU (RCCL refuses two ranks on
+ * one device); not a production transport. */
+HYPRE_Int hypreve_CommCreateLoopback(HYPRE_Int size, HYPRE_Comm *comms);
 
 /* Direct construction of a local ParCSR block from host CSR arrays (global
  * column indices), equivalent to IJ create/set/assemble in one call. */

@@ -22,6 +22,9 @@ if [[ $WHAT == all || $WHAT == tests ]]; then
   step pytest_gpu 900 python -m pytest tests -m gpu -x -q
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
+if [[ $WHAT == all || $WHAT == multi ]]; then
+  step loopback2 600 python bench.py --loopback 2 --n 128 --steps 5 --warmup 1 --cpu-cycles 0
+fi
 if [[ $WHAT == all || $WHAT == bench ]]; then
   step bench 900 python bench.py --steps 10 --warmup 2
 fi

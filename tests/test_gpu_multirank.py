@@ -1,0 +1,76 @@
+"""Partitioned (multi-rank) solve path on one GPU through the loopback hub.
+
+RCCL refuses two ranks on one device, so the N-rank data path -- row-block
+ownership per level, [local | halo] operators split into interior / boundary
+rows, halo exchange on the side stream, rank-0 setup shipped to every rank,
+redundant coarse solve after a sum over ranks -- runs here as N virtual ranks,
+one host thread each, on the box's single GPU.  The iterates must equal the
+1-rank iterates bit for bit (every row sum keeps the global entry order);
+only the residual norms may differ in the last bits (the inner product is
+summed over ranks in another order), so the iteration counts must agree.
+The production transport (RCCL, one process per GPU) shares all of this code
+except DevComm::exchange / allreduce_sum.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _solve_1rank(hv, nx, ny, nz, kw):
+    A = hv.ParCSRMatrix.laplacian(nx, ny, nz)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup(A)
+    b = hv.ParVector(A.n, np.ones(A.n))
+    x = hv.ParVector(A.n, np.zeros(A.n))
+    it, rr = amg.solve(A, b, x)
+    return x.get(), it, rr, amg.num_levels()
+
+
+def _solve_nranks(hv, nx, ny, nz, kw, nranks, timeout=300):
+    comms = hv.Comm.loopback(nranks)
+    out, errs = [None] * nranks, [None] * nranks
+
+    def worker(r):
+        try:
+            c = comms[r]
+            A = hv.ParCSRMatrix.laplacian(nx, ny, nz, comm=c, P=1, Q=1, R=nranks, p=0, q=0, r=r)
+            amg = hv.BoomerAMG(**kw)
+            amg.setup(A)
+            b = hv.ParVector(A.n, np.ones(A.n), comm=c, first=A.first, global_n=A.global_n)
+            x = hv.ParVector(A.n, np.zeros(A.n), comm=c, first=A.first, global_n=A.global_n)
+            it, rr = amg.solve(A, b, x)
+            out[r] = (A.first, x.get(), it, rr, amg.num_levels())
+        except Exception as e:  # reported by the main thread
+            errs[r] = e
+
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout)
+    assert not any(t.is_alive() for t in th), "a virtual rank did not finish (exchange mismatch?)"
+    for e in errs:
+        if e is not None:
+            raise e
+    out.sort(key=lambda o: o[0])
+    x = np.concatenate([o[1] for o in out])
+    return x, [o[2] for o in out], [o[3] for o in out], out[0][4]
+
+
+@pytest.mark.parametrize("nranks,nx,nz", [(2, 16, 16), (3, 14, 20), (4, 12, 13)])
+@pytest.mark.parametrize("relax", [18, 0])
+def test_loopback_partitioned_solve_bitwise(hv, nranks, nx, nz, relax):
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=relax, tol=1e-8, max_iter=60)
+    if relax == 0:
+        kw.update(relax_wt=0.6)
+    x1, it1, rr1, nl1 = _solve_1rank(hv, nx, nx, nz, kw)
+    xN, itN, rrN, nlN = _solve_nranks(hv, nx, nx, nz, kw, nranks)
+    assert nlN == nl1
+    assert all(i == it1 for i in itN), (it1, itN)
+    assert all(abs(r - rr1) <= 1e-10 * rr1 for r in rrN), (rr1, rrN)
+    assert x1.shape == xN.shape
+    assert np.array_equal(x1, xN), f"max |diff| {np.max(np.abs(x1 - xN))}"
