@@ -13,6 +13,8 @@
 #include "../host/layout.hpp"
 #include "runtime.hpp"
 
+#include <cstdlib>
+
 namespace hve {
 
 void check_hip(hipError_t e, const char* what) {
@@ -42,8 +44,16 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h) {
   // Sort rows inside windows (SELL-C-sigma) only where the plain layout pads
   // noticeably: the Galerkin levels' rows range over 7..150 entries, the
   // finest 7-point operator is nearly uniform and keeps contiguous rows.
-  const int64_t pad0 = sell_padded_nnz(A, 0);
-  const int sigma = (A.nnz() > 0 && pad0 > A.nnz() + A.nnz() / 20) ? kSellSigma : 0;
+  // Measured on MI355X (256^3 Poisson, PMIS/ext+i): sorting a 1024-row window
+  // cut level-1 padding from 1.40x to 1.03x but slowed its SpMV 745 -> 1073 us,
+  // because a wave's 64 rows then gather x from a 16x wider range.  Off by
+  // default; HVE_SELL_SIGMA=<rows> re-enables it for experiments.
+  static const int sigma_env = [] {
+    const char* e = getenv("HVE_SELL_SIGMA");
+    return e ? atoi(e) : 0;
+  }();
+  const int64_t pad0 = sigma_env > 0 ? sell_padded_nnz(A, 0) : 0;
+  const int sigma = (sigma_env > 0 && A.nnz() > 0 && pad0 > A.nnz() + A.nnz() / 20) ? sigma_env : 0;
   build_sell_host(A, sigma, perm, sp, col, val);
   nrows = A.nrows;
   ncols = A.ncols;

@@ -25,8 +25,6 @@ enum { HYPRE_ERROR_GENERIC_CODE = 1, HYPRE_ERROR_CONV_CODE = 256 };
 void check_hip(hipError_t e, const char* what);
 #define HVE_HIP(x) ::hve::check_hip((x), #x)
 
-constexpr int kSellSigma = 1024;  // SELL-C-sigma sort window (rows)
-
 struct DevSell {
   int nrows = 0, ncols = 0, nslices = 0;
   int64_t nnz = 0, nnz_pad = 0;

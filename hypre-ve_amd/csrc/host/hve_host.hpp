@@ -60,6 +60,7 @@ struct AMGParams {
   double max_row_sum = 0.9;
   int coarsen_type = 10;          // 8 PMIS, 9 PMIS(seq rand), 10 HMIS
   int measure_type = 0;
+  int coarsen_cut_factor = 0;
   int interp_type = 6;            // 6 ext+i, 3 direct
   int P_max_elmts = 4;
   double trunc_factor = 0.0;
@@ -112,7 +113,9 @@ void generate_laplacian_7pt_block(int nx, int ny, int nz, int P, int Q, int R, i
 // ---- setup building blocks ----
 void create_strength(const CSR& A, double thr, double max_row_sum, Pattern& S);
 void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf);
-void coarsen_hmis(const Pattern& S, int measure_type, std::vector<int>& cf);
+void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, int cut_factor,
+                             std::vector<int>& cf);
+void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf);
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P);
 void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,

@@ -322,8 +322,26 @@ void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
         }
       }
     }
+    const bool first_seeded = cf_init && iter == 0;
     ++iter;
-    // set C and F points
+    if (first_seeded) {
+      // The seeded C points (Ruge pass) can be demoted below (measure < 1)
+      // while their neighbours test them; follow the reference's row order:
+      // graph is ascending, so a neighbour j < i in the graph already holds
+      // its new marker.
+      for (int ig = 0; ig < gs; ++ig) {
+        const int i = graph[ig];
+        if (measure[i] < 1) cf[i] = F_PT;
+        if (cf[i] > 0) {
+          cf[i] = C_PT;
+        } else {
+          for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
+            if (cf[S.j[k]] > 0) { cf[i] = F_PT; break; }
+          }
+        }
+      }
+    } else {
+    // set C and F points (no marker > 0 is demoted here: order-free)
 #pragma omp parallel for schedule(static)
     for (int ig = 0; ig < gs; ++ig) {
       int i = graph[ig];
@@ -337,6 +355,7 @@ void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
         }
       }
     }
+    }
     graph2.clear();
     for (int ig = 0; ig < gs; ++ig) {
       int i = graph[ig];
@@ -347,8 +366,230 @@ void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
   }
 }
 
-void coarsen_hmis(const Pattern& /*S*/, int /*measure_type*/, std::vector<int>& /*cf*/) {
-  throw std::runtime_error("coarsen_type 10 (HMIS) is not available yet: use 8 (PMIS) or 9");
+// ---------------------------------------------------------------------------
+// Ruge-Stueben first pass, parcsr_ls/par_coarsen.c:874 hypre_BoomerAMGCoarsenRuge
+// for one process (no offd part).  The point selection order is defined by the
+// list-of-lists of utilities/amg_linklist.c: buckets of equal measure kept in
+// decreasing measure order, each a FIFO threaded through lists[] / where[];
+// the next C point is the head of the largest bucket.  The structure is
+// restated as is (including how a point with measure 0, already marked, can
+// re-enter the lists) because the coarse grid depends on it.
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kListHead = -1, kListTail = -2;  // amg_linklist.c:16
+
+struct MeasureLists {
+  struct Elt { int data, head, tail, prev, next; };
+  std::vector<Elt> pool;
+  std::vector<int> free_;
+  int head = -1, tail = -1;  // LoL_head / LoL_tail
+  std::vector<int> lists, where;
+  explicit MeasureLists(int n) : lists(n, 0), where(n, 0) {}
+
+  int create(int item) {
+    int e;
+    if (!free_.empty()) { e = free_.back(); free_.pop_back(); }
+    else { e = (int)pool.size(); pool.push_back({}); }
+    pool[e] = {item, kListTail, kListHead, -1, -1};
+    return e;
+  }
+  // amg_linklist.c:41 hypre_remove_point
+  void remove(int measure, int index) {
+    for (int lp = head; lp != -1; lp = pool[lp].next) {
+      Elt& L = pool[lp];
+      if (L.data != measure) continue;
+      if (L.head == index && L.tail == index) {
+        if (lp == head && lp == tail) { head = tail = -1; }
+        else if (lp == head) { pool[L.next].prev = -1; head = L.next; }
+        else if (lp == tail) { pool[L.prev].next = -1; tail = L.prev; }
+        else { pool[L.next].prev = L.prev; pool[L.prev].next = L.next; }
+        free_.push_back(lp);
+      } else if (L.head == index) {
+        L.head = lists[index];
+        where[lists[index]] = kListHead;
+      } else if (L.tail == index) {
+        L.tail = where[index];
+        lists[where[index]] = kListTail;
+      } else {
+        lists[where[index]] = lists[index];
+        where[lists[index]] = where[index];
+      }
+      return;
+    }
+    throw std::runtime_error("Ruge coarsening: no such list");
+  }
+  // amg_linklist.c:168 hypre_enter_on_lists
+  void enter(int measure, int index) {
+    if (head == -1) {
+      int e = create(measure);
+      pool[e].head = pool[e].tail = index;
+      lists[index] = kListTail;
+      where[index] = kListHead;
+      head = tail = e;
+      return;
+    }
+    for (int lp = head; lp != -1; lp = pool[lp].next) {
+      if (measure > pool[lp].data) {
+        int e = create(measure);
+        pool[e].head = pool[e].tail = index;
+        lists[index] = kListTail;
+        where[index] = kListHead;
+        if (pool[lp].prev != -1) {
+          pool[e].prev = pool[lp].prev;
+          pool[pool[lp].prev].next = e;
+          pool[lp].prev = e;
+          pool[e].next = lp;
+        } else {
+          pool[e].next = lp;
+          pool[lp].prev = e;
+          pool[e].prev = -1;
+          head = e;
+        }
+        return;
+      } else if (measure == pool[lp].data) {
+        const int old_tail = pool[lp].tail;
+        lists[old_tail] = index;
+        where[index] = old_tail;
+        lists[index] = kListTail;
+        pool[lp].tail = index;
+        return;
+      }
+    }
+    int e = create(measure);
+    pool[e].head = pool[e].tail = index;
+    lists[index] = kListTail;
+    where[index] = kListHead;
+    pool[tail].next = e;
+    pool[e].prev = tail;
+    pool[e].next = -1;
+    tail = e;
+  }
+};
+}  // namespace
+
+// coarsen_type 10 -> first pass only with Z_PT for measure-0 points
+// (par_coarsen.c:1082-1086, 1347-1354).
+void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, int cut_factor,
+                             std::vector<int>& cf) {
+  constexpr int UNDECIDED = 0, SC_PT = 3;
+  const int n = S.n;
+  const bool agg_2 = (measure_type == 3 || measure_type == 4);
+  const int f_pnt = Z_PT;
+  // ST = transpose of S (par_coarsen.c:1032-1057), counting sort
+  std::vector<int> ST_i(n + 1, 0), ST_j(S.j.size());
+  for (size_t k = 0; k < S.j.size(); ++k) ST_i[S.j[k] + 1]++;
+  for (int i = 0; i < n; ++i) ST_i[i + 1] += ST_i[i];
+  {
+    std::vector<int> pos(ST_i.begin(), ST_i.end() - 1);
+    for (int i = 0; i < n; ++i)
+      for (int k = S.i[i]; k < S.i[i + 1]; ++k) ST_j[pos[S.j[k]]++] = i;
+  }
+  std::vector<int> measure(n);
+  for (int i = 0; i < n; ++i) measure[i] = ST_i[i + 1] - ST_i[i];
+
+  cf.assign(n, 0);  // CF_marker allocated by the coarsening (all UNDECIDED)
+  int num_left = 0;
+  for (int j = 0; j < n; ++j) {
+    if (cf[j] == 0) {
+      if (S.i[j + 1] - S.i[j] == 0) {
+        cf[j] = agg_2 ? SC_PT : SF_PT;
+        measure[j] = 0;
+      } else {
+        cf[j] = UNDECIDED;
+        num_left++;
+      }
+    } else {
+      measure[j] = 0;
+    }
+  }
+  if (cut_factor > 0 && A && n > 0) {
+    const int64_t avg = (int64_t)A->nnz() / n;
+    const int64_t cut = cut_factor * avg;
+    for (int j = 0; j < n; ++j) {
+      if (A->i[j + 1] - A->i[j] > cut) {
+        if (cf[j] == UNDECIDED) num_left--;
+        cf[j] = SF_PT;
+      }
+    }
+  }
+  MeasureLists L(n);
+  for (int j = 0; j < n; ++j) {
+    const int m = measure[j];
+    if (cf[j] != SF_PT && cf[j] != SC_PT) {
+      if (m > 0) {
+        L.enter(m, j);
+      } else {
+        if (m < 0) throw std::runtime_error("negative measure");
+        cf[j] = f_pnt;
+        for (int k = S.i[j]; k < S.i[j + 1]; ++k) {
+          const int nb = S.j[k];
+          if (cf[nb] != SF_PT && cf[nb] != SC_PT) {
+            if (nb < j) {
+              if (measure[nb] > 0) L.remove(measure[nb], nb);
+              L.enter(++measure[nb], nb);
+            } else {
+              ++measure[nb];
+            }
+          }
+        }
+        --num_left;
+      }
+    }
+  }
+  while (num_left > 0) {
+    if (L.head == -1) throw std::runtime_error("Ruge coarsening: lists exhausted with points left");
+    const int index = L.pool[L.head].head;
+    cf[index] = C_PT;
+    const int m = measure[index];
+    measure[index] = 0;
+    --num_left;
+    L.remove(m, index);
+    for (int k = ST_i[index]; k < ST_i[index + 1]; ++k) {
+      const int nb = ST_j[k];
+      if (cf[nb] == UNDECIDED) {
+        cf[nb] = F_PT;
+        L.remove(measure[nb], nb);
+        --num_left;
+        for (int k2 = S.i[nb]; k2 < S.i[nb + 1]; ++k2) {
+          const int nb2 = S.j[k2];
+          if (cf[nb2] == UNDECIDED) {
+            L.remove(measure[nb2], nb2);
+            L.enter(++measure[nb2], nb2);
+          }
+        }
+      }
+    }
+    for (int k = S.i[index]; k < S.i[index + 1]; ++k) {
+      const int nb = S.j[k];
+      if (cf[nb] == UNDECIDED) {
+        int mm = measure[nb];
+        L.remove(mm, nb);
+        measure[nb] = --mm;
+        if (mm > 0) {
+          L.enter(mm, nb);
+        } else {
+          cf[nb] = F_PT;
+          --num_left;
+          for (int k2 = S.i[nb]; k2 < S.i[nb + 1]; ++k2) {
+            const int nb2 = S.j[k2];
+            if (cf[nb2] == UNDECIDED) {
+              L.remove(measure[nb2], nb2);
+              L.enter(++measure[nb2], nb2);
+            }
+          }
+        }
+      }
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    if (cf[i] == SC_PT) cf[i] = C_PT;
+}
+
+// par_coarsen.c:2774 hypre_BoomerAMGCoarsenHMIS: Ruge first pass, then PMIS
+// seeded with its C points (CF_init = 1).
+void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf) {
+  coarsen_ruge_first_pass(S, A, measure_type, cut_factor, cf);
+  coarsen_pmis(S, 1, cf);
 }
 
 // ---------------------------------------------------------------------------
@@ -770,7 +1011,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     std::vector<int> cf;
     if (coarsen_type == 8) coarsen_pmis(S, 0, cf);
     else if (coarsen_type == 9) coarsen_pmis(S, 2, cf);
-    else if (coarsen_type == 10) coarsen_hmis(S, prm.measure_type, cf);
+    else if (coarsen_type == 10) coarsen_hmis(S, &L.A, prm.measure_type, prm.coarsen_cut_factor, cf);
     else throw std::runtime_error("unsupported coarsen_type " + std::to_string(coarsen_type));
     double t2 = now();
     t_c += t2 - t1;

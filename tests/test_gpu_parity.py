@@ -42,10 +42,12 @@ def test_fixture_default_on_gpu(gpu, orc, relax):
         assert it == 48
 
 
-@pytest.mark.parametrize("n3,relax", [((24, 20, 16), 18), ((17, 13, 11), 0), ((33, 33, 33), 18)])
-def test_single_cycle_bitwise(gpu, orc, n3, relax):
+@pytest.mark.parametrize("n3,relax,coarsen", [((24, 20, 16), 18, 8), ((17, 13, 11), 0, 8), ((33, 33, 33), 18, 8),
+                                              ((24, 20, 16), 18, 10), ((31, 29, 27), 0, 10)])
+def test_single_cycle_bitwise(gpu, orc, n3, relax, coarsen):
+    """One V-cycle from a random iterate; coarsen 10 = HMIS (test/ij.c default)."""
     hv = gpu
-    A, amg, O = setup_pair(hv, orc, n3, coarsen_type=8, relax_type=relax)
+    A, amg, O = setup_pair(hv, orc, n3, coarsen_type=coarsen, relax_type=relax)
     n = A.n
     rng = np.random.default_rng(7)
     f_h = rng.standard_normal(n)

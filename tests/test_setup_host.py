@@ -5,6 +5,7 @@ import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -13,7 +14,7 @@ import sys, hashlib, numpy as np
 sys.path.insert(0, %r)
 import hypreve as hv
 A = hv.ParCSRMatrix.laplacian(24, 22, 20)
-amg = hv.BoomerAMG(**hv.ij_amg_defaults(0)); amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4)
+amg = hv.BoomerAMG(**hv.ij_amg_defaults(0)); amg.set(coarsen_type=int(sys.argv[1]), relax_type=18, P_max_elmts=4)
 amg.setup_host(A)
 h = hashlib.sha256()
 for l in range(amg.num_levels()):
@@ -25,21 +26,24 @@ print(h.hexdigest())
 """ % os.path.join(ROOT, "hypre-ve_amd")
 
 
-def _digest(threads):
+def _digest(threads, coarsen_type):
     env = dict(os.environ, OMP_NUM_THREADS=str(threads))
-    out = subprocess.run([sys.executable, "-c", _SCRIPT], env=env, capture_output=True, text=True, check=True)
+    out = subprocess.run([sys.executable, "-c", _SCRIPT, str(coarsen_type)], env=env, capture_output=True,
+                         text=True, check=True)
     return out.stdout.strip()
 
 
-def test_setup_bitwise_independent_of_threads():
-    d1 = _digest(1)
-    assert d1 == _digest(3) == _digest(8)
+@pytest.mark.parametrize("coarsen_type", [8, 10])
+def test_setup_bitwise_independent_of_threads(coarsen_type):
+    d1 = _digest(1, coarsen_type)
+    assert d1 == _digest(3, coarsen_type) == _digest(8, coarsen_type)
 
 
-def test_hierarchy_invariants(hv):
+@pytest.mark.parametrize("coarsen_type", [8, 10])
+def test_hierarchy_invariants(hv, coarsen_type):
     A = hv.ParCSRMatrix.laplacian(16, 16, 16)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
-    amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4)
+    amg.set(coarsen_type=coarsen_type, relax_type=18, P_max_elmts=4)
     amg.setup_host(A)
     nl = amg.num_levels()
     assert nl >= 3
@@ -56,6 +60,14 @@ def test_hierarchy_invariants(hv):
         # C points interpolate by injection
         c = np.where(cf == 1)[0]
         assert np.allclose(P[c].toarray().max(axis=1), 1.0)
+        assert set(np.unique(cf)) <= {1, -1, -3}
+        # every F point with strong connections has a strong C neighbour
+        # (PMIS / HMIS second phase); on these M-matrices every off-diagonal
+        # entry is strong at threshold 0.25 unless the row sum test drops it
+        Aoff = Al.copy(); Aoff.setdiag(0); Aoff.eliminate_zeros()
+        fpts = np.where(cf == -1)[0]
+        hasC = (abs(Aoff[fpts]) @ (cf == 1).astype(float)) > 0
+        assert hasC.all()
         ip, jj, vv, cshp = amg.level_matrix(l + 1, 0)
         Ac = sp.csr_matrix((vv, jj, ip), shape=cshp)
         # Galerkin: A_c == P^T A P (values; order of summation may differ slightly)
