@@ -1007,6 +1007,82 @@ HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver s, HYPRE_Int reps, HYPRE_Real* avg_
   API_END
 }
 
+// Average time of one application of a level operator (which: 0 = A_l as the
+// residual r = f - A u, 1 = P_l as prolongation u_l += P u_{l+1}, 2 = R_l as
+// restriction f_{l+1} = R r_l) with its algorithmic bytes: every stored
+// nonzero once (8 B value + 4 B column), each input vector entry once, each
+// output entry read and/or written once.  Interior rows only on multi-rank.
+HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,
+                               HYPRE_Real* avg_ms, HYPRE_Real* bytes, HYPRE_Real* padded_nnz) {
+  CHECK_ARG(s && s->dev && s->dev->built(), 1);
+  CHECK_ARG(level >= 0 && level < s->dev->num_levels(), 2);
+  CHECK_ARG(which >= 0 && which <= 2 && (which == 0 || level < s->dev->num_levels() - 1), 3);
+  CHECK_ARG(reps > 0, 4);
+  API_BEGIN
+  DevAMG& D = *s->dev;
+  const DevLevel& L = D.level(level);
+  const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
+  const int op = which == 0 ? K_RESID : which == 1 ? K_PROLONG : K_RESTRICT;
+  hipStream_t st = D.stream();
+  double* x = D.scratch(0);
+  double* b = D.scratch(1);
+  double* y = D.scratch(2);
+  HVE_HIP(launch_set(D.ws_n(), 1.0, x, st));
+  HVE_HIP(launch_set(D.ws_n(), 0.5, b, st));
+  HVE_HIP(launch_set(D.ws_n(), 0.0, y, st));
+  for (int w = 0; w < 3; ++w) HVE_HIP(launch_sell(op, M.view(), x, b, nullptr, nullptr, 0, y, -1.0, 0.0, st));
+  hipEvent_t e0, e1;
+  HVE_HIP(hipEventCreate(&e0));
+  HVE_HIP(hipEventCreate(&e1));
+  HVE_HIP(hipEventRecord(e0, st));
+  for (int r = 0; r < reps; ++r) HVE_HIP(launch_sell(op, M.view(), x, b, nullptr, nullptr, 0, y, -1.0, 0.0, st));
+  HVE_HIP(hipEventRecord(e1, st));
+  HVE_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HVE_HIP(hipEventElapsedTime(&ms, e0, e1));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (avg_ms) *avg_ms = ms / reps;
+  const double out_rw = which == 0 ? 16.0 : which == 1 ? 16.0 : 8.0;  // b read + y write / y rw / y write
+  if (bytes)
+    *bytes = (double)M.nnz * 12.0 + (double)M.nrows * out_rw + (double)M.ncols * 8.0 + (double)(M.nslices + 1) * 4.0 +
+             (M.rowmap ? (double)M.nrows * 4.0 : 0.0);
+  if (padded_nnz) *padded_nnz = (double)M.nnz_pad;
+  API_END
+}
+
+// Read-only streaming kernel over n elements of elem_bytes (4 or 8) each: the
+// calibration pass for rocprofv3 FETCH_SIZE at this access width and the
+// achievable-bandwidth reference for the roofline.
+HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real* avg_ms) {
+  CHECK_ARG(elem_bytes == 4 || elem_bytes == 8, 1);
+  CHECK_ARG(n > 0, 2);
+  CHECK_ARG(reps > 0, 3);
+  API_BEGIN
+  void* buf = nullptr;
+  double* out = nullptr;
+  hipStream_t st = lib_stream();
+  HVE_HIP(hipMalloc(&buf, (size_t)n * elem_bytes));
+  HVE_HIP(hipMalloc((void**)&out, sizeof(double)));
+  HVE_HIP(hipMemsetAsync(buf, 0, (size_t)n * elem_bytes, st));
+  for (int w = 0; w < 2; ++w) HVE_HIP(launch_stream_read(n, elem_bytes, buf, out, st));
+  hipEvent_t e0, e1;
+  HVE_HIP(hipEventCreate(&e0));
+  HVE_HIP(hipEventCreate(&e1));
+  HVE_HIP(hipEventRecord(e0, st));
+  for (int r = 0; r < reps; ++r) HVE_HIP(launch_stream_read(n, elem_bytes, buf, out, st));
+  HVE_HIP(hipEventRecord(e1, st));
+  HVE_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HVE_HIP(hipEventElapsedTime(&ms, e0, e1));
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  (void)hipFree(buf);
+  (void)hipFree(out);
+  if (avg_ms) *avg_ms = ms / reps;
+  API_END
+}
+
 // ---------------------------------------------------------------------------
 // PCG
 // ---------------------------------------------------------------------------

@@ -24,6 +24,8 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 // op: 0 l1-Jacobi w=1, 1 l1-Jacobi weighted, 2 Jacobi (s = diagonal)
 hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u,
                              hipStream_t st);
+int sell_batch();
+hipError_t launch_stream_read(int64_t n, int elem_bytes, const void* buf, double* out, hipStream_t st);
 hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st);
 hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,
                        hipStream_t st);

@@ -21,6 +21,8 @@
 
 #include "kernels.h"
 
+#include <cstdlib>
+
 namespace hve {
 
 static constexpr int kWave = 64;
@@ -94,9 +96,8 @@ __device__ __forceinline__ double sell_row(const int* __restrict__ cp, const dou
   return t;
 }
 
-template <int OP, bool CFSEL>
+template <int OP, bool CFSEL, int B>
 __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
-  constexpr int B = 8;
   const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
   const int row = lb * 256 + threadIdx.x;
   if (row >= p.nrows) return;
@@ -297,10 +298,15 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.w = w; a.temp = temp; a.relax_points = relax_points;
   dim3 grid(a.nblocks_pad), block(256);
   const bool cfsel = (relax_points != 0 && cf != nullptr);
-#define HVE_L(OPV)                                                                       \
-  case OPV:                                                                              \
-    if (cfsel) hipLaunchKernelGGL((k_sell<OPV, true>), grid, block, 0, s, a);           \
-    else hipLaunchKernelGGL((k_sell<OPV, false>), grid, block, 0, s, a);                \
+  const int bsel = sell_batch();
+#define HVE_LB(OPV, CF)                                                        \
+  if (bsel == 4) hipLaunchKernelGGL((k_sell<OPV, CF, 4>), grid, block, 0, s, a);  \
+  else if (bsel == 16) hipLaunchKernelGGL((k_sell<OPV, CF, 16>), grid, block, 0, s, a); \
+  else hipLaunchKernelGGL((k_sell<OPV, CF, 8>), grid, block, 0, s, a);
+#define HVE_L(OPV)              \
+  case OPV:                     \
+    if (cfsel) { HVE_LB(OPV, true) } \
+    else { HVE_LB(OPV, false) }      \
     break;
   switch (op) {
     HVE_L(OP_RESID) HVE_L(OP_MATVEC) HVE_L(OP_L1JAC) HVE_L(OP_L1JAC_W) HVE_L(OP_JAC)
@@ -308,6 +314,31 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     default: return hipErrorInvalidValue;
   }
 #undef HVE_L
+#undef HVE_LB
+  return hipGetLastError();
+}
+
+// Entries per load batch in the SELL row loop: 8 by default (see sell_row);
+// HVE_SELL_BATCH=4|16 selects the other instantiations for experiments.
+int sell_batch() {
+  static const int b = [] {
+    const char* e = getenv("HVE_SELL_BATCH");
+    const int v = e ? atoi(e) : 8;
+    return (v == 4 || v == 16) ? v : 8;
+  }();
+  return b;
+}
+
+__global__ void __launch_bounds__(256) k_stream_read(int64_t n, int elem_bytes, const void* __restrict__ buf,
+                                                     double* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  double v = 0.0;
+  if (i < n) v = elem_bytes == 4 ? (double)((const int*)buf)[i] : ((const double*)buf)[i];
+  if (v == 12345.678) out[0] = v;  // keeps the load; never true for the zero-filled buffer
+}
+hipError_t launch_stream_read(int64_t n, int elem_bytes, const void* buf, double* out, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_stream_read, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, elem_bytes, buf, out);
   return hipGetLastError();
 }
 

@@ -163,6 +163,8 @@ SIGNATURES = [
     ("hypreve_BoomerAMGCycle", _i, [_p, _p, _p]),
     ("hypreve_BoomerAMGGetKernelStats", _i, [_p, _pd, _i]),
     ("hypreve_BenchFineSpMV", _i, [_p, _i, _pd, _pd]),
+    ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
+    ("hypreve_BenchStream", _i, [_i, C.c_int64, _i, _pd]),
     ("hypreve_DeviceSynchronize", _i, []),
     ("hypreve_BuildInfo", C.c_char_p, []),
     ("hypreve_LastErrorMessage", C.c_char_p, []),
@@ -449,6 +451,13 @@ class BoomerAMG:
         return dict(relax_type=rt.tolist(), num_sweeps=ns.tolist(), relax_weight=float(w[0]), omega=float(w[1]),
                     relax_order=int(misc[0]), cycle_type=int(misc[1]), num_blocks=int(misc[2]))
 
+    def bench_level_op(self, level, which=0, reps=20):
+        """(avg_ms, algorithmic bytes, padded entries) of A_l (0), P_l (1) or R_l (2)."""
+        ms, by, pz = C.c_double(), C.c_double(), C.c_double()
+        check(lib().hypreve_BenchLevelOp(self.h, level, which, reps, C.byref(ms), C.byref(by), C.byref(pz)),
+              "BenchLevelOp")
+        return ms.value, by.value, pz.value
+
     def bench_fine_spmv(self, reps=20):
         ms, by = C.c_double(), C.c_double()
         check(lib().hypreve_BenchFineSpMV(self.h, reps, C.byref(ms), C.byref(by)), "BenchFineSpMV")
@@ -499,6 +508,13 @@ class PCG:
 
 def init():
     check(lib().HYPRE_Init(), "HYPRE_Init")
+
+
+def bench_stream(elem_bytes, n, reps=20):
+    """Average ms of a read-only stream over n elements of elem_bytes (4 or 8)."""
+    ms = C.c_double()
+    check(lib().hypreve_BenchStream(elem_bytes, n, reps, C.byref(ms)), "BenchStream")
+    return ms.value
 
 
 def ij_amg_defaults(solver_id=0):

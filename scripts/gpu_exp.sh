@@ -1,0 +1,37 @@
+#!/bin/bash
+# Kernel-variant sweep and PMC counter passes (one gpurun call).  Each GPU step
+# has its own time limit; after a fault / abort / timeout nothing further runs.
+set -u
+mkdir -p gpurun_out/exp
+OUT=gpurun_out/exp
+export TMPDIR=/tmp
+step() {  # step <name> <seconds> <cmd...>
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -3 "$OUT/$name.log"
+  case $rc in
+    0|1|2|5) return 0 ;;
+    *) echo "=== stopping after $name (rc=$rc)"; exit $rc ;;
+  esac
+}
+WHAT=${1:-all}
+if [[ $WHAT == all || $WHAT == tests ]]; then
+  step pytest_gpu 600 python -m pytest tests -m gpu -x -q
+fi
+if [[ $WHAT == all || $WHAT == sweep ]]; then
+  step sweep_b8 300 python scripts/level_sweep.py --json $OUT/sweep_b8.json
+  export HVE_SELL_BATCH=4;  step sweep_b4 300 python scripts/level_sweep.py --json $OUT/sweep_b4.json
+  export HVE_SELL_BATCH=16; step sweep_b16 300 python scripts/level_sweep.py --json $OUT/sweep_b16.json
+  unset HVE_SELL_BATCH
+  export HVE_SELL_SIGMA=128; step sweep_s128 300 python scripts/level_sweep.py --json $OUT/sweep_s128.json
+  unset HVE_SELL_SIGMA
+fi
+if [[ $WHAT == all || $WHAT == pmc ]]; then
+  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python scripts/level_sweep.py --reps 3
+  step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python scripts/level_sweep.py --reps 3
+  step pmc_tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d $OUT/pmc_tcc -o run --output-format csv -- python scripts/level_sweep.py --reps 3
+fi
+echo "=== done"
