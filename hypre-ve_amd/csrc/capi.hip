@@ -1051,11 +1051,11 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
   API_END
 }
 
-// Read-only streaming kernel over n elements of elem_bytes (4 or 8) each: the
+// Read-only streaming kernel over n elements of elem_bytes (4, 8 or 16) each: the
 // calibration pass for rocprofv3 FETCH_SIZE at this access width and the
 // achievable-bandwidth reference for the roofline.
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real* avg_ms) {
-  CHECK_ARG(elem_bytes == 4 || elem_bytes == 8, 1);
+  CHECK_ARG(elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16, 1);
   CHECK_ARG(n > 0, 2);
   CHECK_ARG(reps > 0, 3);
   API_BEGIN
@@ -1065,12 +1065,12 @@ HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, H
   HVE_HIP(hipMalloc(&buf, (size_t)n * elem_bytes));
   HVE_HIP(hipMalloc((void**)&out, sizeof(double)));
   HVE_HIP(hipMemsetAsync(buf, 0, (size_t)n * elem_bytes, st));
-  for (int w = 0; w < 2; ++w) HVE_HIP(launch_stream_read(n, elem_bytes, buf, out, st));
+  for (int w = 0; w < 2; ++w) HVE_HIP(launch_stream_read((int64_t)n * elem_bytes, elem_bytes, buf, out, st));
   hipEvent_t e0, e1;
   HVE_HIP(hipEventCreate(&e0));
   HVE_HIP(hipEventCreate(&e1));
   HVE_HIP(hipEventRecord(e0, st));
-  for (int r = 0; r < reps; ++r) HVE_HIP(launch_stream_read(n, elem_bytes, buf, out, st));
+  for (int r = 0; r < reps; ++r) HVE_HIP(launch_stream_read((int64_t)n * elem_bytes, elem_bytes, buf, out, st));
   HVE_HIP(hipEventRecord(e1, st));
   HVE_HIP(hipEventSynchronize(e1));
   float ms = 0.f;

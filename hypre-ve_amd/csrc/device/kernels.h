@@ -12,6 +12,7 @@ struct SellView {
   const int* rowmap = nullptr;     // subset row -> local row, nullptr = identity
   int nrows = 0;
   int ncols = 0;
+  int batch = 0;                   // entries per load batch (8 or 16), 0 = default
 };
 
 enum : int {
@@ -24,8 +25,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 // op: 0 l1-Jacobi w=1, 1 l1-Jacobi weighted, 2 Jacobi (s = diagonal)
 hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u,
                              hipStream_t st);
-int sell_batch();
-hipError_t launch_stream_read(int64_t n, int elem_bytes, const void* buf, double* out, hipStream_t st);
+int sell_batch_override();
+bool sell_pipe();
+hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, double* out, hipStream_t st);
 hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st);
 hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,
                        hipStream_t st);

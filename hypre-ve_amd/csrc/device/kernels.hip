@@ -71,9 +71,51 @@ struct SpArgs {
 // chains in flight per lane (a lane-per-row loop with one load pair per step is
 // latency-bound on the long rows of the Galerkin levels) without changing the
 // order or rounding of the row sum.
+template <int B>
+__device__ __forceinline__ void sell_load(const int* __restrict__ cp, const double* __restrict__ vp, int k, int width,
+                                          int (&c)[B], double (&a)[B]) {
+#pragma unroll
+  for (int q = 0; q < B; ++q) {
+    const bool in = (k + q) < width;
+    c[q] = in ? cp[(k + q) * kWave] : -1;
+    a[q] = in ? vp[(k + q) * kWave] : 0.0;
+  }
+}
+
+// Software-pipelined form: the column/value loads of batch k+1 are issued
+// between the x gathers and the adds of batch k, so a wave keeps two batches
+// of loads in flight (counted vmcnt) instead of draining at every batch.
 template <bool SUB, int B>
+__device__ __forceinline__ double sell_row_pipe(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
+                                                int width, const double* __restrict__ x, double t) {
+  if (k0 >= width) return t;
+  int c[B];
+  double a[B];
+  sell_load<B>(cp, vp, k0, width, c, a);
+  for (int k = k0; k < width; k += B) {
+    double xv[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) xv[q] = c[q] >= 0 ? x[c[q]] : 0.0;
+    int cn[B];
+    double an[B];
+    sell_load<B>(cp, vp, k + B, width, cn, an);
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      if (c[q] >= 0) {
+        if (SUB) t -= a[q] * xv[q];
+        else t += a[q] * xv[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) { c[q] = cn[q]; a[q] = an[q]; }
+  }
+  return t;
+}
+
+template <bool SUB, int B, bool PIPE>
 __device__ __forceinline__ double sell_row(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
                                            int width, const double* __restrict__ x, double t) {
+  if (PIPE) return sell_row_pipe<SUB, B>(cp, vp, k0, width, x, t);
   for (int k = k0; k < width; k += B) {
     int c[B];
     double a[B], xv[B];
@@ -96,7 +138,7 @@ __device__ __forceinline__ double sell_row(const int* __restrict__ cp, const dou
   return t;
 }
 
-template <int OP, bool CFSEL, int B>
+template <int OP, bool CFSEL, int B, bool PIPE>
 __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
   const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
   const int row = lb * 256 + threadIdx.x;
@@ -117,22 +159,22 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
   }
 
   if (OP == OP_RESID || OP == OP_L1JAC) {
-    const double t = sell_row<true, B>(cp, vp, 0, width, p.x, p.b[g]);
+    const double t = sell_row<true, B, PIPE>(cp, vp, 0, width, p.x, p.b[g]);
     if (OP == OP_RESID) p.y[g] = t;
     else p.y[g] = p.x[g] + t / p.l1[g];
   } else if (OP == OP_L1JAC_W) {
-    const double t = sell_row<false, B>(cp, vp, 0, width, p.x, -p.b[g]);
+    const double t = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, -p.b[g]);
     const double v = (-p.w) * t;
     p.y[g] = p.x[g] + v / p.l1[g];
   } else if (OP == OP_MATVEC || OP == OP_RESTRICT) {
-    p.y[g] = sell_row<false, B>(cp, vp, 0, width, p.x, 0.0);
+    p.y[g] = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, 0.0);
   } else if (OP == OP_PROLONG) {
-    p.y[g] = sell_row<false, B>(cp, vp, 0, width, p.x, p.y[g]);
+    p.y[g] = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, p.y[g]);
   } else if (OP == OP_JAC) {
     const double d = vp[0];  // diagonal stored first
     const double uo = p.x[g];
     if (d == 0.0) { p.y[g] = uo; return; }
-    const double t = sell_row<true, B>(cp, vp, 1, width, p.x, p.b[g]);
+    const double t = sell_row<true, B, PIPE>(cp, vp, 1, width, p.x, p.b[g]);
     double u = uo * (1.0 - p.w);
     u += p.w * t / d;
     p.y[g] = u;
@@ -145,8 +187,8 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     else if (temp == -1.0) t = neg ? p.b[g] : -p.b[g];
     else if (temp == 1.0) t = neg ? -p.b[g] : p.b[g];
     else t = neg ? -p.b[g] * temp : p.b[g] * temp;
-    if (neg) t = sell_row<true, B>(cp, vp, 0, width, p.x, t);
-    else t = sell_row<false, B>(cp, vp, 0, width, p.x, t);
+    if (neg) t = sell_row<true, B, PIPE>(cp, vp, 0, width, p.x, t);
+    else t = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, t);
     p.y[g] = (alpha == 1.0 || neg) ? t : alpha * t;
   }
 }
@@ -298,11 +340,14 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.w = w; a.temp = temp; a.relax_points = relax_points;
   dim3 grid(a.nblocks_pad), block(256);
   const bool cfsel = (relax_points != 0 && cf != nullptr);
-  const int bsel = sell_batch();
-#define HVE_LB(OPV, CF)                                                        \
-  if (bsel == 4) hipLaunchKernelGGL((k_sell<OPV, CF, 4>), grid, block, 0, s, a);  \
-  else if (bsel == 16) hipLaunchKernelGGL((k_sell<OPV, CF, 16>), grid, block, 0, s, a); \
-  else hipLaunchKernelGGL((k_sell<OPV, CF, 8>), grid, block, 0, s, a);
+  const int bsel = sell_batch_override() ? sell_batch_override() : (M.batch ? M.batch : 8);
+  const bool pipe = sell_pipe();
+#define HVE_LP(OPV, CF, BB)                                                             \
+  if (pipe) hipLaunchKernelGGL((k_sell<OPV, CF, BB, true>), grid, block, 0, s, a);     \
+  else hipLaunchKernelGGL((k_sell<OPV, CF, BB, false>), grid, block, 0, s, a);
+#define HVE_LB(OPV, CF)                    \
+  if (bsel == 16) { HVE_LP(OPV, CF, 16) } \
+  else { HVE_LP(OPV, CF, 8) }
 #define HVE_L(OPV)              \
   case OPV:                     \
     if (cfsel) { HVE_LB(OPV, true) } \
@@ -315,30 +360,50 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   }
 #undef HVE_L
 #undef HVE_LB
+#undef HVE_LP
   return hipGetLastError();
 }
 
-// Entries per load batch in the SELL row loop: 8 by default (see sell_row);
-// HVE_SELL_BATCH=4|16 selects the other instantiations for experiments.
-int sell_batch() {
+// Entries per load batch in the SELL row loop: chosen per operator at upload
+// (SellView::batch); HVE_SELL_BATCH=8|16 overrides it and HVE_SELL_PIPE=1
+// selects the software-pipelined loop, for experiments.
+int sell_batch_override() {
   static const int b = [] {
     const char* e = getenv("HVE_SELL_BATCH");
-    const int v = e ? atoi(e) : 8;
-    return (v == 4 || v == 16) ? v : 8;
+    const int v = e ? atoi(e) : 0;
+    return (v == 8 || v == 16) ? v : 0;
   }();
   return b;
 }
-
-__global__ void __launch_bounds__(256) k_stream_read(int64_t n, int elem_bytes, const void* __restrict__ buf,
-                                                     double* __restrict__ out) {
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  double v = 0.0;
-  if (i < n) v = elem_bytes == 4 ? (double)((const int*)buf)[i] : ((const double*)buf)[i];
-  if (v == 12345.678) out[0] = v;  // keeps the load; never true for the zero-filled buffer
+bool sell_pipe() {
+  static const bool p = [] {
+    const char* e = getenv("HVE_SELL_PIPE");
+    return e && atoi(e) != 0;
+  }();
+  return p;
 }
-hipError_t launch_stream_read(int64_t n, int elem_bytes, const void* buf, double* out, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_stream_read, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, n, elem_bytes, buf, out);
+
+// Grid-stride read-only stream (4, 8 or 16 B per lane and load): the
+// calibration pass for FETCH_SIZE at each width and the achievable-bandwidth
+// reference.  The sum is only stored when it equals a value the zero-filled
+// buffer never produces, so the loads stay and nothing is written.
+template <typename T>
+__global__ void __launch_bounds__(256) k_stream_read(int64_t n, const T* __restrict__ buf, double* __restrict__ out) {
+  double acc = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const T v = buf[i];
+    if constexpr (sizeof(T) == 16) acc += (double)v.x + (double)v.y + (double)v.z + (double)v.w;
+    else acc += (double)v;
+  }
+  if (acc == 12345.678) out[0] = acc;
+}
+hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, double* out, hipStream_t st) {
+  if (n_bytes <= 0) return hipSuccess;
+  const int64_t n = n_bytes / elem_bytes;
+  const dim3 grid(256 * 16), block(256);  // 16 workgroups per CU, 4 waves each
+  if (elem_bytes == 4) hipLaunchKernelGGL(k_stream_read<int>, grid, block, 0, st, n, (const int*)buf, out);
+  else if (elem_bytes == 8) hipLaunchKernelGGL(k_stream_read<double>, grid, block, 0, st, n, (const double*)buf, out);
+  else hipLaunchKernelGGL(k_stream_read<int4>, grid, block, 0, st, n, (const int4*)buf, out);
   return hipGetLastError();
 }
 

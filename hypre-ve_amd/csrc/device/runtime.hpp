@@ -32,9 +32,10 @@ struct DevSell {
   int* col = nullptr;
   double* val = nullptr;
   int* rowmap = nullptr;
+  int batch = 8;
   SellView view() const {
     SellView v;
-    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.nrows = nrows; v.ncols = ncols;
+    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.nrows = nrows; v.ncols = ncols; v.batch = batch;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map

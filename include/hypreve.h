@@ -245,7 +245,7 @@ HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver solver, HYPRE_Int reps, HYPRE_Real 
  * as restriction): average ms over reps, algorithmic bytes, padded entries. */
 HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,
                                HYPRE_Real *avg_ms, HYPRE_Real *bytes, HYPRE_Real *padded_nnz);
-/* Read-only streaming kernel (elem_bytes 4 or 8): FETCH_SIZE calibration. */
+/* Read-only streaming kernel (elem_bytes 4, 8 or 16): FETCH_SIZE calibration. */
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real *avg_ms);
 HYPRE_Int hypreve_DeviceSynchronize(void);
 const char *hypreve_BuildInfo(void);

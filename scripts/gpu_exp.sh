@@ -22,12 +22,11 @@ if [[ $WHAT == all || $WHAT == tests ]]; then
   step pytest_gpu 600 python -m pytest tests -m gpu -x -q
 fi
 if [[ $WHAT == all || $WHAT == sweep ]]; then
-  step sweep_b8 300 python scripts/level_sweep.py --json $OUT/sweep_b8.json
-  export HVE_SELL_BATCH=4;  step sweep_b4 300 python scripts/level_sweep.py --json $OUT/sweep_b4.json
-  export HVE_SELL_BATCH=16; step sweep_b16 300 python scripts/level_sweep.py --json $OUT/sweep_b16.json
-  unset HVE_SELL_BATCH
-  export HVE_SELL_SIGMA=128; step sweep_s128 300 python scripts/level_sweep.py --json $OUT/sweep_s128.json
-  unset HVE_SELL_SIGMA
+  step sweep_auto 300 python scripts/level_sweep.py --json $OUT/sweep_auto.json
+  export HVE_SELL_PIPE=1; step sweep_pipe 300 python scripts/level_sweep.py --json $OUT/sweep_pipe.json
+  export HVE_SELL_BATCH=8; step sweep_pipe_b8 300 python scripts/level_sweep.py --json $OUT/sweep_pipe_b8.json
+  unset HVE_SELL_PIPE HVE_SELL_BATCH
+  step bench 600 python bench.py --steps 10 --warmup 2 --cpu-cycles 0
 fi
 if [[ $WHAT == all || $WHAT == pmc ]]; then
   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python scripts/level_sweep.py --reps 3

@@ -30,10 +30,10 @@ def main():
     import hypreve as hv
 
     hv.init()
-    variant = {k: os.environ.get(k, "") for k in ("HVE_SELL_BATCH", "HVE_SELL_SIGMA")}
+    variant = {k: os.environ.get(k, "") for k in ("HVE_SELL_BATCH", "HVE_SELL_SIGMA", "HVE_SELL_PIPE")}
     print(f"variant {variant}", flush=True)
     rows = []
-    for eb in (4, 8):
+    for eb in (4, 8, 16):
         n = (1 << 31) // eb  # 2 GiB
         ms = hv.bench_stream(eb, n, args.reps)
         gbs = n * eb / (ms * 1e-3) / 1e9
