@@ -1007,6 +1007,34 @@ HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver s, HYPRE_Int reps, HYPRE_Real* avg_
   API_END
 }
 
+// Host check of every hybrid Gauss-Seidel level schedule of the hierarchy
+// (both directions, diagonal and l1 scaling) against the sequential sweep.
+HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver s, HYPRE_Int num_blocks) {
+  CHECK_ARG(s && s->kind == KIND_AMG && !s->H.lev.empty(), 1);
+  CHECK_ARG(num_blocks >= 1, 2);
+  API_BEGIN
+  for (size_t l = 0; l < s->H.lev.size(); ++l) {
+    const CSR& A = s->H.lev[l].A;
+    std::vector<double> l1 = s->H.lev[l].l1;
+    if (l1.empty()) {
+      l1.resize(A.nrows);
+      for (int i = 0; i < A.nrows; ++i) {
+        double t = 0;
+        for (int k = A.i[i]; k < A.i[i + 1]; ++k) t += std::fabs(A.a[k]);
+        l1[i] = t;
+      }
+    }
+    for (int fwd = 0; fwd < 2; ++fwd)
+      for (int use_l1 = 0; use_l1 < 2; ++use_l1) {
+        std::string msg;
+        if (gs_schedule_self_check(A, num_blocks, fwd != 0, use_l1 != 0, l1, msg))
+          throw std::runtime_error("level " + std::to_string(l) + (fwd ? " forward" : " backward") +
+                                   (use_l1 ? " l1" : "") + ": " + msg);
+      }
+  }
+  API_END
+}
+
 // Average time of one application of a level operator (which: 0 = A_l as the
 // residual r = f - A u, 1 = P_l as prolongation u_l += P u_{l+1}, 2 = R_l as
 // restriction f_{l+1} = R r_l) with its algorithmic bytes: every stored

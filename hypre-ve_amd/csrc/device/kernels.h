@@ -25,6 +25,20 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 // op: 0 l1-Jacobi w=1, 1 l1-Jacobi weighted, 2 Jacobi (s = diagonal)
 hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u,
                              hipStream_t st);
+// Device view of a hybrid Gauss-Seidel level schedule (host/layout.hpp GsSchedule).
+struct GsView {
+  const int* block_start = nullptr;
+  const int* block_level = nullptr;
+  const int* level_slice = nullptr;
+  const int* slice_ptr = nullptr;
+  const int* col = nullptr;
+  const double* val = nullptr;
+  const int* rowmap = nullptr;
+  int nblocks = 0;
+  int wg = 64;  // workgroup size: 64, or 256 for wide levels
+};
+hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const double* l1, const int* cf,
+                            int relax_points, const double* tmp, double* u, hipStream_t st);
 int sell_batch_override();
 bool sell_pipe();
 hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, double* out, hipStream_t st);

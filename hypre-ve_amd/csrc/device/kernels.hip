@@ -193,6 +193,106 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Hybrid Gauss-Seidel sweep over a level schedule (host: build_gs_schedule).
+// One workgroup per hypre thread block [ns, ne); its levels run in order with
+// a workgroup barrier between them, the rows of a level in parallel (lane per
+// row).  In-block columns read the iterate being updated (already relaxed for
+// the rows of earlier levels, not yet relaxed for later ones, exactly as the
+// sequential sweep sees them); out-of-block columns read tmp, the copy taken
+// before the sweep (par_relax.c tmp_data / Vext_data).
+//   L1 = true : cases 8/13/14, res = f - sum_all a*u, u += res / l1
+//   L1 = false: cases 3/4/6,   res = f - sum_offdiag a*u, u = res / a_ii
+// ---------------------------------------------------------------------------
+struct GsArgs {
+  const int* __restrict__ block_start;
+  const int* __restrict__ block_level;
+  const int* __restrict__ level_slice;
+  const int* __restrict__ slice_ptr;
+  const int* __restrict__ col;
+  const double* __restrict__ val;
+  const int* __restrict__ rowmap;
+  const double* __restrict__ f;
+  const double* __restrict__ l1;
+  const int* __restrict__ cf;
+  const double* tmp;
+  double* u;
+  int relax_points;
+};
+
+template <bool L1, bool CFSEL, int WG>
+__global__ void __launch_bounds__(WG) k_hybrid_gs(GsArgs p) {
+  constexpr int B = 8;
+  const int blk = blockIdx.x;
+  const int ns = p.block_start[blk], ne = p.block_start[blk + 1];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
+  constexpr int nwaves = WG / kWave;
+  for (int lv = p.block_level[blk]; lv < p.block_level[blk + 1]; ++lv) {
+    for (int sl = p.level_slice[lv] + wave; sl < p.level_slice[lv + 1]; sl += nwaves) {
+      const int i = p.rowmap[(size_t)sl * kWave + lane];
+      if (i < 0) continue;
+      if (CFSEL && p.cf[i] != p.relax_points) continue;
+      const int beg = p.slice_ptr[sl];
+      const int width = (p.slice_ptr[sl + 1] - beg) >> 6;
+      const int* __restrict__ cp = p.col + beg + lane;
+      const double* __restrict__ vp = p.val + beg + lane;
+      double scale;
+      int k0;
+      if (L1) {
+        scale = p.l1[i];
+        k0 = 0;
+      } else {
+        scale = vp[0];  // diagonal stored first
+        k0 = 1;
+      }
+      if (scale == 0.0) continue;
+      double res = p.f[i];
+      for (int k = k0; k < width; k += B) {
+        int c[B];
+        double a[B], xv[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const bool in = (k + q) < width;
+          c[q] = in ? cp[(k + q) * kWave] : -1;
+          a[q] = in ? vp[(k + q) * kWave] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const int cc = c[q];
+          xv[q] = cc < 0 ? 0.0 : ((cc >= ns && cc < ne) ? p.u[cc] : p.tmp[cc]);
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+          if (c[q] >= 0) res -= a[q] * xv[q];
+      }
+      if (L1) p.u[i] += res / scale;
+      else p.u[i] = res / scale;
+    }
+    __syncthreads();  // workgroup-scope release/acquire: the level's updates are visible to the next
+  }
+}
+
+hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const double* l1, const int* cf,
+                            int relax_points, const double* tmp, double* u, hipStream_t st) {
+  if (S.nblocks <= 0) return hipSuccess;
+  GsArgs a;
+  a.block_start = S.block_start; a.block_level = S.block_level; a.level_slice = S.level_slice;
+  a.slice_ptr = S.slice_ptr; a.col = S.col; a.val = S.val; a.rowmap = S.rowmap;
+  a.f = f; a.l1 = l1; a.cf = cf; a.tmp = tmp ? tmp : u; a.u = u; a.relax_points = relax_points;
+  const bool cfsel = relax_points != 0 && cf != nullptr;
+  const dim3 grid(S.nblocks);
+#define HVE_G(L1V, CFV)                                                                       \
+  if (S.wg == 256) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, 256>), grid, dim3(256), 0, st, a); \
+  else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, 64>), grid, dim3(64), 0, st, a);
+  if (use_l1) {
+    if (cfsel) { HVE_G(true, true) } else { HVE_G(true, false) }
+  } else {
+    if (cfsel) { HVE_G(false, true) } else { HVE_G(false, false) }
+  }
+#undef HVE_G
+  return hipGetLastError();
+}
+
 // Zero-initial-guess smoothers (coarse levels right after U_c = 0): A*0 is
 // exactly zero, so the reference's arithmetic reduces to elementwise forms.
 //   l1-Jacobi, w = 1: u = 0 + f/l1       ams.c:96 (v = f - A*0; u += v/l1)

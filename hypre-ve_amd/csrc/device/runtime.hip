@@ -86,6 +86,31 @@ void DevSell::release() {
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0;
 }
 
+void DevGs::upload(const CSR& A, int num_blocks, bool forward) {
+  release();
+  GsSchedule S;
+  build_gs_schedule(A, hypre_block_starts(A.nrows, num_blocks), forward, S);
+  nblocks = (int)S.block_start.size() - 1;
+  max_levels = S.max_levels;
+  wg = S.avg_rows_per_level > 96.0 ? 256 : 64;
+  block_start = dupload(S.block_start.data(), S.block_start.size());
+  block_level = dupload(S.block_level.data(), S.block_level.size());
+  level_slice = dupload(S.level_slice.data(), S.level_slice.size());
+  slice_ptr = dupload(S.slice_ptr.data(), S.slice_ptr.size());
+  col = dupload(S.col.data(), std::max<size_t>(1, S.col.size()));
+  val = dupload(S.val.data(), std::max<size_t>(1, S.val.size()));
+  rowmap = dupload(S.rowmap.data(), std::max<size_t>(1, S.rowmap.size()));
+}
+void DevGs::release() {
+  for (void* p : {(void*)block_start, (void*)block_level, (void*)level_slice, (void*)slice_ptr, (void*)col,
+                  (void*)val, (void*)rowmap})
+    if (p) (void)hipFree(p);
+  block_start = block_level = level_slice = slice_ptr = col = rowmap = nullptr;
+  val = nullptr;
+  nblocks = 0;
+  max_levels = 0;
+}
+
 void DevOp::upload(const RankOp& op) {
   in.upload(op.interior, op.map_int);
   bd.upload(op.boundary, op.map_bnd);
@@ -128,7 +153,9 @@ void DevAMG::release() {
   for (auto& L : lev_) {
     L.A.release(); L.P.release(); L.R.release();
     L.hu.release(); L.hv.release();
-    for (void* p : {(void*)L.l1, (void*)L.cf, (void*)L.F, (void*)L.U[0], (void*)L.U[1], (void*)L.V})
+    L.gs_fwd.release(); L.gs_bwd.release();
+    for (void* p : {(void*)L.l1, (void*)L.cf, (void*)L.F, (void*)L.U[0], (void*)L.U[1], (void*)L.V,
+                    (void*)L.gs_tmp})
       if (p) (void)hipFree(p);
   }
   lev_.clear();
@@ -198,6 +225,26 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     HVE_HIP(hipMemset(D.U[0], 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
     HVE_HIP(hipMemset(D.U[1], 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
     HVE_HIP(hipMemset(D.V, 0, sizeof(double) * std::max(1, D.n + D.hv.n_halo)));
+  }
+  // Hybrid Gauss-Seidel schedules for the relax types the cycle uses
+  // (num_blocks = hypre's thread count: row blocks of each level).
+  {
+    bool fwd = false, bwd = false;
+    for (int c = 0; c < 4; ++c) {
+      const int rt = prm.relax_type[c];
+      fwd = fwd || rt == 3 || rt == 6 || rt == 8 || rt == 13;
+      bwd = bwd || rt == 4 || rt == 6 || rt == 8 || rt == 14;
+    }
+    if ((fwd || bwd) && comm_)
+      throw std::runtime_error("hybrid Gauss-Seidel (relax 3/4/6/8/13/14) across ranks is not available in this build");
+    for (int l = 0; l < nl && (fwd || bwd); ++l) {
+      const RankLevel& L = R.lev[l];
+      DevLevel& D = lev_[l];
+      if (l == nl - 1 && R.coarse_n > 0) break;  // coarsest level: direct solve
+      if (fwd) D.gs_fwd.upload(L.A.interior, prm.num_blocks, true);
+      if (bwd) D.gs_bwd.upload(L.A.interior, prm.num_blocks, false);
+      D.gs_tmp = dalloc<double>(D.n + D.hu.n_halo);
+    }
   }
   coarse_n_ = R.coarse_n;
   if (coarse_n_ > 0) {
@@ -313,6 +360,27 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       if (zero_guess) HVE_HIP(launch_set(n, 0.0, u_cur, s));
       apply(L.A, &L.hu, K_JAC, u_cur, f, nullptr, L.cf, relax_points, u_alt, w, 0.0, s);
       std::swap(u_cur, u_alt);
+      break;
+    }
+    case 3: case 4: case 6: case 8: case 13: case 14: {
+      // par_relax.c:354 (3), :1875 (4), :2266 (6), :3492 (8), :4340 (13), :4732 (14)
+      if (w != 1.0 || prm.outer_weight != 1.0)
+        throw std::runtime_error("weighted hybrid Gauss-Seidel / SOR (relax_wt or outer_wt != 1) is not available "
+                                 "on the GPU path in this build");
+      const bool use_l1 = relax_type == 8 || relax_type == 13 || relax_type == 14;
+      const bool fw = relax_type == 3 || relax_type == 6 || relax_type == 8 || relax_type == 13;
+      const bool bw = relax_type == 4 || relax_type == 6 || relax_type == 8 || relax_type == 14;
+      if (use_l1 && !L.l1) throw std::runtime_error("l1 norms missing for l1 hybrid Gauss-Seidel");
+      if ((fw && !L.gs_fwd.built()) || (bw && !L.gs_bwd.built()))
+        throw std::runtime_error("hybrid Gauss-Seidel schedule missing on level " + std::to_string(level));
+      if (zero_guess) HVE_HIP(launch_set(n, 0.0, u_cur, s));
+      const double* tmp = nullptr;
+      if (L.gs_fwd.built() ? L.gs_fwd.nblocks > 1 : L.gs_bwd.nblocks > 1) {
+        HVE_HIP(launch_copy(n, u_cur, L.gs_tmp, s));  // tmp_data[i] = u_data[i]
+        tmp = L.gs_tmp;
+      }
+      if (fw) HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, s));
+      if (bw) HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, s));
       break;
     }
     default:

@@ -53,6 +53,27 @@ struct DevOp {
   void release() { in.release(); bd.release(); }
 };
 
+// Level schedule of one hybrid Gauss-Seidel sweep direction, in HBM.
+struct DevGs {
+  int* block_start = nullptr;
+  int* block_level = nullptr;
+  int* level_slice = nullptr;
+  int* slice_ptr = nullptr;
+  int* col = nullptr;
+  double* val = nullptr;
+  int* rowmap = nullptr;
+  int nblocks = 0, wg = 64, max_levels = 0;
+  bool built() const { return nblocks > 0; }
+  GsView view() const {
+    GsView v;
+    v.block_start = block_start; v.block_level = block_level; v.level_slice = level_slice;
+    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.nblocks = nblocks; v.wg = wg;
+    return v;
+  }
+  void upload(const CSR& A, int num_blocks, bool forward);
+  void release();
+};
+
 struct DevHalo {
   int n_loc = 0, n_halo = 0, n_send = 0;
   std::vector<int> peers, recv_cnt, recv_off, send_cnt, send_off;
@@ -73,6 +94,8 @@ struct DevLevel {
   double* F = nullptr;
   double* U[2] = {nullptr, nullptr};  // n + hu.n_halo each
   double* V = nullptr;                // n + hv.n_halo
+  DevGs gs_fwd, gs_bwd;               // hybrid Gauss-Seidel schedules (when a cycle uses them)
+  double* gs_tmp = nullptr;           // pre-sweep copy of u (n + hu.n_halo)
 };
 
 class DevAMG {

@@ -1,5 +1,6 @@
 // Host-side construction of the HBM layouts consumed by the device runtime.
 #include <algorithm>
+#include <cstdint>
 #include <cstring>
 #include <stdexcept>
 
@@ -66,6 +67,175 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
     }
   }
   if (sigma <= 0) perm.clear();
+}
+
+std::vector<int> hypre_block_starts(int n, int nb) {
+  if (nb < 1) nb = 1;
+  std::vector<int> st(nb + 1);
+  const int size = n / nb, rest = n - size * nb;
+  for (int j = 0; j < nb; ++j) st[j] = j < rest ? j * size + j : j * size + rest;
+  st[nb] = n;
+  return st;
+}
+
+void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool forward, GsSchedule& S) {
+  const int nb = (int)block_start.size() - 1;
+  S.block_start = block_start;
+  // per block: levels of its rows, then rows grouped by level (ascending row
+  // order inside a level, as the reference's stable sort by level leaves them)
+  std::vector<std::vector<int>> lvl_rows_ptr(nb), lvl_rows(nb);
+  std::vector<int> level(A.nrows, 0), floor_(A.nrows, 0);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int b = 0; b < nb; ++b) {
+    const int ns = block_start[b], ne = block_start[b + 1];
+    int nlev = 0;
+    for (int q = 0; q < ne - ns; ++q) {
+      const int i = forward ? ns + q : ne - 1 - q;
+      int m = -1;
+      for (int k = A.i[i]; k < A.i[i + 1]; ++k) {
+        const int c = A.j[k];
+        if (c < ns || c >= ne || c == i) continue;
+        if ((forward && c < i) || (!forward && c > i)) m = std::max(m, level[c]);
+      }
+      const int L = std::max(m + 1, floor_[i]);
+      level[i] = L;
+      nlev = std::max(nlev, L + 1);
+      for (int k = A.i[i]; k < A.i[i + 1]; ++k) {
+        const int c = A.j[k];
+        if (c < ns || c >= ne || c == i) continue;
+        if ((forward && c > i) || (!forward && c < i)) floor_[c] = std::max(floor_[c], L + 1);
+      }
+    }
+    auto& ptr = lvl_rows_ptr[b];
+    auto& rows = lvl_rows[b];
+    ptr.assign(nlev + 1, 0);
+    for (int i = ns; i < ne; ++i) ptr[level[i] + 1]++;
+    for (int l = 0; l < nlev; ++l) ptr[l + 1] += ptr[l];
+    rows.resize(ne - ns);
+    std::vector<int> pos(ptr.begin(), ptr.end() - 1);
+    for (int i = ns; i < ne; ++i) rows[pos[level[i]]++] = i;
+  }
+  // pack: block -> levels -> slices of 64 rows
+  S.block_level.assign(nb + 1, 0);
+  S.level_slice.assign(1, 0);
+  S.slice_ptr.assign(1, 0);
+  S.rowmap.clear();
+  S.max_levels = 0;
+  int64_t entries = 0;
+  int nslices = 0;
+  for (int b = 0; b < nb; ++b) {
+    const int nlev = (int)lvl_rows_ptr[b].size() - 1;
+    S.max_levels = std::max(S.max_levels, nlev);
+    S.block_level[b + 1] = S.block_level[b] + nlev;
+    for (int l = 0; l < nlev; ++l) {
+      const int r0 = lvl_rows_ptr[b][l], r1 = lvl_rows_ptr[b][l + 1];
+      for (int s0 = r0; s0 < r1; s0 += 64) {
+        int w = 0;
+        for (int t = s0; t < std::min(r1, s0 + 64); ++t) {
+          const int i = lvl_rows[b][t];
+          w = std::max(w, A.i[i + 1] - A.i[i]);
+        }
+        entries += (int64_t)w * 64;
+        if (entries > 0x7fffffffLL) throw std::runtime_error("Gauss-Seidel schedule exceeds 2^31 entries");
+        S.slice_ptr.push_back((int)entries);
+        for (int t = 0; t < 64; ++t) S.rowmap.push_back(s0 + t < r1 ? lvl_rows[b][s0 + t] : -1);
+        ++nslices;
+      }
+      S.level_slice.push_back(nslices);
+    }
+  }
+  S.col.assign((size_t)entries, -1);
+  S.val.assign((size_t)entries, 0.0);
+#pragma omp parallel for schedule(static)
+  for (int sl = 0; sl < nslices; ++sl) {
+    for (int lane = 0; lane < 64; ++lane) {
+      const int i = S.rowmap[(size_t)sl * 64 + lane];
+      if (i < 0) continue;
+      for (int k = A.i[i]; k < A.i[i + 1]; ++k) {
+        const size_t p = (size_t)S.slice_ptr[sl] + (size_t)(k - A.i[i]) * 64 + lane;
+        S.col[p] = A.j[k];
+        S.val[p] = A.a[k];
+      }
+    }
+  }
+  const int nlev_total = (int)S.level_slice.size() - 1;
+  S.avg_rows_per_level = nlev_total ? (double)A.nrows / nlev_total : 0.0;
+}
+
+int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_l1, const std::vector<double>& l1,
+                           std::string& msg) {
+  const int n = A.nrows;
+  const std::vector<int> bs = hypre_block_starts(n, num_blocks);
+  GsSchedule S;
+  build_gs_schedule(A, bs, forward, S);
+  std::vector<double> f(n), u0(n);
+  uint64_t st = 0x9e3779b97f4a7c15ULL;
+  auto rnd = [&] { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return (double)(st >> 11) / 9007199254740992.0 - 0.5; };
+  for (int i = 0; i < n; ++i) { f[i] = rnd(); u0[i] = rnd(); }
+  auto row_update = [&](int i, int ns, int ne, const std::vector<double>& u, const std::vector<double>& tmp,
+                        bool* skip) {
+    const double scale = use_l1 ? l1[i] : A.a[A.i[i]];
+    *skip = scale == 0.0;
+    if (*skip) return 0.0;
+    double res = f[i];
+    for (int k = A.i[i] + (use_l1 ? 0 : 1); k < A.i[i + 1]; ++k) {
+      const int c = A.j[k];
+      res -= A.a[k] * ((c >= ns && c < ne) ? u[c] : tmp[c]);
+    }
+    return use_l1 ? u[i] + res / scale : res / scale;
+  };
+  // reference: sequential sweep per block (par_relax.c thread loops)
+  std::vector<double> ref = u0, tmp = u0;
+  for (int b = 0; b + 1 < (int)bs.size(); ++b) {
+    const int ns = bs[b], ne = bs[b + 1];
+    for (int q = 0; q < ne - ns; ++q) {
+      const int i = forward ? ns + q : ne - 1 - q;
+      bool skip;
+      const double v = row_update(i, ns, ne, ref, tmp, &skip);
+      if (!skip) ref[i] = v;
+    }
+  }
+  // schedule: levels in order, each level reads everything before writing
+  std::vector<double> u = u0;
+  if (S.rowmap.size() != (size_t)(S.slice_ptr.size() - 1) * 64) { msg = "rowmap size"; return 1; }
+  std::vector<int> seen(n, 0);
+  for (int b = 0; b + 1 < (int)bs.size(); ++b) {
+    const int ns = bs[b], ne = bs[b + 1];
+    for (int lv = S.block_level[b]; lv < S.block_level[b + 1]; ++lv) {
+      std::vector<std::pair<int, double>> upd;
+      for (int sl = S.level_slice[lv]; sl < S.level_slice[lv + 1]; ++sl) {
+        for (int lane = 0; lane < 64; ++lane) {
+          const int i = S.rowmap[(size_t)sl * 64 + lane];
+          if (i < 0) continue;
+          if (i < ns || i >= ne) { msg = "row outside its block"; return 1; }
+          seen[i]++;
+          // the stored row must be the CSR row, entry for entry
+          const int w = (S.slice_ptr[sl + 1] - S.slice_ptr[sl]) / 64;
+          for (int k = 0; k < w; ++k) {
+            const size_t p = (size_t)S.slice_ptr[sl] + (size_t)k * 64 + lane;
+            const int kk = A.i[i] + k;
+            if (kk < A.i[i + 1] ? (S.col[p] != A.j[kk] || S.val[p] != A.a[kk]) : S.col[p] != -1) {
+              msg = "stored row differs from the CSR row";
+              return 1;
+            }
+          }
+          bool skip;
+          const double v = row_update(i, ns, ne, u, tmp, &skip);
+          if (!skip) upd.push_back({i, v});
+        }
+      }
+      for (auto& pr : upd) u[pr.first] = pr.second;
+    }
+  }
+  for (int i = 0; i < n; ++i)
+    if (seen[i] != 1) { msg = "row " + std::to_string(i) + " scheduled " + std::to_string(seen[i]) + " times"; return 1; }
+  for (int i = 0; i < n; ++i)
+    if (!(u[i] == ref[i])) {
+      msg = "row " + std::to_string(i) + " differs from the sequential sweep";
+      return 1;
+    }
+  msg = "ok: " + std::to_string(S.level_slice.size() - 1) + " levels, max per block " + std::to_string(S.max_levels);
+  return 0;
 }
 
 // hypre_gselim (sstruct_ls/gselim.h) forward elimination of the matrix alone:

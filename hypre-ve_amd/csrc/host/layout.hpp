@@ -1,4 +1,5 @@
 #pragma once
+#include <string>
 #include <vector>
 
 #include "hve_host.hpp"
@@ -13,6 +14,35 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
                      std::vector<int>& col, std::vector<double>& val);
 // Padded entry count of the SELL-64 layout for a given sigma (0 = no sort).
 int64_t sell_padded_nnz(const CSR& A, int sigma);
+// Level schedule of one hybrid Gauss-Seidel sweep (par_relax.c cases 3/4/6/
+// 8/13/14 with hypre's num_threads row blocks; the level scheduling of the
+// reference's relax-6 path, par_relax.c:2340-2650).  Inside each block rows
+// are grouped into levels: a row's level exceeds that of every in-block
+// neighbour it must see updated (lower rows for a forward sweep), and every
+// in-block neighbour it must see un-updated is pushed strictly above it, so the
+// rows of one level never reference each other and a level is one parallel
+// step.  Each level is stored SELL-64 (lane per row, entries in CSR order, so
+// every row sum is formed in the reference's order).
+struct GsSchedule {
+  std::vector<int> block_start;  // nb + 1 row boundaries (hypre's ns / ne)
+  std::vector<int> block_level;  // nb + 1: level range of each block
+  std::vector<int> level_slice;  // nlevels + 1: slice range of each level
+  std::vector<int> slice_ptr;    // nslices + 1 entry offsets
+  std::vector<int> col;          // padded, -1 = padding
+  std::vector<double> val;
+  std::vector<int> rowmap;       // nslices * 64: row of each lane, -1 = none
+  int max_levels = 0;            // longest block schedule
+  double avg_rows_per_level = 0;
+};
+void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool forward, GsSchedule& S);
+// Host check of a schedule: the level-parallel sweep (every read of a level
+// before any of its writes) against the sequential per-block sweep of the
+// reference, on random f / u; returns 0 when bitwise equal.
+int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_l1, const std::vector<double>& l1,
+                           std::string& msg);
+// hypre's thread partition of n rows into nb blocks (par_relax.c size / rest).
+std::vector<int> hypre_block_starts(int n, int nb);
+
 void gselim_factor(int n, const std::vector<double>& dense, std::vector<double>& L, std::vector<unsigned char>& mask,
                    std::vector<double>& U);
 void csr_to_dense(const CSR& A, std::vector<double>& dense);

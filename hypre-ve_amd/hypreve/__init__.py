@@ -163,6 +163,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGCycle", _i, [_p, _p, _p]),
     ("hypreve_BoomerAMGGetKernelStats", _i, [_p, _pd, _i]),
     ("hypreve_BenchFineSpMV", _i, [_p, _i, _pd, _pd]),
+    ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchStream", _i, [_i, C.c_int64, _i, _pd]),
     ("hypreve_DeviceSynchronize", _i, []),
@@ -450,6 +451,9 @@ class BoomerAMG:
                                             _ptr(misc, C.c_int))
         return dict(relax_type=rt.tolist(), num_sweeps=ns.tolist(), relax_weight=float(w[0]), omega=float(w[1]),
                     relax_order=int(misc[0]), cycle_type=int(misc[1]), num_blocks=int(misc[2]))
+
+    def gs_schedule_check(self, num_blocks):
+        check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
 
     def bench_level_op(self, level, which=0, reps=20):
         """(avg_ms, algorithmic bytes, padded entries) of A_l (0), P_l (1) or R_l (2)."""

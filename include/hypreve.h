@@ -241,6 +241,9 @@ HYPRE_Int hypreve_BoomerAMGGetKernelStats(HYPRE_Solver solver, HYPRE_Real *stats
  * events on the solver's stream; returns avg ms and the algorithmic bytes. */
 HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver solver, HYPRE_Int reps, HYPRE_Real *avg_ms,
                                 HYPRE_Real *bytes);
+/* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
+ * reproduces the sequential per-block sweep bit for bit on random data. */
+HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_blocks);
 /* One level operator (which 0 = A as residual, 1 = P as prolongation, 2 = R
  * as restriction): average ms over reps, algorithmic bytes, padded entries. */
 HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,

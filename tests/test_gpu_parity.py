@@ -115,3 +115,41 @@ def test_large_solve_properties(gpu):
     r = hv.ParVector(n, np.ones(n))
     A.matvec(-1.0, x, 1.0, r)
     assert np.sqrt(r.dot(r)) / np.sqrt(n) < 2e-8
+
+
+@pytest.mark.parametrize("relax", [3, 4, 6, 8, 13, 14])
+@pytest.mark.parametrize("num_blocks", [1, 13, 256])
+def test_hybrid_gs_cycle_bitwise(gpu, orc, relax, num_blocks):
+    """Hybrid Gauss-Seidel (par_relax.c cases 3/4/6/8/13/14) with num_blocks =
+    hypre's thread blocks, run on the GPU as per-block level schedules: one
+    V-cycle equals the oracle's sequential per-block sweeps bit for bit."""
+    hv = gpu
+    A, amg, O = setup_pair(hv, orc, (18, 14, 12), coarsen_type=8, relax_type=relax, num_blocks=num_blocks)
+    n = A.n
+    rng = np.random.default_rng(relax * 100 + num_blocks)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+
+
+@pytest.mark.parametrize("coarsen", [8, 10])
+def test_boomeramg_default_smoothers_solve(gpu, orc, coarsen):
+    """BoomerAMG's default smoothers (l1 hybrid GS forward down, backward up,
+    Gaussian elimination coarsest: relax 13 / 14 / 9) over a whole solve."""
+    hv = gpu
+    A, amg, O = setup_pair(hv, orc, (20, 20, 20), coarsen_type=coarsen, num_blocks=64,
+                           cycle_relax_type={1: 13, 2: 14, 3: 9})
+    n = A.n
+    b = hv.ParVector(n, np.ones(n))
+    x = hv.ParVector(n, np.zeros(n))
+    it, rr = amg.solve(A, b, x)
+    u = np.zeros(n)
+    st = O.solve(np.ones(n), u, 1e-8, 100)
+    assert it == st["iterations"]
+    assert np.array_equal(x.get(), u)
+    assert abs(rr - st["rel_res"]) <= RTOL_NORM * st["rel_res"]
