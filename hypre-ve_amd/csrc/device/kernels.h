@@ -17,11 +17,12 @@ struct SellView {
 
 enum : int {
   K_RESID = 0, K_MATVEC = 1, K_L1JAC = 2, K_L1JAC_W = 3, K_JAC = 4,
-  K_PROLONG = 5, K_RESTRICT = 6, K_GENERAL = 7,
+  K_PROLONG = 5, K_RESTRICT = 6, K_GENERAL = 7, K_RESID_L1JAC = 8,
 };
 
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
-                       const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s);
+                       const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
+                       double* y2 = nullptr);
 // op: 0 l1-Jacobi w=1, 1 l1-Jacobi weighted, 2 Jacobi (s = diagonal)
 hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u,
                              hipStream_t st);

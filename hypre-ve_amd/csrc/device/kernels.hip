@@ -46,6 +46,8 @@ enum SpOp : int {
   OP_PROLONG = 5,     // u += P uc                   (alpha=1, beta=1)
   OP_RESTRICT = 6,    // fc = R v                    (MatvecT, alpha=1, beta=0)
   OP_GENERAL = 7,     // y = alpha*A*x + beta*b, hypre's branch structure
+  OP_RESID_L1JAC = 8, // y = b - A x and y2 = x + y/l1 (solve-loop residual fused with
+                      // the next cycle's first l1-Jacobi sweep: the same row sum)
 };
 
 struct SpArgs {
@@ -60,6 +62,7 @@ struct SpArgs {
   const int* __restrict__ cf;     // CF marker (relax_points != 0 only)
   const int* __restrict__ rowmap; // subset row -> local row (nullptr: identity)
   double* __restrict__ y;         // output
+  double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double w;                       // relax weight / alpha
   double temp;                    // beta/alpha for OP_GENERAL
   int relax_points;
@@ -158,9 +161,12 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     }
   }
 
-  if (OP == OP_RESID || OP == OP_L1JAC) {
+  if (OP == OP_RESID || OP == OP_L1JAC || OP == OP_RESID_L1JAC) {
     const double t = sell_row<true, B, PIPE>(cp, vp, 0, width, p.x, p.b[g]);
-    if (OP == OP_RESID) p.y[g] = t;
+    if (OP == OP_RESID_L1JAC) {
+      p.y[g] = t;
+      p.y2[g] = p.x[g] + t / p.l1[g];
+    } else if (OP == OP_RESID) p.y[g] = t;
     else p.y[g] = p.x[g] + t / p.l1[g];
   } else if (OP == OP_L1JAC_W) {
     const double t = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, -p.b[g]);
@@ -431,13 +437,14 @@ static inline int blocks_for(int n) { return (n + 255) / 256; }
 static inline int blocks_pad8(int n) { int b = blocks_for(n); return ((b + 7) / 8) * 8; }
 
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
-                       const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s) {
+                       const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
+                       double* y2) {
   if (M.nrows <= 0) return hipSuccess;
   SpArgs a;
   a.rowmap = M.rowmap;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
   a.nblocks_pad = blocks_pad8(M.nrows);
-  a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.w = w; a.temp = temp; a.relax_points = relax_points;
+  a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.y2 = y2; a.w = w; a.temp = temp; a.relax_points = relax_points;
   dim3 grid(a.nblocks_pad), block(256);
   const bool cfsel = (relax_points != 0 && cf != nullptr);
   const int bsel = sell_batch_override() ? sell_batch_override() : (M.batch ? M.batch : 8);
@@ -455,7 +462,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     break;
   switch (op) {
     HVE_L(OP_RESID) HVE_L(OP_MATVEC) HVE_L(OP_L1JAC) HVE_L(OP_L1JAC_W) HVE_L(OP_JAC)
-    HVE_L(OP_PROLONG) HVE_L(OP_RESTRICT) HVE_L(OP_GENERAL)
+    HVE_L(OP_PROLONG) HVE_L(OP_RESTRICT) HVE_L(OP_GENERAL) HVE_L(OP_RESID_L1JAC)
     default: return hipErrorInvalidValue;
   }
 #undef HVE_L

@@ -298,13 +298,25 @@ void DevAMG::halo_start(const DevHalo& h, double* x, hipStream_t s) {
 void DevAMG::halo_finish(hipStream_t s) { HVE_HIP(hipStreamWaitEvent(s, ev_halo_, 0)); }
 
 void DevAMG::apply(const DevOp& M, const DevHalo* hx, int op, double* x, const double* b, const double* l1,
-                   const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s) {
+                   const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s, double* y2) {
   const bool ex = hx && hx->active() && comm_;
   if (ex) halo_start(*hx, x, s);
-  HVE_HIP(launch_sell(op, M.in.view(), x, b, l1, cf, relax_points, y, w, temp, s));
+  HVE_HIP(launch_sell(op, M.in.view(), x, b, l1, cf, relax_points, y, w, temp, s, y2));
   if (ex) halo_finish(s);
-  if (M.bd.nrows > 0) HVE_HIP(launch_sell(op, M.bd.view(), x, b, l1, cf, relax_points, y, w, temp, s));
+  if (M.bd.nrows > 0) HVE_HIP(launch_sell(op, M.bd.view(), x, b, l1, cf, relax_points, y, w, temp, s, y2));
 }
+
+// The solve loop's residual r = f - A u forms, row for row, the same sum as
+// the next cycle's first level-0 l1-Jacobi sweep (relax 7/18, weight 1,
+// u + (f - A u)/l1), so one kernel can write both (OP_RESID_L1JAC) and the
+// cycle starts after that sweep: one pass over A_0 fewer per iteration, same
+// bits.
+bool DevAMG::can_fuse_presmooth() const {
+  if (lev_.size() < 2 || !lev_[0].l1) return false;
+  const int rt = prm.relax_type[1];
+  return (rt == 18 || rt == 7) && prm.relax_weight == 1.0 && prm.num_sweeps[1] >= 1;
+}
+double* DevAMG::presmooth_buffer() { return u0_buf_[1] ? u0_buf_[1] : lev_[0].U[0]; }
 
 void DevAMG::fine_apply(int op, const double* x, const double* b, double* y, double alpha, double temp,
                         hipStream_t s) {
@@ -390,7 +402,7 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
 }
 
 // par_cycle.c:22 hypre_BoomerAMGCycle, emitted as a kernel sequence.
-void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s) {
+void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed) {
   const int nl = (int)lev_.size();
   std::vector<int> lev_counter(nl, prm.cycle_type);
   std::vector<double*> ucur(nl), ualt(nl);
@@ -398,12 +410,20 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s) {
   std::vector<char> zero(nl, 0);
   lev_counter[0] = 1;
   if (u0_buf_[0]) {
-    HVE_HIP(launch_copy(lev_[0].n, u0, u0_buf_[0], s));
+    if (!presmoothed) HVE_HIP(launch_copy(lev_[0].n, u0, u0_buf_[0], s));
     ucur[0] = u0_buf_[0];
     ualt[0] = u0_buf_[1];
   } else {
     ucur[0] = u0;
     ualt[0] = lev_[0].U[0];
+  }
+  // the first level-0 sweep was formed by the fused residual into ualt[0]:
+  // take the state the relax call would have left (its output, swapped in)
+  bool skip_first = false;
+  if (presmoothed) {
+    if (!can_fuse_presmooth()) throw std::runtime_error("cycle: presmoothed iterate without a fusable smoother");
+    std::swap(ucur[0], ualt[0]);
+    skip_first = true;
   }
   fl[0] = f0;
   for (int l = 1; l < nl; ++l) {
@@ -425,6 +445,10 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s) {
     }
     for (int j = 0; j < num_sweep; ++j) {
       ops += (double)lev_[level].A.nnz();
+      if (skip_first) {
+        skip_first = false;
+        continue;
+      }
       if (relax_type == 9 || relax_type == 99 || relax_type == 19 || relax_type == 98) {
         coarse_solve(level, fl[level], ucur[level], s);
         zero[level] = 0;
@@ -473,18 +497,20 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s) {
   cycle_ops_ = ops;
 }
 
-void DevAMG::cycle(const double* f, double* u, hipStream_t s) {
+void DevAMG::cycle(const double* f, double* u, hipStream_t s, const double* presmoothed) {
+  const bool pre = presmoothed != nullptr;
+  if (pre && presmoothed != presmooth_buffer()) throw std::runtime_error("cycle: unexpected presmoothed buffer");
   if (!use_graph_) {
-    emit_cycle(f, u, s);
+    emit_cycle(f, u, s, pre);
     return;
   }
-  auto key = std::make_pair((const void*)f, (const void*)u);
+  auto key = std::make_tuple((const void*)f, (const void*)u, pre);
   auto it = graphs_.find(key);
   if (it == graphs_.end()) {
     hipGraph_t g;
     HVE_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     try {
-      emit_cycle(f, u, s);
+      emit_cycle(f, u, s, pre);
     } catch (...) {
       hipGraph_t tmp = nullptr;
       (void)hipStreamEndCapture(s, &tmp);
@@ -511,9 +537,30 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
   const double tol = prm.tol;
   double resid_nrm = 1.0, resid_nrm_init = 0.0, rhs_norm = 0.0, relative_resid = 1.0;
   int cycle_count = 0;
+  const bool fuse = tol > 0. && can_fuse_presmooth();
+  double* pre = fuse ? presmooth_buffer() : nullptr;
+  // r = f - A u, and with fusion the first sweep of the next cycle
+  auto residual = [&](bool initial) {
+    if (fuse) {
+      DevLevel& L = lev_[0];
+      double* xin = u;
+      if (x0_buf_) {
+        HVE_HIP(launch_copy(L.n, u, x0_buf_, s));
+        xin = x0_buf_;
+      }
+      apply(L.A, &L.hu, K_RESID_L1JAC, xin, f, L.l1, nullptr, 0, V, 1.0, 0.0, s, pre);
+    } else if (initial) {
+      // Vtemp = A u - f  (hypre copies f then Matvec(1, A, u, -1, Vtemp)); the
+      // same numbers as f - A u up to the sign, so the norms agree bit for bit
+      fine_apply(K_GENERAL, u, f, V, 1.0, -1.0, s);
+    } else {
+      fine_apply(K_RESID, u, f, V, -1.0, 0.0, s);
+    }
+  };
+  bool pre_ready = false;
   if (tol > 0.) {
-    // Vtemp = A u - f  (hypre copies f then Matvec(1, A, u, -1, Vtemp))
-    fine_apply(K_GENERAL, u, f, V, 1.0, -1.0, s);
+    residual(true);
+    pre_ready = fuse;
     resid_nrm = std::sqrt(dot_host(n, V, V, s));
     if (resid_nrm != 0.) {
       double ieee = resid_nrm / resid_nrm;
@@ -526,9 +573,11 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
     }
   }
   while ((relative_resid >= tol || cycle_count < prm.min_iter) && cycle_count < prm.max_iter) {
-    cycle(f, u, s);
+    cycle(f, u, s, pre_ready ? pre : nullptr);
+    pre_ready = false;
     if (tol > 0.) {
-      fine_apply(K_RESID, u, f, V, -1.0, 0.0, s);
+      residual(false);
+      pre_ready = fuse;
       resid_nrm = std::sqrt(dot_host(n, V, V, s));
       if (prm.converge_type == 0) relative_resid = rhs_norm ? resid_nrm / rhs_norm : resid_nrm;
       else relative_resid = resid_nrm / resid_nrm_init;

@@ -110,7 +110,9 @@ class DevAMG {
   bool built() const { return !lev_.empty(); }
 
   // One hypre_BoomerAMGCycle on device vectors f, u (owned rows, length n0).
-  void cycle(const double* f, double* u, hipStream_t s);
+  // presmoothed: level-0 iterate after the first down sweep, already formed by
+  // a fused residual (OP_RESID_L1JAC); nullptr = run that sweep here.
+  void cycle(const double* f, double* u, hipStream_t s, const double* presmoothed = nullptr);
   int solve(const double* f, double* u, hipStream_t s, int* iters, double* rel_res);
   // y = op(A_0) x on owned rows (halo exchanged through an internal buffer)
   void fine_apply(int op, const double* x, const double* b, double* y, double alpha, double temp, hipStream_t s);
@@ -129,12 +131,15 @@ class DevAMG {
   AMGParams prm;
 
  private:
-  void emit_cycle(const double* f0, double* u0, hipStream_t s);
+  void emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed);
+  bool can_fuse_presmooth() const;
+  double* presmooth_buffer();
   void relax(int level, int relax_type, int relax_points, const double* f, double*& u_cur, double*& u_alt,
              bool zero_guess, hipStream_t s);
   // y = op(M) x with the halo of x exchanged first (interior rows overlap it)
   void apply(const DevOp& M, const DevHalo* hx, int op, double* x, const double* b, const double* l1,
-             const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s);
+             const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
+             double* y2 = nullptr);
   void halo_start(const DevHalo& h, double* x, hipStream_t s);
   void halo_finish(hipStream_t s);
   void coarse_solve(int level, const double* f, double* u, hipStream_t s);
@@ -159,7 +164,7 @@ class DevAMG {
   bool use_graph_ = true;
   double cycle_ops_ = 0;
   int ws_n_ = 0;
-  std::map<std::pair<const void*, const void*>, hipGraphExec_t> graphs_;
+  std::map<std::tuple<const void*, const void*, bool>, hipGraphExec_t> graphs_;
 };
 
 // PCG (krylov/pcg.c:262).
