@@ -24,6 +24,26 @@ sys.path.insert(0, os.path.join(ROOT, "hypre-ve_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
+PROFILE_DIR = os.path.join(ROOT, "profiles")
+
+
+def committed_traffic(n, algorithmic_bytes):
+    """HBM bytes per launch of the finest residual SpMV from the newest
+    committed rocprofv3 PMC summary for this workload (scripts/pmc_traffic.py),
+    or None.  Counters need their own profiler passes, so the bench reports
+    the committed measurement of the same kernel and grid."""
+    best = None
+    for rnd in sorted(os.listdir(PROFILE_DIR)) if os.path.isdir(PROFILE_DIR) else []:
+        p = os.path.join(PROFILE_DIR, rnd, f"pmc_traffic_{n}.json")
+        if os.path.exists(p):
+            best = p
+    if not best:
+        return None
+    with open(best) as f:
+        d = json.load(f)
+    return round(d["traffic_bytes"], 0)
+
+
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
@@ -76,8 +96,9 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     # roofline: finest-level SpMV (the dominant kernel), HIP events on the solver stream
     spmv_ms, spmv_bytes = amg.bench_fine_spmv(args.spmv_reps)
     achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    traffic = committed_traffic(n, spmv_bytes)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": "k_sell<OP_RESID> finest level (r = b - A x)", "avg_ms": round(spmv_ms, 4),
             "bytes_per_launch": spmv_bytes}
     if rank == 0:

@@ -13,6 +13,7 @@ struct SellView {
   int nrows = 0;
   int ncols = 0;
   int batch = 0;                   // entries per load batch (8 or 16), 0 = default
+  int pipe = 0;                    // 1 = software-pipelined row loop
 };
 
 enum : int {
@@ -41,7 +42,7 @@ struct GsView {
 hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const double* l1, const int* cf,
                             int relax_points, const double* tmp, double* u, hipStream_t st);
 int sell_batch_override();
-bool sell_pipe();
+int sell_pipe_override();
 hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, double* out, hipStream_t st);
 hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st);
 hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,

@@ -448,7 +448,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   dim3 grid(a.nblocks_pad), block(256);
   const bool cfsel = (relax_points != 0 && cf != nullptr);
   const int bsel = sell_batch_override() ? sell_batch_override() : (M.batch ? M.batch : 8);
-  const bool pipe = sell_pipe();
+  const bool pipe = sell_pipe_override() >= 0 ? sell_pipe_override() == 1 : M.pipe != 0;
 #define HVE_LP(OPV, CF, BB)                                                             \
   if (pipe) hipLaunchKernelGGL((k_sell<OPV, CF, BB, true>), grid, block, 0, s, a);     \
   else hipLaunchKernelGGL((k_sell<OPV, CF, BB, false>), grid, block, 0, s, a);
@@ -473,7 +473,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 
 // Entries per load batch in the SELL row loop: chosen per operator at upload
 // (SellView::batch); HVE_SELL_BATCH=8|16 overrides it and HVE_SELL_PIPE=1
-// selects the software-pipelined loop, for experiments.
+// (0|1) overrides the per-operator choice of the software-pipelined loop.
 int sell_batch_override() {
   static const int b = [] {
     const char* e = getenv("HVE_SELL_BATCH");
@@ -482,10 +482,10 @@ int sell_batch_override() {
   }();
   return b;
 }
-bool sell_pipe() {
-  static const bool p = [] {
+int sell_pipe_override() {
+  static const int p = [] {
     const char* e = getenv("HVE_SELL_PIPE");
-    return e && atoi(e) != 0;
+    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
   }();
   return p;
 }

@@ -33,9 +33,10 @@ struct DevSell {
   double* val = nullptr;
   int* rowmap = nullptr;
   int batch = 8;
+  int pipe = 0;
   SellView view() const {
     SellView v;
-    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.nrows = nrows; v.ncols = ncols; v.batch = batch;
+    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map

@@ -1,0 +1,49 @@
+"""HBM traffic per launch of the finest-level residual SpMV from rocprofv3 PMC
+passes over bench.py (one pass FETCH_SIZE, one pass WRITE_SIZE, each with
+--kernel-trace only, as MI355X_MICROARCH.md's HBM/rocprofv3 section asks).
+
+Corrections (MI355X_MICROARCH.md, "HBM [CDNA4]"): FETCH_SIZE is in KiB and on
+gfx950 reports half the bytes of a streaming read -- checked here for our own
+widths with the stream-read calibration kernel (4 B and 8 B per lane both read
+back exactly 0.5x); WRITE_SIZE (KiB) is exact.  traffic = 2 * FETCH + WRITE.
+
+    python scripts/pmc_traffic.py <dir with pmc_fetch/ pmc_write/> <grid> [out.json]
+
+grid = Grid_Size of the finest-level launches (256 * blocks, 16777216 at 256^3).
+"""
+import csv
+import json
+import os
+import sys
+
+
+def mean_counter(path, counter, grid, name_prefix="hve::k_sell<0,"):
+    vals = []
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter or int(r["Grid_Size"]) != grid:
+            continue
+        nm = r["Kernel_Name"].replace("void ", "")
+        if nm.startswith(name_prefix):
+            vals.append(float(r["Counter_Value"]))
+    return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def main():
+    root, grid = sys.argv[1], int(sys.argv[2])
+    fetch, nf = mean_counter(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE", grid)
+    write, nw = mean_counter(os.path.join(root, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE", grid)
+    if fetch is None or write is None:
+        raise SystemExit("no matching dispatches")
+    out = {"kernel": "k_sell<OP_RESID> finest level", "grid": grid, "dispatches": [nf, nw],
+           "fetch_kib": fetch, "write_kib": write,
+           "traffic_bytes": 2.0 * fetch * 1024 + write * 1024,
+           "correction": "traffic = 2*FETCH_SIZE + WRITE_SIZE (KiB->B); FETCH x2 per MI355X_MICROARCH.md, "
+                         "checked with the 4/8-B stream calibration kernel"}
+    print(json.dumps(out, indent=1))
+    if len(sys.argv) > 3:
+        with open(sys.argv[3], "w") as f:
+            json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
