@@ -43,6 +43,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const
                             int relax_points, const double* tmp, double* u, hipStream_t st);
 int sell_batch_override();
 int sell_pipe_override();
+bool sell_nt();
 hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, double* out, hipStream_t st);
 hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st);
 hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,

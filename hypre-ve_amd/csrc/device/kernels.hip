@@ -74,34 +74,43 @@ struct SpArgs {
 // chains in flight per lane (a lane-per-row loop with one load pair per step is
 // latency-bound on the long rows of the Galerkin levels) without changing the
 // order or rounding of the row sum.
-template <int B>
+// Matrix stream loads: read once per sweep, so with NT they carry the
+// non-temporal hint and do not evict the x-vector window that the row
+// gathers re-read from L2.
+template <bool NT, typename T>
+__device__ __forceinline__ T mload(const T* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
+template <int B, bool NT>
 __device__ __forceinline__ void sell_load(const int* __restrict__ cp, const double* __restrict__ vp, int k, int width,
                                           int (&c)[B], double (&a)[B]) {
 #pragma unroll
   for (int q = 0; q < B; ++q) {
     const bool in = (k + q) < width;
-    c[q] = in ? cp[(k + q) * kWave] : -1;
-    a[q] = in ? vp[(k + q) * kWave] : 0.0;
+    c[q] = in ? mload<NT>(cp + (k + q) * kWave) : -1;
+    a[q] = in ? mload<NT>(vp + (k + q) * kWave) : 0.0;
   }
 }
 
 // Software-pipelined form: the column/value loads of batch k+1 are issued
 // between the x gathers and the adds of batch k, so a wave keeps two batches
 // of loads in flight (counted vmcnt) instead of draining at every batch.
-template <bool SUB, int B>
+template <bool SUB, int B, bool NT>
 __device__ __forceinline__ double sell_row_pipe(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
                                                 int width, const double* __restrict__ x, double t) {
   if (k0 >= width) return t;
   int c[B];
   double a[B];
-  sell_load<B>(cp, vp, k0, width, c, a);
+  sell_load<B, NT>(cp, vp, k0, width, c, a);
   for (int k = k0; k < width; k += B) {
     double xv[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) xv[q] = c[q] >= 0 ? x[c[q]] : 0.0;
     int cn[B];
     double an[B];
-    sell_load<B>(cp, vp, k + B, width, cn, an);
+    sell_load<B, NT>(cp, vp, k + B, width, cn, an);
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       if (c[q] >= 0) {
@@ -115,18 +124,18 @@ __device__ __forceinline__ double sell_row_pipe(const int* __restrict__ cp, cons
   return t;
 }
 
-template <bool SUB, int B, bool PIPE>
+template <bool SUB, int B, bool PIPE, bool NT>
 __device__ __forceinline__ double sell_row(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
                                            int width, const double* __restrict__ x, double t) {
-  if (PIPE) return sell_row_pipe<SUB, B>(cp, vp, k0, width, x, t);
+  if (PIPE) return sell_row_pipe<SUB, B, NT>(cp, vp, k0, width, x, t);
   for (int k = k0; k < width; k += B) {
     int c[B];
     double a[B], xv[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       const bool in = (k + q) < width;
-      c[q] = in ? cp[(k + q) * kWave] : -1;
-      a[q] = in ? vp[(k + q) * kWave] : 0.0;
+      c[q] = in ? mload<NT>(cp + (k + q) * kWave) : -1;
+      a[q] = in ? mload<NT>(vp + (k + q) * kWave) : 0.0;
     }
 #pragma unroll
     for (int q = 0; q < B; ++q) xv[q] = c[q] >= 0 ? x[c[q]] : 0.0;
@@ -141,7 +150,7 @@ __device__ __forceinline__ double sell_row(const int* __restrict__ cp, const dou
   return t;
 }
 
-template <int OP, bool CFSEL, int B, bool PIPE>
+template <int OP, bool CFSEL, int B, bool PIPE, bool NT>
 __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
   const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
   const int row = lb * 256 + threadIdx.x;
@@ -162,25 +171,25 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
   }
 
   if (OP == OP_RESID || OP == OP_L1JAC || OP == OP_RESID_L1JAC) {
-    const double t = sell_row<true, B, PIPE>(cp, vp, 0, width, p.x, p.b[g]);
+    const double t = sell_row<true, B, PIPE, NT>(cp, vp, 0, width, p.x, p.b[g]);
     if (OP == OP_RESID_L1JAC) {
       p.y[g] = t;
       p.y2[g] = p.x[g] + t / p.l1[g];
     } else if (OP == OP_RESID) p.y[g] = t;
     else p.y[g] = p.x[g] + t / p.l1[g];
   } else if (OP == OP_L1JAC_W) {
-    const double t = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, -p.b[g]);
+    const double t = sell_row<false, B, PIPE, NT>(cp, vp, 0, width, p.x, -p.b[g]);
     const double v = (-p.w) * t;
     p.y[g] = p.x[g] + v / p.l1[g];
   } else if (OP == OP_MATVEC || OP == OP_RESTRICT) {
-    p.y[g] = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, 0.0);
+    p.y[g] = sell_row<false, B, PIPE, NT>(cp, vp, 0, width, p.x, 0.0);
   } else if (OP == OP_PROLONG) {
-    p.y[g] = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, p.y[g]);
+    p.y[g] = sell_row<false, B, PIPE, NT>(cp, vp, 0, width, p.x, p.y[g]);
   } else if (OP == OP_JAC) {
     const double d = vp[0];  // diagonal stored first
     const double uo = p.x[g];
     if (d == 0.0) { p.y[g] = uo; return; }
-    const double t = sell_row<true, B, PIPE>(cp, vp, 1, width, p.x, p.b[g]);
+    const double t = sell_row<true, B, PIPE, NT>(cp, vp, 1, width, p.x, p.b[g]);
     double u = uo * (1.0 - p.w);
     u += p.w * t / d;
     p.y[g] = u;
@@ -193,8 +202,8 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     else if (temp == -1.0) t = neg ? p.b[g] : -p.b[g];
     else if (temp == 1.0) t = neg ? -p.b[g] : p.b[g];
     else t = neg ? -p.b[g] * temp : p.b[g] * temp;
-    if (neg) t = sell_row<true, B, PIPE>(cp, vp, 0, width, p.x, t);
-    else t = sell_row<false, B, PIPE>(cp, vp, 0, width, p.x, t);
+    if (neg) t = sell_row<true, B, PIPE, NT>(cp, vp, 0, width, p.x, t);
+    else t = sell_row<false, B, PIPE, NT>(cp, vp, 0, width, p.x, t);
     p.y[g] = (alpha == 1.0 || neg) ? t : alpha * t;
   }
 }
@@ -449,9 +458,13 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   const bool cfsel = (relax_points != 0 && cf != nullptr);
   const int bsel = sell_batch_override() ? sell_batch_override() : (M.batch ? M.batch : 8);
   const bool pipe = sell_pipe_override() >= 0 ? sell_pipe_override() == 1 : M.pipe != 0;
-#define HVE_LP(OPV, CF, BB)                                                             \
-  if (pipe) hipLaunchKernelGGL((k_sell<OPV, CF, BB, true>), grid, block, 0, s, a);     \
-  else hipLaunchKernelGGL((k_sell<OPV, CF, BB, false>), grid, block, 0, s, a);
+  const bool nt = sell_nt();
+#define HVE_LN(OPV, CF, BB, PP)                                                          \
+  if (nt) hipLaunchKernelGGL((k_sell<OPV, CF, BB, PP, true>), grid, block, 0, s, a);    \
+  else hipLaunchKernelGGL((k_sell<OPV, CF, BB, PP, false>), grid, block, 0, s, a);
+#define HVE_LP(OPV, CF, BB)                  \
+  if (pipe) { HVE_LN(OPV, CF, BB, true) }   \
+  else { HVE_LN(OPV, CF, BB, false) }
 #define HVE_LB(OPV, CF)                    \
   if (bsel == 16) { HVE_LP(OPV, CF, 16) } \
   else { HVE_LP(OPV, CF, 8) }
@@ -468,6 +481,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_L
 #undef HVE_LB
 #undef HVE_LP
+#undef HVE_LN
   return hipGetLastError();
 }
 
@@ -481,6 +495,13 @@ int sell_batch_override() {
     return (v == 8 || v == 16) ? v : 0;
   }();
   return b;
+}
+bool sell_nt() {
+  static const bool v = [] {
+    const char* e = getenv("HVE_SELL_NT");
+    return e ? atoi(e) != 0 : false;
+  }();
+  return v;
 }
 int sell_pipe_override() {
   static const int p = [] {

@@ -23,9 +23,9 @@ if [[ $WHAT == all || $WHAT == tests ]]; then
 fi
 if [[ $WHAT == all || $WHAT == sweep ]]; then
   step sweep_auto 300 python scripts/level_sweep.py --json $OUT/sweep_auto.json
-  export HVE_SELL_PIPE=1; step sweep_pipe 300 python scripts/level_sweep.py --json $OUT/sweep_pipe.json
-  export HVE_SELL_BATCH=8; step sweep_pipe_b8 300 python scripts/level_sweep.py --json $OUT/sweep_pipe_b8.json
-  unset HVE_SELL_PIPE HVE_SELL_BATCH
+  export HVE_SELL_NT=1; step sweep_nt 300 python scripts/level_sweep.py --json $OUT/sweep_nt.json
+  step bench_nt 600 python bench.py --steps 10 --warmup 2 --cpu-cycles 0
+  unset HVE_SELL_NT
   step bench 600 python bench.py --steps 10 --warmup 2 --cpu-cycles 0
 fi
 if [[ $WHAT == all || $WHAT == pmc ]]; then
