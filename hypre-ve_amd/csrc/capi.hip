@@ -424,8 +424,13 @@ HYPRE_ParCSRMatrix GenerateLaplacian27pt(HYPRE_Comm comm, HYPRE_BigInt nx, HYPRE
                                          HYPRE_Int P, HYPRE_Int Q, HYPRE_Int R, HYPRE_Int p, HYPRE_Int q,
                                          HYPRE_Int r, HYPRE_Real* value) {
   try {
-    if (P * Q * R != 1) throw std::runtime_error("GenerateLaplacian27pt: multi-rank partition not built in");
     CSR A;
+    if (P * Q * R != 1) {
+      if (!comm || comm->size != P * Q * R) throw std::runtime_error("GenerateLaplacian27pt: P*Q*R != communicator size");
+      int64_t first = 0;
+      generate_laplacian_27pt_block((int)nx, (int)ny, (int)nz, P, Q, R, p, q, r, value, A, first);
+      return wrap_matrix(comm, std::move(A), (HYPRE_BigInt)first, (HYPRE_BigInt)nx * ny * nz);
+    }
     generate_laplacian_27pt((int)nx, (int)ny, (int)nz, A);
     for (int i = 0; i < A.nrows; ++i) {
       A.a[A.i[i]] = value[0];

@@ -105,6 +105,8 @@ struct Hierarchy {
 // 7-point Laplacian on nx*ny*nz with coefficients (cx,cy,cz), single partition,
 // same row/entry ordering as GenerateLaplacian with P=Q=R=1.
 void generate_laplacian_7pt(int nx, int ny, int nz, double cx, double cy, double cz, CSR& A);
+void generate_laplacian_27pt_block(int nx, int ny, int nz, int P, int Q, int R, int p, int q, int r,
+                                   const double* value, CSR& A, int64_t& first_row);
 void generate_laplacian_27pt(int nx, int ny, int nz, CSR& A);
 // Rank (p,q,r) of a P x Q x R process grid; global column indices, sets first_row.
 void generate_laplacian_7pt_block(int nx, int ny, int nz, int P, int Q, int R, int p, int q, int r,

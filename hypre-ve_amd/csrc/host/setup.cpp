@@ -116,6 +116,68 @@ void generate_laplacian_7pt_block(int nx, int ny, int nz, int P, int Q, int R, i
   }
 }
 
+// GenerateLaplacian27pt's block (p, q, r) of a P x Q x R processor grid
+// (par_laplace_27pt.c:15): hypre_GeneratePartitioning per axis and the
+// processor-block-contiguous global numbering (global_part, par_laplace_27pt.c:78);
+// entries in the single-process order (diagonal, then the 3x3x3 box z-major),
+// global column indices.
+void generate_laplacian_27pt_block(int nx, int ny, int nz, int P, int Q, int R, int p, int q, int r,
+                                   const double* value, CSR& A, int64_t& first_row) {
+  const auto xp = gen_part(nx, P), yp = gen_part(ny, Q), zp = gen_part(nz, R);
+  auto owner = [](const std::vector<int64_t>& part, int64_t c) {
+    return (int)(std::upper_bound(part.begin(), part.end(), c) - part.begin()) - 1;
+  };
+  auto map = [&](int64_t ix, int64_t iy, int64_t iz) -> int64_t {
+    const int pp = owner(xp, ix), qq = owner(yp, iy), rr = owner(zp, iz);
+    const int64_t nxl = xp[pp + 1] - xp[pp], nyl = yp[qq + 1] - yp[qq], nzl = zp[rr + 1] - zp[rr];
+    int64_t g = zp[rr] * nx * ny + yp[qq] * nx * nzl + xp[pp] * (nyl * nzl);
+    g += ((iz - zp[rr]) * nyl + (iy - yp[qq])) * nxl + (ix - xp[pp]);
+    return g;
+  };
+  const int nxl = (int)(xp[p + 1] - xp[p]), nyl = (int)(yp[q + 1] - yp[q]), nzl = (int)(zp[r + 1] - zp[r]);
+  const int64_t nloc = (int64_t)nxl * nyl * nzl;
+  if ((int64_t)nx * ny * nz > 0x7fffffffLL) throw std::runtime_error("global grid exceeds 2^31 rows");
+  first_row = map(xp[p], yp[q], zp[r]);
+  A.resize_rows((int)nloc, (int)((int64_t)nx * ny * nz));
+  auto coord = [&](int64_t t, int64_t& ix, int64_t& iy, int64_t& iz) {
+    ix = xp[p] + t % nxl;
+    iy = yp[q] + (t / nxl) % nyl;
+    iz = zp[r] + t / ((int64_t)nxl * nyl);
+  };
+  std::vector<int> len(nloc);
+#pragma omp parallel for schedule(static)
+  for (int64_t t = 0; t < nloc; ++t) {
+    int64_t ix, iy, iz;
+    coord(t, ix, iy, iz);
+    const int cx = 1 + (ix > 0) + (ix + 1 < nx), cy = 1 + (iy > 0) + (iy + 1 < ny), cz = 1 + (iz > 0) + (iz + 1 < nz);
+    len[t] = cx * cy * cz;
+  }
+  for (int64_t t = 0; t < nloc; ++t) {
+    A.i[t + 1] = A.i[t] + len[t];
+    if (A.i[t + 1] < 0) throw std::runtime_error("nnz overflow (use more GPUs)");
+  }
+  A.j.resize(A.i[nloc]);
+  A.a.resize(A.i[nloc]);
+#pragma omp parallel for schedule(static)
+  for (int64_t t = 0; t < nloc; ++t) {
+    int64_t ix, iy, iz;
+    coord(t, ix, iy, iz);
+    int k = A.i[t];
+    A.j[k] = (int)map(ix, iy, iz);
+    A.a[k++] = value[0];
+    for (int dz = -1; dz <= 1; ++dz)
+      for (int dy = -1; dy <= 1; ++dy)
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (!dx && !dy && !dz) continue;
+          const int64_t x = ix + dx, y = iy + dy, z = iz + dz;
+          if (x >= 0 && x < nx && y >= 0 && y < ny && z >= 0 && z < nz) {
+            A.j[k] = (int)map(x, y, z);
+            A.a[k++] = value[1];
+          }
+        }
+  }
+}
+
 // parcsr_ls/par_laplace_27pt.c GenerateLaplacian27pt (P=Q=R=1): diagonal 26,
 // every neighbour in the 3x3x3 box -1, neighbours visited z-major, then y, then x.
 void generate_laplacian_27pt(int nx, int ny, int nz, CSR& A) {

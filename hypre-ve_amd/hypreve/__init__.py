@@ -260,12 +260,19 @@ class ParCSRMatrix:
         return r0.value, r1.value
 
     @classmethod
-    def laplacian27(cls, nx, ny, nz):
+    def laplacian27(cls, nx, ny, nz, comm=None, P=1, Q=1, R=1, p=0, q=0, r=0):
+        """GenerateLaplacian27pt (diagonal 26, neighbours -1); with a Comm this
+        rank's block (p, q, r) of the P x Q x R processor grid."""
         vals = np.array([26.0, -1.0], dtype=np.float64)
-        h = lib().GenerateLaplacian27pt(None, nx, ny, nz, 1, 1, 1, 0, 0, 0, _ptr(vals, C.c_double))
+        h = lib().GenerateLaplacian27pt(comm.h if comm else None, nx, ny, nz, P, Q, R, p, q, r,
+                                        _ptr(vals, C.c_double))
         if not h:
             check(lib().HYPRE_GetError() or 1, "GenerateLaplacian27pt")
-        return cls(h, nx * ny * nz)
+        M = cls(h, nx * ny * nz)
+        M.first, last = M.local_range()
+        M.n = last - M.first + 1
+        M.global_n = nx * ny * nz
+        return M
 
     @classmethod
     def from_scipy(cls, A):

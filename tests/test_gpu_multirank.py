@@ -19,8 +19,14 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _solve_1rank(hv, nx, ny, nz, kw):
-    A = hv.ParCSRMatrix.laplacian(nx, ny, nz)
+def _gen(hv, stencil, nx, ny, nz, **part):
+    if stencil == 27:
+        return hv.ParCSRMatrix.laplacian27(nx, ny, nz, **part)
+    return hv.ParCSRMatrix.laplacian(nx, ny, nz, **part)
+
+
+def _solve_1rank(hv, nx, ny, nz, kw, stencil=7):
+    A = _gen(hv, stencil, nx, ny, nz)
     amg = hv.BoomerAMG(**kw)
     amg.setup(A)
     b = hv.ParVector(A.n, np.ones(A.n))
@@ -29,14 +35,14 @@ def _solve_1rank(hv, nx, ny, nz, kw):
     return x.get(), it, rr, amg.num_levels()
 
 
-def _solve_nranks(hv, nx, ny, nz, kw, nranks, timeout=300):
+def _solve_nranks(hv, nx, ny, nz, kw, nranks, timeout=300, stencil=7):
     comms = hv.Comm.loopback(nranks)
     out, errs = [None] * nranks, [None] * nranks
 
     def worker(r):
         try:
             c = comms[r]
-            A = hv.ParCSRMatrix.laplacian(nx, ny, nz, comm=c, P=1, Q=1, R=nranks, p=0, q=0, r=r)
+            A = _gen(hv, stencil, nx, ny, nz, comm=c, P=1, Q=1, R=nranks, p=0, q=0, r=r)
             amg = hv.BoomerAMG(**kw)
             amg.setup(A)
             b = hv.ParVector(A.n, np.ones(A.n), comm=c, first=A.first, global_n=A.global_n)
@@ -74,3 +80,14 @@ def test_loopback_partitioned_solve_bitwise(hv, nranks, nx, nz, relax):
     assert all(abs(r - rr1) <= 1e-10 * rr1 for r in rrN), (rr1, rrN)
     assert x1.shape == xN.shape
     assert np.array_equal(x1, xN), f"max |diff| {np.max(np.abs(x1 - xN))}"
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_loopback_partitioned_27pt(hv, nranks):
+    """27-point operator (configs[3]'s stencil), z-slab row blocks."""
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-8, max_iter=60)
+    x1, it1, rr1, nl1 = _solve_1rank(hv, 13, 12, 15, kw, stencil=27)
+    xN, itN, rrN, nlN = _solve_nranks(hv, 13, 12, 15, kw, nranks, stencil=27)
+    assert nlN == nl1 and all(i == it1 for i in itN)
+    assert np.array_equal(x1, xN)
