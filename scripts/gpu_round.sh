@@ -24,6 +24,7 @@ if [[ $WHAT == all || $WHAT == tests ]]; then
 fi
 if [[ $WHAT == all || $WHAT == multi ]]; then
   step loopback2 600 python bench.py --loopback 2 --n 128 --steps 5 --warmup 1 --cpu-cycles 0
+  step loopback8 900 python bench.py --loopback 8 --n ${LOOPBACK_N:-128} --steps 3 --warmup 1 --cpu-cycles 0
 fi
 if [[ $WHAT == all || $WHAT == bench ]]; then
   step bench 900 python bench.py --steps 10 --warmup 2
