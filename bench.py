@@ -102,7 +102,9 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
             "kernel": "k_sell<OP_RESID> finest level (r = b - A x)", "avg_ms": round(spmv_ms, 4),
             "bytes_per_launch": spmv_bytes}
     if rank == 0:
-        log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {spmv_bytes/1e9:.3f} GB -> {achieved:.1f} GB/s")
+        import resource
+        log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {spmv_bytes/1e9:.3f} GB -> {achieved:.1f} GB/s; "
+            f"host peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6:.1f} GB")
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_cycles > 0:
