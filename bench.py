@@ -108,6 +108,9 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_cycles > 0:
+        # The reference's CPU solve path, restated in C (oracle/oracle.c, the
+        # parity checker) and run with OpenMP over rows on this host's cores,
+        # on the same hierarchy and right-hand side.  Sample sized to ~10 s.
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle_py
 
@@ -115,12 +118,19 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
         bh = np.ones(nrows)
         u = np.zeros(nrows)
         tc = time.perf_counter()
-        st = O.solve(bh, u, 1e-300, args.cpu_cycles)
+        O.solve(bh, u, 1e-300, 1)
+        t1 = time.perf_counter() - tc
+        iters = int(max(2, min(args.cpu_cycles_max, round(args.cpu_seconds / max(t1, 1e-3)))))
+        u[:] = 0.0
+        tc = time.perf_counter()
+        st = O.solve(bh, u, 1e-300, iters)
         tcpu = time.perf_counter() - tc
-        cpu = {"value": round(nrows * st["iterations"] / tcpu, 1), "unit": "DOF/s", "cores": 1, "kind": "port",
+        threads = oracle_py.num_threads()
+        cpu = {"value": round(nrows * st["iterations"] / tcpu, 1), "unit": "DOF/s", "cores": threads, "kind": "port",
                "sample": f"{st['iterations']} solve iterations (V-cycle + residual norm) of the same {n}^3 "
-                         f"hierarchy by the C oracle (oracle/oracle.c), 1 thread, {tcpu:.1f}s"}
-        log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({tcpu:.1f}s)")
+                         f"hierarchy by the C oracle (oracle/oracle.c), OpenMP {threads} threads, {tcpu:.1f}s"}
+        log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({st['iterations']} iterations, {tcpu:.1f}s, "
+            f"{threads} threads)")
     if rank != 0:
         return None
     return {
@@ -153,7 +163,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=256, help="grid edge per GPU (n^3 rows per GPU)")
-    ap.add_argument("--cpu-cycles", type=int, default=3, help="oracle V-cycles for the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-cycles", type=int, default=1, help="run the CPU baseline (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
+    ap.add_argument("--cpu-cycles-max", type=int, default=60)
     ap.add_argument("--spmv-reps", type=int, default=50)
     ap.add_argument("--loopback", type=int, default=0,
                     help="rehearsal only: N virtual ranks (threads) sharing this process's GPU")

@@ -20,6 +20,17 @@ double orc_dot(int n, const double *x, const double *y) {
   return s;
 }
 
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+int orc_num_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
 /* ---- seq_mv/csr_matvec.c:24-330 (generic, non-rownnz path) ---- */
 void orc_matvec(double alpha, const orc_csr *A, const double *x, double beta,
                 const double *b, double *y) {
@@ -28,6 +39,7 @@ void orc_matvec(double alpha, const orc_csr *A, const double *x, double beta,
   const double *Aa = A->a;
   double *xcopy = NULL;
   if (alpha == 0.0) {
+#pragma omp parallel for schedule(static) if (n > 8192)
     for (int i = 0; i < n; i++) y[i] = beta * b[i];
     return;
   }
@@ -37,6 +49,8 @@ void orc_matvec(double alpha, const orc_csr *A, const double *x, double beta,
     x = xcopy;
   }
   const double temp = beta / alpha;
+  /* rows are independent: the OpenMP split changes no row's arithmetic */
+#pragma omp parallel for schedule(static) if (n > 8192)
   for (int i = 0; i < n; i++) {
     double t;
     if (temp == 0.0) {
@@ -90,6 +104,8 @@ static void hybrid_gs(const orc_csr *A, const double *f, const int *cf, int rela
   const double *Aa = A->a;
   if (nb < 1) nb = 1;
   if (nb > 1) memcpy(tmp, u, sizeof(double) * (size_t)n);
+  /* blocks interact only through tmp: independent, as hypre's threads are */
+#pragma omp parallel for schedule(dynamic, 1) if (nb > 1)
   for (int b = 0; b < nb; b++) {
     int ns, ne;
     block_range(n, nb, b, &ns, &ne);
@@ -134,6 +150,7 @@ int orc_relax(const orc_csr *A, const double *f, const int *cf, int relax_type,
     case 0: { /* par_relax.c:139 weighted Jacobi */
       const double omw = 1.0 - relax_weight;
       memcpy(vtemp, u, sizeof(double) * (size_t)n);
+#pragma omp parallel for schedule(static) if (n > 8192)
       for (int i = 0; i < n; i++) {
         if (relax_points != 0 && cf[i] != relax_points) continue;
         const double d = Aa[Ai[i]];
@@ -150,6 +167,7 @@ int orc_relax(const orc_csr *A, const double *f, const int *cf, int relax_type,
       if (relax_points != 0) return 1; /* CF l1-Jacobi not restated */
       memcpy(vtemp, f, sizeof(double) * (size_t)n);
       orc_matvec(-relax_weight, A, u, relax_weight, vtemp, vtemp);
+#pragma omp parallel for schedule(static) if (n > 8192)
       for (int i = 0; i < n; i++) u[i] += vtemp[i] / l1[i];
       return 0;
     }
@@ -255,7 +273,21 @@ int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
       const int fine = level, coarse = level + 1;
       memset(U[coarse], 0, sizeof(double) * (size_t)amg->A[coarse].nrows);
       orc_matvec(-1.0, &amg->A[fine], U[fine], 1.0, F[fine], vtemp);
-      orc_matvecT(1.0, &amg->P[fine], vtemp, 0.0, F[coarse]);
+      if (amg->R[fine].i) {
+        /* hypre_CSRMatrixMatvecT (alpha 1, beta 0) scatters y[j] += a_ij x_i
+         * for i ascending; R = P^T with ascending rows gathers the same terms
+         * in the same order, so each F_c entry is bitwise the scatter's */
+        const orc_csr *R = &amg->R[fine];
+        double *Fc = F[coarse];
+#pragma omp parallel for schedule(static) if (R->nrows > 8192)
+        for (int j = 0; j < R->nrows; j++) {
+          double t = 0.0;
+          for (int k = R->i[j]; k < R->i[j + 1]; k++) t += R->a[k] * vtemp[R->j[k]];
+          Fc[j] = t;
+        }
+      } else {
+        orc_matvecT(1.0, &amg->P[fine], vtemp, 0.0, F[coarse]);
+      }
       ++level;
       lev_counter[level] = lev_counter[level] > amg->cycle_type ? lev_counter[level] : amg->cycle_type;
       cycle_param = (level == nl - 1) ? 3 : 1;

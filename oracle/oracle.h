@@ -41,7 +41,11 @@ typedef struct {
   int num_sweeps[4];
   double relax_weight, omega;
   int relax_order, cycle_type, num_blocks;
+  orc_csr R[ORC_MAX_LEVELS]; /* optional P[l]^T with ascending rows (i == NULL: scatter) */
 } orc_amg;
+
+/* OpenMP threads the row-parallel loops use (1 without OpenMP). */
+int orc_num_threads(void);
 
 /* seq_mv/csr_matvec.c:24 hypre_CSRMatrixMatvecOutOfPlaceHost:
  * y = alpha*A*x + beta*b (generic non-VE path, one thread). */

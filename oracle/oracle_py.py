@@ -30,7 +30,8 @@ class orc_amg(C.Structure):
                 ("coarse_n", C.c_int), ("coarse_A", C.POINTER(C.c_double)),
                 ("relax_type", C.c_int * 4), ("num_sweeps", C.c_int * 4),
                 ("relax_weight", C.c_double), ("omega", C.c_double),
-                ("relax_order", C.c_int), ("cycle_type", C.c_int), ("num_blocks", C.c_int)]
+                ("relax_order", C.c_int), ("cycle_type", C.c_int), ("num_blocks", C.c_int),
+                ("R", orc_csr * MAXL)]
 
 
 _lib = None
@@ -39,6 +40,10 @@ _lib = None
 def build():
     subprocess.run(["make", "-s"], cwd=HERE, check=True)
     return LIB
+
+
+def num_threads():
+    return lib().orc_num_threads()
 
 
 def lib():
@@ -57,6 +62,7 @@ def lib():
         L.orc_cycle.restype = C.c_int
         L.orc_amg_solve.argtypes = [C.POINTER(orc_amg), dp, dp, C.c_double, C.c_int, C.c_int, C.c_int, dp]
         L.orc_amg_solve.restype = C.c_int
+        L.orc_num_threads.restype = C.c_int
         L.orc_pcg_amg.argtypes = [C.POINTER(orc_amg), dp, dp, C.c_double, C.c_int, C.c_int, dp]
         L.orc_pcg_amg.restype = C.c_int
         L.orc_dot.argtypes = [C.c_int, dp, dp]
@@ -97,6 +103,13 @@ class OracleAMG:
             if l < nl - 1:
                 ip, jj, vv, shp = amg.level_matrix(l, 1)
                 s.P[l] = make_csr(ip, jj, vv, shp, self.keep)
+                # R = P^T, rows ascending in the fine index: the restriction
+                # becomes a row-parallel gather with the scatter's term order
+                import scipy.sparse as sp
+                R = sp.csr_matrix((vv, jj, ip), shape=shp).T.tocsr()
+                R.sort_indices()
+                s.R[l] = make_csr(R.indptr.astype(np.int32), R.indices.astype(np.int32),
+                                  R.data.astype(np.float64), R.shape, self.keep)
             cf = amg.level_vector(l, 0)
             if cf.size:
                 self.keep.append(cf)

@@ -54,3 +54,41 @@ def test_rand_stream_matches_sequential(hv, orc):
     # (seq_mv/vector.c:286); checked through the host helper exposed by the oracle.
     assert np.all((seq > 0) & (seq < 1))
     assert abs(seq[0] - (16807 * 2747 % 2147483647) / 2147483647) < 1e-17
+
+
+def test_oracle_parallel_paths_bitwise(hv, orc):
+    """The oracle's OpenMP row loops and its gather restriction (R = P^T with
+    ascending rows) reproduce the sequential csr_matvec.c:424 scatter bit for
+    bit: one V-cycle with and without the transposes, at 1 and N threads."""
+    import ctypes as C
+    import os
+    import subprocess
+    import sys
+    A = hv.ParCSRMatrix.laplacian(30, 28, 26)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4)
+    amg.setup_host(A)
+    O = orc.OracleAMG(amg)
+    rng = np.random.default_rng(5)
+    f = rng.standard_normal(A.n)
+    u0 = rng.standard_normal(A.n)
+    u_gather = u0.copy()
+    O.cycle(f, u_gather)
+    for l in range(O.s.num_levels):
+        O.s.R[l].i = C.POINTER(C.c_int)()  # NULL: fall back to the scatter
+    u_scatter = u0.copy()
+    O.cycle(f, u_scatter)
+    assert np.array_equal(u_gather, u_scatter)
+    # thread count: rerun in a child with OMP_NUM_THREADS=1 and compare digests
+    script = (
+        "import sys, numpy as np, hashlib; sys.path[:0] = %r\n"
+        "import hypreve as hv, oracle_py as orc\n"
+        "A = hv.ParCSRMatrix.laplacian(30, 28, 26)\n"
+        "amg = hv.BoomerAMG(**hv.ij_amg_defaults(0)); amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4)\n"
+        "amg.setup_host(A); O = orc.OracleAMG(amg); rng = np.random.default_rng(5)\n"
+        "f = rng.standard_normal(A.n); u = rng.standard_normal(A.n); O.cycle(f, u)\n"
+        "print(hashlib.sha256(u.tobytes()).hexdigest())\n" % (sys.path[:3],))
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    out = subprocess.run([sys.executable, "-c", script], env=env, capture_output=True, text=True, check=True)
+    import hashlib
+    assert out.stdout.strip() == hashlib.sha256(u_gather.tobytes()).hexdigest()
