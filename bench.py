@@ -48,6 +48,28 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+class heartbeat:
+    """Prints a progress line every `every` s while a long host phase (the
+    setup at 512^3 takes minutes) runs inside a ctypes call (GIL released)."""
+
+    def __init__(self, what, every=30.0):
+        import threading
+        self.what, self.every, self.t0 = what, every, time.time()
+        self.stop = threading.Event()
+        self.th = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        while not self.stop.wait(self.every):
+            log(f"[bench] {self.what}: {time.time() - self.t0:.0f}s")
+
+    def __enter__(self):
+        self.th.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+
+
 def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     """One rank's part of the bench; returns the JSON dict on rank 0."""
     import torch
@@ -64,7 +86,8 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-300, max_iter=args.warmup,
               min_iter=0)
     amg = hv.BoomerAMG(**kw)
-    amg.setup(A)
+    with heartbeat(f"rank {rank} setup"):
+        amg.setup(A)
     t_setup = time.time() - t0
     g, o, c = amg.complexities()
     if rank == 0:

@@ -1079,7 +1079,7 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
   const double out_rw = which == 0 ? 16.0 : which == 1 ? 16.0 : 8.0;  // b read + y write / y rw / y write
   if (bytes)
     *bytes = (double)M.nnz * 12.0 + (double)M.nrows * out_rw + (double)M.ncols * 8.0 + (double)(M.nslices + 1) * 4.0 +
-             (M.rowmap ? (double)M.nrows * 4.0 : 0.0);
+             (M.rowmap ? (double)M.nrows * 4.0 : 0.0) + (M.rowlen ? (double)M.nrows * 4.0 : 0.0);
   if (padded_nnz) *padded_nnz = (double)M.nnz_pad;
   API_END
 }

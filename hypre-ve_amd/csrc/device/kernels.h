@@ -4,12 +4,13 @@
 
 namespace hve {
 
-// Device view of one SELL-64 operator (see kernels.hip header comment).
+// Device view of one SELL-64 operator, padded or jagged (see kernels.hip).
 struct SellView {
   const int* slice_ptr = nullptr;  // nslices + 1 offsets (in entries)
   const int* col = nullptr;        // padded; -1 marks padding
   const double* val = nullptr;
   const int* rowmap = nullptr;     // subset row -> local row, nullptr = identity
+  const int* rowlen = nullptr;     // jagged layout (no stored padding): stored row -> length
   int nrows = 0;
   int ncols = 0;
   int batch = 0;                   // entries per load batch (8 or 16), 0 = default

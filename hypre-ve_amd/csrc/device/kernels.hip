@@ -61,6 +61,7 @@ struct SpArgs {
   const double* __restrict__ l1;  // l1 norms (or diag) for smoothers
   const int* __restrict__ cf;     // CF marker (relax_points != 0 only)
   const int* __restrict__ rowmap; // subset row -> local row (nullptr: identity)
+  const int* __restrict__ rowlen; // jagged layout: stored row -> its length
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double w;                       // relax weight / alpha
@@ -130,6 +131,54 @@ __device__ __forceinline__ double sell_row_pipe(const int* __restrict__ cp, cons
   return t;
 }
 
+// Jagged SELL-64 (host: build_sell_jagged_host).  A slice's rows are sorted by
+// descending length, so entry k exists exactly for lanes 0..cnt_k-1, with
+// cnt_k = popcount(ballot(k < rowlen)), and is stored at slice base +
+// cnt_0 + ... + cnt_{k-1} + lane: no padding in memory.  The running offset
+// P is wave-uniform (SGPR).  blen is the lane's true length (it must take part
+// in every ballot, even when the lane's row is not relaxed), llen the length
+// it loads (0 for a skipped row).
+template <int B, bool NT>
+__device__ __forceinline__ void jag_load(const int* __restrict__ cp, const double* __restrict__ vp, int& P, int k,
+                                         int blen, int llen, int (&c)[B], double (&a)[B]) {
+#pragma unroll
+  for (int q = 0; q < B; ++q) {
+    const bool in = (k + q) < llen;
+    c[q] = in ? mload<NT>(cp + P) : -1;
+    a[q] = in ? mload<NT>(vp + P) : 0.0;
+    P += __popcll(__ballot((k + q) < blen));
+  }
+}
+
+template <bool SUB, int B, bool NT>
+__device__ __forceinline__ double jag_row(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
+                                          int width, int blen, int llen, const double* __restrict__ x, double t) {
+  int P = 0;
+  for (int k = 0; k < k0; ++k) P += __popcll(__ballot(k < blen));
+  if (k0 >= width) return t;
+  int c[B];
+  double a[B];
+  jag_load<B, NT>(cp, vp, P, k0, blen, llen, c, a);
+  for (int k = k0; k < width; k += B) {
+    double xv[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) xv[q] = c[q] >= 0 ? x[c[q]] : 0.0;
+    int cn[B];
+    double an[B];
+    jag_load<B, NT>(cp, vp, P, k + B, blen, llen, cn, an);
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      if (c[q] >= 0) {
+        if (SUB) t -= a[q] * xv[q];
+        else t += a[q] * xv[q];
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) { c[q] = cn[q]; a[q] = an[q]; }
+  }
+  return t;
+}
+
 template <bool SUB, int B, bool PIPE, bool NT>
 __device__ __forceinline__ double sell_row(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
                                            int width, const double* __restrict__ x, double t) {
@@ -156,46 +205,75 @@ __device__ __forceinline__ double sell_row(const int* __restrict__ cp, const dou
   return t;
 }
 
-template <int OP, bool CFSEL, int B, bool PIPE, bool NT>
+// Row sum of the current lane's row: plain SELL-64 (lane-strided, padded) or
+// jagged SELL-64 (JAG), both in stored (reference) entry order.
+template <bool SUB, int B, bool PIPE, bool NT, bool JAG>
+__device__ __forceinline__ double row_sum(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
+                                          int width, int blen, int llen, const double* __restrict__ x, double t) {
+  if (JAG) return jag_row<SUB, B, NT>(cp, vp, k0, width, blen, llen, x, t);
+  return sell_row<SUB, B, PIPE, NT>(cp, vp, k0, width, x, t);
+}
+
+template <int OP, bool CFSEL, int B, bool PIPE, bool NT, bool JAG>
 __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
   const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
   const int row = lb * 256 + threadIdx.x;
+  // Lanes past the last row hold no entries (rowlen 0), so they may leave
+  // before the ballots of the jagged layout.
   if (row >= p.nrows) return;
   const int lane = threadIdx.x & (kWave - 1);
   const int slice = row >> 6;
   const int g = p.rowmap ? mload<NT>(p.rowmap + row) : row;  // row of the local vectors
   const int beg = p.slice_ptr[slice];
-  const int width = (p.slice_ptr[slice + 1] - beg) >> 6;
+  int width, blen = 0;
+  if (JAG) {
+    blen = mload<NT>(p.rowlen + row);
+    width = __builtin_amdgcn_readfirstlane(blen);  // lane 0 holds the slice's longest row
+  } else {
+    width = (p.slice_ptr[slice + 1] - beg) >> 6;
+  }
   const int* __restrict__ cp = p.col + beg + lane;
   const double* __restrict__ vp = p.val + beg + lane;
 
-  if (CFSEL) {
-    if (p.cf[g] != p.relax_points) {
-      if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) sstore<NT>(p.y + g, p.x[g]);
-      return;
-    }
+  bool skip = false;
+  if (CFSEL) skip = p.cf[g] != p.relax_points;
+  if (CFSEL && !JAG && skip) {
+    if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) sstore<NT>(p.y + g, p.x[g]);
+    return;
   }
+  const int llen = skip ? 0 : blen;
+#define HVE_ROW(SUBV, K0, T0) row_sum<SUBV, B, PIPE, NT, JAG>(cp, vp, K0, width, blen, llen, p.x, T0)
 
   if (OP == OP_RESID || OP == OP_L1JAC || OP == OP_RESID_L1JAC) {
-    const double t = sell_row<true, B, PIPE, NT>(cp, vp, 0, width, p.x, mload<NT>(p.b + g));
+    const double t = HVE_ROW(true, 0, skip ? 0.0 : mload<NT>(p.b + g));
+    if (skip) {
+      if (OP == OP_L1JAC) sstore<NT>(p.y + g, p.x[g]);
+      return;
+    }
     if (OP == OP_RESID_L1JAC) {
       sstore<NT>(p.y + g, t);
       sstore<NT>(p.y2 + g, p.x[g] + t / mload<NT>(p.l1 + g));
     } else if (OP == OP_RESID) sstore<NT>(p.y + g, t);
     else sstore<NT>(p.y + g, p.x[g] + t / mload<NT>(p.l1 + g));
   } else if (OP == OP_L1JAC_W) {
-    const double t = sell_row<false, B, PIPE, NT>(cp, vp, 0, width, p.x, -mload<NT>(p.b + g));
+    const double t = HVE_ROW(false, 0, skip ? 0.0 : -mload<NT>(p.b + g));
+    if (skip) { sstore<NT>(p.y + g, p.x[g]); return; }
     const double v = (-p.w) * t;
     sstore<NT>(p.y + g, p.x[g] + v / mload<NT>(p.l1 + g));
   } else if (OP == OP_MATVEC || OP == OP_RESTRICT) {
-    sstore<NT>(p.y + g, sell_row<false, B, PIPE, NT>(cp, vp, 0, width, p.x, 0.0));
+    const double t = HVE_ROW(false, 0, 0.0);
+    if (!skip) sstore<NT>(p.y + g, t);
   } else if (OP == OP_PROLONG) {
-    sstore<NT>(p.y + g, sell_row<false, B, PIPE, NT>(cp, vp, 0, width, p.x, mload<NT>(p.y + g)));
+    const double t = HVE_ROW(false, 0, skip ? 0.0 : mload<NT>(p.y + g));
+    if (!skip) sstore<NT>(p.y + g, t);
   } else if (OP == OP_JAC) {
-    const double d = vp[0];  // diagonal stored first
+    // diagonal stored first (entry 0 sits at offset lane in both layouts)
+    const double d = (JAG ? (llen > 0) : !skip) ? vp[0] : 0.0;
     const double uo = p.x[g];
-    if (d == 0.0) { sstore<NT>(p.y + g, uo); return; }
-    const double t = sell_row<true, B, PIPE, NT>(cp, vp, 1, width, p.x, mload<NT>(p.b + g));
+    const bool nod = skip || d == 0.0;
+    // every lane runs the loop (ballots); lanes without a usable diagonal load nothing
+    const double t = HVE_ROW(true, 1, nod ? 0.0 : mload<NT>(p.b + g));
+    if (nod) { sstore<NT>(p.y + g, uo); return; }
     double u = uo * (1.0 - p.w);
     u += p.w * t / d;
     sstore<NT>(p.y + g, u);
@@ -208,10 +286,11 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     else if (temp == -1.0) t = neg ? mload<NT>(p.b + g) : -mload<NT>(p.b + g);
     else if (temp == 1.0) t = neg ? -mload<NT>(p.b + g) : mload<NT>(p.b + g);
     else t = neg ? -mload<NT>(p.b + g) * temp : mload<NT>(p.b + g) * temp;
-    if (neg) t = sell_row<true, B, PIPE, NT>(cp, vp, 0, width, p.x, t);
-    else t = sell_row<false, B, PIPE, NT>(cp, vp, 0, width, p.x, t);
-    sstore<NT>(p.y + g, (alpha == 1.0 || neg) ? t : alpha * t);
+    if (neg) t = HVE_ROW(true, 0, t);
+    else t = HVE_ROW(false, 0, t);
+    if (!skip) sstore<NT>(p.y + g, (alpha == 1.0 || neg) ? t : alpha * t);
   }
+#undef HVE_ROW
 }
 
 // ---------------------------------------------------------------------------
@@ -457,6 +536,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   if (M.nrows <= 0) return hipSuccess;
   SpArgs a;
   a.rowmap = M.rowmap;
+  a.rowlen = M.rowlen;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
   a.nblocks_pad = blocks_pad8(M.nrows);
   a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.y2 = y2; a.w = w; a.temp = temp; a.relax_points = relax_points;
@@ -465,12 +545,14 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   const int bsel = sell_batch_override() ? sell_batch_override() : (M.batch ? M.batch : 8);
   const bool pipe = sell_pipe_override() >= 0 ? sell_pipe_override() == 1 : M.pipe != 0;
   const bool nt = sell_nt();
-#define HVE_LN(OPV, CF, BB, PP)                                                          \
-  if (nt) hipLaunchKernelGGL((k_sell<OPV, CF, BB, PP, true>), grid, block, 0, s, a);    \
-  else hipLaunchKernelGGL((k_sell<OPV, CF, BB, PP, false>), grid, block, 0, s, a);
-#define HVE_LP(OPV, CF, BB)                  \
-  if (pipe) { HVE_LN(OPV, CF, BB, true) }   \
-  else { HVE_LN(OPV, CF, BB, false) }
+  const bool jag = M.rowlen != nullptr;
+#define HVE_LN(OPV, CF, BB, PP, JG)                                                          \
+  if (nt) hipLaunchKernelGGL((k_sell<OPV, CF, BB, PP, true, JG>), grid, block, 0, s, a);    \
+  else hipLaunchKernelGGL((k_sell<OPV, CF, BB, PP, false, JG>), grid, block, 0, s, a);
+#define HVE_LP(OPV, CF, BB)                         \
+  if (jag) { HVE_LN(OPV, CF, BB, true, true) }     \
+  else if (pipe) { HVE_LN(OPV, CF, BB, true, false) } \
+  else { HVE_LN(OPV, CF, BB, false, false) }
 #define HVE_LB(OPV, CF)                    \
   if (bsel == 16) { HVE_LP(OPV, CF, 16) } \
   else { HVE_LP(OPV, CF, 8) }

@@ -52,9 +52,26 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h) {
     const char* e = getenv("HVE_SELL_SIGMA");
     return e ? atoi(e) : 0;
   }();
-  const int64_t pad0 = sigma_env > 0 ? sell_padded_nnz(A, 0) : 0;
-  const int sigma = (sigma_env > 0 && A.nnz() > 0 && pad0 > A.nnz() + A.nnz() / 20) ? sigma_env : 0;
-  build_sell_host(A, sigma, perm, sp, col, val);
+  // Jagged layout (no stored padding) for large operators with long rows and
+  // more than 10% padding: level-1/2 Galerkin A and R = P^T.  Measured on
+  // MI355X (256^3, PMIS/ext+i): R_0 -16%, A_1 -15%, R_1 -14%, A_2 -4%; but
+  // P (<= 4 entries a row: the 8 B/row of row map + length outweigh the
+  // padding) +14..25%, and operators below ~2^18 rows, which are latency-bound,
+  // +10..20%.  HVE_SELL_JAG=0|1 forces it off / on for experiments.
+  static const int jag_env = [] {
+    const char* e = getenv("HVE_SELL_JAG");
+    return e ? atoi(e) : -1;
+  }();
+  const int64_t pad0 = A.nnz() > 0 ? sell_padded_nnz(A, 0) : 0;
+  const bool jag = jag_env >= 0 ? (jag_env != 0 && A.nnz() > 0)
+                                : (pad0 > A.nnz() + A.nnz() / 10 && A.nnz() >= 8LL * A.nrows && A.nrows >= (1 << 18));
+  std::vector<int> rl;
+  if (jag) {
+    build_sell_jagged_host(A, perm, sp, rl, col, val);
+  } else {
+    const int sigma = (sigma_env > 0 && A.nnz() > 0 && pad0 > A.nnz() + A.nnz() / 20) ? sigma_env : 0;
+    build_sell_host(A, sigma, perm, sp, col, val);
+  }
   nrows = A.nrows;
   ncols = A.ncols;
   nslices = (int)sp.size() - 1;
@@ -63,12 +80,14 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h) {
   // Long rows (Galerkin A, R = P^T) run 16 entries per load batch, short ones
   // (P: <= P_max_elmts, the finest 7-point A) 8: measured on MI355X, 16 was
   // 8% faster on level-1 A and R and 10% slower on P.
-  batch = (nslices > 0 && nnz_pad > (int64_t)nslices * 64 * 8) ? 16 : 8;
+  batch = (nslices > 0 && pad0 > (int64_t)nslices * 64 * 8) ? 16 : 8;
   // Software pipelining (next batch's loads issued before this batch's adds)
   // measured 11% faster on level-1 A, 4-7% on R and P, ~2% slower on the
   // finest 7-point A (one batch per row): on except for mid-length short rows.
+  // The jagged loop is always pipelined.
   const double avg_row = nrows > 0 ? (double)nnz / nrows : 0.0;
-  pipe = (batch == 16 || avg_row < 5.0) ? 1 : 0;
+  pipe = (jag || batch == 16 || avg_row < 5.0) ? 1 : 0;
+  if (jag) rowlen = dupload(rl.data(), rl.size());
   slice_ptr = dupload(sp.data(), sp.size());
   this->col = dupload(col.data(), col.size());
   this->val = dupload(val.data(), val.size());
@@ -87,7 +106,8 @@ void DevSell::release() {
   if (col) (void)hipFree(col);
   if (val) (void)hipFree(val);
   if (rowmap) (void)hipFree(rowmap);
-  slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr;
+  if (rowlen) (void)hipFree(rowlen);
+  slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0;
 }
 

@@ -32,17 +32,19 @@ struct DevSell {
   int* col = nullptr;
   double* val = nullptr;
   int* rowmap = nullptr;
+  int* rowlen = nullptr;  // jagged layout only
   int batch = 8;
   int pipe = 0;
   SellView view() const {
     SellView v;
-    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe;
+    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map
   void upload(const CSR& A, const std::vector<int>& rowmap = {});
   void release();
-  size_t bytes() const { return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * 12 + (rowmap ? (size_t)nrows * 4 : 0); }
+  size_t bytes() const { return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * 12 + (rowmap ? (size_t)nrows * 4 : 0) +
+                         (rowlen ? (size_t)nslices * 256 : 0); }
 };
 
 // Rows of one operator a rank applies, split by whether they read halo values.

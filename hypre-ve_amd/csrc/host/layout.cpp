@@ -69,6 +69,51 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
   if (sigma <= 0) perm.clear();
 }
 
+// Jagged SELL-64: rows sorted by descending length inside each 64-row slice
+// (stable), entry k stored only for the cnt_k lanes whose row is longer than
+// k, at slice_ptr[s] + (cnt_0 + ... + cnt_{k-1}) + lane.  No padding is
+// stored; the device recovers each offset from a wave ballot of
+// (k < rowlen[lane]).
+void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<int>& slice_ptr,
+                            std::vector<int>& rowlen, std::vector<int>& col, std::vector<double>& val) {
+  const int n = A.nrows;
+  const int ns = (n + 63) / 64;
+  sell_order(A, 64, perm);
+  slice_ptr.assign(ns + 1, 0);
+  rowlen.assign((size_t)ns * 64, 0);
+  std::vector<int64_t> sp(ns + 1, 0);
+  for (int s = 0; s < ns; ++s) {
+    int64_t t = 0;
+    const int r1 = std::min(n, (s + 1) * 64);
+    for (int r = s * 64; r < r1; ++r) t += A.i[perm[r] + 1] - A.i[perm[r]];
+    sp[s + 1] = sp[s] + t;
+  }
+  if (sp[ns] > 0x7fffffffLL) throw std::runtime_error("operator exceeds 2^31 entries on one GPU");
+  for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
+  col.assign((size_t)sp[ns], -1);
+  val.assign((size_t)sp[ns], 0.0);
+#pragma omp parallel for schedule(static)
+  for (int s = 0; s < ns; ++s) {
+    const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
+    int len[64] = {0};
+    for (int r = r0; r < r1; ++r) {
+      len[r - r0] = A.i[perm[r] + 1] - A.i[perm[r]];
+      rowlen[r] = len[r - r0];
+    }
+    size_t pos = (size_t)slice_ptr[s];
+    for (int k = 0; k < len[0]; ++k) {
+      int cnt = 0;
+      while (cnt < r1 - r0 && len[cnt] > k) ++cnt;  // lanes sorted by descending length
+      for (int l = 0; l < cnt; ++l) {
+        const int src = perm[r0 + l];
+        col[pos + l] = A.j[A.i[src] + k];
+        val[pos + l] = A.a[A.i[src] + k];
+      }
+      pos += cnt;
+    }
+  }
+}
+
 std::vector<int> hypre_block_starts(int n, int nb) {
   if (nb < 1) nb = 1;
   std::vector<int> st(nb + 1);

@@ -12,6 +12,12 @@ namespace hve {
 // and leaves perm empty.
 void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vector<int>& slice_ptr,
                      std::vector<int>& col, std::vector<double>& val);
+// Jagged SELL-64 (no stored padding): perm[i] = CSR row at stored position i
+// (rows sorted by descending length inside each slice), rowlen[i] its length
+// (nslices*64 entries, 0 past the last row), entry k of the slice's lane r at
+// slice_ptr[s] + sum_{k'<k} #{lanes with rowlen > k'} + r.
+void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<int>& slice_ptr,
+                            std::vector<int>& rowlen, std::vector<int>& col, std::vector<double>& val);
 // Padded entry count of the SELL-64 layout for a given sigma (0 = no sort).
 int64_t sell_padded_nnz(const CSR& A, int sigma);
 // Level schedule of one hybrid Gauss-Seidel sweep (par_relax.c cases 3/4/6/

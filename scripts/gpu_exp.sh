@@ -19,14 +19,16 @@ step() {  # step <name> <seconds> <cmd...>
 }
 WHAT=${1:-all}
 if [[ $WHAT == all || $WHAT == tests ]]; then
-  step pytest_gpu 600 python -m pytest tests -m gpu -x -q
+  step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 fi
 if [[ $WHAT == all || $WHAT == sweep ]]; then
+  # default layout choice against forced variants (env read by the library)
   step sweep_auto 300 python scripts/level_sweep.py --json $OUT/sweep_auto.json
-  export HVE_SELL_NT=1; step sweep_nt 300 python scripts/level_sweep.py --json $OUT/sweep_nt.json
-  step bench_nt 600 python bench.py --steps 10 --warmup 2 --cpu-cycles 0
-  unset HVE_SELL_NT
   step bench 600 python bench.py --steps 10 --warmup 2 --cpu-cycles 0
+  for v in ${SWEEP_VARIANTS:-HVE_SELL_JAG=0}; do
+    env $v python scripts/level_sweep.py --json $OUT/sweep_$v.json > $OUT/sweep_$v.log 2>&1 || exit 1
+    tail -2 $OUT/sweep_$v.log
+  done
 fi
 if [[ $WHAT == all || $WHAT == pmc ]]; then
   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --cpu-cycles 0 --spmv-reps 5

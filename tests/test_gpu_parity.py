@@ -60,6 +60,24 @@ def test_single_cycle_bitwise(gpu, orc, n3, relax, coarsen):
     assert np.array_equal(u.get(), uo)
 
 
+@pytest.mark.parametrize("relax,coarsen", [(18, 8), (0, 8), (18, 10), (7, 10)])
+def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen):
+    """relax_order 1 (C points, then F points on the way down; F then C up):
+    the CF-selective row kernels on padded and jagged operators."""
+    hv = gpu
+    A, amg, O = setup_pair(hv, orc, (26, 22, 19), coarsen_type=coarsen, relax_type=relax, relax_order=1)
+    n = A.n
+    rng = np.random.default_rng(17)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+
+
 def test_matvec_bitwise(gpu, orc):
     hv = gpu
     A, amg, O = setup_pair(hv, orc, (20, 20, 20), coarsen_type=8, relax_type=18)
