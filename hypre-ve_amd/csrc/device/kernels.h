@@ -15,6 +15,7 @@ struct SellView {
   int ncols = 0;
   int batch = 0;                   // entries per load batch (8 or 16), 0 = default
   int pipe = 0;                    // 1 = software-pipelined row loop
+  int wide = 0;                    // 1 = one workgroup per slice (k_sell_wide), padded layout only
 };
 
 enum : int {
@@ -45,6 +46,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const
 int sell_batch_override();
 int sell_pipe_override();
 bool sell_nt();
+bool sell_pw();
 hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, double* out, hipStream_t st);
 hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st);
 hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,

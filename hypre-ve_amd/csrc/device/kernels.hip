@@ -294,6 +294,225 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
 }
 
 // ---------------------------------------------------------------------------
+// Wide SELL row loop for small operators (coarse levels): one 256-thread
+// workgroup per 64-row slice.  The per-row loop above is latency-bound there
+// (few waves, each walking long rows batch after batch); here all 256 threads
+// first form the products a_ik * x_k of a chunk of the slice in parallel, with
+// every load of the chunk in flight at once, and park them in LDS; then the 64
+// lanes of wave 0 add their row's products in stored order.  Each product is
+// rounded exactly as in the row loop (no contraction) and the sums run in the
+// same order, so the result is bitwise the same.  A padding entry contributes
+// a neutral product, +0 for a subtraction and -0 for an addition, which leave
+// every value (signed zeros included) unchanged.
+// ---------------------------------------------------------------------------
+template <int OP>
+__device__ __forceinline__ constexpr bool op_subtracts() {
+  return OP == OP_RESID || OP == OP_L1JAC || OP == OP_RESID_L1JAC || OP == OP_JAC;
+}
+
+// Starting value of a row sum (the b / y term of each op) and the epilogue that
+// writes the row's results; shared by the workgroup- and wave-parallel loops.
+template <int OP, bool NT>
+__device__ __forceinline__ double row_init(const SpArgs& p, int g) {
+  if (OP == OP_RESID || OP == OP_L1JAC || OP == OP_RESID_L1JAC || OP == OP_JAC) return mload<NT>(p.b + g);
+  if (OP == OP_L1JAC_W) return -mload<NT>(p.b + g);
+  if (OP == OP_PROLONG) return mload<NT>(p.y + g);
+  if (OP == OP_GENERAL) {
+    const double alpha = p.w, temp = p.temp;
+    const bool neg = (alpha == -1.0);
+    if (temp == 0.0) return 0.0;
+    if (temp == -1.0) return neg ? mload<NT>(p.b + g) : -mload<NT>(p.b + g);
+    if (temp == 1.0) return neg ? -mload<NT>(p.b + g) : mload<NT>(p.b + g);
+    return neg ? -mload<NT>(p.b + g) * temp : mload<NT>(p.b + g) * temp;
+  }
+  return 0.0;
+}
+
+template <int OP, bool NT>
+__device__ __forceinline__ void row_store(const SpArgs& p, int g, bool skip, double t, double uo, double d) {
+  if (skip) {
+    if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) sstore<NT>(p.y + g, p.x[g]);
+    return;
+  }
+  if (OP == OP_RESID_L1JAC) {
+    sstore<NT>(p.y + g, t);
+    sstore<NT>(p.y2 + g, p.x[g] + t / mload<NT>(p.l1 + g));
+  } else if (OP == OP_RESID) {
+    sstore<NT>(p.y + g, t);
+  } else if (OP == OP_L1JAC) {
+    sstore<NT>(p.y + g, p.x[g] + t / mload<NT>(p.l1 + g));
+  } else if (OP == OP_L1JAC_W) {
+    const double v = (-p.w) * t;
+    sstore<NT>(p.y + g, p.x[g] + v / mload<NT>(p.l1 + g));
+  } else if (OP == OP_MATVEC || OP == OP_RESTRICT || OP == OP_PROLONG) {
+    sstore<NT>(p.y + g, t);
+  } else if (OP == OP_JAC) {
+    if (d == 0.0) { sstore<NT>(p.y + g, uo); return; }
+    double u = uo * (1.0 - p.w);
+    u += p.w * t / d;
+    sstore<NT>(p.y + g, u);
+  } else if (OP == OP_GENERAL) {
+    const double alpha = p.w;
+    const bool neg = (alpha == -1.0);
+    sstore<NT>(p.y + g, (alpha == 1.0 || neg) ? t : alpha * t);
+  }
+}
+
+template <int OP, bool CFSEL, bool NT>
+__global__ void __launch_bounds__(256) k_sell_wide(SpArgs p) {
+  constexpr int KCH = 32;       // entries per row and chunk: 64 x 32 products = 16 KiB of LDS
+  constexpr int PER = KCH / 4;  // products per thread and chunk
+  __shared__ double prod[kWave * KCH];
+  const int slice = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  if (slice * kWave >= p.nrows) return;  // whole workgroup past the end
+  const int tid = threadIdx.x;
+  const int beg = p.slice_ptr[slice];
+  const int width = (p.slice_ptr[slice + 1] - beg) >> 6;
+  const bool SUB = op_subtracts<OP>();
+  // GENERAL with alpha == -1 subtracts too (csr_matvec.c's branch)
+  const bool sub = SUB || (OP == OP_GENERAL && p.w == -1.0);
+  const double neutral = sub ? 0.0 : -0.0;
+
+  // wave 0: the row owned by this lane and its starting value
+  const int row = slice * kWave + tid;
+  const bool own = tid < kWave && row < p.nrows;
+  int g = 0;
+  bool skip = false;
+  double t = 0.0, uo = 0.0, d = 0.0;
+  if (own) {
+    g = p.rowmap ? mload<NT>(p.rowmap + row) : row;
+    if (CFSEL) skip = p.cf[g] != p.relax_points;
+    t = row_init<OP, NT>(p, g);
+    if (OP == OP_JAC) {
+      uo = p.x[g];
+      d = p.val[beg + tid];  // diagonal stored first
+    }
+  }
+  const int k_first = (OP == OP_JAC) ? 1 : 0;
+  for (int k0 = 0; k0 < width; k0 += KCH) {
+    const int kc = min(KCH, width - k0);
+    const int ne = kc * kWave;
+    const int* __restrict__ cp = p.col + beg + k0 * kWave;
+    const double* __restrict__ vp = p.val + beg + k0 * kWave;
+    int c[PER];
+    double a[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = tid + 256 * j;
+      c[j] = e < ne ? mload<NT>(cp + e) : -1;
+      a[j] = e < ne ? mload<NT>(vp + e) : 0.0;
+    }
+    double xv[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) xv[j] = c[j] >= 0 ? p.x[c[j]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int e = tid + 256 * j;
+      if (e < ne) prod[e] = c[j] >= 0 ? a[j] * xv[j] : neutral;
+    }
+    __syncthreads();
+    if (tid < kWave) {
+      const int q0 = (k0 == 0) ? k_first : 0;
+      if (sub) {
+        for (int q = q0; q < kc; ++q) t -= prod[q * kWave + tid];
+      } else {
+        for (int q = q0; q < kc; ++q) t += prod[q * kWave + tid];
+      }
+    }
+    __syncthreads();
+  }
+  if (own) row_store<OP, NT>(p, g, skip, t, uo, d);
+}
+
+// ---------------------------------------------------------------------------
+// Per-wave product-parallel loop over the jagged layout (large operators).  A
+// slice's entries with k in [k0, k0+16) form one contiguous run of the jagged
+// block; the 64 lanes of the wave load that run fully coalesced, no lane idle,
+// form the products and park them in the wave's LDS; then each lane adds its
+// own row's products in stored order.  Rows are sorted by length inside the
+// slice, so entry k of lane r sits at (stored lanes of k0..k-1) + r in the run.
+// Same rounding and order as the row loop, so bitwise the same.  No workgroup
+// barrier: LDS operations of one wave complete in program order.
+// ---------------------------------------------------------------------------
+template <int OP, bool CFSEL, bool NT>
+__global__ void __launch_bounds__(256) k_sell_pw(SpArgs p) {
+  constexpr int KC = 16;  // entries per row and chunk: 64 x 16 products, 8 KiB per wave
+  __shared__ double prod[4][kWave * KC];
+  const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  const int row = lb * 256 + threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int slice = row >> 6;
+  if (slice * kWave >= p.nrows) return;  // whole wave past the end
+  double* __restrict__ lp = prod[threadIdx.x >> 6];
+  const int blen = mload<NT>(p.rowlen + row);  // 0 past the last row
+  const int width = __builtin_amdgcn_readfirstlane(blen);  // sorted: lane 0 is the longest
+  const int beg = __builtin_amdgcn_readfirstlane(p.slice_ptr[slice]);
+  const bool own = row < p.nrows;
+  const bool SUB = op_subtracts<OP>();
+  const bool sub = SUB || (OP == OP_GENERAL && p.w == -1.0);
+  int g = 0;
+  bool skip = false;
+  double t = 0.0, uo = 0.0, d = 0.0;
+  if (own) {
+    g = p.rowmap ? mload<NT>(p.rowmap + row) : row;
+    if (CFSEL) skip = p.cf[g] != p.relax_points;
+    t = row_init<OP, NT>(p, g);
+    if (OP == OP_JAC) {
+      uo = p.x[g];
+      d = blen > 0 ? p.val[beg + lane] : 0.0;  // diagonal stored first
+    }
+  }
+  const int llen = skip ? 0 : blen;
+  const int k_first = (OP == OP_JAC) ? 1 : 0;
+  const int* __restrict__ cb = p.col + beg;
+  const double* __restrict__ vb = p.val + beg;
+  int P0 = 0;
+  for (int k0 = 0; k0 < width; k0 += KC) {
+    int cnt[KC];
+    int m = 0;
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      cnt[q] = __popcll(__ballot((k0 + q) < blen));
+      m += cnt[q];
+    }
+    int c[KC];
+    double a[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const int e = lane + kWave * j;
+      const bool in = e < m;
+      c[j] = in ? mload<NT>(cb + P0 + e) : -1;
+      a[j] = in ? mload<NT>(vb + P0 + e) : 0.0;
+    }
+    double xv[KC];
+#pragma unroll
+    for (int j = 0; j < KC; ++j) xv[j] = c[j] >= 0 ? p.x[c[j]] : 0.0;
+#pragma unroll
+    for (int j = 0; j < KC; ++j) {
+      const int e = lane + kWave * j;
+      if (e < m) lp[e] = a[j] * xv[j];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    int off = 0;
+#pragma unroll
+    for (int q = 0; q < KC; ++q) {
+      const int k = k0 + q;
+      if (k < llen && k >= k_first) {
+        const double pr = lp[off + lane];
+        if (sub) t -= pr;
+        else t += pr;
+      }
+      off += cnt[q];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    P0 += m;
+  }
+  if (own) row_store<OP, NT>(p, g, skip, t, uo, d);
+}
+
+// ---------------------------------------------------------------------------
 // Hybrid Gauss-Seidel sweep over a level schedule (host: build_gs_schedule).
 // One workgroup per hypre thread block [ns, ne); its levels run in order with
 // a workgroup barrier between them, the rows of a level in parallel (lane per
@@ -546,6 +765,42 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   const bool pipe = sell_pipe_override() >= 0 ? sell_pipe_override() == 1 : M.pipe != 0;
   const bool nt = sell_nt();
   const bool jag = M.rowlen != nullptr;
+  if (jag && sell_pw()) {
+#define HVE_P(OPV, CF)                                                                      \
+  if (nt) hipLaunchKernelGGL((k_sell_pw<OPV, CF, true>), grid, block, 0, s, a);            \
+  else hipLaunchKernelGGL((k_sell_pw<OPV, CF, false>), grid, block, 0, s, a);
+#define HVE_PL(OPV)                                               \
+  case OPV:                                                       \
+    if (cfsel) { HVE_P(OPV, true) } else { HVE_P(OPV, false) }   \
+    break;
+    switch (op) {
+      HVE_PL(OP_RESID) HVE_PL(OP_MATVEC) HVE_PL(OP_L1JAC) HVE_PL(OP_L1JAC_W) HVE_PL(OP_JAC)
+      HVE_PL(OP_PROLONG) HVE_PL(OP_RESTRICT) HVE_PL(OP_GENERAL) HVE_PL(OP_RESID_L1JAC)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_PL
+#undef HVE_P
+    return hipGetLastError();
+  }
+  if (M.wide && !jag) {
+    a.nblocks_pad = ((M.nrows + 63) / 64 + 7) / 8 * 8;  // one workgroup per slice
+    const dim3 wgrid(a.nblocks_pad);
+#define HVE_W(OPV, CF)                                                                              \
+  if (nt) hipLaunchKernelGGL((k_sell_wide<OPV, CF, true>), wgrid, block, 0, s, a);                 \
+  else hipLaunchKernelGGL((k_sell_wide<OPV, CF, false>), wgrid, block, 0, s, a);
+#define HVE_WL(OPV)                                 \
+  case OPV:                                         \
+    if (cfsel) { HVE_W(OPV, true) } else { HVE_W(OPV, false) } \
+    break;
+    switch (op) {
+      HVE_WL(OP_RESID) HVE_WL(OP_MATVEC) HVE_WL(OP_L1JAC) HVE_WL(OP_L1JAC_W) HVE_WL(OP_JAC)
+      HVE_WL(OP_PROLONG) HVE_WL(OP_RESTRICT) HVE_WL(OP_GENERAL) HVE_WL(OP_RESID_L1JAC)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_WL
+#undef HVE_W
+    return hipGetLastError();
+  }
 #define HVE_LN(OPV, CF, BB, PP, JG)                                                          \
   if (nt) hipLaunchKernelGGL((k_sell<OPV, CF, BB, PP, true, JG>), grid, block, 0, s, a);    \
   else hipLaunchKernelGGL((k_sell<OPV, CF, BB, PP, false, JG>), grid, block, 0, s, a);
@@ -591,6 +846,15 @@ bool sell_nt() {
   static const bool v = [] {
     const char* e = getenv("HVE_SELL_NT");
     return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
+// Jagged operators: per-wave product-parallel loop (k_sell_pw) instead of the
+// lane-per-row loop; HVE_SELL_PW=0|1.
+bool sell_pw() {
+  static const bool v = [] {
+    const char* e = getenv("HVE_SELL_PW");
+    return e ? atoi(e) != 0 : false;
   }();
   return v;
 }

@@ -35,9 +35,10 @@ struct DevSell {
   int* rowlen = nullptr;  // jagged layout only
   int batch = 8;
   int pipe = 0;
+  int wide = 0;
   SellView view() const {
     SellView v;
-    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe;
+    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map
