@@ -694,6 +694,12 @@ HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver s, HYPRE_Int nb) {
   s->user_num_blocks = nb >= 1;
   return 0;
 }
+HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(policy >= 0 && policy <= 5, 2);
+  s->prm.sell_policy = policy;
+  return 0;
+}
 HYPRE_Int hypreve_BoomerAMGSetUseGraph(HYPRE_Solver s, HYPRE_Int g) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   s->use_graph = g != 0;

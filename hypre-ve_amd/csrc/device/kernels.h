@@ -16,11 +16,16 @@ struct SellView {
   int batch = 0;                   // entries per load batch (8 or 16), 0 = default
   int pipe = 0;                    // 1 = software-pipelined row loop
   int wide = 0;                    // 1 = one workgroup per slice (k_sell_wide), padded layout only
+  int pw = 0;                      // 1 = wave product-parallel loop (k_sell_pw), jagged layout only
+  const unsigned short* col16 = nullptr;  // dictionary layout (k_sell_dict): local columns
+  const int* dict_ptr = nullptr;
+  const int* dict = nullptr;
+  int dmax = 0;                    // dictionary layout: largest slice dictionary (LDS doubles)
 };
 
 enum : int {
   K_RESID = 0, K_MATVEC = 1, K_L1JAC = 2, K_L1JAC_W = 3, K_JAC = 4,
-  K_PROLONG = 5, K_RESTRICT = 6, K_GENERAL = 7, K_RESID_L1JAC = 8,
+  K_PROLONG = 5, K_RESTRICT = 6, K_GENERAL = 7, K_RESID_L1JAC = 8, K_RESTRICT_ZG = 9,
 };
 
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,

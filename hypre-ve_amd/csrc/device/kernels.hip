@@ -48,6 +48,8 @@ enum SpOp : int {
   OP_GENERAL = 7,     // y = alpha*A*x + beta*b, hypre's branch structure
   OP_RESID_L1JAC = 8, // y = b - A x and y2 = x + y/l1 (solve-loop residual fused with
                       // the next cycle's first l1-Jacobi sweep: the same row sum)
+  OP_RESTRICT_ZG = 9, // fc = R v and y2 = 0 + fc/l1: the restriction fused with the coarse
+                      // level's first l1-Jacobi sweep from a zero guess (k_zero_guess op 0)
 };
 
 struct SpArgs {
@@ -62,6 +64,9 @@ struct SpArgs {
   const int* __restrict__ cf;     // CF marker (relax_points != 0 only)
   const int* __restrict__ rowmap; // subset row -> local row (nullptr: identity)
   const int* __restrict__ rowlen; // jagged layout: stored row -> its length
+  const unsigned short* __restrict__ col16;  // dictionary layout: local column of each entry
+  const int* __restrict__ dict_ptr;          // dictionary layout: per-slice range of dict
+  const int* __restrict__ dict;              // dictionary layout: distinct columns, ascending
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double w;                       // relax weight / alpha
@@ -260,9 +265,12 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     if (skip) { sstore<NT>(p.y + g, p.x[g]); return; }
     const double v = (-p.w) * t;
     sstore<NT>(p.y + g, p.x[g] + v / mload<NT>(p.l1 + g));
-  } else if (OP == OP_MATVEC || OP == OP_RESTRICT) {
+  } else if (OP == OP_MATVEC || OP == OP_RESTRICT || OP == OP_RESTRICT_ZG) {
     const double t = HVE_ROW(false, 0, 0.0);
-    if (!skip) sstore<NT>(p.y + g, t);
+    if (!skip) {
+      sstore<NT>(p.y + g, t);
+      if (OP == OP_RESTRICT_ZG) sstore<NT>(p.y2 + g, 0.0 + t / mload<NT>(p.l1 + g));
+    }
   } else if (OP == OP_PROLONG) {
     const double t = HVE_ROW(false, 0, skip ? 0.0 : mload<NT>(p.y + g));
     if (!skip) sstore<NT>(p.y + g, t);
@@ -346,6 +354,9 @@ __device__ __forceinline__ void row_store(const SpArgs& p, int g, bool skip, dou
     sstore<NT>(p.y + g, p.x[g] + v / mload<NT>(p.l1 + g));
   } else if (OP == OP_MATVEC || OP == OP_RESTRICT || OP == OP_PROLONG) {
     sstore<NT>(p.y + g, t);
+  } else if (OP == OP_RESTRICT_ZG) {
+    sstore<NT>(p.y + g, t);
+    sstore<NT>(p.y2 + g, 0.0 + t / mload<NT>(p.l1 + g));
   } else if (OP == OP_JAC) {
     if (d == 0.0) { sstore<NT>(p.y + g, uo); return; }
     double u = uo * (1.0 - p.w);
@@ -508,6 +519,103 @@ __global__ void __launch_bounds__(256) k_sell_pw(SpArgs p) {
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_wave_barrier();
     P0 += m;
+  }
+  if (own) row_store<OP, NT>(p, g, skip, t, uo, d);
+}
+
+// ---------------------------------------------------------------------------
+// Jagged SELL-64 with an LDS x-tile (host: build_sell_dict_host).  One
+// wavefront per slice.  The slice's distinct columns, listed ascending once,
+// are gathered from x into LDS first: a sorted list of short runs, so lanes
+// share lines and each x value is fetched once per slice instead of once per
+// entry.  Then the jagged row loop (sorted rows, offsets from wave ballots)
+// reads 2-byte local columns and takes x from LDS.  Same entries, same order,
+// same rounding as every other loop: bitwise the same.
+// ---------------------------------------------------------------------------
+template <int B, bool NT>
+__device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp, const double* __restrict__ vp, int& P,
+                                          int k, int blen, int llen, int (&c)[B], double (&a)[B]) {
+#pragma unroll
+  for (int q = 0; q < B; ++q) {
+    const bool in = (k + q) < llen;
+    c[q] = in ? (int)mload<NT>(cp + P) : -1;
+    a[q] = in ? mload<NT>(vp + P) : 0.0;
+    P += __popcll(__ballot((k + q) < blen));
+  }
+}
+
+template <int OP, bool CFSEL, int B, bool NT>
+__global__ void __launch_bounds__(64) k_sell_dict(SpArgs p) {
+  extern __shared__ double xl[];
+  const int slice = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  if (slice * kWave >= p.nrows) return;  // the (single-wave) workgroup is past the end
+  const int lane = threadIdx.x;
+  const int row = slice * kWave + lane;
+  // 1. x-tile: x[dict[d0 .. d1)] -> LDS, 8 gathers in flight per lane
+  {
+    const int d0 = p.dict_ptr[slice], m = p.dict_ptr[slice + 1] - d0;
+    for (int j0 = 0; j0 < m; j0 += 8 * kWave) {
+      int idx[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int j = j0 + i * kWave + lane;
+        idx[i] = j < m ? mload<NT>(p.dict + d0 + j) : -1;
+      }
+      double v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = idx[i] >= 0 ? p.x[idx[i]] : 0.0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int j = j0 + i * kWave + lane;
+        if (j < m) xl[j] = v[i];
+      }
+    }
+  }
+  __syncthreads();
+  // 2. jagged row loop over local columns
+  const int blen = mload<NT>(p.rowlen + row);  // 0 past the last row
+  const int width = __builtin_amdgcn_readfirstlane(blen);  // sorted: lane 0 is the longest
+  const int beg = p.slice_ptr[slice];
+  const bool own = row < p.nrows;
+  const bool SUB = op_subtracts<OP>();
+  const bool sub = SUB || (OP == OP_GENERAL && p.w == -1.0);
+  int g = 0;
+  bool skip = false;
+  double t = 0.0, uo = 0.0, d = 0.0;
+  if (own) {
+    g = p.rowmap ? mload<NT>(p.rowmap + row) : row;
+    if (CFSEL) skip = p.cf[g] != p.relax_points;
+    t = row_init<OP, NT>(p, g);
+    if (OP == OP_JAC) {
+      uo = p.x[g];
+      d = blen > 0 ? p.val[beg + lane] : 0.0;  // diagonal stored first
+    }
+  }
+  const int llen = skip ? 0 : blen;
+  const int k0 = (OP == OP_JAC) ? 1 : 0;
+  const unsigned short* __restrict__ cp = p.col16 + beg + lane;
+  const double* __restrict__ vp = p.val + beg + lane;
+  int P = 0;
+  for (int k = 0; k < k0; ++k) P += __popcll(__ballot(k < blen));
+  if (k0 < width) {
+    int c[B];
+    double a[B];
+    dict_load<B, NT>(cp, vp, P, k0, blen, llen, c, a);
+    for (int k = k0; k < width; k += B) {
+      int cn[B];
+      double an[B];
+      dict_load<B, NT>(cp, vp, P, k + B, blen, llen, cn, an);
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        if (c[q] >= 0) {
+          const double pr = a[q] * xl[c[q]];
+          if (sub) t -= pr;
+          else t += pr;
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < B; ++q) { c[q] = cn[q]; a[q] = an[q]; }
+    }
   }
   if (own) row_store<OP, NT>(p, g, skip, t, uo, d);
 }
@@ -756,6 +864,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   SpArgs a;
   a.rowmap = M.rowmap;
   a.rowlen = M.rowlen;
+  a.col16 = M.col16;
+  a.dict_ptr = M.dict_ptr;
+  a.dict = M.dict;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
   a.nblocks_pad = blocks_pad8(M.nrows);
   a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.y2 = y2; a.w = w; a.temp = temp; a.relax_points = relax_points;
@@ -765,7 +876,30 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   const bool pipe = sell_pipe_override() >= 0 ? sell_pipe_override() == 1 : M.pipe != 0;
   const bool nt = sell_nt();
   const bool jag = M.rowlen != nullptr;
-  if (jag && sell_pw()) {
+  if (M.col16) {  // dictionary layout: one wave per slice, x-tile in LDS
+    a.nblocks_pad = ((M.nrows + 63) / 64 + 7) / 8 * 8;
+    const dim3 dgrid(a.nblocks_pad), dblock(64);
+    const size_t lds = (size_t)M.dmax * sizeof(double);
+#define HVE_D(OPV, CF, BB)                                                                      \
+  if (nt) hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, true>), dgrid, dblock, lds, s, a);      \
+  else hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, false>), dgrid, dblock, lds, s, a);
+#define HVE_DB(OPV, CF) \
+  if (bsel == 16) { HVE_D(OPV, CF, 16) } else { HVE_D(OPV, CF, 8) }
+#define HVE_DL(OPV)                                                 \
+  case OPV:                                                         \
+    if (cfsel) { HVE_DB(OPV, true) } else { HVE_DB(OPV, false) }   \
+    break;
+    switch (op) {
+      HVE_DL(OP_RESID) HVE_DL(OP_MATVEC) HVE_DL(OP_L1JAC) HVE_DL(OP_L1JAC_W) HVE_DL(OP_JAC)
+      HVE_DL(OP_PROLONG) HVE_DL(OP_RESTRICT) HVE_DL(OP_GENERAL) HVE_DL(OP_RESID_L1JAC) HVE_DL(OP_RESTRICT_ZG)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_DL
+#undef HVE_DB
+#undef HVE_D
+    return hipGetLastError();
+  }
+  if (jag && M.pw) {
 #define HVE_P(OPV, CF)                                                                      \
   if (nt) hipLaunchKernelGGL((k_sell_pw<OPV, CF, true>), grid, block, 0, s, a);            \
   else hipLaunchKernelGGL((k_sell_pw<OPV, CF, false>), grid, block, 0, s, a);
@@ -775,7 +909,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     break;
     switch (op) {
       HVE_PL(OP_RESID) HVE_PL(OP_MATVEC) HVE_PL(OP_L1JAC) HVE_PL(OP_L1JAC_W) HVE_PL(OP_JAC)
-      HVE_PL(OP_PROLONG) HVE_PL(OP_RESTRICT) HVE_PL(OP_GENERAL) HVE_PL(OP_RESID_L1JAC)
+      HVE_PL(OP_PROLONG) HVE_PL(OP_RESTRICT) HVE_PL(OP_GENERAL) HVE_PL(OP_RESID_L1JAC) HVE_PL(OP_RESTRICT_ZG)
       default: return hipErrorInvalidValue;
     }
 #undef HVE_PL
@@ -794,7 +928,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     break;
     switch (op) {
       HVE_WL(OP_RESID) HVE_WL(OP_MATVEC) HVE_WL(OP_L1JAC) HVE_WL(OP_L1JAC_W) HVE_WL(OP_JAC)
-      HVE_WL(OP_PROLONG) HVE_WL(OP_RESTRICT) HVE_WL(OP_GENERAL) HVE_WL(OP_RESID_L1JAC)
+      HVE_WL(OP_PROLONG) HVE_WL(OP_RESTRICT) HVE_WL(OP_GENERAL) HVE_WL(OP_RESID_L1JAC) HVE_WL(OP_RESTRICT_ZG)
       default: return hipErrorInvalidValue;
     }
 #undef HVE_WL
@@ -818,7 +952,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     break;
   switch (op) {
     HVE_L(OP_RESID) HVE_L(OP_MATVEC) HVE_L(OP_L1JAC) HVE_L(OP_L1JAC_W) HVE_L(OP_JAC)
-    HVE_L(OP_PROLONG) HVE_L(OP_RESTRICT) HVE_L(OP_GENERAL) HVE_L(OP_RESID_L1JAC)
+    HVE_L(OP_PROLONG) HVE_L(OP_RESTRICT) HVE_L(OP_GENERAL) HVE_L(OP_RESID_L1JAC) HVE_L(OP_RESTRICT_ZG)
     default: return hipErrorInvalidValue;
   }
 #undef HVE_L

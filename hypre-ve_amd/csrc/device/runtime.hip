@@ -37,7 +37,7 @@ static T* dupload(const T* h, size_t n) {
   return p;
 }
 
-void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h) {
+void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy) {
   release();
   std::vector<int> sp, col, perm;
   std::vector<double> val;
@@ -78,8 +78,56 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h) {
           (A.nrows < wide_rows || (wide_rows == (1 << 18) && A.nrows < (1 << 20) && avg_len >= 40.0))) ? 1 : 0;
   bool jag = wide ? false : jag_env >= 0 ? (jag_env != 0 && A.nnz() > 0)
                                 : (pad0 > A.nnz() + A.nnz() / 10 && A.nnz() >= 8LL * A.nrows && A.nrows >= (1 << 18));
-  // the jagged loop addresses x through a buffer descriptor (byte count < 2^31)
-  if (jag && (int64_t)A.ncols * 8 >= (1LL << 31)) jag = false;
+  pw = (jag && sell_pw()) ? 1 : 0;
+  // Dictionary layout (x-tile in LDS, one wave per slice) for large operators
+  // with long rows: level-1 A and R, level-2 A.  Measured on MI355X (256^3):
+  // A_1 516 -> 466 us, R_1 85 -> 76, A_2 177 (wide) -> 135; R_0 (10 entries
+  // a row) 203 -> 211 and every operator below 2^18 rows 2-3x slower, so those
+  // keep the jagged / wide loops.  HVE_SELL_DICT=0 turns it off, 1 forces it
+  // wherever the jagged layout is chosen, 2 also in place of the wide loop.
+  static const int dict_env = [] {
+    const char* e = getenv("HVE_SELL_DICT");
+    return e ? atoi(e) : -1;
+  }();
+  bool use_dict = A.nnz() > 0 &&
+                  (dict_env < 0 ? (A.nrows >= (1 << 18) && avg_len >= 16.0)
+                                : ((dict_env >= 1 && jag) || (dict_env >= 2 && wide)));
+  if (policy != 0) {  // forced (tests): every loop gives the same bits
+    wide = policy == 3 ? 1 : 0;
+    jag = (policy == 2 || policy == 4) && A.nnz() > 0;
+    pw = policy == 4 && jag;
+    use_dict = policy == 5 && A.nnz() > 0;
+  }
+  if (use_dict) {
+    std::vector<unsigned short> c16;
+    std::vector<int> dp, dc, rl2;
+    int mxd = 0;
+    if (build_sell_dict_host(A, 4096, perm, sp, rl2, c16, val, dp, dc, mxd)) {
+      nrows = A.nrows;
+      ncols = A.ncols;
+      nslices = (int)sp.size() - 1;
+      nnz = A.nnz();
+      nnz_pad = nnz;
+      batch = (nslices > 0 && pad0 > (int64_t)nslices * 64 * 8) ? 16 : 8;
+      pipe = 1;
+      wide = 0;
+      pw = 0;
+      dmax = std::max(1, mxd);
+      rowlen = dupload(rl2.data(), rl2.size());
+      slice_ptr = dupload(sp.data(), sp.size());
+      col16 = dupload(c16.data(), c16.size());
+      this->val = dupload(val.data(), val.size());
+      dict_ptr = dupload(dp.data(), dp.size());
+      dict = dupload(dc.data(), std::max<size_t>(1, dc.size()));
+      std::vector<int> map(A.nrows);
+      for (int i = 0; i < A.nrows; ++i) map[i] = rowmap_h.empty() ? perm[i] : rowmap_h[perm[i]];
+      bool ident = true;
+      for (int i = 0; i < A.nrows && ident; ++i) ident = map[i] == i;
+      if (!ident) rowmap = dupload(map.data(), map.size());
+      return;
+    }
+    perm.clear();  // a slice has too many distinct columns: fall back
+  }
   std::vector<int> rl;
   if (jag) {
     build_sell_jagged_host(A, perm, sp, rl, col, val);
@@ -122,8 +170,12 @@ void DevSell::release() {
   if (val) (void)hipFree(val);
   if (rowmap) (void)hipFree(rowmap);
   if (rowlen) (void)hipFree(rowlen);
+  if (col16) (void)hipFree(col16);
+  if (dict_ptr) (void)hipFree(dict_ptr);
+  if (dict) (void)hipFree(dict);
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
-  nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0;
+  col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0;
+  nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;
 }
 
 void DevGs::upload(const CSR& A, int num_blocks, bool forward) {
@@ -151,9 +203,9 @@ void DevGs::release() {
   max_levels = 0;
 }
 
-void DevOp::upload(const RankOp& op) {
-  in.upload(op.interior, op.map_int);
-  bd.upload(op.boundary, op.map_bnd);
+void DevOp::upload(const RankOp& op, int policy) {
+  in.upload(op.interior, op.map_int, policy);
+  bd.upload(op.boundary, op.map_bnd, policy);
   nrows_local = op.nrows_local;
 }
 
@@ -248,11 +300,11 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     D.n = L.n_loc;
     D.first = L.first;
     D.n_glob = L.n_glob;
-    D.A.upload(L.A);
+    D.A.upload(L.A, prm.sell_policy);
     D.hu.upload(L.hu);
     if (l < nl - 1) {
-      D.P.upload(L.P);
-      D.R.upload(L.R);
+      D.P.upload(L.P, prm.sell_policy);
+      D.R.upload(L.R, prm.sell_policy);
       D.hv.upload(L.hv);
     }
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
@@ -447,7 +499,7 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
   std::vector<int> lev_counter(nl, prm.cycle_type);
   std::vector<double*> ucur(nl), ualt(nl);
   std::vector<const double*> fl(nl);
-  std::vector<char> zero(nl, 0);
+  std::vector<char> zero(nl, 0), skip_sweep(nl, 0);
   lev_counter[0] = 1;
   if (u0_buf_[0]) {
     if (!presmoothed) HVE_HIP(launch_copy(lev_[0].n, u0, u0_buf_[0], s));
@@ -489,6 +541,10 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
         skip_first = false;
         continue;
       }
+      if (skip_sweep[level]) {
+        skip_sweep[level] = 0;
+        continue;
+      }
       if (relax_type == 9 || relax_type == 99 || relax_type == 19 || relax_type == 98) {
         coarse_solve(level, fl[level], ucur[level], s);
         zero[level] = 0;
@@ -515,11 +571,25 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       DevLevel& Lf = lev_[fine];
       // Vtemp = f - A u  (csr_matvec.c, alpha=-1 beta=1);  F_c = P^T Vtemp
       apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);
-      apply(Lf.R, &Lf.hv, K_RESTRICT, Lf.V, nullptr, nullptr, nullptr, 0, lev_[coarse].F, 1.0, 0.0, s);
+      // When the coarse level's first down sweep is l1-Jacobi (weight 1) from
+      // the zero guess, u_c = 0 + F_c/l1 is formed by the restriction itself.
+      const bool fuse_zg = coarse != nl - 1 && prm.num_sweeps[1] >= 1 &&
+                           (prm.relax_type[1] == 18 || prm.relax_type[1] == 7) && prm.relax_weight == 1.0 &&
+                           lev_[coarse].l1 != nullptr;
+      if (fuse_zg) {
+        apply(Lf.R, &Lf.hv, K_RESTRICT_ZG, Lf.V, nullptr, lev_[coarse].l1, nullptr, 0, lev_[coarse].F, 1.0, 0.0,
+              s, ucur[coarse]);
+      } else {
+        apply(Lf.R, &Lf.hv, K_RESTRICT, Lf.V, nullptr, nullptr, nullptr, 0, lev_[coarse].F, 1.0, 0.0, s);
+      }
       ++level;
       lev_counter[level] = std::max(lev_counter[level], prm.cycle_type);
       cycle_param = (level == nl - 1) ? 3 : 1;
       zero[level] = 1;  // U_array[coarse] = 0 (par_cycle.c:556), folded into the next smoother
+      if (fuse_zg) {
+        zero[level] = 0;
+        skip_sweep[level] = 1;  // that sweep is done
+      }
     } else if (level != 0) {
       const int fine = level - 1, coarse = level;
       if (zero[coarse]) HVE_HIP(launch_set(lev_[coarse].n, 0.0, ucur[coarse], s));

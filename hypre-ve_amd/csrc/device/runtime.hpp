@@ -33,16 +33,23 @@ struct DevSell {
   double* val = nullptr;
   int* rowmap = nullptr;
   int* rowlen = nullptr;  // jagged layout only
+  unsigned short* col16 = nullptr;  // dictionary layout: local columns
+  int* dict_ptr = nullptr;
+  int* dict = nullptr;
+  int dmax = 0;
   int batch = 8;
   int pipe = 0;
   int wide = 0;
+  int pw = 0;
   SellView view() const {
     SellView v;
-    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide;
+    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
+    v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map
-  void upload(const CSR& A, const std::vector<int>& rowmap = {});
+  // policy: AMGParams::sell_policy
+  void upload(const CSR& A, const std::vector<int>& rowmap = {}, int policy = 0);
   void release();
   size_t bytes() const { return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * 12 + (rowmap ? (size_t)nrows * 4 : 0) +
                          (rowlen ? (size_t)nslices * 256 : 0); }
@@ -53,7 +60,7 @@ struct DevOp {
   DevSell in, bd;
   int nrows_local = 0;
   int64_t nnz() const { return in.nnz + bd.nnz; }
-  void upload(const RankOp& op);
+  void upload(const RankOp& op, int policy = 0);
   void release() { in.release(); bd.release(); }
 };
 

@@ -80,6 +80,12 @@ struct AMGParams {
   // smoothers; hypre's CPU path uses num_threads for this (par_relax.c:4387).
   int num_blocks = 1;
   int agg_num_levels = 0;
+  // Device layout / loop of each SELL operator: 0 automatic (by size, row
+  // length and padding), 1 padded lane-per-row, 2 jagged lane-per-row,
+  // 3 padded workgroup-per-slice (wide), 4 jagged wave-product-parallel,
+  // 5 jagged with a per-slice column dictionary (x-tile in LDS).
+  // Every choice gives the same bits; 1-4 let the tests prove that.
+  int sell_policy = 0;
 };
 
 struct Level {

@@ -18,6 +18,12 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
 // slice_ptr[s] + sum_{k'<k} #{lanes with rowlen > k'} + r.
 void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<int>& slice_ptr,
                             std::vector<int>& rowlen, std::vector<int>& col, std::vector<double>& val);
+// Jagged SELL-64 with a per-slice column dictionary (16-bit local column
+// indices into the slice's ascending list of distinct columns).  false when
+// a slice has more than dmax distinct columns; max_distinct is set either way.
+bool build_sell_dict_host(const CSR& A, int dmax, std::vector<int>& perm, std::vector<int>& slice_ptr,
+                          std::vector<int>& rowlen, std::vector<unsigned short>& col16, std::vector<double>& val,
+                          std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct);
 // Padded entry count of the SELL-64 layout for a given sigma (0 = no sort).
 int64_t sell_padded_nnz(const CSR& A, int sigma);
 // Level schedule of one hybrid Gauss-Seidel sweep (par_relax.c cases 3/4/6/

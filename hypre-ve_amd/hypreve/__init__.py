@@ -152,6 +152,7 @@ SIGNATURES = [
     ("hypreve_ParVectorSetRandomValues", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetNumBlocks", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetUseGraph", _i, [_p, _i]),
+    ("hypreve_BoomerAMGSetSellPolicy", _i, [_p, _i]),
     ("hypreve_BoomerAMGGetComplexities", _i, [_p, _pd, _pd, _pd]),
     ("hypreve_BoomerAMGGetLevelInfo", _i, [_p, _i, _pi, _pi64, _pi64]),
     ("hypreve_BoomerAMGGetLevelMatrix", _i, [_p, _i, _i, _pi, _pi, _pi64, _pi, _pi, _pd]),
@@ -355,6 +356,7 @@ class BoomerAMG:
         "relax_wt": ("HYPRE_BoomerAMGSetRelaxWt", float), "outer_wt": ("HYPRE_BoomerAMGSetOuterWt", float),
         "print_level": ("HYPRE_BoomerAMGSetPrintLevel", int), "converge_type": ("HYPRE_BoomerAMGSetConvergeType", int),
         "num_blocks": ("hypreve_BoomerAMGSetNumBlocks", int), "use_graph": ("hypreve_BoomerAMGSetUseGraph", int),
+        "sell_policy": ("hypreve_BoomerAMGSetSellPolicy", int),
     }
 
     def __init__(self, **kw):

@@ -209,6 +209,12 @@ HYPRE_Int hypreve_ParVectorSetRandomValues(HYPRE_ParVector v, HYPRE_Int seed); /
 /* Number of contiguous row blocks used by the hybrid Gauss-Seidel smoothers
  * (reference: OMP_NUM_THREADS on the CPU path). 0 = automatic. */
 HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_blocks);
+/* Device layout / row loop of the hierarchy's SELL operators (takes effect at
+ * Setup): 0 automatic, 1 padded lane-per-row, 2 jagged lane-per-row, 3 padded
+ * workgroup-per-slice, 4 jagged wave-product-parallel, 5 jagged with an LDS
+ * x-tile (per-slice column dictionary).  All give identical
+ * bits; the forced settings exist for parity tests and experiments. */
+HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* Whole-cycle hipGraph capture on/off (default on). */
 HYPRE_Int hypreve_BoomerAMGSetUseGraph(HYPRE_Solver solver, HYPRE_Int use_graph);
 /* Statistics after Setup: levels, complexities, per-level rows/nnz. */

@@ -78,6 +78,37 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen):
     assert np.array_equal(u.get(), uo)
 
 
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
+def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
+    """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
+    workgroup-per-slice, jagged wave-product-parallel) forced on every
+    operator of the hierarchy: the same bits as the oracle.  The automatic
+    choice only uses jagged and wide loops on operators too large for the
+    other tests, so this is where those loops meet the oracle."""
+    hv = gpu
+    A, amg, O = setup_pair(hv, orc, (30, 27, 25), coarsen_type=8, interp_type=6, P_max_elmts=4,
+                           relax_type=relax, relax_order=order, sell_policy=policy)
+    n = A.n
+    rng = np.random.default_rng(23 + policy)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+    b = hv.ParVector(n, f_h)
+    x = hv.ParVector(n, np.zeros(n))
+    amg.set(tol=1e-7, max_iter=40)
+    it, rr = amg.solve(A, b, x)
+    xo = np.zeros(n)
+    st = O.solve(f_h, xo, 1e-7, 40)
+    assert it == st["iterations"]
+    assert np.array_equal(x.get(), xo)
+
+
 def test_matvec_bitwise(gpu, orc):
     hv = gpu
     A, amg, O = setup_pair(hv, orc, (20, 20, 20), coarsen_type=8, relax_type=18)
