@@ -146,6 +146,36 @@ def test_pcg_amg_l1jacobi(gpu, orc):
     assert rr < 1e-8
 
 
+@pytest.mark.parametrize("relax", [None, 18])
+def test_pcg_ij_64(gpu, orc, relax):
+    """BASELINE configs[0]: ij's 3-D 7-point Laplacian 64^3, BoomerAMG-PCG
+    (-solver 1), with ij's BoomerAMG settings (HMIS, ext+i Pmx 4, hybrid l1
+    Gauss-Seidel 13/14 down/up, Gaussian elimination coarsest; relax=18: the
+    l1-Jacobi variant the bench runs).  Same PCG iteration count as the CPU
+    oracle and final relative residuals within 1e-6 (PCG's dot products are
+    reduced in a different order)."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(64, 64, 64)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(1))
+    if relax is not None:
+        amg.set(relax_type=relax)
+    pcg = hv.PCG(tol=1e-8, max_iter=100, two_norm=1)
+    pcg.set_precond_amg(amg)
+    n = A.n
+    b_h = np.ones(n)
+    b = hv.ParVector(n, b_h)
+    x = hv.ParVector(n, np.zeros(n))
+    pcg.setup(A, b, x)
+    it, rr = pcg.solve(A, b, x)
+    O = orc.OracleAMG(amg)
+    xo = np.zeros(n)
+    ito, rro = O.pcg(b_h, xo, 1e-8, 100, 1)
+    assert it == ito
+    assert abs(rr - rro) <= 1e-6 * rro
+    assert rr < 1e-8
+    assert np.allclose(x.get(), xo, rtol=1e-9, atol=1e-12)
+
+
 def test_large_solve_properties(gpu):
     """128^3 (2.1M rows): the GPU V-cycle converges monotonically and its
     average factor is in the range the reference reports for this stencil."""
