@@ -76,7 +76,7 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
 
     n = args.n
     t0 = time.time()
-    if world > 1:
+    if comm is not None:
         # weak scaling: n x n x (n * world) grid, rank r owns z-slab r
         A = hv.ParCSRMatrix.laplacian(n, n, n * world, comm=comm, P=1, Q=1, R=world, p=0, q=0, r=rank)
     else:
@@ -93,7 +93,7 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     if rank == 0:
         log(f"[bench] ranks={world} n={n}^3/rank rows/rank={nrows} levels={amg.num_levels()} grid={g:.4f} "
             f"op={o:.4f} setup={t_setup:.1f}s")
-    first = A.first if world > 1 else 0
+    first = A.first if comm is not None else 0
     b = hv.ParVector(nrows, np.ones(nrows), comm=comm, first=first, global_n=nrows * world)
     x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=nrows * world)
 
@@ -190,6 +190,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
     ap.add_argument("--cpu-cycles-max", type=int, default=60)
     ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--dist", action="store_true",
+                    help="take the torch.distributed + RCCL path even with one rank (rehearses the multi-GPU "
+                         "launch on a one-GPU box: a 1-rank RCCL communicator, partitioned solve path)")
     ap.add_argument("--loopback", type=int, default=0,
                     help="rehearsal only: N virtual ranks (threads) sharing this process's GPU")
     args = ap.parse_args()
@@ -239,7 +242,7 @@ def main():
 
     dist = None
     comm = None
-    if world > 1:
+    if world > 1 or args.dist:
         import torch.distributed as dist
 
         torch.cuda.set_device(local_rank)

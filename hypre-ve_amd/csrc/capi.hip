@@ -38,7 +38,9 @@ struct hypre_ParCSRMatrix_struct {
   CSR diag;         // host: owned rows, GLOBAL column indices, diagonal first
   DevSell dA;       // device copy (SELL-64) used by Matvec (one rank)
   bool dev = false;
-  bool multi() const { return comm && comm->size > 1; }
+  // partitioned path: any communicator with a transport (a 1-rank RCCL
+  // communicator included, which runs the partitioned code with one rank)
+  bool multi() const { return comm && comm->dc; }
   void ensure_device() {
     if (multi()) throw std::runtime_error("ParCSR matvec across ranks needs a BoomerAMG setup on this matrix");
     if (!dev) { dA.upload(diag); dev = true; }

@@ -149,7 +149,7 @@ class LoopComm final : public DevComm {
       HVE_HIP(hipEventRecord(ev, s));
       std::lock_guard<std::mutex> lk(H.m);
       for (const auto& m : sends) {
-        if (m.peer < 0 || m.peer >= n || m.peer == rank_) throw std::runtime_error("loopback: bad send peer");
+        if (m.peer < 0 || m.peer >= n) throw std::runtime_error("loopback: bad send peer");
         hipEvent_t e = ev;
         if (&m != &sends.front()) e = dup_event(s);
         H.mail[(size_t)rank_ * n + m.peer].push_back({m.buf, m.bytes, e});
@@ -158,7 +158,7 @@ class LoopComm final : public DevComm {
     }
     // 2. receive: wait for the matching post, copy after its ready event
     for (const auto& m : recvs) {
-      if (m.peer < 0 || m.peer >= n || m.peer == rank_) throw std::runtime_error("loopback: bad recv peer");
+      if (m.peer < 0 || m.peer >= n) throw std::runtime_error("loopback: bad recv peer");
       LoopHub::Post p;
       {
         std::unique_lock<std::mutex> lk(H.m);

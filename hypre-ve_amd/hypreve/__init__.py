@@ -143,6 +143,7 @@ SIGNATURES = [
     ("hypreve_CommGetUniqueId", _i, [_p]),
     ("hypreve_CommCreate", _i, [_i, _i, _p, C.POINTER(_p)]),
     ("hypreve_CommDestroy", _i, [_p]),
+    ("hypreve_CommSelfTest", _i, [_p]),
     ("hypreve_CommCreateLoopback", _i, [_i, C.POINTER(_p)]),
     ("hypreve_ParCSRMatrixCreateFromCSR", _i, [_p, _i, _i, _i, _pi, _pi, _pd, C.POINTER(_p)]),
     ("hypreve_ParVectorDeviceData", _p, [_p]),
@@ -223,6 +224,11 @@ class Comm:
         hs = (_p * size)()
         check(lib().hypreve_CommCreateLoopback(size, hs), "CommCreateLoopback")
         return [cls(_p(hs[r]), r, size) for r in range(size)]
+
+    def self_test(self):
+        """Collective transport check (exchange incl. self, all-reduce,
+        all-gather, broadcast); raises on a mismatch."""
+        check(lib().hypreve_CommSelfTest(self.h), "CommSelfTest")
 
     def destroy(self):
         if self.h:

@@ -187,6 +187,11 @@ HYPRE_Int hypreve_CommGetUniqueId(void *nccl_id_128);
 HYPRE_Int hypreve_CommCreate(HYPRE_Int rank, HYPRE_Int size, const void *nccl_id_128,
                              HYPRE_Comm *comm);
 HYPRE_Int hypreve_CommDestroy(HYPRE_Comm comm);
+/* Transport self-test (collective): grouped exchange with every rank, self
+ * included, all-reduce, all-gather and broadcast, each checked.  0 = pass.
+ * hypreve_CommCreate with size 1 and an id makes a 1-rank RCCL communicator,
+ * which runs the partitioned solve path with one rank. */
+HYPRE_Int hypreve_CommSelfTest(HYPRE_Comm comm);
 /* `size` communicators of virtual ranks sharing one GPU inside this process
  * (comms[0..size-1]); each rank must be driven from its own host thread.  Used
  * to check the partitioned solve on a single GPU (RCCL refuses two ranks on

@@ -23,6 +23,9 @@ if [[ $WHAT == all || $WHAT == tests ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if [[ $WHAT == all || $WHAT == multi ]]; then
+  # the driver's multi-GPU launch shape, with one rank: torch.distributed.run,
+  # gloo for the unique id and the timing max, a 1-rank RCCL communicator
+  step dist1 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29555 bench.py --gpus 1 --dist --steps 5 --warmup 1 --cpu-cycles 0
   step loopback2 600 python bench.py --loopback 2 --n 128 --steps 5 --warmup 1 --cpu-cycles 0
   step loopback8 900 python bench.py --loopback 8 --n ${LOOPBACK_N:-128} --steps 3 --warmup 1 --cpu-cycles 0
 fi

@@ -91,3 +91,49 @@ def test_loopback_partitioned_27pt(hv, nranks):
     xN, itN, rrN, nlN = _solve_nranks(hv, 13, 12, 15, kw, nranks, stencil=27)
     assert nlN == nl1 and all(i == it1 for i in itN)
     assert np.array_equal(x1, xN)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_loopback_comm_selftest(hv, nranks):
+    """Every transport operation the solve uses, checked value by value."""
+    hv.init()
+    comms = hv.Comm.loopback(nranks)
+    errs = [None] * nranks
+
+    def worker(r):
+        try:
+            comms[r].self_test()
+        except Exception as e:
+            errs[r] = e
+
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(120)
+    assert not any(t.is_alive() for t in th)
+    assert errs == [None] * nranks, errs
+
+
+def test_rccl_single_rank(hv):
+    """The production transport on a one-GPU box: a 1-rank RCCL communicator
+    (RCCL refuses two ranks on one device).  The self-test sends to its own
+    rank through ncclGroupStart/Send/Recv/GroupEnd and runs ncclAllReduce;
+    then a BoomerAMG solve over that communicator takes the partitioned path
+    (rank-0 setup shipped over RCCL, dots summed by ncclAllReduce) and must
+    reproduce the communicator-free solve bit for bit."""
+    hv.init()
+    c = hv.Comm.create(0, 1, hv.Comm.unique_id())
+    c.self_test()
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, relax_type=18, tol=1e-8, max_iter=60)
+    x1, it1, rr1, nl1 = _solve_1rank(hv, 20, 18, 16, kw)
+    A = hv.ParCSRMatrix.laplacian(20, 18, 16, comm=c, P=1, Q=1, R=1, p=0, q=0, r=0)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup(A)
+    b = hv.ParVector(A.n, np.ones(A.n), comm=c, first=A.first, global_n=A.global_n)
+    x = hv.ParVector(A.n, np.zeros(A.n), comm=c, first=A.first, global_n=A.global_n)
+    it, rr = amg.solve(A, b, x)
+    assert it == it1
+    assert np.array_equal(x.get(), x1)
+    assert abs(rr - rr1) <= 1e-10 * rr1
