@@ -812,11 +812,13 @@ static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
       for (int q = 0; q < (int)all[3 * r]; ++q) G.i[starts0[r] + q + 1] = (int)(nnzoff[r] + li[q + 1]);
     }
     amg_setup(G, s->prm, s->H);
+    { CSR().swap(G); }  // the gathered matrix is level 0 of H now
     bufs.resize(size);
+    std::vector<RankHierarchy> parts;
+    partition_hierarchy_all(s->H, starts0, size, parts);
     for (int r = 0; r < size; ++r) {
-      RankHierarchy RR;
-      partition_hierarchy(s->H, starts0, r, size, RR);
-      serialize(RR, bufs[r]);
+      serialize(parts[r], bufs[r]);
+      parts[r] = RankHierarchy();  // release as we go
     }
   }
   (void)hipFree(d_i); (void)hipFree(d_j); (void)hipFree(d_a);

@@ -260,6 +260,11 @@ int partition_self_check(const Hierarchy& H, int size, std::string& msg) {
   return errs;
 }
 
+void partition_hierarchy_all(const Hierarchy& H, const std::vector<int>& starts0, int size,
+                             std::vector<RankHierarchy>& out) {
+  partition_all(H, starts0, size, out);
+}
+
 void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, int rank, int size,
                          RankHierarchy& out) {
   std::vector<RankHierarchy> all;

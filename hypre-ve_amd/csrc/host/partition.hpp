@@ -61,6 +61,10 @@ struct RankHierarchy {
 // starts0: level-0 row starts (size+1 entries).
 void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, int rank, int size,
                          RankHierarchy& out);
+// Every rank's part in one pass (O(global) work; partition_hierarchy
+// partitions all ranks to return one).
+void partition_hierarchy_all(const Hierarchy& H, const std::vector<int>& starts0, int size,
+                             std::vector<RankHierarchy>& out);
 // Whole hierarchy as one rank (no halo), used for the single-GPU path.
 void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out);
 
