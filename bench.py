@@ -82,31 +82,48 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     else:
         A = hv.ParCSRMatrix.laplacian(n, n, n)
     nrows = A.n
-    kw = hv.ij_amg_defaults(0)
-    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-300, max_iter=args.warmup,
-              min_iter=0)
-    amg = hv.BoomerAMG(**kw)
-    with heartbeat(f"rank {rank} setup"):
-        amg.setup(A)
+    pcg = args.solver == "pcg"
+    first = A.first if comm is not None else 0
+    b = hv.ParVector(nrows, np.ones(nrows), comm=comm, first=first, global_n=nrows * world)
+    x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=nrows * world)
+    if pcg:
+        # ij -solver 1: PCG (two-norm) preconditioned by one BoomerAMG V-cycle
+        kw = hv.ij_amg_defaults(1)
+        kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
+        amg = hv.BoomerAMG(**kw)
+        krylov = hv.PCG(tol=0.0, max_iter=max(1, args.warmup), two_norm=1)
+        krylov.set_precond_amg(amg)
+        with heartbeat(f"rank {rank} setup"):
+            krylov.setup(A, b, x)
+    else:
+        kw = hv.ij_amg_defaults(0)
+        kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-300, max_iter=args.warmup,
+                  min_iter=0)
+        amg = hv.BoomerAMG(**kw)
+        with heartbeat(f"rank {rank} setup"):
+            amg.setup(A)
     t_setup = time.time() - t0
     g, o, c = amg.complexities()
     if rank == 0:
         log(f"[bench] ranks={world} n={n}^3/rank rows/rank={nrows} levels={amg.num_levels()} grid={g:.4f} "
             f"op={o:.4f} setup={t_setup:.1f}s")
-    first = A.first if comm is not None else 0
-    b = hv.ParVector(nrows, np.ones(nrows), comm=comm, first=first, global_n=nrows * world)
-    x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=nrows * world)
-
     # warmup (also instantiates the cycle hipGraph)
     if args.warmup > 0:
-        amg.set(max_iter=args.warmup)
-        amg.solve(A, b, x)
+        if pcg:
+            krylov.set(max_iter=args.warmup)
+            krylov.solve(A, b, x)
+        else:
+            amg.set(max_iter=args.warmup)
+            amg.solve(A, b, x)
     x.fill(0.0)
-    amg.set(max_iter=args.steps)
+    if pcg:
+        krylov.set(max_iter=args.steps)
+    else:
+        amg.set(max_iter=args.steps)
     torch.cuda.synchronize()
     barrier()
     t_start = time.perf_counter()
-    it, rr = amg.solve(A, b, x)
+    it, rr = (krylov if pcg else amg).solve(A, b, x)
     torch.cuda.synchronize()
     barrier()
     elapsed = max_over_ranks(time.perf_counter() - t_start)
@@ -140,20 +157,25 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
         O = oracle_py.OracleAMG(amg)
         bh = np.ones(nrows)
         u = np.zeros(nrows)
+        def cpu_run(k):
+            u[:] = 0.0
+            if pcg:
+                return O.pcg(bh, u, 0.0, k, 1)[0]
+            return O.solve(bh, u, 1e-300, k)["iterations"]
+
         tc = time.perf_counter()
-        O.solve(bh, u, 1e-300, 1)
+        cpu_run(1)
         t1 = time.perf_counter() - tc
         iters = int(max(2, min(args.cpu_cycles_max, round(args.cpu_seconds / max(t1, 1e-3)))))
-        u[:] = 0.0
         tc = time.perf_counter()
-        st = O.solve(bh, u, 1e-300, iters)
+        done = cpu_run(iters)
         tcpu = time.perf_counter() - tc
         threads = oracle_py.num_threads()
-        cpu = {"value": round(nrows * st["iterations"] / tcpu, 1), "unit": "DOF/s", "cores": threads, "kind": "port",
-               "sample": f"{st['iterations']} solve iterations (V-cycle + residual norm) of the same {n}^3 "
-                         f"hierarchy by the C oracle (oracle/oracle.c), OpenMP {threads} threads, {tcpu:.1f}s"}
-        log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({st['iterations']} iterations, {tcpu:.1f}s, "
-            f"{threads} threads)")
+        what = "PCG iterations (one V-cycle preconditioner each)" if pcg else "solve iterations (V-cycle + residual norm)"
+        cpu = {"value": round(nrows * done / tcpu, 1), "unit": "DOF/s", "cores": threads, "kind": "port",
+               "sample": f"{done} {what} of the same {n}^3 hierarchy by the C oracle (oracle/oracle.c), "
+                         f"OpenMP {threads} threads, {tcpu:.1f}s"}
+        log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({done} iterations, {tcpu:.1f}s, {threads} threads)")
     if rank != 0:
         return None
     return {
@@ -170,8 +192,8 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
         "dtype": "f64",
         "data": "synthetic (GenerateLaplacian 7-point, rhs = ones)",
         "config": {"workload": f"3D 7-point Laplacian {n}^3 per GPU ({n}x{n}x{n * world} global, z-slab row "
-                               f"blocks), BoomerAMG V-cycle, PMIS + ext+i (Pmx 4), l1-Jacobi (relax 18) down/up, "
-                               f"Gaussian elimination coarsest",
+                               f"blocks), {'BoomerAMG-PCG (one V-cycle per PCG iteration)' if pcg else 'BoomerAMG V-cycle'}"
+                               f", PMIS + ext+i (Pmx 4), l1-Jacobi (relax 18) down/up, Gaussian elimination coarsest",
                    "rows_per_gpu": nrows, "levels": amg.num_levels(), "grid_complexity": round(g, 6),
                    "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
                    "parallelism": f"rows{world}"},
@@ -190,6 +212,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
     ap.add_argument("--cpu-cycles-max", type=int, default=60)
     ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--solver", choices=["amg", "pcg"], default="amg",
+                    help="amg: a step is one BoomerAMG solve iteration (the metric); pcg: one PCG iteration "
+                         "preconditioned by one V-cycle (configs[2], reported separately)")
     ap.add_argument("--dist", action="store_true",
                     help="take the torch.distributed + RCCL path even with one rank (rehearses the multi-GPU "
                          "launch on a one-GPU box: a 1-rank RCCL communicator, partitioned solve path)")

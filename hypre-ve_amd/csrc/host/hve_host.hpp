@@ -129,6 +129,13 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
 void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                          double trunc_factor, int max_elmts, CSR& P);
 void truncate_rows(CSR& P, double tol, int max_elmts);
+// Universe-indexed cores of ext+i and RAP shared by the one-process and the
+// distributed setup (see setup.cpp).
+void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
+                int nrows, int ncoarse, int nuniv, CSR& P);
+void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& row_ic,
+              const std::vector<int>& coarse_glob, int nfine_univ, int ncoarse_univ, int ncoarse_glob, CSR& C);
+double hypre_rand_at(int64_t k, int seed);
 void transpose(const CSR& A, CSR& AT);
 void rap(const CSR& P, const CSR& A, CSR& RAP);
 void compute_l1_norms(const CSR& A, int option, const int* cf, int num_blocks,

@@ -739,23 +739,25 @@ void truncate_rows(CSR& P, double tol, int max_elmts) {
 // Extended+i interpolation: par_lr_interp.c:1041
 // hypre_BoomerAMGBuildExtPIInterpHost, single process, one thread.
 // ---------------------------------------------------------------------------
-void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
-                        double trunc_factor, int max_elmts, CSR& P) {
+// Ext+i rows [0, nrows) of P.  A and S are indexed in a "universe" of nuniv
+// points (the whole matrix in one process; owned rows + ghost points in the
+// distributed setup); cf and fine_to_coarse (global coarse index of C points)
+// are given for every universe point; rows of A and S are needed for the
+// computed rows and their strong F neighbours.  P's columns are global coarse
+// indices (ncoarse in all).
+void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
+                int nrows, int ncoarse, int nuniv, CSR& P) {
   // Row-parallel restatement.  Each row's P entries depend only on the
   // markers set while processing that row (stale markers of earlier rows of
   // the same thread are below jj_begin_row or are other negative stamps), so a
   // thread-local P_marker processed in increasing row order reproduces the
   // single-thread result entry for entry.
-  const int n = A.nrows;
-  std::vector<int> fine_to_coarse(n, -1);
-  int coarse_counter = 0;
-  for (int i = 0; i < n; ++i)
-    if (cf[i] >= 0) fine_to_coarse[i] = coarse_counter++;
-  P.resize_rows(n, coarse_counter);
+  const int n = nrows;
+  P.resize_rows(n, ncoarse);
   std::vector<int> rowcnt(n, 0);
 #pragma omp parallel
   {
-    std::vector<int> P_marker(n, -1);
+    std::vector<int> P_marker(nuniv, -1);
 #pragma omp for schedule(static)
     for (int i = 0; i < n; ++i) {
       // first pass (par_lr_interp.c:1290-1370): |C-hat_i|, stamped by row id
@@ -785,7 +787,7 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
   P.a.assign(nnzP, 0.0);
 #pragma omp parallel
   {
-    std::vector<int> P_marker(n, -1);
+    std::vector<int> P_marker(nuniv, -1);
     int strong_f_marker = -2;
 #pragma omp for schedule(static)
     for (int i = 0; i < n; ++i) {
@@ -848,6 +850,16 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
       strong_f_marker--;
     }
   }
+}
+
+void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
+                        double trunc_factor, int max_elmts, CSR& P) {
+  const int n = A.nrows;
+  std::vector<int> fine_to_coarse(n, -1);
+  int coarse_counter = 0;
+  for (int i = 0; i < n; ++i)
+    if (cf[i] >= 0) fine_to_coarse[i] = coarse_counter++;
+  extpi_core(A, S, cf, fine_to_coarse, n, coarse_counter, n, P);
   if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
   for (int i = 0; i < n; ++i)
     if (cf[i] == SF_PT) cf[i] = F_PT;
@@ -932,11 +944,15 @@ void transpose(const CSR& A, CSR& AT) {
 // column order and the diagonal placed first).  Parallel over coarse rows with
 // the row structure computed in a first pass.
 // ---------------------------------------------------------------------------
-void rap(const CSR& P, const CSR& A, CSR& C) {
-  CSR R;
-  transpose(P, R);
-  const int nc = P.ncols;
-  C.resize_rows(nc, nc);
+// Rows of C for the coarse rows R holds.  Universe indexing as in
+// extpi_core: R's columns and A's rows / columns are fine-universe indices,
+// P's rows fine-universe and columns coarse-universe indices; row q of R is
+// coarse-universe point row_ic[q]; C's columns are coarse_glob[] of the
+// coarse-universe points (global coarse indices).
+void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& row_ic,
+              const std::vector<int>& coarse_glob, int nfine_univ, int ncoarse_univ, int ncoarse_glob, CSR& C) {
+  const int nc = R.nrows;
+  C.resize_rows(nc, ncoarse_glob);
   std::vector<int> rowlen(nc, 0);
   // Each thread keeps its own markers.  Two passes: sizes, then values.
   for (int pass = 0; pass < 2; ++pass) {
@@ -947,7 +963,7 @@ void rap(const CSR& P, const CSR& A, CSR& C) {
     }
 #pragma omp parallel
     {
-      std::vector<int> A_marker(A.ncols, -1), P_marker(nc, -1);
+      std::vector<int> A_marker(nfine_univ, -1), P_marker(ncoarse_univ, -1);
       std::vector<int> ra_j;
       std::vector<double> ra_a;
       ra_j.reserve(4096);
@@ -955,10 +971,11 @@ void rap(const CSR& P, const CSR& A, CSR& C) {
       std::vector<int> tj;
       std::vector<double> ta;
 #pragma omp for schedule(dynamic, 256)
-      for (int ic = 0; ic < nc; ++ic) {
+      for (int q = 0; q < nc; ++q) {
+        const int ic = row_ic[q];
         ra_j.clear();
         ra_a.clear();
-        for (int jj1 = R.i[ic]; jj1 < R.i[ic + 1]; ++jj1) {
+        for (int jj1 = R.i[q]; jj1 < R.i[q + 1]; ++jj1) {
           const int i1 = R.j[jj1];
           const double r_entry = R.a[jj1];
           for (int jj2 = A.i[i1]; jj2 < A.i[i1 + 1]; ++jj2) {
@@ -979,9 +996,9 @@ void rap(const CSR& P, const CSR& A, CSR& C) {
         P_marker[ic] = 0;
         tj.push_back(ic);
         ta.push_back(0.0);
-        for (size_t q = 0; q < ra_j.size(); ++q) {
-          const int i1 = ra_j[q];
-          const double rap_ = ra_a[q];
+        for (size_t k = 0; k < ra_j.size(); ++k) {
+          const int i1 = ra_j[k];
+          const double rap_ = ra_a[k];
           for (int jj2 = P.i[i1]; jj2 < P.i[i1 + 1]; ++jj2) {
             const int i2 = P.j[jj2];
             const int marker = P_marker[i2];
@@ -996,14 +1013,26 @@ void rap(const CSR& P, const CSR& A, CSR& C) {
         }
         for (int c : tj) P_marker[c] = -1;
         if (pass == 0) {
-          rowlen[ic] = (int)tj.size();
+          rowlen[q] = (int)tj.size();
         } else {
-          std::copy(tj.begin(), tj.end(), C.j.begin() + C.i[ic]);
-          std::copy(ta.begin(), ta.end(), C.a.begin() + C.i[ic]);
+          int o = C.i[q];
+          for (size_t k = 0; k < tj.size(); ++k, ++o) {
+            C.j[o] = coarse_glob.empty() ? tj[k] : coarse_glob[tj[k]];
+            C.a[o] = ta[k];
+          }
         }
       }
     }
   }
+}
+
+void rap(const CSR& P, const CSR& A, CSR& C) {
+  CSR R;
+  transpose(P, R);
+  const int nc = P.ncols;
+  std::vector<int> row_ic(nc);
+  for (int q = 0; q < nc; ++q) row_ic[q] = q;
+  rap_core(R, A, P, row_ic, {}, A.ncols, nc, nc, C);
 }
 
 // ---------------------------------------------------------------------------

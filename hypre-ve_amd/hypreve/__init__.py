@@ -499,6 +499,12 @@ class PCG:
         lib().HYPRE_ParCSRPCGSetPrintLevel(h, print_level)
         self.precond = None
 
+    def set(self, tol=None, max_iter=None):
+        if tol is not None:
+            check(lib().HYPRE_ParCSRPCGSetTol(self.h, float(tol)), "PCGSetTol")
+        if max_iter is not None:
+            check(lib().HYPRE_ParCSRPCGSetMaxIter(self.h, int(max_iter)), "PCGSetMaxIter")
+
     def set_precond_amg(self, amg: BoomerAMG):
         L = lib()
         solve = C.cast(L.HYPRE_BoomerAMGSolve, C.c_void_p)
