@@ -17,6 +17,8 @@
 #include "host/hve_host.hpp"
 #include "host/layout.hpp"
 #include "host/partition.hpp"
+#include "host/dsetup.hpp"
+#include "host/hostcomm.hpp"
 
 using namespace hve;
 
@@ -719,6 +721,18 @@ HYPRE_Int hypreve_BoomerAMGPartitionCheck(HYPRE_Solver s, HYPRE_Int size) {
   API_END
 }
 
+HYPRE_Int hypreve_BoomerAMGDistSetupCheck(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_Int size) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(A && !A->multi(), 2);
+  CHECK_ARG(size >= 1, 3);
+  API_BEGIN
+  std::string msg;
+  if (!dist_setup_supported(s->prm, &msg)) return set_err(HYPRE_ERROR_ARG, "distributed setup: " + msg);
+  const int errs = dist_setup_self_check(A->diag, s->prm, size, msg);
+  if (errs) return set_err(HYPRE_ERROR_GENERIC, msg);
+  API_END
+}
+
 HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(A, 2);
@@ -854,6 +868,106 @@ static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
   deserialize(mybuf, s->RH);
 }
 
+// HostComm over the device communicator (RCCL, or the loopback hub): host
+// buffers staged through device memory.  The byte counts of every pair go
+// round first (an all-gather of each rank's send sizes), then one grouped
+// exchange moves all non-empty messages; a rank's message to itself is a
+// host copy.
+class DevHostComm final : public HostComm {
+ public:
+  explicit DevHostComm(DevComm& dc) : HostComm(dc.rank(), dc.size()), dc_(dc) {
+    HVE_HIP(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+  }
+  ~DevHostComm() override { (void)hipStreamDestroy(st_); }
+
+  void alltoallv(const std::vector<std::vector<char>>& send, std::vector<std::vector<char>>& recv) override {
+    const int n = size_, r = rank_;
+    std::vector<int64_t> mine(n), all((size_t)n * n);
+    for (int p = 0; p < n; ++p) mine[p] = (int64_t)send[p].size();
+    {
+      int64_t *dm = nullptr, *da = nullptr;
+      HVE_HIP(hipMalloc((void**)&dm, sizeof(int64_t) * n));
+      HVE_HIP(hipMalloc((void**)&da, sizeof(int64_t) * n * n));
+      HVE_HIP(hipMemcpyAsync(dm, mine.data(), sizeof(int64_t) * n, hipMemcpyHostToDevice, st_));
+      dc_.allgather(dm, da, sizeof(int64_t) * n, st_);
+      HVE_HIP(hipMemcpyAsync(all.data(), da, sizeof(int64_t) * n * n, hipMemcpyDeviceToHost, st_));
+      HVE_HIP(hipStreamSynchronize(st_));
+      (void)hipFree(dm);
+      (void)hipFree(da);
+    }
+    // all[p * n + q] = bytes p sends to q
+    std::vector<size_t> soff(n + 1, 0), roff(n + 1, 0);
+    for (int p = 0; p < n; ++p) {
+      soff[p + 1] = soff[p] + (p == r ? 0 : (size_t)all[(size_t)r * n + p]);
+      roff[p + 1] = roff[p] + (p == r ? 0 : (size_t)all[(size_t)p * n + r]);
+    }
+    char *ds = nullptr, *dr = nullptr;
+    HVE_HIP(hipMalloc((void**)&ds, std::max<size_t>(1, soff[n])));
+    HVE_HIP(hipMalloc((void**)&dr, std::max<size_t>(1, roff[n])));
+    std::vector<P2PMsg> sends, recvs;
+    for (int p = 0; p < n; ++p) {
+      if (p == r) continue;
+      const size_t sb = soff[p + 1] - soff[p], rb = roff[p + 1] - roff[p];
+      if (sb) {
+        HVE_HIP(hipMemcpyAsync(ds + soff[p], send[p].data(), sb, hipMemcpyHostToDevice, st_));
+        sends.push_back({p, ds + soff[p], sb});
+      }
+      if (rb) recvs.push_back({p, dr + roff[p], rb});
+    }
+    dc_.exchange(sends, recvs, st_);
+    recv.assign(n, {});
+    for (int p = 0; p < n; ++p) {
+      if (p == r) {
+        recv[p] = send[p];
+        continue;
+      }
+      recv[p].resize(roff[p + 1] - roff[p]);
+      if (!recv[p].empty())
+        HVE_HIP(hipMemcpyAsync(recv[p].data(), dr + roff[p], recv[p].size(), hipMemcpyDeviceToHost, st_));
+    }
+    HVE_HIP(hipStreamSynchronize(st_));
+    (void)hipFree(ds);
+    (void)hipFree(dr);
+  }
+
+  std::vector<int64_t> allgather(int64_t v) override {
+    const int n = size_;
+    std::vector<int64_t> out(n);
+    int64_t *dm = nullptr, *da = nullptr;
+    HVE_HIP(hipMalloc((void**)&dm, sizeof(int64_t)));
+    HVE_HIP(hipMalloc((void**)&da, sizeof(int64_t) * n));
+    HVE_HIP(hipMemcpyAsync(dm, &v, sizeof(int64_t), hipMemcpyHostToDevice, st_));
+    dc_.allgather(dm, da, sizeof(int64_t), st_);
+    HVE_HIP(hipMemcpyAsync(out.data(), da, sizeof(int64_t) * n, hipMemcpyDeviceToHost, st_));
+    HVE_HIP(hipStreamSynchronize(st_));
+    (void)hipFree(dm);
+    (void)hipFree(da);
+    return out;
+  }
+
+ private:
+  DevComm& dc_;
+  hipStream_t st_ = nullptr;
+};
+
+// Multi-rank setup path: every rank sets up its own rows (dsetup.cpp) where
+// the parameters allow it, the rank-0 gather (setup_multi) otherwise.
+// HVE_SETUP=gather forces the gather path.
+static bool use_dist_setup(const AMGParams& prm) {
+  const char* e = getenv("HVE_SETUP");
+  if (e && std::string(e) == "gather") return false;
+  return dist_setup_supported(prm);
+}
+
+static void setup_dist(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
+  DevHostComm hc(*A->comm->dc);
+  s->H = Hierarchy();
+  std::string log;
+  if (amg_setup_dist(A->diag, A->first_row, s->prm, hc, s->RH, &log) != 0)
+    throw std::runtime_error("distributed setup refused its parameters");
+  if (s->prm.print_level > 0) fputs(log.c_str(), stderr);
+}
+
 extern "C" {
 
 HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVector b, HYPRE_ParVector x) {
@@ -862,7 +976,8 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
   API_BEGIN
   s->comm = A->comm;
   if (A->multi()) {
-    setup_multi(s, A);
+    if (use_dist_setup(s->prm)) setup_dist(s, A);
+    else setup_multi(s, A);
   } else {
     amg_setup(A->diag, s->prm, s->H);
     single_rank_hierarchy(s->H, s->RH);
@@ -920,20 +1035,31 @@ HYPRE_Int hypreve_BoomerAMGGetComplexities(HYPRE_Solver s, HYPRE_Real* grid, HYP
   if (cycle) {
     // par_cycle.c op count: one smoothing sweep costs nnz(A_l)
     double ops = 0;
-    const int nl = (int)s->H.lev.size();
+    const bool dist = s->H.lev.empty();
+    const int nl = dist ? (int)s->RH.nnz_A.size() : (int)s->H.lev.size();
+    const AMGParams& p = dist ? s->RH.prm : s->H.prm;
+    auto nnz = [&](int l) { return dist ? (double)s->RH.nnz_A[l] : (double)s->H.lev[l].A.nnz(); };
     for (int l = 0; l < nl; ++l) {
-      const double nz = (double)s->H.lev[l].A.nnz();
+      const double nz = nnz(l);
       if (nl == 1) ops += nz;
-      else if (l < nl - 1) ops += nz * (s->H.prm.num_sweeps[1] + s->H.prm.num_sweeps[2]);
-      else ops += nz * s->H.prm.num_sweeps[3];
+      else if (l < nl - 1) ops += nz * (p.num_sweeps[1] + p.num_sweeps[2]);
+      else ops += nz * p.num_sweeps[3];
     }
-    *cycle = nl ? ops / (double)s->H.lev[0].A.nnz() : 0.0;
+    *cycle = nl ? ops / nnz(0) : 0.0;
   }
   return 0;
 }
 HYPRE_Int hypreve_BoomerAMGGetLevelInfo(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int* rows, int64_t* nnz_A,
                                         int64_t* nnz_P) {
-  CHECK_ARG(s && level >= 0 && level < (int)s->H.lev.size(), 2);
+  CHECK_ARG(s, 1);
+  if (s->H.lev.empty()) {  // distributed setup: global rows / nnz of A only
+    CHECK_ARG(level >= 0 && level < (int)s->RH.rows.size(), 2);
+    if (rows) *rows = (int)s->RH.rows[level];
+    if (nnz_A) *nnz_A = s->RH.nnz_A[level];
+    if (nnz_P) *nnz_P = -1;
+    return 0;
+  }
+  CHECK_ARG(level >= 0 && level < (int)s->H.lev.size(), 2);
   const Level& L = s->H.lev[level];
   if (rows) *rows = L.A.nrows;
   if (nnz_A) *nnz_A = L.A.nnz();
@@ -976,7 +1102,7 @@ HYPRE_Int hypreve_BoomerAMGGetCoarseMatrix(HYPRE_Solver s, HYPRE_Int* n, HYPRE_R
 }
 HYPRE_Int hypreve_BoomerAMGGetRelaxInfo(HYPRE_Solver s, HYPRE_Int* rt, HYPRE_Int* ns, HYPRE_Real* w, HYPRE_Int* misc) {
   CHECK_ARG(s, 1);
-  const AMGParams& p = s->H.lev.empty() ? s->prm : s->H.prm;
+  const AMGParams& p = s->H.lev.empty() ? (s->RH.lev.empty() ? s->prm : s->RH.prm) : s->H.prm;
   for (int i = 0; i < 4; ++i) { if (rt) rt[i] = p.relax_type[i]; if (ns) ns[i] = p.num_sweeps[i]; }
   if (w) { w[0] = p.relax_weight; w[1] = p.outer_weight; }
   if (misc) { misc[0] = p.relax_order; misc[1] = p.cycle_type; misc[2] = p.num_blocks; }

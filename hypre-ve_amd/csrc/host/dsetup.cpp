@@ -1,0 +1,772 @@
+// Distributed BoomerAMG setup (see dsetup.hpp).
+#include "dsetup.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <stdexcept>
+#include <thread>
+
+#include "layout.hpp"
+
+namespace hve {
+
+namespace {
+
+int owner_of(const std::vector<int>& starts, int g) {
+  auto it = std::upper_bound(starts.begin(), starts.end(), g);
+  return (int)(it - starts.begin()) - 1;
+}
+
+void sort_unique(std::vector<int>& v) {
+  std::sort(v.begin(), v.end());
+  v.erase(std::unique(v.begin(), v.end()), v.end());
+}
+
+// Ghost values of a fixed list of off-rank points: who owns which, and which
+// of my points each peer reads.  pull: owner values -> ghost copies; push:
+// ghost-side contributions -> owners (combined by the caller's rule).
+struct GhostPlan {
+  int first = 0, nloc = 0;
+  std::vector<int> want;                // sorted unique off-rank global indices
+  std::vector<int> off;                 // size + 1: want[off[p] .. off[p+1]) owned by p
+  std::vector<std::vector<int>> send;   // send[p]: my local indices p reads, in p's order
+
+  void build(std::vector<int> w, int first_, int nloc_, const std::vector<int>& starts, HostComm& c) {
+    first = first_;
+    nloc = nloc_;
+    sort_unique(w);
+    want.swap(w);
+    const int size = c.size();
+    off.assign(size + 1, 0);
+    for (int p = 0; p <= size; ++p)
+      off[p] = (int)(std::lower_bound(want.begin(), want.end(), starts[p]) - want.begin());
+    std::vector<std::vector<int>> req(size), got;
+    for (int p = 0; p < size; ++p) req[p].assign(want.begin() + off[p], want.begin() + off[p + 1]);
+    c.exchange(req, got);
+    send.assign(size, {});
+    for (int p = 0; p < size; ++p) {
+      send[p].resize(got[p].size());
+      for (size_t k = 0; k < got[p].size(); ++k) send[p][k] = got[p][k] - first;
+    }
+  }
+  int find(int g) const {
+    auto it = std::lower_bound(want.begin(), want.end(), g);
+    return (it != want.end() && *it == g) ? (int)(it - want.begin()) : -1;
+  }
+  template <typename T>
+  void pull(const T* owned, std::vector<T>& ghost, HostComm& c) const {
+    const int size = c.size();
+    std::vector<std::vector<T>> sv(size), rv;
+    for (int p = 0; p < size; ++p) {
+      sv[p].resize(send[p].size());
+      for (size_t k = 0; k < send[p].size(); ++k) sv[p][k] = owned[send[p][k]];
+    }
+    c.exchange(sv, rv);
+    ghost.assign(want.size(), T());
+    for (int p = 0; p < size; ++p)
+      for (size_t k = 0; k < rv[p].size(); ++k) ghost[off[p] + k] = rv[p][k];
+  }
+  template <typename T, typename F>
+  void push(const std::vector<T>& ghost, T* owned, F combine, HostComm& c) const {
+    const int size = c.size();
+    std::vector<std::vector<T>> sv(size), rv;
+    for (int p = 0; p < size; ++p) sv[p].assign(ghost.begin() + off[p], ghost.begin() + off[p + 1]);
+    c.exchange(sv, rv);
+    for (int p = 0; p < size; ++p)
+      for (size_t k = 0; k < rv[p].size(); ++k) {
+        T& o = owned[send[p][k]];
+        o = combine(o, rv[p][k]);
+      }
+  }
+};
+
+// Rows `rows` (sorted unique, all off-rank) of the distributed matrix whose
+// local rows are M (global columns), fetched from their owners; the result's
+// rows follow `rows`, columns stay global.
+CSR fetch_rows(const CSR& M, int first, const std::vector<int>& starts, const std::vector<int>& rows, HostComm& c) {
+  const int size = c.size();
+  std::vector<std::vector<int>> req(size), got;
+  for (int g : rows) req[owner_of(starts, g)].push_back(g);
+  c.exchange(req, got);
+  std::vector<std::vector<int>> len(size), cols(size);
+  std::vector<std::vector<double>> vals(size);
+  for (int p = 0; p < size; ++p)
+    for (int g : got[p]) {
+      const int r = g - first;
+      len[p].push_back(M.i[r + 1] - M.i[r]);
+      cols[p].insert(cols[p].end(), M.j.begin() + M.i[r], M.j.begin() + M.i[r + 1]);
+      vals[p].insert(vals[p].end(), M.a.begin() + M.i[r], M.a.begin() + M.i[r + 1]);
+    }
+  std::vector<std::vector<int>> rlen, rcols;
+  std::vector<std::vector<double>> rvals;
+  c.exchange(len, rlen);
+  c.exchange(cols, rcols);
+  c.exchange(vals, rvals);
+  CSR G;
+  G.resize_rows((int)rows.size(), M.ncols);
+  int q = 0;
+  for (int p = 0; p < size; ++p)
+    for (int l : rlen[p]) { G.i[q + 1] = G.i[q] + l; ++q; }
+  G.j.reserve(G.i[q]);
+  G.a.reserve(G.i[q]);
+  for (int p = 0; p < size; ++p) {
+    G.j.insert(G.j.end(), rcols[p].begin(), rcols[p].end());
+    G.a.insert(G.a.end(), rvals[p].begin(), rvals[p].end());
+  }
+  return G;
+}
+
+// Index of global point g in the universe [owned (first .. first+n) | ghosts
+// (sorted)]; -1 when absent.
+struct Universe {
+  int first = 0, n = 0;
+  std::vector<int> ghosts;  // sorted unique off-rank
+  int size() const { return n + (int)ghosts.size(); }
+  int loc(int g) const {
+    if (g >= first && g < first + n) return g - first;
+    auto it = std::lower_bound(ghosts.begin(), ghosts.end(), g);
+    return (it != ghosts.end() && *it == g) ? n + (int)(it - ghosts.begin()) : -1;
+  }
+  int glob(int u) const { return u < n ? first + u : ghosts[u - n]; }
+};
+
+// rows of `M` (global columns) -> universe columns; absent columns throw
+void map_cols(CSR& M, const Universe& U) {
+  for (auto& c : M.j) {
+    const int l = U.loc(c);
+    if (l < 0) throw std::runtime_error("distributed setup: column outside the ghost universe");
+    c = l;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// PMIS (coarsen_type 8), setup.cpp coarsen_pmis with cf_init 0, distributed.
+// ---------------------------------------------------------------------------
+void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& starts, HostComm& comm,
+               std::vector<int>& cf) {
+  const int size = comm.size();
+  std::vector<int> mcount(n, 0);
+  std::vector<std::vector<int>> contrib(size), got;
+  for (int c : S.j) {
+    if (c >= first && c < first + n) mcount[c - first]++;
+    else contrib[owner_of(starts, c)].push_back(c);
+  }
+  comm.exchange(contrib, got);
+  for (int p = 0; p < size; ++p)
+    for (int g : got[p]) mcount[g - first]++;
+  std::vector<double> measure(n);
+  for (int r = 0; r < n; ++r) {
+    measure[r] = (double)mcount[r];
+    measure[r] += hypre_rand_at((int64_t)first + r, 2747);  // par_indepset.c:25 at the global row
+  }
+  std::vector<int> off;
+  for (int c : S.j)
+    if (c < first || c >= first + n) off.push_back(c);
+  GhostPlan gp;
+  gp.build(off, first, n, starts, comm);
+  // S entries as local (>= 0) or ghost (-1 - position) indices
+  std::vector<int> sidx(S.j.size());
+  for (size_t k = 0; k < S.j.size(); ++k) {
+    const int c = S.j[k];
+    sidx[k] = (c >= first && c < first + n) ? c - first : -1 - gp.find(c);
+  }
+  cf.assign(n, 0);
+  std::vector<int> graph, graph2;
+  for (int r = 0; r < n; ++r) {
+    if (S.i[r + 1] - S.i[r] == 0) {
+      cf[r] = SF_PT;
+      measure[r] = 0;
+    } else {
+      graph.push_back(r);
+    }
+  }
+  std::vector<double> gmeas;
+  std::vector<int> gcf, gdem;
+  while (comm.allreduce_sum((int64_t)graph.size()) > 0) {
+    gp.pull(measure.data(), gmeas, comm);
+    const int gs = (int)graph.size();
+#pragma omp parallel for schedule(static)
+    for (int ig = 0; ig < gs; ++ig) {
+      const int i = graph[ig];
+      if (measure[i] > 1) cf[i] = 1;
+    }
+    gdem.assign(gp.want.size(), 0);
+#pragma omp parallel for schedule(static)
+    for (int ig = 0; ig < gs; ++ig) {
+      const int i = graph[ig];
+      if (measure[i] > 1) {
+        for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
+          const int j = sidx[k];
+          const double mj = j >= 0 ? measure[j] : gmeas[-1 - j];
+          if (mj > 1) {
+            if (measure[i] > mj) {
+              if (j >= 0) {
+#pragma omp atomic write
+                cf[j] = 0;
+              } else {
+#pragma omp atomic write
+                gdem[-1 - j] = 1;
+              }
+            } else if (mj > measure[i]) {
+#pragma omp atomic write
+              cf[i] = 0;
+            }
+          }
+        }
+      }
+    }
+    gp.push(gdem, cf.data(), [](int cur, int flag) { return flag ? 0 : cur; }, comm);
+    gp.pull(cf.data(), gcf, comm);
+#pragma omp parallel for schedule(static)
+    for (int ig = 0; ig < gs; ++ig) {
+      const int i = graph[ig];
+      if (measure[i] < 1) cf[i] = F_PT;
+      if (cf[i] > 0) {
+        cf[i] = C_PT;
+      } else {
+        for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
+          const int j = sidx[k];
+          int cj;
+          if (j >= 0) {
+#pragma omp atomic read
+            cj = cf[j];
+          } else {
+            cj = gcf[-1 - j];
+          }
+          if (cj > 0) { cf[i] = F_PT; break; }
+        }
+      }
+    }
+    graph2.clear();
+    for (int ig = 0; ig < gs; ++ig) {
+      const int i = graph[ig];
+      if (cf[i] != 0) measure[i] = 0;
+      else graph2.push_back(i);
+    }
+    graph.swap(graph2);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Ext+i rows of the owned fine points (extpi_core over owned + ghost points).
+// ---------------------------------------------------------------------------
+void extpi_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, int first, int n,
+                const std::vector<int>& starts, const std::vector<int>& cstarts, double strong_threshold,
+                double max_row_sum, HostComm& comm, CSR& P) {
+  const int rank = comm.rank(), size = comm.size();
+  std::vector<int> f2c(n, -1);
+  int cc = cstarts[rank];
+  for (int i = 0; i < n; ++i)
+    if (cf[i] >= 0) f2c[i] = cc++;
+  // G1: off-rank neighbours of owned rows (their A and S rows are read)
+  std::vector<int> g1;
+  for (int c : A.j)
+    if (c < first || c >= first + n) g1.push_back(c);
+  sort_unique(g1);
+  CSR AG1 = fetch_rows(A, first, starts, g1, comm);
+  Pattern SG1;
+  create_strength(AG1, strong_threshold, max_row_sum, SG1);
+  // G2: off-rank points the G1 rows reference
+  std::vector<int> gh = g1;
+  for (int c : AG1.j)
+    if (c < first || c >= first + n) gh.push_back(c);
+  sort_unique(gh);
+  Universe U;
+  U.first = first;
+  U.n = n;
+  U.ghosts = gh;
+  GhostPlan gp;
+  gp.build(gh, first, n, starts, comm);
+  std::vector<int> gcf, gf2c;
+  gp.pull(cf.data(), gcf, comm);
+  gp.pull(f2c.data(), gf2c, comm);
+  const int nU = U.size();
+  std::vector<int> cfU(nU), f2cU(nU);
+  for (int i = 0; i < n; ++i) { cfU[i] = cf[i]; f2cU[i] = f2c[i]; }
+  for (size_t k = 0; k < gh.size(); ++k) { cfU[n + k] = gcf[k]; f2cU[n + k] = gf2c[k]; }
+  // A and S over the universe: rows of owned points and of G1, others empty
+  CSR AU;
+  AU.resize_rows(nU, nU);
+  Pattern SU;
+  SU.n = nU;
+  SU.i.assign(nU + 1, 0);
+  std::vector<int> g1pos(g1.size());
+  for (size_t k = 0; k < g1.size(); ++k) g1pos[k] = U.loc(g1[k]);
+  {
+    std::vector<int> rowlenA(nU, 0), rowlenS(nU, 0);
+    for (int i = 0; i < n; ++i) { rowlenA[i] = A.i[i + 1] - A.i[i]; rowlenS[i] = S.i[i + 1] - S.i[i]; }
+    for (size_t k = 0; k < g1.size(); ++k) {
+      rowlenA[g1pos[k]] = AG1.i[k + 1] - AG1.i[k];
+      rowlenS[g1pos[k]] = SG1.i[k + 1] - SG1.i[k];
+    }
+    for (int u = 0; u < nU; ++u) { AU.i[u + 1] = AU.i[u] + rowlenA[u]; SU.i[u + 1] = SU.i[u] + rowlenS[u]; }
+    AU.j.resize(AU.i[nU]);
+    AU.a.resize(AU.i[nU]);
+    SU.j.resize(SU.i[nU]);
+    for (int i = 0; i < n; ++i) {
+      std::copy(A.j.begin() + A.i[i], A.j.begin() + A.i[i + 1], AU.j.begin() + AU.i[i]);
+      std::copy(A.a.begin() + A.i[i], A.a.begin() + A.i[i + 1], AU.a.begin() + AU.i[i]);
+      std::copy(S.j.begin() + S.i[i], S.j.begin() + S.i[i + 1], SU.j.begin() + SU.i[i]);
+    }
+    for (size_t k = 0; k < g1.size(); ++k) {
+      const int u = g1pos[k];
+      std::copy(AG1.j.begin() + AG1.i[k], AG1.j.begin() + AG1.i[k + 1], AU.j.begin() + AU.i[u]);
+      std::copy(AG1.a.begin() + AG1.i[k], AG1.a.begin() + AG1.i[k + 1], AU.a.begin() + AU.i[u]);
+      std::copy(SG1.j.begin() + SG1.i[k], SG1.j.begin() + SG1.i[k + 1], SU.j.begin() + SU.i[u]);
+    }
+  }
+  map_cols(AU, U);
+  for (auto& c : SU.j) {
+    const int l = U.loc(c);
+    if (l < 0) throw std::runtime_error("distributed setup: strength column outside the ghost universe");
+    c = l;
+  }
+  int64_t ncoarse = cstarts[size];
+  extpi_core(AU, SU, cfU, f2cU, n, (int)ncoarse, nU, P);
+}
+
+// ---------------------------------------------------------------------------
+// R = P^T rows of the owned coarse points: every P entry goes to the owner of
+// its coarse column; rows list fine indices ascending (csr_matop.c:578).
+// ---------------------------------------------------------------------------
+void transpose_dist(const CSR& P, int first, int nfine_glob, const std::vector<int>& cstarts, HostComm& comm,
+                    CSR& R) {
+  const int rank = comm.rank(), size = comm.size();
+  std::vector<std::vector<int>> sic(size), sfi(size), ric, rfi;
+  std::vector<std::vector<double>> sva(size), rva;
+  for (int i = 0; i < P.nrows; ++i)
+    for (int k = P.i[i]; k < P.i[i + 1]; ++k) {
+      const int q = owner_of(cstarts, P.j[k]);
+      sic[q].push_back(P.j[k]);
+      sfi[q].push_back(first + i);
+      sva[q].push_back(P.a[k]);
+    }
+  comm.exchange(sic, ric);
+  comm.exchange(sfi, rfi);
+  comm.exchange(sva, rva);
+  const int c0 = cstarts[rank], nc = cstarts[rank + 1] - c0;
+  R.resize_rows(nc, nfine_glob);
+  for (int p = 0; p < size; ++p)
+    for (int ic : ric[p]) R.i[ic - c0 + 1]++;
+  for (int r = 0; r < nc; ++r) R.i[r + 1] += R.i[r];
+  R.j.resize(R.i[nc]);
+  R.a.resize(R.i[nc]);
+  std::vector<int> pos(R.i.begin(), R.i.end() - 1);
+  // senders in rank order hold ascending fine rows, each in row order
+  for (int p = 0; p < size; ++p)
+    for (size_t k = 0; k < ric[p].size(); ++k) {
+      const int r = ric[p][k] - c0;
+      R.j[pos[r]] = rfi[p][k];
+      R.a[pos[r]] = rva[p][k];
+      pos[r]++;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Coarse operator rows of the owned coarse points (rap_core).
+// ---------------------------------------------------------------------------
+void rap_dist(const CSR& R, const CSR& A, const CSR& P, int first, const std::vector<int>& starts,
+              const std::vector<int>& cstarts, HostComm& comm, CSR& Ac) {
+  const int rank = comm.rank(), size = comm.size();
+  const int n = A.nrows;
+  // F1: off-rank fine rows R reads (their A rows are needed)
+  std::vector<int> f1;
+  for (int c : R.j)
+    if (c < first || c >= first + n) f1.push_back(c);
+  sort_unique(f1);
+  CSR AF1 = fetch_rows(A, first, starts, f1, comm);
+  // F2: off-rank columns of the A rows of owned and F1 points (their P rows)
+  std::vector<int> f2;
+  for (int c : A.j)
+    if (c < first || c >= first + n) f2.push_back(c);
+  for (int c : AF1.j)
+    if (c < first || c >= first + n) f2.push_back(c);
+  sort_unique(f2);
+  CSR PF2 = fetch_rows(P, first, starts, f2, comm);
+  Universe UF;
+  UF.first = first;
+  UF.n = n;
+  UF.ghosts = f1;
+  UF.ghosts.insert(UF.ghosts.end(), f2.begin(), f2.end());
+  sort_unique(UF.ghosts);
+  const int nUF = UF.size();
+  // coarse universe: owned coarse points, then the off-rank ones P rows reach
+  Universe UC;
+  UC.first = cstarts[rank];
+  UC.n = cstarts[rank + 1] - cstarts[rank];
+  for (int c : P.j)
+    if (c < UC.first || c >= UC.first + UC.n) UC.ghosts.push_back(c);
+  for (int c : PF2.j)
+    if (c < UC.first || c >= UC.first + UC.n) UC.ghosts.push_back(c);
+  sort_unique(UC.ghosts);
+  const int nUC = UC.size();
+  std::vector<int> coarse_glob(nUC);
+  for (int u = 0; u < nUC; ++u) coarse_glob[u] = UC.glob(u);
+  // fine-universe A (owned + F1 rows) and P (owned + F2 rows)
+  auto assemble = [&](const CSR& own, const CSR& ghost, const std::vector<int>& grows, CSR& out) {
+    out.resize_rows(nUF, own.ncols);
+    std::vector<int> gpos(grows.size());
+    std::vector<int> len(nUF, 0);
+    for (int i = 0; i < n; ++i) len[i] = own.i[i + 1] - own.i[i];
+    for (size_t k = 0; k < grows.size(); ++k) {
+      gpos[k] = UF.loc(grows[k]);
+      len[gpos[k]] = ghost.i[k + 1] - ghost.i[k];
+    }
+    for (int u = 0; u < nUF; ++u) out.i[u + 1] = out.i[u] + len[u];
+    out.j.resize(out.i[nUF]);
+    out.a.resize(out.i[nUF]);
+    for (int i = 0; i < n; ++i) {
+      std::copy(own.j.begin() + own.i[i], own.j.begin() + own.i[i + 1], out.j.begin() + out.i[i]);
+      std::copy(own.a.begin() + own.i[i], own.a.begin() + own.i[i + 1], out.a.begin() + out.i[i]);
+    }
+    for (size_t k = 0; k < grows.size(); ++k) {
+      std::copy(ghost.j.begin() + ghost.i[k], ghost.j.begin() + ghost.i[k + 1], out.j.begin() + out.i[gpos[k]]);
+      std::copy(ghost.a.begin() + ghost.i[k], ghost.a.begin() + ghost.i[k + 1], out.a.begin() + out.i[gpos[k]]);
+    }
+  };
+  CSR AU, PU;
+  assemble(A, AF1, f1, AU);
+  assemble(P, PF2, f2, PU);
+  // A rows of F2-only points are empty; their columns never get visited.
+  map_cols(AU, UF);
+  for (auto& c : PU.j) {
+    const int l = UC.loc(c);
+    if (l < 0) throw std::runtime_error("distributed setup: coarse column outside the ghost universe");
+    c = l;
+  }
+  CSR RU = R;
+  map_cols(RU, UF);
+  std::vector<int> row_ic(R.nrows);
+  for (int q = 0; q < R.nrows; ++q) row_ic[q] = q;
+  rap_core(RU, AU, PU, row_ic, coarse_glob, nUF, nUC, cstarts[size], Ac);
+}
+
+// l1 norms of the owned rows (setup.cpp compute_l1_norms with global indices).
+void l1_dist(const CSR& A, int first, int nglob, int option, const std::vector<int>* cf, const GhostPlan* gp,
+             const std::vector<int>* gcf, int num_blocks, std::vector<double>& l1) {
+  const int n = A.nrows;
+  l1.assign(n, 0.0);
+  const int nb = std::max(1, num_blocks);
+  const int bsize = nglob / nb, rest = nglob - bsize * nb;
+  auto cf_of = [&](int c) -> int {
+    if (c >= first && c < first + n) return (*cf)[c - first];
+    return (*gcf)[gp->find(c)];
+  };
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    const int gi = first + i;
+    int k;  // hypre's block of global row gi (par_relax.c size / rest partition)
+    if (gi < rest * (bsize + 1)) k = gi / (bsize + 1);
+    else k = rest + (gi - rest * (bsize + 1)) / std::max(1, bsize);
+    int ns, ne;
+    if (k < rest) { ns = k * bsize + k; ne = (k + 1) * bsize + k + 1; }
+    else { ns = k * bsize + rest; ne = (k + 1) * bsize + rest; }
+    double s = 0.0;
+    if (option == 1) {
+      for (int q = A.i[i]; q < A.i[i + 1]; ++q)
+        if (!cf || (*cf)[i] == cf_of(A.j[q])) s += std::fabs(A.a[q]);
+    } else if (option == 4) {
+      double diag = 0.0;
+      for (int q = A.i[i]; q < A.i[i + 1]; ++q) {
+        const int c = A.j[q];
+        if ((c == gi || c < ns || c >= ne) && (!cf || (*cf)[i] == cf_of(c))) {
+          if (c == gi) { diag = std::fabs(A.a[q]); s += std::fabs(A.a[q]); }
+          else s += 0.5 * std::fabs(A.a[q]);
+        }
+      }
+      if (s <= 4.0 / 3.0 * diag) s = diag;
+    }
+    l1[i] = s;
+  }
+  for (int i = 0; i < n; ++i)
+    if (A.a[A.i[i]] < 0.0) l1[i] = -l1[i];
+}
+
+bool uses_l1_gs(int t) { return t == 8 || t == 13 || t == 14; }
+
+struct DLevel {
+  CSR A, P, R;  // owned rows, global columns
+  std::vector<int> cf;
+  std::vector<double> l1;
+  std::vector<int> starts;  // row starts of this level over the ranks
+  int first = 0, nloc = 0, nglob = 0;
+  int64_t nnz_glob = 0;
+};
+
+// Halo of a vector owned in `starts` with the given off-rank reads: the
+// RankHalo partition_all builds (peers ascending, per-peer counts, the local
+// indices each peer reads).
+RankHalo make_halo(const std::vector<int>& halo, int first, int nloc, const std::vector<int>& starts, HostComm& comm) {
+  const int rank = comm.rank(), size = comm.size();
+  RankHalo h;
+  h.n_loc = nloc;
+  h.n_halo = (int)halo.size();
+  h.halo_glob = halo;
+  std::vector<std::vector<int>> req(size), got;
+  for (int g : halo) req[owner_of(starts, g)].push_back(g);
+  comm.exchange(req, got);
+  for (int p = 0; p < size; ++p) {
+    if (p == rank) continue;
+    const int rc = (int)req[p].size(), sc = (int)got[p].size();
+    if (rc == 0 && sc == 0) continue;
+    h.peers.push_back(p);
+    h.recv_cnt.push_back(rc);
+    h.send_cnt.push_back(sc);
+    for (int g : got[p]) h.send_idx.push_back(g - first);
+  }
+  return h;
+}
+
+void offrank_cols(const CSR& M, int a, int b, std::vector<int>& out) {
+  for (int c : M.j)
+    if (c < a || c >= b) out.push_back(c);
+}
+
+}  // namespace
+
+bool dist_setup_supported(const AMGParams& prm, std::string* why) {
+  auto no = [&](const char* w) { if (why) *why = w; return false; };
+  if (prm.coarsen_type != 8) return no("coarsen_type != 8 (PMIS)");
+  if (prm.interp_type != 6) return no("interp_type != 6 (ext+i)");
+  if (prm.agg_num_levels > 0) return no("aggressive coarsening");
+  return true;
+}
+
+int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostComm& comm, RankHierarchy& out,
+                   std::string* log) {
+  if (!dist_setup_supported(prm_in)) return 1;
+  const int rank = comm.rank(), size = comm.size();
+  AMGParams prm = prm_in;
+  std::vector<DLevel> L(1);
+  L[0].A = A0;
+  {
+    auto cnt = comm.allgather(A0.nrows);
+    L[0].starts.assign(size + 1, 0);
+    for (int p = 0; p < size; ++p) L[0].starts[p + 1] = L[0].starts[p] + (int)cnt[p];
+    if (L[0].starts[rank] != first_row) throw std::runtime_error("distributed setup: row blocks out of rank order");
+    L[0].first = first_row;
+    L[0].nloc = A0.nrows;
+    L[0].nglob = L[0].starts[size];
+  }
+  int level = 0;
+  bool finished = prm.max_levels <= 1;
+  char buf[256];
+  while (!finished) {
+    const int n = L[level].nloc, first = L[level].first, fine_size = L[level].nglob;
+    Pattern S;
+    create_strength(L[level].A, prm.strong_threshold, prm.max_row_sum, S);
+    std::vector<int> cf;
+    pmis_dist(S, first, n, L[level].starts, comm, cf);
+    int64_t nc_loc = 0;
+    for (int v : cf) nc_loc += (v == C_PT);
+    const auto ncs = comm.allgather(nc_loc);
+    int64_t coarse_size = 0;
+    for (auto v : ncs) coarse_size += v;
+    if (coarse_size == 0 || coarse_size == fine_size) {
+      if (prm.relax_type[3] == 9 || prm.relax_type[3] == 99 || prm.relax_type[3] == 19 || prm.relax_type[3] == 98) {
+        prm.relax_type[3] = prm.relax_type[0];
+        prm.num_sweeps[3] = 1;
+      }
+      break;
+    }
+    if (coarse_size < prm.min_coarse_size) break;
+    std::vector<int> cstarts(size + 1, 0);
+    for (int p = 0; p < size; ++p) cstarts[p + 1] = cstarts[p] + (int)ncs[p];
+    CSR P;
+    extpi_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm.strong_threshold, prm.max_row_sum, comm, P);
+    if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
+    for (int i = 0; i < n; ++i)
+      if (cf[i] == SF_PT) cf[i] = F_PT;
+    CSR R;
+    transpose_dist(P, first, fine_size, cstarts, comm, R);
+    CSR Ac;
+    rap_dist(R, L[level].A, P, first, L[level].starts, cstarts, comm, Ac);
+    snprintf(buf, sizeof buf, "rank %d level %d: rows %d/%d -> coarse %d/%lld\n", rank, level, n, fine_size,
+             (int)ncs[rank], (long long)coarse_size);
+    if (log) *log += buf;
+    L[level].cf.swap(cf);
+    L[level].P.swap(P);
+    L[level].R.swap(R);
+    L.emplace_back();
+    DLevel& C = L[level + 1];
+    C.A.swap(Ac);
+    C.starts = cstarts;
+    C.first = cstarts[rank];
+    C.nloc = (int)ncs[rank];
+    C.nglob = (int)coarse_size;
+    ++level;
+    if (prm.coarsen_type > 0 && coarse_size >= (int64_t)(fine_size * 0.75))
+      throw std::runtime_error("slow coarsening (coarse >= 0.75 fine) would switch to CLJP: unsupported");
+    if (level == prm.max_levels - 1 || coarse_size <= prm.max_coarse_size) finished = true;
+  }
+  const int nl = (int)L.size();
+  for (auto& D : L) D.nnz_glob = comm.allreduce_sum(D.A.nnz());
+  // l1 norms (amg_setup's sequence, global indices)
+  for (int j = 0; j < nl; ++j) {
+    DLevel& D = L[j];
+    // rank-uniform condition (a rank may own no rows of a level, hence an
+    // empty cf): every rank must take part in the same exchanges
+    const bool use_cf = prm.relax_order && j < nl - 1;
+    GhostPlan gp;
+    std::vector<int> gcf;
+    if (use_cf) {
+      std::vector<int> off;
+      offrank_cols(D.A, D.first, D.first + D.nloc, off);
+      gp.build(off, D.first, D.nloc, D.starts, comm);
+      gp.pull(D.cf.data(), gcf, comm);
+    }
+    const std::vector<int>* cfp = use_cf ? &D.cf : nullptr;
+    if (j < nl - 1 && (uses_l1_gs(prm.relax_type[1]) || uses_l1_gs(prm.relax_type[2])))
+      l1_dist(D.A, D.first, D.nglob, 4, cfp, &gp, &gcf, prm.num_blocks, D.l1);
+    else if (j == nl - 1 && uses_l1_gs(prm.relax_type[3]))
+      l1_dist(D.A, D.first, D.nglob, 4, nullptr, nullptr, nullptr, prm.num_blocks, D.l1);
+    if (j < nl - 1 && (prm.relax_type[1] == 18 || prm.relax_type[2] == 18))
+      l1_dist(D.A, D.first, D.nglob, 1, cfp, &gp, &gcf, 1, D.l1);
+    else if (j == nl - 1 && prm.relax_type[3] == 18)
+      l1_dist(D.A, D.first, D.nglob, 1, nullptr, nullptr, nullptr, 1, D.l1);
+    if (prm.relax_type[1] == 7 || prm.relax_type[2] == 7 || (prm.relax_type[3] == 7 && j == nl - 1)) {
+      D.l1.resize(D.nloc);
+      for (int r = 0; r < D.nloc; ++r) {
+        const double d = D.A.a[D.A.i[r]];
+        D.l1[r] = (d == 0.0) ? 1.0 : d;
+      }
+    }
+  }
+  out = RankHierarchy();
+  out.rank = rank;
+  out.size = size;
+  out.prm = prm;
+  // coarsest-level direct solve: the coarsest operator gathered on every rank
+  if (nl > 1 && (prm.relax_type[3] == 9 || prm.relax_type[3] == 99 || prm.relax_type[3] == 19 ||
+                 prm.relax_type[3] == 98)) {
+    const DLevel& D = L[nl - 1];
+    if (D.nglob > 8192) throw std::runtime_error("coarsest level too large for the dense direct solve");
+    std::vector<int> len(D.nloc);
+    for (int r = 0; r < D.nloc; ++r) len[r] = D.A.i[r + 1] - D.A.i[r];
+    auto alen = comm.allgatherv(len);
+    auto acol = comm.allgatherv(D.A.j);
+    auto aval = comm.allgatherv(D.A.a);
+    CSR G;
+    G.resize_rows(D.nglob, D.nglob);
+    for (int r = 0; r < D.nglob; ++r) G.i[r + 1] = G.i[r] + alen[r];
+    G.j.swap(acol);
+    G.a.swap(aval);
+    out.coarse_n = D.nglob;
+    csr_to_dense(G, out.coarse_dense);
+  }
+  double tot_rows = 0, tot_nnz = 0;
+  for (auto& D : L) { tot_rows += D.nglob; tot_nnz += (double)D.nnz_glob; }
+  out.grid_complexity = tot_rows / L[0].nglob;
+  out.operator_complexity = tot_nnz / (double)L[0].nnz_glob;
+  for (auto& D : L) {
+    out.nnz_A.push_back(D.nnz_glob);
+    out.rows.push_back(D.nglob);
+  }
+  // this rank's operators with [local | halo] columns and halo plans
+  std::vector<std::vector<int>> hu(nl), hv(nl);
+  for (int l = 0; l < nl; ++l) {
+    const DLevel& D = L[l];
+    std::vector<int> u;
+    offrank_cols(D.A, D.first, D.first + D.nloc, u);
+    if (l > 0) offrank_cols(L[l - 1].P, D.first, D.first + D.nloc, u);
+    sort_unique(u);
+    hu[l].swap(u);
+    if (l + 1 < nl) {
+      std::vector<int> v;
+      offrank_cols(D.R, D.first, D.first + D.nloc, v);
+      sort_unique(v);
+      hv[l].swap(v);
+    }
+  }
+  out.lev.resize(nl);
+  for (int l = 0; l < nl; ++l) {
+    const DLevel& D = L[l];
+    RankLevel& RL = out.lev[l];
+    RL.n_loc = D.nloc;
+    RL.first = D.first;
+    RL.n_glob = D.nglob;
+    make_rank_op(D.A, 0, D.nloc, D.first, D.first + D.nloc, hu[l], RL.A);
+    if (l + 1 < nl) {
+      const DLevel& C = L[l + 1];
+      make_rank_op(D.P, 0, D.nloc, C.first, C.first + C.nloc, hu[l + 1], RL.P);
+      make_rank_op(D.R, 0, C.nloc, D.first, D.first + D.nloc, hv[l], RL.R);
+    }
+    RL.l1 = D.l1;
+    RL.cf = D.cf;
+    RL.hu = make_halo(hu[l], D.first, D.nloc, D.starts, comm);
+    if (l + 1 < nl) RL.hv = make_halo(hv[l], D.first, D.nloc, D.starts, comm);
+  }
+  return 0;
+}
+
+int dist_setup_self_check(const CSR& A, const AMGParams& prm, int size, std::string& msg) {
+  Hierarchy H;
+  amg_setup(A, prm, H);
+  const int n0 = A.nrows;
+  std::vector<int> s0(size + 1);
+  for (int r = 0; r <= size; ++r) s0[r] = (int)((int64_t)n0 * r / size);
+  std::vector<RankHierarchy> ref;
+  partition_hierarchy_all(H, s0, size, ref);
+  auto comms = make_thread_host_comms(size);
+  std::vector<RankHierarchy> got(size);
+  std::vector<std::string> err(size);
+  std::vector<std::thread> th;
+  for (int r = 0; r < size; ++r) {
+    th.emplace_back([&, r] {
+      try {
+        CSR Ar;
+        Ar.resize_rows(s0[r + 1] - s0[r], A.ncols);
+        for (int i = s0[r]; i < s0[r + 1]; ++i) Ar.i[i - s0[r] + 1] = Ar.i[i - s0[r]] + (A.i[i + 1] - A.i[i]);
+        Ar.j.assign(A.j.begin() + A.i[s0[r]], A.j.begin() + A.i[s0[r + 1]]);
+        Ar.a.assign(A.a.begin() + A.i[s0[r]], A.a.begin() + A.i[s0[r + 1]]);
+        if (amg_setup_dist(Ar, s0[r], prm, *comms[r], got[r]) != 0) err[r] = "unsupported parameters";
+      } catch (const std::exception& e) {
+        err[r] = e.what();
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  int bad = 0;
+  for (int r = 0; r < size; ++r) {
+    if (!err[r].empty()) {
+      msg += "rank " + std::to_string(r) + ": " + err[r] + "\n";
+      ++bad;
+      continue;
+    }
+    std::vector<char> b1, b2;
+    serialize(ref[r], b1);
+    serialize(got[r], b2);
+    if (b1 != b2) {
+      ++bad;
+      msg += "rank " + std::to_string(r) + ": distributed hierarchy differs (levels " +
+             std::to_string(got[r].lev.size()) + " vs " + std::to_string(ref[r].lev.size()) + ")\n";
+      // first differing level / part
+      const size_t nl = std::min(got[r].lev.size(), ref[r].lev.size());
+      for (size_t l = 0; l < nl && msg.size() < 2000; ++l) {
+        const RankLevel &x = got[r].lev[l], &y = ref[r].lev[l];
+        auto cmp = [&](const CSR& p, const CSR& q, const char* what) {
+          if (p.i != q.i || p.j != q.j || p.a != q.a || p.nrows != q.nrows || p.ncols != q.ncols)
+            msg += "  level " + std::to_string(l) + " " + what + " differs\n";
+        };
+        cmp(x.A.interior, y.A.interior, "A.interior");
+        cmp(x.A.boundary, y.A.boundary, "A.boundary");
+        cmp(x.P.interior, y.P.interior, "P.interior");
+        cmp(x.P.boundary, y.P.boundary, "P.boundary");
+        cmp(x.R.interior, y.R.interior, "R.interior");
+        cmp(x.R.boundary, y.R.boundary, "R.boundary");
+        if (x.cf != y.cf) msg += "  level " + std::to_string(l) + " cf differs\n";
+        if (x.l1 != y.l1) msg += "  level " + std::to_string(l) + " l1 differs\n";
+        if (x.hu.send_idx != y.hu.send_idx || x.hu.peers != y.hu.peers || x.hu.halo_glob != y.hu.halo_glob)
+          msg += "  level " + std::to_string(l) + " hu differs\n";
+        if (x.hv.send_idx != y.hv.send_idx || x.hv.peers != y.hv.peers || x.hv.halo_glob != y.hv.halo_glob)
+          msg += "  level " + std::to_string(l) + " hv differs\n";
+      }
+      if (got[r].coarse_dense != ref[r].coarse_dense) msg += "  coarse_dense differs\n";
+      if (got[r].nnz_A != ref[r].nnz_A) msg += "  nnz_A differs\n";
+    }
+  }
+  return bad;
+}
+
+}  // namespace hve

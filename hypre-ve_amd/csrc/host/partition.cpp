@@ -72,6 +72,10 @@ void make_op(const CSR& M, int r0, int r1, int a, int b, const std::vector<int>&
 
 }  // namespace
 
+void make_rank_op(const CSR& M, int r0, int r1, int a, int b, const std::vector<int>& halo, RankOp& op) {
+  make_op(M, r0, r1, a, b, halo, op);
+}
+
 static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, int size,
                           std::vector<RankHierarchy>& out) {
   const int nl = (int)H.lev.size();

@@ -61,6 +61,10 @@ struct RankHierarchy {
 // starts0: level-0 row starts (size+1 entries).
 void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, int rank, int size,
                          RankHierarchy& out);
+// Rows [r0, r1) of M (global columns) as a rank's operator whose input vector
+// is owned on [a, b) with the sorted off-rank reads `halo`: columns in the
+// [local | halo] space, rows split into interior and boundary.
+void make_rank_op(const CSR& M, int r0, int r1, int a, int b, const std::vector<int>& halo, RankOp& op);
 // Every rank's part in one pass (O(global) work; partition_hierarchy
 // partitions all ranks to return one).
 void partition_hierarchy_all(const Hierarchy& H, const std::vector<int>& starts0, int size,

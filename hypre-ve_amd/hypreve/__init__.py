@@ -162,6 +162,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGGetRelaxInfo", _i, [_p, _pi, _pi, _pd, _pi]),
     ("hypreve_BoomerAMGSetupHost", _i, [_p, _p]),
     ("hypreve_BoomerAMGPartitionCheck", _i, [_p, _i]),
+    ("hypreve_BoomerAMGDistSetupCheck", _i, [_p, _p, _i]),
     ("hypreve_BoomerAMGCycle", _i, [_p, _p, _p]),
     ("hypreve_BoomerAMGGetKernelStats", _i, [_p, _pd, _i]),
     ("hypreve_BenchFineSpMV", _i, [_p, _i, _pd, _pd]),
@@ -389,6 +390,9 @@ class BoomerAMG:
 
     def partition_check(self, size):
         check(lib().hypreve_BoomerAMGPartitionCheck(self.h, size), "PartitionCheck")
+
+    def dist_setup_check(self, A, size):
+        check(lib().hypreve_BoomerAMGDistSetupCheck(self.h, A.h, size), "DistSetupCheck")
 
     def setup_host(self, A):
         check(lib().hypreve_BoomerAMGSetupHost(self.h, A.h), "BoomerAMGSetupHost")

@@ -244,6 +244,10 @@ HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver solver, HYPRE_ParCSRMatrix A);
 /* CPU self-check of the row partition of the host hierarchy over `size`
  * ranks: reassembly, pairwise halo plans, emulated distributed apply. */
 HYPRE_Int hypreve_BoomerAMGPartitionCheck(HYPRE_Solver solver, HYPRE_Int size);
+/* CPU self-check of the distributed setup: the one-process matrix A split in
+ * `size` row blocks, set up by `size` host threads exchanging ghost rows,
+ * against the one-process setup partitioned the same way (bytewise). */
+HYPRE_Int hypreve_BoomerAMGDistSetupCheck(HYPRE_Solver solver, HYPRE_ParCSRMatrix A, HYPRE_Int size);
 /* Run exactly one cycle (hypre_BoomerAMGCycle) on device vectors f, u. */
 HYPRE_Int hypreve_BoomerAMGCycle(HYPRE_Solver solver, HYPRE_ParVector f, HYPRE_ParVector u);
 /* Device timing of the last Solve, per kernel class (ms), for bench/profiling. */

@@ -92,6 +92,24 @@ def test_partition_self_check(hv):
         amg.partition_check(size)
 
 
+@pytest.mark.parametrize("size", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("stencil,relax,order", [(7, 18, 0), (7, 0, 1), (27, 18, 0), (7, 13, 0)])
+def test_distributed_setup_matches_one_process(hv, size, stencil, relax, order):
+    """Distributed setup (each rank builds its rows' levels from a ghost
+    layer: PMIS passes exchanging measures / demotions / C-F state, ext+i over
+    fetched neighbour rows, R from P entries sent to their coarse owner, RAP
+    over fetched A and P rows) on `size` host threads: every rank's part of
+    every level equals the one-process hierarchy partitioned the same way,
+    byte for byte (operators, C/F, l1 norms, halo plans, coarsest operator)."""
+    if stencil == 27:
+        A = hv.ParCSRMatrix.laplacian27(17, 15, 19)
+    else:
+        A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=1.0, cy=0.7 if relax == 0 else 1.0, cz=1.0)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=8, interp_type=6, relax_type=relax, relax_order=order, P_max_elmts=4)
+    amg.dist_setup_check(A, size)
+
+
 @pytest.mark.parametrize("coarsen_type", [8, 10])
 def test_gs_level_schedule_matches_sequential_sweep(hv, coarsen_type):
     """Hybrid Gauss-Seidel on the GPU runs each hypre thread block as a level
