@@ -137,12 +137,17 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     spmv_ms, spmv_bytes = amg.bench_fine_spmv(args.spmv_reps)
     achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
     traffic = committed_traffic(n, spmv_bytes)
+    # the box's achievable read bandwidth: a grid-stride 8 B/lane stream over 2 GiB
+    stream_n = (1 << 31) // 8
+    stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 10) * 1e-3) / 1e9
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
             "kernel": "k_sell<OP_RESID> finest level (r = b - A x)", "avg_ms": round(spmv_ms, 4),
-            "bytes_per_launch": spmv_bytes}
+            "bytes_per_launch": spmv_bytes,
+            "stream_read_gbs": round(stream_gbs, 1), "frac_of_stream": round(achieved / stream_gbs, 4)}
     if rank == 0:
         import resource
+        log(f"[bench] read stream {stream_gbs:.0f} GB/s; fine SpMV at {achieved / stream_gbs:.3f} of it")
         log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {spmv_bytes/1e9:.3f} GB -> {achieved:.1f} GB/s; "
             f"host peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6:.1f} GB")
 

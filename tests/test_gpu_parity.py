@@ -109,6 +109,31 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     assert np.array_equal(x.get(), xo)
 
 
+@pytest.mark.parametrize("coef", [(0.001, 1.0, 1.0), (1.0, 1.0, 100.0)])
+def test_anisotropic_solve_bitwise(gpu, orc, coef):
+    """configs[4]'s operator family at test size: anisotropic diffusion
+    (GenerateLaplacian with cx, cy, cz), PMIS + ext+i Pmx 4, l1-Jacobi.  The
+    strong-coupling pattern is one-dimensional, rows of the Galerkin levels are
+    irregular; the GPU iterates equal the oracle's bit for bit."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(28, 26, 24, cx=coef[0], cy=coef[1], cz=coef[2])
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-7, max_iter=60)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup(A)
+    O = orc.OracleAMG(amg)
+    n = A.n
+    rng = np.random.default_rng(31)
+    b_h = rng.standard_normal(n)
+    b = hv.ParVector(n, b_h)
+    x = hv.ParVector(n, np.zeros(n))
+    it, rr = amg.solve(A, b, x)
+    xo = np.zeros(n)
+    st = O.solve(b_h, xo, 1e-7, 60)
+    assert it == st["iterations"]
+    assert np.array_equal(x.get(), xo)
+
+
 def test_matvec_bitwise(gpu, orc):
     hv = gpu
     A, amg, O = setup_pair(hv, orc, (20, 20, 20), coarsen_type=8, relax_type=18)

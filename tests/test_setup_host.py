@@ -110,6 +110,16 @@ def test_distributed_setup_matches_one_process(hv, size, stencil, relax, order):
     amg.dist_setup_check(A, size)
 
 
+@pytest.mark.parametrize("size", [2, 4, 7])
+def test_distributed_setup_anisotropic(hv, size):
+    """configs[4]'s operator family (anisotropic diffusion, strong couplings in
+    one direction only): the distributed setup still equals the one-process one."""
+    A = hv.ParCSRMatrix.laplacian(21, 19, 25, cx=0.001, cy=1.0, cz=1.0)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=8, interp_type=6, relax_type=18, P_max_elmts=4)
+    amg.dist_setup_check(A, size)
+
+
 @pytest.mark.parametrize("coarsen_type", [8, 10])
 def test_gs_level_schedule_matches_sequential_sweep(hv, coarsen_type):
     """Hybrid Gauss-Seidel on the GPU runs each hypre thread block as a level
