@@ -551,28 +551,8 @@ __global__ void __launch_bounds__(64) k_sell_dict(SpArgs p) {
   if (slice * kWave >= p.nrows) return;  // the (single-wave) workgroup is past the end
   const int lane = threadIdx.x;
   const int row = slice * kWave + lane;
-  // 1. x-tile: x[dict[d0 .. d1)] -> LDS, 8 gathers in flight per lane
-  {
-    const int d0 = p.dict_ptr[slice], m = p.dict_ptr[slice + 1] - d0;
-    for (int j0 = 0; j0 < m; j0 += 8 * kWave) {
-      int idx[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int j = j0 + i * kWave + lane;
-        idx[i] = j < m ? mload<NT>(p.dict + d0 + j) : -1;
-      }
-      double v[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = idx[i] >= 0 ? p.x[idx[i]] : 0.0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const int j = j0 + i * kWave + lane;
-        if (j < m) xl[j] = v[i];
-      }
-    }
-  }
-  __syncthreads();
-  // 2. jagged row loop over local columns
+  // Row metadata and the first batch of matrix loads go out before the
+  // x-tile gather, so their latency overlaps it.
   const int blen = mload<NT>(p.rowlen + row);  // 0 past the last row
   const int width = __builtin_amdgcn_readfirstlane(blen);  // sorted: lane 0 is the longest
   const int beg = p.slice_ptr[slice];
@@ -597,25 +577,46 @@ __global__ void __launch_bounds__(64) k_sell_dict(SpArgs p) {
   const double* __restrict__ vp = p.val + beg + lane;
   int P = 0;
   for (int k = 0; k < k0; ++k) P += __popcll(__ballot(k < blen));
-  if (k0 < width) {
-    int c[B];
-    double a[B];
-    dict_load<B, NT>(cp, vp, P, k0, blen, llen, c, a);
-    for (int k = k0; k < width; k += B) {
-      int cn[B];
-      double an[B];
-      dict_load<B, NT>(cp, vp, P, k + B, blen, llen, cn, an);
+  int c[B];
+  double a[B];
+  dict_load<B, NT>(cp, vp, P, k0, blen, llen, c, a);
+  // 1. x-tile: x[dict[d0 .. d1)] -> LDS, TG gathers in flight per lane
+  {
+    constexpr int TG = 16;
+    const int d0 = p.dict_ptr[slice], m = p.dict_ptr[slice + 1] - d0;
+    for (int j0 = 0; j0 < m; j0 += TG * kWave) {
+      int idx[TG];
 #pragma unroll
-      for (int q = 0; q < B; ++q) {
-        if (c[q] >= 0) {
-          const double pr = a[q] * xl[c[q]];
-          if (sub) t -= pr;
-          else t += pr;
-        }
+      for (int i = 0; i < TG; ++i) {
+        const int j = j0 + i * kWave + lane;
+        idx[i] = j < m ? mload<NT>(p.dict + d0 + j) : -1;
       }
+      double v[TG];
 #pragma unroll
-      for (int q = 0; q < B; ++q) { c[q] = cn[q]; a[q] = an[q]; }
+      for (int i = 0; i < TG; ++i) v[i] = idx[i] >= 0 ? p.x[idx[i]] : 0.0;
+#pragma unroll
+      for (int i = 0; i < TG; ++i) {
+        const int j = j0 + i * kWave + lane;
+        if (j < m) xl[j] = v[i];
+      }
     }
+  }
+  __syncthreads();
+  // 2. jagged row loop over local columns
+  for (int k = k0; k < width; k += B) {
+    int cn[B];
+    double an[B];
+    dict_load<B, NT>(cp, vp, P, k + B, blen, llen, cn, an);
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      if (c[q] >= 0) {
+        const double pr = a[q] * xl[c[q]];
+        if (sub) t -= pr;
+        else t += pr;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) { c[q] = cn[q]; a[q] = an[q]; }
   }
   if (own) row_store<OP, NT>(p, g, skip, t, uo, d);
 }
