@@ -662,6 +662,11 @@ AMG_SET(RelaxWt, relax_weight, HYPRE_Real)
 AMG_SET(OuterWt, outer_weight, HYPRE_Real)
 AMG_SET(PrintLevel, print_level, HYPRE_Int)
 AMG_SET(Logging, logging, HYPRE_Int)
+AMG_SET(ChebyOrder, cheby_order, HYPRE_Int)
+AMG_SET(ChebyFraction, cheby_fraction, HYPRE_Real)
+AMG_SET(ChebyScale, cheby_scale, HYPRE_Int)
+AMG_SET(ChebyVariant, cheby_variant, HYPRE_Int)
+AMG_SET(ChebyEigEst, cheby_eig_est, HYPRE_Int)
 
 // par_amg.c:1962 SetNumSweeps: all of [0..2] (coarsest keeps 1), :2084 SetRelaxType
 HYPRE_Int HYPRE_BoomerAMGSetNumSweeps(HYPRE_Solver s, HYPRE_Int num_sweeps) {
@@ -1087,10 +1092,23 @@ HYPRE_Int hypreve_BoomerAMGGetLevelVector(HYPRE_Solver s, HYPRE_Int level, HYPRE
   if (which == 0) {
     if (n) *n = (int)L.cf.size();
     if (data && !L.cf.empty()) std::memcpy(data, L.cf.data(), sizeof(int) * L.cf.size());
-  } else {
+  } else if (which == 1) {
     if (n) *n = (int)L.l1.size();
     if (data && !L.l1.empty()) std::memcpy(data, L.l1.data(), sizeof(double) * L.l1.size());
+  } else {
+    if (n) *n = (int)L.cheby_ds.size();
+    if (data && !L.cheby_ds.empty()) std::memcpy(data, L.cheby_ds.data(), sizeof(double) * L.cheby_ds.size());
   }
+  return 0;
+}
+HYPRE_Int hypreve_BoomerAMGGetChebyInfo(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int* ncoefs, HYPRE_Real* coefs,
+                                        HYPRE_Real* eig, HYPRE_Int* params) {
+  CHECK_ARG(s && level >= 0 && level < (int)s->H.lev.size(), 2);
+  const Level& L = s->H.lev[level];
+  if (params) { params[0] = s->H.prm.cheby_order; params[1] = s->H.prm.cheby_scale; params[2] = s->H.prm.cheby_variant; }
+  if (ncoefs) *ncoefs = (int)L.cheby_coefs.size();
+  if (coefs && !L.cheby_coefs.empty()) std::memcpy(coefs, L.cheby_coefs.data(), sizeof(double) * L.cheby_coefs.size());
+  if (eig) { eig[0] = L.max_eig; eig[1] = L.min_eig; }
   return 0;
 }
 HYPRE_Int hypreve_BoomerAMGGetCoarseMatrix(HYPRE_Solver s, HYPRE_Int* n, HYPRE_Real* dense) {

@@ -31,6 +31,9 @@ enum : int {
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
                        const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
                        double* y2 = nullptr);
+// Chebyshev steps (kernels.hip k_cheby): 0 start, 1 tmp = ds*u, 2 update, 3 finish
+hipError_t launch_cheby(int n, int step, int scale, double c, const double* ds, const double* f, double* r,
+                        double* tmp, const double* v, double* orig, double* u, hipStream_t st);
 // op: 0 l1-Jacobi w=1, 1 l1-Jacobi weighted, 2 Jacobi (s = diagonal)
 hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u,
                              hipStream_t st);

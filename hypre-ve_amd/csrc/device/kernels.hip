@@ -776,6 +776,32 @@ __global__ void __launch_bounds__(256) k_pcg_p(int n, const double* __restrict__
   p[i] = v;
 }
 
+// Chebyshev smoother steps (par_cheby.c:166 hypre_ParCSRRelax_Cheby_Solve),
+// each the reference's elementwise loop with its expression order.
+//   start (scaled):   r = ds*(f + tmp); orig = u; u = r*c
+//   start (unscaled): orig = u; u = r*c              (r = f - A u already)
+//   scale:            tmp = ds*u
+//   update:           u = mult*r + ds*v   (unscaled: mult*r + v)
+//   finish:           u = orig + ds*u     (unscaled: orig + u)
+__global__ void __launch_bounds__(256) k_cheby(int n, int step, int scale, double c, const double* __restrict__ ds,
+                                               const double* __restrict__ f, double* __restrict__ r,
+                                               double* __restrict__ tmp, const double* __restrict__ v,
+                                               double* __restrict__ orig, double* __restrict__ u) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= n) return;
+  if (step == 0) {
+    if (scale) r[j] = ds[j] * (f[j] + tmp[j]);
+    orig[j] = u[j];
+    u[j] = r[j] * c;
+  } else if (step == 1) {
+    tmp[j] = ds[j] * u[j];
+  } else if (step == 2) {
+    u[j] = scale ? c * r[j] + ds[j] * v[j] : c * r[j] + v[j];
+  } else {
+    u[j] = scale ? orig[j] + ds[j] * u[j] : orig[j] + u[j];
+  }
+}
+
 // Deterministic two-stage dot product: stage 1 writes one partial per block.
 __global__ void __launch_bounds__(256) k_dot_partial(int n, const double* __restrict__ x, const double* __restrict__ y,
                                                      double* __restrict__ part) {
@@ -1041,6 +1067,12 @@ hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hi
   return hipGetLastError();
 }
 
+hipError_t launch_cheby(int n, int step, int scale, double c, const double* ds, const double* f, double* r,
+                        double* tmp, const double* v, double* orig, double* u, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_cheby, dim3(blocks_for(n)), dim3(256), 0, st, n, step, scale, c, ds, f, r, tmp, v, orig, u);
+  return hipGetLastError();
+}
 hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_zero_guess, dim3(blocks_for(n)), dim3(256), 0, st, n, op, w, f, s, u);

@@ -247,7 +247,7 @@ void DevAMG::release() {
     L.hu.release(); L.hv.release();
     L.gs_fwd.release(); L.gs_bwd.release();
     for (void* p : {(void*)L.l1, (void*)L.cf, (void*)L.F, (void*)L.U[0], (void*)L.U[1], (void*)L.V,
-                    (void*)L.gs_tmp})
+                    (void*)L.gs_tmp, (void*)L.cheby_ds, (void*)L.cheby_r, (void*)L.cheby_t, (void*)L.cheby_o})
       if (p) (void)hipFree(p);
   }
   lev_.clear();
@@ -317,6 +317,14 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     HVE_HIP(hipMemset(D.U[0], 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
     HVE_HIP(hipMemset(D.U[1], 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
     HVE_HIP(hipMemset(D.V, 0, sizeof(double) * std::max(1, D.n + D.hv.n_halo)));
+    if (!L.cheby_coefs.empty()) {
+      D.cheby_coefs = L.cheby_coefs;
+      if (!L.cheby_ds.empty()) D.cheby_ds = dupload(L.cheby_ds.data(), L.cheby_ds.size());
+      D.cheby_r = dalloc<double>(D.n);
+      D.cheby_t = dalloc<double>(D.n + D.hu.n_halo);
+      D.cheby_o = dalloc<double>(D.n);
+      HVE_HIP(hipMemset(D.cheby_t, 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
+    }
   }
   // Hybrid Gauss-Seidel schedules for the relax types the cycle uses
   // (num_blocks = hypre's thread count: row blocks of each level).
@@ -485,6 +493,40 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       }
       if (fw) HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, s));
       if (bw) HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, s));
+      break;
+    }
+    case 16: {
+      // par_cheby.c:166 hypre_ParCSRRelax_Cheby_Solve (par_cycle.c:445)
+      if (L.cheby_coefs.empty()) throw std::runtime_error("Chebyshev coefficients missing on level " +
+                                                          std::to_string(level));
+      if (zero_guess) HVE_HIP(launch_set(n, 0.0, u_cur, s));
+      int order = prm.cheby_order;
+      if (order > 4) order = 4;
+      if (order < 1) order = 1;
+      const int co = order - 1;
+      const int scale = prm.cheby_scale ? 1 : 0;
+      if (scale && !L.cheby_ds) throw std::runtime_error("Chebyshev scaling vector missing");
+      double* r = L.cheby_r;
+      double* tmp = L.cheby_t;
+      double* v = L.V;
+      if (scale) {
+        // tmp = -A u  (ParCSRMatrixMatvec(-1.0, A, u, 0.0, tmp))
+        apply(L.A, &L.hu, K_GENERAL, u_cur, nullptr, nullptr, nullptr, 0, tmp, -1.0, 0.0, s);
+      } else {
+        // r = f - A u  (ParVectorCopy(f, r); Matvec(-1.0, A, u, 1.0, r))
+        apply(L.A, &L.hu, K_RESID, u_cur, f, nullptr, nullptr, 0, r, -1.0, 0.0, s);
+      }
+      HVE_HIP(launch_cheby(n, 0, scale, L.cheby_coefs[co], L.cheby_ds, f, r, tmp, nullptr, L.cheby_o, u_cur, s));
+      for (int i = co - 1; i >= 0; --i) {
+        if (scale) {
+          HVE_HIP(launch_cheby(n, 1, scale, 0.0, L.cheby_ds, nullptr, nullptr, tmp, nullptr, nullptr, u_cur, s));
+          apply(L.A, &L.hu, K_MATVEC, tmp, nullptr, nullptr, nullptr, 0, v, 1.0, 0.0, s);
+        } else {
+          apply(L.A, &L.hu, K_MATVEC, u_cur, nullptr, nullptr, nullptr, 0, v, 1.0, 0.0, s);
+        }
+        HVE_HIP(launch_cheby(n, 2, scale, L.cheby_coefs[i], L.cheby_ds, nullptr, r, nullptr, v, nullptr, u_cur, s));
+      }
+      HVE_HIP(launch_cheby(n, 3, scale, 0.0, L.cheby_ds, nullptr, nullptr, nullptr, nullptr, L.cheby_o, u_cur, s));
       break;
     }
     default:

@@ -107,6 +107,11 @@ struct DevLevel {
   double* V = nullptr;                // n + hv.n_halo
   DevGs gs_fwd, gs_bwd;               // hybrid Gauss-Seidel schedules (when a cycle uses them)
   double* gs_tmp = nullptr;           // pre-sweep copy of u (n + hu.n_halo)
+  // Chebyshev (relax 16): ds on the device, coefficients on the host (kernel
+  // arguments), work vectors r, tmp (n + halo: A is applied to it), orig
+  double* cheby_ds = nullptr;
+  std::vector<double> cheby_coefs;
+  double *cheby_r = nullptr, *cheby_t = nullptr, *cheby_o = nullptr;
 };
 
 class DevAMG {

@@ -530,6 +530,8 @@ bool dist_setup_supported(const AMGParams& prm, std::string* why) {
   if (prm.coarsen_type != 8) return no("coarsen_type != 8 (PMIS)");
   if (prm.interp_type != 6) return no("interp_type != 6 (ext+i)");
   if (prm.agg_num_levels > 0) return no("aggressive coarsening");
+  for (int k = 0; k < 4; ++k)  // its eigenvalue estimate reduces over all rows in one order
+    if (prm.relax_type[k] == 16) return no("Chebyshev smoother (relax 16)");
   return true;
 }
 

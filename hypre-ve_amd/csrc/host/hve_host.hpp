@@ -86,6 +86,12 @@ struct AMGParams {
   // 5 jagged with a per-slice column dictionary (x-tile in LDS).
   // Every choice gives the same bits; 1-4 let the tests prove that.
   int sell_policy = 0;
+  // Chebyshev smoother (relax type 16): par_amg.c:225-229 defaults
+  int cheby_order = 2;      // order of the residual polynomial (1..4)
+  int cheby_variant = 0;    // 0 standard, 1 modified
+  int cheby_scale = 1;      // scale by D^{-1/2}
+  int cheby_eig_est = 10;   // CG steps of the eigenvalue estimate (0: inf-norm bound)
+  double cheby_fraction = 0.3;
 };
 
 struct Level {
@@ -95,6 +101,10 @@ struct Level {
   std::vector<int> cf;          // CF marker (C_PT / F_PT), empty on coarsest
   std::vector<double> l1;       // row norms for the l1 smoothers (may be empty)
   std::vector<double> dinv;     // unused slot (Jacobi uses A's diagonal directly)
+  // Chebyshev (relax 16): 1/sqrt(a_ii) when scaled, polynomial coefficients,
+  // eigenvalue estimates (par_amg_setup.c:3139-3164)
+  std::vector<double> cheby_ds, cheby_coefs;
+  double max_eig = 0.0, min_eig = 0.0;
 };
 
 struct Hierarchy {
@@ -136,6 +146,18 @@ void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, cons
 void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& row_ic,
               const std::vector<int>& coarse_glob, int nfine_univ, int ncoarse_univ, int ncoarse_glob, CSR& C);
 double hypre_rand_at(int64_t k, int seed);
+// Chebyshev smoother setup (one process, one thread, as the reference's host
+// path): par_relax_more.c:115 hypre_ParCSRMaxEigEstimateCG (random start
+// vector of hypre_ParVectorSetRandomValues(r, 1), Lanczos tridiagonal from CG,
+// eigenvalues by LINPACK tql1), par_relax_more.c:25 hypre_ParCSRMaxEigEstimate
+// (inf-norm bound), par_cheby.c:36 hypre_ParCSRRelax_Cheby_Setup.
+void max_eig_estimate_cg(const CSR& A, int scale, int max_iter, double* max_eig, double* min_eig);
+void max_eig_estimate_norm(const CSR& A, int scale, double* max_eig);
+void cheby_setup(const CSR& A, double max_eig, double min_eig, double fraction, int order, int scale, int variant,
+                 std::vector<double>& coefs, std::vector<double>& ds);
+// EISPACK tql1 (par_relax_more.c:753): eigenvalues of the symmetric
+// tridiagonal (d, e[1..n-1]) in ascending order into d; 0 or the failing index.
+int linpack_tql1(int n, double* d, double* e);
 void transpose(const CSR& A, CSR& AT);
 void rap(const CSR& P, const CSR& A, CSR& RAP);
 void compute_l1_norms(const CSR& A, int option, const int* cf, int num_blocks,
@@ -145,6 +167,18 @@ void compute_l1_norms(const CSR& A, int option, const int* cf, int num_blocks,
 int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H);
 
 // Park-Miller generator used by hypre_Rand (utilities/random.c:40-71).
-double hypre_rand_at(int64_t k, int seed);  // value of the (k+1)-th draw after SeedRand(seed)
+double hypre_rand_at(int64_t k, int seed);
+// Chebyshev smoother setup (one process, one thread, as the reference's host
+// path): par_relax_more.c:115 hypre_ParCSRMaxEigEstimateCG (random start
+// vector of hypre_ParVectorSetRandomValues(r, 1), Lanczos tridiagonal from CG,
+// eigenvalues by LINPACK tql1), par_relax_more.c:25 hypre_ParCSRMaxEigEstimate
+// (inf-norm bound), par_cheby.c:36 hypre_ParCSRRelax_Cheby_Setup.
+void max_eig_estimate_cg(const CSR& A, int scale, int max_iter, double* max_eig, double* min_eig);
+void max_eig_estimate_norm(const CSR& A, int scale, double* max_eig);
+void cheby_setup(const CSR& A, double max_eig, double min_eig, double fraction, int order, int scale, int variant,
+                 std::vector<double>& coefs, std::vector<double>& ds);
+// EISPACK tql1 (par_relax_more.c:753): eigenvalues of the symmetric
+// tridiagonal (d, e[1..n-1]) in ascending order into d; 0 or the failing index.
+int linpack_tql1(int n, double* d, double* e);  // value of the (k+1)-th draw after SeedRand(seed)
 
 }  // namespace hve

@@ -143,6 +143,8 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
       }
       if (!L.l1.empty()) RL.l1.assign(L.l1.begin() + a, L.l1.begin() + b);
       if (!L.cf.empty()) RL.cf.assign(L.cf.begin() + a, L.cf.begin() + b);
+      if (!L.cheby_ds.empty()) RL.cheby_ds.assign(L.cheby_ds.begin() + a, L.cheby_ds.begin() + b);
+      RL.cheby_coefs = L.cheby_coefs;
       // halo plans
       for (int which = 0; which < 2; ++which) {
         if (which == 1 && l + 1 >= nl) break;
@@ -324,7 +326,7 @@ struct Rd {
     pod(h.n_loc); pod(h.n_halo); vec(h.peers); vec(h.recv_cnt); vec(h.send_cnt); vec(h.send_idx); vec(h.halo_glob);
   }
 };
-const int64_t kMagic = 0x48564531414d47LL;  // "HVE1AMG"
+const int64_t kMagic = 0x48564532414d47LL;  // "HVE2AMG"
 }  // namespace
 
 void serialize(const RankHierarchy& R, std::vector<char>& buf) {
@@ -338,6 +340,7 @@ void serialize(const RankHierarchy& R, std::vector<char>& buf) {
     w.op(L.A); w.op(L.P); w.op(L.R);
     w.halo(L.hu); w.halo(L.hv);
     w.vec(L.l1); w.vec(L.cf);
+    w.vec(L.cheby_ds); w.vec(L.cheby_coefs);
   }
   w.pod(R.coarse_n); w.vec(R.coarse_dense);
   w.pod(R.grid_complexity); w.pod(R.operator_complexity);
@@ -358,6 +361,7 @@ void deserialize(const std::vector<char>& buf, RankHierarchy& R) {
     r.op(L.A); r.op(L.P); r.op(L.R);
     r.halo(L.hu); r.halo(L.hv);
     r.vec(L.l1); r.vec(L.cf);
+    r.vec(L.cheby_ds); r.vec(L.cheby_coefs);
   }
   r.pod(R.coarse_n); r.vec(R.coarse_dense);
   r.pod(R.grid_complexity); r.pod(R.operator_complexity);

@@ -46,6 +46,8 @@ struct RankLevel {
   RankHalo hv;       // halo of V_l (R_l needs)
   std::vector<double> l1;
   std::vector<int> cf;
+  std::vector<double> cheby_ds;     // Chebyshev: 1/sqrt(a_ii) of the owned rows (scaled variant)
+  std::vector<double> cheby_coefs;  // Chebyshev polynomial coefficients (replicated)
 };
 
 struct RankHierarchy {

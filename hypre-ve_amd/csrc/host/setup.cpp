@@ -1075,6 +1075,255 @@ void compute_l1_norms(const CSR& A, int option, const int* cf, int num_blocks, s
 }
 
 // ---------------------------------------------------------------------------
+// Chebyshev smoother setup (relax type 16).
+// ---------------------------------------------------------------------------
+// par_relax_more.c cgpthy: sqrt(a^2 + b^2) without destructive over/underflow
+static double linpack_pythag(double a, double b) {
+  double p = std::max(std::fabs(a), std::fabs(b));
+  if (!p) return p;
+  double d = std::min(std::fabs(a), std::fabs(b)) / p;
+  double r = d * d;
+  for (;;) {
+    const double t = r + 4.;
+    if (t == 4.) break;
+    const double s = r / t;
+    const double u = s * 2. + 1.;
+    p = u * p;
+    d = s / u;
+    r = d * d * r;
+  }
+  return p;
+}
+
+// par_relax_more.c:753 hypre_LINPACKcgtql1, restated with the same 1-based
+// indexing and statement order.
+int linpack_tql1(int n_, double* d0, double* e0) {
+  const int n = n_;
+  double* d = d0 - 1;
+  double* e = e0 - 1;
+  int ierr = 0;
+  double c, f, g, h, p, r, s, c2, c3 = 0.0, s2 = 0.0, dl1, el1, tst1, tst2, ds;
+  int i, j, l, m, l1, l2, ii, mml;
+  if (n == 1) return 0;
+  for (i = 2; i <= n; ++i) e[i - 1] = e[i];
+  f = 0.;
+  tst1 = 0.;
+  e[n] = 0.;
+  for (l = 1; l <= n; ++l) {
+    j = 0;
+    h = std::fabs(d[l]) + std::fabs(e[l]);
+    if (tst1 < h) tst1 = h;
+    for (m = l; m <= n; ++m) {
+      tst2 = tst1 + std::fabs(e[m]);
+      if (tst2 == tst1) break;
+    }
+    if (m != l) {
+      for (;;) {  // L130
+        if (j == 30) return l;
+        ++j;
+        l1 = l + 1;
+        l2 = l1 + 1;
+        g = d[l];
+        p = (d[l1] - g) / (e[l] * 2.);
+        r = linpack_pythag(p, 1.0);
+        ds = 1.0;
+        if (p < 0.0) ds = -1.0;
+        d[l] = e[l] / (p + ds * r);
+        d[l1] = e[l] * (p + ds * r);
+        dl1 = d[l1];
+        h = g - d[l];
+        if (l2 <= n)
+          for (i = l2; i <= n; ++i) d[i] -= h;
+        f += h;
+        p = d[m];
+        c = 1.;
+        c2 = c;
+        el1 = e[l1];
+        s = 0.;
+        mml = m - l;
+        for (ii = 1; ii <= mml; ++ii) {
+          c3 = c2;
+          c2 = c;
+          s2 = s;
+          i = m - ii;
+          g = c * e[i];
+          h = c * p;
+          r = linpack_pythag(p, e[i]);
+          e[i + 1] = s * r;
+          s = e[i] / r;
+          c = p / r;
+          p = c * d[i] - s * g;
+          d[i + 1] = h + s * (c * g + s * d[i]);
+        }
+        p = -s * s2 * c3 * el1 * e[l] / dl1;
+        e[l] = s * p;
+        d[l] = c * p;
+        tst2 = tst1 + std::fabs(e[l]);
+        if (!(tst2 > tst1)) break;
+      }
+    }
+    // L210
+    p = d[l] + f;
+    i = 1;
+    if (l != 1) {
+      bool placed = false;
+      for (ii = 2; ii <= l; ++ii) {
+        i = l + 2 - ii;
+        if (p >= d[i - 1]) { placed = true; break; }
+        d[i] = d[i - 1];
+      }
+      if (!placed) i = 1;
+    }
+    d[i] = p;
+  }
+  return ierr;
+}
+
+// y = A x (csr_matvec.c, alpha 1 beta 0), one thread
+static void host_matvec(const CSR& A, const std::vector<double>& x, std::vector<double>& y) {
+  for (int r = 0; r < A.nrows; ++r) {
+    double t = 0.0;
+    for (int k = A.i[r]; k < A.i[r + 1]; ++k) t += A.a[k] * x[A.j[k]];
+    y[r] = t;
+  }
+}
+static double host_dot(const std::vector<double>& x, const std::vector<double>& y) {
+  double s = 0.0;
+  for (size_t i = 0; i < x.size(); ++i) s += y[i] * x[i];  // hypre_SeqVectorInnerProd: y_i * x_i
+  return s;
+}
+
+void max_eig_estimate_cg(const CSR& A, int scale, int max_iter, double* max_eig, double* min_eig) {
+  const int n = A.nrows;
+  if (n < max_iter) max_iter = n;
+  std::vector<double> r(n), p(n, 0.0), s(n, 0.0), ds(n), u(n, 0.0);
+  std::vector<double> tridiag(max_iter + 1, 0.0), trioffd(max_iter + 1, 0.0);
+  // hypre_ParVectorSetRandomValues(r, 1): seed 1 * (my_id + 1), 2*rand - 1
+  for (int i = 0; i < n; ++i) r[i] = 2.0 * hypre_rand_at(i, 1) - 1.0;
+  if (scale) {
+    for (int i = 0; i < n; ++i) ds[i] = 1 / std::sqrt(A.a[A.i[i]]);
+  } else {
+    for (int i = 0; i < n; ++i) ds[i] = 1.0;
+  }
+  double gamma = host_dot(r, p), gamma_old, beta, alpha, sdotp, alphainv;
+  int i = 0;
+  while (i < max_iter) {
+    s = r;
+    gamma_old = gamma;
+    gamma = host_dot(r, s);
+    if (i == 0) {
+      beta = 1.0;
+      p = s;
+    } else {
+      beta = gamma / gamma_old;
+      for (int k = 0; k < n; ++k) p[k] = s[k] + beta * p[k];
+    }
+    if (scale) {
+      for (int k = 0; k < n; ++k) u[k] = ds[k] * p[k];
+      host_matvec(A, u, s);
+      for (int k = 0; k < n; ++k) s[k] = ds[k] * s[k];
+    } else {
+      host_matvec(A, p, s);
+    }
+    sdotp = host_dot(s, p);
+    alpha = gamma / sdotp;
+    alphainv = 1.0 / alpha;
+    tridiag[i + 1] = alphainv;
+    tridiag[i] *= beta;
+    tridiag[i] += alphainv;
+    trioffd[i + 1] = alphainv;
+    trioffd[i] *= std::sqrt(beta);
+    for (int k = 0; k < n; ++k) r[k] += (-alpha) * s[k];  // hypre_ParVectorAxpy(-alpha, s, r)
+    i++;
+  }
+  linpack_tql1(i, tridiag.data(), trioffd.data());
+  *max_eig = tridiag[i - 1];
+  *min_eig = tridiag[0];
+}
+
+void max_eig_estimate_norm(const CSR& A, int scale, double* max_eig) {
+  double max_norm = 0.0;
+  int pos_diag = 0, neg_diag = 0;
+  for (int i = 0; i < A.nrows; ++i) {
+    const int start = A.i[i];
+    double diag_value = A.a[start];
+    if (diag_value > 0) pos_diag++;
+    if (diag_value < 0) { neg_diag++; diag_value = -diag_value; }
+    double row_sum = diag_value;
+    for (int j = start + 1; j < A.i[i + 1]; ++j) row_sum += std::fabs(A.a[j]);
+    if (scale && diag_value != 0.0) row_sum = row_sum / diag_value;
+    if (row_sum > max_norm) max_norm = row_sum;
+  }
+  if (pos_diag == 0 && neg_diag > 0) max_norm = -max_norm;
+  *max_eig = max_norm;
+}
+
+void cheby_setup(const CSR& A, double max_eig, double min_eig, double fraction, int order, int scale, int variant,
+                 std::vector<double>& coefs, std::vector<double>& ds) {
+  if (order > 4) order = 4;
+  if (order < 1) order = 1;
+  coefs.assign(order + 1, 0.0);
+  const int cheby_order = order - 1;
+  const double upper_bound = max_eig * 1.1;
+  const double lower_bound = (upper_bound - min_eig) * fraction + min_eig;
+  const double theta = (upper_bound + lower_bound) / 2;
+  const double delta = (upper_bound - lower_bound) / 2;
+  double den;
+  if (variant == 1) {
+    switch (cheby_order) {
+      case 0: coefs[0] = 1.0 / theta; break;
+      case 1:
+        den = (theta * theta + delta * theta);
+        coefs[0] = (delta + 2 * theta) / den;
+        coefs[1] = -1.0 / den;
+        break;
+      case 2:
+        den = 2 * delta * theta * theta - delta * delta * theta - std::pow(delta, 3) + 2 * std::pow(theta, 3);
+        coefs[0] = (4 * delta * theta - std::pow(delta, 2) + 6 * std::pow(theta, 2)) / den;
+        coefs[1] = -(2 * delta + 6 * theta) / den;
+        coefs[2] = 2 / den;
+        break;
+      case 3:
+        den = -(4 * delta * std::pow(theta, 3) - 3 * std::pow(delta, 2) * std::pow(theta, 2) -
+                3 * std::pow(delta, 3) * theta + 4 * std::pow(theta, 4));
+        coefs[0] = (6 * std::pow(delta, 2) * theta - 12 * delta * std::pow(theta, 2) + 3 * std::pow(delta, 3) -
+                    16 * std::pow(theta, 3)) / den;
+        coefs[1] = (12 * delta * theta - 3 * std::pow(delta, 2) + 24 * std::pow(theta, 2)) / den;
+        coefs[2] = -(4 * delta + 16 * theta) / den;
+        coefs[3] = 4 / den;
+        break;
+    }
+  } else {
+    switch (cheby_order) {
+      case 0: coefs[0] = 1.0 / theta; break;
+      case 1:
+        den = delta * delta - 2 * theta * theta;
+        coefs[0] = -4 * theta / den;
+        coefs[1] = 2 / den;
+        break;
+      case 2:
+        den = 3 * (delta * delta) * theta - 4 * (theta * theta * theta);
+        coefs[0] = (3 * delta * delta - 12 * theta * theta) / den;
+        coefs[1] = 12 * theta / den;
+        coefs[2] = -4 / den;
+        break;
+      case 3:
+        den = std::pow(delta, 4) - 8 * delta * delta * theta * theta + 8 * std::pow(theta, 4);
+        coefs[0] = (32 * std::pow(theta, 3) - 16 * delta * delta * theta) / den;
+        coefs[1] = (8 * delta * delta - 48 * theta * theta) / den;
+        coefs[2] = 32 * theta / den;
+        coefs[3] = -8 / den;
+        break;
+    }
+  }
+  ds.clear();
+  if (scale) {
+    ds.resize(A.nrows);
+    for (int j = 0; j < A.nrows; ++j) ds[j] = 1 / std::sqrt(A.a[A.i[j]]);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Setup driver: par_amg_setup.c:889-2880 (coarsening loop), :2990-3120 (l1 norms).
 // ---------------------------------------------------------------------------
 static bool uses_l1_gs(int t) { return t == 8 || t == 13 || t == 14; }
@@ -1159,6 +1408,16 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
       compute_l1_norms(L.A, 1, cfp, 1, L.l1);
     else if (j == nl - 1 && prm.relax_type[3] == 18)
       compute_l1_norms(L.A, 1, nullptr, 1, L.l1);
+    // par_amg_setup.c:3139: Chebyshev (relax 16) eigenvalue estimate and coefficients
+    if (prm.relax_type[1] == 16 || prm.relax_type[2] == 16 || (prm.relax_type[3] == 16 && j == nl - 1)) {
+      double max_eig = 0.0, min_eig = 0.0;
+      if (prm.cheby_eig_est) max_eig_estimate_cg(L.A, prm.cheby_scale, prm.cheby_eig_est, &max_eig, &min_eig);
+      else max_eig_estimate_norm(L.A, prm.cheby_scale, &max_eig);
+      L.max_eig = max_eig;
+      L.min_eig = min_eig;
+      cheby_setup(L.A, max_eig, min_eig, prm.cheby_fraction, prm.cheby_order, prm.cheby_scale, prm.cheby_variant,
+                  L.cheby_coefs, L.cheby_ds);
+    }
     // par_amg_setup.c:3122: relax type 7 scales by the diagonal (ams.c option 5)
     if (prm.relax_type[1] == 7 || prm.relax_type[2] == 7 || (prm.relax_type[3] == 7 && j == nl - 1)) {
       L.l1.resize(L.A.nrows);

@@ -126,6 +126,12 @@ SIGNATURES = [
     ("HYPRE_BoomerAMGSetRelaxOrder", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetRelaxWt", _i, [_p, _d]),
     ("HYPRE_BoomerAMGSetOuterWt", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetChebyOrder", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetChebyFraction", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetChebyScale", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetChebyVariant", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetChebyEigEst", _i, [_p, _i]),
+    ("hypreve_BoomerAMGGetChebyInfo", _i, [_p, _i, C.POINTER(_i), C.POINTER(_d), C.POINTER(_d), C.POINTER(_i)]),
     ("HYPRE_BoomerAMGSetPrintLevel", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetLogging", _i, [_p, _i]),
     ("HYPRE_BoomerAMGGetNumLevels", _i, [_p, _pi]),
@@ -364,6 +370,9 @@ class BoomerAMG:
         "print_level": ("HYPRE_BoomerAMGSetPrintLevel", int), "converge_type": ("HYPRE_BoomerAMGSetConvergeType", int),
         "num_blocks": ("hypreve_BoomerAMGSetNumBlocks", int), "use_graph": ("hypreve_BoomerAMGSetUseGraph", int),
         "sell_policy": ("hypreve_BoomerAMGSetSellPolicy", int),
+        "cheby_order": ("HYPRE_BoomerAMGSetChebyOrder", int), "cheby_fraction": ("HYPRE_BoomerAMGSetChebyFraction", float),
+        "cheby_scale": ("HYPRE_BoomerAMGSetChebyScale", int), "cheby_variant": ("HYPRE_BoomerAMGSetChebyVariant", int),
+        "cheby_eig_est": ("HYPRE_BoomerAMGSetChebyEigEst", int),
     }
 
     def __init__(self, **kw):
@@ -448,10 +457,19 @@ class BoomerAMG:
     def level_vector(self, l, which):
         n = C.c_int()
         check(lib().hypreve_BoomerAMGGetLevelVector(self.h, l, which, C.byref(n), None), "GetLevelVector")
-        out = np.zeros(n.value, dtype=np.int32 if which == 0 else np.float64)
+        out = np.zeros(n.value, dtype=np.int32 if which == 0 else np.float64)  # 0 cf, 1 l1, 2 Chebyshev ds
         if n.value:
             lib().hypreve_BoomerAMGGetLevelVector(self.h, l, which, None, out.ctypes.data_as(C.c_void_p))
         return out
+
+    def cheby_info(self, l):
+        """(coefficients, (max_eig, min_eig), (order, scale, variant)) of level l's Chebyshev smoother."""
+        n = C.c_int()
+        co = (C.c_double * 5)()
+        eig = (C.c_double * 2)()
+        prm = (C.c_int * 3)()
+        check(lib().hypreve_BoomerAMGGetChebyInfo(self.h, l, C.byref(n), co, eig, prm), "GetChebyInfo")
+        return np.array(co[: n.value]), (eig[0], eig[1]), (prm[0], prm[1], prm[2])
 
     def coarse_matrix(self):
         n = C.c_int()

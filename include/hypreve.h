@@ -159,6 +159,12 @@ HYPRE_Int HYPRE_BoomerAMGSetRelaxOrder(HYPRE_Solver solver, HYPRE_Int relax_orde
 HYPRE_Int HYPRE_BoomerAMGSetRelaxWt(HYPRE_Solver solver, HYPRE_Real relax_weight); /* :805 */
 HYPRE_Int HYPRE_BoomerAMGSetOuterWt(HYPRE_Solver solver, HYPRE_Real omega);       /* :839 */
 HYPRE_Int HYPRE_BoomerAMGSetPrintLevel(HYPRE_Solver solver, HYPRE_Int print_level); /* :1103 */
+/* Chebyshev smoother (relax type 16), HYPRE_parcsr_ls.h:857-889 */
+HYPRE_Int HYPRE_BoomerAMGSetChebyOrder(HYPRE_Solver solver, HYPRE_Int order);          /* :857 */
+HYPRE_Int HYPRE_BoomerAMGSetChebyFraction(HYPRE_Solver solver, HYPRE_Real ratio);      /* :864 */
+HYPRE_Int HYPRE_BoomerAMGSetChebyScale(HYPRE_Solver solver, HYPRE_Int scale);          /* :871 */
+HYPRE_Int HYPRE_BoomerAMGSetChebyVariant(HYPRE_Solver solver, HYPRE_Int variant);      /* :878 */
+HYPRE_Int HYPRE_BoomerAMGSetChebyEigEst(HYPRE_Solver solver, HYPRE_Int eig_est);       /* :889 */
 HYPRE_Int HYPRE_BoomerAMGSetLogging(HYPRE_Solver solver, HYPRE_Int logging);
 HYPRE_Int HYPRE_BoomerAMGGetNumLevels(HYPRE_Solver solver, HYPRE_Int *num_levels);
 
@@ -233,7 +239,12 @@ HYPRE_Int hypreve_BoomerAMGGetLevelMatrix(HYPRE_Solver solver, HYPRE_Int level, 
                                           HYPRE_Int *nrows, HYPRE_Int *ncols, int64_t *nnz,
                                           HYPRE_Int *row_ptr, HYPRE_Int *cols, HYPRE_Real *vals);
 HYPRE_Int hypreve_BoomerAMGGetLevelVector(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,
-                                          HYPRE_Int *n, void *data); /* 0 cf (int), 1 l1 (double) */
+                                          HYPRE_Int *n, void *data); /* 0 cf (int), 1 l1, 2 Chebyshev ds (double) */
+/* Chebyshev data of one level: coefficient count / values (up to 5), the
+ * eigenvalue estimates eig[0] = max, eig[1] = min, and params[0..2] = order,
+ * scale, variant. */
+HYPRE_Int hypreve_BoomerAMGGetChebyInfo(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int *ncoefs,
+                                        HYPRE_Real *coefs, HYPRE_Real *eig, HYPRE_Int *params);
 HYPRE_Int hypreve_BoomerAMGGetCoarseMatrix(HYPRE_Solver solver, HYPRE_Int *n, HYPRE_Real *dense);
 HYPRE_Int hypreve_BoomerAMGGetRelaxInfo(HYPRE_Solver solver, HYPRE_Int *relax_type4,
                                         HYPRE_Int *num_sweeps4, HYPRE_Real *weights2,

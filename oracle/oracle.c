@@ -222,6 +222,48 @@ static void gauss_elim_solve(int n, const double *Amat, const double *f, double 
 
 /* ---- parcsr_ls/par_cycle.c:22 hypre_BoomerAMGCycle (smooth_num_levels = 0,
  * no grid_relax_points, no block mode) ---- */
+int orc_cheby(const orc_csr *A, const double *f, const double *ds, const double *coefs, int order, int scale,
+              double *u, double *v, double *r) {
+  const int n = A->nrows;
+  if (order > 4) order = 4;
+  if (order < 1) order = 1;
+  const int cheby_order = order - 1;
+  double *orig_u = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+  if (!scale) {
+    /* r = f - A u */
+    orc_matvec(-1.0, A, u, 1.0, f, r);
+    for (int i = 0; i < n; i++) {
+      orig_u[i] = u[i];
+      u[i] = r[i] * coefs[cheby_order];
+    }
+    for (int i = cheby_order - 1; i >= 0; i--) {
+      orc_matvec(1.0, A, u, 0.0, NULL, v);
+      const double mult = coefs[i];
+      for (int j = 0; j < n; j++) u[j] = mult * r[j] + v[j];
+    }
+    for (int i = 0; i < n; i++) u[i] = orig_u[i] + u[i];
+  } else {
+    double *tmp = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+    /* tmp = -A u; r = D^{-1/2} (f + tmp) */
+    orc_matvec(-1.0, A, u, 0.0, NULL, tmp);
+    for (int j = 0; j < n; j++) r[j] = ds[j] * (f[j] + tmp[j]);
+    for (int j = 0; j < n; j++) {
+      orig_u[j] = u[j];
+      u[j] = r[j] * coefs[cheby_order];
+    }
+    for (int i = cheby_order - 1; i >= 0; i--) {
+      for (int j = 0; j < n; j++) tmp[j] = ds[j] * u[j];
+      orc_matvec(1.0, A, tmp, 0.0, NULL, v);
+      const double mult = coefs[i];
+      for (int j = 0; j < n; j++) u[j] = mult * r[j] + ds[j] * v[j];
+    }
+    for (int j = 0; j < n; j++) u[j] = orig_u[j] + ds[j] * u[j];
+    free(tmp);
+  }
+  free(orig_u);
+  return 0;
+}
+
 int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
   const int nl = amg->num_levels;
   int lev_counter[ORC_MAX_LEVELS];
@@ -247,6 +289,10 @@ int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
       ops += (double)amg->A[level].i[amg->A[level].nrows];
       if (relax_type == 9 || relax_type == 99 || relax_type == 199) {
         gauss_elim_solve(amg->coarse_n, amg->coarse_A, F[level], U[level]);
+      } else if (relax_type == 16) {
+        /* par_cycle.c:445 scaled Chebyshev: Aux_F, Aux_U, Vtemp, Ztemp */
+        err = orc_cheby(&amg->A[level], F[level], amg->cheby_ds[level], amg->cheby_coefs[level],
+                        amg->cheby_order, amg->cheby_scale, U[level], vtemp, ztemp);
       } else if (relax_type == 18 || relax_type == 7) {
         err = orc_relax(&amg->A[level], F[level], amg->cf[level], relax_type, 0,
                         amg->relax_weight, amg->omega, amg->l1[level], amg->num_blocks,

@@ -42,6 +42,11 @@ typedef struct {
   double relax_weight, omega;
   int relax_order, cycle_type, num_blocks;
   orc_csr R[ORC_MAX_LEVELS]; /* optional P[l]^T with ascending rows (i == NULL: scatter) */
+  /* Chebyshev smoother (relax type 16): per level 1/sqrt(a_ii) (scaled
+   * variant) and the polynomial coefficients; order and scaling */
+  const double *cheby_ds[ORC_MAX_LEVELS];
+  double cheby_coefs[ORC_MAX_LEVELS][5];
+  int cheby_order, cheby_scale;
 } orc_amg;
 
 /* OpenMP threads the row-parallel loops use (1 without OpenMP). */
@@ -58,6 +63,11 @@ void orc_matvecT(double alpha, const orc_csr *A, const double *x, double beta, d
 int orc_relax(const orc_csr *A, const double *f, const int *cf, int relax_type,
               int relax_points, double relax_weight, double omega, const double *l1,
               int num_blocks, double *u, double *vtemp, double *ztemp);
+
+/* parcsr_ls/par_cheby.c:166 hypre_ParCSRRelax_Cheby_Solve (variant 0 and 1
+ * share the solve; the coefficients differ). v, r: temporaries of n. */
+int orc_cheby(const orc_csr *A, const double *f, const double *ds, const double *coefs, int order, int scale,
+              double *u, double *v, double *r);
 
 /* parcsr_ls/par_cycle.c:22 hypre_BoomerAMGCycle.  F[l], U[l] per level.
  * Returns cycle_op_count contribution via *op_count (may be NULL). */

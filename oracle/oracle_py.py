@@ -31,7 +31,9 @@ class orc_amg(C.Structure):
                 ("relax_type", C.c_int * 4), ("num_sweeps", C.c_int * 4),
                 ("relax_weight", C.c_double), ("omega", C.c_double),
                 ("relax_order", C.c_int), ("cycle_type", C.c_int), ("num_blocks", C.c_int),
-                ("R", orc_csr * MAXL)]
+                ("R", orc_csr * MAXL),
+                ("cheby_ds", C.POINTER(C.c_double) * MAXL), ("cheby_coefs", (C.c_double * 5) * MAXL),
+                ("cheby_order", C.c_int), ("cheby_scale", C.c_int)]
 
 
 _lib = None
@@ -118,6 +120,15 @@ class OracleAMG:
             if l1.size:
                 self.keep.append(l1)
                 s.l1[l] = _dp(l1)
+            if 16 in amg.relax_info()["relax_type"]:
+                ds = amg.level_vector(l, 2)
+                if ds.size:
+                    self.keep.append(ds)
+                    s.cheby_ds[l] = _dp(ds)
+                co, _, prm = amg.cheby_info(l)
+                for k, c in enumerate(co):
+                    s.cheby_coefs[l][k] = c
+                s.cheby_order, s.cheby_scale = prm[0], prm[1]
         cm = amg.coarse_matrix()
         if cm.size:
             cm = np.ascontiguousarray(cm.ravel())

@@ -134,6 +134,33 @@ def test_anisotropic_solve_bitwise(gpu, orc, coef):
     assert np.array_equal(x.get(), xo)
 
 
+@pytest.mark.parametrize("order,scale,variant", [(2, 1, 0), (1, 1, 0), (3, 0, 0), (4, 1, 1), (2, 0, 1)])
+def test_chebyshev_cycle_bitwise(gpu, orc, order, scale, variant):
+    """Relax type 16 (par_cheby.c:166 scaled / unscaled Chebyshev, standard
+    and modified polynomial): V-cycles and a solve equal the oracle's bits."""
+    hv = gpu
+    A, amg, O = setup_pair(hv, orc, (23, 21, 19), coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=16,
+                           cheby_order=order, cheby_scale=scale, cheby_variant=variant)
+    n = A.n
+    rng = np.random.default_rng(41 + order)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+    b = hv.ParVector(n, f_h)
+    x = hv.ParVector(n, np.zeros(n))
+    amg.set(tol=1e-8, max_iter=40)
+    it, rr = amg.solve(A, b, x)
+    xo = np.zeros(n)
+    st = O.solve(f_h, xo, 1e-8, 40)
+    assert it == st["iterations"]
+    assert np.array_equal(x.get(), xo)
+
+
 def test_matvec_bitwise(gpu, orc):
     hv = gpu
     A, amg, O = setup_pair(hv, orc, (20, 20, 20), coarsen_type=8, relax_type=18)

@@ -162,3 +162,39 @@ def test_gs_level_schedule_nonsymmetric(hv):
     amg.setup_host(P)
     for nb in (1, 3, 17):
         amg.gs_schedule_check(nb)
+
+
+@pytest.mark.parametrize("scale", [0, 1])
+def test_chebyshev_setup(hv, scale):
+    """Relax type 16 setup (par_amg_setup.c:3139): the CG / Lanczos estimate of
+    the largest eigenvalue of D^-1/2 A D^-1/2 (or A) from 10 steps lies just
+    below the true one (numpy), the smallest above the true smallest, and the
+    order-2 coefficients are par_cheby.c's closed form for that interval.
+    Parity unpinned: no reference output covers relax 16 at np=1; the
+    estimate and the coefficients are restated from par_relax_more.c:115 and
+    par_cheby.c:36."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as sla
+    A = hv.ParCSRMatrix.laplacian(12, 11, 10)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=8, relax_type=16, cheby_scale=scale, cheby_order=2, cheby_fraction=0.3)
+    amg.setup_host(A)
+    for l in range(amg.num_levels() - 1):
+        ip, jj, vv, shp = amg.level_matrix(l, 0)
+        M = sp.csr_matrix((vv, jj, ip), shape=shp)
+        if scale:
+            d = 1.0 / np.sqrt(M.diagonal())
+            M = sp.diags(d) @ M @ sp.diags(d)
+            assert np.array_equal(amg.level_vector(l, 2), 1 / np.sqrt(sp.csr_matrix((vv, jj, ip), shape=shp).diagonal()))
+        lam = np.linalg.eigvalsh(M.toarray()) if shp[0] <= 2000 else sla.eigsh(M, 1, which="LA")[0]
+        co, (emax, emin), prm = amg.cheby_info(l)
+        assert prm == (2, scale, 0)
+        assert emax <= lam.max() * (1 + 1e-10) and emax >= 0.8 * lam.max()
+        assert emin >= lam.min() * (1 - 1e-10)
+        ub = emax * 1.1
+        lb = (ub - emin) * 0.3 + emin
+        th, de = (ub + lb) / 2, (ub - lb) / 2
+        # order 2 = residual polynomial of degree 2: s(A) of degree 1 (case 1)
+        den = de * de - 2 * th * th
+        ref = [-4 * th / den, 2 / den, 0.0]
+        assert np.allclose(co, ref, rtol=1e-13, atol=0)
