@@ -703,6 +703,11 @@ HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver s, HYPRE_Int nb) {
   s->user_num_blocks = nb >= 1;
   return 0;
 }
+HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver s, HYPRE_Int rows) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  s->prm.agglo_rows = rows < 0 ? 0 : rows;
+  return 0;
+}
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(policy >= 0 && policy <= 5, 2);

@@ -294,6 +294,8 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   prm = R.prm;
   const int nl = (int)R.lev.size();
   lev_.resize(nl);
+  agg_level_ = comm_ ? R.agg_level : -1;
+  agg_starts_ = R.agg_starts;
   for (int l = 0; l < nl; ++l) {
     const RankLevel& L = R.lev[l];
     DevLevel& D = lev_[l];
@@ -429,10 +431,25 @@ void DevAMG::fine_apply(int op, const double* x, const double* b, double* y, dou
   apply(L.A, &L.hu, op, xin, b, nullptr, nullptr, 0, y, alpha, temp, s);
 }
 
+// v holds starts[r] .. starts[r+1] of every rank r; each rank fills in its own
+// share and receives the others' (one grouped exchange).
+void DevAMG::allgather_rows(double* v, const std::vector<int>& starts, hipStream_t s) {
+  const int me = comm_->rank(), n = comm_->size();
+  std::vector<P2PMsg> sends, recvs;
+  const size_t mine = (size_t)(starts[me + 1] - starts[me]) * sizeof(double);
+  for (int p = 0; p < n; ++p) {
+    if (p == me) continue;
+    if (mine) sends.push_back({p, v + starts[me], mine});
+    const size_t theirs = (size_t)(starts[p + 1] - starts[p]) * sizeof(double);
+    if (theirs) recvs.push_back({p, v + starts[p], theirs});
+  }
+  comm_->exchange(sends, recvs, s);
+}
+
 void DevAMG::coarse_solve(int level, const double* f, double* u, hipStream_t s) {
   DevLevel& L = lev_[level];
   if (coarse_n_ != L.n_glob) throw std::runtime_error("coarse solve size mismatch");
-  if (!comm_) {
+  if (!comm_ || agg_level_ >= 0) {  // one rank, or the coarsest level is replicated
     HVE_HIP(launch_coarse(coarse_n_, coarse_L_, coarse_mask_, coarse_U_, f, u, s));
     return;
   }
@@ -615,12 +632,18 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);
       // When the coarse level's first down sweep is l1-Jacobi (weight 1) from
       // the zero guess, u_c = 0 + F_c/l1 is formed by the restriction itself.
-      const bool fuse_zg = coarse != nl - 1 && prm.num_sweeps[1] >= 1 &&
+      const bool into_agg = agg_level_ >= 0 && coarse == agg_level_;
+      const bool fuse_zg = !into_agg && coarse != nl - 1 && prm.num_sweeps[1] >= 1 &&
                            (prm.relax_type[1] == 18 || prm.relax_type[1] == 7) && prm.relax_weight == 1.0 &&
                            lev_[coarse].l1 != nullptr;
       if (fuse_zg) {
         apply(Lf.R, &Lf.hv, K_RESTRICT_ZG, Lf.V, nullptr, lev_[coarse].l1, nullptr, 0, lev_[coarse].F, 1.0, 0.0,
               s, ucur[coarse]);
+      } else if (into_agg) {
+        // this rank's share of the replicated level's rows, then everyone's
+        const int r0 = agg_starts_[comm_->rank()];
+        apply(Lf.R, &Lf.hv, K_RESTRICT, Lf.V, nullptr, nullptr, nullptr, 0, lev_[coarse].F + r0, 1.0, 0.0, s);
+        allgather_rows(lev_[coarse].F, agg_starts_, s);
       } else {
         apply(Lf.R, &Lf.hv, K_RESTRICT, Lf.V, nullptr, nullptr, nullptr, 0, lev_[coarse].F, 1.0, 0.0, s);
       }

@@ -159,6 +159,7 @@ class DevAMG {
   void halo_start(const DevHalo& h, double* x, hipStream_t s);
   void halo_finish(hipStream_t s);
   void coarse_solve(int level, const double* f, double* u, hipStream_t s);
+  void allgather_rows(double* v, const std::vector<int>& starts, hipStream_t s);
 
   std::vector<DevLevel> lev_;
   int coarse_n_ = 0;
@@ -181,6 +182,8 @@ class DevAMG {
   double cycle_ops_ = 0;
   int ws_n_ = 0;
   std::map<std::tuple<const void*, const void*, bool>, hipGraphExec_t> graphs_;
+  int agg_level_ = -1;            // first replicated level (RankHierarchy::agg_level)
+  std::vector<int> agg_starts_;   // its rows' distributed owners
 };
 
 // PCG (krylov/pcg.c:262).

@@ -639,23 +639,54 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
   out.rank = rank;
   out.size = size;
   out.prm = prm;
+  // rows of every rank, in rank order (= global row order), on every rank
+  auto gather_rows = [&](const CSR& M, int nglob_rows) {
+    std::vector<int> len(M.nrows);
+    for (int r = 0; r < M.nrows; ++r) len[r] = M.i[r + 1] - M.i[r];
+    auto alen = comm.allgatherv(len);
+    auto acol = comm.allgatherv(M.j);
+    auto aval = comm.allgatherv(M.a);
+    CSR G;
+    G.resize_rows(nglob_rows, M.ncols);
+    for (int r = 0; r < nglob_rows; ++r) G.i[r + 1] = G.i[r] + alen[r];
+    G.j.swap(acol);
+    G.a.swap(aval);
+    return G;
+  };
   // coarsest-level direct solve: the coarsest operator gathered on every rank
   if (nl > 1 && (prm.relax_type[3] == 9 || prm.relax_type[3] == 99 || prm.relax_type[3] == 19 ||
                  prm.relax_type[3] == 98)) {
     const DLevel& D = L[nl - 1];
     if (D.nglob > 8192) throw std::runtime_error("coarsest level too large for the dense direct solve");
-    std::vector<int> len(D.nloc);
-    for (int r = 0; r < D.nloc; ++r) len[r] = D.A.i[r + 1] - D.A.i[r];
-    auto alen = comm.allgatherv(len);
-    auto acol = comm.allgatherv(D.A.j);
-    auto aval = comm.allgatherv(D.A.a);
-    CSR G;
-    G.resize_rows(D.nglob, D.nglob);
-    for (int r = 0; r < D.nglob; ++r) G.i[r + 1] = G.i[r] + alen[r];
-    G.j.swap(acol);
-    G.a.swap(aval);
+    CSR G = gather_rows(D.A, D.nglob);
+    G.ncols = D.nglob;
     out.coarse_n = D.nglob;
     csr_to_dense(G, out.coarse_dense);
+  }
+  // coarse-level agglomeration (partition.hpp): levels >= agg held whole
+  std::vector<int64_t> grows(nl);
+  for (int l = 0; l < nl; ++l) grows[l] = L[l].nglob;
+  const int agg = agglomeration_level(prm, grows, size);
+  int agg_share = 0;  // this rank's rows of level agg (the restriction's output)
+  out.agg_level = agg;
+  if (agg >= 0) {
+    out.agg_starts = L[agg].starts;
+    agg_share = L[agg].nloc;
+    for (int l = agg; l < nl; ++l) {
+      DLevel& D = L[l];
+      D.A = gather_rows(D.A, D.nglob);
+      if (l + 1 < nl) {
+        D.P = gather_rows(D.P, D.nglob);
+        D.R = gather_rows(D.R, L[l + 1].nglob);
+      }
+      D.cf = comm.allgatherv(D.cf);
+      D.l1 = comm.allgatherv(D.l1);
+    }
+    for (int l = agg; l < nl; ++l) {
+      DLevel& D = L[l];
+      D.first = 0;
+      D.nloc = D.nglob;
+    }
   }
   double tot_rows = 0, tot_nnz = 0;
   for (auto& D : L) { tot_rows += D.nglob; tot_nnz += (double)D.nnz_glob; }
@@ -669,6 +700,7 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
   std::vector<std::vector<int>> hu(nl), hv(nl);
   for (int l = 0; l < nl; ++l) {
     const DLevel& D = L[l];
+    if (agg >= 0 && l >= agg) continue;  // replicated: no halos
     std::vector<int> u;
     offrank_cols(D.A, D.first, D.first + D.nloc, u);
     if (l > 0) offrank_cols(L[l - 1].P, D.first, D.first + D.nloc, u);
@@ -692,12 +724,18 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     if (l + 1 < nl) {
       const DLevel& C = L[l + 1];
       make_rank_op(D.P, 0, D.nloc, C.first, C.first + C.nloc, hu[l + 1], RL.P);
-      make_rank_op(D.R, 0, C.nloc, D.first, D.first + D.nloc, hv[l], RL.R);
+      const int rrows = (agg >= 0 && l + 1 == agg) ? agg_share : C.nloc;
+      make_rank_op(D.R, 0, rrows, D.first, D.first + D.nloc, hv[l], RL.R);
     }
     RL.l1 = D.l1;
     RL.cf = D.cf;
-    RL.hu = make_halo(hu[l], D.first, D.nloc, D.starts, comm);
-    if (l + 1 < nl) RL.hv = make_halo(hv[l], D.first, D.nloc, D.starts, comm);
+    if (agg >= 0 && l >= agg) {
+      RL.hu.n_loc = D.nloc;
+      if (l + 1 < nl) RL.hv.n_loc = D.nloc;
+    } else {
+      RL.hu = make_halo(hu[l], D.first, D.nloc, D.starts, comm);
+      if (l + 1 < nl) RL.hv = make_halo(hv[l], D.first, D.nloc, D.starts, comm);
+    }
   }
   return 0;
 }

@@ -92,6 +92,9 @@ struct AMGParams {
   int cheby_scale = 1;      // scale by D^{-1/2}
   int cheby_eig_est = 10;   // CG steps of the eigenvalue estimate (0: inf-norm bound)
   double cheby_fraction = 0.3;
+  // Multi-rank: levels from the first one with at most agglo_rows global rows
+  // down are replicated on every rank (0 = never); see partition.hpp.
+  int agglo_rows = 20000;
 };
 
 struct Level {

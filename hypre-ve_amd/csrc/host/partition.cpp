@@ -89,6 +89,12 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
     for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] == 1);
     for (int r = 0; r <= size; ++r) starts[l + 1][r] = pref[starts[l][r]];
   }
+  std::vector<int64_t> grows(nl);
+  for (int l = 0; l < nl; ++l) grows[l] = H.lev[l].A.nrows;
+  const int agg = agglomeration_level(H.prm, grows, size);
+  // rows of level l this rank holds: its block, or all of a replicated level
+  auto lo = [&](int l, int r) { return (agg >= 0 && l >= agg) ? 0 : starts[l][r]; };
+  auto hi = [&](int l, int r) { return (agg >= 0 && l >= agg) ? H.lev[l].A.nrows : starts[l][r + 1]; };
   out.assign(size, RankHierarchy());
   for (int r = 0; r < size; ++r) {
     RankHierarchy& R = out[r];
@@ -104,6 +110,8 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
       R.nnz_A.push_back(H.lev[l].A.nnz());
       R.rows.push_back(H.lev[l].A.nrows);
     }
+    R.agg_level = agg;
+    if (agg >= 0) R.agg_starts = starts[agg];
   }
   // halo sets per rank per level: u_l (A_l and P_{l-1}) and V_l (R_l)
   std::vector<std::vector<std::vector<int>>> hu(nl, std::vector<std::vector<int>>(size)),
@@ -112,15 +120,19 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
     const Level& L = H.lev[l];
 #pragma omp parallel for schedule(dynamic)
     for (int r = 0; r < size; ++r) {
-      const int a = starts[l][r], b = starts[l][r + 1];
+      const int a = lo(l, r), b = hi(l, r);
       std::vector<int> u;
       halo_cols(L.A, a, b, a, b, u);
-      if (l > 0) halo_cols(H.lev[l - 1].P, starts[l - 1][r], starts[l - 1][r + 1], a, b, u);
+      if (l > 0) halo_cols(H.lev[l - 1].P, lo(l - 1, r), hi(l - 1, r), a, b, u);
       sort_unique(u);
       hu[l][r].swap(u);
       if (l + 1 < nl) {
+        // R_l rows: this rank's rows of level l+1 in the distributed sense
+        // (its share of the restriction into a replicated level too)
         std::vector<int> v;
-        halo_cols(L.R, starts[l + 1][r], starts[l + 1][r + 1], a, b, v);
+        const int ra = (agg >= 0 && l >= agg) ? 0 : starts[l + 1][r];
+        const int rb = (agg >= 0 && l >= agg) ? H.lev[l + 1].A.nrows : starts[l + 1][r + 1];
+        halo_cols(L.R, ra, rb, a, b, v);
         sort_unique(v);
         hv[l][r].swap(v);
       }
@@ -131,15 +143,17 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
 #pragma omp parallel for schedule(dynamic)
     for (int r = 0; r < size; ++r) {
       RankLevel& RL = out[r].lev[l];
-      const int a = starts[l][r], b = starts[l][r + 1];
+      const int a = lo(l, r), b = hi(l, r);
       RL.n_loc = b - a;
       RL.first = a;
       RL.n_glob = L.A.nrows;
       make_op(L.A, a, b, a, b, hu[l][r], RL.A);
       if (l + 1 < nl) {
-        const int ca = starts[l + 1][r], cb = starts[l + 1][r + 1];
+        const int ca = lo(l + 1, r), cb = hi(l + 1, r);
         make_op(L.P, a, b, ca, cb, hu[l + 1][r], RL.P);
-        make_op(L.R, ca, cb, a, b, hv[l][r], RL.R);
+        const int ra = (agg >= 0 && l >= agg) ? 0 : starts[l + 1][r];
+        const int rb = (agg >= 0 && l >= agg) ? H.lev[l + 1].A.nrows : starts[l + 1][r + 1];
+        make_op(L.R, ra, rb, a, b, hv[l][r], RL.R);
       }
       if (!L.l1.empty()) RL.l1.assign(L.l1.begin() + a, L.l1.begin() + b);
       if (!L.cf.empty()) RL.cf.assign(L.cf.begin() + a, L.cf.begin() + b);
@@ -161,9 +175,9 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
         for (int p = 0; p < size; ++p) {
           if (p == r) continue;
           const std::vector<int>& theirs = which == 0 ? hu[l][p] : hv[l][p];
-          auto lo = std::lower_bound(theirs.begin(), theirs.end(), a);
-          auto hi = std::lower_bound(theirs.begin(), theirs.end(), b);
-          for (auto it = lo; it != hi; ++it) sidx[p].push_back(*it - a);
+          auto lo_it = std::lower_bound(theirs.begin(), theirs.end(), a);
+          auto hi_it = std::lower_bound(theirs.begin(), theirs.end(), b);
+          for (auto it = lo_it; it != hi_it; ++it) sidx[p].push_back(*it - a);
           sc[p] = (int)sidx[p].size();
         }
         for (int p = 0; p < size; ++p) {
@@ -176,6 +190,13 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
       }
     }
   }
+}
+
+int agglomeration_level(const AMGParams& prm, const std::vector<int64_t>& rows, int size) {
+  if (size <= 1 || prm.agglo_rows <= 0) return -1;
+  for (size_t l = 1; l < rows.size(); ++l)
+    if (rows[l] <= prm.agglo_rows) return (int)l;
+  return -1;
 }
 
 // Self-check used by the CPU test-suite: reassembles every rank's operators,
@@ -222,7 +243,11 @@ int partition_self_check(const Hierarchy& H, int size, std::string& msg) {
         for (int i = 0; i < in_loc; ++i) xl[i] = x[in_first + i];
         for (int k = 0; k < h.n_halo; ++k) xl[in_loc + k] = x[h.halo_glob[k]];
         const RankOp& op = which == 0 ? L.A : (which == 1 ? L.P : L.R);
-        const int out_first = which == 2 ? all[r].lev[l + 1].first : L.first;
+        // the restriction into the first replicated level writes this rank's
+        // share of its rows (agg_starts); everything else its held rows
+        const int agg = all[r].agg_level;
+        const int out_first = which == 2 ? ((agg >= 0 && l + 1 == agg) ? all[r].agg_starts[r] : all[r].lev[l + 1].first)
+                                         : L.first;
         for (int part = 0; part < 2; ++part) {
           const CSR& M = part == 0 ? op.interior : op.boundary;
           const std::vector<int>& mp = part == 0 ? op.map_int : op.map_bnd;
@@ -345,6 +370,7 @@ void serialize(const RankHierarchy& R, std::vector<char>& buf) {
   w.pod(R.coarse_n); w.vec(R.coarse_dense);
   w.pod(R.grid_complexity); w.pod(R.operator_complexity);
   w.vec(R.nnz_A); w.vec(R.rows);
+  w.pod(R.agg_level); w.vec(R.agg_starts);
 }
 
 void deserialize(const std::vector<char>& buf, RankHierarchy& R) {
@@ -366,6 +392,7 @@ void deserialize(const std::vector<char>& buf, RankHierarchy& R) {
   r.pod(R.coarse_n); r.vec(R.coarse_dense);
   r.pod(R.grid_complexity); r.pod(R.operator_complexity);
   r.vec(R.nnz_A); r.vec(R.rows);
+  r.pod(R.agg_level); r.vec(R.agg_starts);
 }
 
 }  // namespace hve

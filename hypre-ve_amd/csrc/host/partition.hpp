@@ -58,7 +58,18 @@ struct RankHierarchy {
   std::vector<double> coarse_dense;  // replicated coarsest operator
   double grid_complexity = 0, operator_complexity = 0;
   std::vector<int64_t> nnz_A, rows;  // global per-level statistics
+  // Coarse-level agglomeration: levels >= agg_level are held whole by every
+  // rank (first 0, n_loc = n_glob, no halos) and cycled redundantly, without
+  // communication; the restriction into agg_level writes this rank's rows
+  // agg_starts[rank] .. agg_starts[rank+1] and an all-gather completes the
+  // vector.  P of level agg_level-1 reads the replicated vector directly.
+  // -1: no agglomeration (one rank, or agglo_rows 0).
+  int agg_level = -1;
+  std::vector<int> agg_starts;
 };
+// First replicated level for `size` ranks (rank-independent): the first level
+// l >= 1 with rows[l] <= prm.agglo_rows, or -1.
+int agglomeration_level(const AMGParams& prm, const std::vector<int64_t>& rows, int size);
 
 // starts0: level-0 row starts (size+1 entries).
 void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, int rank, int size,

@@ -160,6 +160,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGSetNumBlocks", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetUseGraph", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetSellPolicy", _i, [_p, _i]),
+    ("hypreve_BoomerAMGSetAggloRows", _i, [_p, _i]),
     ("hypreve_BoomerAMGGetComplexities", _i, [_p, _pd, _pd, _pd]),
     ("hypreve_BoomerAMGGetLevelInfo", _i, [_p, _i, _pi, _pi64, _pi64]),
     ("hypreve_BoomerAMGGetLevelMatrix", _i, [_p, _i, _i, _pi, _pi, _pi64, _pi, _pi, _pd]),
@@ -370,6 +371,7 @@ class BoomerAMG:
         "print_level": ("HYPRE_BoomerAMGSetPrintLevel", int), "converge_type": ("HYPRE_BoomerAMGSetConvergeType", int),
         "num_blocks": ("hypreve_BoomerAMGSetNumBlocks", int), "use_graph": ("hypreve_BoomerAMGSetUseGraph", int),
         "sell_policy": ("hypreve_BoomerAMGSetSellPolicy", int),
+        "agglo_rows": ("hypreve_BoomerAMGSetAggloRows", int),
         "cheby_order": ("HYPRE_BoomerAMGSetChebyOrder", int), "cheby_fraction": ("HYPRE_BoomerAMGSetChebyFraction", float),
         "cheby_scale": ("HYPRE_BoomerAMGSetChebyScale", int), "cheby_variant": ("HYPRE_BoomerAMGSetChebyVariant", int),
         "cheby_eig_est": ("HYPRE_BoomerAMGSetChebyEigEst", int),

@@ -226,6 +226,11 @@ HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_block
  * x-tile (per-slice column dictionary).  All give identical
  * bits; the forced settings exist for parity tests and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
+/* Multi-rank: coarse levels with at most `rows` global rows (from the first
+ * such level down) are held whole by every rank and cycled redundantly, with
+ * one all-gather on the way down instead of halo exchanges on every coarse
+ * level (same bits).  0 = never; default 20000. */
+HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver solver, HYPRE_Int rows);
 /* Whole-cycle hipGraph capture on/off (default on). */
 HYPRE_Int hypreve_BoomerAMGSetUseGraph(HYPRE_Solver solver, HYPRE_Int use_graph);
 /* Statistics after Setup: levels, complexities, per-level rows/nnz. */

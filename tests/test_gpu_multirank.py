@@ -67,10 +67,13 @@ def _solve_nranks(hv, nx, ny, nz, kw, nranks, timeout=300, stencil=7):
 
 
 @pytest.mark.parametrize("nranks,nx,nz", [(2, 16, 16), (3, 14, 20), (4, 12, 13)])
+@pytest.mark.parametrize("agglo", [0, 2000])
 @pytest.mark.parametrize("relax", [18, 0])
-def test_loopback_partitioned_solve_bitwise(hv, nranks, nx, nz, relax):
+def test_loopback_partitioned_solve_bitwise(hv, nranks, nx, nz, relax, agglo):
+    """agglo 0: every level distributed; 2000: the coarse levels from the first
+    one under 2000 rows are replicated on every rank (one all-gather down)."""
     kw = hv.ij_amg_defaults(0)
-    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=relax, tol=1e-8, max_iter=60)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=relax, tol=1e-8, max_iter=60, agglo_rows=agglo)
     if relax == 0:
         kw.update(relax_wt=0.6)
     x1, it1, rr1, nl1 = _solve_1rank(hv, nx, nx, nz, kw)

@@ -85,16 +85,18 @@ def test_partition_self_check(hv):
     [local | halo] vectors reproduce the global operators row for row (bitwise),
     and the pairwise halo send/recv plans agree."""
     A = hv.ParCSRMatrix.laplacian(20, 18, 24)
-    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
-    amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4)
-    amg.setup_host(A)
-    for size in (1, 2, 3, 4, 7, 8):
-        amg.partition_check(size)
+    for agglo in (0, 2000, 20000):
+        amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+        amg.set(coarsen_type=8, relax_type=18, P_max_elmts=4, agglo_rows=agglo)
+        amg.setup_host(A)
+        for size in (1, 2, 3, 4, 7, 8):
+            amg.partition_check(size)
 
 
+@pytest.mark.parametrize("agglo", [0, 20000])
 @pytest.mark.parametrize("size", [1, 2, 3, 5, 8])
 @pytest.mark.parametrize("stencil,relax,order", [(7, 18, 0), (7, 0, 1), (27, 18, 0), (7, 13, 0)])
-def test_distributed_setup_matches_one_process(hv, size, stencil, relax, order):
+def test_distributed_setup_matches_one_process(hv, size, stencil, relax, order, agglo):
     """Distributed setup (each rank builds its rows' levels from a ghost
     layer: PMIS passes exchanging measures / demotions / C-F state, ext+i over
     fetched neighbour rows, R from P entries sent to their coarse owner, RAP
@@ -106,7 +108,7 @@ def test_distributed_setup_matches_one_process(hv, size, stencil, relax, order):
     else:
         A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=1.0, cy=0.7 if relax == 0 else 1.0, cz=1.0)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
-    amg.set(coarsen_type=8, interp_type=6, relax_type=relax, relax_order=order, P_max_elmts=4)
+    amg.set(coarsen_type=8, interp_type=6, relax_type=relax, relax_order=order, P_max_elmts=4, agglo_rows=agglo)
     amg.dist_setup_check(A, size)
 
 
