@@ -20,7 +20,8 @@ struct SellView {
   const unsigned short* col16 = nullptr;  // dictionary layout (k_sell_dict): local columns
   const int* dict_ptr = nullptr;
   const int* dict = nullptr;
-  int dmax = 0;                    // dictionary layout: largest slice dictionary (LDS doubles)
+  int dmax = 0;                    // dictionary layout: largest dictionary (LDS doubles)
+  int dict_group = 1;              // dictionary layout: slices per dictionary / workgroup (1 or 4)
 };
 
 enum : int {

@@ -544,19 +544,23 @@ __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp,
   }
 }
 
-template <int OP, bool CFSEL, int B, bool NT>
-__global__ void __launch_bounds__(64) k_sell_dict(SpArgs p) {
+template <int OP, bool CFSEL, int B, bool NT, int G>
+__global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   extern __shared__ double xl[];
-  const int slice = xcd_logical_block(blockIdx.x, p.nblocks_pad);
-  if (slice * kWave >= p.nrows) return;  // the (single-wave) workgroup is past the end
-  const int lane = threadIdx.x;
+  // G waves per workgroup share one dictionary (the distinct columns of G
+  // consecutive slices); wave w runs slice group * G + w.
+  const int group = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  if (group * G * kWave >= p.nrows) return;  // the whole workgroup is past the end
+  const int lane = threadIdx.x & (kWave - 1);
+  const int slice = group * G + (threadIdx.x >> 6);
+  const bool wave_live = slice * kWave < p.nrows;  // uniform per wave
   const int row = slice * kWave + lane;
   // Row metadata and the first batch of matrix loads go out before the
   // x-tile gather, so their latency overlaps it.
-  const int blen = mload<NT>(p.rowlen + row);  // 0 past the last row
+  const int blen = wave_live ? mload<NT>(p.rowlen + row) : 0;  // 0 past the last row
   const int width = __builtin_amdgcn_readfirstlane(blen);  // sorted: lane 0 is the longest
-  const int beg = p.slice_ptr[slice];
-  const bool own = row < p.nrows;
+  const int beg = wave_live ? p.slice_ptr[slice] : 0;
+  const bool own = wave_live && row < p.nrows;
   const bool SUB = op_subtracts<OP>();
   const bool sub = SUB || (OP == OP_GENERAL && p.w == -1.0);
   int g = 0;
@@ -580,15 +584,16 @@ __global__ void __launch_bounds__(64) k_sell_dict(SpArgs p) {
   int c[B];
   double a[B];
   dict_load<B, NT>(cp, vp, P, k0, blen, llen, c, a);
-  // 1. x-tile: x[dict[d0 .. d1)] -> LDS, TG gathers in flight per lane
+  // 1. x-tile: x[dict[d0 .. d1)] -> LDS, TG gathers in flight per thread
   {
-    constexpr int TG = 16;
-    const int d0 = p.dict_ptr[slice], m = p.dict_ptr[slice + 1] - d0;
-    for (int j0 = 0; j0 < m; j0 += TG * kWave) {
+    constexpr int TG = 16 / G > 4 ? 16 / G : 4;
+    constexpr int NT_ = 64 * G;
+    const int d0 = p.dict_ptr[group], m = p.dict_ptr[group + 1] - d0;
+    for (int j0 = 0; j0 < m; j0 += TG * NT_) {
       int idx[TG];
 #pragma unroll
       for (int i = 0; i < TG; ++i) {
-        const int j = j0 + i * kWave + lane;
+        const int j = j0 + i * NT_ + (int)threadIdx.x;
         idx[i] = j < m ? mload<NT>(p.dict + d0 + j) : -1;
       }
       double v[TG];
@@ -596,12 +601,13 @@ __global__ void __launch_bounds__(64) k_sell_dict(SpArgs p) {
       for (int i = 0; i < TG; ++i) v[i] = idx[i] >= 0 ? p.x[idx[i]] : 0.0;
 #pragma unroll
       for (int i = 0; i < TG; ++i) {
-        const int j = j0 + i * kWave + lane;
+        const int j = j0 + i * NT_ + (int)threadIdx.x;
         if (j < m) xl[j] = v[i];
       }
     }
   }
   __syncthreads();
+  if (!wave_live) return;
   // 2. jagged row loop over local columns
   for (int k = k0; k < width; k += B) {
     int cn[B];
@@ -903,13 +909,20 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   const bool pipe = sell_pipe_override() >= 0 ? sell_pipe_override() == 1 : M.pipe != 0;
   const bool nt = sell_nt();
   const bool jag = M.rowlen != nullptr;
-  if (M.col16) {  // dictionary layout: one wave per slice, x-tile in LDS
-    a.nblocks_pad = ((M.nrows + 63) / 64 + 7) / 8 * 8;
-    const dim3 dgrid(a.nblocks_pad), dblock(64);
+  if (M.col16) {  // dictionary layout: G waves per workgroup share an x-tile in LDS
+    const int G = M.dict_group > 1 ? 4 : 1;
+    const int ngroups = ((M.nrows + 63) / 64 + G - 1) / G;
+    a.nblocks_pad = (ngroups + 7) / 8 * 8;
+    const dim3 dgrid(a.nblocks_pad), dblock(64 * G);
     const size_t lds = (size_t)M.dmax * sizeof(double);
-#define HVE_D(OPV, CF, BB)                                                                      \
-  if (nt) hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, true>), dgrid, dblock, lds, s, a);      \
-  else hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, false>), dgrid, dblock, lds, s, a);
+#define HVE_D(OPV, CF, BB)                                                                             \
+  if (G == 4) {                                                                                        \
+    if (nt) hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, true, 4>), dgrid, dblock, lds, s, a);        \
+    else hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, false, 4>), dgrid, dblock, lds, s, a);          \
+  } else {                                                                                             \
+    if (nt) hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, true, 1>), dgrid, dblock, lds, s, a);        \
+    else hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, false, 1>), dgrid, dblock, lds, s, a);          \
+  }
 #define HVE_DB(OPV, CF) \
   if (bsel == 16) { HVE_D(OPV, CF, 16) } else { HVE_D(OPV, CF, 8) }
 #define HVE_DL(OPV)                                                 \

@@ -102,7 +102,22 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
     std::vector<unsigned short> c16;
     std::vector<int> dp, dc, rl2;
     int mxd = 0;
-    if (build_sell_dict_host(A, 4096, perm, sp, rl2, c16, val, dp, dc, mxd)) {
+    // Square operators: one dictionary per workgroup of 4 slices
+    // (neighbouring slices share most of their columns; A1 at 256^3 419 vs
+    // 472 us) where it fits 64 KiB of LDS, else per slice.  Restrictions keep
+    // one per slice (R1 76 vs 83 us grouped).  HVE_SELL_DICT_GROUP=1|4 forces it.
+    static const int group_env = [] {
+      const char* e = getenv("HVE_SELL_DICT_GROUP");
+      return e ? atoi(e) : 0;
+    }();
+    int group = group_env == 1 ? 1 : group_env == 4 ? 4 : (A.nrows == A.ncols ? 4 : 1);
+    bool built = build_sell_dict_host(A, group == 4 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd);
+    if (!built && group == 4 && group_env == 0) {
+      group = 1;
+      built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd);
+    }
+    if (built) {
+      dict_group = group;
       nrows = A.nrows;
       ncols = A.ncols;
       nslices = (int)sp.size() - 1;
@@ -174,7 +189,7 @@ void DevSell::release() {
   if (dict_ptr) (void)hipFree(dict_ptr);
   if (dict) (void)hipFree(dict);
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
-  col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0;
+  col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;
 }
 

@@ -37,6 +37,7 @@ struct DevSell {
   int* dict_ptr = nullptr;
   int* dict = nullptr;
   int dmax = 0;
+  int dict_group = 1;
   int batch = 8;
   int pipe = 0;
   int wide = 0;
@@ -44,7 +45,7 @@ struct DevSell {
   SellView view() const {
     SellView v;
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
-    v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax;
+    v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map

@@ -122,70 +122,76 @@ void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<in
 // loop.  Entry order, row order (sorted inside the slice) and rowlen are those
 // of build_sell_jagged_host.  Returns false (and builds nothing) when a slice
 // references more than dmax distinct columns.
-bool build_sell_dict_host(const CSR& A, int dmax, std::vector<int>& perm, std::vector<int>& slice_ptr,
+bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& perm, std::vector<int>& slice_ptr,
                           std::vector<int>& rowlen, std::vector<unsigned short>& col16, std::vector<double>& val,
                           std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct) {
   if (dmax > 65535) dmax = 65535;
+  if (group < 1) group = 1;
   const int n = A.nrows;
   const int ns = (n + 63) / 64;
+  const int ng = (ns + group - 1) / group;
   sell_order(A, 64, perm);
-  // distinct columns per slice
-  std::vector<int64_t> dcount(ns, 0);
-  int mx = 0;
-#pragma omp parallel for schedule(static) reduction(max : mx)
-  for (int s = 0; s < ns; ++s) {
-    std::vector<int> cols;
-    const int r1 = std::min(n, (s + 1) * 64);
-    for (int r = s * 64; r < r1; ++r)
+  // distinct columns of each group of `group` slices (one workgroup)
+  auto group_cols = [&](int g, std::vector<int>& cols) {
+    cols.clear();
+    const int r0 = g * group * 64, r1 = std::min(n, (g + 1) * group * 64);
+    for (int r = r0; r < r1; ++r)
       for (int k = A.i[perm[r]]; k < A.i[perm[r] + 1]; ++k) cols.push_back(A.j[k]);
     std::sort(cols.begin(), cols.end());
-    const int d = (int)(std::unique(cols.begin(), cols.end()) - cols.begin());
-    dcount[s] = d;
-    mx = std::max(mx, d);
+    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
+  };
+  std::vector<int64_t> dcount(ng, 0);
+  int mx = 0;
+#pragma omp parallel for schedule(static) reduction(max : mx)
+  for (int g = 0; g < ng; ++g) {
+    std::vector<int> cols;
+    group_cols(g, cols);
+    dcount[g] = (int64_t)cols.size();
+    mx = std::max(mx, (int)cols.size());
   }
   max_distinct = mx;
   if (mx > dmax) return false;
-  std::vector<int64_t> sp(ns + 1, 0), dp(ns + 1, 0);
+  std::vector<int64_t> sp(ns + 1, 0), dp(ng + 1, 0);
   for (int s = 0; s < ns; ++s) {
     int64_t t = 0;
     const int r1 = std::min(n, (s + 1) * 64);
     for (int r = s * 64; r < r1; ++r) t += A.i[perm[r] + 1] - A.i[perm[r]];
     sp[s + 1] = sp[s] + t;
-    dp[s + 1] = dp[s] + dcount[s];
   }
-  if (sp[ns] > 0x7fffffffLL || dp[ns] > 0x7fffffffLL) throw std::runtime_error("operator exceeds 2^31 entries on one GPU");
+  for (int g = 0; g < ng; ++g) dp[g + 1] = dp[g] + dcount[g];
+  if (sp[ns] > 0x7fffffffLL || dp[ng] > 0x7fffffffLL) throw std::runtime_error("operator exceeds 2^31 entries on one GPU");
   slice_ptr.assign(ns + 1, 0);
-  dict_ptr.assign(ns + 1, 0);
-  for (int s = 0; s <= ns; ++s) { slice_ptr[s] = (int)sp[s]; dict_ptr[s] = (int)dp[s]; }
+  dict_ptr.assign(ng + 1, 0);
+  for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
+  for (int g = 0; g <= ng; ++g) dict_ptr[g] = (int)dp[g];
   rowlen.assign((size_t)ns * 64, 0);
   col16.assign((size_t)sp[ns], 0xFFFF);
   val.assign((size_t)sp[ns], 0.0);
-  dict.assign((size_t)dp[ns], 0);
+  dict.assign((size_t)dp[ng], 0);
 #pragma omp parallel for schedule(static)
-  for (int s = 0; s < ns; ++s) {
-    const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
+  for (int g = 0; g < ng; ++g) {
     std::vector<int> cols;
-    for (int r = r0; r < r1; ++r)
-      for (int k = A.i[perm[r]]; k < A.i[perm[r] + 1]; ++k) cols.push_back(A.j[k]);
-    std::sort(cols.begin(), cols.end());
-    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
-    std::copy(cols.begin(), cols.end(), dict.begin() + dict_ptr[s]);
-    int len[64] = {0};
-    for (int r = r0; r < r1; ++r) {
-      len[r - r0] = A.i[perm[r] + 1] - A.i[perm[r]];
-      rowlen[r] = len[r - r0];
-    }
-    size_t pos = (size_t)slice_ptr[s];
-    for (int k = 0; k < len[0]; ++k) {
-      int cnt = 0;
-      while (cnt < r1 - r0 && len[cnt] > k) ++cnt;  // lanes sorted by descending length
-      for (int l = 0; l < cnt; ++l) {
-        const int src = perm[r0 + l];
-        const int c = A.j[A.i[src] + k];
-        col16[pos + l] = (unsigned short)(std::lower_bound(cols.begin(), cols.end(), c) - cols.begin());
-        val[pos + l] = A.a[A.i[src] + k];
+    group_cols(g, cols);
+    std::copy(cols.begin(), cols.end(), dict.begin() + dict_ptr[g]);
+    for (int s = g * group; s < std::min(ns, (g + 1) * group); ++s) {
+      const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
+      int len[64] = {0};
+      for (int r = r0; r < r1; ++r) {
+        len[r - r0] = A.i[perm[r] + 1] - A.i[perm[r]];
+        rowlen[r] = len[r - r0];
       }
-      pos += cnt;
+      size_t pos = (size_t)slice_ptr[s];
+      for (int k = 0; k < len[0]; ++k) {
+        int cnt = 0;
+        while (cnt < r1 - r0 && len[cnt] > k) ++cnt;  // lanes sorted by descending length
+        for (int l = 0; l < cnt; ++l) {
+          const int src = perm[r0 + l];
+          const int c = A.j[A.i[src] + k];
+          col16[pos + l] = (unsigned short)(std::lower_bound(cols.begin(), cols.end(), c) - cols.begin());
+          val[pos + l] = A.a[A.i[src] + k];
+        }
+        pos += cnt;
+      }
     }
   }
   return true;

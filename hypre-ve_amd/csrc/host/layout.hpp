@@ -21,7 +21,8 @@ void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<in
 // Jagged SELL-64 with a per-slice column dictionary (16-bit local column
 // indices into the slice's ascending list of distinct columns).  false when
 // a slice has more than dmax distinct columns; max_distinct is set either way.
-bool build_sell_dict_host(const CSR& A, int dmax, std::vector<int>& perm, std::vector<int>& slice_ptr,
+// group: slices sharing one dictionary (one workgroup of `group` waves).
+bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& perm, std::vector<int>& slice_ptr,
                           std::vector<int>& rowlen, std::vector<unsigned short>& col16, std::vector<double>& val,
                           std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct);
 // Padded entry count of the SELL-64 layout for a given sigma (0 = no sort).

@@ -26,7 +26,7 @@ if [[ $WHAT == all || $WHAT == sweep ]]; then
   step sweep_auto 300 python scripts/level_sweep.py --json $OUT/sweep_auto.json
   step bench 600 python bench.py --steps 10 --warmup 2 --cpu-cycles 0
   for v in ${SWEEP_VARIANTS:-HVE_SELL_JAG=0}; do
-    env ${v//,/ } python scripts/level_sweep.py --json $OUT/sweep_$v.json > $OUT/sweep_$v.log 2>&1 || exit 1
+    timeout -k 10 300 env ${v//,/ } python scripts/level_sweep.py --json $OUT/sweep_$v.json > $OUT/sweep_$v.log 2>&1 || exit 1
     tail -2 $OUT/sweep_$v.log
   done
 fi
