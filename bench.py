@@ -136,14 +136,21 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     # roofline: finest-level SpMV (the dominant kernel), HIP events on the solver stream
     spmv_ms, spmv_bytes = amg.bench_fine_spmv(args.spmv_reps)
     achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    stored_bytes = amg.fine_spmv_stored_bytes()
     traffic = committed_traffic(n, spmv_bytes)
     # the box's achievable read bandwidth: a grid-stride 8 B/lane stream over 2 GiB
     stream_n = (1 << 31) // 8
     stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 10) * 1e-3) / 1e9
+    if args.calib:
+        for eb in (2, 4, 8):
+            hv.bench_stream(eb, (1 << 29) // eb, 1)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "k_sell<OP_RESID> finest level (r = b - A x)", "avg_ms": round(spmv_ms, 4),
+            "kernel": "k_sell_delta<OP_RESID> finest level (r = b - A x)", "avg_ms": round(spmv_ms, 4),
             "bytes_per_launch": spmv_bytes,
+            # what the stored layout streams (10 B an entry with 16-bit column deltas)
+            "stored_bytes_per_launch": stored_bytes,
+            "stored_gbs": round(stored_bytes / (spmv_ms * 1e-3) / 1e9, 1),
             "stream_read_gbs": round(stream_gbs, 1), "frac_of_stream": round(achieved / stream_gbs, 4)}
     if rank == 0:
         import resource
@@ -217,6 +224,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
     ap.add_argument("--cpu-cycles-max", type=int, default=60)
     ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--calib", action="store_true",
+                    help="also run 512 MiB read streams of 2/4/8-B elements (PMC FETCH_SIZE calibration)")
     ap.add_argument("--solver", choices=["amg", "pcg"], default="amg",
                     help="amg: a step is one BoomerAMG solve iteration (the metric); pcg: one PCG iteration "
                          "preconditioned by one V-cycle (configs[2], reported separately)")

@@ -710,7 +710,7 @@ HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver s, HYPRE_Int rows) {
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  CHECK_ARG(policy >= 0 && policy <= 5, 2);
+  CHECK_ARG(policy >= 0 && policy <= 6, 2);
   s->prm.sell_policy = policy;
   return 0;
 }
@@ -1171,6 +1171,17 @@ HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver s, HYPRE_Int reps, HYPRE_Real* avg_
   API_END
 }
 
+// Bytes the finest residual SpMV streams in its stored layout (padding, 16-bit
+// column deltas and their slot bases included) plus the three vectors: what
+// the layout moves, beside BenchFineSpMV's algorithmic (CSR) bytes.
+HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver s, HYPRE_Real* bytes) {
+  CHECK_ARG(s && s->dev && s->dev->built() && bytes, 1);
+  API_BEGIN
+  const DevSell& A = s->dev->level(0).A.in;
+  *bytes = (double)A.bytes() + (double)A.nrows * 24.0;
+  API_END
+}
+
 // Host check of every hybrid Gauss-Seidel level schedule of the hierarchy
 // (both directions, diagonal and l1 scaling) against the sequential sweep.
 HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver s, HYPRE_Int num_blocks) {
@@ -1247,7 +1258,7 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
 // calibration pass for rocprofv3 FETCH_SIZE at this access width and the
 // achievable-bandwidth reference for the roofline.
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real* avg_ms) {
-  CHECK_ARG(elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16, 1);
+  CHECK_ARG(elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16, 1);
   CHECK_ARG(n > 0, 2);
   CHECK_ARG(reps > 0, 3);
   API_BEGIN

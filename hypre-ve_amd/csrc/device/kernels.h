@@ -22,6 +22,8 @@ struct SellView {
   const int* dict = nullptr;
   int dmax = 0;                    // dictionary layout: largest dictionary (LDS doubles)
   int dict_group = 1;              // dictionary layout: slices per dictionary / workgroup (1 or 4)
+  const short* dcol = nullptr;     // delta layout (k_sell_delta): col - row - slot base, padded
+  const int* slot_base = nullptr;  // delta layout: base offset per (slice, slot)
 };
 
 enum : int {

@@ -67,6 +67,8 @@ struct SpArgs {
   const unsigned short* __restrict__ col16;  // dictionary layout: local column of each entry
   const int* __restrict__ dict_ptr;          // dictionary layout: per-slice range of dict
   const int* __restrict__ dict;              // dictionary layout: distinct columns, ascending
+  const short* __restrict__ dcol;            // delta layout: col - row - slot base
+  const int* __restrict__ slot_base;         // delta layout: per (slice, slot) base offset
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double w;                       // relax weight / alpha
@@ -367,6 +369,77 @@ __device__ __forceinline__ void row_store(const SpArgs& p, int g, bool skip, dou
     const bool neg = (alpha == -1.0);
     sstore<NT>(p.y + g, (alpha == 1.0 || neg) ? t : alpha * t);
   }
+}
+
+// ---------------------------------------------------------------------------
+// SELL-64 with 16-bit column deltas (host: build_sell_delta_host), for
+// stencil-like operators: column = row + slot_base[slice slot k] + delta, so
+// an entry streams 10 B instead of 12.  The slot base is wave-uniform (scalar
+// load); a padding slot (kDeltaPad) may sit between a row's entries and is
+// skipped, so each row still sums its entries in stored order.
+// ---------------------------------------------------------------------------
+template <int OP, bool CFSEL, int B, bool NT>
+__global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
+  constexpr short PAD = -32768;
+  const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  const int row = lb * 256 + threadIdx.x;
+  if (row >= p.nrows) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int slice = __builtin_amdgcn_readfirstlane(row >> 6);
+  const int g = p.rowmap ? mload<NT>(p.rowmap + row) : row;
+  const int beg = p.slice_ptr[slice];
+  const int width = (p.slice_ptr[slice + 1] - beg) >> 6;
+  const int* __restrict__ sb = p.slot_base + (beg >> 6);
+  const short* __restrict__ cp = p.dcol + beg + lane;
+  const double* __restrict__ vp = p.val + beg + lane;
+  bool skip = false;
+  if (CFSEL) skip = p.cf[g] != p.relax_points;
+  if (CFSEL && skip) {
+    if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) sstore<NT>(p.y + g, p.x[g]);
+    return;
+  }
+  const bool SUB = op_subtracts<OP>();
+  const bool sub = SUB || (OP == OP_GENERAL && p.w == -1.0);
+  double t = row_init<OP, NT>(p, g);
+  double uo = 0.0, d = 0.0;
+  int k0 = 0;
+  if (OP == OP_JAC) {
+    uo = p.x[g];
+    d = width > 0 ? vp[0] : 0.0;  // diagonal stored first, slot 0 of every row
+    k0 = 1;
+  }
+  // Branch-free batches (the host pads slot_base by B slots, so the scalar
+  // base loads run unmasked; a slot past the slice's width re-reads slot k):
+  // a padding entry gathers x[0] (one broadcast line) and its product is
+  // dropped by a select.
+  for (int k = k0; k < width; k += B) {
+    int base[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) base[q] = sb[k + q];
+    short dv[B];
+    double a[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      // a slot past the slice re-reads slot k (same lines, no new bytes)
+      const int kk = (k + q) < width ? k + q : k;
+      dv[q] = mload<NT>(cp + kk * kWave);
+      a[q] = mload<NT>(vp + kk * kWave);
+    }
+    bool on[B];
+    double xv[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      on[q] = (k + q) < width && dv[q] != PAD;
+      xv[q] = p.x[on[q] ? row + base[q] + dv[q] : 0];
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const double pr = a[q] * xv[q];
+      const double tn = sub ? t - pr : t + pr;
+      t = on[q] ? tn : t;
+    }
+  }
+  row_store<OP, NT>(p, g, false, t, uo, d);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -900,6 +973,8 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   a.col16 = M.col16;
   a.dict_ptr = M.dict_ptr;
   a.dict = M.dict;
+  a.dcol = M.dcol;
+  a.slot_base = M.slot_base;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
   a.nblocks_pad = blocks_pad8(M.nrows);
   a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.y2 = y2; a.w = w; a.temp = temp; a.relax_points = relax_points;
@@ -937,6 +1012,26 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_DL
 #undef HVE_DB
 #undef HVE_D
+    return hipGetLastError();
+  }
+  if (M.dcol) {  // 16-bit column deltas, lane per row
+#define HVE_X(OPV, CF, BB)                                                                 \
+  if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true>), grid, block, 0, s, a);    \
+  else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false>), grid, block, 0, s, a);
+#define HVE_XB(OPV, CF) \
+  if (bsel == 16) { HVE_X(OPV, CF, 16) } else { HVE_X(OPV, CF, 8) }
+#define HVE_XL(OPV)                                                 \
+  case OPV:                                                         \
+    if (cfsel) { HVE_XB(OPV, true) } else { HVE_XB(OPV, false) }   \
+    break;
+    switch (op) {
+      HVE_XL(OP_RESID) HVE_XL(OP_MATVEC) HVE_XL(OP_L1JAC) HVE_XL(OP_L1JAC_W) HVE_XL(OP_JAC)
+      HVE_XL(OP_PROLONG) HVE_XL(OP_RESTRICT) HVE_XL(OP_GENERAL) HVE_XL(OP_RESID_L1JAC) HVE_XL(OP_RESTRICT_ZG)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_XL
+#undef HVE_XB
+#undef HVE_X
     return hipGetLastError();
   }
   if (jag && M.pw) {
@@ -1058,7 +1153,8 @@ hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, 
   if (n_bytes <= 0) return hipSuccess;
   const int64_t n = n_bytes / elem_bytes;
   const dim3 grid(256 * 16), block(256);  // 16 workgroups per CU, 4 waves each
-  if (elem_bytes == 4) hipLaunchKernelGGL(k_stream_read<int>, grid, block, 0, st, n, (const int*)buf, out);
+  if (elem_bytes == 2) hipLaunchKernelGGL(k_stream_read<short>, grid, block, 0, st, n, (const short*)buf, out);
+  else if (elem_bytes == 4) hipLaunchKernelGGL(k_stream_read<int>, grid, block, 0, st, n, (const int*)buf, out);
   else if (elem_bytes == 8) hipLaunchKernelGGL(k_stream_read<double>, grid, block, 0, st, n, (const double*)buf, out);
   else hipLaunchKernelGGL(k_stream_read<int4>, grid, block, 0, st, n, (const int4*)buf, out);
   return hipGetLastError();

@@ -98,6 +98,45 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
     pw = policy == 4 && jag;
     use_dict = policy == 5 && A.nnz() > 0;
   }
+  // 16-bit column deltas against per-(slice, slot) bases where the padded
+  // layout stays and rows are stencil-long (the finest A): 10 B an entry
+  // instead of 12.  Measured on MI355X (256^3): A_0 317 -> 302 us; P (<= 4
+  // entries a row) no gain at level 0 and 59 -> 72 us at level 1, so P keeps
+  // 32-bit columns.  HVE_SELL_DELTA=0 turns it off, 1 also on short rows.
+  static const int delta_env = [] {
+    const char* e = getenv("HVE_SELL_DELTA");
+    return e ? atoi(e) : -1;
+  }();
+  bool use_delta = A.nnz() > 0 && !wide && !jag && !use_dict && delta_env != 0 && sigma_env == 0 &&
+                   (avg_len >= 5.0 || delta_env == 1);
+  if (policy != 0) use_delta = policy == 6 && A.nnz() > 0;
+  if (use_delta) {
+    std::vector<short> dc;
+    std::vector<int> sb;
+    if (build_sell_delta_host(A, sp, sb, dc, val)) {
+      nrows = A.nrows;
+      ncols = A.ncols;
+      nslices = (int)sp.size() - 1;
+      nnz = A.nnz();
+      nnz_pad = (int64_t)sp.back();
+      batch = (nslices > 0 && pad0 > (int64_t)nslices * 64 * 8) ? 16 : 8;
+      pipe = 0;
+      wide = 0;
+      pw = 0;
+      slice_ptr = dupload(sp.data(), sp.size());
+      dcol = dupload(dc.data(), dc.size());
+      slot_base = dupload(sb.data(), std::max<size_t>(1, sb.size()));
+      this->val = dupload(val.data(), val.size());
+      if (!rowmap_h.empty()) {
+        bool ident = true;
+        for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
+        if (!ident) rowmap = dupload(rowmap_h.data(), rowmap_h.size());
+      }
+      return;
+    }
+    sp.clear();
+    val.clear();
+  }
   if (use_dict) {
     std::vector<unsigned short> c16;
     std::vector<int> dp, dc, rl2;
@@ -188,6 +227,9 @@ void DevSell::release() {
   if (col16) (void)hipFree(col16);
   if (dict_ptr) (void)hipFree(dict_ptr);
   if (dict) (void)hipFree(dict);
+  if (dcol) (void)hipFree(dcol);
+  if (slot_base) (void)hipFree(slot_base);
+  dcol = nullptr; slot_base = nullptr;
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
   col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;

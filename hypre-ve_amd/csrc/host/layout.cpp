@@ -69,6 +69,64 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
   if (sigma <= 0) perm.clear();
 }
 
+// SELL-64 with 16-bit column deltas.  Stencil-like operators reference, in
+// entry slot k of a slice, columns at nearly the same offset from their row
+// (the 7-point operator: slot k is the same neighbour for every interior lane).
+// Each (slice, slot) stores one 32-bit base offset; each entry stores
+// col - row - base as a signed 16-bit delta (kDeltaPad = padding).  Rows keep
+// their entry order; a row shorter than the slice's longest is laid into the
+// slots greedily (leftmost slot whose base reaches its next entry, which is
+// optimal for an order-preserving match), so a missing stencil neighbour
+// becomes an interior padding slot instead of shifting the ones after it.
+// Bases come from the slice's first longest row.  Returns false when some row
+// does not fit its slice's slots (the operator then keeps 32-bit columns).
+bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vector<int>& slot_base,
+                           std::vector<short>& dcol, std::vector<double>& val) {
+  const int n = A.nrows;
+  const int ns = (n + 63) / 64;
+  slice_ptr.assign(ns + 1, 0);
+  std::vector<int64_t> sp(ns + 1, 0);
+  std::vector<int> ref(ns, -1);
+  for (int s = 0; s < ns; ++s) {
+    int w = 0;
+    for (int r = s * 64; r < std::min(n, (s + 1) * 64); ++r) {
+      const int len = A.i[r + 1] - A.i[r];
+      if (len > w) { w = len; ref[s] = r; }
+    }
+    sp[s + 1] = sp[s] + (int64_t)w * 64;
+  }
+  if (sp[ns] > 0x7fffffffLL) return false;
+  for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
+  slot_base.assign((size_t)(sp[ns] / 64), 0);
+  dcol.assign((size_t)sp[ns], kDeltaPad);
+  val.assign((size_t)sp[ns], 0.0);
+  int ok = 1;
+#pragma omp parallel for schedule(static) reduction(min : ok)
+  for (int s = 0; s < ns; ++s) {
+    if (ref[s] < 0) continue;
+    const int w = (slice_ptr[s + 1] - slice_ptr[s]) / 64;
+    int* base = slot_base.data() + slice_ptr[s] / 64;
+    const int rr = ref[s];
+    for (int k = 0; k < w; ++k) base[k] = A.j[A.i[rr] + k] - rr;
+    for (int r = s * 64; r < std::min(n, (s + 1) * 64) && ok; ++r) {
+      int k = 0;
+      for (int e = A.i[r]; e < A.i[r + 1]; ++e, ++k) {
+        const int64_t off = (int64_t)A.j[e] - r;
+        while (k < w && (off - base[k] < -32767 || off - base[k] > 32767)) ++k;
+        if (k == w) { ok = 0; break; }
+        const size_t pos = (size_t)slice_ptr[s] + (size_t)k * 64 + (r & 63);
+        dcol[pos] = (short)(off - base[k]);
+        val[pos] = A.a[e];
+      }
+    }
+  }
+  // B = 16 slots of tail padding: the device issues a batch's loads unmasked
+  slot_base.resize(slot_base.size() + 16, 0);
+  dcol.resize(dcol.size() + 16 * 64, kDeltaPad);
+  val.resize(val.size() + 16 * 64, 0.0);
+  return ok != 0;
+}
+
 // Jagged SELL-64: rows sorted by descending length inside each 64-row slice
 // (stable), entry k stored only for the cnt_k lanes whose row is longer than
 // k, at slice_ptr[s] + (cnt_0 + ... + cnt_{k-1}) + lane.  No padding is

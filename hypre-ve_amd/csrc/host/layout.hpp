@@ -12,6 +12,13 @@ namespace hve {
 // and leaves perm empty.
 void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vector<int>& slice_ptr,
                      std::vector<int>& col, std::vector<double>& val);
+// SELL-64 with 16-bit column deltas (row order and entry order kept; padded
+// slots may sit between a row's entries): entry k of the slice's lane r at
+// slice_ptr[s] + 64k + r holds col - row - slot_base[slice_ptr[s]/64 + k], or
+// kDeltaPad for padding.  false when some row does not fit (no layout built).
+constexpr short kDeltaPad = -32768;
+bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vector<int>& slot_base,
+                           std::vector<short>& dcol, std::vector<double>& val);
 // Jagged SELL-64 (no stored padding): perm[i] = CSR row at stored position i
 // (rows sorted by descending length inside each slice), rowlen[i] its length
 // (nslices*64 entries, 0 past the last row), entry k of the slice's lane r at

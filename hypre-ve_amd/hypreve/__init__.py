@@ -173,6 +173,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGCycle", _i, [_p, _p, _p]),
     ("hypreve_BoomerAMGGetKernelStats", _i, [_p, _pd, _i]),
     ("hypreve_BenchFineSpMV", _i, [_p, _i, _pd, _pd]),
+    ("hypreve_BenchFineSpMVStoredBytes", _i, [_p, _pd]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchStream", _i, [_i, C.c_int64, _i, _pd]),
@@ -506,6 +507,12 @@ class BoomerAMG:
         check(lib().hypreve_BenchFineSpMV(self.h, reps, C.byref(ms), C.byref(by)), "BenchFineSpMV")
         return ms.value, by.value
 
+    def fine_spmv_stored_bytes(self):
+        """Bytes the finest SpMV streams in its stored layout (+ vectors)."""
+        by = C.c_double()
+        check(lib().hypreve_BenchFineSpMVStoredBytes(self.h, C.byref(by)), "BenchFineSpMVStoredBytes")
+        return by.value
+
     def destroy(self):
         if self.h:
             lib().HYPRE_BoomerAMGDestroy(self.h)
@@ -560,7 +567,7 @@ def init():
 
 
 def bench_stream(elem_bytes, n, reps=20):
-    """Average ms of a read-only stream over n elements of elem_bytes (4 or 8)."""
+    """Average ms of a read-only stream over n elements of elem_bytes (2, 4, 8 or 16)."""
     ms = C.c_double()
     check(lib().hypreve_BenchStream(elem_bytes, n, reps, C.byref(ms)), "BenchStream")
     return ms.value

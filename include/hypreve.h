@@ -223,7 +223,8 @@ HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_block
 /* Device layout / row loop of the hierarchy's SELL operators (takes effect at
  * Setup): 0 automatic, 1 padded lane-per-row, 2 jagged lane-per-row, 3 padded
  * workgroup-per-slice, 4 jagged wave-product-parallel, 5 jagged with an LDS
- * x-tile (per-slice column dictionary).  All give identical
+ * x-tile (per-slice column dictionary), 6 padded with 16-bit column deltas
+ * against per-slot bases (where a slice's rows fit).  All give identical
  * bits; the forced settings exist for parity tests and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* Multi-rank: coarse levels with at most `rows` global rows (from the first
@@ -272,6 +273,9 @@ HYPRE_Int hypreve_BoomerAMGGetKernelStats(HYPRE_Solver solver, HYPRE_Real *stats
  * events on the solver's stream; returns avg ms and the algorithmic bytes. */
 HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver solver, HYPRE_Int reps, HYPRE_Real *avg_ms,
                                 HYPRE_Real *bytes);
+/* Bytes the same launch streams in the stored layout (padding, 16-bit column
+ * deltas and slot bases included) plus its three vectors. */
+HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver solver, HYPRE_Real *bytes);
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
 HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_blocks);
@@ -279,7 +283,7 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_bl
  * as restriction): average ms over reps, algorithmic bytes, padded entries. */
 HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,
                                HYPRE_Real *avg_ms, HYPRE_Real *bytes, HYPRE_Real *padded_nnz);
-/* Read-only streaming kernel (elem_bytes 4, 8 or 16): FETCH_SIZE calibration. */
+/* Read-only streaming kernel (elem_bytes 2, 4, 8 or 16): FETCH_SIZE calibration. */
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real *avg_ms);
 HYPRE_Int hypreve_DeviceSynchronize(void);
 const char *hypreve_BuildInfo(void);

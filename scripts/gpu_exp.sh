@@ -31,7 +31,7 @@ if [[ $WHAT == all || $WHAT == sweep ]]; then
   done
 fi
 if [[ $WHAT == all || $WHAT == pmc ]]; then
-  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --cpu-cycles 0 --spmv-reps 5
+  step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d $OUT/pmc_fetch -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --cpu-cycles 0 --spmv-reps 5 --calib
   step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d $OUT/pmc_write -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --cpu-cycles 0 --spmv-reps 5
   step pmc_tcc 600 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum --kernel-trace -d $OUT/pmc_tcc -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --cpu-cycles 0 --spmv-reps 5
   python scripts/pmc_traffic.py $OUT 16777216 $OUT/pmc_traffic_256.json > $OUT/pmc_traffic.log 2>&1

@@ -17,15 +17,31 @@ import os
 import sys
 
 
-def mean_counter(path, counter, grid, name_prefix="hve::k_sell<0,"):
+PREFIXES = ("hve::k_sell<0,", "hve::k_sell_delta<0,")
+
+
+def mean_counter(path, counter, grid, prefixes=PREFIXES):
     vals = []
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter or int(r["Grid_Size"]) != grid:
             continue
         nm = r["Kernel_Name"].replace("void ", "")
-        if nm.startswith(name_prefix):
+        if nm.startswith(prefixes):
             vals.append(float(r["Counter_Value"]))
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
+
+
+def stream_calibration(path):
+    """FETCH_SIZE (bytes) / bytes read of bench.py --calib's 512 MiB streams."""
+    out = {}
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != "FETCH_SIZE":
+            continue
+        nm = r["Kernel_Name"].replace("void ", "")
+        for t, eb in (("short", 2), ("int", 4), ("double", 8)):
+            if nm.startswith(f"hve::k_stream_read<{t}>"):
+                out.setdefault(f"{eb}B", []).append(float(r["Counter_Value"]) * 1024 / (1 << 29))
+    return {k: round(min(v), 4) for k, v in out.items()}
 
 
 def main():
@@ -34,11 +50,13 @@ def main():
     write, nw = mean_counter(os.path.join(root, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE", grid)
     if fetch is None or write is None:
         raise SystemExit("no matching dispatches")
-    out = {"kernel": "k_sell<OP_RESID> finest level", "grid": grid, "dispatches": [nf, nw],
+    out = {"kernel": "k_sell / k_sell_delta <OP_RESID> finest level", "grid": grid, "dispatches": [nf, nw],
            "fetch_kib": fetch, "write_kib": write,
            "traffic_bytes": 2.0 * fetch * 1024 + write * 1024,
            "correction": "traffic = 2*FETCH_SIZE + WRITE_SIZE (KiB->B); FETCH x2 per MI355X_MICROARCH.md, "
-                         "checked with the 4/8-B stream calibration kernel"}
+                         "checked with the 4/8-B stream calibration kernel",
+           "fetch_ratio_of_stream_bytes": stream_calibration(
+               os.path.join(root, "pmc_fetch", "run_counter_collection.csv"))}
     print(json.dumps(out, indent=1))
     if len(sys.argv) > 3:
         with open(sys.argv[3], "w") as f:

@@ -78,11 +78,12 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen):
     assert np.array_equal(u.get(), uo)
 
 
-@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5])
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6])
 @pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
 def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
-    workgroup-per-slice, jagged wave-product-parallel) forced on every
+    workgroup-per-slice, jagged wave-product-parallel, jagged with an LDS
+    x-tile, padded with 16-bit column deltas) forced on every
     operator of the hierarchy: the same bits as the oracle.  The automatic
     choice only uses jagged and wide loops on operators too large for the
     other tests, so this is where those loops meet the oracle."""
@@ -107,6 +108,26 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     st = O.solve(f_h, xo, 1e-7, 40)
     assert it == st["iterations"]
     assert np.array_equal(x.get(), xo)
+
+
+def test_delta_layout_wide_stride_bitwise(gpu, orc):
+    """16-bit column deltas where the z-neighbour is 36000 rows away: the
+    per-slot base carries the stride, and the z = 0 / z = last planes (one
+    neighbour missing) put a padding slot between a row's entries.  One cycle
+    and the residual equal the oracle's bits."""
+    hv = gpu
+    A, amg, O = setup_pair(hv, orc, (200, 180, 3), coarsen_type=8, interp_type=6, P_max_elmts=4,
+                           relax_type=18, sell_policy=6)
+    n = A.n
+    rng = np.random.default_rng(5)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
 
 
 @pytest.mark.parametrize("coef", [(0.001, 1.0, 1.0), (1.0, 1.0, 100.0)])
