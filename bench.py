@@ -27,11 +27,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PROFILE_DIR = os.path.join(ROOT, "profiles")
 
 
-def committed_traffic(n, algorithmic_bytes):
+def committed_traffic(n, kernel_suffix):
     """HBM bytes per launch of the finest residual SpMV from the newest
     committed rocprofv3 PMC summary for this workload (scripts/pmc_traffic.py),
-    or None.  Counters need their own profiler passes, so the bench reports
-    the committed measurement of the same kernel and grid."""
+    or None when that summary measured another kernel / layout (its kernel
+    names must end with kernel_suffix).  Counters need their own profiler
+    passes, so the bench reports the committed measurement of the same kernel
+    and grid."""
     best = None
     for rnd in sorted(os.listdir(PROFILE_DIR)) if os.path.isdir(PROFILE_DIR) else []:
         p = os.path.join(PROFILE_DIR, rnd, f"pmc_traffic_{n}.json")
@@ -41,6 +43,9 @@ def committed_traffic(n, algorithmic_bytes):
         return None
     with open(best) as f:
         d = json.load(f)
+    names = d.get("kernel_names", [])
+    if not names or not all(nm.endswith(kernel_suffix) for nm in names):
+        return None
     return round(d["traffic_bytes"], 0)
 
 
@@ -133,11 +138,18 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     if rank == 0:
         log(f"[bench] {args.steps} steps in {elapsed*1e3:.2f} ms -> {ms_per_step:.3f} ms/step, rel.res {rr:.3e}")
 
-    # roofline: finest-level SpMV (the dominant kernel), HIP events on the solver stream
-    spmv_ms, spmv_bytes = amg.bench_fine_spmv(args.spmv_reps)
-    achieved = spmv_bytes / (spmv_ms * 1e-3) / 1e9
+    # roofline: finest-level SpMV (the dominant kernel), HIP events on the solver stream.
+    # achieved = the bytes its stored layout must move (every stored slot once:
+    # 16-bit column delta + 8-bit value index with the value table, 16-bit
+    # delta + 8-B value without; slot bases; x, b, y once) / launch time.  The
+    # CSR-equivalent rate (12 B a nonzero) is reported beside it.
+    spmv_ms, csr_bytes = amg.bench_fine_spmv(args.spmv_reps)
     stored_bytes = amg.fine_spmv_stored_bytes()
-    traffic = committed_traffic(n, spmv_bytes)
+    achieved = stored_bytes / (spmv_ms * 1e-3) / 1e9
+    csr_gbs = csr_bytes / (spmv_ms * 1e-3) / 1e9
+    vt = os.environ.get("HVE_SELL_VALTAB", "1") != "0"
+    # k_sell_delta<OP_RESID, no CF, batch 8, NT, value table?>
+    traffic = committed_traffic(n, "k_sell_delta<0, false, 8, true, %s>(hve::SpArgs)" % ("true" if vt else "false"))
     # the box's achievable read bandwidth: a grid-stride 8 B/lane stream over 2 GiB
     stream_n = (1 << 31) // 8
     stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 10) * 1e-3) / 1e9
@@ -146,16 +158,16 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
             hv.bench_stream(eb, (1 << 29) // eb, 1)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "k_sell_delta<OP_RESID> finest level (r = b - A x)", "avg_ms": round(spmv_ms, 4),
-            "bytes_per_launch": spmv_bytes,
-            # what the stored layout streams (10 B an entry with 16-bit column deltas)
-            "stored_bytes_per_launch": stored_bytes,
-            "stored_gbs": round(stored_bytes / (spmv_ms * 1e-3) / 1e9, 1),
+            "kernel": "k_sell_delta<OP_RESID> finest level (r = b - A x), SELL-64 with 16-bit column deltas" +
+                      (" and an 8-bit value table" if vt else ""),
+            "avg_ms": round(spmv_ms, 4), "bytes_per_launch": stored_bytes,
+            "csr_bytes_per_launch": csr_bytes, "csr_equivalent_gbs": round(csr_gbs, 1),
             "stream_read_gbs": round(stream_gbs, 1), "frac_of_stream": round(achieved / stream_gbs, 4)}
     if rank == 0:
         import resource
         log(f"[bench] read stream {stream_gbs:.0f} GB/s; fine SpMV at {achieved / stream_gbs:.3f} of it")
-        log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {spmv_bytes/1e9:.3f} GB -> {achieved:.1f} GB/s; "
+        log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {stored_bytes/1e9:.3f} GB stored -> {achieved:.1f} GB/s "
+            f"(CSR-equivalent {csr_gbs:.1f} GB/s); "
             f"host peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6:.1f} GB")
 
     cpu = None

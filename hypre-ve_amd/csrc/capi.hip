@@ -710,7 +710,7 @@ HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver s, HYPRE_Int rows) {
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  CHECK_ARG(policy >= 0 && policy <= 6, 2);
+  CHECK_ARG(policy >= 0 && policy <= 7, 2);
   s->prm.sell_policy = policy;
   return 0;
 }

@@ -24,6 +24,9 @@ struct SellView {
   int dict_group = 1;              // dictionary layout: slices per dictionary / workgroup (1 or 4)
   const short* dcol = nullptr;     // delta layout (k_sell_delta): col - row - slot base, padded
   const int* slot_base = nullptr;  // delta layout: base offset per (slice, slot)
+  const unsigned char* vidx = nullptr;  // delta layout: 8-bit value indices (val unused)
+  const double* vtab = nullptr;         // the operator's distinct values
+  int nvtab = 0;
 };
 
 enum : int {

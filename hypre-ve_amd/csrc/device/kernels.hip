@@ -69,6 +69,9 @@ struct SpArgs {
   const int* __restrict__ dict;              // dictionary layout: distinct columns, ascending
   const short* __restrict__ dcol;            // delta layout: col - row - slot base
   const int* __restrict__ slot_base;         // delta layout: per (slice, slot) base offset
+  const unsigned char* __restrict__ vidx;    // delta layout, value table: entry -> vtab index
+  const double* __restrict__ vtab;           // distinct values (<= 256)
+  int nvtab;
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double w;                       // relax weight / alpha
@@ -378,9 +381,16 @@ __device__ __forceinline__ void row_store(const SpArgs& p, int g, bool skip, dou
 // load); a padding slot (kDeltaPad) may sit between a row's entries and is
 // skipped, so each row still sums its entries in stored order.
 // ---------------------------------------------------------------------------
-template <int OP, bool CFSEL, int B, bool NT>
+template <int OP, bool CFSEL, int B, bool NT, bool VI>
 __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
   constexpr short PAD = -32768;
+  // VI: values stored as 8-bit indices into a table of the operator's
+  // distinct values (exact doubles), staged in LDS: 3 B an entry
+  __shared__ double vt[VI ? 256 : 1];
+  if (VI) {
+    for (int i = threadIdx.x; i < p.nvtab; i += 256) vt[i] = p.vtab[i];
+    __syncthreads();
+  }
   const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
   const int row = lb * 256 + threadIdx.x;
   if (row >= p.nrows) return;
@@ -391,7 +401,8 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
   const int width = (p.slice_ptr[slice + 1] - beg) >> 6;
   const int* __restrict__ sb = p.slot_base + (beg >> 6);
   const short* __restrict__ cp = p.dcol + beg + lane;
-  const double* __restrict__ vp = p.val + beg + lane;
+  const double* __restrict__ vp = VI ? nullptr : p.val + beg + lane;
+  const unsigned char* __restrict__ ip = VI ? p.vidx + beg + lane : nullptr;
   bool skip = false;
   if (CFSEL) skip = p.cf[g] != p.relax_points;
   if (CFSEL && skip) {
@@ -405,7 +416,7 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
   int k0 = 0;
   if (OP == OP_JAC) {
     uo = p.x[g];
-    d = width > 0 ? vp[0] : 0.0;  // diagonal stored first, slot 0 of every row
+    d = width > 0 ? (VI ? vt[ip[0]] : vp[0]) : 0.0;  // diagonal stored first, slot 0 of every row
     k0 = 1;
   }
   // Branch-free batches (the host pads slot_base by B slots, so the scalar
@@ -423,7 +434,8 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
       // a slot past the slice re-reads slot k (same lines, no new bytes)
       const int kk = (k + q) < width ? k + q : k;
       dv[q] = mload<NT>(cp + kk * kWave);
-      a[q] = mload<NT>(vp + kk * kWave);
+      if (VI) a[q] = vt[mload<NT>(ip + kk * kWave)];
+      else a[q] = mload<NT>(vp + kk * kWave);
     }
     bool on[B];
     double xv[B];
@@ -975,6 +987,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   a.dict = M.dict;
   a.dcol = M.dcol;
   a.slot_base = M.slot_base;
+  a.vidx = M.vidx;
+  a.vtab = M.vtab;
+  a.nvtab = M.nvtab;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
   a.nblocks_pad = blocks_pad8(M.nrows);
   a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.y2 = y2; a.w = w; a.temp = temp; a.relax_points = relax_points;
@@ -1016,8 +1031,13 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   }
   if (M.dcol) {  // 16-bit column deltas, lane per row
 #define HVE_X(OPV, CF, BB)                                                                 \
-  if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true>), grid, block, 0, s, a);    \
-  else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false>), grid, block, 0, s, a);
+  if (M.vidx) {                                                                                   \
+    if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true, true>), grid, block, 0, s, a);    \
+    else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false, true>), grid, block, 0, s, a);      \
+  } else {                                                                                        \
+    if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true, false>), grid, block, 0, s, a);   \
+    else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false, false>), grid, block, 0, s, a);     \
+  }
 #define HVE_XB(OPV, CF) \
   if (bsel == 16) { HVE_X(OPV, CF, 16) } else { HVE_X(OPV, CF, 8) }
 #define HVE_XL(OPV)                                                 \

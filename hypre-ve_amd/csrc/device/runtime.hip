@@ -109,7 +109,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
   }();
   bool use_delta = A.nnz() > 0 && !wide && !jag && !use_dict && delta_env != 0 && sigma_env == 0 &&
                    (avg_len >= 5.0 || delta_env == 1);
-  if (policy != 0) use_delta = policy == 6 && A.nnz() > 0;
+  if (policy != 0) use_delta = (policy == 6 || policy == 7) && A.nnz() > 0;
   if (use_delta) {
     std::vector<short> dc;
     std::vector<int> sb;
@@ -126,7 +126,22 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
       slice_ptr = dupload(sp.data(), sp.size());
       dcol = dupload(dc.data(), dc.size());
       slot_base = dupload(sb.data(), std::max<size_t>(1, sb.size()));
-      this->val = dupload(val.data(), val.size());
+      // Few distinct values (a constant-coefficient stencil): 8-bit indices
+      // into a table of them, 3 B an entry in all.  HVE_SELL_VALTAB=0 keeps
+      // 8-byte values.
+      static const int vt_env = [] {
+        const char* e = getenv("HVE_SELL_VALTAB");
+        return e ? atoi(e) : 1;
+      }();
+      std::vector<unsigned char> vi;
+      std::vector<double> tab;
+      if ((vt_env != 0 || policy == 7) && policy != 6 && build_value_table(val, 256, vi, tab)) {
+        vidx = dupload(vi.data(), vi.size());
+        vtab = dupload(tab.data(), tab.size());
+        nvtab = (int)tab.size();
+      } else {
+        this->val = dupload(val.data(), val.size());
+      }
       if (!rowmap_h.empty()) {
         bool ident = true;
         for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
@@ -229,7 +244,9 @@ void DevSell::release() {
   if (dict) (void)hipFree(dict);
   if (dcol) (void)hipFree(dcol);
   if (slot_base) (void)hipFree(slot_base);
-  dcol = nullptr; slot_base = nullptr;
+  if (vidx) (void)hipFree(vidx);
+  if (vtab) (void)hipFree(vtab);
+  dcol = nullptr; slot_base = nullptr; vidx = nullptr; vtab = nullptr; nvtab = 0;
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
   col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;

@@ -127,6 +127,48 @@ bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vecto
   return ok != 0;
 }
 
+// Value table (value-indexed storage, lossless): when the stored values take
+// at most maxv distinct bit patterns (constant-coefficient stencils: 2-4),
+// each entry keeps an 8-bit index into the ascending-by-bits table instead of
+// its 8-byte value.  Padding entries index their own (+0.0) pattern.
+bool build_value_table(const std::vector<double>& val, int maxv, std::vector<unsigned char>& idx,
+                       std::vector<double>& tab) {
+  if (maxv > 256) maxv = 256;
+  const size_t n = val.size();
+  std::vector<uint64_t> all;
+  bool over = false;
+#pragma omp parallel
+  {
+    std::vector<uint64_t> mine;
+#pragma omp for schedule(static)
+    for (size_t i = 0; i < n; ++i) {
+      if (over) continue;
+      uint64_t b;
+      std::memcpy(&b, &val[i], 8);
+      if (std::find(mine.begin(), mine.end(), b) == mine.end()) {
+        mine.push_back(b);
+        if ((int)mine.size() > maxv) over = true;
+      }
+    }
+#pragma omp critical
+    all.insert(all.end(), mine.begin(), mine.end());
+  }
+  if (over) return false;
+  std::sort(all.begin(), all.end());
+  all.erase(std::unique(all.begin(), all.end()), all.end());
+  if ((int)all.size() > maxv) return false;
+  tab.resize(all.size());
+  for (size_t t = 0; t < all.size(); ++t) std::memcpy(&tab[t], &all[t], 8);
+  idx.assign(n, 0);
+#pragma omp parallel for schedule(static)
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t b;
+    std::memcpy(&b, &val[i], 8);
+    idx[i] = (unsigned char)(std::lower_bound(all.begin(), all.end(), b) - all.begin());
+  }
+  return true;
+}
+
 // Jagged SELL-64: rows sorted by descending length inside each 64-row slice
 // (stable), entry k stored only for the cnt_k lanes whose row is longer than
 // k, at slice_ptr[s] + (cnt_0 + ... + cnt_{k-1}) + lane.  No padding is

@@ -19,6 +19,11 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
 constexpr short kDeltaPad = -32768;
 bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vector<int>& slot_base,
                            std::vector<short>& dcol, std::vector<double>& val);
+// Lossless value table: idx[i] indexes tab (ascending by bit pattern) with
+// tab[idx[i]] bitwise equal to val[i]; false when more than maxv (<= 256)
+// distinct values occur.
+bool build_value_table(const std::vector<double>& val, int maxv, std::vector<unsigned char>& idx,
+                       std::vector<double>& tab);
 // Jagged SELL-64 (no stored padding): perm[i] = CSR row at stored position i
 // (rows sorted by descending length inside each slice), rowlen[i] its length
 // (nslices*64 entries, 0 past the last row), entry k of the slice's lane r at

@@ -224,7 +224,9 @@ HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_block
  * Setup): 0 automatic, 1 padded lane-per-row, 2 jagged lane-per-row, 3 padded
  * workgroup-per-slice, 4 jagged wave-product-parallel, 5 jagged with an LDS
  * x-tile (per-slice column dictionary), 6 padded with 16-bit column deltas
- * against per-slot bases (where a slice's rows fit).  All give identical
+ * against per-slot bases (where a slice's rows fit), 7 as 6 plus 8-bit value
+ * indices into a table of the operator's distinct values (where at most 256
+ * occur).  All give identical
  * bits; the forced settings exist for parity tests and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* Multi-rank: coarse levels with at most `rows` global rows (from the first

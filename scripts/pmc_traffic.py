@@ -20,7 +20,7 @@ import sys
 PREFIXES = ("hve::k_sell<0,", "hve::k_sell_delta<0,")
 
 
-def mean_counter(path, counter, grid, prefixes=PREFIXES):
+def mean_counter(path, counter, grid, prefixes=PREFIXES, names=None):
     vals = []
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter or int(r["Grid_Size"]) != grid:
@@ -28,6 +28,8 @@ def mean_counter(path, counter, grid, prefixes=PREFIXES):
         nm = r["Kernel_Name"].replace("void ", "")
         if nm.startswith(prefixes):
             vals.append(float(r["Counter_Value"]))
+            if names is not None:
+                names.add(nm)
     return (sum(vals) / len(vals), len(vals)) if vals else (None, 0)
 
 
@@ -46,11 +48,14 @@ def stream_calibration(path):
 
 def main():
     root, grid = sys.argv[1], int(sys.argv[2])
-    fetch, nf = mean_counter(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE", grid)
+    names = set()
+    fetch, nf = mean_counter(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE", grid,
+                             names=names)
     write, nw = mean_counter(os.path.join(root, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE", grid)
     if fetch is None or write is None:
         raise SystemExit("no matching dispatches")
-    out = {"kernel": "k_sell / k_sell_delta <OP_RESID> finest level", "grid": grid, "dispatches": [nf, nw],
+    out = {"kernel": "k_sell / k_sell_delta <OP_RESID> finest level", "kernel_names": sorted(names),
+           "grid": grid, "dispatches": [nf, nw],
            "fetch_kib": fetch, "write_kib": write,
            "traffic_bytes": 2.0 * fetch * 1024 + write * 1024,
            "correction": "traffic = 2*FETCH_SIZE + WRITE_SIZE (KiB->B); FETCH x2 per MI355X_MICROARCH.md, "

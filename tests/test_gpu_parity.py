@@ -78,12 +78,13 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen):
     assert np.array_equal(u.get(), uo)
 
 
-@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
 def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
     workgroup-per-slice, jagged wave-product-parallel, jagged with an LDS
-    x-tile, padded with 16-bit column deltas) forced on every
+    x-tile, padded with 16-bit column deltas, the same with a value table)
+    forced on every
     operator of the hierarchy: the same bits as the oracle.  The automatic
     choice only uses jagged and wide loops on operators too large for the
     other tests, so this is where those loops meet the oracle."""
@@ -110,14 +111,15 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     assert np.array_equal(x.get(), xo)
 
 
-def test_delta_layout_wide_stride_bitwise(gpu, orc):
+@pytest.mark.parametrize("policy", [6, 7])
+def test_delta_layout_wide_stride_bitwise(gpu, orc, policy):
     """16-bit column deltas where the z-neighbour is 36000 rows away: the
     per-slot base carries the stride, and the z = 0 / z = last planes (one
     neighbour missing) put a padding slot between a row's entries.  One cycle
     and the residual equal the oracle's bits."""
     hv = gpu
     A, amg, O = setup_pair(hv, orc, (200, 180, 3), coarsen_type=8, interp_type=6, P_max_elmts=4,
-                           relax_type=18, sell_policy=6)
+                           relax_type=18, sell_policy=policy)
     n = A.n
     rng = np.random.default_rng(5)
     f_h = rng.standard_normal(n)
