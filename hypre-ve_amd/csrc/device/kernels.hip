@@ -419,6 +419,12 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
     d = width > 0 ? (VI ? vt[ip[0]] : vp[0]) : 0.0;  // diagonal stored first, slot 0 of every row
     k0 = 1;
   }
+  // l1 norms formed on the fly (p.l1 == nullptr, set up only where the host
+  // verified that this reproduces the stored norms bit for bit): saves the
+  // l1 stream of the l1-Jacobi sweeps
+  const bool fly = (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC) && p.l1 == nullptr;
+  double s1 = 0.0;
+  bool neg = false, seen = false;
   // Branch-free batches (the host pads slot_base by B slots, so the scalar
   // base loads run unmasked; a slot past the slice's width re-reads slot k):
   // a padding entry gathers x[0] (one broadcast line) and its product is
@@ -450,6 +456,28 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
       const double tn = sub ? t - pr : t + pr;
       t = on[q] ? tn : t;
     }
+    if (fly) {
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        if (on[q] && !seen) { neg = a[q] < 0.0; seen = true; }
+        s1 = on[q] ? s1 + fabs(a[q]) : s1;
+      }
+    }
+  }
+  if (fly) {
+    // compute_l1_norms option 1: sum of |a_ij| in stored order, negated when
+    // the row's first stored entry (its diagonal) is negative
+    const double l1v = neg ? -s1 : s1;
+    if (OP == OP_RESID_L1JAC) {
+      sstore<NT>(p.y + g, t);
+      sstore<NT>(p.y2 + g, p.x[g] + t / l1v);
+    } else if (OP == OP_L1JAC) {
+      sstore<NT>(p.y + g, p.x[g] + t / l1v);
+    } else if (OP == OP_L1JAC_W) {
+      const double v = (-p.w) * t;
+      sstore<NT>(p.y + g, p.x[g] + v / l1v);
+    }
+    return;
   }
   row_store<OP, NT>(p, g, false, t, uo, d);
 }

@@ -233,6 +233,32 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
   for (int i = 0; i < A.nrows && ident; ++i) ident = map[i] == i;
   if (!ident) rowmap = dupload(map.data(), map.size());
 }
+// True when every row's stored l1 norm equals, bit for bit, the sum of |a_ij|
+// over its stored entries in order, negated for a negative first entry
+// (compute_l1_norms option 1 without C/F restriction): the device kernels can
+// then form it on the fly instead of streaming it.
+static bool l1_on_the_fly(const RankOp& op, const std::vector<double>& l1) {
+  static const bool off = [] {
+    const char* e = getenv("HVE_L1_FLY");
+    return e && atoi(e) == 0;
+  }();
+  if (off) return false;
+  int ok = 1;
+  for (int part = 0; part < 2; ++part) {
+    const CSR& A = part == 0 ? op.interior : op.boundary;
+    const std::vector<int>& map = part == 0 ? op.map_int : op.map_bnd;
+#pragma omp parallel for schedule(static) reduction(min : ok)
+    for (int i = 0; i < A.nrows; ++i) {
+      double s = 0.0;
+      for (int q = A.i[i]; q < A.i[i + 1]; ++q) s += std::fabs(A.a[q]);
+      if (A.i[i + 1] > A.i[i] && A.a[A.i[i]] < 0.0) s = -s;
+      const int g = map.empty() ? i : map[i];
+      if (g < 0 || g >= (int)l1.size() || std::memcmp(&s, &l1[g], sizeof(double)) != 0) ok = 0;
+    }
+  }
+  return ok != 0;
+}
+
 void DevSell::release() {
   if (slice_ptr) (void)hipFree(slice_ptr);
   if (col) (void)hipFree(col);
@@ -384,6 +410,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       D.hv.upload(L.hv);
     }
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
+    D.l1_fly = !L.l1.empty() && l1_on_the_fly(L.A, L.l1) && D.A.in.dcol && (D.A.bd.nrows == 0 || D.A.bd.dcol);
     if (!L.cf.empty()) D.cf = dupload(L.cf.data(), L.cf.size());
     D.F = dalloc<double>(D.n);
     D.U[0] = dalloc<double>(D.n + D.hu.n_halo);
@@ -554,7 +581,8 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       if (zero_guess) {
         HVE_HIP(launch_zero_guess(n, w == 1.0 ? 0 : 1, w, f, L.l1, u_cur, s));
       } else {
-        apply(L.A, &L.hu, w == 1.0 ? K_L1JAC : K_L1JAC_W, u_cur, f, L.l1, nullptr, 0, u_alt, w, 0.0, s);
+        apply(L.A, &L.hu, w == 1.0 ? K_L1JAC : K_L1JAC_W, u_cur, f, L.l1_fly ? nullptr : L.l1, nullptr, 0, u_alt,
+              w, 0.0, s);
         std::swap(u_cur, u_alt);
       }
       break;
@@ -797,7 +825,7 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
         HVE_HIP(launch_copy(L.n, u, x0_buf_, s));
         xin = x0_buf_;
       }
-      apply(L.A, &L.hu, K_RESID_L1JAC, xin, f, L.l1, nullptr, 0, V, 1.0, 0.0, s, pre);
+      apply(L.A, &L.hu, K_RESID_L1JAC, xin, f, L.l1_fly ? nullptr : L.l1, nullptr, 0, V, 1.0, 0.0, s, pre);
     } else if (initial) {
       // Vtemp = A u - f  (hypre copies f then Matvec(1, A, u, -1, Vtemp)); the
       // same numbers as f - A u up to the sign, so the norms agree bit for bit

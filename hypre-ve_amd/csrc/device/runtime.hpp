@@ -109,6 +109,7 @@ struct DevLevel {
   DevOp A, P, R;
   DevHalo hu, hv;
   double* l1 = nullptr;
+  bool l1_fly = false;  // the l1-Jacobi kernels form the l1 norms from A's entries
   int* cf = nullptr;
   double* F = nullptr;
   double* U[2] = {nullptr, nullptr};  // n + hu.n_halo each
