@@ -710,7 +710,7 @@ HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver s, HYPRE_Int rows) {
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  CHECK_ARG(policy >= 0 && policy <= 7, 2);
+  CHECK_ARG(policy >= 0 && policy <= 9, 2);
   s->prm.sell_policy = policy;
   return 0;
 }
@@ -1179,6 +1179,23 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver s, HYPRE_Real* bytes) {
   API_BEGIN
   const DevSell& A = s->dev->level(0).A.in;
   *bytes = (double)A.bytes() + (double)A.nrows * 24.0;
+  API_END
+}
+
+// Device layout of a level operator's interior rows (which: 0 A, 1 P, 2 R):
+// 0 padded SELL-64, 1 jagged, 2 workgroup-per-slice, 3 jagged wave-product,
+// 4 dictionary (LDS x-tile), 5 16-bit column deltas, 6 deltas + 8-bit value
+// table, 7 deltas + 16-bit value table, 8 padded + 16-bit value table,
+// 9 jagged + 16-bit value table.
+HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int* kind) {
+  CHECK_ARG(s && s->dev && s->dev->built() && kind, 1);
+  CHECK_ARG(level >= 0 && level < s->dev->num_levels(), 2);
+  CHECK_ARG(which >= 0 && which <= 2 && (which == 0 || level < s->dev->num_levels() - 1), 3);
+  API_BEGIN
+  const DevLevel& L = s->dev->level(level);
+  const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
+  *kind = M.dcol ? (M.vidx16 ? 7 : M.vidx ? 6 : 5)
+                 : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? 4 : M.pw ? 3 : M.rowlen ? 1 : M.wide ? 2 : 0;
   API_END
 }
 

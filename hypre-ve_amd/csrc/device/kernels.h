@@ -25,6 +25,7 @@ struct SellView {
   const short* dcol = nullptr;     // delta layout (k_sell_delta): col - row - slot base, padded
   const int* slot_base = nullptr;  // delta layout: base offset per (slice, slot)
   const unsigned char* vidx = nullptr;  // delta layout: 8-bit value indices (val unused)
+  const unsigned short* vidx16 = nullptr;  // delta layout: 16-bit value indices (val unused)
   const double* vtab = nullptr;         // the operator's distinct values
   int nvtab = 0;
 };

@@ -21,6 +21,7 @@
 
 #include "kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace hve {
@@ -70,6 +71,7 @@ struct SpArgs {
   const short* __restrict__ dcol;            // delta layout: col - row - slot base
   const int* __restrict__ slot_base;         // delta layout: per (slice, slot) base offset
   const unsigned char* __restrict__ vidx;    // delta layout, value table: entry -> vtab index
+  const unsigned short* __restrict__ vidx16; // the same, 16-bit
   const double* __restrict__ vtab;           // distinct values (<= 256)
   int nvtab;
   double* __restrict__ y;         // output
@@ -100,39 +102,66 @@ __device__ __forceinline__ void sstore(T* p, T v) {
   else *p = v;
 }
 
-template <int B, bool NT>
-__device__ __forceinline__ void sell_load(const int* __restrict__ cp, const double* __restrict__ vp, int k, int width,
-                                          int (&c)[B], double (&a)[B]) {
+// Value streams of the row loops: 8-byte values (ValF64) or 16-bit indices
+// into the operator's table of distinct values staged in LDS (ValT16; the
+// table reproduces every value bit for bit).  `at` is the entry's offset from
+// the lane's first entry.
+// The loaded word (raw) is turned into the value only where it is used, so a
+// table lookup does not wait on its index load at issue time and the
+// pipelined loop keeps the next batch's loads in flight.
+struct ValF64 {
+  using raw = double;
+  const double* __restrict__ vp;
+  __device__ static ValF64 make(const SpArgs& p, const double*, int off);
+  template <bool NT>
+  __device__ __forceinline__ raw load(int at) const { return mload<NT>(vp + at); }
+  __device__ __forceinline__ double value(raw r) const { return r; }
+  __device__ __forceinline__ static raw none() { return 0.0; }
+};
+struct ValT16 {
+  using raw = unsigned;
+  const unsigned short* __restrict__ ip;
+  const double* vt;
+  __device__ static ValT16 make(const SpArgs& p, const double* vt, int off);
+  template <bool NT>
+  __device__ __forceinline__ raw load(int at) const { return mload<NT>(ip + at); }
+  __device__ __forceinline__ double value(raw r) const { return vt[r]; }
+  __device__ __forceinline__ static raw none() { return 0u; }
+};
+
+template <int B, bool NT, class V>
+__device__ __forceinline__ void sell_load(const int* __restrict__ cp, const V& vl, int k, int width,
+                                          int (&c)[B], typename V::raw (&a)[B]) {
 #pragma unroll
   for (int q = 0; q < B; ++q) {
     const bool in = (k + q) < width;
     c[q] = in ? mload<NT>(cp + (k + q) * kWave) : -1;
-    a[q] = in ? mload<NT>(vp + (k + q) * kWave) : 0.0;
+    a[q] = in ? vl.template load<NT>((k + q) * kWave) : V::none();
   }
 }
 
 // Software-pipelined form: the column/value loads of batch k+1 are issued
 // between the x gathers and the adds of batch k, so a wave keeps two batches
 // of loads in flight (counted vmcnt) instead of draining at every batch.
-template <bool SUB, int B, bool NT>
-__device__ __forceinline__ double sell_row_pipe(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
+template <bool SUB, int B, bool NT, class V>
+__device__ __forceinline__ double sell_row_pipe(const int* __restrict__ cp, const V& vl, int k0,
                                                 int width, const double* __restrict__ x, double t) {
   if (k0 >= width) return t;
   int c[B];
-  double a[B];
-  sell_load<B, NT>(cp, vp, k0, width, c, a);
+  typename V::raw a[B];
+  sell_load<B, NT>(cp, vl, k0, width, c, a);
   for (int k = k0; k < width; k += B) {
     double xv[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) xv[q] = c[q] >= 0 ? x[c[q]] : 0.0;
     int cn[B];
-    double an[B];
-    sell_load<B, NT>(cp, vp, k + B, width, cn, an);
+    typename V::raw an[B];
+    sell_load<B, NT>(cp, vl, k + B, width, cn, an);
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       if (c[q] >= 0) {
-        if (SUB) t -= a[q] * xv[q];
-        else t += a[q] * xv[q];
+        if (SUB) t -= vl.value(a[q]) * xv[q];
+        else t += vl.value(a[q]) * xv[q];
       }
     }
 #pragma unroll
@@ -148,39 +177,39 @@ __device__ __forceinline__ double sell_row_pipe(const int* __restrict__ cp, cons
 // P is wave-uniform (SGPR).  blen is the lane's true length (it must take part
 // in every ballot, even when the lane's row is not relaxed), llen the length
 // it loads (0 for a skipped row).
-template <int B, bool NT>
-__device__ __forceinline__ void jag_load(const int* __restrict__ cp, const double* __restrict__ vp, int& P, int k,
-                                         int blen, int llen, int (&c)[B], double (&a)[B]) {
+template <int B, bool NT, class V>
+__device__ __forceinline__ void jag_load(const int* __restrict__ cp, const V& vl, int& P, int k,
+                                         int blen, int llen, int (&c)[B], typename V::raw (&a)[B]) {
 #pragma unroll
   for (int q = 0; q < B; ++q) {
     const bool in = (k + q) < llen;
     c[q] = in ? mload<NT>(cp + P) : -1;
-    a[q] = in ? mload<NT>(vp + P) : 0.0;
+    a[q] = in ? vl.template load<NT>(P) : V::none();
     P += __popcll(__ballot((k + q) < blen));
   }
 }
 
-template <bool SUB, int B, bool NT>
-__device__ __forceinline__ double jag_row(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
+template <bool SUB, int B, bool NT, class V>
+__device__ __forceinline__ double jag_row(const int* __restrict__ cp, const V& vl, int k0,
                                           int width, int blen, int llen, const double* __restrict__ x, double t) {
   int P = 0;
   for (int k = 0; k < k0; ++k) P += __popcll(__ballot(k < blen));
   if (k0 >= width) return t;
   int c[B];
-  double a[B];
-  jag_load<B, NT>(cp, vp, P, k0, blen, llen, c, a);
+  typename V::raw a[B];
+  jag_load<B, NT>(cp, vl, P, k0, blen, llen, c, a);
   for (int k = k0; k < width; k += B) {
     double xv[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) xv[q] = c[q] >= 0 ? x[c[q]] : 0.0;
     int cn[B];
-    double an[B];
-    jag_load<B, NT>(cp, vp, P, k + B, blen, llen, cn, an);
+    typename V::raw an[B];
+    jag_load<B, NT>(cp, vl, P, k + B, blen, llen, cn, an);
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       if (c[q] >= 0) {
-        if (SUB) t -= a[q] * xv[q];
-        else t += a[q] * xv[q];
+        if (SUB) t -= vl.value(a[q]) * xv[q];
+        else t += vl.value(a[q]) * xv[q];
       }
     }
 #pragma unroll
@@ -189,26 +218,27 @@ __device__ __forceinline__ double jag_row(const int* __restrict__ cp, const doub
   return t;
 }
 
-template <bool SUB, int B, bool PIPE, bool NT>
-__device__ __forceinline__ double sell_row(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
+template <bool SUB, int B, bool PIPE, bool NT, class V>
+__device__ __forceinline__ double sell_row(const int* __restrict__ cp, const V& vl, int k0,
                                            int width, const double* __restrict__ x, double t) {
-  if (PIPE) return sell_row_pipe<SUB, B, NT>(cp, vp, k0, width, x, t);
+  if (PIPE) return sell_row_pipe<SUB, B, NT>(cp, vl, k0, width, x, t);
   for (int k = k0; k < width; k += B) {
     int c[B];
-    double a[B], xv[B];
+    typename V::raw a[B];
+    double xv[B];
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       const bool in = (k + q) < width;
       c[q] = in ? mload<NT>(cp + (k + q) * kWave) : -1;
-      a[q] = in ? mload<NT>(vp + (k + q) * kWave) : 0.0;
+      a[q] = in ? vl.template load<NT>((k + q) * kWave) : V::none();
     }
 #pragma unroll
     for (int q = 0; q < B; ++q) xv[q] = c[q] >= 0 ? x[c[q]] : 0.0;
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       if (c[q] >= 0) {
-        if (SUB) t -= a[q] * xv[q];
-        else t += a[q] * xv[q];
+        if (SUB) t -= vl.value(a[q]) * xv[q];
+        else t += vl.value(a[q]) * xv[q];
       }
     }
   }
@@ -217,17 +247,18 @@ __device__ __forceinline__ double sell_row(const int* __restrict__ cp, const dou
 
 // Row sum of the current lane's row: plain SELL-64 (lane-strided, padded) or
 // jagged SELL-64 (JAG), both in stored (reference) entry order.
-template <bool SUB, int B, bool PIPE, bool NT, bool JAG>
-__device__ __forceinline__ double row_sum(const int* __restrict__ cp, const double* __restrict__ vp, int k0,
+template <bool SUB, int B, bool PIPE, bool NT, bool JAG, class V>
+__device__ __forceinline__ double row_sum(const int* __restrict__ cp, const V& vl, int k0,
                                           int width, int blen, int llen, const double* __restrict__ x, double t) {
-  if (JAG) return jag_row<SUB, B, NT>(cp, vp, k0, width, blen, llen, x, t);
-  return sell_row<SUB, B, PIPE, NT>(cp, vp, k0, width, x, t);
+  if (JAG) return jag_row<SUB, B, NT>(cp, vl, k0, width, blen, llen, x, t);
+  return sell_row<SUB, B, PIPE, NT>(cp, vl, k0, width, x, t);
 }
 
-template <int OP, bool CFSEL, int B, bool PIPE, bool NT, bool JAG>
-__global__ void __launch_bounds__(256) k_sell(SpArgs p) {
-  const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
-  const int row = lb * 256 + threadIdx.x;
+__device__ ValF64 ValF64::make(const SpArgs& p, const double*, int off) { return ValF64{p.val + off}; }
+__device__ ValT16 ValT16::make(const SpArgs& p, const double* vt, int off) { return ValT16{p.vidx16 + off, vt}; }
+
+template <int OP, bool CFSEL, int B, bool PIPE, bool NT, bool JAG, class V>
+__device__ __forceinline__ void sell_row_op(const SpArgs& p, const double* vt, int row) {
   // Lanes past the last row hold no entries (rowlen 0), so they may leave
   // before the ballots of the jagged layout.
   if (row >= p.nrows) return;
@@ -243,7 +274,7 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     width = (p.slice_ptr[slice + 1] - beg) >> 6;
   }
   const int* __restrict__ cp = p.col + beg + lane;
-  const double* __restrict__ vp = p.val + beg + lane;
+  const V vl = V::make(p, vt, beg + lane);
 
   bool skip = false;
   if (CFSEL) skip = p.cf[g] != p.relax_points;
@@ -252,7 +283,7 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     return;
   }
   const int llen = skip ? 0 : blen;
-#define HVE_ROW(SUBV, K0, T0) row_sum<SUBV, B, PIPE, NT, JAG>(cp, vp, K0, width, blen, llen, p.x, T0)
+#define HVE_ROW(SUBV, K0, T0) row_sum<SUBV, B, PIPE, NT, JAG>(cp, vl, K0, width, blen, llen, p.x, T0)
 
   if (OP == OP_RESID || OP == OP_L1JAC || OP == OP_RESID_L1JAC) {
     const double t = HVE_ROW(true, 0, skip ? 0.0 : mload<NT>(p.b + g));
@@ -281,7 +312,7 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     if (!skip) sstore<NT>(p.y + g, t);
   } else if (OP == OP_JAC) {
     // diagonal stored first (entry 0 sits at offset lane in both layouts)
-    const double d = (JAG ? (llen > 0) : !skip) ? vp[0] : 0.0;
+    const double d = (JAG ? (llen > 0) : !skip) ? vl.value(vl.template load<false>(0)) : 0.0;
     const double uo = p.x[g];
     const bool nod = skip || d == 0.0;
     // every lane runs the loop (ballots); lanes without a usable diagonal load nothing
@@ -304,6 +335,29 @@ __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
     if (!skip) sstore<NT>(p.y + g, (alpha == 1.0 || neg) ? t : alpha * t);
   }
 #undef HVE_ROW
+}
+
+template <int OP, bool CFSEL, int B, bool PIPE, bool NT, bool JAG>
+__global__ void __launch_bounds__(256) k_sell(SpArgs p) {
+  const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  sell_row_op<OP, CFSEL, B, PIPE, NT, JAG, ValF64>(p, nullptr, lb * 256 + (int)threadIdx.x);
+}
+
+// Padded or jagged SELL-64 with 16-bit value indices (P and R of the 7-point
+// hierarchy: ~1200 distinct interpolation weights): 6 B an entry instead of
+// 12.  Persistent grid, so each workgroup stages the table in LDS once; the
+// row blocks are walked as in k_sell_delta.
+template <int OP, bool CFSEL, int B, bool JAG>
+__global__ void __launch_bounds__(256) k_sell_vt(SpArgs p) {
+  extern __shared__ double vt[];
+  for (int i = threadIdx.x; i < p.nvtab; i += 256) vt[i] = p.vtab[i];
+  __syncthreads();
+  const int nrb = (p.nrows + 255) >> 8;
+  const int per_xcd = (nrb + 7) >> 3;
+  const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
+  const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
+  for (int rb = r0 + (int)(blockIdx.x >> 3); rb < r1; rb += per_wg)
+    sell_row_op<OP, CFSEL, B, true, true, JAG, ValT16>(p, vt, rb * 256 + (int)threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -381,20 +435,22 @@ __device__ __forceinline__ void row_store(const SpArgs& p, int g, bool skip, dou
 // load); a padding slot (kDeltaPad) may sit between a row's entries and is
 // skipped, so each row still sums its entries in stored order.
 // ---------------------------------------------------------------------------
-template <int OP, bool CFSEL, int B, bool NT, bool VI>
-__global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
+// VI: 0 = 8-byte values; 1 / 2 = 8- / 16-bit indices into a table of the
+// operator's distinct values (exact doubles) staged in LDS.
+template <int VI>
+__device__ __forceinline__ double vt_value(const SpArgs& p, const double* vt, const double* vp, int beg_lane, int k,
+                                           bool nt) {
+  if (VI == 1) return vt[nt ? __builtin_nontemporal_load(p.vidx + beg_lane + k * kWave) : p.vidx[beg_lane + k * kWave]];
+  if (VI == 2)
+    return vt[nt ? __builtin_nontemporal_load(p.vidx16 + beg_lane + k * kWave) : p.vidx16[beg_lane + k * kWave]];
+  return nt ? __builtin_nontemporal_load(vp + k * kWave) : vp[k * kWave];
+}
+
+template <int OP, bool CFSEL, int B, bool NT, int VI>
+__device__ __forceinline__ void delta_row(const SpArgs& p, const double* vt, int row) {
   constexpr short PAD = -32768;
-  // VI: values stored as 8-bit indices into a table of the operator's
-  // distinct values (exact doubles), staged in LDS: 3 B an entry
-  __shared__ double vt[VI ? 256 : 1];
-  if (VI) {
-    for (int i = threadIdx.x; i < p.nvtab; i += 256) vt[i] = p.vtab[i];
-    __syncthreads();
-  }
-  const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
-  const int row = lb * 256 + threadIdx.x;
   if (row >= p.nrows) return;
-  const int lane = threadIdx.x & (kWave - 1);
+  const int lane = row & (kWave - 1);
   const int slice = __builtin_amdgcn_readfirstlane(row >> 6);
   const int g = p.rowmap ? mload<NT>(p.rowmap + row) : row;
   const int beg = p.slice_ptr[slice];
@@ -402,7 +458,7 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
   const int* __restrict__ sb = p.slot_base + (beg >> 6);
   const short* __restrict__ cp = p.dcol + beg + lane;
   const double* __restrict__ vp = VI ? nullptr : p.val + beg + lane;
-  const unsigned char* __restrict__ ip = VI ? p.vidx + beg + lane : nullptr;
+  const int bl = beg + lane;
   bool skip = false;
   if (CFSEL) skip = p.cf[g] != p.relax_points;
   if (CFSEL && skip) {
@@ -416,7 +472,7 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
   int k0 = 0;
   if (OP == OP_JAC) {
     uo = p.x[g];
-    d = width > 0 ? (VI ? vt[ip[0]] : vp[0]) : 0.0;  // diagonal stored first, slot 0 of every row
+    d = width > 0 ? vt_value<VI>(p, vt, vp, bl, 0, false) : 0.0;  // diagonal stored first, slot 0 of every row
     k0 = 1;
   }
   // l1 norms formed on the fly (p.l1 == nullptr, set up only where the host
@@ -440,8 +496,7 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
       // a slot past the slice re-reads slot k (same lines, no new bytes)
       const int kk = (k + q) < width ? k + q : k;
       dv[q] = mload<NT>(cp + kk * kWave);
-      if (VI) a[q] = vt[mload<NT>(ip + kk * kWave)];
-      else a[q] = mload<NT>(vp + kk * kWave);
+      a[q] = vt_value<VI>(p, vt, vp, bl, kk, NT);
     }
     bool on[B];
     double xv[B];
@@ -480,6 +535,25 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
     return;
   }
   row_store<OP, NT>(p, g, false, t, uo, d);
+}
+
+// Row blocks of 256 rows; gridDim.x (a multiple of 8) workgroups, each XCD's
+// share walking one contiguous eighth of the row blocks.  With one workgroup
+// per row block this is the usual XCD-aware map; the 16-bit value table runs
+// a persistent grid so that each workgroup stages the table once.
+template <int OP, bool CFSEL, int B, bool NT, int VI>
+__global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
+  extern __shared__ double vt[];  // nvtab doubles (VI > 0)
+  if (VI) {
+    for (int i = threadIdx.x; i < p.nvtab; i += 256) vt[i] = p.vtab[i];
+    __syncthreads();
+  }
+  const int nrb = (p.nrows + 255) >> 8;
+  const int per_xcd = (nrb + 7) >> 3;
+  const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
+  const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
+  for (int rb = r0 + (int)(blockIdx.x >> 3); rb < r1; rb += per_wg)
+    delta_row<OP, CFSEL, B, NT, VI>(p, vt, rb * 256 + (int)threadIdx.x);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -1016,6 +1090,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   a.dcol = M.dcol;
   a.slot_base = M.slot_base;
   a.vidx = M.vidx;
+  a.vidx16 = M.vidx16;
   a.vtab = M.vtab;
   a.nvtab = M.nvtab;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
@@ -1028,7 +1103,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   const bool nt = sell_nt();
   const bool jag = M.rowlen != nullptr;
   if (M.col16) {  // dictionary layout: G waves per workgroup share an x-tile in LDS
-    const int G = M.dict_group > 1 ? 4 : 1;
+    const int G = M.dict_group;
     const int ngroups = ((M.nrows + 63) / 64 + G - 1) / G;
     a.nblocks_pad = (ngroups + 7) / 8 * 8;
     const dim3 dgrid(a.nblocks_pad), dblock(64 * G);
@@ -1037,6 +1112,10 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   if (G == 4) {                                                                                        \
     if (nt) hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, true, 4>), dgrid, dblock, lds, s, a);        \
     else hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, false, 4>), dgrid, dblock, lds, s, a);          \
+  } else if (G == 2) {                                                                                 \
+    hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, true, 2>), dgrid, dblock, lds, s, a);                \
+  } else if (G == 8) {                                                                                 \
+    hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, true, 8>), dgrid, dblock, lds, s, a);                \
   } else {                                                                                             \
     if (nt) hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, true, 1>), dgrid, dblock, lds, s, a);        \
     else hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, false, 1>), dgrid, dblock, lds, s, a);          \
@@ -1058,16 +1137,22 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     return hipGetLastError();
   }
   if (M.dcol) {  // 16-bit column deltas, lane per row
-#define HVE_X(OPV, CF, BB)                                                                 \
-  if (M.vidx) {                                                                                   \
-    if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true, true>), grid, block, 0, s, a);    \
-    else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false, true>), grid, block, 0, s, a);      \
-  } else {                                                                                        \
-    if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true, false>), grid, block, 0, s, a);   \
-    else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false, false>), grid, block, 0, s, a);     \
+    // 16-bit value table: persistent grid of 8 workgroups per CU
+    const dim3 xgrid(M.vidx16 ? std::min(a.nblocks_pad, 2048) : a.nblocks_pad);
+    const size_t lds = (size_t)M.nvtab * sizeof(double);
+#define HVE_X(OPV, CF, BB)                                                                       \
+  if (M.vidx16) {                                                                                       \
+    if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true, 2>), xgrid, block, lds, s, a);         \
+    else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false, 2>), xgrid, block, lds, s, a);           \
+  } else if (M.vidx) {                                                                                  \
+    if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true, 1>), xgrid, block, lds, s, a);         \
+    else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false, 1>), xgrid, block, lds, s, a);           \
+  } else {                                                                                              \
+    if (nt) hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, true, 0>), xgrid, block, 0, s, a);           \
+    else hipLaunchKernelGGL((k_sell_delta<OPV, CF, BB, false, 0>), xgrid, block, 0, s, a);             \
   }
 #define HVE_XB(OPV, CF) \
-  if (bsel == 16) { HVE_X(OPV, CF, 16) } else { HVE_X(OPV, CF, 8) }
+  if (bsel == 16) { HVE_X(OPV, CF, 16) } else if (M.batch == 4) { HVE_X(OPV, CF, 4) } else { HVE_X(OPV, CF, 8) }
 #define HVE_XL(OPV)                                                 \
   case OPV:                                                         \
     if (cfsel) { HVE_XB(OPV, true) } else { HVE_XB(OPV, false) }   \
@@ -1097,6 +1182,28 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     }
 #undef HVE_PL
 #undef HVE_P
+    return hipGetLastError();
+  }
+  if (M.vidx16) {  // 32-bit columns, 16-bit value indices (padded or jagged)
+    const dim3 vgrid(std::min(a.nblocks_pad, 2048));
+    const size_t lds = (size_t)M.nvtab * sizeof(double);
+#define HVE_V(OPV, CF, BB)                                                                           \
+  if (jag) hipLaunchKernelGGL((k_sell_vt<OPV, CF, BB, true>), vgrid, block, lds, s, a);              \
+  else hipLaunchKernelGGL((k_sell_vt<OPV, CF, BB, false>), vgrid, block, lds, s, a);
+#define HVE_VB(OPV, CF) \
+  if (bsel == 16) { HVE_V(OPV, CF, 16) } else { HVE_V(OPV, CF, 8) }
+#define HVE_VL(OPV)                                                 \
+  case OPV:                                                         \
+    if (cfsel) { HVE_VB(OPV, true) } else { HVE_VB(OPV, false) }   \
+    break;
+    switch (op) {
+      HVE_VL(OP_RESID) HVE_VL(OP_MATVEC) HVE_VL(OP_L1JAC) HVE_VL(OP_L1JAC_W) HVE_VL(OP_JAC)
+      HVE_VL(OP_PROLONG) HVE_VL(OP_RESTRICT) HVE_VL(OP_GENERAL) HVE_VL(OP_RESID_L1JAC) HVE_VL(OP_RESTRICT_ZG)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_VL
+#undef HVE_VB
+#undef HVE_V
     return hipGetLastError();
   }
   if (M.wide && !jag) {

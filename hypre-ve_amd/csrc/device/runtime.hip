@@ -37,6 +37,15 @@ static T* dupload(const T* h, size_t n) {
   return p;
 }
 
+// HVE_SELL_VALTAB=0 keeps 8-byte values in every layout (default 1).
+static int sell_valtab_env() {
+  static const int v = [] {
+    const char* e = getenv("HVE_SELL_VALTAB");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy) {
   release();
   std::vector<int> sp, col, perm;
@@ -92,9 +101,17 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
   bool use_dict = A.nnz() > 0 &&
                   (dict_env < 0 ? (A.nrows >= (1 << 18) && avg_len >= 16.0)
                                 : ((dict_env >= 1 && jag) || (dict_env >= 2 && wide)));
+  // With 16-bit value indices a padding slot costs 6 B instead of 12, and the
+  // padded layout's natural row order gathers x better than the sorted jagged
+  // one: R_0 at 256^3 187 us padded+vt16 against 197 jagged+vt16 (202 jagged).
+  if (policy == 0 && jag && !pw && sell_valtab_env() != 0) {
+    std::vector<unsigned short> probe;
+    std::vector<double> probe_tab;
+    if (build_value_table16(A.a, 4096, probe, probe_tab)) jag = false;
+  }
   if (policy != 0) {  // forced (tests): every loop gives the same bits
     wide = policy == 3 ? 1 : 0;
-    jag = (policy == 2 || policy == 4) && A.nnz() > 0;
+    jag = (policy == 2 || policy == 4 || policy == 9) && A.nnz() > 0;
     pw = policy == 4 && jag;
     use_dict = policy == 5 && A.nnz() > 0;
   }
@@ -107,8 +124,9 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
     const char* e = getenv("HVE_SELL_DELTA");
     return e ? atoi(e) : -1;
   }();
-  bool use_delta = A.nnz() > 0 && !wide && !jag && !use_dict && delta_env != 0 && sigma_env == 0 &&
-                   (avg_len >= 5.0 || delta_env == 1);
+  // Short-row operators (P) take it only together with a value table.
+  const bool short_rows = avg_len < 5.0 && delta_env != 1;
+  bool use_delta = A.nnz() > 0 && !wide && !jag && !use_dict && delta_env != 0 && sigma_env == 0;
   if (policy != 0) use_delta = (policy == 6 || policy == 7) && A.nnz() > 0;
   if (use_delta) {
     std::vector<short> dc;
@@ -129,19 +147,28 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
       // Few distinct values (a constant-coefficient stencil): 8-bit indices
       // into a table of them, 3 B an entry in all.  HVE_SELL_VALTAB=0 keeps
       // 8-byte values.
-      static const int vt_env = [] {
-        const char* e = getenv("HVE_SELL_VALTAB");
-        return e ? atoi(e) : 1;
-      }();
+      const int vt_env = sell_valtab_env();
+      // Up to 4096 distinct values (P of the 7-point hierarchy: ~1200): 16-bit
+      // indices, the table (<= 32 KiB) in LDS.
       std::vector<unsigned char> vi;
+      std::vector<unsigned short> vi16;
       std::vector<double> tab;
-      if ((vt_env != 0 || policy == 7) && policy != 6 && build_value_table(val, 256, vi, tab)) {
+      const bool try_vt = (vt_env != 0 || policy == 7) && policy != 6;
+      if (try_vt && build_value_table(val, 256, vi, tab)) {
         vidx = dupload(vi.data(), vi.size());
-        vtab = dupload(tab.data(), tab.size());
-        nvtab = (int)tab.size();
+      } else if (try_vt && build_value_table16(val, 4096, vi16, tab)) {
+        vidx16 = dupload(vi16.data(), vi16.size());
+      } else if (short_rows && policy == 0) {
+        release();  // no gain without a value table: plain layout
+        goto plain;
       } else {
         this->val = dupload(val.data(), val.size());
       }
+      if (!tab.empty()) {
+        vtab = dupload(tab.data(), tab.size());
+        nvtab = (int)tab.size();
+      }
+      if (nslices > 0 && pad0 <= (int64_t)nslices * 64 * 4) batch = 4;  // rows of <= 4 entries
       if (!rowmap_h.empty()) {
         bool ident = true;
         for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
@@ -149,6 +176,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
       }
       return;
     }
+  plain:
     sp.clear();
     val.clear();
   }
@@ -164,9 +192,10 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
       const char* e = getenv("HVE_SELL_DICT_GROUP");
       return e ? atoi(e) : 0;
     }();
-    int group = group_env == 1 ? 1 : group_env == 4 ? 4 : (A.nrows == A.ncols ? 4 : 1);
-    bool built = build_sell_dict_host(A, group == 4 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd);
-    if (!built && group == 4 && group_env == 0) {
+    int group = (group_env == 1 || group_env == 2 || group_env == 4 || group_env == 8) ? group_env
+                                                                                     : (A.nrows == A.ncols ? 4 : 1);
+    bool built = build_sell_dict_host(A, group > 1 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd);
+    if (!built && group > 1 && group_env == 0) {
       group = 1;
       built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd);
     }
@@ -182,6 +211,9 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
       wide = 0;
       pw = 0;
       dmax = std::max(1, mxd);
+      if (getenv("HVE_LAYOUT_LOG"))
+        fprintf(stderr, "[layout] dict rows=%d group=%d dmax=%d mean dictionary=%.0f\n", A.nrows, group, dmax,
+                (double)dc.size() / std::max<size_t>(1, dp.size() - 1));
       rowlen = dupload(rl2.data(), rl2.size());
       slice_ptr = dupload(sp.data(), sp.size());
       col16 = dupload(c16.data(), c16.size());
@@ -222,7 +254,21 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
   if (jag) rowlen = dupload(rl.data(), rl.size());
   slice_ptr = dupload(sp.data(), sp.size());
   this->col = dupload(col.data(), col.size());
-  this->val = dupload(val.data(), val.size());
+  // 16-bit indices into the operator's distinct values where at most 4096
+  // occur (P and R of the 7-point hierarchy at every size: ~1200), off for the
+  // workgroup-per-slice loop of small operators.  HVE_SELL_VALTAB=0 turns it off.
+  std::vector<unsigned short> vi16;
+  std::vector<double> tab;
+  const bool try_vt16 = policy == 8 || policy == 9 || (policy == 0 && !wide && sell_valtab_env() != 0);
+  if (try_vt16 && A.nnz() > 0 && build_value_table16(val, 4096, vi16, tab)) {
+    vidx16 = dupload(vi16.data(), vi16.size());
+    vtab = dupload(tab.data(), tab.size());
+    nvtab = (int)tab.size();
+    wide = 0;
+    pipe = 1;
+  } else {
+    this->val = dupload(val.data(), val.size());
+  }
   // stored row i -> local output row: subset map composed with the sort order
   std::vector<int> map(A.nrows);
   for (int i = 0; i < A.nrows; ++i) {
@@ -271,8 +317,9 @@ void DevSell::release() {
   if (dcol) (void)hipFree(dcol);
   if (slot_base) (void)hipFree(slot_base);
   if (vidx) (void)hipFree(vidx);
+  if (vidx16) (void)hipFree(vidx16);
   if (vtab) (void)hipFree(vtab);
-  dcol = nullptr; slot_base = nullptr; vidx = nullptr; vtab = nullptr; nvtab = 0;
+  dcol = nullptr; slot_base = nullptr; vidx = nullptr; vidx16 = nullptr; vtab = nullptr; nvtab = 0;
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
   col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;

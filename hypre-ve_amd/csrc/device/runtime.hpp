@@ -41,6 +41,7 @@ struct DevSell {
   short* dcol = nullptr;   // delta layout: 16-bit column deltas
   int* slot_base = nullptr;
   unsigned char* vidx = nullptr;  // delta layout with a value table
+  unsigned short* vidx16 = nullptr;
   double* vtab = nullptr;
   int nvtab = 0;
   int batch = 8;
@@ -51,14 +52,14 @@ struct DevSell {
     SellView v;
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
     v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group;
-    v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vtab = vtab; v.nvtab = nvtab;
+    v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vidx16 = vidx16; v.vtab = vtab; v.nvtab = nvtab;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map
   // policy: AMGParams::sell_policy
   void upload(const CSR& A, const std::vector<int>& rowmap = {}, int policy = 0);
   void release();
-  size_t bytes() const { return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * (vidx ? 3 : dcol ? 10 : 12) +
+  size_t bytes() const { return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * (vidx ? 3 : vidx16 ? 4 : dcol ? 10 : 12) +
                          (dcol ? (size_t)nnz_pad / 16 : 0) + (rowmap ? (size_t)nrows * 4 : 0) +
                          (rowlen ? (size_t)nslices * 256 : 0); }
 };

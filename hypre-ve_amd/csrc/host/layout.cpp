@@ -1,8 +1,10 @@
 // Host-side construction of the HBM layouts consumed by the device runtime.
 #include <algorithm>
+#include <climits>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
+#include <unordered_set>
 
 #include "hve_host.hpp"
 #include "layout.hpp"
@@ -78,7 +80,9 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
 // slots greedily (leftmost slot whose base reaches its next entry, which is
 // optimal for an order-preserving match), so a missing stencil neighbour
 // becomes an interior padding slot instead of shifting the ones after it.
-// Bases come from the slice's first longest row.  Returns false when some row
+// Bases come from the slice's first longest row; a slice that does not fit
+// so takes one base for all its slots (entries in their natural slots) when
+// its column offsets span less than 64K.  Returns false when some row
 // does not fit its slice's slots (the operator then keeps 32-bit columns).
 bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vector<int>& slot_base,
                            std::vector<short>& dcol, std::vector<double>& val) {
@@ -103,22 +107,50 @@ bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vecto
   int ok = 1;
 #pragma omp parallel for schedule(static) reduction(min : ok)
   for (int s = 0; s < ns; ++s) {
-    if (ref[s] < 0) continue;
+    if (ref[s] < 0 || !ok) continue;
     const int w = (slice_ptr[s + 1] - slice_ptr[s]) / 64;
     int* base = slot_base.data() + slice_ptr[s] / 64;
-    const int rr = ref[s];
-    for (int k = 0; k < w; ++k) base[k] = A.j[A.i[rr] + k] - rr;
-    for (int r = s * 64; r < std::min(n, (s + 1) * 64) && ok; ++r) {
-      int k = 0;
-      for (int e = A.i[r]; e < A.i[r + 1]; ++e, ++k) {
-        const int64_t off = (int64_t)A.j[e] - r;
-        while (k < w && (off - base[k] < -32767 || off - base[k] > 32767)) ++k;
-        if (k == w) { ok = 0; break; }
-        const size_t pos = (size_t)slice_ptr[s] + (size_t)k * 64 + (r & 63);
-        dcol[pos] = (short)(off - base[k]);
-        val[pos] = A.a[e];
+    const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
+    // mode 0: per-slot bases from the first longest row, greedy slot match;
+    // mode 1 (when 0 fails): one base for the whole slice (the middle of its
+    // offset range) and every entry in its natural slot -- fits operators
+    // whose offsets in a slice span < 64K columns (P: coarse neighbours of
+    // 64 consecutive fine rows)
+    bool fit = false;
+    for (int mode = 0; mode < 2 && !fit; ++mode) {
+      for (int r = r0; r < r1; ++r)
+        for (int k = 0; k < w; ++k) {
+          const size_t pos = (size_t)slice_ptr[s] + (size_t)k * 64 + (r & 63);
+          dcol[pos] = kDeltaPad;
+          val[pos] = 0.0;
+        }
+      if (mode == 0) {
+        const int rr = ref[s];
+        for (int k = 0; k < w; ++k) base[k] = A.j[A.i[rr] + k] - rr;
+      } else {
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (int r = r0; r < r1; ++r)
+          for (int e = A.i[r]; e < A.i[r + 1]; ++e) {
+            lo = std::min(lo, (int64_t)A.j[e] - r);
+            hi = std::max(hi, (int64_t)A.j[e] - r);
+          }
+        if (hi - lo > 65534) break;
+        for (int k = 0; k < w; ++k) base[k] = (int)(lo + (hi - lo) / 2);
+      }
+      fit = true;
+      for (int r = r0; r < r1 && fit; ++r) {
+        int k = 0;
+        for (int e = A.i[r]; e < A.i[r + 1]; ++e, ++k) {
+          const int64_t off = (int64_t)A.j[e] - r;
+          while (k < w && (off - base[k] < -32767 || off - base[k] > 32767)) ++k;
+          if (k == w) { fit = false; break; }
+          const size_t pos = (size_t)slice_ptr[s] + (size_t)k * 64 + (r & 63);
+          dcol[pos] = (short)(off - base[k]);
+          val[pos] = A.a[e];
+        }
       }
     }
+    if (!fit) ok = 0;
   }
   // B = 16 slots of tail padding: the device issues a batch's loads unmasked
   slot_base.resize(slot_base.size() + 16, 0);
@@ -131,24 +163,20 @@ bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vecto
 // at most maxv distinct bit patterns (constant-coefficient stencils: 2-4),
 // each entry keeps an 8-bit index into the ascending-by-bits table instead of
 // its 8-byte value.  Padding entries index their own (+0.0) pattern.
-bool build_value_table(const std::vector<double>& val, int maxv, std::vector<unsigned char>& idx,
-                       std::vector<double>& tab) {
-  if (maxv > 256) maxv = 256;
+template <typename I>
+static bool value_table_impl(const std::vector<double>& val, int maxv, std::vector<I>& idx, std::vector<double>& tab) {
   const size_t n = val.size();
   std::vector<uint64_t> all;
   bool over = false;
 #pragma omp parallel
   {
-    std::vector<uint64_t> mine;
+    std::unordered_set<uint64_t> mine;
 #pragma omp for schedule(static)
     for (size_t i = 0; i < n; ++i) {
       if (over) continue;
       uint64_t b;
       std::memcpy(&b, &val[i], 8);
-      if (std::find(mine.begin(), mine.end(), b) == mine.end()) {
-        mine.push_back(b);
-        if ((int)mine.size() > maxv) over = true;
-      }
+      if (mine.insert(b).second && (int)mine.size() > maxv) over = true;
     }
 #pragma omp critical
     all.insert(all.end(), mine.begin(), mine.end());
@@ -164,9 +192,17 @@ bool build_value_table(const std::vector<double>& val, int maxv, std::vector<uns
   for (size_t i = 0; i < n; ++i) {
     uint64_t b;
     std::memcpy(&b, &val[i], 8);
-    idx[i] = (unsigned char)(std::lower_bound(all.begin(), all.end(), b) - all.begin());
+    idx[i] = (I)(std::lower_bound(all.begin(), all.end(), b) - all.begin());
   }
   return true;
+}
+bool build_value_table(const std::vector<double>& val, int maxv, std::vector<unsigned char>& idx,
+                       std::vector<double>& tab) {
+  return value_table_impl(val, std::min(maxv, 256), idx, tab);
+}
+bool build_value_table16(const std::vector<double>& val, int maxv, std::vector<unsigned short>& idx,
+                         std::vector<double>& tab) {
+  return value_table_impl(val, std::min(maxv, 65536), idx, tab);
 }
 
 // Jagged SELL-64: rows sorted by descending length inside each 64-row slice

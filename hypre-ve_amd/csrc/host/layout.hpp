@@ -24,6 +24,9 @@ bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vecto
 // distinct values occur.
 bool build_value_table(const std::vector<double>& val, int maxv, std::vector<unsigned char>& idx,
                        std::vector<double>& tab);
+// The same with 16-bit indices (maxv <= 65536).
+bool build_value_table16(const std::vector<double>& val, int maxv, std::vector<unsigned short>& idx,
+                         std::vector<double>& tab);
 // Jagged SELL-64 (no stored padding): perm[i] = CSR row at stored position i
 // (rows sorted by descending length inside each slice), rowlen[i] its length
 // (nslices*64 entries, 0 past the last row), entry k of the slice's lane r at

@@ -174,6 +174,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGGetKernelStats", _i, [_p, _pd, _i]),
     ("hypreve_BenchFineSpMV", _i, [_p, _i, _pd, _pd]),
     ("hypreve_BenchFineSpMVStoredBytes", _i, [_p, _pd]),
+    ("hypreve_BoomerAMGGetLevelLayout", _i, [_p, _i, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchStream", _i, [_i, C.c_int64, _i, _pd]),
@@ -506,6 +507,15 @@ class BoomerAMG:
         ms, by = C.c_double(), C.c_double()
         check(lib().hypreve_BenchFineSpMV(self.h, reps, C.byref(ms), C.byref(by)), "BenchFineSpMV")
         return ms.value, by.value
+
+    LAYOUTS = ("padded", "jagged", "wide", "jag-pw", "dict", "delta", "delta+vt8", "delta+vt16", "padded+vt16",
+               "jagged+vt16")
+
+    def level_layout(self, level, which=0):
+        """Device layout name of A_l (0), P_l (1) or R_l (2) (interior rows)."""
+        k = C.c_int()
+        check(lib().hypreve_BoomerAMGGetLevelLayout(self.h, level, which, C.byref(k)), "GetLevelLayout")
+        return self.LAYOUTS[k.value]
 
     def fine_spmv_stored_bytes(self):
         """Bytes the finest SpMV streams in its stored layout (+ vectors)."""

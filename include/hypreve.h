@@ -226,7 +226,8 @@ HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_block
  * x-tile (per-slice column dictionary), 6 padded with 16-bit column deltas
  * against per-slot bases (where a slice's rows fit), 7 as 6 plus 8-bit value
  * indices into a table of the operator's distinct values (where at most 256
- * occur).  All give identical
+ * occur), 8 padded and 9 jagged, each with 16-bit value indices (where at
+ * most 4096 distinct values occur).  All give identical
  * bits; the forced settings exist for parity tests and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* Multi-rank: coarse levels with at most `rows` global rows (from the first
@@ -278,6 +279,12 @@ HYPRE_Int hypreve_BenchFineSpMV(HYPRE_Solver solver, HYPRE_Int reps, HYPRE_Real 
 /* Bytes the same launch streams in the stored layout (padding, 16-bit column
  * deltas and slot bases included) plus its three vectors. */
 HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver solver, HYPRE_Real *bytes);
+/* Device layout of a level operator's interior rows (which: 0 A, 1 P, 2 R):
+ * 0 padded SELL-64, 1 jagged, 2 workgroup-per-slice, 3 jagged wave-product,
+ * 4 dictionary, 5 16-bit column deltas, 6 deltas + 8-bit value table,
+ * 7 deltas + 16-bit value table, 8 padded + 16-bit value table, 9 jagged +
+ * 16-bit value table. */
+HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int *kind);
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
 HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_blocks);

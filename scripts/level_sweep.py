@@ -56,7 +56,7 @@ def main():
             nnz = annz if which == 0 else pnnz
             gbs = by / (ms * 1e-3) / 1e9
             print(f"L{l} {name} rows={r if which != 2 else '-':>9} nnz={nnz:>11} pad={pad/max(nnz,1):.3f} "
-                  f"{ms*1e3:9.1f} us {gbs:7.0f} GB/s", flush=True)
+                  f"{ms*1e3:9.1f} us {gbs:7.0f} GB/s  {amg.level_layout(l, which)}", flush=True)
             rows.append({"kind": "op", "level": l, "op": name, "rows": r, "nnz": nnz, "pad": pad / max(nnz, 1),
                          "us": ms * 1e3, "gbs": gbs})
     if args.json:

@@ -78,13 +78,13 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen):
     assert np.array_equal(u.get(), uo)
 
 
-@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9])
 @pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
 def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
     workgroup-per-slice, jagged wave-product-parallel, jagged with an LDS
-    x-tile, padded with 16-bit column deltas, the same with a value table)
-    forced on every
+    x-tile, padded with 16-bit column deltas, the same with a value table,
+    padded / jagged with 16-bit value indices) forced on every
     operator of the hierarchy: the same bits as the oracle.  The automatic
     choice only uses jagged and wide loops on operators too large for the
     other tests, so this is where those loops meet the oracle."""
