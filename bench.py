@@ -148,8 +148,8 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     achieved = stored_bytes / (spmv_ms * 1e-3) / 1e9
     csr_gbs = csr_bytes / (spmv_ms * 1e-3) / 1e9
     vt = os.environ.get("HVE_SELL_VALTAB", "1") != "0"
-    # k_sell_delta<OP_RESID, no CF, batch 8, NT, value table?>
-    traffic = committed_traffic(n, "k_sell_delta<0, false, 8, true, %s>(hve::SpArgs)" % ("true" if vt else "false"))
+    # k_sell_delta<OP_RESID, no CF, batch 8, NT, value table (0 none, 1 8-bit)>
+    traffic = committed_traffic(n, "k_sell_delta<0, false, 8, true, %d>(hve::SpArgs)" % (1 if vt else 0))
     # the box's achievable read bandwidth: a grid-stride 8 B/lane stream over 2 GiB
     stream_n = (1 << 31) // 8
     stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 10) * 1e-3) / 1e9
