@@ -77,6 +77,7 @@ struct hypre_Solver_struct {
   double rel_res = 0.0;
   bool use_graph = true;
   bool user_num_blocks = false;
+  std::vector<int> gs_rank_starts;  // one GPU emulating the GS blocks of an N-rank run
   // PCG
   PCGParams pcg;
   HYPRE_Solver precond = nullptr;
@@ -708,6 +709,20 @@ HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver s, HYPRE_Int rows) {
   s->prm.agglo_rows = rows < 0 ? 0 : rows;
   return 0;
 }
+// Hybrid Gauss-Seidel on one GPU with the row blocks of an N-rank run whose
+// level-0 rows start at starts[0..nranks] (num_blocks blocks per rank on
+// every level, l1 norms to match): the iterates then equal the N-rank ones.
+// nranks <= 1 clears it.  Takes effect at Setup.
+HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver s, HYPRE_Int nranks, const HYPRE_Int* starts) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(nranks <= 1 || starts, 3);
+  s->gs_rank_starts.clear();
+  if (nranks > 1) {
+    for (int r = 0; r < nranks; ++r) CHECK_ARG(starts[r] <= starts[r + 1] && starts[0] == 0, 3);
+    s->gs_rank_starts.assign(starts, starts + nranks + 1);
+  }
+  return 0;
+}
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(policy >= 0 && policy <= 9, 2);
@@ -990,7 +1005,7 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
     else setup_multi(s, A);
   } else {
     amg_setup(A->diag, s->prm, s->H);
-    single_rank_hierarchy(s->H, s->RH);
+    single_rank_hierarchy(s->H, s->RH, s->gs_rank_starts.empty() ? nullptr : &s->gs_rank_starts);
   }
   if (!s->dev) s->dev.reset(new DevAMG);
   s->dev->build(s->RH, A->multi() ? A->comm->dc.get() : nullptr);

@@ -279,6 +279,31 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
   for (int i = 0; i < A.nrows && ident; ++i) ident = map[i] == i;
   if (!ident) rowmap = dupload(map.data(), map.size());
 }
+// A rank operator's rows in local order (interior and boundary merged, each
+// row's entries in stored order, columns in the [local | halo] space).
+static CSR merged_rows(const RankOp& op, int n) {
+  CSR M;
+  M.resize_rows(n, std::max(op.interior.ncols, op.boundary.ncols));
+  for (int part = 0; part < 2; ++part) {
+    const CSR& A = part == 0 ? op.interior : op.boundary;
+    const std::vector<int>& map = part == 0 ? op.map_int : op.map_bnd;
+    for (int i = 0; i < A.nrows; ++i) M.i[(map.empty() ? i : map[i]) + 1] = A.i[i + 1] - A.i[i];
+  }
+  for (int i = 0; i < n; ++i) M.i[i + 1] += M.i[i];
+  M.j.resize(M.i[n]);
+  M.a.resize(M.i[n]);
+  for (int part = 0; part < 2; ++part) {
+    const CSR& A = part == 0 ? op.interior : op.boundary;
+    const std::vector<int>& map = part == 0 ? op.map_int : op.map_bnd;
+    for (int i = 0; i < A.nrows; ++i) {
+      const int g = map.empty() ? i : map[i];
+      std::copy(A.j.begin() + A.i[i], A.j.begin() + A.i[i + 1], M.j.begin() + M.i[g]);
+      std::copy(A.a.begin() + A.i[i], A.a.begin() + A.i[i + 1], M.a.begin() + M.i[g]);
+    }
+  }
+  return M;
+}
+
 // True when every row's stored l1 norm equals, bit for bit, the sum of |a_ij|
 // over its stored entries in order, negated for a negative first entry
 // (compute_l1_norms option 1 without C/F restriction): the device kernels can
@@ -326,9 +351,12 @@ void DevSell::release() {
 }
 
 void DevGs::upload(const CSR& A, int num_blocks, bool forward) {
+  upload(A, hypre_block_starts(A.nrows, num_blocks), forward);
+}
+void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forward) {
   release();
   GsSchedule S;
-  build_gs_schedule(A, hypre_block_starts(A.nrows, num_blocks), forward, S);
+  build_gs_schedule(A, block_starts, forward, S);
   nblocks = (int)S.block_start.size() - 1;
   max_levels = S.max_levels;
   wg = S.avg_rows_per_level > 96.0 ? 256 : 64;
@@ -485,14 +513,18 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       fwd = fwd || rt == 3 || rt == 6 || rt == 8 || rt == 13;
       bwd = bwd || rt == 4 || rt == 6 || rt == 8 || rt == 14;
     }
-    if ((fwd || bwd) && comm_)
-      throw std::runtime_error("hybrid Gauss-Seidel (relax 3/4/6/8/13/14) across ranks is not available in this build");
+    // Across ranks (par_relax.c with num_procs > 1): each rank sweeps its own
+    // rows in num_blocks blocks (RankLevel::gs_blocks), off-rank columns read
+    // the halo exchanged before the sweep, exactly as off-block columns read
+    // the pre-sweep copy.
     for (int l = 0; l < nl && (fwd || bwd); ++l) {
       const RankLevel& L = R.lev[l];
       DevLevel& D = lev_[l];
       if (l == nl - 1 && R.coarse_n > 0) break;  // coarsest level: direct solve
-      if (fwd) D.gs_fwd.upload(L.A.interior, prm.num_blocks, true);
-      if (bwd) D.gs_bwd.upload(L.A.interior, prm.num_blocks, false);
+      const CSR rows = merged_rows(L.A, L.n_loc);
+      const std::vector<int> bs = L.gs_blocks.empty() ? hypre_block_starts(L.n_loc, prm.num_blocks) : L.gs_blocks;
+      if (fwd) D.gs_fwd.upload(rows, bs, true);
+      if (bwd) D.gs_bwd.upload(rows, bs, false);
       D.gs_tmp = dalloc<double>(D.n + D.hu.n_halo);
     }
   }
@@ -652,9 +684,16 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       if ((fw && !L.gs_fwd.built()) || (bw && !L.gs_bwd.built()))
         throw std::runtime_error("hybrid Gauss-Seidel schedule missing on level " + std::to_string(level));
       if (zero_guess) HVE_HIP(launch_set(n, 0.0, u_cur, s));
-      const double* tmp = nullptr;
+      // off-rank values of u before the sweep (par_relax.c: Vext_data)
+      const bool ex = comm_ && L.hu.active();
+      if (ex) {
+        halo_start(L.hu, u_cur, s);
+        halo_finish(s);
+      }
+      const int nh = n + L.hu.n_halo;
+      const double* tmp = L.hu.n_halo > 0 ? u_cur : nullptr;  // halo columns: u's halo, untouched by the sweep
       if (L.gs_fwd.built() ? L.gs_fwd.nblocks > 1 : L.gs_bwd.nblocks > 1) {
-        HVE_HIP(launch_copy(n, u_cur, L.gs_tmp, s));  // tmp_data[i] = u_data[i]
+        HVE_HIP(launch_copy(nh, u_cur, L.gs_tmp, s));  // tmp_data[i] = u_data[i]
         tmp = L.gs_tmp;
       }
       if (fw) HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, s));

@@ -91,6 +91,7 @@ struct DevGs {
     return v;
   }
   void upload(const CSR& A, int num_blocks, bool forward);
+  void upload(const CSR& A, const std::vector<int>& block_starts, bool forward);
   void release();
 };
 

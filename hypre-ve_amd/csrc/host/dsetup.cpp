@@ -443,12 +443,15 @@ void rap_dist(const CSR& R, const CSR& A, const CSR& P, int first, const std::ve
 }
 
 // l1 norms of the owned rows (setup.cpp compute_l1_norms with global indices).
+// Option 4's blocks are num_blocks blocks of this rank's rows (hypre's
+// threads per process; partition.cpp rank_gs_blocks): columns of other ranks
+// are off-block.
 void l1_dist(const CSR& A, int first, int nglob, int option, const std::vector<int>* cf, const GhostPlan* gp,
              const std::vector<int>* gcf, int num_blocks, std::vector<double>& l1) {
+  (void)nglob;
   const int n = A.nrows;
   l1.assign(n, 0.0);
-  const int nb = std::max(1, num_blocks);
-  const int bsize = nglob / nb, rest = nglob - bsize * nb;
+  const std::vector<int> bs = hypre_block_starts(n, std::max(1, num_blocks));
   auto cf_of = [&](int c) -> int {
     if (c >= first && c < first + n) return (*cf)[c - first];
     return (*gcf)[gp->find(c)];
@@ -456,12 +459,8 @@ void l1_dist(const CSR& A, int first, int nglob, int option, const std::vector<i
 #pragma omp parallel for schedule(static)
   for (int i = 0; i < n; ++i) {
     const int gi = first + i;
-    int k;  // hypre's block of global row gi (par_relax.c size / rest partition)
-    if (gi < rest * (bsize + 1)) k = gi / (bsize + 1);
-    else k = rest + (gi - rest * (bsize + 1)) / std::max(1, bsize);
-    int ns, ne;
-    if (k < rest) { ns = k * bsize + k; ne = (k + 1) * bsize + k + 1; }
-    else { ns = k * bsize + rest; ne = (k + 1) * bsize + rest; }
+    const int k = (int)(std::upper_bound(bs.begin(), bs.end(), i) - bs.begin()) - 1;
+    const int ns = first + bs[k], ne = first + bs[k + 1];
     double s = 0.0;
     if (option == 1) {
       for (int q = A.i[i]; q < A.i[i + 1]; ++q)
@@ -484,6 +483,13 @@ void l1_dist(const CSR& A, int first, int nglob, int option, const std::vector<i
 }
 
 bool uses_l1_gs(int t) { return t == 8 || t == 13 || t == 14; }
+bool uses_hybrid_gs_any(const AMGParams& prm) {
+  for (int c = 0; c < 4; ++c) {
+    const int t = prm.relax_type[c];
+    if (t == 3 || t == 4 || t == 6 || uses_l1_gs(t)) return true;
+  }
+  return false;
+}
 
 struct DLevel {
   CSR A, P, R;  // owned rows, global columns
@@ -681,6 +687,12 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
       }
       D.cf = comm.allgatherv(D.cf);
       D.l1 = comm.allgatherv(D.l1);
+      // a replicated level is swept as one rank's rows: its hybrid-GS l1
+      // norms over num_blocks blocks of the whole level
+      bool cfr = false;
+      if (!D.l1.empty() && l1_option_for_level(prm, l, nl, &cfr) == 4)
+        compute_l1_norms_blocks(D.A, 4, (cfr && !D.cf.empty()) ? D.cf.data() : nullptr,
+                                hypre_block_starts(D.nglob, std::max(1, prm.num_blocks)), D.l1);
     }
     for (int l = agg; l < nl; ++l) {
       DLevel& D = L[l];
@@ -729,6 +741,7 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     }
     RL.l1 = D.l1;
     RL.cf = D.cf;
+    if (size > 1 && uses_hybrid_gs_any(prm)) RL.gs_blocks = hypre_block_starts(D.nloc, std::max(1, prm.num_blocks));
     if (agg >= 0 && l >= agg) {
       RL.hu.n_loc = D.nloc;
       if (l + 1 < nl) RL.hv.n_loc = D.nloc;

@@ -165,6 +165,10 @@ void transpose(const CSR& A, CSR& AT);
 void rap(const CSR& P, const CSR& A, CSR& RAP);
 void compute_l1_norms(const CSR& A, int option, const int* cf, int num_blocks,
                       std::vector<double>& l1);
+void compute_l1_norms_blocks(const CSR& A, int option, const int* cf, const std::vector<int>& block_starts,
+                             std::vector<double>& l1);
+// l1 norm option amg_setup computes on level j of nl (0, 1 or 4).
+int l1_option_for_level(const AMGParams& prm, int j, int nl, bool* cf_restricted);
 
 // Full setup; returns 0 on success.
 int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H);

@@ -1,4 +1,5 @@
 // Row partition of the hierarchy (see partition.hpp).
+#include "layout.hpp"
 #include "partition.hpp"
 
 #include <algorithm>
@@ -76,8 +77,8 @@ void make_rank_op(const CSR& M, int r0, int r1, int a, int b, const std::vector<
   make_op(M, r0, r1, a, b, halo, op);
 }
 
-static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, int size,
-                          std::vector<RankHierarchy>& out) {
+// Row starts of every level: a rank owns the C points of its fine rows.
+static std::vector<std::vector<int>> level_starts(const Hierarchy& H, const std::vector<int>& starts0, int size) {
   const int nl = (int)H.lev.size();
   if ((int)starts0.size() != size + 1 || starts0[size] != H.lev[0].A.nrows)
     throw std::runtime_error("partition: level-0 row starts do not cover the matrix");
@@ -89,9 +90,73 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
     for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] == 1);
     for (int r = 0; r <= size; ++r) starts[l + 1][r] = pref[starts[l][r]];
   }
-  std::vector<int64_t> grows(nl);
-  for (int l = 0; l < nl; ++l) grows[l] = H.lev[l].A.nrows;
-  const int agg = agglomeration_level(H.prm, grows, size);
+  return starts;
+}
+
+static int hierarchy_agg_level(const Hierarchy& H, int size) {
+  std::vector<int64_t> grows(H.lev.size());
+  for (size_t l = 0; l < H.lev.size(); ++l) grows[l] = H.lev[l].A.nrows;
+  return agglomeration_level(H.prm, grows, size);
+}
+
+static bool uses_hybrid_gs(const AMGParams& prm) {
+  for (int c = 0; c < 4; ++c) {
+    const int t = prm.relax_type[c];
+    if (t == 3 || t == 4 || t == 6 || t == 8 || t == 13 || t == 14) return true;
+  }
+  return false;
+}
+
+std::vector<std::vector<int>> rank_gs_blocks(const Hierarchy& H, const std::vector<int>& starts0, int size) {
+  const int nl = (int)H.lev.size();
+  const auto starts = level_starts(H, starts0, size);
+  const int agg = hierarchy_agg_level(H, size);
+  const int nb = std::max(1, H.prm.num_blocks);
+  std::vector<std::vector<int>> out(nl);
+  for (int l = 0; l < nl; ++l) {
+    const int n = H.lev[l].A.nrows;
+    if (agg >= 0 && l >= agg) {
+      out[l] = hypre_block_starts(n, nb);
+      continue;
+    }
+    out[l].assign(1, 0);
+    for (int r = 0; r < size; ++r) {
+      const int a = starts[l][r], b = starts[l][r + 1];
+      const std::vector<int> loc = hypre_block_starts(b - a, nb);
+      for (int k = 1; k <= nb; ++k) out[l].push_back(a + loc[k]);
+    }
+  }
+  return out;
+}
+
+// l1 norms of every level as the hybrid-GS row blocks `blocks` give them
+// (option 4 levels only; other levels keep the setup's norms).
+static std::vector<std::vector<double>> l1_for_blocks(const Hierarchy& H, const std::vector<std::vector<int>>& blocks) {
+  const int nl = (int)H.lev.size();
+  std::vector<std::vector<double>> out(nl);
+  for (int l = 0; l < nl; ++l) {
+    const Level& L = H.lev[l];
+    bool cfr = false;
+    if (L.l1.empty() || l1_option_for_level(H.prm, l, nl, &cfr) != 4) {
+      out[l] = L.l1;
+      continue;
+    }
+    const int* cfp = (cfr && !L.cf.empty()) ? L.cf.data() : nullptr;
+    compute_l1_norms_blocks(L.A, 4, cfp, blocks[l], out[l]);
+  }
+  return out;
+}
+
+static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, int size,
+                          std::vector<RankHierarchy>& out) {
+  const int nl = (int)H.lev.size();
+  const std::vector<std::vector<int>> starts = level_starts(H, starts0, size);
+  const int agg = hierarchy_agg_level(H, size);
+  // hybrid GS across ranks: every rank's rows form num_blocks blocks (hypre's
+  // threads per process), and the option-4 l1 norms follow those blocks
+  const bool gs_ranks = size > 1 && uses_hybrid_gs(H.prm);
+  std::vector<std::vector<double>> l1_ranks;
+  if (gs_ranks) l1_ranks = l1_for_blocks(H, rank_gs_blocks(H, starts0, size));
   // rows of level l this rank holds: its block, or all of a replicated level
   auto lo = [&](int l, int r) { return (agg >= 0 && l >= agg) ? 0 : starts[l][r]; };
   auto hi = [&](int l, int r) { return (agg >= 0 && l >= agg) ? H.lev[l].A.nrows : starts[l][r + 1]; };
@@ -155,7 +220,12 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
         const int rb = (agg >= 0 && l >= agg) ? H.lev[l + 1].A.nrows : starts[l + 1][r + 1];
         make_op(L.R, ra, rb, a, b, hv[l][r], RL.R);
       }
-      if (!L.l1.empty()) RL.l1.assign(L.l1.begin() + a, L.l1.begin() + b);
+      if (gs_ranks) {
+        if (!l1_ranks[l].empty()) RL.l1.assign(l1_ranks[l].begin() + a, l1_ranks[l].begin() + b);
+        RL.gs_blocks = hypre_block_starts(b - a, std::max(1, H.prm.num_blocks));
+      } else if (!L.l1.empty()) {
+        RL.l1.assign(L.l1.begin() + a, L.l1.begin() + b);
+      }
       if (!L.cf.empty()) RL.cf.assign(L.cf.begin() + a, L.cf.begin() + b);
       if (!L.cheby_ds.empty()) RL.cheby_ds.assign(L.cheby_ds.begin() + a, L.cheby_ds.begin() + b);
       RL.cheby_coefs = L.cheby_coefs;
@@ -303,9 +373,18 @@ void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, in
   out = std::move(all[rank]);
 }
 
-void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out) {
+void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out, const std::vector<int>* gs_rank_starts) {
   std::vector<int> s0 = {0, H.lev[0].A.nrows};
   partition_hierarchy(H, s0, 0, 1, out);
+  if (gs_rank_starts && gs_rank_starts->size() > 2 && uses_hybrid_gs(H.prm)) {
+    const int size = (int)gs_rank_starts->size() - 1;
+    const auto blocks = rank_gs_blocks(H, *gs_rank_starts, size);
+    const auto l1 = l1_for_blocks(H, blocks);
+    for (size_t l = 0; l < out.lev.size(); ++l) {
+      out.lev[l].gs_blocks = blocks[l];
+      out.lev[l].l1 = l1[l];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -351,7 +430,7 @@ struct Rd {
     pod(h.n_loc); pod(h.n_halo); vec(h.peers); vec(h.recv_cnt); vec(h.send_cnt); vec(h.send_idx); vec(h.halo_glob);
   }
 };
-const int64_t kMagic = 0x48564532414d47LL;  // "HVE2AMG"
+const int64_t kMagic = 0x48564533414d47LL;  // "HVE3AMG"
 }  // namespace
 
 void serialize(const RankHierarchy& R, std::vector<char>& buf) {
@@ -366,6 +445,7 @@ void serialize(const RankHierarchy& R, std::vector<char>& buf) {
     w.halo(L.hu); w.halo(L.hv);
     w.vec(L.l1); w.vec(L.cf);
     w.vec(L.cheby_ds); w.vec(L.cheby_coefs);
+    w.vec(L.gs_blocks);
   }
   w.pod(R.coarse_n); w.vec(R.coarse_dense);
   w.pod(R.grid_complexity); w.pod(R.operator_complexity);
@@ -388,6 +468,7 @@ void deserialize(const std::vector<char>& buf, RankHierarchy& R) {
     r.halo(L.hu); r.halo(L.hv);
     r.vec(L.l1); r.vec(L.cf);
     r.vec(L.cheby_ds); r.vec(L.cheby_coefs);
+    r.vec(L.gs_blocks);
   }
   r.pod(R.coarse_n); r.vec(R.coarse_dense);
   r.pod(R.grid_complexity); r.pod(R.operator_complexity);

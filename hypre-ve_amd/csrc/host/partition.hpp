@@ -48,6 +48,10 @@ struct RankLevel {
   std::vector<int> cf;
   std::vector<double> cheby_ds;     // Chebyshev: 1/sqrt(a_ii) of the owned rows (scaled variant)
   std::vector<double> cheby_coefs;  // Chebyshev polynomial coefficients (replicated)
+  // Hybrid Gauss-Seidel row blocks over the held rows (local numbering, nb+1
+  // starts); empty: hypre_block_starts(n_loc, num_blocks).  Several ranks:
+  // num_blocks blocks of each rank's rows, as hypre's threads per process.
+  std::vector<int> gs_blocks;
 };
 
 struct RankHierarchy {
@@ -83,7 +87,15 @@ void make_rank_op(const CSR& M, int r0, int r1, int a, int b, const std::vector<
 void partition_hierarchy_all(const Hierarchy& H, const std::vector<int>& starts0, int size,
                              std::vector<RankHierarchy>& out);
 // Whole hierarchy as one rank (no halo), used for the single-GPU path.
-void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out);
+// gs_rank_starts (optional, N+1 level-0 row starts): run the hybrid
+// Gauss-Seidel smoothers with the row blocks an N-rank partition would use
+// on every level (num_blocks per rank, l1 norms to match), so that one GPU
+// reproduces the N-rank iterates.
+void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out, const std::vector<int>* gs_rank_starts = nullptr);
+// Per level: global hybrid-GS block starts of an N-rank partition with level-0
+// starts starts0 (num_blocks blocks of every rank's rows; replicated levels
+// num_blocks blocks of the whole level).
+std::vector<std::vector<int>> rank_gs_blocks(const Hierarchy& H, const std::vector<int>& starts0, int size);
 
 int partition_self_check(const Hierarchy& H, int size, std::string& msg);
 

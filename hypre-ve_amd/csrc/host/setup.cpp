@@ -1043,14 +1043,26 @@ void rap(const CSR& P, const CSR& A, CSR& C) {
 // ---------------------------------------------------------------------------
 void compute_l1_norms(const CSR& A, int option, const int* cf, int num_blocks, std::vector<double>& l1) {
   const int n = A.nrows;
-  l1.assign(n, 0.0);
   const int nb = std::max(1, num_blocks);
-#pragma omp parallel for schedule(static)
+  std::vector<int> bs(nb + 1, 0);
   for (int k = 0; k < nb; ++k) {
     int size = n / nb, rest = n - size * nb;
-    int ns, ne;
-    if (k < rest) { ns = k * size + k; ne = (k + 1) * size + k + 1; }
-    else { ns = k * size + rest; ne = (k + 1) * size + rest; }
+    bs[k] = k < rest ? k * size + k : k * size + rest;
+  }
+  bs[nb] = n;
+  compute_l1_norms_blocks(A, option, cf, bs, l1);
+}
+
+// The same over explicit row blocks (bs: nb + 1 ascending starts): with
+// several ranks each rank's rows form hypre's per-process thread blocks.
+void compute_l1_norms_blocks(const CSR& A, int option, const int* cf, const std::vector<int>& bs,
+                             std::vector<double>& l1) {
+  const int n = A.nrows;
+  l1.assign(n, 0.0);
+  const int nb = (int)bs.size() - 1;
+#pragma omp parallel for schedule(static)
+  for (int k = 0; k < nb; ++k) {
+    const int ns = bs[k], ne = bs[k + 1];
     for (int i = ns; i < ne; ++i) {
       double s = 0.0;
       if (option == 1) {
@@ -1327,6 +1339,20 @@ void cheby_setup(const CSR& A, double max_eig, double min_eig, double fraction, 
 // Setup driver: par_amg_setup.c:889-2880 (coarsening loop), :2990-3120 (l1 norms).
 // ---------------------------------------------------------------------------
 static bool uses_l1_gs(int t) { return t == 8 || t == 13 || t == 14; }
+
+// l1 norm option the setup computes on level j of nl (0 none, 1 full row
+// sums for relax 18, 4 hybrid-GS norms for relax 8/13/14); *cf_restricted:
+// whether it uses the C/F marker (relax_order, not on the coarsest level).
+int l1_option_for_level(const AMGParams& prm, int j, int nl, bool* cf_restricted) {
+  int opt = 0;
+  bool cfr = false;
+  if (j < nl - 1 && (uses_l1_gs(prm.relax_type[1]) || uses_l1_gs(prm.relax_type[2]))) { opt = 4; cfr = true; }
+  else if (j == nl - 1 && uses_l1_gs(prm.relax_type[3])) { opt = 4; cfr = false; }
+  if (j < nl - 1 && (prm.relax_type[1] == 18 || prm.relax_type[2] == 18)) { opt = 1; cfr = true; }
+  else if (j == nl - 1 && prm.relax_type[3] == 18) { opt = 1; cfr = false; }
+  if (cf_restricted) *cf_restricted = cfr && prm.relax_order;
+  return opt;
+}
 
 int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
   H = Hierarchy();

@@ -175,6 +175,7 @@ SIGNATURES = [
     ("hypreve_BenchFineSpMV", _i, [_p, _i, _pd, _pd]),
     ("hypreve_BenchFineSpMVStoredBytes", _i, [_p, _pd]),
     ("hypreve_BoomerAMGGetLevelLayout", _i, [_p, _i, _i, _pi]),
+    ("hypreve_BoomerAMGSetGsRankStarts", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchStream", _i, [_i, C.c_int64, _i, _pd]),
@@ -507,6 +508,15 @@ class BoomerAMG:
         ms, by = C.c_double(), C.c_double()
         check(lib().hypreve_BenchFineSpMV(self.h, reps, C.byref(ms), C.byref(by)), "BenchFineSpMV")
         return ms.value, by.value
+
+    def set_gs_rank_starts(self, starts):
+        """Hybrid GS with the row blocks of an N-rank run (level-0 starts, N+1
+        entries); None clears it.  Takes effect at setup."""
+        if starts is None or len(starts) <= 2:
+            check(lib().hypreve_BoomerAMGSetGsRankStarts(self.h, 0, None), "SetGsRankStarts")
+            return
+        arr = (C.c_int * len(starts))(*[int(v) for v in starts])
+        check(lib().hypreve_BoomerAMGSetGsRankStarts(self.h, len(starts) - 1, arr), "SetGsRankStarts")
 
     LAYOUTS = ("padded", "jagged", "wide", "jag-pw", "dict", "delta", "delta+vt8", "delta+vt16", "padded+vt16",
                "jagged+vt16")

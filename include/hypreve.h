@@ -230,6 +230,12 @@ HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_block
  * most 4096 distinct values occur).  All give identical
  * bits; the forced settings exist for parity tests and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
+/* One GPU runs the hybrid Gauss-Seidel smoothers with the row blocks of an
+ * N-rank run whose level-0 rows start at starts[0..nranks] (num_blocks blocks
+ * of each rank's rows on every level, par_relax.c's per-process thread blocks;
+ * l1 norms to match), so its iterates equal the N-rank iterates. nranks <= 1
+ * clears it. Takes effect at Setup. */
+HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver solver, HYPRE_Int nranks, const HYPRE_Int *starts);
 /* Multi-rank: coarse levels with at most `rows` global rows (from the first
  * such level down) are held whole by every rank and cycled redundantly, with
  * one all-gather on the way down instead of halo exchanges on every coarse

@@ -63,6 +63,7 @@ def _solve_nranks(hv, nx, ny, nz, kw, nranks, timeout=300, stencil=7):
             raise e
     out.sort(key=lambda o: o[0])
     x = np.concatenate([o[1] for o in out])
+    _solve_nranks.starts = [o[0] for o in out] + [x.size]  # level-0 row starts of the run
     return x, [o[2] for o in out], [o[3] for o in out], out[0][4]
 
 
@@ -83,6 +84,40 @@ def test_loopback_partitioned_solve_bitwise(hv, nranks, nx, nz, relax, agglo):
     assert all(abs(r - rr1) <= 1e-10 * rr1 for r in rrN), (rr1, rrN)
     assert x1.shape == xN.shape
     assert np.array_equal(x1, xN), f"max |diff| {np.max(np.abs(x1 - xN))}"
+
+
+@pytest.mark.parametrize("nranks,nx,nz", [(2, 14, 16), (3, 12, 17)])
+@pytest.mark.parametrize("relax,order", [(3, 0), (6, 0), (13, 0), (8, 1)])
+@pytest.mark.parametrize("nb", [1, 3])
+@pytest.mark.parametrize("agglo", [0, 2000])
+def test_loopback_hybrid_gs_bitwise(hv, nranks, nx, nz, relax, order, nb, agglo):
+    """Hybrid Gauss-Seidel across ranks (par_relax.c with num_procs > 1): each
+    rank sweeps its rows in num_blocks blocks, off-rank columns read the halo
+    exchanged before the sweep, off-block columns the pre-sweep copy, and the
+    l1 norms (relax 8/13) follow those blocks.  One GPU given the same row
+    blocks (hypreve_BoomerAMGSetGsRankStarts) must reproduce the N-rank
+    iterates bit for bit; relax 8 with C/F ordering exchanges once per
+    point class, as hypre's two relax calls do."""
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=relax, relax_order=order, num_blocks=nb,
+              tol=1e-8, max_iter=40, agglo_rows=agglo)
+    xN, itN, rrN, nlN = _solve_nranks(hv, nx, nx, nz, kw, nranks)
+    starts = _solve_nranks.starts
+    A = _gen(hv, 7, nx, nx, nz)
+    amg = hv.BoomerAMG(**kw)
+    amg.set_gs_rank_starts(starts)
+    amg.setup(A)
+    b = hv.ParVector(A.n, np.ones(A.n))
+    x = hv.ParVector(A.n, np.zeros(A.n))
+    it1, rr1 = amg.solve(A, b, x)
+    x1 = x.get()
+    assert nlN == amg.num_levels()
+    assert all(i == it1 for i in itN), (it1, itN)
+    assert np.array_equal(x1, xN), f"max |diff| {np.max(np.abs(x1 - xN))}"
+    if nb == 1 and agglo == 0 and relax == 3:
+        # control: without the rank blocks one GPU runs a different smoother
+        xp, _, _, _ = _solve_1rank(hv, nx, nx, nz, kw)
+        assert not np.array_equal(xp, xN)
 
 
 @pytest.mark.parametrize("nranks", [2, 3])
