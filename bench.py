@@ -81,11 +81,18 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
 
     n = args.n
     t0 = time.time()
+    cx, cy, cz = (float(v) for v in args.coef.split(","))
+
+    def gen(nz, **part):
+        if args.stencil == 27:
+            return hv.ParCSRMatrix.laplacian27(n, n, nz, **part)
+        return hv.ParCSRMatrix.laplacian(n, n, nz, cx=cx, cy=cy, cz=cz, **part)
+
     if comm is not None:
         # weak scaling: n x n x (n * world) grid, rank r owns z-slab r
-        A = hv.ParCSRMatrix.laplacian(n, n, n * world, comm=comm, P=1, Q=1, R=world, p=0, q=0, r=rank)
+        A = gen(n * world, comm=comm, P=1, Q=1, R=world, p=0, q=0, r=rank)
     else:
-        A = hv.ParCSRMatrix.laplacian(n, n, n)
+        A = gen(n)
     nrows = A.n
     pcg = args.solver == "pcg"
     first = A.first if comm is not None else 0
@@ -148,8 +155,12 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     achieved = stored_bytes / (spmv_ms * 1e-3) / 1e9
     csr_gbs = csr_bytes / (spmv_ms * 1e-3) / 1e9
     vt = os.environ.get("HVE_SELL_VALTAB", "1") != "0"
-    # k_sell_delta<OP_RESID, no CF, batch 8, NT, value table (0 none, 1 8-bit)>
-    traffic = committed_traffic(n, "k_sell_delta<0, false, 8, true, %d>(hve::SpArgs)" % (1 if vt else 0))
+    aniso = args.coef != "1,1,1"
+    default_op = args.stencil == 7 and not aniso
+    # k_sell_delta<OP_RESID, no CF, batch 8, NT, value table (0 none, 1 8-bit)>; the committed PMC
+    # summary measured the default operator only
+    traffic = committed_traffic(n, "k_sell_delta<0, false, 8, true, %d>(hve::SpArgs)" % (1 if vt else 0)) \
+        if default_op else None
     # the box's achievable read bandwidth: a grid-stride 8 B/lane stream over 2 GiB
     stream_n = (1 << 31) // 8
     stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 10) * 1e-3) / 1e9
@@ -214,8 +225,10 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (GenerateLaplacian 7-point, rhs = ones)",
-        "config": {"workload": f"3D 7-point Laplacian {n}^3 per GPU ({n}x{n}x{n * world} global, z-slab row "
+        "data": f"synthetic ({'GenerateLaplacian27pt' if args.stencil == 27 else 'GenerateLaplacian 7-point'}"
+                f"{'' if default_op else ', coefficients ' + args.coef}, rhs = ones)",
+        "config": {"workload": f"3D {args.stencil}-point {'anisotropic diffusion (' + args.coef + ')' if aniso else 'Laplacian'}"
+                               f" {n}^3 per GPU ({n}x{n}x{n * world} global, z-slab row "
                                f"blocks), {'BoomerAMG-PCG (one V-cycle per PCG iteration)' if pcg else 'BoomerAMG V-cycle'}"
                                f", PMIS + ext+i (Pmx 4), l1-Jacobi (relax 18) down/up, Gaussian elimination coarsest",
                    "rows_per_gpu": nrows, "levels": amg.num_levels(), "grid_complexity": round(g, 6),
@@ -232,6 +245,10 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=256, help="grid edge per GPU (n^3 rows per GPU)")
+    ap.add_argument("--stencil", type=int, choices=[7, 27], default=7,
+                    help="7: GenerateLaplacian (configs[1], the bench line); 27: GenerateLaplacian27pt (configs[3])")
+    ap.add_argument("--coef", default="1,1,1",
+                    help="cx,cy,cz of the 7-point operator; e.g. 0.001,1,1 for configs[4]'s anisotropic diffusion")
     ap.add_argument("--cpu-cycles", type=int, default=1, help="run the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
     ap.add_argument("--cpu-cycles-max", type=int, default=60)
