@@ -182,7 +182,9 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
             f"host peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6:.1f} GB")
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_cycles > 0:
+    # The partitioned (--dist) hierarchy keeps no whole level matrices on the
+    # host, so the oracle baseline runs on the one-process path only.
+    if rank == 0 and world == 1 and not args.dist and args.cpu_cycles > 0:
         # The reference's CPU solve path, restated in C (oracle/oracle.c, the
         # parity checker) and run with OpenMP over rows on this host's cores,
         # on the same hierarchy and right-hand side.  Sample sized to ~10 s.
