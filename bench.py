@@ -1,14 +1,16 @@
 """BoomerAMG V-cycle throughput on MI355X (BASELINE.json metric).
 
-Workload (configs[1]): 3-D 7-point Laplacian, 256^3 rows per GPU, BoomerAMG
-with PMIS coarsening, extended+i interpolation (P_max_elmts 4), l1-Jacobi
-down/up smoothing, Gaussian elimination on the coarsest level.
+Workload: 3-D 7-point Laplacian, 512^3 rows per GPU (configs[2]'s grid, the
+north-star size), BoomerAMG with PMIS coarsening, extended+i interpolation
+(P_max_elmts 4), l1-Jacobi down/up smoothing, Gaussian elimination on the
+coarsest level.  On one GPU the 256^3 problem (configs[1]) is measured after
+it into "secondary".
 A step = one BoomerAMG solve iteration (hypre_BoomerAMGSolve loop body): one
 V-cycle plus the fine-grid residual and its norm.  Inputs are resident in HBM
 before the timed region; the host setup phase is not timed.
 
 Multi-GPU: one process per GPU (torch.distributed.run); weak scaling with
-256^3 rows per GPU (global grid 256 x 256 x 256*N, row blocks by z-slab).
+n^3 rows per GPU (global grid n x n x n*N, row blocks by z-slab).
 """
 import argparse
 import json
@@ -27,13 +29,31 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PROFILE_DIR = os.path.join(ROOT, "profiles")
 
 
-def committed_traffic(n, kernel_suffix):
+# hypreve_BoomerAMGGetLevelLayout name -> (residual kernel instantiation as
+# rocprofv3 names it, minus the batch width: "<prefix>B<suffix>"; description)
+KERNEL_OF_LAYOUT = {
+    "delta+vt8": ("k_sell_delta<0, false, |, true, 1>(hve::SpArgs)",
+                  "SELL-64 with 16-bit column deltas and an 8-bit value table"),
+    "delta+vt16": ("k_sell_delta<0, false, |, true, 2>(hve::SpArgs)",
+                   "SELL-64 with 16-bit column deltas and a 16-bit value table"),
+    "delta": ("k_sell_delta<0, false, |, true, 0>(hve::SpArgs)", "SELL-64 with 16-bit column deltas"),
+    "dict": ("k_sell_dict<0, false, |, true, ", "jagged SELL-64 with an LDS x-tile dictionary"),
+    "padded": ("k_sell<0, false, |, ", "padded SELL-64"),
+    "jagged": ("k_sell<0, false, |, ", "jagged SELL-64"),
+    "wide": ("k_sell_wide<0, false, |", "padded SELL-64, one workgroup per slice"),
+    "jag-pw": ("k_sell_pw<0, false, |", "jagged SELL-64, wave-product-parallel"),
+    "padded+vt16": ("k_sell_vt<0, false, |, false>(hve::SpArgs)", "padded SELL-64 with a 16-bit value table"),
+    "jagged+vt16": ("k_sell_vt<0, false, |, true>(hve::SpArgs)", "jagged SELL-64 with a 16-bit value table"),
+}
+
+
+def committed_traffic(n, kname):
     """HBM bytes per launch of the finest residual SpMV from the newest
     committed rocprofv3 PMC summary for this workload (scripts/pmc_traffic.py),
-    or None when that summary measured another kernel / layout (its kernel
-    names must end with kernel_suffix).  Counters need their own profiler
-    passes, so the bench reports the committed measurement of the same kernel
-    and grid."""
+    or None when that summary measured another kernel / layout (every kernel
+    name it matched must contain both halves of kname around the batch width).
+    Counters need their own profiler passes, so the bench reports the committed
+    measurement of the same kernel and grid."""
     best = None
     for rnd in sorted(os.listdir(PROFILE_DIR)) if os.path.isdir(PROFILE_DIR) else []:
         p = os.path.join(PROFILE_DIR, rnd, f"pmc_traffic_{n}.json")
@@ -44,7 +64,9 @@ def committed_traffic(n, kernel_suffix):
     with open(best) as f:
         d = json.load(f)
     names = d.get("kernel_names", [])
-    if not names or not all(nm.endswith(kernel_suffix) for nm in names):
+    pre, post = kname.split("|")
+    if not names or not all(pre in nm and post in nm[nm.index(pre) + len(pre):] for nm in names if pre in nm) \
+            or not all(pre in nm for nm in names):
         return None
     return round(d["traffic_bytes"], 0)
 
@@ -75,11 +97,54 @@ class heartbeat:
         self.stop.set()
 
 
-def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
-    """One rank's part of the bench; returns the JSON dict on rank 0."""
+def oracle_cpu_baseline(amg, nrows, n, pcg, args):
+    """The reference's CPU solve path, restated in C (oracle/oracle.c, the
+    parity checker) and run with OpenMP over rows on this host's cores, on the
+    hierarchy `amg` (one-process setup) with rhs = ones.  Sample sized to
+    about args.cpu_seconds of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+
+    O = oracle_py.OracleAMG(amg)
+    bh = np.ones(nrows)
+    u = np.zeros(nrows)
+
+    def cpu_run(k):
+        u[:] = 0.0
+        if pcg:
+            return O.pcg(bh, u, 0.0, k, 1)[0]
+        return O.solve(bh, u, 1e-300, k)["iterations"]
+
+    tc = time.perf_counter()
+    cpu_run(1)
+    t1 = time.perf_counter() - tc
+    iters = int(max(2, min(args.cpu_cycles_max, round(args.cpu_seconds / max(t1, 1e-3)))))
+    tc = time.perf_counter()
+    done = cpu_run(iters)
+    tcpu = time.perf_counter() - tc
+    threads = oracle_py.num_threads()
+    what = "PCG iterations (one V-cycle preconditioner each)" if pcg else "solve iterations (V-cycle + residual norm)"
+    cpu = {"value": round(nrows * done / tcpu, 1), "unit": "DOF/s", "cores": threads, "kind": "port",
+           "sample": f"{done} {what} of the same {n}^3 hierarchy by the C oracle (oracle/oracle.c), "
+                     f"OpenMP {threads} threads, {tcpu:.1f}s"}
+    log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({done} iterations, {tcpu:.1f}s, {threads} threads)")
+    return cpu
+
+
+def amg_settings(hv, pcg):
+    """The bench's BoomerAMG: PMIS, ext+i (Pmx 4), l1-Jacobi down/up,
+    Gaussian elimination on the coarsest level (ij -pmis -rlx 18)."""
+    kw = hv.ij_amg_defaults(1 if pcg else 0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
+    return kw
+
+
+def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light=False):
+    """One rank's part of the bench; returns the JSON dict on rank 0.  light:
+    a secondary size (no CPU baseline, no stream calibration)."""
     import torch
 
-    n = args.n
+    n = args.n if n is None else n
     t0 = time.time()
     cx, cy, cz = (float(v) for v in args.coef.split(","))
 
@@ -100,17 +165,14 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=nrows * world)
     if pcg:
         # ij -solver 1: PCG (two-norm) preconditioned by one BoomerAMG V-cycle
-        kw = hv.ij_amg_defaults(1)
-        kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
-        amg = hv.BoomerAMG(**kw)
+        amg = hv.BoomerAMG(**amg_settings(hv, True))
         krylov = hv.PCG(tol=0.0, max_iter=max(1, args.warmup), two_norm=1)
         krylov.set_precond_amg(amg)
         with heartbeat(f"rank {rank} setup"):
             krylov.setup(A, b, x)
     else:
-        kw = hv.ij_amg_defaults(0)
-        kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-300, max_iter=args.warmup,
-                  min_iter=0)
+        kw = amg_settings(hv, False)
+        kw.update(tol=1e-300, max_iter=args.warmup, min_iter=0)
         amg = hv.BoomerAMG(**kw)
         with heartbeat(f"rank {rank} setup"):
             amg.setup(A)
@@ -154,26 +216,45 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
     stored_bytes = amg.fine_spmv_stored_bytes()
     achieved = stored_bytes / (spmv_ms * 1e-3) / 1e9
     csr_gbs = csr_bytes / (spmv_ms * 1e-3) / 1e9
-    vt = os.environ.get("HVE_SELL_VALTAB", "1") != "0"
     aniso = args.coef != "1,1,1"
     default_op = args.stencil == 7 and not aniso
-    # k_sell_delta<OP_RESID, no CF, batch 8, NT, value table (0 none, 1 8-bit)>; the committed PMC
-    # summary measured the default operator only
-    traffic = committed_traffic(n, "k_sell_delta<0, false, 8, true, %d>(hve::SpArgs)" % (1 if vt else 0)) \
-        if default_op else None
+    layout0 = amg.level_layout(0, 0)
+    kname, kdesc = KERNEL_OF_LAYOUT[layout0]
+    # the committed PMC summary (scripts/pmc_traffic.py) measured the default
+    # operator's finest residual kernel at this size; reported only for the same kernel
+    traffic = committed_traffic(n, kname) if default_op else None
+    # every large operator of the cycle, each timed alone with HIP events (bytes
+    # of its stored layout + vectors per launch)
+    per_kernel = []
+    nl = amg.num_levels()
+    for lvl, which, what in ((0, 0, "A0 residual"), (0, 1, "P0 prolongation"), (0, 2, "R0 restriction"),
+                             (1, 0, "A1 residual"), (1, 1, "P1 prolongation"), (1, 2, "R1 restriction"),
+                             (2, 0, "A2 residual")):
+        if lvl >= nl or (which and lvl >= nl - 1):
+            continue
+        ms_k, csr_k, _ = amg.bench_level_op(lvl, which, max(5, args.spmv_reps // 2))
+        sb_k = amg.level_op_stored_bytes(lvl, which)
+        per_kernel.append({"op": what, "layout": amg.level_layout(lvl, which), "avg_ms": round(ms_k, 4),
+                           "stored_bytes": round(sb_k), "csr_bytes": round(csr_k),
+                           "gbs": round(sb_k / (ms_k * 1e-3) / 1e9, 1),
+                           "frac": round(sb_k / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)})
+        if rank == 0:
+            log(f"[bench] {what:16s} {per_kernel[-1]['layout']:12s} {ms_k:.4f} ms  "
+                f"{sb_k / 1e9:.3f} GB stored -> {per_kernel[-1]['gbs']:.0f} GB/s ({per_kernel[-1]['frac']:.3f})")
     # the box's achievable read bandwidth: a grid-stride 8 B/lane stream over 2 GiB
     stream_n = (1 << 31) // 8
-    stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 10) * 1e-3) / 1e9
+    stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 3 if light else 10) * 1e-3) / 1e9
     if args.calib:
         for eb in (2, 4, 8):
             hv.bench_stream(eb, (1 << 29) // eb, 1)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": "k_sell_delta<OP_RESID> finest level (r = b - A x), SELL-64 with 16-bit column deltas" +
-                      (" and an 8-bit value table" if vt else ""),
+            "kernel": f"{kname.replace('|', 'B').split('(')[0]} finest level (r = b - A x), {kdesc}",
+            "layout": layout0,
             "avg_ms": round(spmv_ms, 4), "bytes_per_launch": stored_bytes,
             "csr_bytes_per_launch": csr_bytes, "csr_equivalent_gbs": round(csr_gbs, 1),
-            "stream_read_gbs": round(stream_gbs, 1), "frac_of_stream": round(achieved / stream_gbs, 4)}
+            "stream_read_gbs": round(stream_gbs, 1), "frac_of_stream": round(achieved / stream_gbs, 4),
+            "per_kernel": per_kernel}
     if rank == 0:
         import resource
         log(f"[bench] read stream {stream_gbs:.0f} GB/s; fine SpMV at {achieved / stream_gbs:.3f} of it")
@@ -182,37 +263,26 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
             f"host peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6:.1f} GB")
 
     cpu = None
-    # The partitioned (--dist) hierarchy keeps no whole level matrices on the
-    # host, so the oracle baseline runs on the one-process path only.
-    if rank == 0 and world == 1 and not args.dist and args.cpu_cycles > 0:
-        # The reference's CPU solve path, restated in C (oracle/oracle.c, the
-        # parity checker) and run with OpenMP over rows on this host's cores,
-        # on the same hierarchy and right-hand side.  Sample sized to ~10 s.
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import oracle_py
-
-        O = oracle_py.OracleAMG(amg)
-        bh = np.ones(nrows)
-        u = np.zeros(nrows)
-        def cpu_run(k):
-            u[:] = 0.0
-            if pcg:
-                return O.pcg(bh, u, 0.0, k, 1)[0]
-            return O.solve(bh, u, 1e-300, k)["iterations"]
-
-        tc = time.perf_counter()
-        cpu_run(1)
-        t1 = time.perf_counter() - tc
-        iters = int(max(2, min(args.cpu_cycles_max, round(args.cpu_seconds / max(t1, 1e-3)))))
-        tc = time.perf_counter()
-        done = cpu_run(iters)
-        tcpu = time.perf_counter() - tc
-        threads = oracle_py.num_threads()
-        what = "PCG iterations (one V-cycle preconditioner each)" if pcg else "solve iterations (V-cycle + residual norm)"
-        cpu = {"value": round(nrows * done / tcpu, 1), "unit": "DOF/s", "cores": threads, "kind": "port",
-               "sample": f"{done} {what} of the same {n}^3 hierarchy by the C oracle (oracle/oracle.c), "
-                         f"OpenMP {threads} threads, {tcpu:.1f}s"}
-        log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({done} iterations, {tcpu:.1f}s, {threads} threads)")
+    if rank == 0 and not light and args.cpu_cycles > 0:
+        if world == 1 and not args.dist:
+            cpu = oracle_cpu_baseline(amg, nrows, n, pcg, args)
+        else:
+            # The partitioned hierarchy keeps no whole level matrices on the
+            # host: rank 0 times the same CPU path on a one-process hierarchy of
+            # args.cpu_n^3 rows (DOF/s of the host path is size-independent in
+            # this range: 1.1-1.3e8 at 256^3, 1.1e8 at 512^3 on 16 threads).
+            ncpu = args.cpu_n
+            Ac = hv.ParCSRMatrix.laplacian27(ncpu, ncpu, ncpu) if args.stencil == 27 else \
+                hv.ParCSRMatrix.laplacian(ncpu, ncpu, ncpu, cx=cx, cy=cy, cz=cz)
+            ac = hv.BoomerAMG(**amg_settings(hv, pcg))
+            ac.setup(Ac)
+            cpu = oracle_cpu_baseline(ac, Ac.n, ncpu, pcg, args)
+            cpu["sample"] += f" (one-process {ncpu}^3 stand-in for the {world}-rank problem: per-rank equivalent)"
+            ac.destroy()
+            Ac.destroy()
+    nlev = amg.num_levels()
+    for obj in ((krylov,) if pcg else ()) + (amg, A, b, x):
+        obj.destroy()  # release host and device memory before a secondary size runs
     if rank != 0:
         return None
     return {
@@ -233,7 +303,7 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks):
                                f" {n}^3 per GPU ({n}x{n}x{n * world} global, z-slab row "
                                f"blocks), {'BoomerAMG-PCG (one V-cycle per PCG iteration)' if pcg else 'BoomerAMG V-cycle'}"
                                f", PMIS + ext+i (Pmx 4), l1-Jacobi (relax 18) down/up, Gaussian elimination coarsest",
-                   "rows_per_gpu": nrows, "levels": amg.num_levels(), "grid_complexity": round(g, 6),
+                   "rows_per_gpu": nrows, "levels": nlev, "grid_complexity": round(g, 6),
                    "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
                    "parallelism": f"rows{world}"},
         "roofline": roof,
@@ -246,7 +316,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=256, help="grid edge per GPU (n^3 rows per GPU)")
+    ap.add_argument("--n", type=int, default=512,
+                    help="grid edge per GPU (n^3 rows per GPU); 512: configs[2]'s 512^3, the north-star size")
+    ap.add_argument("--secondary-n", type=int, default=256,
+                    help="one GPU: also measure this size (configs[1]'s 256^3) into 'secondary' (0 = skip)")
+    ap.add_argument("--cpu-n", type=int, default=256,
+                    help="N > 1: grid edge of the one-process hierarchy rank 0 times the CPU baseline on")
     ap.add_argument("--stencil", type=int, choices=[7, 27], default=7,
                     help="7: GenerateLaplacian (configs[1], the bench line); 27: GenerateLaplacian27pt (configs[3])")
     ap.add_argument("--coef", default="1,1,1",
@@ -338,6 +413,12 @@ def main():
         return float(tt.item())
 
     out = run_rank(hv, args, comm, rank, world, barrier, max_over_ranks)
+    if out is not None and world == 1 and comm is None and args.secondary_n > 0 and args.secondary_n != args.n:
+        sec = run_rank(hv, args, None, 0, 1, barrier, max_over_ranks, n=args.secondary_n, light=True)
+        out["secondary"] = {k: sec[k] for k in ("value", "unit", "ms_per_step", "steps")}
+        out["secondary"]["config"] = sec["config"]
+        out["secondary"]["roofline"] = {k: sec["roofline"][k] for k in ("achieved", "frac", "avg_ms", "kernel",
+                                                                        "bytes_per_launch", "per_kernel")}
     if out is not None:
         print(json.dumps(out), flush=True)
     if dist:

@@ -76,7 +76,10 @@ struct hypre_Solver_struct {
   int iters = 0;
   double rel_res = 0.0;
   bool use_graph = true;
-  bool user_num_blocks = false;
+  // num_blocks 0 (the default): one hybrid-GS row block per kAutoBlockRows
+  // local rows, resolved at Setup (hypre's CPU path uses its OpenMP thread
+  // count; a single block would run each sweep in one workgroup)
+  bool auto_blocks = true;
   std::vector<int> gs_rank_starts;  // one GPU emulating the GS blocks of an N-rank run
   // PCG
   PCGParams pcg;
@@ -84,6 +87,12 @@ struct hypre_Solver_struct {
   HYPRE_PtrToParSolverFcn precond_solve = nullptr, precond_setup = nullptr;
   std::unique_ptr<DevAMG> ws;
 };
+
+// Automatic hybrid Gauss-Seidel block count (num_blocks 0): one block of about
+// kAutoBlockRows rows each, so a large level's sweep runs on thousands of
+// workgroups while every block keeps hypre's exact in-block GS order.
+static constexpr int kAutoBlockRows = 4096;
+static int auto_num_blocks(int local_rows) { return std::max(1, (local_rows + kAutoBlockRows - 1) / kAutoBlockRows); }
 
 // ---------------------------------------------------------------------------
 // error state (utilities/hypre_error.c semantics)
@@ -700,8 +709,9 @@ HYPRE_Int HYPRE_BoomerAMGSetCycleRelaxType(HYPRE_Solver s, HYPRE_Int relax_type,
 }
 HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver s, HYPRE_Int nb) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  s->prm.num_blocks = nb < 1 ? 1 : nb;
-  s->user_num_blocks = nb >= 1;
+  CHECK_ARG(nb >= 0, 2);
+  s->auto_blocks = nb == 0;
+  if (nb >= 1) s->prm.num_blocks = nb;
   return 0;
 }
 HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver s, HYPRE_Int rows) {
@@ -762,6 +772,7 @@ HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(A, 2);
   API_BEGIN
+  if (s->auto_blocks) s->prm.num_blocks = auto_num_blocks(A->n);
   amg_setup(A->diag, s->prm, s->H);
   API_END
 }
@@ -1000,6 +1011,7 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
   CHECK_ARG(A, 2);
   API_BEGIN
   s->comm = A->comm;
+  if (s->auto_blocks) s->prm.num_blocks = auto_num_blocks(A->n);
   if (A->multi()) {
     if (use_dist_setup(s->prm)) setup_dist(s, A);
     else setup_multi(s, A);
@@ -1283,6 +1295,21 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
     *bytes = (double)M.nnz * 12.0 + (double)M.nrows * out_rw + (double)M.ncols * 8.0 + (double)(M.nslices + 1) * 4.0 +
              (M.rowmap ? (double)M.nrows * 4.0 : 0.0) + (M.rowlen ? (double)M.nrows * 4.0 : 0.0);
   if (padded_nnz) *padded_nnz = (double)M.nnz_pad;
+  API_END
+}
+
+// Bytes one hypreve_BenchLevelOp launch streams in the operator's stored layout
+// (DevSell::bytes: compressed columns / values, padding, bases, dictionaries,
+// row maps) plus its vectors counted as BenchLevelOp counts them.
+HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Real* bytes) {
+  CHECK_ARG(s && s->dev && s->dev->built() && bytes, 1);
+  CHECK_ARG(level >= 0 && level < s->dev->num_levels(), 2);
+  CHECK_ARG(which >= 0 && which <= 2 && (which == 0 || level < s->dev->num_levels() - 1), 3);
+  API_BEGIN
+  const DevLevel& L = s->dev->level(level);
+  const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
+  const double out_rw = which == 0 ? 16.0 : which == 1 ? 16.0 : 8.0;
+  *bytes = (double)M.bytes() + (double)M.nrows * out_rw + (double)M.ncols * 8.0;
   API_END
 }
 

@@ -77,10 +77,4 @@ hipError_t launch_pcg_beta(double* sc, hipStream_t st);
 hipError_t launch_coarse(int n, const double* Lf, const unsigned char* Lmask, const double* U,
                          const double* f, double* u, hipStream_t st);
 
-// Hybrid Gauss-Seidel (block-Jacobi across row blocks, exact GS inside a block).
-struct GSPlan;  // defined in relax_gs.hip
-hipError_t launch_hybrid_gs(const GSPlan& plan, const double* f, const double* l1, const int* cf,
-                            int relax_points, double* u, double* tmp, int fwd, int bwd, int use_l1,
-                            hipStream_t st);
-
 }  // namespace hve

@@ -126,12 +126,26 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
   }();
   // Short-row operators (P) take it only together with a value table.
   const bool short_rows = avg_len < 5.0 && delta_env != 1;
-  bool use_delta = A.nnz() > 0 && !wide && !jag && !use_dict && delta_env != 0 && sigma_env == 0;
+  // A long-row operator with few distinct values (the 27-point stencil: 27
+  // slots, 2 values) takes delta + 8-bit value table (3 B an entry) ahead of
+  // the dictionary (10 B an entry), when the table builds.
+  const bool delta_before_dict = policy == 0 && use_dict && !jag && !wide && delta_env != 0 && sigma_env == 0 &&
+                                 sell_valtab_env() != 0;
+  bool use_delta = (A.nnz() > 0 && !wide && !jag && !use_dict && delta_env != 0 && sigma_env == 0) || delta_before_dict;
   if (policy != 0) use_delta = (policy == 6 || policy == 7) && A.nnz() > 0;
   if (use_delta) {
     std::vector<short> dc;
     std::vector<int> sb;
-    if (build_sell_delta_host(A, sp, sb, dc, val)) {
+    std::vector<unsigned char> vi_probe;
+    std::vector<double> tab_probe;
+    bool delta_ok = build_sell_delta_host(A, sp, sb, dc, val);
+    if (delta_ok && delta_before_dict && !build_value_table(val, 256, vi_probe, tab_probe)) delta_ok = false;
+    if (!delta_ok && delta_before_dict) {
+      sp.clear();
+      val.clear();
+      goto dict;
+    }
+    if (delta_ok) {
       nrows = A.nrows;
       ncols = A.ncols;
       nslices = (int)sp.size() - 1;
@@ -180,6 +194,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
     sp.clear();
     val.clear();
   }
+dict:
   if (use_dict) {
     std::vector<unsigned short> c16;
     std::vector<int> dp, dc, rl2;
@@ -220,6 +235,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
       this->val = dupload(val.data(), val.size());
       dict_ptr = dupload(dp.data(), dp.size());
       dict = dupload(dc.data(), std::max<size_t>(1, dc.size()));
+      ndict = (int64_t)dc.size();
       std::vector<int> map(A.nrows);
       for (int i = 0; i < A.nrows; ++i) map[i] = rowmap_h.empty() ? perm[i] : rowmap_h[perm[i]];
       bool ident = true;
@@ -346,7 +362,7 @@ void DevSell::release() {
   if (vtab) (void)hipFree(vtab);
   dcol = nullptr; slot_base = nullptr; vidx = nullptr; vidx16 = nullptr; vtab = nullptr; nvtab = 0;
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
-  col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1;
+  col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1; ndict = 0;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;
 }
 
@@ -421,7 +437,7 @@ void DevAMG::release() {
     L.A.release(); L.P.release(); L.R.release();
     L.hu.release(); L.hv.release();
     L.gs_fwd.release(); L.gs_bwd.release();
-    for (void* p : {(void*)L.l1, (void*)L.cf, (void*)L.F, (void*)L.U[0], (void*)L.U[1], (void*)L.V,
+    for (void* p : {(void*)L.l1, (void*)L.cf, (void*)L.cf_l1, (void*)L.F, (void*)L.U[0], (void*)L.U[1], (void*)L.V,
                     (void*)L.gs_tmp, (void*)L.cheby_ds, (void*)L.cheby_r, (void*)L.cheby_t, (void*)L.cheby_o})
       if (p) (void)hipFree(p);
   }
@@ -487,6 +503,18 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
     D.l1_fly = !L.l1.empty() && l1_on_the_fly(L.A, L.l1) && D.A.in.dcol && (D.A.bd.nrows == 0 || D.A.bd.dcol);
     if (!L.cf.empty()) D.cf = dupload(L.cf.data(), L.cf.size());
+    if (!L.cf.empty() && prm.relax_order == 1 && (prm.relax_type[1] == 18 || prm.relax_type[2] == 18)) {
+      std::vector<int> m(L.cf.begin(), L.cf.begin() + std::min<size_t>(L.cf.size(), (size_t)L.n_loc));
+      for (int part = 0; part < 2; ++part) {
+        const CSR& A = part == 0 ? L.A.interior : L.A.boundary;
+        const std::vector<int>& map = part == 0 ? L.A.map_int : L.A.map_bnd;
+        for (int i = 0; i < A.nrows; ++i) {
+          const int g = map.empty() ? i : map[i];
+          if (g < (int)m.size() && (A.i[i] == A.i[i + 1] || A.a[A.i[i]] == 0.0)) m[g] = 0;
+        }
+      }
+      D.cf_l1 = dupload(m.data(), m.size());
+    }
     D.F = dalloc<double>(D.n);
     D.U[0] = dalloc<double>(D.n + D.hu.n_halo);
     D.U[1] = dalloc<double>(D.n + D.hu.n_halo);
@@ -596,7 +624,8 @@ void DevAMG::apply(const DevOp& M, const DevHalo* hx, int op, double* x, const d
 bool DevAMG::can_fuse_presmooth() const {
   if (lev_.size() < 2 || !lev_[0].l1) return false;
   const int rt = prm.relax_type[1];
-  return (rt == 18 || rt == 7) && prm.relax_weight == 1.0 && prm.num_sweeps[1] >= 1;
+  // with relax_order 1 the first down sweep is C/F-ordered (18) or one of two (7)
+  return (rt == 18 || rt == 7) && prm.relax_weight == 1.0 && prm.num_sweeps[1] >= 1 && prm.relax_order != 1;
 }
 double* DevAMG::presmooth_buffer() { return u0_buf_[1] ? u0_buf_[1] : lev_[0].U[0]; }
 
@@ -648,6 +677,7 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
   DevLevel& L = lev_[level];
   const double w = prm.relax_weight;
   const int n = L.n;
+  if (relax_type == 7) relax_points = 0;  // par_relax.c:3463: a C/F-ordered call is a full sweep
   if (zero_guess && relax_points != 0) {
     HVE_HIP(launch_set(n, 0.0, u_cur, s));
     zero_guess = false;
@@ -656,7 +686,17 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
     case 18:
     case 7: {
       if (!L.l1) throw std::runtime_error("l1 norms missing for relax type 18/7");
-      if (relax_points != 0) throw std::runtime_error("C/F-ordered l1-Jacobi is not available on the GPU path");
+      if (relax_points != 0) {
+        // par_relax_more.c:991 hypre_ParCSRRelax_L1_Jacobi: rows of class
+        // relax_points with a nonzero diagonal, u += (w (f - A u_old))/l1 with the
+        // C/F-restricted norms; out of place, so every row reads the pre-sweep u
+        // (its Vtemp copy), and the others are copied.  w (f - Au) equals the
+        // weighted kernel's (-w)(-f + Au) bit for bit (negation is exact).
+        if (!L.cf_l1) throw std::runtime_error("C/F marker missing for C/F-ordered l1-Jacobi");
+        apply(L.A, &L.hu, w == 1.0 ? K_L1JAC : K_L1JAC_W, u_cur, f, L.l1, L.cf_l1, relax_points, u_alt, w, 0.0, s);
+        std::swap(u_cur, u_alt);
+        break;
+      }
       if (zero_guess) {
         HVE_HIP(launch_zero_guess(n, w == 1.0 ? 0 : 1, w, f, L.l1, u_cur, s));
       } else {
@@ -795,10 +835,12 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       if (relax_type == 9 || relax_type == 99 || relax_type == 19 || relax_type == 98) {
         coarse_solve(level, fl[level], ucur[level], s);
         zero[level] = 0;
-      } else if (relax_type == 18 || relax_type == 7) {
+      } else if (relax_type == 18 && !(prm.relax_order == 1 && cycle_param < 3)) {
         relax(level, relax_type, 0, fl[level], ucur[level], ualt[level], zero[level], s);
         zero[level] = 0;
       } else {
+        // relax 18 with relax_order 1: C/F-ordered L1_Jacobi twice (par_cycle.c:398-415);
+        // the rest through hypre_BoomerAMGRelaxIF (par_relax_interface.c:35-76)
         if (prm.relax_order == 1 && cycle_param < 3) {
           int pts[2];
           if (cycle_param < 2) { pts[0] = 1; pts[1] = -1; } else { pts[0] = -1; pts[1] = 1; }
@@ -821,7 +863,7 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       // When the coarse level's first down sweep is l1-Jacobi (weight 1) from
       // the zero guess, u_c = 0 + F_c/l1 is formed by the restriction itself.
       const bool into_agg = agg_level_ >= 0 && coarse == agg_level_;
-      const bool fuse_zg = !into_agg && coarse != nl - 1 && prm.num_sweeps[1] >= 1 &&
+      const bool fuse_zg = !into_agg && coarse != nl - 1 && prm.num_sweeps[1] >= 1 && prm.relax_order != 1 &&
                            (prm.relax_type[1] == 18 || prm.relax_type[1] == 7) && prm.relax_weight == 1.0 &&
                            lev_[coarse].l1 != nullptr;
       if (fuse_zg) {
@@ -1021,12 +1063,16 @@ int pcg_solve(DevAMG* amg, int n, const MatvecFn& Aop, const PCGParams& prm, con
     const double gamma = hs[0];
     if (flag != 0.0) {  // zero <s,p> or subnormal alpha: x, r untouched (alpha = 0)
       if (i == 1) i_prod = i_prod_0;
+      ret = HYPRE_ERROR_CONV_CODE;  // pcg.c:516-526 hypre_error_w_msg(HYPRE_ERROR_CONV, ...)
       break;
     }
     i_prod = prm.two_norm ? hs[5] : gamma;
     if (prm.print_level > 1) fprintf(stderr, "% 5d    %e    %e\n", i, std::sqrt(i_prod), std::sqrt(i_prod / bi_prod));
     if (i_prod / bi_prod < eps) break;
-    if (!(gamma > 2.2250738585072014e-308)) break;
+    if (!(gamma > 2.2250738585072014e-308)) {  // pcg.c:680 "Subnormal gamma value"
+      ret = HYPRE_ERROR_CONV_CODE;
+      break;
+    }
     HVE_HIP(launch_pcg_beta(sc, s));
     HVE_HIP(launch_pcg_p(n, sc + 4, sv, p, s));  // p = beta p + s
   }

@@ -59,9 +59,21 @@ struct DevSell {
   // policy: AMGParams::sell_policy
   void upload(const CSR& A, const std::vector<int>& rowmap = {}, int policy = 0);
   void release();
-  size_t bytes() const { return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * (vidx ? 3 : vidx16 ? 4 : dcol ? 10 : 12) +
-                         (dcol ? (size_t)nnz_pad / 16 : 0) + (rowmap ? (size_t)nrows * 4 : 0) +
-                         (rowlen ? (size_t)nslices * 256 : 0); }
+  int64_t ndict = 0;  // dictionary layout: stored distinct-column entries
+  // Bytes one application streams from the stored operator (vectors excluded):
+  // per stored slot its column (32-bit, 16-bit delta or 16-bit local column)
+  // and value (8 B, or an 8/16-bit index into the LDS value table), plus slice
+  // pointers, slot bases, dictionaries, row maps and row lengths.
+  size_t bytes() const {
+    const size_t colb = dcol || col16 ? 2 : 4;
+    const size_t valb = vidx ? 1 : vidx16 ? 2 : 8;
+    size_t b = (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * (colb + valb);
+    if (dcol) b += (size_t)nnz_pad / 16;  // 4 B base per (slice, slot)
+    if (col16) b += (size_t)ndict * 4 + (size_t)((nslices + dict_group - 1) / dict_group + 1) * 4;
+    if (rowmap) b += (size_t)nrows * 4;
+    if (rowlen) b += (size_t)nrows * 4;
+    return b;
+  }
 };
 
 // Rows of one operator a rank applies, split by whether they read halo values.
@@ -113,6 +125,10 @@ struct DevLevel {
   double* l1 = nullptr;
   bool l1_fly = false;  // the l1-Jacobi kernels form the l1 norms from A's entries
   int* cf = nullptr;
+  // C/F-ordered l1-Jacobi (relax 18, relax_order 1): the CF marker with rows
+  // whose diagonal is zero set to 0, which no point class selects
+  // (par_relax_more.c:1135 skips them)
+  int* cf_l1 = nullptr;
   double* F = nullptr;
   double* U[2] = {nullptr, nullptr};  // n + hu.n_halo each
   double* V = nullptr;                // n + hv.n_halo

@@ -1358,6 +1358,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
+  if (prm.agg_num_levels > 0)
+    throw std::runtime_error("aggressive coarsening (agg_num_levels > 0) is not available in this build");
   int coarsen_type = prm.coarsen_type;
   H.lev.emplace_back();
   H.lev[0].A = A0;

@@ -178,6 +178,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGSetGsRankStarts", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
+    ("hypreve_BenchLevelOpStoredBytes", _i, [_p, _i, _i, _pd]),
     ("hypreve_BenchStream", _i, [_i, C.c_int64, _i, _pd]),
     ("hypreve_DeviceSynchronize", _i, []),
     ("hypreve_BuildInfo", C.c_char_p, []),
@@ -503,6 +504,12 @@ class BoomerAMG:
         check(lib().hypreve_BenchLevelOp(self.h, level, which, reps, C.byref(ms), C.byref(by), C.byref(pz)),
               "BenchLevelOp")
         return ms.value, by.value, pz.value
+
+    def level_op_stored_bytes(self, level, which=0):
+        """Bytes one bench_level_op launch streams in the stored layout (+ vectors)."""
+        by = C.c_double()
+        check(lib().hypreve_BenchLevelOpStoredBytes(self.h, level, which, C.byref(by)), "BenchLevelOpStoredBytes")
+        return by.value
 
     def bench_fine_spmv(self, reps=20):
         ms, by = C.c_double(), C.c_double()

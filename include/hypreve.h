@@ -218,7 +218,9 @@ HYPRE_Int hypreve_ParVectorCopyFromHost(HYPRE_ParVector v, const HYPRE_Real *hos
 HYPRE_Int hypreve_ParVectorSetRandomValues(HYPRE_ParVector v, HYPRE_Int seed); /* HYPRE_ParVectorSetRandomValues */
 
 /* Number of contiguous row blocks used by the hybrid Gauss-Seidel smoothers
- * (reference: OMP_NUM_THREADS on the CPU path). 0 = automatic. */
+ * (reference: OMP_NUM_THREADS on the CPU path). 0 = automatic (the default):
+ * one block per 4096 local level-0 rows, resolved at Setup; 1 reproduces the
+ * reference's single-thread sweep. */
 HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_blocks);
 /* Device layout / row loop of the hierarchy's SELL operators (takes effect at
  * Setup): 0 automatic, 1 padded lane-per-row, 2 jagged lane-per-row, 3 padded
@@ -298,6 +300,10 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_bl
  * as restriction): average ms over reps, algorithmic bytes, padded entries. */
 HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,
                                HYPRE_Real *avg_ms, HYPRE_Real *bytes, HYPRE_Real *padded_nnz);
+/* Bytes the same launch streams in the operator's stored (compressed) layout,
+ * vectors included. */
+HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,
+                                          HYPRE_Real *bytes);
 /* Read-only streaming kernel (elem_bytes 2, 4, 8 or 16): FETCH_SIZE calibration. */
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real *avg_ms);
 HYPRE_Int hypreve_DeviceSynchronize(void);

@@ -162,9 +162,26 @@ int orc_relax(const orc_csr *A, const double *f, const int *cf, int relax_type,
       }
       return 0;
     }
-    case 7:   /* par_relax.c:3463 Jacobi through the matvec (l1 = diag) */
-    case 18: { /* ams.c:41 hypre_ParCSRRelax type 1 (l1-scaled Jacobi) */
-      if (relax_points != 0) return 1; /* CF l1-Jacobi not restated */
+    case 18:
+      if (relax_points != 0) {
+        /* par_relax_more.c:991 hypre_ParCSRRelax_L1_Jacobi (par_cycle.c:398-415,
+         * relax_order 1): Vtemp = u; rows of the class relax_points with a
+         * nonzero diagonal: res = f - sum_j a_ij Vtemp_j (stored order, the
+         * diagonal included), u_i += (w*res)/l1_i.  An empty row is skipped
+         * (the reference would read the next row's first entry). */
+        memcpy(vtemp, u, sizeof(double) * (size_t)n);
+#pragma omp parallel for schedule(static) if (n > 8192)
+        for (int i = 0; i < n; i++) {
+          if (cf[i] != relax_points || Ai[i] == Ai[i + 1] || Aa[Ai[i]] == 0.0) continue;
+          double res = f[i];
+          for (int k = Ai[i]; k < Ai[i + 1]; k++) res -= Aa[k] * vtemp[Aj[k]];
+          u[i] += (relax_weight * res) / l1[i];
+        }
+        return 0;
+      }
+      /* fall through: ams.c:41 hypre_ParCSRRelax type 1 (l1-scaled Jacobi) */
+    case 7: { /* par_relax.c:3463 Jacobi through the matvec (l1 = diag); relax_points
+               * is ignored (a C/F-ordered call runs a full sweep) */
       memcpy(vtemp, f, sizeof(double) * (size_t)n);
       orc_matvec(-relax_weight, A, u, relax_weight, vtemp, vtemp);
 #pragma omp parallel for schedule(static) if (n > 8192)
@@ -293,12 +310,15 @@ int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
         /* par_cycle.c:445 scaled Chebyshev: Aux_F, Aux_U, Vtemp, Ztemp */
         err = orc_cheby(&amg->A[level], F[level], amg->cheby_ds[level], amg->cheby_coefs[level],
                         amg->cheby_order, amg->cheby_scale, U[level], vtemp, ztemp);
-      } else if (relax_type == 18 || relax_type == 7) {
+      } else if (relax_type == 18 && !(amg->relax_order == 1 && cycle_param < 3)) {
         err = orc_relax(&amg->A[level], F[level], amg->cf[level], relax_type, 0,
                         amg->relax_weight, amg->omega, amg->l1[level], amg->num_blocks,
                         U[level], vtemp, ztemp);
       } else {
-        /* hypre_BoomerAMGRelaxIF (par_relax_interface.c:19) */
+        /* relax 18 with relax_order 1 (par_cycle.c:398-415): C/F-ordered
+         * hypre_ParCSRRelax_L1_Jacobi twice; every other type through
+         * hypre_BoomerAMGRelaxIF (par_relax_interface.c:19), which for relax 7
+         * means two full sweeps (par_relax.c:3463 ignores relax_points) */
         if (amg->relax_order == 1 && cycle_param < 3) {
           int pts[2];
           if (cycle_param < 2) { pts[0] = 1; pts[1] = -1; } else { pts[0] = -1; pts[1] = 1; }

@@ -60,12 +60,19 @@ def test_single_cycle_bitwise(gpu, orc, n3, relax, coarsen):
     assert np.array_equal(u.get(), uo)
 
 
-@pytest.mark.parametrize("relax,coarsen", [(18, 8), (0, 8), (18, 10), (7, 10)])
-def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen):
-    """relax_order 1 (C points, then F points on the way down; F then C up):
-    the CF-selective row kernels on padded and jagged operators."""
+@pytest.mark.parametrize("relax,coarsen,wt", [(18, 8, 1.0), (0, 8, 1.0), (18, 10, 1.0), (7, 10, 1.0),
+                                              (18, 8, 0.8), (7, 8, 1.0)])
+def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen, wt):
+    """relax_order 1 (C points, then F points on the way down; F then C up).
+    relax 18: hypre_ParCSRRelax_L1_Jacobi per point class with the C/F-restricted
+    l1 norms (par_cycle.c:398-415, par_relax_more.c:991); relax 7: two full
+    sweeps (RelaxIF, par_relax.c:3463 ignores relax_points); relax 0: C/F Jacobi.
+    The oracle's C/F sweep is itself checked against the formula in
+    tests/test_oracle_relax.py.  Control: the same hierarchy with relax_order 0
+    gives different bits, so the C/F path is really taken."""
     hv = gpu
-    A, amg, O = setup_pair(hv, orc, (26, 22, 19), coarsen_type=coarsen, relax_type=relax, relax_order=1)
+    A, amg, O = setup_pair(hv, orc, (26, 22, 19), coarsen_type=coarsen, relax_type=relax, relax_order=1,
+                           relax_wt=wt)
     n = A.n
     rng = np.random.default_rng(17)
     f_h = rng.standard_normal(n)
@@ -76,6 +83,20 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen):
     uo = u0.copy()
     O.cycle(f_h, uo)
     assert np.array_equal(u.get(), uo)
+    O.s.relax_order = 0
+    uc = u0.copy()
+    O.cycle(f_h, uc)
+    assert not np.array_equal(uc, uo)
+    # a solve with the fused solve-loop kernels switched off by relax_order 1
+    b = hv.ParVector(n, f_h)
+    x = hv.ParVector(n, np.zeros(n))
+    amg.set(tol=1e-7, max_iter=30)
+    it, rr = amg.solve(A, b, x)
+    O.s.relax_order = 1
+    xo = np.zeros(n)
+    st = O.solve(f_h, xo, 1e-7, 30)
+    assert it == st["iterations"]
+    assert np.array_equal(x.get(), xo)
 
 
 @pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9])
