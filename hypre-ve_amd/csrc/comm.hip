@@ -44,6 +44,23 @@ HYPRE_Int hypreve_CommCreate(HYPRE_Int rank, HYPRE_Int size, const void* nccl_id
   return 0;
 }
 
+HYPRE_Int hypreve_CommCreateShm(HYPRE_Int rank, HYPRE_Int size, const char* shm_name, HYPRE_Comm* comm) {
+  if (!comm || !shm_name || size < 1 || rank < 0 || rank >= size) return HYPRE_ERROR_ARG;
+  auto* c = new hypreve_comm_struct;
+  c->rank = rank;
+  c->size = size;
+  if (size > 1) {
+    try {
+      c->dc = make_shm_comm(rank, size, shm_name);
+    } catch (...) {
+      delete c;
+      return HYPRE_ERROR_GENERIC;
+    }
+  }
+  *comm = c;
+  return 0;
+}
+
 HYPRE_Int hypreve_CommCreateLoopback(HYPRE_Int size, HYPRE_Comm* comms) {
   if (!comms || size < 1) return HYPRE_ERROR_ARG;
   try {

@@ -55,6 +55,10 @@ std::unique_ptr<DevComm> make_rccl_comm(int rank, int size, const void* id128);
 // `size` communicators sharing one in-process hub; rank r must only be used
 // from one host thread at a time, and every rank from its own thread.
 std::vector<std::unique_ptr<DevComm>> make_loopback_comms(int size);
+// Host-staged transport over the POSIX shared-memory segment `name` (rank 0
+// creates it): `size` processes on one host, e.g. several ranks on one GPU,
+// where RCCL refuses.  Exchanges and all-reduces synchronise the stream.
+std::unique_ptr<DevComm> make_shm_comm(int rank, int size, const char* name);
 
 }  // namespace hve
 

@@ -151,6 +151,7 @@ SIGNATURES = [
     ("hypreve_CommDestroy", _i, [_p]),
     ("hypreve_CommSelfTest", _i, [_p]),
     ("hypreve_CommCreateLoopback", _i, [_i, C.POINTER(_p)]),
+    ("hypreve_CommCreateShm", _i, [_i, _i, C.c_char_p, C.POINTER(_p)]),
     ("hypreve_ParCSRMatrixCreateFromCSR", _i, [_p, _i, _i, _i, _pi, _pi, _pd, C.POINTER(_p)]),
     ("hypreve_ParVectorDeviceData", _p, [_p]),
     ("hypreve_ParVectorLocalSize", _i, [_p]),
@@ -236,6 +237,14 @@ class Comm:
         hs = (_p * size)()
         check(lib().hypreve_CommCreateLoopback(size, hs), "CommCreateLoopback")
         return [cls(_p(hs[r]), r, size) for r in range(size)]
+
+    @classmethod
+    def shm(cls, rank, size, name: str):
+        """One process of `size` on this host over the shared-memory segment
+        `name` (host-staged; several processes may share one GPU)."""
+        h = _p()
+        check(lib().hypreve_CommCreateShm(rank, size, name.encode(), C.byref(h)), "CommCreateShm")
+        return cls(h, rank, size)
 
     def self_test(self):
         """Collective transport check (exchange incl. self, all-reduce,

@@ -203,6 +203,13 @@ HYPRE_Int hypreve_CommSelfTest(HYPRE_Comm comm);
  * to check the partitioned solve on a single GPU (RCCL refuses two ranks on
  * one device); not a production transport. */
 HYPRE_Int hypreve_CommCreateLoopback(HYPRE_Int size, HYPRE_Comm *comms);
+/* Communicator of `size` processes on one host over the POSIX shared-memory
+ * segment `shm_name` (rank 0 creates and finally unlinks it; every rank passes
+ * the same name).  Host-staged: each exchange drains the stream and copies
+ * through host memory.  It lets several processes share one GPU, which RCCL
+ * refuses, so the process-per-rank path can be tested on a one-GPU box; not a
+ * production transport. */
+HYPRE_Int hypreve_CommCreateShm(HYPRE_Int rank, HYPRE_Int size, const char *shm_name, HYPRE_Comm *comm);
 
 /* Direct construction of a local ParCSR block from host CSR arrays (global
  * column indices), equivalent to IJ create/set/assemble in one call. */
