@@ -54,13 +54,13 @@ def committed_traffic(n, kname):
     name it matched must contain both halves of kname around the batch width).
     Counters need their own profiler passes, so the bench reports the committed
     measurement of the same kernel and grid."""
-    best = None
-    for rnd in sorted(os.listdir(PROFILE_DIR)) if os.path.isdir(PROFILE_DIR) else []:
-        p = os.path.join(PROFILE_DIR, rnd, f"pmc_traffic_{n}.json")
-        if os.path.exists(p):
-            best = p
-    if not best:
+    found = []
+    for dirpath, _, files in os.walk(PROFILE_DIR):
+        if f"pmc_traffic_{n}.json" in files:
+            found.append(os.path.join(dirpath, f"pmc_traffic_{n}.json"))
+    if not found:
         return None
+    best = sorted(found)[-1]  # profiles/rNN/<seq>_<name>/: the newest measurement
     with open(best) as f:
         d = json.load(f)
     names = d.get("kernel_names", [])
