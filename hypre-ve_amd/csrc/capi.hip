@@ -663,6 +663,12 @@ AMG_SET(MaxRowSum, max_row_sum, HYPRE_Real)
 AMG_SET(CoarsenType, coarsen_type, HYPRE_Int)
 AMG_SET(MeasureType, measure_type, HYPRE_Int)
 AMG_SET(AggNumLevels, agg_num_levels, HYPRE_Int)
+AMG_SET(AggInterpType, agg_interp_type, HYPRE_Int)
+AMG_SET(AggTruncFactor, agg_trunc_factor, HYPRE_Real)
+AMG_SET(AggP12TruncFactor, agg_P12_trunc_factor, HYPRE_Real)
+AMG_SET(AggPMaxElmts, agg_P_max_elmts, HYPRE_Int)
+AMG_SET(AggP12MaxElmts, agg_P12_max_elmts, HYPRE_Int)
+AMG_SET(NumPaths, num_paths, HYPRE_Int)
 AMG_SET(InterpType, interp_type, HYPRE_Int)
 AMG_SET(TruncFactor, trunc_factor, HYPRE_Real)
 AMG_SET(PMaxElmts, P_max_elmts, HYPRE_Int)
@@ -698,6 +704,7 @@ HYPRE_Int HYPRE_BoomerAMGSetRelaxType(HYPRE_Solver s, HYPRE_Int relax_type) {
   CHECK_ARG(relax_type >= 0, 2);
   for (int i = 0; i < 3; ++i) s->prm.relax_type[i] = relax_type;
   s->prm.relax_type[3] = 9;
+  s->prm.user_relax_type = relax_type;  // par_amg.c:2101-2104
   return 0;
 }
 HYPRE_Int HYPRE_BoomerAMGSetCycleRelaxType(HYPRE_Solver s, HYPRE_Int relax_type, HYPRE_Int k) {
@@ -732,6 +739,17 @@ HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver s, HYPRE_Int nranks, con
     s->gs_rank_starts.assign(starts, starts + nranks + 1);
   }
   return 0;
+}
+// Tuning: re-key the row-block traversal of the built device hierarchy with
+// nbands bands of the grid's y extent (0: natural order; default at Setup:
+// HVE_BLOCK_ORDER, 8).  Only the visiting order of row blocks changes.
+HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands) {
+  CHECK_ARG(s && s->kind == KIND_AMG && s->dev && s->dev->built(), 1);
+  CHECK_ARG(nbands >= 0, 2);
+  API_BEGIN
+  s->dev->set_block_bands(s->RH, nbands);
+  HVE_HIP(hipDeviceSynchronize());
+  API_END
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
@@ -1155,7 +1173,7 @@ HYPRE_Int hypreve_BoomerAMGGetRelaxInfo(HYPRE_Solver s, HYPRE_Int* rt, HYPRE_Int
   const AMGParams& p = s->H.lev.empty() ? (s->RH.lev.empty() ? s->prm : s->RH.prm) : s->H.prm;
   for (int i = 0; i < 4; ++i) { if (rt) rt[i] = p.relax_type[i]; if (ns) ns[i] = p.num_sweeps[i]; }
   if (w) { w[0] = p.relax_weight; w[1] = p.outer_weight; }
-  if (misc) { misc[0] = p.relax_order; misc[1] = p.cycle_type; misc[2] = p.num_blocks; }
+  if (misc) { misc[0] = p.relax_order; misc[1] = p.cycle_type; misc[2] = p.num_blocks; misc[3] = p.user_relax_type; }
   return 0;
 }
 HYPRE_Int hypreve_BoomerAMGGetKernelStats(HYPRE_Solver s, HYPRE_Real* stats, HYPRE_Int n) {

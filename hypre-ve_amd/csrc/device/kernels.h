@@ -28,6 +28,12 @@ struct SellView {
   const unsigned short* vidx16 = nullptr;  // delta layout: 16-bit value indices (val unused)
   const double* vtab = nullptr;         // the operator's distinct values
   int nvtab = 0;
+  // Traversal order of the workgroup row blocks (logical block -> stored row
+  // block, nullptr = identity): blocks are visited so that each XCD streams a
+  // compact region of the grid whose x window stays in its L2.  Only the order
+  // changes, not any row's arithmetic.
+  const int* blk_map = nullptr;
+  int nblk = 0;
 };
 
 enum : int {

@@ -74,12 +74,21 @@ struct SpArgs {
   const unsigned short* __restrict__ vidx16; // the same, 16-bit
   const double* __restrict__ vtab;           // distinct values (<= 256)
   int nvtab;
+  const int* __restrict__ blk_map;           // logical -> stored row block (nullptr: identity)
+  int nblk;                                  // entries of blk_map
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double w;                       // relax weight / alpha
   double temp;                    // beta/alpha for OP_GENERAL
   int relax_points;
 };
+
+// Logical workgroup block -> stored row block (SpArgs::blk_map): the
+// locality-ordered traversal; blocks past the map (grid padding) keep their
+// index and fall past the last row.
+__device__ __forceinline__ int map_block(const SpArgs& p, int lb) {
+  return (p.blk_map != nullptr && lb < p.nblk) ? p.blk_map[lb] : lb;
+}
 
 // Row accumulation in stored order, loads batched B entries at a time: the B
 // column and value loads of a batch are issued together, then the B gathers of
@@ -339,7 +348,7 @@ __device__ __forceinline__ void sell_row_op(const SpArgs& p, const double* vt, i
 
 template <int OP, bool CFSEL, int B, bool PIPE, bool NT, bool JAG>
 __global__ void __launch_bounds__(256) k_sell(SpArgs p) {
-  const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  const int lb = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
   sell_row_op<OP, CFSEL, B, PIPE, NT, JAG, ValF64>(p, nullptr, lb * 256 + (int)threadIdx.x);
 }
 
@@ -357,7 +366,7 @@ __global__ void __launch_bounds__(256) k_sell_vt(SpArgs p) {
   const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
   const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
   for (int rb = r0 + (int)(blockIdx.x >> 3); rb < r1; rb += per_wg)
-    sell_row_op<OP, CFSEL, B, true, true, JAG, ValT16>(p, vt, rb * 256 + (int)threadIdx.x);
+    sell_row_op<OP, CFSEL, B, true, true, JAG, ValT16>(p, vt, map_block(p, rb) * 256 + (int)threadIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -553,7 +562,7 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
   const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
   const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
   for (int rb = r0 + (int)(blockIdx.x >> 3); rb < r1; rb += per_wg)
-    delta_row<OP, CFSEL, B, NT, VI>(p, vt, rb * 256 + (int)threadIdx.x);
+    delta_row<OP, CFSEL, B, NT, VI>(p, vt, map_block(p, rb) * 256 + (int)threadIdx.x);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -561,7 +570,7 @@ __global__ void __launch_bounds__(256) k_sell_wide(SpArgs p) {
   constexpr int KCH = 32;       // entries per row and chunk: 64 x 32 products = 16 KiB of LDS
   constexpr int PER = KCH / 4;  // products per thread and chunk
   __shared__ double prod[kWave * KCH];
-  const int slice = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  const int slice = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
   if (slice * kWave >= p.nrows) return;  // whole workgroup past the end
   const int tid = threadIdx.x;
   const int beg = p.slice_ptr[slice];
@@ -636,7 +645,7 @@ template <int OP, bool CFSEL, bool NT>
 __global__ void __launch_bounds__(256) k_sell_pw(SpArgs p) {
   constexpr int KC = 16;  // entries per row and chunk: 64 x 16 products, 8 KiB per wave
   __shared__ double prod[4][kWave * KC];
-  const int lb = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  const int lb = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
   const int row = lb * 256 + threadIdx.x;
   const int lane = threadIdx.x & (kWave - 1);
   const int slice = row >> 6;
@@ -736,7 +745,7 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   extern __shared__ double xl[];
   // G waves per workgroup share one dictionary (the distinct columns of G
   // consecutive slices); wave w runs slice group * G + w.
-  const int group = xcd_logical_block(blockIdx.x, p.nblocks_pad);
+  const int group = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
   if (group * G * kWave >= p.nrows) return;  // the whole workgroup is past the end
   const int lane = threadIdx.x & (kWave - 1);
   const int slice = group * G + (threadIdx.x >> 6);
@@ -1093,6 +1102,8 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   a.vidx16 = M.vidx16;
   a.vtab = M.vtab;
   a.nvtab = M.nvtab;
+  a.blk_map = M.blk_map;
+  a.nblk = M.nblk;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
   a.nblocks_pad = blocks_pad8(M.nrows);
   a.x = x; a.b = b; a.l1 = l1; a.cf = cf; a.y = y; a.y2 = y2; a.w = w; a.temp = temp; a.relax_points = relax_points;

@@ -3,6 +3,7 @@
 // arithmetic step runs in a HIP kernel (kernels.hip) -- there is no host path.
 #include <hip/hip_runtime.h>
 
+#include <climits>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -46,7 +47,29 @@ static int sell_valtab_env() {
   return v;
 }
 
-void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy) {
+void DevSell::set_block_order(const std::vector<int>& stored_to_local, const std::vector<int64_t>& key) {
+  if (key.empty() || nrows <= 0) return;
+  // the row block one workgroup of the chosen loop runs (kernels.hip launch_sell)
+  const int unit = col16 ? 64 * dict_group : (dcol || vidx16) ? 256 : (wide && !rowlen) ? 64 : 256;
+  const int nb = (nrows + unit - 1) / unit;
+  std::vector<int64_t> bk(nb);
+  for (int b = 0; b < nb; ++b) {
+    const int s = b * unit;
+    const int loc = stored_to_local.empty() ? s : stored_to_local[s];
+    bk[b] = (loc >= 0 && loc < (int)key.size()) ? key[loc] : (int64_t)loc;
+  }
+  std::vector<int> ord(nb);
+  for (int b = 0; b < nb; ++b) ord[b] = b;
+  std::stable_sort(ord.begin(), ord.end(), [&](int a, int b) { return bk[a] < bk[b]; });
+  bool ident = true;
+  for (int b = 0; b < nb && ident; ++b) ident = ord[b] == b;
+  if (ident) return;
+  if (blk_map) (void)hipFree(blk_map);
+  blk_map = dupload(ord.data(), ord.size());
+  nblk = nb;
+}
+
+void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy, const std::vector<int64_t>* key) {
   release();
   std::vector<int> sp, col, perm;
   std::vector<double> val;
@@ -188,6 +211,8 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy)
         for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
         if (!ident) rowmap = dupload(rowmap_h.data(), rowmap_h.size());
       }
+      stored_map = rowmap_h;
+      if (key) set_block_order(rowmap_h, *key);
       return;
     }
   plain:
@@ -241,6 +266,8 @@ dict:
       bool ident = true;
       for (int i = 0; i < A.nrows && ident; ++i) ident = map[i] == i;
       if (!ident) rowmap = dupload(map.data(), map.size());
+      if (!ident) stored_map = map;
+      if (key) set_block_order(map, *key);
       return;
     }
     perm.clear();  // a slice has too many distinct columns: fall back
@@ -294,6 +321,8 @@ dict:
   bool ident = true;
   for (int i = 0; i < A.nrows && ident; ++i) ident = map[i] == i;
   if (!ident) rowmap = dupload(map.data(), map.size());
+  if (!ident) stored_map = map;
+  if (key) set_block_order(map, *key);
 }
 // A rank operator's rows in local order (interior and boundary merged, each
 // row's entries in stored order, columns in the [local | halo] space).
@@ -360,6 +389,11 @@ void DevSell::release() {
   if (vidx) (void)hipFree(vidx);
   if (vidx16) (void)hipFree(vidx16);
   if (vtab) (void)hipFree(vtab);
+  if (blk_map) (void)hipFree(blk_map);
+  blk_map = nullptr;
+  nblk = 0;
+  stored_map.clear();
+  stored_map.shrink_to_fit();
   dcol = nullptr; slot_base = nullptr; vidx = nullptr; vidx16 = nullptr; vtab = nullptr; nvtab = 0;
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
   col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1; ndict = 0;
@@ -394,8 +428,8 @@ void DevGs::release() {
   max_levels = 0;
 }
 
-void DevOp::upload(const RankOp& op, int policy) {
-  in.upload(op.interior, op.map_int, policy);
+void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key) {
+  in.upload(op.interior, op.map_int, policy, key);
   bd.upload(op.boundary, op.map_bnd, policy);
   nrows_local = op.nrows_local;
 }
@@ -479,6 +513,75 @@ void DevAMG::init_workspace(int n, DevComm* comm) {
   ws_n_ = n;
 }
 
+// Plane and line strides of a structured-grid operator, read off its column
+// offsets: over a sample of rows, the most frequent largest offset (the plane,
+// nx*ny) and smallest offset beyond 1 (the line, nx).  False when the operator
+// shows no 3-D structure worth a locality order.
+static bool grid_strides(const CSR& A, const std::vector<int>& map, int n_loc, int64_t* plane, int64_t* line) {
+  const int n = A.nrows;
+  if (n_loc < (1 << 20) || n < n_loc / 2) return false;
+  std::map<int64_t, int> hmax, hmin;
+  const int step = std::max(1, n / 20000);
+  for (int i = 0; i < n; i += step) {
+    const int64_t g = map.empty() ? i : map[i];  // local row
+    int64_t mx = 0, mn = INT64_MAX;
+    for (int k = A.i[i]; k < A.i[i + 1]; ++k) {
+      if (A.j[k] >= n_loc) continue;  // halo column
+      const int64_t d = (int64_t)A.j[k] - g;
+      if (d > mx) mx = d;
+      if (d > 1 && d < mn) mn = d;
+    }
+    if (mx > 0) ++hmax[mx];
+    if (mn != INT64_MAX) ++hmin[mn];
+  }
+  auto mode = [](const std::map<int64_t, int>& h) {
+    int64_t best = 0;
+    int c = -1;
+    for (const auto& kv : h)
+      if (kv.second > c) { best = kv.first; c = kv.second; }
+    return best;
+  };
+  *plane = mode(hmax);
+  *line = mode(hmin);
+  return *line > 1 && *plane >= 8 * *line && *plane >= (1 << 15) && (int64_t)n_loc >= 4 * *plane;
+}
+
+// Locality traversal keys per level (interior rows of every non-replicated
+// level): a row's level-0 point f (C points map down through the CF markers)
+// keyed as (XCD band of f's y coordinate, f).  Each XCD then streams one band
+// of the grid through all its planes, so the x window that the neighbouring
+// planes share stays in its 4 MiB L2 even when a whole plane does not (512^3:
+// 2 MiB of x per plane).  HVE_BLOCK_ORDER=0 keeps the natural order.
+static void locality_keys(const RankHierarchy& R, int agg_level, int nbands, std::vector<std::vector<int64_t>>& keys) {
+  keys.assign(R.lev.size(), {});
+  if (nbands <= 0 || R.lev.empty()) return;
+  const RankLevel& L0 = R.lev[0];
+  int64_t plane = 0, line = 0;
+  if (!grid_strides(L0.A.interior, L0.A.map_int, L0.n_loc, &plane, &line)) return;
+  const int64_t ny = std::max<int64_t>(1, plane / line);
+  const int64_t n0 = L0.n_loc;
+  std::vector<int64_t> f(n0);
+  for (int64_t i = 0; i < n0; ++i) f[i] = i;
+  for (size_t l = 0; l < R.lev.size(); ++l) {
+    if (agg_level >= 0 && (int)l >= agg_level) break;
+    const RankLevel& L = R.lev[l];
+    if ((int64_t)f.size() != L.n_loc) break;
+    std::vector<int64_t>& k = keys[l];
+    k.resize(L.n_loc);
+    for (int i = 0; i < L.n_loc; ++i) {
+      const int64_t y = (f[i] % plane) / line;
+      const int64_t band = std::min<int64_t>(nbands - 1, y * nbands / ny);
+      k[i] = band * n0 + f[i];
+    }
+    if (L.cf.empty()) break;
+    std::vector<int64_t> fc;
+    fc.reserve(L.n_loc / 2);
+    for (int i = 0; i < L.n_loc && i < (int)L.cf.size(); ++i)
+      if (L.cf[i] == 1) fc.push_back(f[i]);
+    f.swap(fc);
+  }
+}
+
 void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   const int n0 = R.lev.empty() ? 0 : R.lev[0].n_loc;
   init_workspace(n0, comm);
@@ -487,17 +590,26 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   lev_.resize(nl);
   agg_level_ = comm_ ? R.agg_level : -1;
   agg_starts_ = R.agg_starts;
+  std::vector<std::vector<int64_t>> keys;
+  static const int nbands_env = [] {
+    const char* e = getenv("HVE_BLOCK_ORDER");
+    return e ? atoi(e) : 8;  // bands of the grid's y extent; 0 = natural order
+  }();
+  locality_keys(R, agg_level_, nbands_env, keys);
   for (int l = 0; l < nl; ++l) {
     const RankLevel& L = R.lev[l];
     DevLevel& D = lev_[l];
     D.n = L.n_loc;
     D.first = L.first;
     D.n_glob = L.n_glob;
-    D.A.upload(L.A, prm.sell_policy);
+    // A_l and P_l rows are level-l rows; R_l rows are level-(l+1) rows
+    const std::vector<int64_t>* kl = keys[l].empty() ? nullptr : &keys[l];
+    const std::vector<int64_t>* kc = (l + 1 < nl && !keys[l + 1].empty()) ? &keys[l + 1] : nullptr;
+    D.A.upload(L.A, prm.sell_policy, kl);
     D.hu.upload(L.hu);
     if (l < nl - 1) {
-      D.P.upload(L.P, prm.sell_policy);
-      D.R.upload(L.R, prm.sell_policy);
+      D.P.upload(L.P, prm.sell_policy, kl);
+      D.R.upload(L.R, prm.sell_policy, kc);
       D.hv.upload(L.hv);
     }
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
@@ -536,8 +648,9 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   // (num_blocks = hypre's thread count: row blocks of each level).
   {
     bool fwd = false, bwd = false;
-    for (int c = 0; c < 4; ++c) {
-      const int rt = prm.relax_type[c];
+    for (int c = 0; c < 5; ++c) {
+      // c == 4: the one-level smoother (par_cycle.c:296-300)
+      const int rt = c < 4 ? prm.relax_type[c] : (nl == 1 ? (prm.user_relax_type >= 0 ? prm.user_relax_type : 6) : -1);
       fwd = fwd || rt == 3 || rt == 6 || rt == 8 || rt == 13;
       bwd = bwd || rt == 4 || rt == 6 || rt == 8 || rt == 14;
     }
@@ -578,6 +691,39 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   }
   if (comm_) use_graph_ = false;  // communication stays outside graph capture in this build
   HVE_HIP(hipDeviceSynchronize());
+}
+
+// Re-key the traversal of every interior operator with `nbands` bands (0:
+// natural order) on the built hierarchy (tuning: the operators stay in place).
+void DevAMG::set_block_bands(const RankHierarchy& R, int nbands) {
+  std::vector<std::vector<int64_t>> keys;
+  locality_keys(R, agg_level_, nbands, keys);
+  const int nl = (int)lev_.size();
+  for (int l = 0; l < nl; ++l) {
+    DevLevel& D = lev_[l];
+    const RankLevel& L = R.lev[l];
+    const std::vector<int64_t> none;
+    const std::vector<int64_t>& kl = keys[l];
+    const std::vector<int64_t>& kc = l + 1 < nl ? keys[l + 1] : none;
+    auto redo = [](DevSell& M, const std::vector<int64_t>& k, const std::vector<int>& map) {
+      if (M.blk_map) (void)hipFree(M.blk_map);
+      M.blk_map = nullptr;
+      M.nblk = 0;
+      if (!k.empty() && M.stored_map.size() == (size_t)M.nrows) M.set_block_order(M.stored_map, k);
+      else if (!k.empty() && !M.rowmap) M.set_block_order(map, k);
+    };
+    redo(D.A.in, kl, {});
+    if (l < nl - 1) {
+      redo(D.P.in, kl, {});
+      redo(D.R.in, kc, {});
+    }
+    (void)L;
+  }
+  graphs_clear();
+}
+void DevAMG::graphs_clear() {
+  for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+  graphs_.clear();
 }
 
 void DevAMG::dot(int n, const double* x, const double* y, double* out, hipStream_t s) {
@@ -820,7 +966,7 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       relax_type = prm.relax_type[cycle_param];
     } else {
       num_sweep = 1;
-      relax_type = prm.relax_type[0] >= 0 ? prm.relax_type[0] : 6;
+      relax_type = prm.user_relax_type >= 0 ? prm.user_relax_type : 6;  // par_cycle.c:296-300
     }
     for (int j = 0; j < num_sweep; ++j) {
       ops += (double)lev_[level].A.nnz();

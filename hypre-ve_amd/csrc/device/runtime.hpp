@@ -48,16 +48,25 @@ struct DevSell {
   int pipe = 0;
   int wide = 0;
   int pw = 0;
+  int* blk_map = nullptr;  // locality traversal of the workgroup row blocks (SellView::blk_map)
+  int nblk = 0;
+  std::vector<int> stored_map;  // host copy of the stored row -> local row map (empty: identity)
   SellView view() const {
     SellView v;
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
     v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group;
     v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vidx16 = vidx16; v.vtab = vtab; v.nvtab = nvtab;
+    v.blk_map = blk_map; v.nblk = nblk;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map
   // policy: AMGParams::sell_policy
-  void upload(const CSR& A, const std::vector<int>& rowmap = {}, int policy = 0);
+  // key: per local row, the sort key of the locality traversal (nullptr: natural order)
+  void upload(const CSR& A, const std::vector<int>& rowmap = {}, int policy = 0,
+              const std::vector<int64_t>* key = nullptr);
+  // Workgroup row blocks visited in ascending key of their first row
+  // (stored_to_local: stored row -> local row, empty = identity).
+  void set_block_order(const std::vector<int>& stored_to_local, const std::vector<int64_t>& key);
   void release();
   int64_t ndict = 0;  // dictionary layout: stored distinct-column entries
   // Bytes one application streams from the stored operator (vectors excluded):
@@ -81,7 +90,7 @@ struct DevOp {
   DevSell in, bd;
   int nrows_local = 0;
   int64_t nnz() const { return in.nnz + bd.nnz; }
-  void upload(const RankOp& op, int policy = 0);
+  void upload(const RankOp& op, int policy = 0, const std::vector<int64_t>* key = nullptr);
   void release() { in.release(); bd.release(); }
 };
 
@@ -170,6 +179,9 @@ class DevAMG {
   void set_use_graph(bool g) { use_graph_ = g; }
   double cycle_op_count() const { return cycle_ops_; }
   bool multi_rank() const { return comm_ != nullptr; }
+  // Re-key the row-block traversal (tuning; see locality_keys in runtime.hip).
+  void set_block_bands(const RankHierarchy& R, int nbands);
+  void graphs_clear();
 
   AMGParams prm;
 

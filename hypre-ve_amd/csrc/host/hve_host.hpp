@@ -64,7 +64,12 @@ struct AMGParams {
   int interp_type = 6;            // 6 ext+i, 3 direct
   int P_max_elmts = 4;
   double trunc_factor = 0.0;
-  int relax_type[4] = {13, 13, 14, 9};   // [0]=all, [1]=down, [2]=up, [3]=coarsest
+  // grid_relax_type (par_amg.c:218-220, 339-341: [0] keeps the 3 of the
+  // first allocation, par_amg.c:2136); [1] down, [2] up, [3] coarsest
+  int relax_type[4] = {3, 13, 14, 9};
+  // hypre_ParAMGDataUserRelaxType: set by SetRelaxType only; a one-level
+  // hierarchy relaxes with it, or with 6 when unset (par_cycle.c:296-300)
+  int user_relax_type = -1;
   int num_sweeps[4] = {1, 1, 1, 1};
   double relax_weight = 1.0;
   double outer_weight = 1.0;
@@ -79,7 +84,17 @@ struct AMGParams {
   // Number of contiguous row blocks for the hybrid (block-Jacobi / in-block GS)
   // smoothers; hypre's CPU path uses num_threads for this (par_relax.c:4387).
   int num_blocks = 1;
+  // Aggressive coarsening (par_amg.c:153-173 defaults): the first
+  // agg_num_levels levels coarsen twice (second pass on S*S + 2S over the C
+  // points, num_paths paths needed) and interpolate with agg_interp_type 4
+  // (multipass), truncated by agg_trunc_factor / agg_P_max_elmts.
   int agg_num_levels = 0;
+  int agg_interp_type = 4;
+  double agg_trunc_factor = 0.0;
+  int agg_P_max_elmts = 0;
+  double agg_P12_trunc_factor = 0.0;
+  int agg_P12_max_elmts = 0;
+  int num_paths = 1;
   // Device layout / loop of each SELL operator: 0 automatic (by size, row
   // length and padding), 1 padded lane-per-row, 2 jagged lane-per-row,
   // 3 padded workgroup-per-slice (wide), 4 jagged wave-product-parallel,
@@ -142,6 +157,12 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
 void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                          double trunc_factor, int max_elmts, CSR& P);
 void truncate_rows(CSR& P, double tol, int max_elmts);
+// Aggressive coarsening (aggressive.cpp): par_strength.c:1729 Create2ndS,
+// :2957 CorrectCFMarker, par_multi_interp.c:16 BuildMultipass.
+void create_2nd_strength(const Pattern& S, std::vector<int>& cf, int num_paths, Pattern& S2);
+void correct_cf_marker(std::vector<int>& cf, const std::vector<int>& new_cf);
+void build_multipass_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                            int max_elmts, CSR& P);
 // Universe-indexed cores of ext+i and RAP shared by the one-process and the
 // distributed setup (see setup.cpp).
 void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
@@ -173,19 +194,5 @@ int l1_option_for_level(const AMGParams& prm, int j, int nl, bool* cf_restricted
 // Full setup; returns 0 on success.
 int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H);
 
-// Park-Miller generator used by hypre_Rand (utilities/random.c:40-71).
-double hypre_rand_at(int64_t k, int seed);
-// Chebyshev smoother setup (one process, one thread, as the reference's host
-// path): par_relax_more.c:115 hypre_ParCSRMaxEigEstimateCG (random start
-// vector of hypre_ParVectorSetRandomValues(r, 1), Lanczos tridiagonal from CG,
-// eigenvalues by LINPACK tql1), par_relax_more.c:25 hypre_ParCSRMaxEigEstimate
-// (inf-norm bound), par_cheby.c:36 hypre_ParCSRRelax_Cheby_Setup.
-void max_eig_estimate_cg(const CSR& A, int scale, int max_iter, double* max_eig, double* min_eig);
-void max_eig_estimate_norm(const CSR& A, int scale, double* max_eig);
-void cheby_setup(const CSR& A, double max_eig, double min_eig, double fraction, int order, int scale, int variant,
-                 std::vector<double>& coefs, std::vector<double>& ds);
-// EISPACK tql1 (par_relax_more.c:753): eigenvalues of the symmetric
-// tridiagonal (d, e[1..n-1]) in ascending order into d; 0 or the failing index.
-int linpack_tql1(int n, double* d, double* e);  // value of the (k+1)-th draw after SeedRand(seed)
 
 }  // namespace hve

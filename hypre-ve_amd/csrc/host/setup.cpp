@@ -291,7 +291,9 @@ void create_strength(const CSR& A, double thr, double max_row_sum, Pattern& S) {
 // ---------------------------------------------------------------------------
 // PMIS coarsening: par_coarsen.c:2031 hypre_BoomerAMGCoarsenPMISHost, one
 // process.  cf_init 0 (coarsen_type 8), 2 (type 9, sequential random stream),
-// 1 (HMIS second stage: cf holds the first-pass C points).
+// 1 (HMIS second stage: cf holds the first-pass C points), 3 / 4 (aggressive
+// second pass of type 8 / 9: isolated points become C points).  In one
+// process the sequential stream (2, 4) equals the per-rank one (0, 3).
 // ---------------------------------------------------------------------------
 void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
   const int n = S.n;
@@ -346,7 +348,7 @@ void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
     cf.assign(n, 0);
     for (int r = 0; r < n; ++r) {
       if (S.i[r + 1] - S.i[r] == 0) {
-        cf[r] = SF_PT;
+        cf[r] = (cf_init == 3 || cf_init == 4) ? C_PT : SF_PT;  // par_coarsen.c:2320-2326
         measure[r] = 0;
       } else {
         graph.push_back(r);
@@ -1358,8 +1360,10 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
-  if (prm.agg_num_levels > 0)
-    throw std::runtime_error("aggressive coarsening (agg_num_levels > 0) is not available in this build");
+  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4)
+    throw std::runtime_error("aggressive coarsening: agg_interp_type " + std::to_string(prm.agg_interp_type) +
+                             " is not available in this build (4, multipass, is)");
+  if (prm.num_paths < 1) throw std::runtime_error("num_paths must be >= 1");
   int coarsen_type = prm.coarsen_type;
   H.lev.emplace_back();
   H.lev[0].A = A0;
@@ -1383,6 +1387,27 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     else throw std::runtime_error("unsupported coarsen_type " + std::to_string(coarsen_type));
     double t2 = now();
     t_c += t2 - t1;
+    // par_amg_setup.c:1239-1285: aggressive levels coarsen the C points
+    // again on S*S + 2S, and the second marker refines the first
+    const bool agg = level < prm.agg_num_levels;
+    if (agg) {
+      Pattern S2;
+      create_2nd_strength(S, cf, prm.num_paths, S2);
+      std::vector<int> cfn;
+      if (coarsen_type == 8) coarsen_pmis(S2, 3, cfn);
+      else if (coarsen_type == 9) coarsen_pmis(S2, 4, cfn);
+      else if (coarsen_type == 10) {
+        CSR S2A;  // hypre passes S2 as the matrix too (only its row lengths, for cut_factor)
+        S2A.resize_rows(S2.n, S2.n);
+        S2A.i = S2.i;
+        S2A.j = S2.j;
+        S2A.a.assign(S2.j.size(), 1.0);
+        coarsen_hmis(S2, &S2A, prm.measure_type + 3, prm.coarsen_cut_factor, cfn);
+      } else {
+        throw std::runtime_error("aggressive coarsening with coarsen_type " + std::to_string(coarsen_type));
+      }
+      correct_cf_marker(cf, cfn);  // agg_interp_type 4: par_amg_setup.c:1590
+    }
     int coarse_size = 0;
     for (int v : cf) coarse_size += (v == 1);
     if (coarse_size == 0 || coarse_size == fine_size) {
@@ -1394,7 +1419,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     }
     if (coarse_size < prm.min_coarse_size) break;
     CSR P;
-    if (prm.interp_type == 6) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
+    if (agg) build_multipass_interp(L.A, cf, S, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
+    else if (prm.interp_type == 6) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));
     double t3 = now();

@@ -115,6 +115,12 @@ SIGNATURES = [
     ("HYPRE_BoomerAMGSetCoarsenType", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetMeasureType", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetAggNumLevels", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetNumPaths", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetAggInterpType", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetAggTruncFactor", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetAggP12TruncFactor", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetAggPMaxElmts", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetAggP12MaxElmts", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetInterpType", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetTruncFactor", _i, [_p, _d]),
     ("HYPRE_BoomerAMGSetPMaxElmts", _i, [_p, _i]),
@@ -159,6 +165,7 @@ SIGNATURES = [
     ("hypreve_ParVectorCopyFromHost", _i, [_p, _pd]),
     ("hypreve_ParVectorSetRandomValues", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetNumBlocks", _i, [_p, _i]),
+    ("hypreve_BoomerAMGSetBlockBands", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetUseGraph", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetSellPolicy", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetAggloRows", _i, [_p, _i]),
@@ -385,6 +392,13 @@ class BoomerAMG:
         "num_blocks": ("hypreve_BoomerAMGSetNumBlocks", int), "use_graph": ("hypreve_BoomerAMGSetUseGraph", int),
         "sell_policy": ("hypreve_BoomerAMGSetSellPolicy", int),
         "agglo_rows": ("hypreve_BoomerAMGSetAggloRows", int),
+        "agg_num_levels": ("HYPRE_BoomerAMGSetAggNumLevels", int), "num_paths": ("HYPRE_BoomerAMGSetNumPaths", int),
+        "agg_interp_type": ("HYPRE_BoomerAMGSetAggInterpType", int),
+        "agg_trunc_factor": ("HYPRE_BoomerAMGSetAggTruncFactor", float),
+        "agg_P_max_elmts": ("HYPRE_BoomerAMGSetAggPMaxElmts", int),
+        "agg_P12_trunc_factor": ("HYPRE_BoomerAMGSetAggP12TruncFactor", float),
+        "agg_P12_max_elmts": ("HYPRE_BoomerAMGSetAggP12MaxElmts", int),
+        "measure_type": ("HYPRE_BoomerAMGSetMeasureType", int),
         "cheby_order": ("HYPRE_BoomerAMGSetChebyOrder", int), "cheby_fraction": ("HYPRE_BoomerAMGSetChebyFraction", float),
         "cheby_scale": ("HYPRE_BoomerAMGSetChebyScale", int), "cheby_variant": ("HYPRE_BoomerAMGSetChebyVariant", int),
         "cheby_eig_est": ("HYPRE_BoomerAMGSetChebyEigEst", int),
@@ -498,11 +512,12 @@ class BoomerAMG:
         rt = np.zeros(4, dtype=np.int32)
         ns = np.zeros(4, dtype=np.int32)
         w = np.zeros(2, dtype=np.float64)
-        misc = np.zeros(3, dtype=np.int32)
+        misc = np.zeros(4, dtype=np.int32)
         lib().hypreve_BoomerAMGGetRelaxInfo(self.h, _ptr(rt, C.c_int), _ptr(ns, C.c_int), _ptr(w, C.c_double),
                                             _ptr(misc, C.c_int))
         return dict(relax_type=rt.tolist(), num_sweeps=ns.tolist(), relax_weight=float(w[0]), omega=float(w[1]),
-                    relax_order=int(misc[0]), cycle_type=int(misc[1]), num_blocks=int(misc[2]))
+                    relax_order=int(misc[0]), cycle_type=int(misc[1]), num_blocks=int(misc[2]),
+                    user_relax_type=int(misc[3]))
 
     def gs_schedule_check(self, num_blocks):
         check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
@@ -513,6 +528,10 @@ class BoomerAMG:
         check(lib().hypreve_BenchLevelOp(self.h, level, which, reps, C.byref(ms), C.byref(by), C.byref(pz)),
               "BenchLevelOp")
         return ms.value, by.value, pz.value
+
+    def set_block_bands(self, nbands):
+        """Re-key the row-block traversal (0 = natural order); tuning only."""
+        check(lib().hypreve_BoomerAMGSetBlockBands(self.h, int(nbands)), "SetBlockBands")
 
     def level_op_stored_bytes(self, level, which=0):
         """Bytes one bench_level_op launch streams in the stored layout (+ vectors)."""

@@ -147,6 +147,14 @@ HYPRE_Int HYPRE_BoomerAMGSetMaxRowSum(HYPRE_Solver solver, HYPRE_Real max_row_su
 HYPRE_Int HYPRE_BoomerAMGSetCoarsenType(HYPRE_Solver solver, HYPRE_Int coarsen_type); /* :310 */
 HYPRE_Int HYPRE_BoomerAMGSetMeasureType(HYPRE_Solver solver, HYPRE_Int measure_type); /* :362 */
 HYPRE_Int HYPRE_BoomerAMGSetAggNumLevels(HYPRE_Solver solver, HYPRE_Int agg_num_levels); /* :369 */
+HYPRE_Int HYPRE_BoomerAMGSetNumPaths(HYPRE_Solver solver, HYPRE_Int num_paths); /* :377 */
+/* Aggressive-level interpolation: 4 (multipass, the default) is available;
+ * Setup fails with HYPRE_ERROR_GENERIC for the other types. */
+HYPRE_Int HYPRE_BoomerAMGSetAggInterpType(HYPRE_Solver solver, HYPRE_Int agg_interp_type); /* :480 */
+HYPRE_Int HYPRE_BoomerAMGSetAggTruncFactor(HYPRE_Solver solver, HYPRE_Real agg_trunc_factor); /* :488 */
+HYPRE_Int HYPRE_BoomerAMGSetAggP12TruncFactor(HYPRE_Solver solver, HYPRE_Real agg_P12_trunc_factor); /* :496 */
+HYPRE_Int HYPRE_BoomerAMGSetAggPMaxElmts(HYPRE_Solver solver, HYPRE_Int agg_P_max_elmts); /* :504 */
+HYPRE_Int HYPRE_BoomerAMGSetAggP12MaxElmts(HYPRE_Solver solver, HYPRE_Int agg_P12_max_elmts); /* :512 */
 HYPRE_Int HYPRE_BoomerAMGSetInterpType(HYPRE_Solver solver, HYPRE_Int interp_type); /* :442 */
 HYPRE_Int HYPRE_BoomerAMGSetTruncFactor(HYPRE_Solver solver, HYPRE_Real trunc_factor); /* :448 */
 HYPRE_Int HYPRE_BoomerAMGSetPMaxElmts(HYPRE_Solver solver, HYPRE_Int P_max_elmts); /* :455 */
@@ -229,6 +237,9 @@ HYPRE_Int hypreve_ParVectorSetRandomValues(HYPRE_ParVector v, HYPRE_Int seed); /
  * one block per 4096 local level-0 rows, resolved at Setup; 1 reproduces the
  * reference's single-thread sweep. */
 HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_blocks);
+/* Tuning: visit the row blocks of every operator in nbands bands of the grid
+ * (0 = natural order) on the built hierarchy; results are unchanged. */
+HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands);
 /* Device layout / row loop of the hierarchy's SELL operators (takes effect at
  * Setup): 0 automatic, 1 padded lane-per-row, 2 jagged lane-per-row, 3 padded
  * workgroup-per-slice, 4 jagged wave-product-parallel, 5 jagged with an LDS
@@ -272,7 +283,8 @@ HYPRE_Int hypreve_BoomerAMGGetChebyInfo(HYPRE_Solver solver, HYPRE_Int level, HY
 HYPRE_Int hypreve_BoomerAMGGetCoarseMatrix(HYPRE_Solver solver, HYPRE_Int *n, HYPRE_Real *dense);
 HYPRE_Int hypreve_BoomerAMGGetRelaxInfo(HYPRE_Solver solver, HYPRE_Int *relax_type4,
                                         HYPRE_Int *num_sweeps4, HYPRE_Real *weights2,
-                                        HYPRE_Int *misc3); /* misc: relax_order, cycle_type, num_blocks */
+                                        HYPRE_Int *misc4); /* misc: relax_order, cycle_type, num_blocks,
+                                                               user relax type (-1: unset) */
 /* Host-only setup (no device upload): lets the CPU test suite check the
  * hierarchy against the reference fixtures on a machine without a GPU. */
 HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver solver, HYPRE_ParCSRMatrix A);

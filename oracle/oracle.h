@@ -37,7 +37,7 @@ typedef struct {
   const double *l1[ORC_MAX_LEVELS];
   int coarse_n;               /* dense coarsest operator for relax type 9 */
   const double *coarse_A;     /* row-major n x n, as hypre_GaussElimSetup builds it */
-  int relax_type[4];
+  int relax_type[4];          /* [0]: the user relax type (one-level smoother, -1 = 6) */
   int num_sweeps[4];
   double relax_weight, omega;
   int relax_order, cycle_type, num_blocks;

@@ -139,6 +139,9 @@ class OracleAMG:
         for k in range(4):
             s.relax_type[k] = info["relax_type"][k]
             s.num_sweeps[k] = info["num_sweeps"][k]
+        # orc_cycle relaxes a one-level hierarchy with relax_type[0] (or 6 when
+        # negative): the user relax type, par_cycle.c:296-300
+        s.relax_type[0] = info["user_relax_type"]
         s.relax_weight = info["relax_weight"]
         s.omega = info["omega"]
         s.relax_order = info["relax_order"]

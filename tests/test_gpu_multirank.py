@@ -175,3 +175,16 @@ def test_rccl_single_rank(hv):
     assert it == it1
     assert np.array_equal(x.get(), x1)
     assert abs(rr - rr1) <= 1e-10 * rr1
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_loopback_aggressive_bitwise(hv, nranks):
+    """Aggressive levels on the multi-rank path (rank-0 setup shipped to the
+    ranks): the N-rank iterates equal the one-rank ones."""
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-8, max_iter=80,
+              agg_num_levels=1)
+    x1, it1, rr1, nl1 = _solve_1rank(hv, 16, 16, 18, kw)
+    xN, itN, rrN, nlN = _solve_nranks(hv, 16, 16, 18, kw, nranks)
+    assert nlN == nl1 and all(i == it1 for i in itN)
+    assert np.array_equal(x1, xN)

@@ -328,3 +328,37 @@ def test_boomeramg_default_smoothers_solve(gpu, orc, coarsen):
     assert it == st["iterations"]
     assert np.array_equal(x.get(), u)
     assert abs(rr - st["rel_res"]) <= RTOL_NORM * st["rel_res"]
+
+
+@pytest.mark.parametrize("agg,coarsen,relax", [(1, 8, 18), (2, 8, 18), (1, 10, 18), (1, 8, 13), (10, 10, 6)])
+@pytest.mark.parametrize("coef", [(0.001, 1.0, 1.0), (1.0, 1.0, 1.0)])
+def test_aggressive_coarsening_bitwise(gpu, orc, agg, coarsen, relax, coef):
+    """configs[4]: anisotropic diffusion with PMIS / HMIS and aggressive levels
+    (second coarsening on S*S + 2S, multipass interpolation; par_amg_setup.c
+    :1239-1285, par_multi_interp.c:16).  The irregular rows of the aggressive
+    Galerkin levels run through the automatic layouts; one V-cycle and a solve
+    equal the oracle's bits."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(28, 26, 24, cx=coef[0], cy=coef[1], cz=coef[2])
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=coarsen, agg_num_levels=agg, relax_type=relax, num_blocks=16, tol=1e-7, max_iter=80)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup(A)
+    O = orc.OracleAMG(amg)
+    n = A.n
+    rng = np.random.default_rng(agg * 10 + coarsen)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+    b = hv.ParVector(n, f_h)
+    x = hv.ParVector(n, np.zeros(n))
+    it, rr = amg.solve(A, b, x)
+    xo = np.zeros(n)
+    st = O.solve(f_h, xo, 1e-7, 80)
+    assert it == st["iterations"]
+    assert np.array_equal(x.get(), xo)
