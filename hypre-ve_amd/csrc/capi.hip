@@ -81,6 +81,10 @@ struct hypre_Solver_struct {
   // count; a single block would run each sweep in one workgroup)
   bool auto_blocks = true;
   std::vector<int> gs_rank_starts;  // one GPU emulating the GS blocks of an N-rank run
+  std::vector<int> rank_emul;       // one process emulating a reference N-rank setup (SetRankEmulation)
+  // per level: those blocks and their l1 norms (host copies for the introspection calls)
+  std::vector<std::vector<int>> gs_blocks_host;
+  std::vector<std::vector<double>> gs_l1_host;
   // PCG
   PCGParams pcg;
   HYPRE_Solver precond = nullptr;
@@ -88,6 +92,9 @@ struct hypre_Solver_struct {
   std::unique_ptr<DevAMG> ws;
 };
 
+// One-process setup, optionally emulating a reference N-rank run (its rows,
+// coarsening and GS blocks; no agglomeration, which the reference lacks).
+static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A);
 // Automatic hybrid Gauss-Seidel block count (num_blocks 0): one block of about
 // kAutoBlockRows rows each, so a large level's sweep runs on thousands of
 // workgroups while every block keeps hypre's exact in-block GS order.
@@ -674,8 +681,6 @@ AMG_SET(TruncFactor, trunc_factor, HYPRE_Real)
 AMG_SET(PMaxElmts, P_max_elmts, HYPRE_Int)
 AMG_SET(CycleType, cycle_type, HYPRE_Int)
 AMG_SET(RelaxOrder, relax_order, HYPRE_Int)
-AMG_SET(RelaxWt, relax_weight, HYPRE_Real)
-AMG_SET(OuterWt, outer_weight, HYPRE_Real)
 AMG_SET(PrintLevel, print_level, HYPRE_Int)
 AMG_SET(Logging, logging, HYPRE_Int)
 AMG_SET(ChebyOrder, cheby_order, HYPRE_Int)
@@ -683,6 +688,48 @@ AMG_SET(ChebyFraction, cheby_fraction, HYPRE_Real)
 AMG_SET(ChebyScale, cheby_scale, HYPRE_Int)
 AMG_SET(ChebyVariant, cheby_variant, HYPRE_Int)
 AMG_SET(ChebyEigEst, cheby_eig_est, HYPRE_Int)
+
+// par_amg.c SetRelaxWt / SetOuterWt overwrite every level's weight;
+// SetLevelRelaxWt / SetLevelOuterWt (par_amg.c:2368) set one level.  A
+// nonpositive weight asks for the reference's CG estimate, not restated here.
+HYPRE_Int HYPRE_BoomerAMGSetRelaxWt(HYPRE_Solver s, HYPRE_Real w) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  if (!(w > 0.0)) return set_err(HYPRE_ERROR_ARG, "relax weight <= 0 (automatic weight) is not available");
+  s->prm.relax_weight = w;
+  s->prm.lev_relax_wt_set = 0;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGSetOuterWt(HYPRE_Solver s, HYPRE_Real w) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  if (!(w > 0.0)) return set_err(HYPRE_ERROR_ARG, "outer weight <= 0 (automatic weight) is not available");
+  s->prm.outer_weight = w;
+  s->prm.lev_outer_wt_set = 0;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGSetLevelRelaxWt(HYPRE_Solver s, HYPRE_Real w, HYPRE_Int level) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(level >= 0 && level < AMGParams::kWeightLevels && level < s->prm.max_levels, 3);
+  if (!(w > 0.0)) return set_err(HYPRE_ERROR_ARG, "relax weight <= 0 (automatic weight) is not available");
+  s->prm.lev_relax_wt[level] = w;
+  s->prm.lev_relax_wt_set |= (uint64_t)1 << level;
+  return 0;
+}
+HYPRE_Int HYPRE_BoomerAMGSetLevelOuterWt(HYPRE_Solver s, HYPRE_Real w, HYPRE_Int level) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(level >= 0 && level < AMGParams::kWeightLevels && level < s->prm.max_levels, 3);
+  if (!(w > 0.0)) return set_err(HYPRE_ERROR_ARG, "outer weight <= 0 (automatic weight) is not available");
+  s->prm.lev_outer_wt[level] = w;
+  s->prm.lev_outer_wt_set |= (uint64_t)1 << level;
+  return 0;
+}
+// Relaxation weight and outer weight (omega) the cycle uses on `level`.
+HYPRE_Int hypreve_BoomerAMGGetLevelWeights(HYPRE_Solver s, HYPRE_Int level, HYPRE_Real* w, HYPRE_Real* omega) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  const AMGParams& p = s->H.lev.empty() ? (s->RH.lev.empty() ? s->prm : s->RH.prm) : s->H.prm;
+  if (w) *w = p.wt(level);
+  if (omega) *omega = p.omega(level);
+  return 0;
+}
 
 // par_amg.c:1962 SetNumSweeps: all of [0..2] (coarsest keeps 1), :2084 SetRelaxType
 HYPRE_Int HYPRE_BoomerAMGSetNumSweeps(HYPRE_Solver s, HYPRE_Int num_sweeps) {
@@ -740,6 +787,18 @@ HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver s, HYPRE_Int nranks, con
   }
   return 0;
 }
+HYPRE_Int hypreve_BoomerAMGSetRankEmulation(HYPRE_Solver s, HYPRE_Int nranks, const HYPRE_Int* starts) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(nranks <= 1 || starts, 3);
+  s->rank_emul.clear();
+  s->gs_rank_starts.clear();
+  if (nranks > 1) {
+    for (int r = 0; r < nranks; ++r) CHECK_ARG(starts[r] <= starts[r + 1] && starts[0] == 0, 3);
+    s->rank_emul.assign(starts, starts + nranks + 1);
+    s->gs_rank_starts = s->rank_emul;
+  }
+  return 0;
+}
 // Tuning: re-key the row-block traversal of the built device hierarchy with
 // nbands bands of the grid's y extent (0: natural order; default at Setup:
 // HVE_BLOCK_ORDER, 8).  Only the visiting order of row blocks changes.
@@ -791,7 +850,7 @@ HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   CHECK_ARG(A, 2);
   API_BEGIN
   if (s->auto_blocks) s->prm.num_blocks = auto_num_blocks(A->n);
-  amg_setup(A->diag, s->prm, s->H);
+  setup_one_process(s, A);
   API_END
 }
 
@@ -1022,6 +1081,17 @@ static void setup_dist(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
   if (s->prm.print_level > 0) fputs(log.c_str(), stderr);
 }
 
+static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
+  if (s->rank_emul.empty()) {
+    amg_setup(A->diag, s->prm, s->H);
+  } else {
+    AMGParams prm = s->prm;
+    prm.agglo_rows = 0;
+    amg_setup(A->diag, prm, s->H, &s->rank_emul);
+  }
+  gs_rank_blocks_host(s->H, s->gs_rank_starts, s->gs_blocks_host, s->gs_l1_host);
+}
+
 extern "C" {
 
 HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVector b, HYPRE_ParVector x) {
@@ -1034,7 +1104,7 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
     if (use_dist_setup(s->prm)) setup_dist(s, A);
     else setup_multi(s, A);
   } else {
-    amg_setup(A->diag, s->prm, s->H);
+    setup_one_process(s, A);
     single_rank_hierarchy(s->H, s->RH, s->gs_rank_starts.empty() ? nullptr : &s->gs_rank_starts);
   }
   if (!s->dev) s->dev.reset(new DevAMG);
@@ -1143,8 +1213,16 @@ HYPRE_Int hypreve_BoomerAMGGetLevelVector(HYPRE_Solver s, HYPRE_Int level, HYPRE
     if (n) *n = (int)L.cf.size();
     if (data && !L.cf.empty()) std::memcpy(data, L.cf.data(), sizeof(int) * L.cf.size());
   } else if (which == 1) {
-    if (n) *n = (int)L.l1.size();
-    if (data && !L.l1.empty()) std::memcpy(data, L.l1.data(), sizeof(double) * L.l1.size());
+    // with the N-rank GS emulation: the norms of its blocks (what the device sweeps with)
+    const std::vector<double>& l1 = level < (int)s->gs_l1_host.size() ? s->gs_l1_host[level] : L.l1;
+    if (n) *n = (int)l1.size();
+    if (data && !l1.empty()) std::memcpy(data, l1.data(), sizeof(double) * l1.size());
+  } else if (which == 3) {
+    // hybrid-GS block starts of the N-rank emulation (empty: hypre's num_blocks partition)
+    static const std::vector<int> none;
+    const std::vector<int>& b = level < (int)s->gs_blocks_host.size() ? s->gs_blocks_host[level] : none;
+    if (n) *n = (int)b.size();
+    if (data && !b.empty()) std::memcpy(data, b.data(), sizeof(int) * b.size());
   } else {
     if (n) *n = (int)L.cheby_ds.size();
     if (data && !L.cheby_ds.empty()) std::memcpy(data, L.cheby_ds.data(), sizeof(double) * L.cheby_ds.size());

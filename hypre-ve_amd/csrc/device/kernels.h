@@ -63,7 +63,8 @@ struct GsView {
   int wg = 64;  // workgroup size: 64, or 256 for wide levels
 };
 hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const double* l1, const int* cf,
-                            int relax_points, const double* tmp, double* u, hipStream_t st);
+                            int relax_points, const double* tmp, double* u, double w, double omega,
+                            hipStream_t st);
 int sell_batch_override();
 int sell_pipe_override();
 bool sell_nt();

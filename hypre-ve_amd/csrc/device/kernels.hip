@@ -833,6 +833,10 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
 // before the sweep (par_relax.c tmp_data / Vext_data).
 //   L1 = true : cases 8/13/14, res = f - sum_all a*u, u += res / l1
 //   L1 = false: cases 3/4/6,   res = f - sum_offdiag a*u, u = res / a_ii
+//   WGT (relax_weight w or omega != 1, par_relax.c:1277/4544): the diagonal
+//   entry skipped; in-block res0 -= a*u, res2 += a*Vtemp; off-block
+//   res -= a*tmp; u = u*(1 - w*omega); u += w*(omega*res + res0 + (1-omega)*res2)/d
+//   with d = l1 or a_ii.  Vtemp and tmp are the same pre-sweep copy.
 // ---------------------------------------------------------------------------
 struct GsArgs {
   const int* __restrict__ block_start;
@@ -848,9 +852,10 @@ struct GsArgs {
   const double* tmp;
   double* u;
   int relax_points;
+  double w, omega;
 };
 
-template <bool L1, bool CFSEL, int WG>
+template <bool L1, bool CFSEL, bool WGT, int WG>
 __global__ void __launch_bounds__(WG) k_hybrid_gs(GsArgs p) {
   constexpr int B = 8;
   const int blk = blockIdx.x;
@@ -870,13 +875,32 @@ __global__ void __launch_bounds__(WG) k_hybrid_gs(GsArgs p) {
       int k0;
       if (L1) {
         scale = p.l1[i];
-        k0 = 0;
+        k0 = WGT ? 1 : 0;
       } else {
         scale = vp[0];  // diagonal stored first
         k0 = 1;
       }
       if (scale == 0.0) continue;
       double res = p.f[i];
+      if (WGT) {
+        double res0 = 0.0, res2 = 0.0;
+        for (int k = k0; k < width; ++k) {
+          const int cc = cp[k * kWave];
+          if (cc < 0) continue;
+          const double a = vp[k * kWave];
+          if (cc >= ns && cc < ne) {
+            res0 -= a * p.u[cc];
+            res2 += a * p.tmp[cc];
+          } else {
+            res -= a * p.tmp[cc];
+          }
+        }
+        double ui = p.u[i];
+        ui *= 1.0 - p.w * p.omega;
+        ui += p.w * (p.omega * res + res0 + (1.0 - p.omega) * res2) / scale;
+        p.u[i] = ui;
+        continue;
+      }
       for (int k = k0; k < width; k += B) {
         int c[B];
         double a[B], xv[B];
@@ -903,22 +927,29 @@ __global__ void __launch_bounds__(WG) k_hybrid_gs(GsArgs p) {
 }
 
 hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const double* l1, const int* cf,
-                            int relax_points, const double* tmp, double* u, hipStream_t st) {
+                            int relax_points, const double* tmp, double* u, double w, double omega,
+                            hipStream_t st) {
   if (S.nblocks <= 0) return hipSuccess;
   GsArgs a;
   a.block_start = S.block_start; a.block_level = S.block_level; a.level_slice = S.level_slice;
   a.slice_ptr = S.slice_ptr; a.col = S.col; a.val = S.val; a.rowmap = S.rowmap;
   a.f = f; a.l1 = l1; a.cf = cf; a.tmp = tmp ? tmp : u; a.u = u; a.relax_points = relax_points;
+  a.w = w; a.omega = omega;
   const bool cfsel = relax_points != 0 && cf != nullptr;
+  const bool wgt = w != 1.0 || omega != 1.0;
+  if (wgt && !tmp) return hipErrorInvalidValue;  // the weighted forms read the pre-sweep copy
   const dim3 grid(S.nblocks);
-#define HVE_G(L1V, CFV)                                                                       \
-  if (S.wg == 256) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, 256>), grid, dim3(256), 0, st, a); \
-  else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, 64>), grid, dim3(64), 0, st, a);
+#define HVE_G(L1V, CFV, WV)                                                                           \
+  if (S.wg == 256) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, 256>), grid, dim3(256), 0, st, a); \
+  else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, 64>), grid, dim3(64), 0, st, a);
+#define HVE_GW(L1V, CFV) \
+  if (wgt) { HVE_G(L1V, CFV, true) } else { HVE_G(L1V, CFV, false) }
   if (use_l1) {
-    if (cfsel) { HVE_G(true, true) } else { HVE_G(true, false) }
+    if (cfsel) { HVE_GW(true, true) } else { HVE_GW(true, false) }
   } else {
-    if (cfsel) { HVE_G(false, true) } else { HVE_G(false, false) }
+    if (cfsel) { HVE_GW(false, true) } else { HVE_GW(false, false) }
   }
+#undef HVE_GW
 #undef HVE_G
   return hipGetLastError();
 }

@@ -771,7 +771,7 @@ bool DevAMG::can_fuse_presmooth() const {
   if (lev_.size() < 2 || !lev_[0].l1) return false;
   const int rt = prm.relax_type[1];
   // with relax_order 1 the first down sweep is C/F-ordered (18) or one of two (7)
-  return (rt == 18 || rt == 7) && prm.relax_weight == 1.0 && prm.num_sweeps[1] >= 1 && prm.relax_order != 1;
+  return (rt == 18 || rt == 7) && prm.wt(0) == 1.0 && prm.num_sweeps[1] >= 1 && prm.relax_order != 1;
 }
 double* DevAMG::presmooth_buffer() { return u0_buf_[1] ? u0_buf_[1] : lev_[0].U[0]; }
 
@@ -821,7 +821,7 @@ void DevAMG::coarse_solve(int level, const double* f, double* u, hipStream_t s) 
 void DevAMG::relax(int level, int relax_type, int relax_points, const double* f, double*& u_cur,
                    double*& u_alt, bool zero_guess, hipStream_t s) {
   DevLevel& L = lev_[level];
-  const double w = prm.relax_weight;
+  const double w = prm.wt(level), omega = prm.omega(level);  // relax_weight[level], omega[level]
   const int n = L.n;
   if (relax_type == 7) relax_points = 0;  // par_relax.c:3463: a C/F-ordered call is a full sweep
   if (zero_guess && relax_points != 0) {
@@ -859,10 +859,9 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       break;
     }
     case 3: case 4: case 6: case 8: case 13: case 14: {
-      // par_relax.c:354 (3), :1875 (4), :2266 (6), :3492 (8), :4340 (13), :4732 (14)
-      if (w != 1.0 || prm.outer_weight != 1.0)
-        throw std::runtime_error("weighted hybrid Gauss-Seidel / SOR (relax_wt or outer_wt != 1) is not available "
-                                 "on the GPU path in this build");
+      // par_relax.c:354 (3), :1875 (4), :2266 (6), :3492 (8), :4340 (13), :4732 (14);
+      // weighted forms (relax_weight or omega != 1): par_relax.c:1277, :2075, :3150, :3785, :4544, :4937
+      const bool weighted = w != 1.0 || omega != 1.0;
       const bool use_l1 = relax_type == 8 || relax_type == 13 || relax_type == 14;
       const bool fw = relax_type == 3 || relax_type == 6 || relax_type == 8 || relax_type == 13;
       const bool bw = relax_type == 4 || relax_type == 6 || relax_type == 8 || relax_type == 14;
@@ -878,12 +877,15 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       }
       const int nh = n + L.hu.n_halo;
       const double* tmp = L.hu.n_halo > 0 ? u_cur : nullptr;  // halo columns: u's halo, untouched by the sweep
-      if (L.gs_fwd.built() ? L.gs_fwd.nblocks > 1 : L.gs_bwd.nblocks > 1) {
-        HVE_HIP(launch_copy(nh, u_cur, L.gs_tmp, s));  // tmp_data[i] = u_data[i]
+      if (weighted || (L.gs_fwd.built() ? L.gs_fwd.nblocks > 1 : L.gs_bwd.nblocks > 1)) {
+        // tmp_data[i] = u_data[i] (= Vtemp_data of the weighted forms, one copy for both halves of 6/8)
+        HVE_HIP(launch_copy(nh, u_cur, L.gs_tmp, s));
         tmp = L.gs_tmp;
       }
-      if (fw) HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, s));
-      if (bw) HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, s));
+      if (fw)
+        HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, w, omega, s));
+      if (bw)
+        HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, w, omega, s));
       break;
     }
     case 16: {
@@ -1010,7 +1012,7 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       // the zero guess, u_c = 0 + F_c/l1 is formed by the restriction itself.
       const bool into_agg = agg_level_ >= 0 && coarse == agg_level_;
       const bool fuse_zg = !into_agg && coarse != nl - 1 && prm.num_sweeps[1] >= 1 && prm.relax_order != 1 &&
-                           (prm.relax_type[1] == 18 || prm.relax_type[1] == 7) && prm.relax_weight == 1.0 &&
+                           (prm.relax_type[1] == 18 || prm.relax_type[1] == 7) && prm.wt(coarse) == 1.0 &&
                            lev_[coarse].l1 != nullptr;
       if (fuse_zg) {
         apply(Lf.R, &Lf.hv, K_RESTRICT_ZG, Lf.V, nullptr, lev_[coarse].l1, nullptr, 0, lev_[coarse].F, 1.0, 0.0,

@@ -73,6 +73,20 @@ struct AMGParams {
   int num_sweeps[4] = {1, 1, 1, 1};
   double relax_weight = 1.0;
   double outer_weight = 1.0;
+  // Per-level weights (hypre's relax_weight[level] / omega[level] arrays:
+  // SetLevelRelaxWt / SetLevelOuterWt, par_amg.c); a level whose bit is clear
+  // takes the global value.  SetRelaxWt / SetOuterWt clear every level's bit,
+  // as hypre overwrites the whole array.
+  static constexpr int kWeightLevels = 64;
+  double lev_relax_wt[kWeightLevels] = {};
+  double lev_outer_wt[kWeightLevels] = {};
+  uint64_t lev_relax_wt_set = 0, lev_outer_wt_set = 0;
+  double wt(int level) const {
+    return (level >= 0 && level < kWeightLevels && (lev_relax_wt_set >> level & 1)) ? lev_relax_wt[level] : relax_weight;
+  }
+  double omega(int level) const {
+    return (level >= 0 && level < kWeightLevels && (lev_outer_wt_set >> level & 1)) ? lev_outer_wt[level] : outer_weight;
+  }
   int relax_order = 0;            // 1 = C/F relaxation
   int cycle_type = 1;             // 1 V, 2 W
   int max_iter = 20;
@@ -148,10 +162,16 @@ void generate_laplacian_7pt_block(int nx, int ny, int nz, int P, int Q, int R, i
 
 // ---- setup building blocks ----
 void create_strength(const CSR& A, double thr, double max_row_sum, Pattern& S);
-void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf);
+// rs (optional): emulate the coarsening of an N-rank run, rank r owning rows
+// [rs[r], rs[r+1]) (per-rank random streams and first passes, hypre's
+// CF_marker_offd semantics).
+void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf, const std::vector<int>* rs = nullptr);
+// full_row_len (optional): strong connections of each row including those the
+// pattern omits (another rank's columns), for the empty-row test.
 void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, int cut_factor,
-                             std::vector<int>& cf);
-void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf);
+                             std::vector<int>& cf, const int* full_row_len = nullptr);
+void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
+                  const std::vector<int>* rs = nullptr);
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P);
 void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
@@ -175,7 +195,8 @@ double hypre_rand_at(int64_t k, int seed);
 // vector of hypre_ParVectorSetRandomValues(r, 1), Lanczos tridiagonal from CG,
 // eigenvalues by LINPACK tql1), par_relax_more.c:25 hypre_ParCSRMaxEigEstimate
 // (inf-norm bound), par_cheby.c:36 hypre_ParCSRRelax_Cheby_Setup.
-void max_eig_estimate_cg(const CSR& A, int scale, int max_iter, double* max_eig, double* min_eig);
+void max_eig_estimate_cg(const CSR& A, int scale, int max_iter, double* max_eig, double* min_eig,
+                         const std::vector<int>* rs = nullptr);  // rs: emulated rank row starts
 void max_eig_estimate_norm(const CSR& A, int scale, double* max_eig);
 void cheby_setup(const CSR& A, double max_eig, double min_eig, double fraction, int order, int scale, int variant,
                  std::vector<double>& coefs, std::vector<double>& ds);
@@ -192,7 +213,10 @@ void compute_l1_norms_blocks(const CSR& A, int option, const int* cf, const std:
 int l1_option_for_level(const AMGParams& prm, int j, int nl, bool* cf_restricted);
 
 // Full setup; returns 0 on success.
-int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H);
+// rank_starts (optional, N+1 level-0 row starts): build the hierarchy an N-rank
+// hypre run builds (rows in ParCSR diag/offd order on every level, per-rank
+// coarsening); the solve path is unchanged.
+int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H, const std::vector<int>* rank_starts = nullptr);
 
 
 }  // namespace hve

@@ -373,6 +373,15 @@ void partition_hierarchy(const Hierarchy& H, const std::vector<int>& starts0, in
   out = std::move(all[rank]);
 }
 
+void gs_rank_blocks_host(const Hierarchy& H, const std::vector<int>& gs_rank_starts,
+                         std::vector<std::vector<int>>& blocks, std::vector<std::vector<double>>& l1) {
+  blocks.clear();
+  l1.clear();
+  if (gs_rank_starts.size() <= 2 || !uses_hybrid_gs(H.prm)) return;
+  blocks = rank_gs_blocks(H, gs_rank_starts, (int)gs_rank_starts.size() - 1);
+  l1 = l1_for_blocks(H, blocks);
+}
+
 void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out, const std::vector<int>* gs_rank_starts) {
   std::vector<int> s0 = {0, H.lev[0].A.nrows};
   partition_hierarchy(H, s0, 0, 1, out);

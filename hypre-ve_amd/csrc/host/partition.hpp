@@ -92,6 +92,11 @@ void partition_hierarchy_all(const Hierarchy& H, const std::vector<int>& starts0
 // on every level (num_blocks per rank, l1 norms to match), so that one GPU
 // reproduces the N-rank iterates.
 void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out, const std::vector<int>* gs_rank_starts = nullptr);
+// The hybrid-GS row blocks and option-4 l1 norms of every level that
+// single_rank_hierarchy gives the device for gs_rank_starts (empty when the
+// emulation is off): exported so the CPU oracle sweeps the same blocks.
+void gs_rank_blocks_host(const Hierarchy& H, const std::vector<int>& gs_rank_starts,
+                         std::vector<std::vector<int>>& blocks, std::vector<std::vector<double>>& l1);
 // Per level: global hybrid-GS block starts of an N-rank partition with level-0
 // starts starts0 (num_blocks blocks of every rank's rows; replicated levels
 // num_blocks blocks of the whole level).

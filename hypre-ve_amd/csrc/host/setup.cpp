@@ -295,7 +295,12 @@ void create_strength(const CSR& A, double thr, double max_row_sum, Pattern& S) {
 // second pass of type 8 / 9: isolated points become C points).  In one
 // process the sequential stream (2, 4) equals the per-rank one (0, 3).
 // ---------------------------------------------------------------------------
-void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
+// Owner rank of row i for row starts rs (rank r owns [rs[r], rs[r+1])).
+static inline int owner_of(const std::vector<int>& rs, int i) {
+  return (int)(std::upper_bound(rs.begin(), rs.end(), i) - rs.begin()) - 1;
+}
+
+void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf, const std::vector<int>* rs) {
   const int n = S.n;
   std::vector<double> measure(n, 0.0);
   // column counts of S (number of points each point influences)
@@ -307,7 +312,19 @@ void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
   }
   // hypre_BoomerAMGIndepSetInit (par_indepset.c:25): seed 2747 + my_id (0),
   // one hypre_Rand() per local row in row order (first_row_index = 0).
-  {
+  // Emulating N ranks (rs): rank r seeds 2747 + r and draws over its own rows,
+  // unless the stream is the sequential one (CF_init 2 / 4, seq_rand).
+  if (rs && !(cf_init == 2 || cf_init == 4)) {
+    const int nr = (int)rs->size() - 1;
+#pragma omp parallel for schedule(static)
+    for (int r = 0; r < nr; ++r) {
+      uint64_t sd = (uint64_t)(2747 + r) % kRandM;
+      for (int i = (*rs)[r]; i < (*rs)[r + 1]; ++i) {
+        sd = (sd * kRandA) % kRandM;
+        measure[i] += (double)sd / (double)kRandM;
+      }
+    }
+  } else {
     const int seed = 2747;
 #pragma omp parallel
     {
@@ -327,13 +344,22 @@ void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
       }
     }
   }
+  // emulated ranks: whether row r has a strong connection owned by another rank
+  // (hypre's S_offd row); such rows drop their first-pass marker (par_coarsen.c:2296)
+  auto has_offd = [&](int r) {
+    if (!rs) return false;
+    const int o = owner_of(*rs, r);
+    for (int k = S.i[r]; k < S.i[r + 1]; ++k)
+      if (owner_of(*rs, S.j[k]) != o) return true;
+    return false;
+  };
   std::vector<int> graph;
   graph.reserve(n);
   if (cf_init == 1) {
     // CF from the first (Ruge) pass: C points keep 1, others reset to 0/F.
     for (int r = 0; r < n; ++r) {
       if (cf[r] != SF_PT) {
-        if (cf[r] == -1) cf[r] = 0;  // no offd in a single process
+        if (cf[r] == -1 || has_offd(r)) cf[r] = 0;
         if (cf[r] == Z_PT) {
           if (measure[r] >= 1.0 || S.i[r + 1] - S.i[r] > 0) { cf[r] = 0; graph.push_back(r); }
           else cf[r] = F_PT;
@@ -392,14 +418,17 @@ void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf) {
       // The seeded C points (Ruge pass) can be demoted below (measure < 1)
       // while their neighbours test them; follow the reference's row order:
       // graph is ascending, so a neighbour j < i in the graph already holds
-      // its new marker.
+      // its new marker.  Emulated ranks: an off-rank neighbour reads
+      // CF_marker_offd, still 0 in this first pass (par_coarsen.c:2348).
       for (int ig = 0; ig < gs; ++ig) {
         const int i = graph[ig];
         if (measure[i] < 1) cf[i] = F_PT;
         if (cf[i] > 0) {
           cf[i] = C_PT;
         } else {
+          const int oi = rs ? owner_of(*rs, i) : 0;
           for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
+            if (rs && owner_of(*rs, S.j[k]) != oi) continue;
             if (cf[S.j[k]] > 0) { cf[i] = F_PT; break; }
           }
         }
@@ -534,7 +563,7 @@ struct MeasureLists {
 // coarsen_type 10 -> first pass only with Z_PT for measure-0 points
 // (par_coarsen.c:1082-1086, 1347-1354).
 void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, int cut_factor,
-                             std::vector<int>& cf) {
+                             std::vector<int>& cf, const int* full_row_len) {
   constexpr int UNDECIDED = 0, SC_PT = 3;
   const int n = S.n;
   const bool agg_2 = (measure_type == 3 || measure_type == 4);
@@ -555,7 +584,8 @@ void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, i
   int num_left = 0;
   for (int j = 0; j < n; ++j) {
     if (cf[j] == 0) {
-      if (S.i[j + 1] - S.i[j] == 0) {
+      // nnzrow counts the diag and offd parts (par_coarsen.c:1137)
+      if ((full_row_len ? full_row_len[j] : S.i[j + 1] - S.i[j]) == 0) {
         cf[j] = agg_2 ? SC_PT : SF_PT;
         measure[j] = 0;
       } else {
@@ -651,9 +681,37 @@ void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, i
 
 // par_coarsen.c:2774 hypre_BoomerAMGCoarsenHMIS: Ruge first pass, then PMIS
 // seeded with its C points (CF_init = 1).
-void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf) {
-  coarsen_ruge_first_pass(S, A, measure_type, cut_factor, cf);
-  coarsen_pmis(S, 1, cf);
+// Emulated ranks (rs): every rank runs the first pass on its own rows with the
+// strong connections it owns (S_diag, local measures, measure_type 0), then
+// PMIS runs over the whole graph.
+void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
+                  const std::vector<int>* rs) {
+  if (!rs) {
+    coarsen_ruge_first_pass(S, A, measure_type, cut_factor, cf);
+  } else {
+    if (cut_factor > 0) throw std::runtime_error("rank emulation: HMIS with a cut factor is not restated");
+    if (measure_type != 0) throw std::runtime_error("rank emulation: HMIS needs local measures (measure_type 0)");
+    const int nr = (int)rs->size() - 1;
+    cf.assign(S.n, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int r = 0; r < nr; ++r) {
+      const int a = (*rs)[r], b = (*rs)[r + 1];
+      Pattern Sl;
+      Sl.n = b - a;
+      Sl.i.assign(Sl.n + 1, 0);
+      std::vector<int> full(Sl.n);
+      for (int i = a; i < b; ++i) {
+        full[i - a] = S.i[i + 1] - S.i[i];
+        for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+          if (S.j[k] >= a && S.j[k] < b) Sl.j.push_back(S.j[k] - a);
+        Sl.i[i - a + 1] = (int)Sl.j.size();
+      }
+      std::vector<int> cl;
+      coarsen_ruge_first_pass(Sl, nullptr, measure_type, 0, cl, full.data());
+      std::copy(cl.begin(), cl.end(), cf.begin() + a);
+    }
+  }
+  coarsen_pmis(S, 1, cf, rs);
 }
 
 // ---------------------------------------------------------------------------
@@ -1207,13 +1265,20 @@ static double host_dot(const std::vector<double>& x, const std::vector<double>& 
   return s;
 }
 
-void max_eig_estimate_cg(const CSR& A, int scale, int max_iter, double* max_eig, double* min_eig) {
+void max_eig_estimate_cg(const CSR& A, int scale, int max_iter, double* max_eig, double* min_eig,
+                         const std::vector<int>* rs) {
   const int n = A.nrows;
   if (n < max_iter) max_iter = n;
   std::vector<double> r(n), p(n, 0.0), s(n, 0.0), ds(n), u(n, 0.0);
   std::vector<double> tridiag(max_iter + 1, 0.0), trioffd(max_iter + 1, 0.0);
   // hypre_ParVectorSetRandomValues(r, 1): seed 1 * (my_id + 1), 2*rand - 1
-  for (int i = 0; i < n; ++i) r[i] = 2.0 * hypre_rand_at(i, 1) - 1.0;
+  // (par_vector.c:337), every rank from its own first row
+  if (rs) {
+    for (size_t k = 0; k + 1 < rs->size(); ++k)
+      for (int i = (*rs)[k]; i < (*rs)[k + 1]; ++i) r[i] = 2.0 * hypre_rand_at(i - (*rs)[k], (int)k + 1) - 1.0;
+  } else {
+    for (int i = 0; i < n; ++i) r[i] = 2.0 * hypre_rand_at(i, 1) - 1.0;
+  }
   if (scale) {
     for (int i = 0; i < n; ++i) ds[i] = 1 / std::sqrt(A.a[A.i[i]]);
   } else {
@@ -1356,7 +1421,28 @@ int l1_option_for_level(const AMGParams& prm, int j, int nl, bool* cf_restricted
   return opt;
 }
 
-int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
+// Rows of an N-rank run (hypre's ParCSR: each row = its diag part, then its
+// offd part, both in their own entry order): stable partition of every row of
+// M by whether the column's owner is the row's owner.
+static void rank_order_rows(CSR& M, const std::vector<int>& rs, const std::vector<int>& cs) {
+  auto owner = [](const std::vector<int>& st, int i) {
+    return (int)(std::upper_bound(st.begin(), st.end(), i) - st.begin()) - 1;
+  };
+  std::vector<int> tj;
+  std::vector<double> ta;
+  for (int r = 0; r < M.nrows; ++r) {
+    const int o = owner(rs, r);
+    tj.clear();
+    ta.clear();
+    for (int pass = 0; pass < 2; ++pass)
+      for (int k = M.i[r]; k < M.i[r + 1]; ++k)
+        if ((owner(cs, M.j[k]) == o) == (pass == 0)) { tj.push_back(M.j[k]); ta.push_back(M.a[k]); }
+    std::copy(tj.begin(), tj.end(), M.j.begin() + M.i[r]);
+    std::copy(ta.begin(), ta.end(), M.a.begin() + M.i[r]);
+  }
+}
+
+int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::vector<int>* rank_starts) {
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
@@ -1367,6 +1453,19 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
   int coarsen_type = prm.coarsen_type;
   H.lev.emplace_back();
   H.lev[0].A = A0;
+  // N-rank emulation: the row starts of every level (rank r owns the C points
+  // of its fine rows), and every row in hypre's ParCSR order (diag, offd)
+  std::vector<int> emul;
+  if (rank_starts && rank_starts->size() > 2) {
+    emul = *rank_starts;
+    if (emul.front() != 0 || emul.back() != A0.nrows) throw std::runtime_error("rank emulation: row starts do not cover A");
+    if (prm.agg_num_levels > 0) throw std::runtime_error("rank emulation: aggressive coarsening is not restated");
+    if (prm.interp_type != 6) throw std::runtime_error("rank emulation: only ext+i interpolation is restated");
+    rank_order_rows(H.lev[0].A, emul, emul);
+  }
+  const std::vector<int>* rs = emul.empty() ? nullptr : &emul;
+  std::vector<std::vector<int>> lev_starts;  // emulated ranks: row starts of every level
+  if (rs) lev_starts.push_back(emul);
   char buf[256];
   int level = 0;
   bool finished = prm.max_levels <= 1;
@@ -1381,9 +1480,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     double t1 = now();
     t_s += t1 - t0;
     std::vector<int> cf;
-    if (coarsen_type == 8) coarsen_pmis(S, 0, cf);
-    else if (coarsen_type == 9) coarsen_pmis(S, 2, cf);
-    else if (coarsen_type == 10) coarsen_hmis(S, &L.A, prm.measure_type, prm.coarsen_cut_factor, cf);
+    if (coarsen_type == 8) coarsen_pmis(S, 0, cf, rs);
+    else if (coarsen_type == 9) coarsen_pmis(S, 2, cf, rs);
+    else if (coarsen_type == 10) coarsen_hmis(S, &L.A, prm.measure_type, prm.coarsen_cut_factor, cf, rs);
     else throw std::runtime_error("unsupported coarsen_type " + std::to_string(coarsen_type));
     double t2 = now();
     t_c += t2 - t1;
@@ -1420,6 +1519,20 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     if (coarse_size < prm.min_coarse_size) break;
     CSR P;
     if (agg) build_multipass_interp(L.A, cf, S, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
+    else if (prm.interp_type == 6 && !emul.empty()) {
+      // par_csr_matrix.c:2671 truncates the row [P_diag | P_offd] and splits
+      // the kept entries back into the two parts in their sorted order
+      std::vector<int> cs(emul.size(), 0);
+      {
+        std::vector<int> pref(cf.size() + 1, 0);
+        for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] == 1);
+        for (size_t r = 0; r < emul.size(); ++r) cs[r] = pref[emul[r]];
+      }
+      build_extpi_interp(L.A, cf, S, 0.0, 0, P);
+      rank_order_rows(P, emul, cs);
+      if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
+      rank_order_rows(P, emul, cs);
+    }
     else if (prm.interp_type == 6) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));
@@ -1427,6 +1540,15 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     t_i += t3 - t2;
     CSR Ac;
     rap(P, L.A, Ac);
+    std::vector<int> emul_c;
+    if (!emul.empty()) {
+      // hypre's RAP keeps each coarse row as diag then offd (par_rap.c)
+      std::vector<int> pref(cf.size() + 1, 0);
+      for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] == 1);
+      emul_c.resize(emul.size());
+      for (size_t r = 0; r < emul.size(); ++r) emul_c[r] = pref[emul[r]];
+      rank_order_rows(Ac, emul_c, emul_c);
+    }
     double t4 = now();
     t_r += t4 - t3;
     L.cf.swap(cf);
@@ -1438,6 +1560,10 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     H.log += buf;
     H.lev.emplace_back();
     H.lev[level + 1].A.swap(Ac);
+    if (!emul.empty()) {
+      emul.swap(emul_c);
+      lev_starts.push_back(emul);
+    }
     ++level;
     if (coarsen_type > 0 && coarse_size >= (int)(fine_size * 0.75)) {
       // par_amg_setup.c:2858 switches to CLJP; not available in this build.
@@ -1465,7 +1591,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H) {
     // par_amg_setup.c:3139: Chebyshev (relax 16) eigenvalue estimate and coefficients
     if (prm.relax_type[1] == 16 || prm.relax_type[2] == 16 || (prm.relax_type[3] == 16 && j == nl - 1)) {
       double max_eig = 0.0, min_eig = 0.0;
-      if (prm.cheby_eig_est) max_eig_estimate_cg(L.A, prm.cheby_scale, prm.cheby_eig_est, &max_eig, &min_eig);
+      if (prm.cheby_eig_est)
+        max_eig_estimate_cg(L.A, prm.cheby_scale, prm.cheby_eig_est, &max_eig, &min_eig,
+                            lev_starts.empty() ? nullptr : &lev_starts[j]);
       else max_eig_estimate_norm(L.A, prm.cheby_scale, &max_eig);
       L.max_eig = max_eig;
       L.min_eig = min_eig;

@@ -132,6 +132,9 @@ SIGNATURES = [
     ("HYPRE_BoomerAMGSetRelaxOrder", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetRelaxWt", _i, [_p, _d]),
     ("HYPRE_BoomerAMGSetOuterWt", _i, [_p, _d]),
+    ("HYPRE_BoomerAMGSetLevelRelaxWt", _i, [_p, _d, _i]),
+    ("HYPRE_BoomerAMGSetLevelOuterWt", _i, [_p, _d, _i]),
+    ("hypreve_BoomerAMGGetLevelWeights", _i, [_p, _i, _pd, _pd]),
     ("HYPRE_BoomerAMGSetChebyOrder", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetChebyFraction", _i, [_p, _d]),
     ("HYPRE_BoomerAMGSetChebyScale", _i, [_p, _i]),
@@ -184,6 +187,7 @@ SIGNATURES = [
     ("hypreve_BenchFineSpMVStoredBytes", _i, [_p, _pd]),
     ("hypreve_BoomerAMGGetLevelLayout", _i, [_p, _i, _i, _pi]),
     ("hypreve_BoomerAMGSetGsRankStarts", _i, [_p, _i, _pi]),
+    ("hypreve_BoomerAMGSetRankEmulation", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchLevelOpStoredBytes", _i, [_p, _i, _i, _pd]),
@@ -416,6 +420,10 @@ class BoomerAMG:
                 for kk, t in v.items():
                     check(lib().HYPRE_BoomerAMGSetCycleRelaxType(self.h, int(t), int(kk)), k)
                 continue
+            if k in ("level_relax_wt", "level_outer_wt"):  # (weight, level), ij -wl / -owl
+                fn = "HYPRE_BoomerAMGSetLevelRelaxWt" if k == "level_relax_wt" else "HYPRE_BoomerAMGSetLevelOuterWt"
+                check(getattr(lib(), fn)(self.h, float(v[0]), int(v[1])), fn)
+                continue
             if k == "cycle_num_sweeps":
                 for kk, t in v.items():
                     check(lib().HYPRE_BoomerAMGSetCycleNumSweeps(self.h, int(t), int(kk)), k)
@@ -486,7 +494,8 @@ class BoomerAMG:
     def level_vector(self, l, which):
         n = C.c_int()
         check(lib().hypreve_BoomerAMGGetLevelVector(self.h, l, which, C.byref(n), None), "GetLevelVector")
-        out = np.zeros(n.value, dtype=np.int32 if which == 0 else np.float64)  # 0 cf, 1 l1, 2 Chebyshev ds
+        # 0 cf, 1 l1, 2 Chebyshev ds, 3 hybrid-GS block starts (N-rank emulation)
+        out = np.zeros(n.value, dtype=np.int32 if which in (0, 3) else np.float64)
         if n.value:
             lib().hypreve_BoomerAMGGetLevelVector(self.h, l, which, None, out.ctypes.data_as(C.c_void_p))
         return out
@@ -518,6 +527,12 @@ class BoomerAMG:
         return dict(relax_type=rt.tolist(), num_sweeps=ns.tolist(), relax_weight=float(w[0]), omega=float(w[1]),
                     relax_order=int(misc[0]), cycle_type=int(misc[1]), num_blocks=int(misc[2]),
                     user_relax_type=int(misc[3]))
+
+    def level_weights(self, level):
+        """(relax_weight, omega) the cycle uses on level."""
+        w, o = C.c_double(), C.c_double()
+        check(lib().hypreve_BoomerAMGGetLevelWeights(self.h, level, C.byref(w), C.byref(o)), "GetLevelWeights")
+        return w.value, o.value
 
     def gs_schedule_check(self, num_blocks):
         check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
@@ -552,6 +567,15 @@ class BoomerAMG:
             return
         arr = (C.c_int * len(starts))(*[int(v) for v in starts])
         check(lib().hypreve_BoomerAMGSetGsRankStarts(self.h, len(starts) - 1, arr), "SetGsRankStarts")
+
+    def set_rank_emulation(self, starts):
+        """Reproduce a reference N-rank setup in one process (level-0 row starts,
+        N+1 entries; hypreve_BoomerAMGSetRankEmulation); None clears it."""
+        if starts is None or len(starts) <= 2:
+            check(lib().hypreve_BoomerAMGSetRankEmulation(self.h, 0, None), "SetRankEmulation")
+            return
+        arr = (C.c_int * len(starts))(*[int(v) for v in starts])
+        check(lib().hypreve_BoomerAMGSetRankEmulation(self.h, len(starts) - 1, arr), "SetRankEmulation")
 
     LAYOUTS = ("padded", "jagged", "wide", "jag-pw", "dict", "delta", "delta+vt8", "delta+vt16", "padded+vt16",
                "jagged+vt16")

@@ -166,6 +166,10 @@ HYPRE_Int HYPRE_BoomerAMGSetCycleRelaxType(HYPRE_Solver solver, HYPRE_Int relax_
 HYPRE_Int HYPRE_BoomerAMGSetRelaxOrder(HYPRE_Solver solver, HYPRE_Int relax_order); /* :770 */
 HYPRE_Int HYPRE_BoomerAMGSetRelaxWt(HYPRE_Solver solver, HYPRE_Real relax_weight); /* :805 */
 HYPRE_Int HYPRE_BoomerAMGSetOuterWt(HYPRE_Solver solver, HYPRE_Real omega);       /* :839 */
+HYPRE_Int HYPRE_BoomerAMGSetLevelRelaxWt(HYPRE_Solver solver, HYPRE_Real relax_weight,
+                                         HYPRE_Int level);                          /* :815 */
+HYPRE_Int HYPRE_BoomerAMGSetLevelOuterWt(HYPRE_Solver solver, HYPRE_Real omega,
+                                         HYPRE_Int level);                          /* :849 */
 HYPRE_Int HYPRE_BoomerAMGSetPrintLevel(HYPRE_Solver solver, HYPRE_Int print_level); /* :1103 */
 /* Chebyshev smoother (relax type 16), HYPRE_parcsr_ls.h:857-889 */
 HYPRE_Int HYPRE_BoomerAMGSetChebyOrder(HYPRE_Solver solver, HYPRE_Int order);          /* :857 */
@@ -256,6 +260,20 @@ HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
  * l1 norms to match), so its iterates equal the N-rank iterates. nranks <= 1
  * clears it. Takes effect at Setup. */
 HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver solver, HYPRE_Int nranks, const HYPRE_Int *starts);
+/* One process reproduces the setup and smoothing of a reference N-rank run
+ * (mpirun -np N) whose level-0 rows start at starts[0..nranks]: every row in
+ * ParCSR order (the rank's own columns, then the others; par_csr_matrix.c),
+ * per-rank PMIS random streams (par_indepset.c:25, seed 2747 + rank), per-rank
+ * HMIS first passes (par_coarsen.c:874 on S_diag), the CF_marker_offd
+ * semantics of par_coarsen.c:2296/2348, ext+i truncation over [P_diag | P_offd]
+ * (par_csr_matrix.c:2671), and the hybrid GS blocks of SetGsRankStarts.
+ * Coarse-level agglomeration is off (the reference has none).  This pins the
+ * product to the reference's own np > 1 saved outputs.  nranks <= 1 clears it.
+ * Takes effect at Setup; ext+i (interp_type 6), no aggressive levels. */
+/* The relaxation weight and outer weight (omega) the cycle uses on `level`. */
+HYPRE_Int hypreve_BoomerAMGGetLevelWeights(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Real *relax_weight,
+                                           HYPRE_Real *omega);
+HYPRE_Int hypreve_BoomerAMGSetRankEmulation(HYPRE_Solver solver, HYPRE_Int nranks, const HYPRE_Int *starts);
 /* Multi-rank: coarse levels with at most `rows` global rows (from the first
  * such level down) are held whole by every rank and cycled redundantly, with
  * one all-gather on the way down instead of halo exchanges on every coarse
@@ -274,7 +292,8 @@ HYPRE_Int hypreve_BoomerAMGGetLevelMatrix(HYPRE_Solver solver, HYPRE_Int level, 
                                           HYPRE_Int *nrows, HYPRE_Int *ncols, int64_t *nnz,
                                           HYPRE_Int *row_ptr, HYPRE_Int *cols, HYPRE_Real *vals);
 HYPRE_Int hypreve_BoomerAMGGetLevelVector(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,
-                                          HYPRE_Int *n, void *data); /* 0 cf (int), 1 l1, 2 Chebyshev ds (double) */
+                                          HYPRE_Int *n, void *data); /* 0 cf (int), 1 l1, 2 Chebyshev ds (double),
+                                                                        3 hybrid-GS block starts of the N-rank emulation (int) */
 /* Chebyshev data of one level: coefficient count / values (up to 5), the
  * eigenvalue estimates eig[0] = max, eig[1] = min, and params[0..2] = order,
  * scale, variant. */

@@ -94,28 +94,57 @@ static void block_range(int n, int nb, int k, int *ns, int *ne) {
   else { *ns = k * size + rest; *ne = (k + 1) * size + rest; }
 }
 
-/* hybrid GS (3 fwd, 4 bwd, 6 sym) and l1 hybrid GS (13, 14, 8), weights 1.
- * par_relax.c:354 (3), :1875 (4), :2266 (6), :3492 (8), :4340 (13), :4732 (14). */
+/* hybrid GS (3 fwd, 4 bwd, 6 sym) and l1 hybrid GS (13, 14, 8).
+ * par_relax.c:354 (3), :1875 (4), :2266 (6), :3492 (8), :4340 (13), :4732 (14).
+ * Blocks: hypre's thread partition of num_blocks (block_range), or explicit
+ * starts bst[0..nb] (the blocks an N-rank run sweeps: every rank's rows split
+ * into its threads; off-rank columns read Vext, the pre-sweep values, as
+ * off-block columns read tmp).
+ * Weights 1 (par_relax.c:1040, :4387): res = f - sum a u (the diagonal
+ * included for the l1 forms), u += res/l1 or u = res/a_ii.
+ * Weighted (relax_weight or omega != 1, par_relax.c:1277, :3150, :3785, :4544):
+ * Vtemp = tmp = u before the sweep; the diagonal entry skipped; in-block
+ * res0 -= a u, res2 += a Vtemp; off-block res -= a tmp;
+ * u *= 1 - w*omega; u += w*(omega*res + res0 + (1-omega)*res2) / d,
+ * d = a_ii or l1_i.  A symmetric sweep keeps the one Vtemp for both halves. */
 static void hybrid_gs(const orc_csr *A, const double *f, const int *cf, int relax_points,
-                      const double *l1, int nb, int fwd, int bwd, int use_l1,
-                      double *u, double *tmp) {
+                      const double *l1, int nb, const int *bst, int fwd, int bwd, int use_l1,
+                      double w, double omega, double *u, double *tmp) {
   const int n = A->nrows;
   const int *Ai = A->i, *Aj = A->j;
   const double *Aa = A->a;
+  const int weighted = (w != 1.0 || omega != 1.0);
+  const double prod = 1.0 - w * omega, omo = 1.0 - omega;
   if (nb < 1) nb = 1;
-  if (nb > 1) memcpy(tmp, u, sizeof(double) * (size_t)n);
+  if (nb > 1 || weighted) memcpy(tmp, u, sizeof(double) * (size_t)n);
   /* blocks interact only through tmp: independent, as hypre's threads are */
 #pragma omp parallel for schedule(dynamic, 1) if (nb > 1)
   for (int b = 0; b < nb; b++) {
     int ns, ne;
-    block_range(n, nb, b, &ns, &ne);
-    if (nb == 1) { ns = 0; ne = n; }
+    if (bst) { ns = bst[b]; ne = bst[b + 1]; }
+    else if (nb == 1) { ns = 0; ne = n; }
+    else block_range(n, nb, b, &ns, &ne);
     for (int pass = 0; pass < 2; pass++) {
       if ((pass == 0 && !fwd) || (pass == 1 && !bwd)) continue;
       for (int q = 0; q < ne - ns; q++) {
         const int i = pass == 0 ? ns + q : ne - 1 - q;
         if (relax_points != 0 && cf[i] != relax_points) continue;
-        if (use_l1) {
+        if (weighted) {
+          const double d = use_l1 ? l1[i] : Aa[Ai[i]];
+          if (d == 0.0) continue;
+          double res = f[i], res0 = 0.0, res2 = 0.0;
+          for (int k = Ai[i] + 1; k < Ai[i + 1]; k++) {
+            const int c = Aj[k];
+            if (c >= ns && c < ne) {
+              res0 -= Aa[k] * u[c];
+              res2 += Aa[k] * tmp[c];
+            } else {
+              res -= Aa[k] * tmp[c];
+            }
+          }
+          u[i] *= prod;
+          u[i] += w * (omega * res + res0 + omo * res2) / d;
+        } else if (use_l1) {
           if (l1[i] == 0.0) continue;
           double res = f[i];
           for (int k = Ai[i]; k < Ai[i + 1]; k++) {
@@ -140,9 +169,20 @@ static void hybrid_gs(const orc_csr *A, const double *f, const int *cf, int rela
   }
 }
 
+static int relax_impl(const orc_csr *A, const double *f, const int *cf, int relax_type,
+                      int relax_points, double relax_weight, double omega, const double *l1,
+                      int num_blocks, const int *bst, double *u, double *vtemp, double *ztemp);
+
 int orc_relax(const orc_csr *A, const double *f, const int *cf, int relax_type,
               int relax_points, double relax_weight, double omega, const double *l1,
               int num_blocks, double *u, double *vtemp, double *ztemp) {
+  return relax_impl(A, f, cf, relax_type, relax_points, relax_weight, omega, l1, num_blocks, NULL, u,
+                    vtemp, ztemp);
+}
+
+static int relax_impl(const orc_csr *A, const double *f, const int *cf, int relax_type,
+                      int relax_points, double relax_weight, double omega, const double *l1,
+                      int num_blocks, const int *bst, double *u, double *vtemp, double *ztemp) {
   const int n = A->nrows;
   const int *Ai = A->i, *Aj = A->j;
   const double *Aa = A->a;
@@ -189,11 +229,11 @@ int orc_relax(const orc_csr *A, const double *f, const int *cf, int relax_type,
       return 0;
     }
     case 3: case 4: case 6: case 8: case 13: case 14: {
-      if (relax_weight != 1.0 || omega != 1.0) return 2; /* weighted variants not restated */
       const int fwd = (relax_type == 3 || relax_type == 6 || relax_type == 8 || relax_type == 13);
       const int bwd = (relax_type == 4 || relax_type == 6 || relax_type == 8 || relax_type == 14);
       const int use_l1 = (relax_type == 8 || relax_type == 13 || relax_type == 14);
-      hybrid_gs(A, f, cf, relax_points, l1, num_blocks, fwd, bwd, use_l1, u, ztemp);
+      hybrid_gs(A, f, cf, relax_points, l1, num_blocks, bst, fwd, bwd, use_l1, relax_weight, omega, u,
+                ztemp);
       return 0;
     }
     default:
@@ -293,6 +333,12 @@ int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
   lev_counter[0] = 1;
   for (int k = 1; k < nl; k++) lev_counter[k] = amg->cycle_type;
   int level = 0, cycle_param = 1, not_finished = 1;
+  /* the level's hybrid-GS blocks: explicit (N-rank emulation) or num_blocks */
+#define RELAX(pts)                                                                              \
+  relax_impl(&amg->A[level], F[level], amg->cf[level], relax_type, (pts),                      \
+             amg->lev_weights ? amg->lev_w[level] : amg->relax_weight,                          \
+             amg->lev_weights ? amg->lev_omega[level] : amg->omega, amg->l1[level], amg->gs_blocks[level] ? amg->gs_nblocks[level] : amg->num_blocks, \
+             amg->gs_blocks[level], U[level], vtemp, ztemp)
   while (not_finished) {
     int num_sweep, relax_type;
     if (nl > 1) {
@@ -311,9 +357,7 @@ int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
         err = orc_cheby(&amg->A[level], F[level], amg->cheby_ds[level], amg->cheby_coefs[level],
                         amg->cheby_order, amg->cheby_scale, U[level], vtemp, ztemp);
       } else if (relax_type == 18 && !(amg->relax_order == 1 && cycle_param < 3)) {
-        err = orc_relax(&amg->A[level], F[level], amg->cf[level], relax_type, 0,
-                        amg->relax_weight, amg->omega, amg->l1[level], amg->num_blocks,
-                        U[level], vtemp, ztemp);
+        err = RELAX(0);
       } else {
         /* relax 18 with relax_order 1 (par_cycle.c:398-415): C/F-ordered
          * hypre_ParCSRRelax_L1_Jacobi twice; every other type through
@@ -323,13 +367,9 @@ int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
           int pts[2];
           if (cycle_param < 2) { pts[0] = 1; pts[1] = -1; } else { pts[0] = -1; pts[1] = 1; }
           for (int q = 0; q < 2 && !err; q++)
-            err = orc_relax(&amg->A[level], F[level], amg->cf[level], relax_type, pts[q],
-                            amg->relax_weight, amg->omega, amg->l1[level], amg->num_blocks,
-                            U[level], vtemp, ztemp);
+            err = RELAX(pts[q]);
         } else {
-          err = orc_relax(&amg->A[level], F[level], amg->cf[level], relax_type, 0,
-                          amg->relax_weight, amg->omega, amg->l1[level], amg->num_blocks,
-                          U[level], vtemp, ztemp);
+          err = RELAX(0);
         }
       }
       if (err) goto done;
@@ -371,6 +411,7 @@ done:
   free(ztemp);
   if (op_count) *op_count = ops;
   return err;
+#undef RELAX
 }
 
 /* ---- parcsr_ls/par_amg_solve.c:22 ---- */

@@ -47,6 +47,14 @@ typedef struct {
   const double *cheby_ds[ORC_MAX_LEVELS];
   double cheby_coefs[ORC_MAX_LEVELS][5];
   int cheby_order, cheby_scale;
+  /* optional per-level hybrid-GS block starts (gs_nblocks[l] + 1 entries):
+   * the blocks of an N-rank run; NULL = hypre's num_blocks thread partition */
+  const int *gs_blocks[ORC_MAX_LEVELS];
+  int gs_nblocks[ORC_MAX_LEVELS];
+  /* optional per-level relax_weight / omega (par_cycle.c reads
+   * relax_weight[level], omega[level]); used when lev_weights != 0 */
+  int lev_weights;
+  double lev_w[ORC_MAX_LEVELS], lev_omega[ORC_MAX_LEVELS];
 } orc_amg;
 
 /* OpenMP threads the row-parallel loops use (1 without OpenMP). */

@@ -33,7 +33,9 @@ class orc_amg(C.Structure):
                 ("relax_order", C.c_int), ("cycle_type", C.c_int), ("num_blocks", C.c_int),
                 ("R", orc_csr * MAXL),
                 ("cheby_ds", C.POINTER(C.c_double) * MAXL), ("cheby_coefs", (C.c_double * 5) * MAXL),
-                ("cheby_order", C.c_int), ("cheby_scale", C.c_int)]
+                ("cheby_order", C.c_int), ("cheby_scale", C.c_int),
+                ("gs_blocks", C.POINTER(C.c_int) * MAXL), ("gs_nblocks", C.c_int * MAXL),
+                ("lev_weights", C.c_int), ("lev_w", C.c_double * MAXL), ("lev_omega", C.c_double * MAXL)]
 
 
 _lib = None
@@ -120,6 +122,11 @@ class OracleAMG:
             if l1.size:
                 self.keep.append(l1)
                 s.l1[l] = _dp(l1)
+            gb = amg.level_vector(l, 3)
+            if gb.size > 1:
+                self.keep.append(gb)
+                s.gs_blocks[l] = _ip(gb)
+                s.gs_nblocks[l] = gb.size - 1
             if 16 in amg.relax_info()["relax_type"]:
                 ds = amg.level_vector(l, 2)
                 if ds.size:
@@ -147,6 +154,9 @@ class OracleAMG:
         s.relax_order = info["relax_order"]
         s.cycle_type = info["cycle_type"]
         s.num_blocks = info["num_blocks"] if num_blocks is None else num_blocks
+        s.lev_weights = 1
+        for l in range(nl):
+            s.lev_w[l], s.lev_omega[l] = amg.level_weights(l)
         self.s = s
 
     def solve(self, f, u, tol, max_iter, min_iter=0, converge_type=0):

@@ -1,0 +1,89 @@
+"""Inputs of the reference's np > 1 `ij` runs, rebuilt for one process.
+
+Test infrastructure: the matrix and right-hand side that `mpirun -np N ./ij
+-P p q r [-27pt] [-rhsrand]` builds (test/ij.c BuildParLaplacian[27pt],
+parcsr_ls/par_laplace.c:15 / par_laplace_27pt.c, hypre_GeneratePartitioning),
+stacked rank by rank.  Rows are in rank order and each row keeps its
+generation order; hypreve_BoomerAMGSetRankEmulation puts every row into ParCSR
+order (own columns first) and emulates the per-rank coarsening.
+"""
+import numpy as np
+import scipy.sparse as sp
+
+
+def partition(n, p):
+    """hypre_GeneratePartitioning: p pieces of n, the first n % p one longer."""
+    size, rest = n // p, n % p
+    return [i * size + min(i, rest) for i in range(p + 1)]
+
+
+def laplacian_ranks(nx, ny, nz, P, Q, R, c=(1.0, 1.0, 1.0), pt27=False):
+    """(scipy CSR, level-0 rank starts) of GenerateLaplacian / GenerateLaplacian27pt
+    on a P x Q x R process grid; rank = p + P*q + P*Q*r."""
+    xp, yp, zp = partition(nx, P), partition(ny, Q), partition(nz, R)
+    own_x = np.searchsorted(xp, np.arange(nx), side="right") - 1
+    own_y = np.searchsorted(yp, np.arange(ny), side="right") - 1
+    own_z = np.searchsorted(zp, np.arange(nz), side="right") - 1
+    offs = {}
+    o = 0
+    for r in range(R):
+        for q in range(Q):
+            for p in range(P):
+                offs[p + P * q + P * Q * r] = o
+                o += (xp[p + 1] - xp[p]) * (yp[q + 1] - yp[q]) * (zp[r + 1] - zp[r])
+
+    def gidx(ix, iy, iz):
+        p, q, r = own_x[ix], own_y[iy], own_z[iz]
+        nxl, nyl = xp[p + 1] - xp[p], yp[q + 1] - yp[q]
+        return offs[p + P * q + P * Q * r] + (ix - xp[p]) + nxl * ((iy - yp[q]) + nyl * (iz - zp[r]))
+
+    cx, cy, cz = c
+    v0 = (2 * cx if nx > 1 else 0.0) + (2 * cy if ny > 1 else 0.0) + (2 * cz if nz > 1 else 0.0)
+    ip, jj, vv, starts = [0], [], [], [0]
+    for rk in range(P * Q * R):
+        p, q, r = rk % P, (rk // P) % Q, rk // (P * Q)
+        for iz in range(zp[r], zp[r + 1]):
+            for iy in range(yp[q], yp[q + 1]):
+                for ix in range(xp[p], xp[p + 1]):
+                    row = gidx(ix, iy, iz)
+                    if pt27:
+                        ent = [(row, 26.0)]
+                        for dz in (-1, 0, 1):
+                            for dy in (-1, 0, 1):
+                                for dx in (-1, 0, 1):
+                                    jx, jy, jz = ix + dx, iy + dy, iz + dz
+                                    if (dx or dy or dz) and 0 <= jx < nx and 0 <= jy < ny and 0 <= jz < nz:
+                                        ent.append((gidx(jx, jy, jz), -1.0))
+                    else:
+                        ent = [(row, v0)]
+                        for jx, jy, jz, v in ((ix, iy, iz - 1, -cz), (ix, iy - 1, iz, -cy), (ix - 1, iy, iz, -cx),
+                                              (ix + 1, iy, iz, -cx), (ix, iy + 1, iz, -cy), (ix, iy, iz + 1, -cz)):
+                            if 0 <= jx < nx and 0 <= jy < ny and 0 <= jz < nz:
+                                ent.append((gidx(jx, jy, jz), v))
+                    for col, v in ent:
+                        jj.append(col)
+                        vv.append(v)
+                    ip.append(len(jj))
+        starts.append(len(ip) - 1)
+    n = nx * ny * nz
+    A = sp.csr_matrix((np.array(vv), np.array(jj, dtype=np.int32), np.array(ip, dtype=np.int32)), shape=(n, n))
+    return A, starts
+
+
+def rand_stream(n, seed):
+    """n draws of hypre_Rand() after hypre_SeedRand(seed) (utilities/random.c)."""
+    a, m = 16807, 2147483647
+    s = seed if seed >= 1 else 1
+    out = np.empty(n)
+    for i in range(n):
+        s = (a * s) % m
+        out[i] = s / m
+    return out
+
+
+def rhsrand(starts):
+    """ij -rhsrand (ij.c:2750): HYPRE_ParVectorSetRandomValues(b, 22775), every
+    rank seeding 22775 * (rank + 1) (par_vector.c:337), then b /= ||b||."""
+    b = np.concatenate([2.0 * rand_stream(starts[k + 1] - starts[k], 22775 * (k + 1)) - 1.0
+                        for k in range(len(starts) - 1)])
+    return b * (1.0 / np.sqrt(np.dot(b, b)))

@@ -1,0 +1,116 @@
+"""Host setup + oracle pinned to the reference's own saved outputs of np > 1
+`ij` runs (tests/golden/ij_rank_fixtures.json, from src/test/TEST_ij/*.saved).
+
+One process reproduces an N-rank reference run through
+hypreve_BoomerAMGSetRankEmulation: every row in ParCSR order (own columns,
+then the rest), per-rank PMIS random streams (par_indepset.c:25), per-rank
+HMIS first passes (par_coarsen.c:874), CF_marker_offd semantics
+(par_coarsen.c:2296/2348), ext+i truncation over [P_diag | P_offd]
+(par_csr_matrix.c:2671), per-rank random vectors in the Chebyshev eigenvalue
+estimate (par_relax_more.c:209) and one hybrid-GS block per rank
+(par_relax.c with num_procs > 1).  The inputs are the -P process grid's
+GenerateLaplacian[27pt] matrix and ij -rhsrand's per-rank random right-hand
+side (tests/ij_emul.py).
+
+This pins, against reference-held numbers: PMIS, PMIS1 and HMIS; ext+i with
+Pmx 0 and 4; 7- and 27-point operators; relax 0 and 18 C/F-ordered, 18, the
+l1 hybrid GS 13/14 (also C/F-ordered and weighted, w = 1.1), hybrid GS 4 up,
+8 under PCG, Chebyshev (order 2/3, unscaled, variant 1) and BoomerAMG-PCG.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import ij_emul
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CASES = json.load(open(os.path.join(HERE, "golden", "ij_rank_fixtures.json")))["cases"]
+
+
+def build(hv, case):
+    prob = case["problem"]
+    A_s, starts = ij_emul.laplacian_ranks(*prob["n"], *prob["P"], c=tuple(prob.get("c", (1.0, 1.0, 1.0))),
+                                          pt27=prob["stencil"] == 27)
+    A = hv.ParCSRMatrix.from_scipy(A_s)
+    kw = hv.ij_amg_defaults(0 if case["solver"] == "amg" else 1)
+    kw.update(num_blocks=1)
+    st = dict(case["settings"])
+    if "cycle_relax_type" in st:
+        st["cycle_relax_type"] = {int(k): v for k, v in st["cycle_relax_type"].items()}
+    kw.update(st)
+    amg = hv.BoomerAMG(**kw)
+    amg.set_rank_emulation(starts)
+    b = ij_emul.rhsrand(starts) if case["rhs"] == "rhsrand" else np.ones(A.n)
+    return A, amg, b, starts
+
+
+def check_stats(case, amg, st=None, it=None, rr=None):
+    exp = case["expect"]
+    if "grid" in exp:
+        g, o, _ = amg.complexities()
+        assert f"{g:f}" == f"{exp['grid']:f}"
+        assert f"{o:f}" == f"{exp['operator']:f}"
+    if "conv_factor" in exp:
+        assert f"{st['conv_factor']:f}" == f"{exp['conv_factor']:f}"
+        assert abs(st["cycle_complexity"] - exp["cycle"]) < 1.5e-6
+    if "iterations" in exp:
+        assert it == exp["iterations"]
+        assert f"{rr:e}" == f"{exp['rel_res']:e}"
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
+def test_rank_fixture(hv, orc, case):
+    A, amg, b, _ = build(hv, case)
+    amg.setup_host(A)
+    O = orc.OracleAMG(amg)
+    x = np.zeros(A.n)
+    if case["solver"] == "amg":
+        st = O.solve(b, x, 1e-8, 100)
+        check_stats(case, amg, st, st["iterations"], st["rel_res"])
+    else:
+        it, rr = O.pcg(b, x, 1e-8, 1000, 1)
+        check_stats(case, amg, None, it, rr)
+    amg.destroy()
+    A.destroy()
+
+
+def test_emulation_has_teeth(hv, orc):
+    """Without the emulation (one process over the same matrix) coarsening.out.13
+    and smoother.out.0 give other numbers: the pins depend on the per-rank
+    behaviour, not just on the matrix."""
+    for name in ("coarsening.out.13", "smoother.out.0"):
+        case = next(c for c in CASES if c["name"] == name)
+        A, amg, b, _ = build(hv, case)
+        amg.set_rank_emulation(None)
+        amg.setup_host(A)
+        st = orc.OracleAMG(amg).solve(b, np.zeros(A.n), 1e-8, 100)
+        exp = case["expect"]
+        same = (st["iterations"] == exp.get("iterations") and f"{st['rel_res']:e}" == f"{exp.get('rel_res', 0):e}") \
+            or f"{st['conv_factor']:f}" == f"{exp.get('conv_factor', -1):f}"
+        assert not same, name
+
+
+def test_rank_order_rows(hv):
+    """Every level's rows are in ParCSR order under the emulation: the rank's own
+    columns (diagonal first) before the other ranks' columns."""
+    case = next(c for c in CASES if c["name"] == "interp.out.3")
+    A, amg, b, starts = build(hv, case)
+    amg.setup_host(A)
+    rs = list(starts)
+    for l in range(amg.num_levels()):
+        ip, jj, vv, (nr, nc) = amg.level_matrix(l, 0)
+        own = np.searchsorted(rs, np.arange(nr), side="right") - 1
+        for i in range(nr):
+            cols = jj[ip[i]:ip[i + 1]]
+            if len(cols):
+                assert cols[0] == i
+            mine = own[np.clip(cols, 0, nr - 1)] == own[i]
+            # own-rank entries form a prefix of the row
+            k = int(np.argmin(mine)) if not mine.all() else len(mine)
+            assert mine[:k].all() and not mine[k:].any()
+        if l + 1 < amg.num_levels():
+            cf = amg.level_vector(l, 0)
+            pref = np.concatenate([[0], np.cumsum(cf == 1)])
+            rs = [int(pref[s]) for s in rs]
