@@ -38,6 +38,7 @@ KERNEL_OF_LAYOUT = {
                    "SELL-64 with 16-bit column deltas and a 16-bit value table"),
     "delta": ("k_sell_delta<0, false, |, true, 0>(hve::SpArgs)", "SELL-64 with 16-bit column deltas"),
     "dict": ("k_sell_dict<0, false, |, true, ", "jagged SELL-64 with an LDS x-tile dictionary"),
+    "dict-ranges": ("k_sell_dict<0, false, |, true, ", "jagged SELL-64 with an LDS x-tile of column ranges"),
     "padded": ("k_sell<0, false, |, ", "padded SELL-64"),
     "jagged": ("k_sell<0, false, |, ", "jagged SELL-64"),
     "wide": ("k_sell_wide<0, false, |", "padded SELL-64, one workgroup per slice"),
@@ -244,6 +245,10 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
     # the box's achievable read bandwidth: a grid-stride 8 B/lane stream over 2 GiB
     stream_n = (1 << 31) // 8
     stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 3 if light else 10) * 1e-3) / 1e9
+    # and its read/write mix: 5 double streams read and one written per element
+    # (48 B; the finest residual reads ~4.8 bytes for each one it writes)
+    mix_n = (1 << 27)
+    mix_gbs = mix_n * 48 / (hv.bench_stream(-5, mix_n, 3 if light else 10) * 1e-3) / 1e9
     if args.calib:
         for eb in (2, 4, 8):
             hv.bench_stream(eb, (1 << 29) // eb, 1)
@@ -254,10 +259,12 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
             "avg_ms": round(spmv_ms, 4), "bytes_per_launch": stored_bytes,
             "csr_bytes_per_launch": csr_bytes, "csr_equivalent_gbs": round(csr_gbs, 1),
             "stream_read_gbs": round(stream_gbs, 1), "frac_of_stream": round(achieved / stream_gbs, 4),
+            "stream_mix_gbs": round(mix_gbs, 1), "frac_of_mix_stream": round(achieved / mix_gbs, 4),
             "per_kernel": per_kernel}
     if rank == 0:
         import resource
-        log(f"[bench] read stream {stream_gbs:.0f} GB/s; fine SpMV at {achieved / stream_gbs:.3f} of it")
+        log(f"[bench] read stream {stream_gbs:.0f} GB/s, 5:1 read/write mix {mix_gbs:.0f} GB/s; "
+            f"fine SpMV at {achieved / stream_gbs:.3f} / {achieved / mix_gbs:.3f} of them")
         log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {stored_bytes/1e9:.3f} GB stored -> {achieved:.1f} GB/s "
             f"(CSR-equivalent {csr_gbs:.1f} GB/s); "
             f"host peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6:.1f} GB")

@@ -802,17 +802,18 @@ HYPRE_Int hypreve_BoomerAMGSetRankEmulation(HYPRE_Solver s, HYPRE_Int nranks, co
 // Tuning: re-key the row-block traversal of the built device hierarchy with
 // nbands bands of the grid's y extent (0: natural order; default at Setup:
 // HVE_BLOCK_ORDER, 8).  Only the visiting order of row blocks changes.
-HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands) {
+HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands, HYPRE_Int which_mask) {
   CHECK_ARG(s && s->kind == KIND_AMG && s->dev && s->dev->built(), 1);
   CHECK_ARG(nbands >= 0, 2);
+  CHECK_ARG(which_mask >= 0 && which_mask <= 7, 3);
   API_BEGIN
-  s->dev->set_block_bands(s->RH, nbands);
+  s->dev->set_block_bands(s->RH, nbands, which_mask ? which_mask : 7);
   HVE_HIP(hipDeviceSynchronize());
   API_END
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  CHECK_ARG(policy >= 0 && policy <= 9, 2);
+  CHECK_ARG(policy >= 0 && policy <= 10, 2);
   s->prm.sell_policy = policy;
   return 0;
 }
@@ -1309,7 +1310,7 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver s, HYPRE_Real* bytes) {
 // 0 padded SELL-64, 1 jagged, 2 workgroup-per-slice, 3 jagged wave-product,
 // 4 dictionary (LDS x-tile), 5 16-bit column deltas, 6 deltas + 8-bit value
 // table, 7 deltas + 16-bit value table, 8 padded + 16-bit value table,
-// 9 jagged + 16-bit value table.
+// 9 jagged + 16-bit value table, 10 range dictionary.
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int* kind) {
   CHECK_ARG(s && s->dev && s->dev->built() && kind, 1);
   CHECK_ARG(level >= 0 && level < s->dev->num_levels(), 2);
@@ -1318,7 +1319,8 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE
   const DevLevel& L = s->dev->level(level);
   const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
   *kind = M.dcol ? (M.vidx16 ? 7 : M.vidx ? 6 : 5)
-                 : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? 4 : M.pw ? 3 : M.rowlen ? 1 : M.wide ? 2 : 0;
+                 : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? (M.dict_ranges ? 10 : 4) : M.pw ? 3 : M.rowlen ? 1
+                 : M.wide ? 2 : 0;
   API_END
 }
 
@@ -1413,10 +1415,36 @@ HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver s, HYPRE_Int level, HYPRE
 // calibration pass for rocprofv3 FETCH_SIZE at this access width and the
 // achievable-bandwidth reference for the roofline.
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real* avg_ms) {
-  CHECK_ARG(elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16, 1);
+  CHECK_ARG(elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16 || elem_bytes == -1 ||
+                elem_bytes == -2 || elem_bytes == -5,
+            1);
   CHECK_ARG(n > 0, 2);
   CHECK_ARG(reps > 0, 3);
   API_BEGIN
+  if (elem_bytes < 0) {  // read/write mix: -R = R double reads + 1 double write per element
+    const int R = -elem_bytes;
+    double *src = nullptr, *y = nullptr;
+    hipStream_t st = lib_stream();
+    HVE_HIP(hipMalloc((void**)&src, (size_t)n * R * sizeof(double)));
+    HVE_HIP(hipMalloc((void**)&y, (size_t)n * sizeof(double)));
+    HVE_HIP(hipMemsetAsync(src, 0, (size_t)n * R * sizeof(double), st));
+    for (int w = 0; w < 2; ++w) HVE_HIP(launch_stream_mix(n, R, src, y, st));
+    hipEvent_t e0, e1;
+    HVE_HIP(hipEventCreate(&e0));
+    HVE_HIP(hipEventCreate(&e1));
+    HVE_HIP(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; ++r) HVE_HIP(launch_stream_mix(n, R, src, y, st));
+    HVE_HIP(hipEventRecord(e1, st));
+    HVE_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HVE_HIP(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    (void)hipFree(src);
+    (void)hipFree(y);
+    if (avg_ms) *avg_ms = ms / reps;
+    return 0;
+  }
   void* buf = nullptr;
   double* out = nullptr;
   hipStream_t st = lib_stream();

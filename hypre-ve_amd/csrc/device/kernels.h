@@ -22,6 +22,7 @@ struct SellView {
   const int* dict = nullptr;
   int dmax = 0;                    // dictionary layout: largest dictionary (LDS doubles)
   int dict_group = 1;              // dictionary layout: slices per dictionary / workgroup (1 or 4)
+  int dict_ranges = 0;             // dictionary layout: 1 = (start, offset) column ranges
   const short* dcol = nullptr;     // delta layout (k_sell_delta): col - row - slot base, padded
   const int* slot_base = nullptr;  // delta layout: base offset per (slice, slot)
   const unsigned char* vidx = nullptr;  // delta layout: 8-bit value indices (val unused)
@@ -69,6 +70,9 @@ int sell_batch_override();
 int sell_pipe_override();
 bool sell_nt();
 bool sell_pw();
+// y = sum of `reads` (1, 2 or 5) consecutive n-double streams of src: a
+// read/write mix of reads*8 B in and 8 B out per element.
+hipError_t launch_stream_mix(int64_t n, int reads, const double* src, double* y, hipStream_t st);
 hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, double* out, hipStream_t st);
 hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st);
 hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,

@@ -68,6 +68,8 @@ struct SpArgs {
   const unsigned short* __restrict__ col16;  // dictionary layout: local column of each entry
   const int* __restrict__ dict_ptr;          // dictionary layout: per-slice range of dict
   const int* __restrict__ dict;              // dictionary layout: distinct columns, ascending
+                                             // (dict_ranges: (start, offset) pairs of column ranges)
+  int dict_ranges;                           // 1: range dictionary (k_sell_dict phase 1 copies ranges)
   const short* __restrict__ dcol;            // delta layout: col - row - slot base
   const int* __restrict__ slot_base;         // delta layout: per (slice, slot) base offset
   const unsigned char* __restrict__ vidx;    // delta layout, value table: entry -> vtab index
@@ -740,6 +742,9 @@ __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp,
   }
 }
 
+#ifndef HVE_DICT_TG
+#define HVE_DICT_TG (G == 4 ? 12 : 16 / G > 4 ? 16 / G : 4)
+#endif
 template <int OP, bool CFSEL, int B, bool NT, int G>
 __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   extern __shared__ double xl[];
@@ -780,10 +785,48 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   int c[B];
   double a[B];
   dict_load<B, NT>(cp, vp, P, k0, blen, llen, c, a);
-  // 1. x-tile: x[dict[d0 .. d1)] -> LDS, TG gathers in flight per thread
-  {
-    constexpr int TG = 16 / G > 4 ? 16 / G : 4;
-    constexpr int NT_ = 64 * G;
+  // 1. x-tile -> LDS, TG loads in flight per thread
+  constexpr int TG = HVE_DICT_TG;
+  constexpr int NT_ = 64 * G;
+  if (p.dict_ranges) {
+    // Range dictionary: the tile is the concatenation of at most 63 column
+    // ranges; lane k of every wave holds pair k (start, offset; the terminal
+    // pair's offset is the tile length).  Each position finds its range by a
+    // binary search over the lanes, so the copies are independent loads of
+    // consecutive columns.
+    const int r0 = p.dict_ptr[group], nrp = p.dict_ptr[group + 1] - r0;
+    const int* __restrict__ rp = p.dict + 2 * r0;
+    const int rst = lane < nrp ? rp[2 * lane] : 0x7fffffff;
+    const int rof = lane < nrp ? rp[2 * lane + 1] : 0x7fffffff;
+    const int m = __shfl(rof, nrp - 1);
+    for (int j0 = 0; j0 < m; j0 += TG * NT_) {
+      int cix[TG];
+#pragma unroll
+      for (int i = 0; i < TG; ++i) {
+        const int pos = j0 + i * NT_ + (int)threadIdx.x;
+        const int q = pos < m ? pos : m - 1;
+        int lo = 0, hi = nrp - 2;
+#pragma unroll
+        for (int it = 0; it < 6; ++it) {
+          const int mid = (lo + hi + 1) >> 1;
+          const int o = __shfl(rof, mid);
+          if (o <= q) lo = mid;
+          else hi = mid - 1;
+        }
+        const int st = __shfl(rst, lo), of = __shfl(rof, lo);
+        cix[i] = pos < m ? st + (q - of) : -1;
+      }
+      double v[TG];
+#pragma unroll
+      for (int i = 0; i < TG; ++i) v[i] = cix[i] >= 0 ? p.x[cix[i]] : 0.0;
+#pragma unroll
+      for (int i = 0; i < TG; ++i) {
+        const int pos = j0 + i * NT_ + (int)threadIdx.x;
+        if (pos < m) xl[pos] = v[i];
+      }
+    }
+  } else {
+    // x[dict[d0 .. d1)]: the ascending distinct columns, gathered
     const int d0 = p.dict_ptr[group], m = p.dict_ptr[group + 1] - d0;
     for (int j0 = 0; j0 < m; j0 += TG * NT_) {
       int idx[TG];
@@ -1127,6 +1170,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   a.col16 = M.col16;
   a.dict_ptr = M.dict_ptr;
   a.dict = M.dict;
+  a.dict_ranges = M.dict_ranges;
   a.dcol = M.dcol;
   a.slot_base = M.slot_base;
   a.vidx = M.vidx;
@@ -1354,6 +1398,27 @@ hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, 
   else if (elem_bytes == 4) hipLaunchKernelGGL(k_stream_read<int>, grid, block, 0, st, n, (const int*)buf, out);
   else if (elem_bytes == 8) hipLaunchKernelGGL(k_stream_read<double>, grid, block, 0, st, n, (const double*)buf, out);
   else hipLaunchKernelGGL(k_stream_read<int4>, grid, block, 0, st, n, (const int4*)buf, out);
+  return hipGetLastError();
+}
+
+// Read/write mix: y[i] = sum of R streams (doubles), R reads + 1 write per
+// element, grid-stride; the ceiling for kernels that read ~R bytes per byte
+// written (the finest residual reads ~4.8 for each one it writes).
+template <int R>
+__global__ void __launch_bounds__(256) k_stream_mix(int64_t n, const double* __restrict__ src, double* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc += __builtin_nontemporal_load(src + (int64_t)r * n + i);
+    __builtin_nontemporal_store(acc, y + i);
+  }
+}
+hipError_t launch_stream_mix(int64_t n, int reads, const double* src, double* y, hipStream_t st) {
+  const dim3 grid(256 * 16), block(256);
+  if (reads == 1) hipLaunchKernelGGL(k_stream_mix<1>, grid, block, 0, st, n, src, y);
+  else if (reads == 2) hipLaunchKernelGGL(k_stream_mix<2>, grid, block, 0, st, n, src, y);
+  else if (reads == 5) hipLaunchKernelGGL(k_stream_mix<5>, grid, block, 0, st, n, src, y);
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -136,7 +136,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
     wide = policy == 3 ? 1 : 0;
     jag = (policy == 2 || policy == 4 || policy == 9) && A.nnz() > 0;
     pw = policy == 4 && jag;
-    use_dict = policy == 5 && A.nnz() > 0;
+    use_dict = (policy == 5 || policy == 10) && A.nnz() > 0;
   }
   // 16-bit column deltas against per-(slice, slot) bases where the padded
   // layout stays and rows are stencil-long (the finest A): 10 B an entry
@@ -234,13 +234,39 @@ dict:
     }();
     int group = (group_env == 1 || group_env == 2 || group_env == 4 || group_env == 8) ? group_env
                                                                                      : (A.nrows == A.ncols ? 4 : 1);
-    bool built = build_sell_dict_host(A, group > 1 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd);
-    if (!built && group > 1 && group_env == 0) {
-      group = 1;
-      built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd);
+    // Range dictionary (square operators: the x-tile as at most 63 column
+    // ranges, copied instead of gathered through a 4-byte index list) where
+    // the ranges cover at most 1.5x the distinct columns.  Measured on MI355X:
+    // A_1 at 256^3 411 vs 412 us, at 512^3 4.31 vs 3.66 ms (the larger tiles
+    // cost occupancy), so it is off by default: HVE_DICT_RANGES=1 turns it on,
+    // policy 10 forces it (tests).
+    static const int ranges_env = [] {
+      const char* e = getenv("HVE_DICT_RANGES");
+      return e ? atoi(e) : 0;
+    }();
+    const bool try_ranges = policy == 10 || (policy == 0 && ranges_env != 0 && A.nrows == A.ncols);
+    bool built = false, ranges = false;
+    if (try_ranges) {
+      built = build_sell_dict_host(A, group > 1 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd, 63,
+                                   policy == 10 ? 1e30 : 1.5);
+      if (!built && group > 1 && group_env == 0) {
+        group = 1;
+        built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd, 63, policy == 10 ? 1e30 : 1.5);
+      }
+      ranges = built;
+      if (!built) group = (group_env == 1 || group_env == 2 || group_env == 4 || group_env == 8) ? group_env
+                                                                                          : (A.nrows == A.ncols ? 4 : 1);
+    }
+    if (!built && policy != 10) {
+      built = build_sell_dict_host(A, group > 1 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd);
+      if (!built && group > 1 && group_env == 0) {
+        group = 1;
+        built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd);
+      }
     }
     if (built) {
       dict_group = group;
+      dict_ranges = ranges ? 1 : 0;
       nrows = A.nrows;
       ncols = A.ncols;
       nslices = (int)sp.size() - 1;
@@ -260,7 +286,7 @@ dict:
       this->val = dupload(val.data(), val.size());
       dict_ptr = dupload(dp.data(), dp.size());
       dict = dupload(dc.data(), std::max<size_t>(1, dc.size()));
-      ndict = (int64_t)dc.size();
+      ndict = (int64_t)dc.size();  // ints: distinct columns, or 2 per range pair
       std::vector<int> map(A.nrows);
       for (int i = 0; i < A.nrows; ++i) map[i] = rowmap_h.empty() ? perm[i] : rowmap_h[perm[i]];
       bool ident = true;
@@ -396,7 +422,7 @@ void DevSell::release() {
   stored_map.shrink_to_fit();
   dcol = nullptr; slot_base = nullptr; vidx = nullptr; vidx16 = nullptr; vtab = nullptr; nvtab = 0;
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
-  col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1; ndict = 0;
+  col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1; dict_ranges = 0; ndict = 0;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;
 }
 
@@ -596,6 +622,18 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     return e ? atoi(e) : 8;  // bands of the grid's y extent; 0 = natural order
   }();
   locality_keys(R, agg_level_, nbands_env, keys);
+  // Restrictions gather from a window of ~10 fine planes per in-flight coarse
+  // row range (R_0: the fine residual), wider than A's 3 planes, so they keep
+  // it in L2 with narrower bands.  Measured on MI355X (512^3, R_0 alone):
+  // 0 / 8 / 16 / 32 / 64 / 128 / 256 bands 1.92 / 1.81 / 1.67 / 1.63 / 1.61 /
+  // 1.62 / 1.78 ms; A_0 and P_0 are best at 8.  HVE_BLOCK_ORDER_R overrides.
+  static const int nbands_r_env = [] {
+    const char* e = getenv("HVE_BLOCK_ORDER_R");
+    return e ? atoi(e) : 32;
+  }();
+  std::vector<std::vector<int64_t>> keys_r;
+  if (nbands_r_env != nbands_env) locality_keys(R, agg_level_, nbands_r_env, keys_r);
+  const std::vector<std::vector<int64_t>>& kr = nbands_r_env != nbands_env ? keys_r : keys;
   for (int l = 0; l < nl; ++l) {
     const RankLevel& L = R.lev[l];
     DevLevel& D = lev_[l];
@@ -604,7 +642,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     D.n_glob = L.n_glob;
     // A_l and P_l rows are level-l rows; R_l rows are level-(l+1) rows
     const std::vector<int64_t>* kl = keys[l].empty() ? nullptr : &keys[l];
-    const std::vector<int64_t>* kc = (l + 1 < nl && !keys[l + 1].empty()) ? &keys[l + 1] : nullptr;
+    const std::vector<int64_t>* kc = (l + 1 < nl && !kr[l + 1].empty()) ? &kr[l + 1] : nullptr;
     D.A.upload(L.A, prm.sell_policy, kl);
     D.hu.upload(L.hu);
     if (l < nl - 1) {
@@ -695,7 +733,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
 
 // Re-key the traversal of every interior operator with `nbands` bands (0:
 // natural order) on the built hierarchy (tuning: the operators stay in place).
-void DevAMG::set_block_bands(const RankHierarchy& R, int nbands) {
+void DevAMG::set_block_bands(const RankHierarchy& R, int nbands, int which_mask) {
   std::vector<std::vector<int64_t>> keys;
   locality_keys(R, agg_level_, nbands, keys);
   const int nl = (int)lev_.size();
@@ -712,10 +750,10 @@ void DevAMG::set_block_bands(const RankHierarchy& R, int nbands) {
       if (!k.empty() && M.stored_map.size() == (size_t)M.nrows) M.set_block_order(M.stored_map, k);
       else if (!k.empty() && !M.rowmap) M.set_block_order(map, k);
     };
-    redo(D.A.in, kl, {});
+    if (which_mask & 1) redo(D.A.in, kl, {});
     if (l < nl - 1) {
-      redo(D.P.in, kl, {});
-      redo(D.R.in, kc, {});
+      if (which_mask & 2) redo(D.P.in, kl, {});
+      if (which_mask & 4) redo(D.R.in, kc, {});
     }
     (void)L;
   }

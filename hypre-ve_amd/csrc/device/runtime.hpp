@@ -38,6 +38,7 @@ struct DevSell {
   int* dict = nullptr;
   int dmax = 0;
   int dict_group = 1;
+  int dict_ranges = 0;     // dictionary layout: the tile is a union of column ranges
   short* dcol = nullptr;   // delta layout: 16-bit column deltas
   int* slot_base = nullptr;
   unsigned char* vidx = nullptr;  // delta layout with a value table
@@ -54,7 +55,7 @@ struct DevSell {
   SellView view() const {
     SellView v;
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
-    v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group;
+    v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group; v.dict_ranges = dict_ranges;
     v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vidx16 = vidx16; v.vtab = vtab; v.nvtab = nvtab;
     v.blk_map = blk_map; v.nblk = nblk;
     return v;
@@ -180,7 +181,8 @@ class DevAMG {
   double cycle_op_count() const { return cycle_ops_; }
   bool multi_rank() const { return comm_ != nullptr; }
   // Re-key the row-block traversal (tuning; see locality_keys in runtime.hip).
-  void set_block_bands(const RankHierarchy& R, int nbands);
+  // which_mask: bit 0 the A operators, bit 1 P, bit 2 R
+  void set_block_bands(const RankHierarchy& R, int nbands, int which_mask = 7);
   void graphs_clear();
 
   AMGParams prm;

@@ -258,9 +258,51 @@ void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<in
 // loop.  Entry order, row order (sorted inside the slice) and rowlen are those
 // of build_sell_jagged_host.  Returns false (and builds nothing) when a slice
 // references more than dmax distinct columns.
+// Ranges covering the ascending distinct columns `cols` with at most
+// max_ranges pieces: break at the max_ranges - 1 largest holes.  rs gets
+// (start, offset) pairs and the terminal (-1, covered).
+static void cover_ranges(const std::vector<int>& cols, int max_ranges, std::vector<int>& rs) {
+  rs.clear();
+  if (cols.empty()) {
+    rs.push_back(-1);
+    rs.push_back(0);
+    return;
+  }
+  const int m = (int)cols.size();
+  std::vector<int> brk;  // positions i where a new range starts at cols[i]
+  {
+    std::vector<std::pair<int, int>> holes;  // (hole size, position)
+    for (int i = 1; i < m; ++i)
+      if (cols[i] - cols[i - 1] > 1) holes.push_back({cols[i] - cols[i - 1] - 1, i});
+    const size_t keep = std::min<size_t>(holes.size(), (size_t)std::max(0, max_ranges - 1));
+    std::partial_sort(holes.begin(), holes.begin() + keep, holes.end(),
+                      [](const std::pair<int, int>& a, const std::pair<int, int>& b) {
+                        return a.first != b.first ? a.first > b.first : a.second < b.second;
+                      });
+    for (size_t k = 0; k < keep; ++k) brk.push_back(holes[k].second);
+    std::sort(brk.begin(), brk.end());
+  }
+  int off = 0, start = cols[0];
+  size_t bi = 0;
+  for (int i = 1; i <= m; ++i) {
+    if (i == m || (bi < brk.size() && brk[bi] == i)) {
+      rs.push_back(start);
+      rs.push_back(off);
+      off += cols[i - 1] - start + 1;
+      if (i < m) {
+        start = cols[i];
+        ++bi;
+      }
+    }
+  }
+  rs.push_back(-1);
+  rs.push_back(off);
+}
+
 bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& perm, std::vector<int>& slice_ptr,
                           std::vector<int>& rowlen, std::vector<unsigned short>& col16, std::vector<double>& val,
-                          std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct) {
+                          std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct, int max_ranges,
+                          double max_cover) {
   if (dmax > 65535) dmax = 65535;
   if (group < 1) group = 1;
   const int n = A.nrows;
@@ -276,17 +318,29 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
     std::sort(cols.begin(), cols.end());
     cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
   };
+  const bool ranges = max_ranges > 0;
   std::vector<int64_t> dcount(ng, 0);
   int mx = 0;
-#pragma omp parallel for schedule(static) reduction(max : mx)
+  int64_t tot_distinct = 0, tot_cover = 0;
+#pragma omp parallel for schedule(static) reduction(max : mx) reduction(+ : tot_distinct, tot_cover)
   for (int g = 0; g < ng; ++g) {
-    std::vector<int> cols;
+    std::vector<int> cols, rs;
     group_cols(g, cols);
-    dcount[g] = (int64_t)cols.size();
-    mx = std::max(mx, (int)cols.size());
+    int cover = (int)cols.size();
+    if (ranges) {
+      cover_ranges(cols, max_ranges, rs);
+      cover = rs.back();
+      dcount[g] = (int64_t)rs.size() / 2;  // pairs, terminal included
+    } else {
+      dcount[g] = (int64_t)cols.size();
+    }
+    tot_distinct += (int64_t)cols.size();
+    tot_cover += cover;
+    mx = std::max(mx, cover);
   }
   max_distinct = mx;
   if (mx > dmax) return false;
+  if (ranges && (double)tot_cover > max_cover * (double)std::max<int64_t>(1, tot_distinct)) return false;
   std::vector<int64_t> sp(ns + 1, 0), dp(ng + 1, 0);
   for (int s = 0; s < ns; ++s) {
     int64_t t = 0;
@@ -303,12 +357,29 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
   rowlen.assign((size_t)ns * 64, 0);
   col16.assign((size_t)sp[ns], 0xFFFF);
   val.assign((size_t)sp[ns], 0.0);
-  dict.assign((size_t)dp[ng], 0);
+  dict.assign((size_t)dp[ng] * (ranges ? 2 : 1), 0);
 #pragma omp parallel for schedule(static)
   for (int g = 0; g < ng; ++g) {
-    std::vector<int> cols;
+    std::vector<int> cols, rs;
     group_cols(g, cols);
-    std::copy(cols.begin(), cols.end(), dict.begin() + dict_ptr[g]);
+    if (ranges) {
+      cover_ranges(cols, max_ranges, rs);
+      std::copy(rs.begin(), rs.end(), dict.begin() + 2 * (size_t)dict_ptr[g]);
+    } else {
+      std::copy(cols.begin(), cols.end(), dict.begin() + dict_ptr[g]);
+    }
+    const int nrg = (int)rs.size() / 2 - 1;
+    // position of column c in the group's x-tile
+    auto local = [&](int c) -> int {
+      if (!ranges) return (int)(std::lower_bound(cols.begin(), cols.end(), c) - cols.begin());
+      int lo = 0, hi = nrg - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) / 2;
+        if (rs[2 * mid] <= c) lo = mid;
+        else hi = mid - 1;
+      }
+      return rs[2 * lo + 1] + (c - rs[2 * lo]);
+    };
     for (int s = g * group; s < std::min(ns, (g + 1) * group); ++s) {
       const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
       int len[64] = {0};
@@ -323,7 +394,7 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
         for (int l = 0; l < cnt; ++l) {
           const int src = perm[r0 + l];
           const int c = A.j[A.i[src] + k];
-          col16[pos + l] = (unsigned short)(std::lower_bound(cols.begin(), cols.end(), c) - cols.begin());
+          col16[pos + l] = (unsigned short)local(c);
           val[pos + l] = A.a[A.i[src] + k];
         }
         pos += cnt;

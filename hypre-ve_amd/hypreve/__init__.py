@@ -44,7 +44,9 @@ def lib() -> C.CDLL:
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"{LIB_PATH} is missing: run `make -C hypre-ve_amd` (no fallback path exists)")
-        _lib = C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+        # HVE_LIB_PATH: another build of the same sources (A/B experiments on
+        # compile-time variants); the default is the in-tree library
+        _lib = C.CDLL(os.environ.get("HVE_LIB_PATH", LIB_PATH), mode=C.RTLD_GLOBAL)
         _declare(_lib)
     return _lib
 
@@ -168,7 +170,7 @@ SIGNATURES = [
     ("hypreve_ParVectorCopyFromHost", _i, [_p, _pd]),
     ("hypreve_ParVectorSetRandomValues", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetNumBlocks", _i, [_p, _i]),
-    ("hypreve_BoomerAMGSetBlockBands", _i, [_p, _i]),
+    ("hypreve_BoomerAMGSetBlockBands", _i, [_p, _i, _i]),
     ("hypreve_BoomerAMGSetUseGraph", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetSellPolicy", _i, [_p, _i]),
     ("hypreve_BoomerAMGSetAggloRows", _i, [_p, _i]),
@@ -544,9 +546,11 @@ class BoomerAMG:
               "BenchLevelOp")
         return ms.value, by.value, pz.value
 
-    def set_block_bands(self, nbands):
-        """Re-key the row-block traversal (0 = natural order); tuning only."""
-        check(lib().hypreve_BoomerAMGSetBlockBands(self.h, int(nbands)), "SetBlockBands")
+    def set_block_bands(self, nbands, which="APR"):
+        """Re-key the row-block traversal of the A / P / R operators (0 bands =
+        natural order); tuning only."""
+        mask = (1 if "A" in which else 0) | (2 if "P" in which else 0) | (4 if "R" in which else 0)
+        check(lib().hypreve_BoomerAMGSetBlockBands(self.h, int(nbands), mask), "SetBlockBands")
 
     def level_op_stored_bytes(self, level, which=0):
         """Bytes one bench_level_op launch streams in the stored layout (+ vectors)."""
@@ -578,7 +582,7 @@ class BoomerAMG:
         check(lib().hypreve_BoomerAMGSetRankEmulation(self.h, len(starts) - 1, arr), "SetRankEmulation")
 
     LAYOUTS = ("padded", "jagged", "wide", "jag-pw", "dict", "delta", "delta+vt8", "delta+vt16", "padded+vt16",
-               "jagged+vt16")
+               "jagged+vt16", "dict-ranges")
 
     def level_layout(self, level, which=0):
         """Device layout name of A_l (0), P_l (1) or R_l (2) (interior rows)."""
@@ -646,7 +650,9 @@ def init():
 
 
 def bench_stream(elem_bytes, n, reps=20):
-    """Average ms of a read-only stream over n elements of elem_bytes (2, 4, 8 or 16)."""
+    """Average ms of a read-only stream over n elements of elem_bytes (2, 4, 8 or 16),
+    or (elem_bytes -1 / -2 / -5) of a read/write mix: that many n-double streams
+    read and one written."""
     ms = C.c_double()
     check(lib().hypreve_BenchStream(elem_bytes, n, reps, C.byref(ms)), "BenchStream")
     return ms.value

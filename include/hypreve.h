@@ -243,7 +243,8 @@ HYPRE_Int hypreve_ParVectorSetRandomValues(HYPRE_ParVector v, HYPRE_Int seed); /
 HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver solver, HYPRE_Int num_blocks);
 /* Tuning: visit the row blocks of every operator in nbands bands of the grid
  * (0 = natural order) on the built hierarchy; results are unchanged. */
-HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands);
+HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands,
+                                         HYPRE_Int which_mask); /* bit 0 A, 1 P, 2 R (0 = all) */
 /* Device layout / row loop of the hierarchy's SELL operators (takes effect at
  * Setup): 0 automatic, 1 padded lane-per-row, 2 jagged lane-per-row, 3 padded
  * workgroup-per-slice, 4 jagged wave-product-parallel, 5 jagged with an LDS
@@ -251,7 +252,8 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands);
  * against per-slot bases (where a slice's rows fit), 7 as 6 plus 8-bit value
  * indices into a table of the operator's distinct values (where at most 256
  * occur), 8 padded and 9 jagged, each with 16-bit value indices (where at
- * most 4096 distinct values occur).  All give identical
+ * most 4096 distinct values occur), 10 jagged with an LDS x-tile made of at
+ * most 63 contiguous column ranges (range dictionary).  All give identical
  * bits; the forced settings exist for parity tests and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* One GPU runs the hybrid Gauss-Seidel smoothers with the row blocks of an
@@ -342,7 +344,10 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int w
  * vectors included. */
 HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,
                                           HYPRE_Real *bytes);
-/* Read-only streaming kernel (elem_bytes 2, 4, 8 or 16): FETCH_SIZE calibration. */
+/* Read-only streaming kernel (elem_bytes 2, 4, 8 or 16): FETCH_SIZE calibration.
+ * elem_bytes -1 / -2 / -5: a read/write mix, R = 1, 2 or 5 streams of n doubles
+ * read and one written per element (the achievable bandwidth of a kernel that
+ * reads R bytes for each byte it writes). */
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real *avg_ms);
 HYPRE_Int hypreve_DeviceSynchronize(void);
 const char *hypreve_BuildInfo(void);

@@ -99,7 +99,7 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen, wt):
     assert np.array_equal(x.get(), xo)
 
 
-@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9])
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 @pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
 def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
