@@ -42,9 +42,14 @@ enum : int {
   K_PROLONG = 5, K_RESTRICT = 6, K_GENERAL = 7, K_RESID_L1JAC = 8, K_RESTRICT_ZG = 9,
 };
 
+// nrm (K_RESID_L1JAC on the delta layout only): the residual's squares summed
+// per workgroup into nrm[0 .. sell_nrm_parts(M)) (y may then be null: r not stored).
+int sell_nrm_parts(const SellView& M);
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
                        const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
-                       double* y2 = nullptr);
+                       double* y2 = nullptr, double* nrm = nullptr);
+// *out = sum of part[0 .. nparts) in a fixed order (work: 1024 doubles)
+hipError_t launch_sum(int nparts, const double* part, double* work, double* out, hipStream_t st);
 // Chebyshev steps (kernels.hip k_cheby): 0 start, 1 tmp = ds*u, 2 update, 3 finish
 hipError_t launch_cheby(int n, int step, int scale, double c, const double* ds, const double* f, double* r,
                         double* tmp, const double* v, double* orig, double* u, hipStream_t st);

@@ -80,6 +80,7 @@ struct SpArgs {
   int nblk;                                  // entries of blk_map
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
+  double* __restrict__ nrm;       // OP_RESID_L1JAC (delta layout): per-workgroup sums of r_i^2 (y may be null)
   double w;                       // relax weight / alpha
   double temp;                    // beta/alpha for OP_GENERAL
   int relax_points;
@@ -458,7 +459,7 @@ __device__ __forceinline__ double vt_value(const SpArgs& p, const double* vt, co
 }
 
 template <int OP, bool CFSEL, int B, bool NT, int VI>
-__device__ __forceinline__ void delta_row(const SpArgs& p, const double* vt, int row) {
+__device__ __forceinline__ void delta_row(const SpArgs& p, const double* vt, int row, double& acc) {
   constexpr short PAD = -32768;
   if (row >= p.nrows) return;
   const int lane = row & (kWave - 1);
@@ -535,7 +536,8 @@ __device__ __forceinline__ void delta_row(const SpArgs& p, const double* vt, int
     // the row's first stored entry (its diagonal) is negative
     const double l1v = neg ? -s1 : s1;
     if (OP == OP_RESID_L1JAC) {
-      sstore<NT>(p.y + g, t);
+      if (p.y) sstore<NT>(p.y + g, t);
+      if (p.nrm) acc += t * t;
       sstore<NT>(p.y2 + g, p.x[g] + t / l1v);
     } else if (OP == OP_L1JAC) {
       sstore<NT>(p.y + g, p.x[g] + t / l1v);
@@ -545,7 +547,23 @@ __device__ __forceinline__ void delta_row(const SpArgs& p, const double* vt, int
     }
     return;
   }
+  if (OP == OP_RESID_L1JAC) {
+    if (p.y) sstore<NT>(p.y + g, t);
+    if (p.nrm) acc += t * t;
+    sstore<NT>(p.y2 + g, p.x[g] + t / mload<NT>(p.l1 + g));
+    return;
+  }
   row_store<OP, NT>(p, g, false, t, uo, d);
+}
+
+// Sum of one value per thread over the workgroup (256 threads), in a fixed
+// order; thread 0 writes it to out.
+__device__ __forceinline__ void wg_sum_store(double v, double* out) {
+  __shared__ double sh[4];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) *out = (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
 // Row blocks of 256 rows; gridDim.x (a multiple of 8) workgroups, each XCD's
@@ -563,8 +581,12 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
   const int per_xcd = (nrb + 7) >> 3;
   const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
   const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
+  double acc = 0.0;
   for (int rb = r0 + (int)(blockIdx.x >> 3); rb < r1; rb += per_wg)
-    delta_row<OP, CFSEL, B, NT, VI>(p, vt, map_block(p, rb) * 256 + (int)threadIdx.x);
+    delta_row<OP, CFSEL, B, NT, VI>(p, vt, map_block(p, rb) * 256 + (int)threadIdx.x, acc);
+  // the solve loop's residual norm, fused: one partial per workgroup (every
+  // workgroup writes one, rows or not)
+  if (OP == OP_RESID_L1JAC && p.nrm) wg_sum_store(acc, p.nrm + blockIdx.x);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -1162,9 +1184,11 @@ static inline int blocks_pad8(int n) { int b = blocks_for(n); return ((b + 7) / 
 
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
                        const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
-                       double* y2) {
-  if (M.nrows <= 0) return hipSuccess;
+                       double* y2, double* nrm) {
+  if (nrm && (op != OP_RESID_L1JAC || !M.dcol)) return hipErrorInvalidValue;
+  if (M.nrows <= 0 && !nrm) return hipSuccess;
   SpArgs a;
+  a.nrm = nrm;
   a.rowmap = M.rowmap;
   a.rowlen = M.rowlen;
   a.col16 = M.col16;
@@ -1223,7 +1247,8 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     return hipGetLastError();
   }
   if (M.dcol) {  // 16-bit column deltas, lane per row
-    // 16-bit value table: persistent grid of 8 workgroups per CU
+    // 16-bit value table: persistent grid of 8 workgroups per CU (the fused
+    // residual norm writes one partial per workgroup: sell_nrm_parts)
     const dim3 xgrid(M.vidx16 ? std::min(a.nblocks_pad, 2048) : a.nblocks_pad);
     const size_t lds = (size_t)M.nvtab * sizeof(double);
 #define HVE_X(OPV, CF, BB)                                                                       \
@@ -1477,6 +1502,29 @@ hipError_t launch_pcg_p(int n, const double* beta_p, const double* s, double* p,
 int dot_num_parts(int n) {
   int b = blocks_for(n);
   return b < 1024 ? (b < 1 ? 1 : b) : 1024;
+}
+int sell_nrm_parts(const SellView& M) {
+  const int nb = blocks_pad8(std::max(M.nrows, 1));
+  return M.vidx16 ? std::min(nb, 2048) : nb;
+}
+__global__ void __launch_bounds__(256) k_sum_partial(int n, const double* __restrict__ x, double* __restrict__ part) {
+  __shared__ double sh[4];
+  double s = 0.0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) s += x[i];
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_down(s, o, 64);
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) part[blockIdx.x] = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+hipError_t launch_sum(int nparts, const double* part, double* work, double* out, hipStream_t st) {
+  if (nparts <= 4096) {
+    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, st, nparts, part, out);
+  } else {
+    const int np2 = std::min(1024, (nparts + 255) / 256);
+    hipLaunchKernelGGL(k_sum_partial, dim3(np2), dim3(256), 0, st, nparts, part, work);
+    hipLaunchKernelGGL(k_dot_final, dim3(1), dim3(256), 0, st, np2, work, out);
+  }
+  return hipGetLastError();
 }
 hipError_t launch_dot(int n, const double* x, const double* y, double* part, double* out, hipStream_t st) {
   const int np = dot_num_parts(n);

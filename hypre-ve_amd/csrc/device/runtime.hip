@@ -507,6 +507,8 @@ void DevAMG::release() {
     if (p) (void)hipFree(p);
   coarse_L_ = nullptr; coarse_mask_ = nullptr; coarse_U_ = nullptr; coarse_f_ = nullptr; coarse_u_ = nullptr;
   u0_buf_[0] = u0_buf_[1] = nullptr; x0_buf_ = nullptr; dot_part_ = nullptr; dscal_ = nullptr;
+  if (nrm_part_) (void)hipFree(nrm_part_);
+  nrm_part_ = nullptr;
   if (hscal_) (void)hipHostFree(hscal_);
   hscal_ = nullptr;
   for (auto& s : scratch_) { if (s) (void)hipFree(s); s = nullptr; }
@@ -532,6 +534,7 @@ void DevAMG::init_workspace(int n, DevComm* comm) {
   comm_ = (comm && comm->size() > 1) ? comm : nullptr;
   init_common(&stream_, &comm_stream_, &ev_packed_, &ev_halo_);
   dot_part_ = dalloc<double>(1024);
+  nrm_part_ = dalloc<double>(2 * ((size_t)n / 256 + 16));  // fused residual norm: one partial per row block
   dscal_ = dalloc<double>(16);
   HVE_HIP(hipMemset(dscal_, 0, 16 * sizeof(double)));
   HVE_HIP(hipHostMalloc((void**)&hscal_, 16 * sizeof(double), hipHostMallocDefault));
@@ -1130,9 +1133,40 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
   int cycle_count = 0;
   const bool fuse = tol > 0. && can_fuse_presmooth();
   double* pre = fuse ? presmooth_buffer() : nullptr;
+  // With the fused residual + first sweep on the delta layout the residual is
+  // needed only for its norm: the kernel sums r_i^2 per workgroup and stores
+  // no r (one write and one read of the fine vector fewer per iteration).
+  // Norms then reduce in another order than the dot kernel's (as the oracle's
+  // differs from both); iterates are unchanged.
+  const DevLevel& L0 = lev_[0];
+  const bool fuse_nrm = fuse && L0.A.in.dcol && (L0.A.bd.nrows == 0 || L0.A.bd.dcol) && nrm_fusion_;
+  double resid_sq = 0.0;
   // r = f - A u, and with fusion the first sweep of the next cycle
   auto residual = [&](bool initial) {
-    if (fuse) {
+    if (fuse_nrm) {
+      DevLevel& L = lev_[0];
+      double* xin = u;
+      if (x0_buf_) {
+        HVE_HIP(launch_copy(L.n, u, x0_buf_, s));
+        xin = x0_buf_;
+      }
+      const double* l1 = L.l1_fly ? nullptr : L.l1;
+      const bool ex = L.hu.active() && comm_;
+      if (ex) halo_start(L.hu, xin, s);
+      HVE_HIP(launch_sell(K_RESID_L1JAC, L.A.in.view(), xin, f, l1, nullptr, 0, nullptr, 1.0, 0.0, s, pre, nrm_part_));
+      if (ex) halo_finish(s);
+      int np = sell_nrm_parts(L.A.in.view());
+      if (L.A.bd.nrows > 0) {
+        HVE_HIP(launch_sell(K_RESID_L1JAC, L.A.bd.view(), xin, f, l1, nullptr, 0, nullptr, 1.0, 0.0, s, pre,
+                            nrm_part_ + np));
+        np += sell_nrm_parts(L.A.bd.view());
+      }
+      HVE_HIP(launch_sum(np, nrm_part_, dot_part_, dscal_ + 15, s));
+      if (comm_) comm_->allreduce_sum(dscal_ + 15, 1, s);
+      HVE_HIP(hipMemcpyAsync(hscal_ + 15, dscal_ + 15, sizeof(double), hipMemcpyDeviceToHost, s));
+      HVE_HIP(hipStreamSynchronize(s));
+      resid_sq = hscal_[15];
+    } else if (fuse) {
       DevLevel& L = lev_[0];
       double* xin = u;
       if (x0_buf_) {
@@ -1152,7 +1186,7 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
   if (tol > 0.) {
     residual(true);
     pre_ready = fuse;
-    resid_nrm = std::sqrt(dot_host(n, V, V, s));
+    resid_nrm = std::sqrt(fuse_nrm ? resid_sq : dot_host(n, V, V, s));
     if (resid_nrm != 0.) {
       double ieee = resid_nrm / resid_nrm;
       if (ieee != ieee) return HYPRE_ERROR_GENERIC_CODE;
@@ -1169,7 +1203,7 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
     if (tol > 0.) {
       residual(false);
       pre_ready = fuse;
-      resid_nrm = std::sqrt(dot_host(n, V, V, s));
+      resid_nrm = std::sqrt(fuse_nrm ? resid_sq : dot_host(n, V, V, s));
       if (prm.converge_type == 0) relative_resid = rhs_norm ? resid_nrm / rhs_norm : resid_nrm;
       else relative_resid = resid_nrm / resid_nrm_init;
       if (prm.print_level > 1)

@@ -11,6 +11,7 @@
 #include <string>
 #include <tuple>
 #include <utility>
+#include <cstdlib>
 #include <vector>
 
 #include "../host/hve_host.hpp"
@@ -212,6 +213,7 @@ class DevAMG {
   double* u0_buf_[2] = {nullptr, nullptr};  // level-0 iterate with halo space (multi-rank)
   double* x0_buf_ = nullptr;                // fine_apply input with halo space
   double* dot_part_ = nullptr;
+  double* nrm_part_ = nullptr;
   double* dscal_ = nullptr;  // device scalars
   double* hscal_ = nullptr;  // pinned host scalars
   double* scratch_[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -220,6 +222,12 @@ class DevAMG {
   hipEvent_t ev_packed_ = nullptr, ev_halo_ = nullptr;
   DevComm* comm_ = nullptr;  // not owned
   bool use_graph_ = true;
+  // the solve loop's residual norm summed inside the fused residual + sweep
+  // kernel (no r stored); HVE_NRM_FUSE=0 stores r and runs the dot kernel
+  bool nrm_fusion_ = [] {
+    const char* e = std::getenv("HVE_NRM_FUSE");
+    return !e || std::atoi(e) != 0;
+  }();
   double cycle_ops_ = 0;
   int ws_n_ = 0;
   std::map<std::tuple<const void*, const void*, bool>, hipGraphExec_t> graphs_;

@@ -20,7 +20,11 @@ amg = hv.BoomerAMG(**kw)
 t = time.time()
 amg.setup(A)
 row = {"n": n, "env": {k: v for k, v in os.environ.items() if k.startswith("HVE_")}, "setup_s": round(time.time() - t, 1)}
-for l, w, name in [(0, 0, "A0"), (0, 1, "P0"), (0, 2, "R0"), (1, 0, "A1"), (1, 1, "P1"), (1, 2, "R1"), (2, 0, "A2")]:
+nl = amg.num_levels()
+for l, w, name in [(0, 0, "A0"), (0, 1, "P0"), (0, 2, "R0"), (1, 0, "A1"), (1, 1, "P1"), (1, 2, "R1"), (2, 0, "A2"),
+                   (2, 1, "P2"), (2, 2, "R2"), (3, 0, "A3"), (3, 1, "P3"), (3, 2, "R3"), (4, 0, "A4")]:
+    if l >= nl or (w and l >= nl - 1):
+        continue
     ms = amg.bench_level_op(l, w, 20)[0]
     row[name] = [amg.level_layout(l, w), round(ms, 4), round(amg.level_op_stored_bytes(l, w) / ms / 1e6, 0)]
 b = hv.ParVector(A.n, np.ones(A.n))
