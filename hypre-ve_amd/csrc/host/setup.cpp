@@ -690,7 +690,9 @@ void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_fact
     coarsen_ruge_first_pass(S, A, measure_type, cut_factor, cf);
   } else {
     if (cut_factor > 0) throw std::runtime_error("rank emulation: HMIS with a cut factor is not restated");
-    if (measure_type != 0) throw std::runtime_error("rank emulation: HMIS needs local measures (measure_type 0)");
+    // local measures: 0, or 3 (the aggressive second pass: local, agg_2)
+    if (measure_type != 0 && measure_type != 3)
+      throw std::runtime_error("rank emulation: HMIS needs local measures (measure_type 0 or 3)");
     const int nr = (int)rs->size() - 1;
     cf.assign(S.n, 0);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -1459,7 +1461,6 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   if (rank_starts && rank_starts->size() > 2) {
     emul = *rank_starts;
     if (emul.front() != 0 || emul.back() != A0.nrows) throw std::runtime_error("rank emulation: row starts do not cover A");
-    if (prm.agg_num_levels > 0) throw std::runtime_error("rank emulation: aggressive coarsening is not restated");
     if (prm.interp_type != 6) throw std::runtime_error("rank emulation: only ext+i interpolation is restated");
     rank_order_rows(H.lev[0].A, emul, emul);
   }
@@ -1492,16 +1493,24 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     if (agg) {
       Pattern S2;
       create_2nd_strength(S, cf, prm.num_paths, S2);
+      // emulated ranks: S2's rows (the first pass's C points) split as the fine rows
+      std::vector<int> rs2;
+      if (rs) {
+        std::vector<int> pref(cf.size() + 1, 0);
+        for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] > 0);
+        for (int v : *rs) rs2.push_back(pref[v]);
+      }
+      const std::vector<int>* rsc = rs ? &rs2 : nullptr;
       std::vector<int> cfn;
-      if (coarsen_type == 8) coarsen_pmis(S2, 3, cfn);
-      else if (coarsen_type == 9) coarsen_pmis(S2, 4, cfn);
+      if (coarsen_type == 8) coarsen_pmis(S2, 3, cfn, rsc);
+      else if (coarsen_type == 9) coarsen_pmis(S2, 4, cfn, rsc);
       else if (coarsen_type == 10) {
         CSR S2A;  // hypre passes S2 as the matrix too (only its row lengths, for cut_factor)
         S2A.resize_rows(S2.n, S2.n);
         S2A.i = S2.i;
         S2A.j = S2.j;
         S2A.a.assign(S2.j.size(), 1.0);
-        coarsen_hmis(S2, &S2A, prm.measure_type + 3, prm.coarsen_cut_factor, cfn);
+        coarsen_hmis(S2, &S2A, prm.measure_type + 3, prm.coarsen_cut_factor, cfn, rsc);
       } else {
         throw std::runtime_error("aggressive coarsening with coarsen_type " + std::to_string(coarsen_type));
       }
@@ -1518,7 +1527,15 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     }
     if (coarse_size < prm.min_coarse_size) break;
     CSR P;
-    if (agg) build_multipass_interp(L.A, cf, S, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
+    if (agg) {
+      build_multipass_interp(L.A, cf, S, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
+      if (!emul.empty()) {  // P_diag | P_offd
+        std::vector<int> cs(emul.size(), 0), pref(cf.size() + 1, 0);
+        for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] == 1);
+        for (size_t r = 0; r < emul.size(); ++r) cs[r] = pref[emul[r]];
+        rank_order_rows(P, emul, cs);
+      }
+    }
     else if (prm.interp_type == 6 && !emul.empty()) {
       // par_csr_matrix.c:2671 truncates the row [P_diag | P_offd] and splits
       // the kept entries back into the two parts in their sorted order

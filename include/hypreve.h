@@ -271,7 +271,8 @@ HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver solver, HYPRE_Int nranks
  * (par_csr_matrix.c:2671), and the hybrid GS blocks of SetGsRankStarts.
  * Coarse-level agglomeration is off (the reference has none).  This pins the
  * product to the reference's own np > 1 saved outputs.  nranks <= 1 clears it.
- * Takes effect at Setup; ext+i (interp_type 6), no aggressive levels. */
+ * Aggressive levels: the second pass per rank as well, multipass rows in
+ * P_diag | P_offd order.  Takes effect at Setup; ext+i (interp_type 6). */
 /* The relaxation weight and outer weight (omega) the cycle uses on `level`. */
 HYPRE_Int hypreve_BoomerAMGGetLevelWeights(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Real *relax_weight,
                                            HYPRE_Real *omega);

@@ -15,7 +15,10 @@ side (tests/ij_emul.py).
 This pins, against reference-held numbers: PMIS, PMIS1 and HMIS; ext+i with
 Pmx 0 and 4; 7- and 27-point operators; relax 0 and 18 C/F-ordered, 18, the
 l1 hybrid GS 13/14 (also C/F-ordered and weighted, w = 1.1), hybrid GS 4 up,
-8 under PCG, Chebyshev (order 2/3, unscaled, variant 1) and BoomerAMG-PCG.
+6 and 8 under PCG, Chebyshev (order 2/3, unscaled, variant 1),
+BoomerAMG-PCG, and aggressive coarsening (HMIS second pass on S*S + 2S with
+local measures per rank, multipass interpolation, 1 and 10 aggressive levels,
+7- and 27-point: agg_interp.out.4/8, coarsening.out.7).
 """
 import json
 import os
