@@ -40,8 +40,9 @@ def build(hv, case):
     kw = hv.ij_amg_defaults(0 if case["solver"] == "amg" else 1)
     kw.update(num_blocks=1)
     st = dict(case["settings"])
-    if "cycle_relax_type" in st:
-        st["cycle_relax_type"] = {int(k): v for k, v in st["cycle_relax_type"].items()}
+    for key in ("cycle_relax_type", "cycle_num_sweeps"):
+        if key in st:
+            st[key] = {int(k): v for k, v in st[key].items()}
     kw.update(st)
     amg = hv.BoomerAMG(**kw)
     amg.set_rank_emulation(starts)
