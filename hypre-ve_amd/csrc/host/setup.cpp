@@ -1407,6 +1407,164 @@ void cheby_setup(const CSR& A, double max_eig, double min_eig, double fraction, 
 // ---------------------------------------------------------------------------
 // Setup driver: par_amg_setup.c:889-2880 (coarsening loop), :2990-3120 (l1 norms).
 // ---------------------------------------------------------------------------
+
+// ---------------------------------------------------------------------------
+// Automatic relaxation weights: par_cg_relax_wt.c hypre_BoomerAMGCGRelaxWt.
+// CG on A preconditioned by one sweep of the level's down smoother (weights 1,
+// from zero) starting at a random vector (seed 5128, per rank when emulating);
+// the Lanczos tridiagonal's largest eigenvalue (hypre_Bisection, par_cg_relax_wt.c:362)
+// gives the weight 1/lambda_max, stopping when it moves by less than 1e-3.
+// ---------------------------------------------------------------------------
+static void bisection(int n, const double* diag, const double* offd, double y, double z, double tol, int k,
+                      double* ev) {
+  while (std::fabs(y - z) > tol * (std::fabs(y) + std::fabs(z))) {
+    const double x = (y + z) / 2;
+    int sign_change = 0;
+    double p0 = 1, p1 = diag[0] - x, p2;
+    if (p0 * p1 <= 0) sign_change++;
+    for (int i = 1; i < n; i++) {
+      p2 = (diag[i] - x) * p1 - offd[i] * offd[i] * p0;
+      p0 = p1;
+      p1 = p2;
+      if (p0 * p1 <= 0) sign_change++;
+    }
+    if (sign_change >= k) z = x;
+    else y = x;
+  }
+  *ev = (y + z) / 2;
+}
+
+// One sweep of relax_type with weights 1 (par_relax.c), blocks bs (hybrid GS),
+// relax_points 0; u is updated in place (tmp: scratch of A.nrows).
+static void host_relax_w1(const CSR& A, const std::vector<double>& f, int relax_type, const std::vector<double>& l1,
+                          const std::vector<int>& bs, std::vector<double>& u, std::vector<double>& tmp) {
+  const int n = A.nrows;
+  switch (relax_type) {
+    case 0: {  // par_relax.c:139, weight 1
+      tmp = u;
+      for (int i = 0; i < n; ++i) {
+        const double d = A.a[A.i[i]];
+        if (d == 0.0) continue;
+        double res = f[i];
+        for (int k = A.i[i] + 1; k < A.i[i + 1]; ++k) res -= A.a[k] * tmp[A.j[k]];
+        u[i] *= 0.0;
+        u[i] += 1.0 * res / d;
+      }
+      return;
+    }
+    case 7: case 18: {  // u += (f - A u)/l1 (ams.c:41 with the l1 norms; 7: the diagonal)
+      tmp = f;
+      for (int i = 0; i < n; ++i) {
+        double t = tmp[i];
+        for (int k = A.i[i]; k < A.i[i + 1]; ++k) t -= A.a[k] * u[A.j[k]];
+        tmp[i] = t;
+      }
+      for (int i = 0; i < n; ++i) u[i] += tmp[i] / l1[i];
+      return;
+    }
+    case 3: case 4: case 6: case 8: case 13: case 14: {
+      const bool fwd = relax_type == 3 || relax_type == 6 || relax_type == 8 || relax_type == 13;
+      const bool bwd = relax_type == 4 || relax_type == 6 || relax_type == 8 || relax_type == 14;
+      const bool use_l1 = relax_type == 8 || relax_type == 13 || relax_type == 14;
+      const int nb = (int)bs.size() - 1;
+      tmp = u;
+      for (int b = 0; b < nb; ++b) {
+        const int ns = bs[b], ne = bs[b + 1];
+        for (int pass = 0; pass < 2; ++pass) {
+          if ((pass == 0 && !fwd) || (pass == 1 && !bwd)) continue;
+          for (int q = 0; q < ne - ns; ++q) {
+            const int i = pass == 0 ? ns + q : ne - 1 - q;
+            if (use_l1) {
+              if (l1[i] == 0.0) continue;
+              double res = f[i];
+              for (int k = A.i[i]; k < A.i[i + 1]; ++k) {
+                const int c = A.j[k];
+                res -= A.a[k] * ((nb == 1 || (c >= ns && c < ne)) ? u[c] : tmp[c]);
+              }
+              u[i] += res / l1[i];
+            } else {
+              const double d = A.a[A.i[i]];
+              if (d == 0.0) continue;
+              double res = f[i];
+              for (int k = A.i[i] + 1; k < A.i[i + 1]; ++k) {
+                const int c = A.j[k];
+                res -= A.a[k] * ((nb == 1 || (c >= ns && c < ne)) ? u[c] : tmp[c]);
+              }
+              u[i] = res / d;
+            }
+          }
+        }
+      }
+      return;
+    }
+    default:
+      throw std::runtime_error("automatic relaxation weight (negative weight) with relax type " +
+                               std::to_string(relax_type) + " is not available");
+  }
+}
+
+static double cg_relax_weight(const CSR& A, int relax_type, const std::vector<double>& l1, const std::vector<int>& bs,
+                              int num_cg_sweeps, const std::vector<int>* rs) {
+  const int n = A.nrows;
+  auto dot = [&](const std::vector<double>& x, const std::vector<double>& y) {
+    if (!rs) return host_dot(x, y);
+    double t = 0.0;  // per-rank sums (hypre_SeqVectorInnerProd), then the sum over ranks
+    for (size_t r = 0; r + 1 < rs->size(); ++r) {
+      double sr = 0.0;
+      for (int i = (*rs)[r]; i < (*rs)[r + 1]; ++i) sr += y[i] * x[i];
+      t += sr;
+    }
+    return t;
+  };
+  std::vector<double> R(n), Z(n), P(n, 0.0), V(n), tmp(n);
+  // hypre_ParVectorSetRandomValues(Rtemp, 5128): 2 rand - 1, seed 5128 (my_id + 1)
+  if (rs) {
+    for (size_t r = 0; r + 1 < rs->size(); ++r)
+      for (int i = (*rs)[r]; i < (*rs)[r + 1]; ++i) R[i] = 2.0 * hypre_rand_at(i - (*rs)[r], 5128 * ((int)r + 1)) - 1.0;
+  } else {
+    for (int i = 0; i < n; ++i) R[i] = 2.0 * hypre_rand_at(i, 5128) - 1.0;
+  }
+  std::vector<double> tridiag(num_cg_sweeps + 1, 0.0), trioffd(num_cg_sweeps + 1, 0.0);
+  double gamma = 1.0, gammaold, alpha, beta, alphinv, row_sum, max_row_sum = 0.0;
+  double rlx_wt = 0.0, rlx_wt_old = 0.0, lambda_max = 0.0, lambda_max_old;
+  for (int jj = 0; jj < num_cg_sweeps; ++jj) {
+    std::fill(Z.begin(), Z.end(), 0.0);
+    host_relax_w1(A, R, relax_type, l1, bs, Z, tmp);
+    gammaold = gamma;
+    gamma = dot(R, Z);
+    if (jj == 0) {
+      P = Z;
+      beta = 1.0;
+    } else {
+      beta = gamma / gammaold;
+      for (int i = 0; i < n; ++i) P[i] = Z[i] + beta * P[i];
+    }
+    host_matvec(A, P, V);
+    alpha = gamma / dot(P, V);
+    alphinv = 1.0 / alpha;
+    tridiag[jj + 1] = alphinv;
+    tridiag[jj] *= beta;
+    tridiag[jj] += alphinv;
+    trioffd[jj] *= std::sqrt(beta);
+    trioffd[jj + 1] = -alphinv;
+    row_sum = std::fabs(tridiag[jj]) + std::fabs(trioffd[jj]);
+    if (row_sum > max_row_sum) max_row_sum = row_sum;
+    if (jj > 0) {
+      row_sum = std::fabs(tridiag[jj - 1]) + std::fabs(trioffd[jj - 1]) + std::fabs(trioffd[jj]);
+      if (row_sum > max_row_sum) max_row_sum = row_sum;
+      lambda_max_old = lambda_max;
+      rlx_wt_old = rlx_wt;
+      bisection(jj + 1, tridiag.data(), trioffd.data(), lambda_max_old, max_row_sum, 1.e-3, jj + 1, &lambda_max);
+      rlx_wt = 1.0 / lambda_max;
+      if (std::fabs(rlx_wt - rlx_wt_old) < 1.e-3) break;
+    } else {
+      lambda_max = tridiag[0];
+    }
+    for (int i = 0; i < n; ++i) R[i] += (-alpha) * V[i];  // hypre_ParVectorAxpy(-alpha, Vtemp, Rtemp)
+  }
+  return rlx_wt;
+}
+
 static bool uses_l1_gs(int t) { return t == 8 || t == 13 || t == 14; }
 
 // l1 norm option the setup computes on level j of nl (0 none, 1 full row
@@ -1624,6 +1782,46 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         double d = L.A.a[L.A.i[r]];
         L.l1[r] = (d == 0.0) ? 1.0 : d;
       }
+    }
+  }
+  // par_amg_setup.c:3290-3305: a negative relax_weight[j] / omega[j] asks for
+  // -w CG steps of hypre_BoomerAMGCGRelaxWt on that level (every level but a
+  // Gaussian-elimination coarsest one, or one of at most 9 rows)
+  for (int j = 0; j < nl; ++j) {
+    const bool ge = prm.relax_type[3] == 9 || prm.relax_type[3] == 99 || prm.relax_type[3] == 19 ||
+                    prm.relax_type[3] == 98;
+    if (!(j < nl - 1 || (!ge && H.lev[j].A.nrows > 9))) continue;
+    const double w0 = prm.wt(j), o0 = prm.omega(j);
+    if (w0 >= 0 && o0 >= 0) continue;
+    if (j >= AMGParams::kWeightLevels) throw std::runtime_error("automatic weights beyond level 63");
+    const Level& L = H.lev[j];
+    // the blocks of hypre's threads, or of every emulated rank (num_blocks each)
+    std::vector<int> bs;
+    std::vector<double> l1 = L.l1;
+    const int nbk = std::max(1, prm.num_blocks);
+    if (!lev_starts.empty()) {
+      const std::vector<int>& st = lev_starts[j];
+      bs.push_back(0);
+      for (size_t r = 0; r + 1 < st.size(); ++r) {
+        const std::vector<int> loc = hypre_block_starts(st[r + 1] - st[r], nbk);
+        for (int k = 1; k <= nbk; ++k) bs.push_back(st[r] + loc[k]);
+      }
+      bool cfr = false;
+      if (!l1.empty() && l1_option_for_level(prm, j, nl, &cfr) == 4)
+        compute_l1_norms_blocks(L.A, 4, (cfr && !L.cf.empty()) ? L.cf.data() : nullptr, bs, l1);
+    } else {
+      bs = hypre_block_starts(L.A.nrows, nbk);
+    }
+    const int rt = prm.relax_type[1];
+    if ((rt == 18 || rt == 7 || uses_l1_gs(rt)) && l1.empty()) throw std::runtime_error("l1 norms missing");
+    const std::vector<int>* rsj = lev_starts.empty() ? nullptr : &lev_starts[j];
+    if (w0 < 0) {
+      prm.lev_relax_wt[j] = cg_relax_weight(L.A, rt, l1, bs, (int)(-w0), rsj);
+      prm.lev_relax_wt_set |= (uint64_t)1 << j;
+    }
+    if (o0 < 0) {
+      prm.lev_outer_wt[j] = cg_relax_weight(L.A, rt, l1, bs, (int)(-o0), rsj);
+      prm.lev_outer_wt_set |= (uint64_t)1 << j;
     }
   }
   // coarsest-level direct solve
