@@ -132,11 +132,13 @@ def oracle_cpu_baseline(amg, nrows, n, pcg, args):
     return cpu
 
 
-def amg_settings(hv, pcg):
+def amg_settings(hv, pcg, agg=0):
     """The bench's BoomerAMG: PMIS, ext+i (Pmx 4), l1-Jacobi down/up,
-    Gaussian elimination on the coarsest level (ij -pmis -rlx 18)."""
+    Gaussian elimination on the coarsest level (ij -pmis -rlx 18); agg > 0:
+    that many aggressive levels with multipass interpolation (configs[4],
+    ij -agg_nl)."""
     kw = hv.ij_amg_defaults(1 if pcg else 0)
-    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, agg_num_levels=agg)
     return kw
 
 
@@ -166,13 +168,13 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
     x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=nrows * world)
     if pcg:
         # ij -solver 1: PCG (two-norm) preconditioned by one BoomerAMG V-cycle
-        amg = hv.BoomerAMG(**amg_settings(hv, True))
+        amg = hv.BoomerAMG(**amg_settings(hv, True, args.agg))
         krylov = hv.PCG(tol=0.0, max_iter=max(1, args.warmup), two_norm=1)
         krylov.set_precond_amg(amg)
         with heartbeat(f"rank {rank} setup"):
             krylov.setup(A, b, x)
     else:
-        kw = amg_settings(hv, False)
+        kw = amg_settings(hv, False, args.agg)
         kw.update(tol=1e-300, max_iter=args.warmup, min_iter=0)
         amg = hv.BoomerAMG(**kw)
         with heartbeat(f"rank {rank} setup"):
@@ -218,7 +220,7 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
     achieved = stored_bytes / (spmv_ms * 1e-3) / 1e9
     csr_gbs = csr_bytes / (spmv_ms * 1e-3) / 1e9
     aniso = args.coef != "1,1,1"
-    default_op = args.stencil == 7 and not aniso
+    default_op = args.stencil == 7 and not aniso and not args.agg
     layout0 = amg.level_layout(0, 0)
     kname, kdesc = KERNEL_OF_LAYOUT[layout0]
     # the committed PMC summary (scripts/pmc_traffic.py) measured the default
@@ -309,7 +311,9 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
         "config": {"workload": f"3D {args.stencil}-point {'anisotropic diffusion (' + args.coef + ')' if aniso else 'Laplacian'}"
                                f" {n}^3 per GPU ({n}x{n}x{n * world} global, z-slab row "
                                f"blocks), {'BoomerAMG-PCG (one V-cycle per PCG iteration)' if pcg else 'BoomerAMG V-cycle'}"
-                               f", PMIS + ext+i (Pmx 4), l1-Jacobi (relax 18) down/up, Gaussian elimination coarsest",
+                               f", PMIS + ext+i (Pmx 4)"
+                               f"{f', {args.agg} aggressive level(s) (multipass)' if args.agg else ''}"
+                               f", l1-Jacobi (relax 18) down/up, Gaussian elimination coarsest",
                    "rows_per_gpu": nrows, "levels": nlev, "grid_complexity": round(g, 6),
                    "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
                    "parallelism": f"rows{world}"},
@@ -333,6 +337,8 @@ def main():
                     help="7: GenerateLaplacian (configs[1], the bench line); 27: GenerateLaplacian27pt (configs[3])")
     ap.add_argument("--coef", default="1,1,1",
                     help="cx,cy,cz of the 7-point operator; e.g. 0.001,1,1 for configs[4]'s anisotropic diffusion")
+    ap.add_argument("--agg", type=int, default=0,
+                    help="aggressive coarsening levels (configs[4]: with --coef 0.001,1,1), multipass interpolation")
     ap.add_argument("--cpu-cycles", type=int, default=1, help="run the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
     ap.add_argument("--cpu-cycles-max", type=int, default=60)

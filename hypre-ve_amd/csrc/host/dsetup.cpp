@@ -143,8 +143,11 @@ void map_cols(CSR& M, const Universe& U) {
 // ---------------------------------------------------------------------------
 // PMIS (coarsen_type 8), setup.cpp coarsen_pmis with cf_init 0, distributed.
 // ---------------------------------------------------------------------------
+// cf_init 3 (the aggressive second pass, setup.cpp coarsen_pmis(S2, 3)):
+// rows without strong connections become C points, and the first pass skips
+// the independent-set selection (only F points are decided there: order-free).
 void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& starts, HostComm& comm,
-               std::vector<int>& cf) {
+               std::vector<int>& cf, int cf_init = 0) {
   const int size = comm.size();
   std::vector<int> mcount(n, 0);
   std::vector<std::vector<int>> contrib(size), got;
@@ -175,7 +178,7 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
   std::vector<int> graph, graph2;
   for (int r = 0; r < n; ++r) {
     if (S.i[r + 1] - S.i[r] == 0) {
-      cf[r] = SF_PT;
+      cf[r] = cf_init == 3 ? C_PT : SF_PT;
       measure[r] = 0;
     } else {
       graph.push_back(r);
@@ -183,19 +186,22 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
   }
   std::vector<double> gmeas;
   std::vector<int> gcf, gdem;
+  int iter = 0;
   while (comm.allreduce_sum((int64_t)graph.size()) > 0) {
     gp.pull(measure.data(), gmeas, comm);
     const int gs = (int)graph.size();
+    const bool select = !cf_init || iter > 0;
+    ++iter;
 #pragma omp parallel for schedule(static)
     for (int ig = 0; ig < gs; ++ig) {
       const int i = graph[ig];
-      if (measure[i] > 1) cf[i] = 1;
+      if (select && measure[i] > 1) cf[i] = 1;
     }
     gdem.assign(gp.want.size(), 0);
 #pragma omp parallel for schedule(static)
     for (int ig = 0; ig < gs; ++ig) {
       const int i = graph[ig];
-      if (measure[i] > 1) {
+      if (select && measure[i] > 1) {
         for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
           const int j = sidx[k];
           const double mj = j >= 0 ? measure[j] : gmeas[-1 - j];
@@ -246,6 +252,282 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
     }
     graph.swap(graph2);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Aggressive levels, distributed (par_amg_setup.c:1239-1285 as setup.cpp runs
+// it in one process): second strength over the first pass's C points,
+// PMIS on it, CorrectCFMarker, multipass interpolation.  Every row is built
+// from the same global rows in the same order, so the result is the
+// one-process hierarchy's rows.
+// ---------------------------------------------------------------------------
+Pattern fetch_pattern_rows(const Pattern& S, int first, const std::vector<int>& starts, const std::vector<int>& rows,
+                           HostComm& c) {
+  CSR M;
+  M.resize_rows(S.n, 0);
+  M.i = S.i;
+  M.j = S.j;
+  M.a.assign(S.j.size(), 1.0);
+  CSR G = fetch_rows(M, first, starts, rows, c);
+  Pattern P;
+  P.n = G.nrows;
+  P.i = G.i;
+  P.j.swap(G.j);
+  return P;
+}
+
+// setup.cpp create_2nd_strength for the owned rows: S2 rows of the owned
+// first-pass C points (cf > 0) in the global numbering of those points
+// (c1starts); cf of an owned point whose S2 row is empty becomes 2.
+void second_strength_dist(const Pattern& S, std::vector<int>& cf, int first, int n, const std::vector<int>& starts,
+                          int num_paths, HostComm& comm, std::vector<int>& c1starts, Pattern& S2) {
+  const int rank = comm.rank(), size = comm.size();
+  int64_t nc1 = 0;
+  for (int v : cf) nc1 += (v > 0);
+  const auto cnt = comm.allgather(nc1);
+  c1starts.assign(size + 1, 0);
+  for (int p = 0; p < size; ++p) c1starts[p + 1] = c1starts[p] + (int)cnt[p];
+  std::vector<int> f2c(n, -1);
+  int cc = c1starts[rank];
+  for (int i = 0; i < n; ++i)
+    if (cf[i] > 0) f2c[i] = cc++;
+  // G1: off-rank strong neighbours (their S rows are read); G2: theirs
+  std::vector<int> g1;
+  for (int c : S.j)
+    if (c < first || c >= first + n) g1.push_back(c);
+  sort_unique(g1);
+  const Pattern SG1 = fetch_pattern_rows(S, first, starts, g1, comm);
+  std::vector<int> gh = g1;
+  for (int c : SG1.j)
+    if (c < first || c >= first + n) gh.push_back(c);
+  sort_unique(gh);
+  GhostPlan gp;
+  gp.build(gh, first, n, starts, comm);
+  std::vector<int> gcf, gf2c;
+  gp.pull(cf.data(), gcf, comm);
+  gp.pull(f2c.data(), gf2c, comm);
+  auto cf_of = [&](int g) { return (g >= first && g < first + n) ? cf[g - first] : gcf[gp.find(g)]; };
+  auto f2c_of = [&](int g) { return (g >= first && g < first + n) ? f2c[g - first] : gf2c[gp.find(g)]; };
+  auto srow = [&](int g, const int*& b, const int*& e) {
+    if (g >= first && g < first + n) {
+      b = S.j.data() + S.i[g - first];
+      e = S.j.data() + S.i[g - first + 1];
+    } else {
+      const int k = (int)(std::lower_bound(g1.begin(), g1.end(), g) - g1.begin());
+      b = SG1.j.data() + SG1.i[k];
+      e = SG1.j.data() + SG1.i[k + 1];
+    }
+  };
+  const int nc_loc = (int)nc1;
+  S2.n = nc_loc;
+  S2.i.assign(nc_loc + 1, 0);
+  S2.j.clear();
+  std::vector<int> touch, count, mark_pos;
+  std::vector<int> marker_keys;  // global C-space index -> position in touch (small per row)
+  int ic = 0;
+  for (int i = 0; i < n; ++i) {
+    if (cf[i] <= 0) continue;
+    const int myc = f2c[i];
+    touch.clear();
+    count.clear();
+    auto add = [&](int index, int w) {
+      for (size_t t = 0; t < touch.size(); ++t)
+        if (touch[t] == index) { count[t] += w; return; }
+      touch.push_back(index);
+      count.push_back(w);
+    };
+    for (int k1 = S.i[i]; k1 < S.i[i + 1]; ++k1) {
+      const int i2 = S.j[k1];
+      if (cf_of(i2) > 0) add(f2c_of(i2), 2);
+      const int *b, *e;
+      srow(i2, b, e);
+      for (const int* q = b; q < e; ++q) {
+        const int i3 = *q;
+        if (cf_of(i3) > 0 && f2c_of(i3) != myc) add(f2c_of(i3), 1);
+      }
+    }
+    int kept = 0;
+    for (size_t t = 0; t < touch.size(); ++t)
+      if (count[t] >= num_paths) {
+        S2.j.push_back(touch[t]);
+        ++kept;
+      }
+    S2.i[ic + 1] = S2.i[ic] + kept;
+    if (kept == 0) cf[i] = 2;
+    ++ic;
+  }
+}
+
+// setup.cpp build_multipass_interp for the owned rows (global coarse columns
+// from cstarts).  Passes are global (every rank runs the same count); a pass
+// reads the assignment of ghost neighbours and, for its weights, the P rows of
+// the ghost neighbours of the previous pass.  A row whose sum_C * a_ii is 0
+// would reuse the previous row's weight factor in the reference's sequential
+// loop; that has no distributed counterpart and is refused.
+void multipass_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, int first, int n,
+                    const std::vector<int>& starts, const std::vector<int>& cstarts, double trunc_factor,
+                    int max_elmts, HostComm& comm, CSR& P) {
+  const int rank = comm.rank();
+  constexpr int max_num_passes = 10;
+  std::vector<int> f2c(n, -1);
+  int cc = cstarts[rank];
+  for (int i = 0; i < n; ++i)
+    if (cf[i] == 1) f2c[i] = cc++;
+  std::vector<int> g1;
+  for (int c : A.j)
+    if (c < first || c >= first + n) g1.push_back(c);
+  sort_unique(g1);
+  GhostPlan gp;
+  gp.build(g1, first, n, starts, comm);
+  std::vector<int> gcf, gf2c, gassigned;
+  gp.pull(cf.data(), gcf, comm);
+  gp.pull(f2c.data(), gf2c, comm);
+  auto gidx = [&](int g) { return gp.find(g); };
+  auto cf_of = [&](int g) { return (g >= first && g < first + n) ? cf[g - first] : gcf[gidx(g)]; };
+  auto f2c_of = [&](int g) { return (g >= first && g < first + n) ? f2c[g - first] : gf2c[gidx(g)]; };
+  std::vector<int> assigned(n, -1);
+  std::vector<std::vector<int>> rows_of_pass(max_num_passes + 1);
+  for (int i = 0; i < n; ++i)
+    if (cf[i] == 1) assigned[i] = 0;
+  // pass 1: F points with a strong C neighbour
+  for (int i = 0; i < n; ++i) {
+    if (cf[i] != -1) continue;
+    for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+      if (cf_of(S.j[k]) == 1) { assigned[i] = 1; break; }
+    if (assigned[i] == 1) rows_of_pass[1].push_back(i);
+  }
+  auto unassigned = [&]() {
+    int64_t u = 0;
+    for (int i = 0; i < n; ++i) u += (cf[i] == -1 && assigned[i] < 0);
+    return u;
+  };
+  int pass = 2;
+  while (comm.allreduce_sum(unassigned()) > 0 && pass < max_num_passes) {
+    gp.pull(assigned.data(), gassigned, comm);
+    auto asg_of = [&](int g) { return (g >= first && g < first + n) ? assigned[g - first] : gassigned[gidx(g)]; };
+    std::vector<int> now;
+    for (int i = 0; i < n; ++i) {
+      if (cf[i] != -1 || assigned[i] >= 0) continue;
+      for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+        if (asg_of(S.j[k]) == pass - 1) { now.push_back(i); break; }
+    }
+    for (int i : now) assigned[i] = pass;
+    rows_of_pass[pass].swap(now);
+    ++pass;
+  }
+  const int num_passes = pass;
+  gp.pull(assigned.data(), gassigned, comm);
+  auto asg_of = [&](int g) { return (g >= first && g < first + n) ? assigned[g - first] : gassigned[gidx(g)]; };
+  // rows: C points (the point itself), then pass by pass
+  std::vector<std::vector<int>> pj(n);
+  std::vector<std::vector<double>> pa(n);
+  for (int i = 0; i < n; ++i)
+    if (cf[i] == 1) { pj[i] = {f2c[i]}; pa[i] = {1.0}; }
+  auto refuse = []() {
+    throw std::runtime_error("distributed multipass: a row with sum_C * a_ii == 0 (sequential weight reuse)");
+  };
+  // pass 1: direct weights from the strong C neighbours, in A-row order
+  for (int i : rows_of_pass[1]) {
+    std::vector<int> strong;
+    for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+      if (cf_of(S.j[k]) == 1) strong.push_back(S.j[k]);
+    double sum_C = 0, sum_N = 0;
+    for (int k = A.i[i] + 1; k < A.i[i + 1]; ++k) {
+      const int j1 = A.j[k];
+      if (cf_of(j1) != -3) sum_N += A.a[k];
+      if (std::find(strong.begin(), strong.end(), j1) != strong.end()) {
+        pa[i].push_back(A.a[k]);
+        pj[i].push_back(f2c_of(j1));
+        sum_C += A.a[k];
+      }
+    }
+    const double diagonal = A.a[A.i[i]];
+    if (!(sum_C * diagonal != 0)) refuse();
+    const double alfa = -sum_N / (sum_C * diagonal);
+    for (double& v : pa[i]) v *= alfa;
+  }
+  // passes >= 2: through the P rows of the previous pass (ghost rows fetched)
+  for (pass = 2; pass < num_passes; ++pass) {
+    // P rows of the previous pass, owned -> CSR with global columns, ghosts fetched
+    std::vector<int> want;
+    for (int i : rows_of_pass[pass]) {
+      for (int k = S.i[i]; k < S.i[i + 1]; ++k) {
+        const int j = S.j[k];
+        if ((j < first || j >= first + n) && asg_of(j) == pass - 1) want.push_back(j);
+      }
+    }
+    sort_unique(want);
+    CSR Pown;
+    Pown.resize_rows(n, 0);
+    for (int i = 0; i < n; ++i) Pown.i[i + 1] = Pown.i[i] + (assigned[i] == pass - 1 ? (int)pj[i].size() : 0);
+    for (int i = 0; i < n; ++i)
+      if (assigned[i] == pass - 1) {
+        Pown.j.insert(Pown.j.end(), pj[i].begin(), pj[i].end());
+        Pown.a.insert(Pown.a.end(), pa[i].begin(), pa[i].end());
+      }
+    const CSR PG = fetch_rows(Pown, first, starts, want, comm);
+    auto prow = [&](int g, const int*& cb, const double*& ab, int& len) {
+      if (g >= first && g < first + n) {
+        cb = pj[g - first].data();
+        ab = pa[g - first].data();
+        len = (int)pj[g - first].size();
+      } else {
+        const int k = (int)(std::lower_bound(want.begin(), want.end(), g) - want.begin());
+        cb = PG.j.data() + PG.i[k];
+        ab = PG.a.data() + PG.i[k];
+        len = PG.i[k + 1] - PG.i[k];
+      }
+    };
+    for (int i : rows_of_pass[pass]) {
+      std::vector<int>& cols = pj[i];
+      std::vector<double>& vals = pa[i];
+      // columns: the previous-pass rows of the strong neighbours, first touch
+      std::vector<int> nb;
+      for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+        if (asg_of(S.j[k]) == pass - 1) nb.push_back(S.j[k]);
+      for (int j1 : nb) {
+        const int* cb;
+        const double* ab;
+        int len;
+        prow(j1, cb, ab, len);
+        for (int q = 0; q < len; ++q)
+          if (std::find(cols.begin(), cols.end(), cb[q]) == cols.end()) cols.push_back(cb[q]);
+      }
+      vals.assign(cols.size(), 0.0);
+      double sum_C = 0, sum_N = 0;
+      for (int k = A.i[i] + 1; k < A.i[i + 1]; ++k) {
+        const int j1 = A.j[k];
+        if (std::find(nb.begin(), nb.end(), j1) != nb.end()) {
+          const int* cb;
+          const double* ab;
+          int len;
+          prow(j1, cb, ab, len);
+          for (int q = 0; q < len; ++q) {
+            const double alfa = A.a[k] * ab[q];
+            const size_t pos = std::find(cols.begin(), cols.end(), cb[q]) - cols.begin();
+            vals[pos] += alfa;
+            sum_C += alfa;
+            sum_N += alfa;
+          }
+        } else if (cf_of(j1) != -3) {
+          sum_N += A.a[k];
+        }
+      }
+      const double diagonal = A.a[A.i[i]];
+      if (!(sum_C * diagonal != 0)) refuse();
+      const double alfa = -sum_N / (sum_C * diagonal);
+      for (double& v : vals) v *= alfa;
+    }
+  }
+  P.resize_rows(n, cstarts.back());
+  for (int i = 0; i < n; ++i) P.i[i + 1] = P.i[i] + (int)pj[i].size();
+  P.j.reserve(P.i[n]);
+  P.a.reserve(P.i[n]);
+  for (int i = 0; i < n; ++i) {
+    P.j.insert(P.j.end(), pj[i].begin(), pj[i].end());
+    P.a.insert(P.a.end(), pa[i].begin(), pa[i].end());
+  }
+  if (trunc_factor != 0.0 || max_elmts != 0) truncate_rows(P, trunc_factor, max_elmts);
 }
 
 // ---------------------------------------------------------------------------
@@ -535,7 +817,7 @@ bool dist_setup_supported(const AMGParams& prm, std::string* why) {
   auto no = [&](const char* w) { if (why) *why = w; return false; };
   if (prm.coarsen_type != 8) return no("coarsen_type != 8 (PMIS)");
   if (prm.interp_type != 6) return no("interp_type != 6 (ext+i)");
-  if (prm.agg_num_levels > 0) return no("aggressive coarsening");
+  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4) return no("aggressive coarsening with agg_interp_type != 4");
   for (int k = 0; k < 4; ++k)  // its eigenvalue estimate reduces over all rows in one order
     if (prm.relax_type[k] == 16) return no("Chebyshev smoother (relax 16)");
   return true;
@@ -566,6 +848,16 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     create_strength(L[level].A, prm.strong_threshold, prm.max_row_sum, S);
     std::vector<int> cf;
     pmis_dist(S, first, n, L[level].starts, comm, cf);
+    // aggressive level: PMIS again on S*S + 2S of the C points, and the second
+    // marker refines the first (setup.cpp amg_setup, par_amg_setup.c:1239)
+    const bool agg_lvl = level < prm.agg_num_levels;
+    if (agg_lvl) {
+      Pattern S2;
+      std::vector<int> c1starts, cfn;
+      second_strength_dist(S, cf, first, n, L[level].starts, prm.num_paths, comm, c1starts, S2);
+      pmis_dist(S2, c1starts[rank], S2.n, c1starts, comm, cfn, 3);
+      correct_cf_marker(cf, cfn);
+    }
     int64_t nc_loc = 0;
     for (int v : cf) nc_loc += (v == C_PT);
     const auto ncs = comm.allgather(nc_loc);
@@ -582,10 +874,16 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     std::vector<int> cstarts(size + 1, 0);
     for (int p = 0; p < size; ++p) cstarts[p + 1] = cstarts[p] + (int)ncs[p];
     CSR P;
-    extpi_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm.strong_threshold, prm.max_row_sum, comm, P);
-    if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
-    for (int i = 0; i < n; ++i)
-      if (cf[i] == SF_PT) cf[i] = F_PT;
+    if (agg_lvl) {
+      multipass_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm.agg_trunc_factor, prm.agg_P_max_elmts,
+                     comm, P);
+    } else {
+      extpi_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm.strong_threshold, prm.max_row_sum, comm,
+                 P);
+      if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
+      for (int i = 0; i < n; ++i)
+        if (cf[i] == SF_PT) cf[i] = F_PT;
+    }
     CSR R;
     transpose_dist(P, first, fine_size, cstarts, comm, R);
     CSR Ac;

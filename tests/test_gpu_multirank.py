@@ -179,8 +179,9 @@ def test_rccl_single_rank(hv):
 
 @pytest.mark.parametrize("nranks", [2, 3])
 def test_loopback_aggressive_bitwise(hv, nranks):
-    """Aggressive levels on the multi-rank path (rank-0 setup shipped to the
-    ranks): the N-rank iterates equal the one-rank ones."""
+    """Aggressive levels on the multi-rank path (the distributed setup: second
+    PMIS pass and multipass interpolation across ranks): the N-rank iterates
+    equal the one-rank ones."""
     kw = hv.ij_amg_defaults(0)
     kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-8, max_iter=80,
               agg_num_levels=1)

@@ -112,6 +112,19 @@ def test_distributed_setup_matches_one_process(hv, size, stencil, relax, order, 
     amg.dist_setup_check(A, size)
 
 
+@pytest.mark.parametrize("size", [2, 3, 5])
+@pytest.mark.parametrize("agg,cx", [(1, 1.0), (2, 1.0), (1, 0.001), (10, 0.001)])
+def test_distributed_setup_aggressive(hv, size, agg, cx):
+    """configs[4]: aggressive levels in the distributed setup (second strength
+    over the C points from fetched neighbour S rows, PMIS with CF_init 3,
+    CorrectCFMarker, multipass interpolation pass by pass with the previous
+    pass's ghost P rows fetched) equal the one-process hierarchy byte for byte."""
+    A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=cx)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=8, interp_type=6, relax_type=18, P_max_elmts=4, agg_num_levels=agg)
+    amg.dist_setup_check(A, size)
+
+
 @pytest.mark.parametrize("size", [2, 4, 7])
 def test_distributed_setup_anisotropic(hv, size):
     """configs[4]'s operator family (anisotropic diffusion, strong couplings in
