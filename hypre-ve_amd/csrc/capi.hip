@@ -1528,20 +1528,25 @@ HYPRE_Int HYPRE_ParCSRPCGSolve(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
     // HYPRE_BoomerAMGSolve(precond, A, r, z) on device buffers, honoring the
     // preconditioner's tol / max_iter (tol 0, max_iter 1 = one cycle)
     hypre_Solver_struct* P = s->precond;
-    pre = [amg, P, st](const double* r, double* z) {
+    pre = [amg, P, st](const double* r, double* z, bool z_zero) {
       amg->prm.tol = P->prm.tol;
       amg->prm.max_iter = P->prm.max_iter;
       amg->prm.min_iter = P->prm.min_iter;
       amg->prm.converge_type = P->prm.converge_type;
       amg->prm.print_level = 0;
-      if (P->prm.tol == 0.0 && P->prm.max_iter == 1) amg->cycle(r, z, st);
-      else amg->solve(r, z, st, &P->iters, &P->rel_res);
+      if (P->prm.tol == 0.0 && P->prm.max_iter == 1) {
+        amg->cycle(r, z, st, nullptr, z_zero);  // one cycle from the cleared z: zero-guess first sweep
+      } else {
+        if (z_zero) HVE_HIP(launch_set(amg->n0(), 0.0, z, st));
+        amg->solve(r, z, st, &P->iters, &P->rel_res);
+      }
     };
   } else if (s->precond_solve && s->precond) {
     const int n = A->n;
     hypre_Solver_struct* P = s->precond;
     auto fn = s->precond_solve;
-    pre = [fn, P, A, n, st](const double* r, double* z) {
+    pre = [fn, P, A, n, st](const double* r, double* z, bool z_zero) {
+      if (z_zero) HVE_HIP(launch_set(n, 0.0, z, st));
       HVE_HIP(hipStreamSynchronize(st));
       hypre_ParVector_struct rv, zv;
       rv.n = zv.n = n; rv.d = const_cast<double*>(r); zv.d = z; rv.owns = zv.owns = false;
@@ -1549,18 +1554,20 @@ HYPRE_Int HYPRE_ParCSRPCGSolve(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
     };
   } else {
     const int n = A->n;
-    pre = [n, st](const double* r, double* z) { HVE_HIP(launch_copy(n, r, z, st)); };
+    pre = [n, st](const double* r, double* z, bool) { HVE_HIP(launch_copy(n, r, z, st)); };
   }
   MatvecFn Aop;
   if (amg) {
-    Aop = [amg, st](int op, const double* xx, const double* bb, double* yy) {
-      amg->fine_apply(op, xx, bb, yy, op == K_RESID ? -1.0 : 1.0, 0.0, st);
+    Aop = [amg, st](int op, const double* xx, const double* bb, double* yy, double* dot) {
+      if (op == K_MATVEC && dot) amg->fine_matvec_dot(xx, yy, dot, st);
+      else amg->fine_apply(op, xx, bb, yy, op == K_RESID ? -1.0 : 1.0, 0.0, st);
     };
   } else {
     A->ensure_device();
     DevSell* dA = &A->dA;
-    Aop = [dA, st](int op, const double* xx, const double* bb, double* yy) {
+    Aop = [dA, ws, n = A->n, st](int op, const double* xx, const double* bb, double* yy, double* dot) {
       HVE_HIP(launch_sell(op, dA->view(), xx, bb, nullptr, nullptr, 0, yy, op == K_RESID ? -1.0 : 1.0, 0.0, st));
+      if (dot) ws->dot(n, yy, xx, dot, st);
     };
   }
   const int rc = pcg_solve(ws, A->n, Aop, s->pcg, pre, b->d, x->d, st, &s->iters, &s->rel_res);

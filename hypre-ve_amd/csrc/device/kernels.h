@@ -48,6 +48,11 @@ int sell_nrm_parts(const SellView& M);
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
                        const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
                        double* y2 = nullptr, double* nrm = nullptr);
+// PCG: x += alpha p; r += (-alpha) s; part[0 .. pcg_xr_parts()) = per-workgroup
+// sums of the new r_i^2 (part may be null)
+hipError_t launch_pcg_xr(int n, const double* alpha_p, const double* p, const double* s, double* x, double* r,
+                         double* part, hipStream_t st);
+int pcg_xr_parts();
 // *out = sum of part[0 .. nparts) in a fixed order (work: 1024 doubles)
 hipError_t launch_sum(int nparts, const double* part, double* work, double* out, hipStream_t st);
 // Chebyshev steps (kernels.hip k_cheby): 0 start, 1 tmp = ds*u, 2 update, 3 finish

@@ -553,6 +553,7 @@ __device__ __forceinline__ void delta_row(const SpArgs& p, const double* vt, int
     sstore<NT>(p.y2 + g, p.x[g] + t / mload<NT>(p.l1 + g));
     return;
   }
+  if (OP == OP_MATVEC && p.nrm) acc += p.x[g] * t;  // PCG's <s, p> with s = A p, fused
   row_store<OP, NT>(p, g, false, t, uo, d);
 }
 
@@ -586,7 +587,7 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
     delta_row<OP, CFSEL, B, NT, VI>(p, vt, map_block(p, rb) * 256 + (int)threadIdx.x, acc);
   // the solve loop's residual norm, fused: one partial per workgroup (every
   // workgroup writes one, rows or not)
-  if (OP == OP_RESID_L1JAC && p.nrm) wg_sum_store(acc, p.nrm + blockIdx.x);
+  if ((OP == OP_RESID_L1JAC || OP == OP_MATVEC) && p.nrm) wg_sum_store(acc, p.nrm + blockIdx.x);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -1064,6 +1065,33 @@ __global__ void __launch_bounds__(256) k_copy(int n, const double* __restrict__ 
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i < n) y[i] = x[i];
 }
+// PCG (krylov/pcg.c:536-560): x += alpha p; r += (-alpha) s; and, for the
+// two-norm test, r.r summed per workgroup (persistent grid, kNrmGrid partials)
+static constexpr int kNrmGrid = 2048;
+__global__ void __launch_bounds__(256) k_pcg_xr(int n, const double* __restrict__ alpha_p, const double* __restrict__ p,
+                                                const double* __restrict__ s, double* __restrict__ x,
+                                                double* __restrict__ r, double* __restrict__ part) {
+  const double a = 1.0 * (*alpha_p), na = -1.0 * (*alpha_p);
+  double acc = 0.0;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    double xi = x[i];
+    xi += a * p[i];
+    x[i] = xi;
+    double ri = r[i];
+    ri += na * s[i];
+    r[i] = ri;
+    acc += ri * ri;
+  }
+  if (part) wg_sum_store(acc, part + blockIdx.x);
+}
+hipError_t launch_pcg_xr(int n, const double* alpha_p, const double* p, const double* s, double* x, double* r,
+                         double* part, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pcg_xr, dim3(kNrmGrid), dim3(256), 0, st, n, alpha_p, p, s, x, r, part);
+  return hipGetLastError();
+}
+int pcg_xr_parts() { return kNrmGrid; }
+
 // p = s + beta*p  done as hypre does it: p *= beta; p += 1.0*s
 __global__ void __launch_bounds__(256) k_pcg_p(int n, const double* __restrict__ beta_p, const double* __restrict__ s,
                                                double* __restrict__ p) {
@@ -1185,7 +1213,7 @@ static inline int blocks_pad8(int n) { int b = blocks_for(n); return ((b + 7) / 
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
                        const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
                        double* y2, double* nrm) {
-  if (nrm && (op != OP_RESID_L1JAC || !M.dcol)) return hipErrorInvalidValue;
+  if (nrm && ((op != OP_RESID_L1JAC && op != OP_MATVEC) || !M.dcol)) return hipErrorInvalidValue;
   if (M.nrows <= 0 && !nrm) return hipSuccess;
   SpArgs a;
   a.nrm = nrm;

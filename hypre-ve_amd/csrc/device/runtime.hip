@@ -534,7 +534,8 @@ void DevAMG::init_workspace(int n, DevComm* comm) {
   comm_ = (comm && comm->size() > 1) ? comm : nullptr;
   init_common(&stream_, &comm_stream_, &ev_packed_, &ev_halo_);
   dot_part_ = dalloc<double>(1024);
-  nrm_part_ = dalloc<double>(2 * ((size_t)n / 256 + 16));  // fused residual norm: one partial per row block
+  // fused norms / dots: one partial per row block (delta kernels) or per workgroup (PCG update)
+  nrm_part_ = dalloc<double>(std::max<size_t>(2 * ((size_t)n / 256 + 16), 4096));
   dscal_ = dalloc<double>(16);
   HVE_HIP(hipMemset(dscal_, 0, 16 * sizeof(double)));
   HVE_HIP(hipHostMalloc((void**)&hscal_, 16 * sizeof(double), hipHostMallocDefault));
@@ -827,6 +828,42 @@ void DevAMG::fine_apply(int op, const double* x, const double* b, double* y, dou
   apply(L.A, &L.hu, op, xin, b, nullptr, nullptr, 0, y, alpha, temp, s);
 }
 
+// s = A p and <s, p> into the device scalar dot_out: one pass on the delta
+// layout (partials summed afterwards), else the matvec and the dot kernel.
+void DevAMG::fine_matvec_dot(const double* p, double* sv, double* dot_out, hipStream_t s) {
+  DevLevel& L = lev_[0];
+  const bool fused = L.A.in.dcol && (L.A.bd.nrows == 0 || L.A.bd.dcol) && nrm_fusion_ && !x0_buf_;
+  if (!fused) {
+    fine_apply(K_MATVEC, p, nullptr, sv, 1.0, 0.0, s);
+    dot(L.n, sv, p, dot_out, s);
+    return;
+  }
+  double* pin = const_cast<double*>(p);
+  const bool ex = L.hu.active() && comm_;
+  if (ex) halo_start(L.hu, pin, s);
+  HVE_HIP(launch_sell(K_MATVEC, L.A.in.view(), pin, nullptr, nullptr, nullptr, 0, sv, 1.0, 0.0, s, nullptr,
+                      nrm_part_));
+  if (ex) halo_finish(s);
+  int np = sell_nrm_parts(L.A.in.view());
+  if (L.A.bd.nrows > 0) {
+    HVE_HIP(launch_sell(K_MATVEC, L.A.bd.view(), pin, nullptr, nullptr, nullptr, 0, sv, 1.0, 0.0, s, nullptr,
+                        nrm_part_ + np));
+    np += sell_nrm_parts(L.A.bd.view());
+  }
+  HVE_HIP(launch_sum(np, nrm_part_, dot_part_, dot_out, s));
+  if (comm_) comm_->allreduce_sum(dot_out, 1, s);
+}
+
+// PCG's x += alpha p; r -= alpha s, and (rr_out != null) <r, r> of the new r.
+void DevAMG::pcg_update(int n, const double* alpha_p, const double* p, const double* sv, double* x, double* r,
+                        double* rr_out, hipStream_t s) {
+  HVE_HIP(launch_pcg_xr(n, alpha_p, p, sv, x, r, rr_out ? nrm_part_ : nullptr, s));
+  if (rr_out) {
+    HVE_HIP(launch_sum(pcg_xr_parts(), nrm_part_, dot_part_, rr_out, s));
+    if (comm_) comm_->allreduce_sum(rr_out, 1, s);
+  }
+}
+
 // v holds starts[r] .. starts[r+1] of every rank r; each rank fills in its own
 // share and receives the others' (one grouped exchange).
 void DevAMG::allgather_rows(double* v, const std::vector<int>& starts, hipStream_t s) {
@@ -970,15 +1007,19 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
 }
 
 // par_cycle.c:22 hypre_BoomerAMGCycle, emitted as a kernel sequence.
-void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed) {
+// zero_u: u0 holds zeros on entry (PCG's cleared preconditioner output,
+// pcg.c:434), so the first level-0 sweep takes the zero-guess form and u0 is
+// neither cleared nor read.
+void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed, bool zero_u) {
   const int nl = (int)lev_.size();
   std::vector<int> lev_counter(nl, prm.cycle_type);
   std::vector<double*> ucur(nl), ualt(nl);
   std::vector<const double*> fl(nl);
   std::vector<char> zero(nl, 0), skip_sweep(nl, 0);
   lev_counter[0] = 1;
+  if (zero_u) zero[0] = 1;
   if (u0_buf_[0]) {
-    if (!presmoothed) HVE_HIP(launch_copy(lev_[0].n, u0, u0_buf_[0], s));
+    if (!presmoothed && !zero_u) HVE_HIP(launch_copy(lev_[0].n, u0, u0_buf_[0], s));
     ucur[0] = u0_buf_[0];
     ualt[0] = u0_buf_[1];
   } else {
@@ -1091,20 +1132,21 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
   cycle_ops_ = ops;
 }
 
-void DevAMG::cycle(const double* f, double* u, hipStream_t s, const double* presmoothed) {
+void DevAMG::cycle(const double* f, double* u, hipStream_t s, const double* presmoothed, bool zero_u) {
   const bool pre = presmoothed != nullptr;
   if (pre && presmoothed != presmooth_buffer()) throw std::runtime_error("cycle: unexpected presmoothed buffer");
+  if (pre && zero_u) throw std::runtime_error("cycle: a presmoothed iterate is not zero");
   if (!use_graph_) {
-    emit_cycle(f, u, s, pre);
+    emit_cycle(f, u, s, pre, zero_u);
     return;
   }
-  auto key = std::make_tuple((const void*)f, (const void*)u, pre);
+  auto key = std::make_tuple((const void*)f, (const void*)u, (int)pre + 2 * (int)zero_u);
   auto it = graphs_.find(key);
   if (it == graphs_.end()) {
     hipGraph_t g;
     HVE_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     try {
-      emit_cycle(f, u, s, pre);
+      emit_cycle(f, u, s, pre, zero_u);
     } catch (...) {
       hipGraph_t tmp = nullptr;
       (void)hipStreamEndCapture(s, &tmp);
@@ -1231,10 +1273,9 @@ int pcg_solve(DevAMG* amg, int n, const MatvecFn& Aop, const PCGParams& prm, con
   HVE_HIP(hipMalloc((void**)&sc, 8 * sizeof(double)));
   HVE_HIP(hipHostMalloc((void**)&hs, 8 * sizeof(double), hipHostMallocDefault));
   HVE_HIP(hipMemsetAsync(sc, 0, 8 * sizeof(double), s));
-  auto precond = [&](const double* rr, double* zz) {
-    HVE_HIP(launch_set(n, 0.0, zz, s));  // ClearVector (pcg.c:434)
-    user_precond(rr, zz);
-  };
+  // ClearVector(z) (pcg.c:434) and the preconditioner: the callee knows z is
+  // zero (a BoomerAMG cycle starts with the zero-guess sweep instead)
+  auto precond = [&](const double* rr, double* zz) { user_precond(rr, zz, true); };
   auto read = [&]() {
     HVE_HIP(hipMemcpyAsync(hs, sc, 8 * sizeof(double), hipMemcpyDeviceToHost, s));
     HVE_HIP(hipStreamSynchronize(s));
@@ -1262,7 +1303,7 @@ int pcg_solve(DevAMG* amg, int n, const MatvecFn& Aop, const PCGParams& prm, con
     return 0;
   }
   // r = b - A x
-  Aop(K_RESID, x, b, r);
+  Aop(K_RESID, x, b, r, nullptr);
   precond(r, p);
   amg->dot(n, r, p, sc + 0, s);  // gamma
   if (prm.two_norm) amg->dot(n, r, r, sc + 5, s);
@@ -1270,14 +1311,12 @@ int pcg_solve(DevAMG* amg, int n, const MatvecFn& Aop, const PCGParams& prm, con
   i_prod_0 = prm.two_norm ? hs[5] : hs[0];
   while (i + 1 <= prm.max_iter) {
     ++i;
-    Aop(K_MATVEC, p, nullptr, sv);
-    amg->dot(n, sv, p, sc + 2, s);
+    Aop(K_MATVEC, p, nullptr, sv, sc + 2);                 // s = A p, sdotp = <s,p>
     HVE_HIP(launch_pcg_alpha(sc, s));
-    HVE_HIP(launch_axpy(n, sc + 3, 0.0, 1.0, p, x, s));    // x += alpha p
-    HVE_HIP(launch_axpy(n, sc + 3, 0.0, -1.0, sv, r, s));  // r += -alpha s
+    // x += alpha p; r += -alpha s; i_prod = <r,r> (two-norm test)
+    amg->pcg_update(n, sc + 3, p, sv, x, r, prm.two_norm ? sc + 5 : nullptr, s);
     precond(r, sv);
     amg->dot(n, r, sv, sc + 0, s);                         // gamma = <r,s>
-    if (prm.two_norm) amg->dot(n, r, r, sc + 5, s);
     read();
     const double flag = hs[6];
     const double gamma = hs[0];

@@ -166,7 +166,12 @@ class DevAMG {
   // One hypre_BoomerAMGCycle on device vectors f, u (owned rows, length n0).
   // presmoothed: level-0 iterate after the first down sweep, already formed by
   // a fused residual (OP_RESID_L1JAC); nullptr = run that sweep here.
-  void cycle(const double* f, double* u, hipStream_t s, const double* presmoothed = nullptr);
+  // zero_u: u holds zeros on entry (the first level-0 sweep takes the zero-guess form)
+  void cycle(const double* f, double* u, hipStream_t s, const double* presmoothed = nullptr, bool zero_u = false);
+  // PCG pieces: s = A p with <s,p> (fused on the delta layout); x/r update with <r,r>
+  void fine_matvec_dot(const double* p, double* sv, double* dot_out, hipStream_t s);
+  void pcg_update(int n, const double* alpha_p, const double* p, const double* sv, double* x, double* r,
+                  double* rr_out, hipStream_t s);
   int solve(const double* f, double* u, hipStream_t s, int* iters, double* rel_res);
   // y = op(A_0) x on owned rows (halo exchanged through an internal buffer)
   void fine_apply(int op, const double* x, const double* b, double* y, double alpha, double temp, hipStream_t s);
@@ -189,7 +194,7 @@ class DevAMG {
   AMGParams prm;
 
  private:
-  void emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed);
+  void emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed, bool zero_u = false);
   bool can_fuse_presmooth() const;
   double* presmooth_buffer();
   void relax(int level, int relax_type, int relax_points, const double* f, double*& u_cur, double*& u_alt,
@@ -230,7 +235,7 @@ class DevAMG {
   }();
   double cycle_ops_ = 0;
   int ws_n_ = 0;
-  std::map<std::tuple<const void*, const void*, bool>, hipGraphExec_t> graphs_;
+  std::map<std::tuple<const void*, const void*, int>, hipGraphExec_t> graphs_;  // (f, u, presmoothed + 2 zero_u)
   int agg_level_ = -1;            // first replicated level (RankHierarchy::agg_level)
   std::vector<int> agg_starts_;   // its rows' distributed owners
 };
@@ -243,9 +248,12 @@ struct PCGParams {
   int print_level = 0;
 };
 // precond(r, z): z = M^{-1} r on stream s.
-using Precond = std::function<void(const double* r, double* z)>;
-// apply(op, x, b, y): op K_MATVEC (y = A x) or K_RESID (y = b - A x)
-using MatvecFn = std::function<void(int op, const double* x, const double* b, double* y)>;
+// precond(r, z, z_zero): z = C r; z_zero: z holds zeros on entry... or not yet:
+// with z_zero the callee must treat z as cleared (it may skip the clearing)
+using Precond = std::function<void(const double* r, double* z, bool z_zero)>;
+// apply(op, x, b, y, dot): op K_MATVEC (y = A x; dot != null: <y, x> into that
+// device scalar) or K_RESID (y = b - A x)
+using MatvecFn = std::function<void(int op, const double* x, const double* b, double* y, double* dot)>;
 int pcg_solve(DevAMG* ws, int n, const MatvecFn& A, const PCGParams& prm, const Precond& precond, const double* b,
               double* x, hipStream_t s, int* iters, double* rel_res);
 
