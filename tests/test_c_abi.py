@@ -26,7 +26,9 @@ def _has_gpu():
     try:
         sys.path.insert(0, os.path.join(ROOT, "hypre-ve_amd"))
         import hypreve
-        return hypreve.lib().HYPRE_Init() == 0
+        ok = hypreve.lib().HYPRE_Init() == 0
+        hypreve.lib().HYPRE_ClearAllErrors()  # the error flag is sticky (hypre_error.c)
+        return ok
     except Exception:
         return False
 
