@@ -32,6 +32,9 @@ PROFILE_DIR = os.path.join(ROOT, "profiles")
 # hypreve_BoomerAMGGetLevelLayout name -> (residual kernel instantiation as
 # rocprofv3 names it, minus the batch width: "<prefix>B<suffix>"; description)
 KERNEL_OF_LAYOUT = {
+    "stencil": ("k_sell_delta<0, false, |, true, 3>(hve::SpArgs)",
+                "slot-uniform SELL-64 (per slice and slot one column offset, one value and a lane mask; "
+                "nothing stored per entry)"),
     "delta+vt8": ("k_sell_delta<0, false, |, true, 1>(hve::SpArgs)",
                   "SELL-64 with 16-bit column deltas and an 8-bit value table"),
     "delta+vt16": ("k_sell_delta<0, false, |, true, 2>(hve::SpArgs)",
@@ -132,14 +135,25 @@ def oracle_cpu_baseline(amg, nrows, n, pcg, args):
     return cpu
 
 
-def amg_settings(hv, pcg, agg=0):
+def amg_settings(hv, pcg, agg=0, relax=18, coarsen=8):
     """The bench's BoomerAMG: PMIS, ext+i (Pmx 4), l1-Jacobi down/up,
     Gaussian elimination on the coarsest level (ij -pmis -rlx 18); agg > 0:
     that many aggressive levels with multipass interpolation (configs[4],
-    ij -agg_nl)."""
+    ij -agg_nl).  relax < 0 keeps BoomerAMG's default smoothers (l1 hybrid
+    Gauss-Seidel 13 down / 14 up, automatic block count); coarsen 10 = HMIS."""
     kw = hv.ij_amg_defaults(1 if pcg else 0)
-    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, agg_num_levels=agg)
+    kw.update(coarsen_type=coarsen, interp_type=6, P_max_elmts=4, agg_num_levels=agg)
+    if relax >= 0:
+        kw.update(relax_type=relax)
     return kw
+
+
+def smoother_name(relax):
+    if relax < 0:
+        return "l1 hybrid Gauss-Seidel (relax 13 down / 14 up, BoomerAMG's default)"
+    if relax == 18:
+        return "l1-Jacobi (relax 18) down/up"
+    return f"relax {relax} down/up"
 
 
 def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light=False):
@@ -168,13 +182,13 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
     x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=nrows * world)
     if pcg:
         # ij -solver 1: PCG (two-norm) preconditioned by one BoomerAMG V-cycle
-        amg = hv.BoomerAMG(**amg_settings(hv, True, args.agg))
+        amg = hv.BoomerAMG(**amg_settings(hv, True, args.agg, args.relax, args.coarsen))
         krylov = hv.PCG(tol=0.0, max_iter=max(1, args.warmup), two_norm=1)
         krylov.set_precond_amg(amg)
         with heartbeat(f"rank {rank} setup"):
             krylov.setup(A, b, x)
     else:
-        kw = amg_settings(hv, False, args.agg)
+        kw = amg_settings(hv, False, args.agg, args.relax, args.coarsen)
         kw.update(tol=1e-300, max_iter=args.warmup, min_iter=0)
         amg = hv.BoomerAMG(**kw)
         with heartbeat(f"rank {rank} setup"):
@@ -220,7 +234,7 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
     achieved = stored_bytes / (spmv_ms * 1e-3) / 1e9
     csr_gbs = csr_bytes / (spmv_ms * 1e-3) / 1e9
     aniso = args.coef != "1,1,1"
-    default_op = args.stencil == 7 and not aniso and not args.agg
+    default_op = args.stencil == 7 and not aniso and not args.agg and args.relax == 18 and args.coarsen == 8
     layout0 = amg.level_layout(0, 0)
     kname, kdesc = KERNEL_OF_LAYOUT[layout0]
     # the committed PMC summary (scripts/pmc_traffic.py) measured the default
@@ -283,7 +297,7 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
             ncpu = args.cpu_n
             Ac = hv.ParCSRMatrix.laplacian27(ncpu, ncpu, ncpu) if args.stencil == 27 else \
                 hv.ParCSRMatrix.laplacian(ncpu, ncpu, ncpu, cx=cx, cy=cy, cz=cz)
-            ac = hv.BoomerAMG(**amg_settings(hv, pcg))
+            ac = hv.BoomerAMG(**amg_settings(hv, pcg, args.agg, args.relax, args.coarsen))
             ac.setup(Ac)
             cpu = oracle_cpu_baseline(ac, Ac.n, ncpu, pcg, args)
             cpu["sample"] += f" (one-process {ncpu}^3 stand-in for the {world}-rank problem: per-rank equivalent)"
@@ -311,9 +325,9 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
         "config": {"workload": f"3D {args.stencil}-point {'anisotropic diffusion (' + args.coef + ')' if aniso else 'Laplacian'}"
                                f" {n}^3 per GPU ({n}x{n}x{n * world} global, z-slab row "
                                f"blocks), {'BoomerAMG-PCG (one V-cycle per PCG iteration)' if pcg else 'BoomerAMG V-cycle'}"
-                               f", PMIS + ext+i (Pmx 4)"
+                               f", {'HMIS' if args.coarsen == 10 else 'PMIS'} + ext+i (Pmx 4)"
                                f"{f', {args.agg} aggressive level(s) (multipass)' if args.agg else ''}"
-                               f", l1-Jacobi (relax 18) down/up, Gaussian elimination coarsest",
+                               f", {smoother_name(args.relax)}, Gaussian elimination coarsest",
                    "rows_per_gpu": nrows, "levels": nlev, "grid_complexity": round(g, 6),
                    "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
                    "parallelism": f"rows{world}"},
@@ -339,6 +353,10 @@ def main():
                     help="cx,cy,cz of the 7-point operator; e.g. 0.001,1,1 for configs[4]'s anisotropic diffusion")
     ap.add_argument("--agg", type=int, default=0,
                     help="aggressive coarsening levels (configs[4]: with --coef 0.001,1,1), multipass interpolation")
+    ap.add_argument("--relax", type=int, default=18,
+                    help="relax type down/up (18: l1-Jacobi, the bench line); -1: BoomerAMG's default hybrid "
+                         "Gauss-Seidel 13/14 with the automatic block count")
+    ap.add_argument("--coarsen", type=int, choices=[8, 10], default=8, help="8: PMIS (the bench line), 10: HMIS")
     ap.add_argument("--cpu-cycles", type=int, default=1, help="run the CPU baseline (0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
     ap.add_argument("--cpu-cycles-max", type=int, default=60)

@@ -814,7 +814,7 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands, HYPRE
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  CHECK_ARG(policy >= 0 && policy <= 10, 2);
+  CHECK_ARG(policy >= 0 && policy <= 11, 2);
   s->prm.sell_policy = policy;
   return 0;
 }
@@ -1311,7 +1311,8 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver s, HYPRE_Real* bytes) {
 // 0 padded SELL-64, 1 jagged, 2 workgroup-per-slice, 3 jagged wave-product,
 // 4 dictionary (LDS x-tile), 5 16-bit column deltas, 6 deltas + 8-bit value
 // table, 7 deltas + 16-bit value table, 8 padded + 16-bit value table,
-// 9 jagged + 16-bit value table, 10 range dictionary.
+// 9 jagged + 16-bit value table, 10 range dictionary, 11 slot-uniform stencil
+// (no per-entry data).
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int* kind) {
   CHECK_ARG(s && s->dev && s->dev->built() && kind, 1);
   CHECK_ARG(level >= 0 && level < s->dev->num_levels(), 2);
@@ -1319,7 +1320,8 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE
   API_BEGIN
   const DevLevel& L = s->dev->level(level);
   const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
-  *kind = M.dcol ? (M.vidx16 ? 7 : M.vidx ? 6 : 5)
+  *kind = M.slot_mask ? 11
+         : M.dcol ? (M.vidx16 ? 7 : M.vidx ? 6 : 5)
                  : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? (M.dict_ranges ? 10 : 4) : M.pw ? 3 : M.rowlen ? 1
                  : M.wide ? 2 : 0;
   API_END
@@ -1417,11 +1419,34 @@ HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver s, HYPRE_Int level, HYPRE
 // achievable-bandwidth reference for the roofline.
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real* avg_ms) {
   CHECK_ARG(elem_bytes == 2 || elem_bytes == 4 || elem_bytes == 8 || elem_bytes == 16 || elem_bytes == -1 ||
-                elem_bytes == -2 || elem_bytes == -5,
+                elem_bytes == -2 || elem_bytes == -5 || elem_bytes == -8 || elem_bytes == -9,
             1);
   CHECK_ARG(n > 0, 2);
   CHECK_ARG(reps > 0, 3);
   API_BEGIN
+  if (elem_bytes == -8 || elem_bytes == -9) {  // n doubles in per-wave segments (-9: interleaved)
+    double *buf = nullptr, *out = nullptr;
+    hipStream_t st = lib_stream();
+    HVE_HIP(hipMalloc((void**)&buf, (size_t)n * sizeof(double)));
+    HVE_HIP(hipMalloc((void**)&out, sizeof(double)));
+    HVE_HIP(hipMemsetAsync(buf, 0, (size_t)n * sizeof(double), st));
+    for (int w = 0; w < 2; ++w) HVE_HIP(launch_stream_seg(n, elem_bytes == -9, buf, out, st));
+    hipEvent_t e0, e1;
+    HVE_HIP(hipEventCreate(&e0));
+    HVE_HIP(hipEventCreate(&e1));
+    HVE_HIP(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; ++r) HVE_HIP(launch_stream_seg(n, elem_bytes == -9, buf, out, st));
+    HVE_HIP(hipEventRecord(e1, st));
+    HVE_HIP(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HVE_HIP(hipEventElapsedTime(&ms, e0, e1));
+    hipEventDestroy(e0);
+    hipEventDestroy(e1);
+    (void)hipFree(buf);
+    (void)hipFree(out);
+    if (avg_ms) *avg_ms = ms / reps;
+    return 0;
+  }
   if (elem_bytes < 0) {  // read/write mix: -R = R double reads + 1 double write per element
     const int R = -elem_bytes;
     double *src = nullptr, *y = nullptr;

@@ -28,6 +28,9 @@ struct SellView {
   const unsigned char* vidx = nullptr;  // delta layout: 8-bit value indices (val unused)
   const unsigned short* vidx16 = nullptr;  // delta layout: 16-bit value indices (val unused)
   const double* vtab = nullptr;         // the operator's distinct values
+  const int* slot_vi = nullptr;         // stencil layout (no per-entry data): value index,
+  const uint64_t* slot_mask = nullptr;  // lanes present, offset (slot_base) per (slice, slot)
+  int stencil_w = 0;                    // stencil layout: slots per slice
   int nvtab = 0;
   // Traversal order of the workgroup row blocks (logical block -> stored row
   // block, nullptr = identity): blocks are visited so that each XCD streams a
@@ -77,6 +80,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const
                             int relax_points, const double* tmp, double* u, double w, double omega,
                             hipStream_t st);
 int sell_batch_override();
+int stencil_slices_per_wave();
 int sell_pipe_override();
 bool sell_nt();
 bool sell_pw();
@@ -84,6 +88,9 @@ bool sell_pw();
 // read/write mix of reads*8 B in and 8 B out per element.
 hipError_t launch_stream_mix(int64_t n, int reads, const double* src, double* y, hipStream_t st);
 hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, double* out, hipStream_t st);
+// n doubles read as per-wave 16 KiB segments (interleave: a workgroup's 4 waves
+// alternate over 512-B chunks of its 64 KiB)
+hipError_t launch_stream_seg(int64_t n, bool interleave, const double* buf, double* out, hipStream_t st);
 hipError_t launch_gather(int n, const int* idx, const double* x, double* out, hipStream_t st);
 hipError_t launch_axpy(int n, const double* alpha_p, double alpha, double sgn, const double* x, double* y,
                        hipStream_t st);

@@ -76,6 +76,9 @@ struct SpArgs {
   const unsigned short* __restrict__ vidx16; // the same, 16-bit
   const double* __restrict__ vtab;           // distinct values (<= 256)
   int nvtab;
+  const int* __restrict__ slot_vi;           // stencil layout: value index per (slice, slot)
+  const uint64_t* __restrict__ slot_mask;    // stencil layout: lanes present per (slice, slot)
+  int sw;                                    // stencil layout: slots per slice
   const int* __restrict__ blk_map;           // logical -> stored row block (nullptr: identity)
   int nblk;                                  // entries of blk_map
   double* __restrict__ y;         // output
@@ -565,6 +568,142 @@ __device__ __forceinline__ void wg_sum_store(double v, double* out) {
   if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
   __syncthreads();
   if (threadIdx.x == 0) *out = (sh[0] + sh[1]) + (sh[2] + sh[3]);
+}
+
+// ---------------------------------------------------------------------------
+// Slot-uniform SELL-64 (host: build_sell_stencil_host), for constant-
+// coefficient stencils: slot k of a slice is one neighbour offset and one value
+// for all its lanes, so nothing is streamed per entry.  Every slice has W slots
+// (slot k of slice s at s*W + k: no slice pointer to chase); a slot's offset,
+// value index and lane mask are wave-uniform scalar loads, and so is its value
+// from the table.  Each wave runs R consecutive slices with all
+// their loads of a batch in flight together: per row only x (gathered at
+// row + off: consecutive rows, one offset, coalesced), b and y move, so R
+// slices per wave keep enough bytes in flight to cover HBM latency.  Each row
+// adds its present slots in slot (= stored) order with the same rounding as
+// every other row loop: bitwise the same.
+// ---------------------------------------------------------------------------
+template <int OP, bool CFSEL, bool NT, int R>
+__global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
+  constexpr int B = 8;  // slots per batch and slice
+  const int lb = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
+  const int lane = threadIdx.x & (kWave - 1);
+  const int W = p.sw;
+  const int slice0 = __builtin_amdgcn_readfirstlane((lb * 4 + (int)(threadIdx.x >> 6)) * R);  // wave-uniform
+  const bool SUB = op_subtracts<OP>();
+  const bool sub = SUB || (OP == OP_GENERAL && p.w == -1.0);
+  const bool fly = (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC) && p.l1 == nullptr;
+  double acc = 0.0;
+  if (slice0 * kWave < p.nrows) {
+    int row[R], g[R];
+    bool act[R];
+    double t[R], uo[R], d[R], s1[R];
+    bool neg[R], seen[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      row[r] = (slice0 + r) * kWave + lane;
+      const bool ex = row[r] < p.nrows;
+      g[r] = ex ? (p.rowmap ? mload<NT>(p.rowmap + row[r]) : row[r]) : 0;
+      bool skip = false;
+      if (CFSEL && ex) skip = p.cf[g[r]] != p.relax_points;
+      if (CFSEL && ex && skip && (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC))
+        sstore<NT>(p.y + g[r], p.x[g[r]]);
+      act[r] = ex && !skip;
+      t[r] = act[r] ? row_init<OP, NT>(p, g[r]) : 0.0;
+      uo[r] = 0.0;
+      d[r] = 0.0;
+      s1[r] = 0.0;
+      neg[r] = false;
+      seen[r] = false;
+    }
+    int k0 = 0;
+    if (OP == OP_JAC) {
+      // the diagonal is every row's first entry, in slot 0 (the host checks it)
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint64_t m0 = p.slot_mask[(size_t)(slice0 + r) * W];
+        const double d0 = p.vtab[__builtin_amdgcn_readfirstlane(p.slot_vi[(size_t)(slice0 + r) * W])];
+        if (act[r]) {
+          uo[r] = p.x[g[r]];
+          d[r] = ((m0 >> lane) & 1) ? d0 : 0.0;
+        }
+      }
+      k0 = 1;
+    }
+    for (int k = k0; k < W; k += B) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        // the batch's slot data (scalar; slots past W read the next slice's or
+        // the tail padding and are dropped)
+        // (readfirstlane keeps every load of the batch unconditional and scalar:
+        // the compiler would otherwise sink each one into its lane-masked use)
+        const size_t sb = (size_t)(slice0 + r) * W + k;
+        int off[B], vi[B];
+        uint32_t mlo[B], mhi[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          off[q] = __builtin_amdgcn_readfirstlane(p.slot_base[sb + q]);
+          vi[q] = __builtin_amdgcn_readfirstlane(p.slot_vi[sb + q]);
+          const uint64_t m = p.slot_mask[sb + q];
+          mlo[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
+          mhi[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32));
+        }
+        bool on[B];
+        double xv[B], a[B];
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const uint32_t mw = lane < 32 ? mlo[q] : mhi[q];
+          on[q] = act[r] & ((k + q) < W) & (((mw >> (lane & 31)) & 1u) != 0);
+          const int idx = on[q] ? row[r] + off[q] : g[r];
+          xv[q] = p.x[idx];
+        }
+#pragma unroll
+        for (int q = 0; q < B; ++q) a[q] = p.vtab[vi[q]];  // uniform address: scalar load
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const double pr = a[q] * xv[q];
+          const double tn = sub ? t[r] - pr : t[r] + pr;
+          t[r] = on[q] ? tn : t[r];
+        }
+        if (fly) {
+#pragma unroll
+          for (int q = 0; q < B; ++q) {
+            if (on[q] && !seen[r]) { neg[r] = a[q] < 0.0; seen[r] = true; }
+            s1[r] = on[q] ? s1[r] + fabs(a[q]) : s1[r];
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (!act[r]) continue;
+      const int gg = g[r];
+      if (fly) {
+        // compute_l1_norms option 1 (ams.c:571), as in delta_row
+        const double l1v = neg[r] ? -s1[r] : s1[r];
+        if (OP == OP_RESID_L1JAC) {
+          if (p.y) sstore<NT>(p.y + gg, t[r]);
+          if (p.nrm) acc += t[r] * t[r];
+          sstore<NT>(p.y2 + gg, p.x[gg] + t[r] / l1v);
+        } else if (OP == OP_L1JAC) {
+          sstore<NT>(p.y + gg, p.x[gg] + t[r] / l1v);
+        } else if (OP == OP_L1JAC_W) {
+          const double v = (-p.w) * t[r];
+          sstore<NT>(p.y + gg, p.x[gg] + v / l1v);
+        }
+        continue;
+      }
+      if (OP == OP_RESID_L1JAC) {
+        if (p.y) sstore<NT>(p.y + gg, t[r]);
+        if (p.nrm) acc += t[r] * t[r];
+        sstore<NT>(p.y2 + gg, p.x[gg] + t[r] / mload<NT>(p.l1 + gg));
+        continue;
+      }
+      if (OP == OP_MATVEC && p.nrm) acc += p.x[gg] * t[r];
+      row_store<OP, NT>(p, gg, false, t[r], uo[r], d[r]);
+    }
+  }
+  if ((OP == OP_RESID_L1JAC || OP == OP_MATVEC) && p.nrm) wg_sum_store(acc, p.nrm + blockIdx.x);
 }
 
 // Row blocks of 256 rows; gridDim.x (a multiple of 8) workgroups, each XCD's
@@ -1213,7 +1352,8 @@ static inline int blocks_pad8(int n) { int b = blocks_for(n); return ((b + 7) / 
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
                        const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
                        double* y2, double* nrm) {
-  if (nrm && ((op != OP_RESID_L1JAC && op != OP_MATVEC) || !M.dcol)) return hipErrorInvalidValue;
+  const bool delta_like = M.dcol != nullptr || M.slot_mask != nullptr;
+  if (nrm && ((op != OP_RESID_L1JAC && op != OP_MATVEC) || !delta_like)) return hipErrorInvalidValue;
   if (M.nrows <= 0 && !nrm) return hipSuccess;
   SpArgs a;
   a.nrm = nrm;
@@ -1229,6 +1369,8 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   a.vidx16 = M.vidx16;
   a.vtab = M.vtab;
   a.nvtab = M.nvtab;
+  a.slot_vi = M.slot_vi;
+  a.slot_mask = M.slot_mask;
   a.blk_map = M.blk_map;
   a.nblk = M.nblk;
   a.slice_ptr = M.slice_ptr; a.col = M.col; a.val = M.val; a.nrows = M.nrows;
@@ -1274,7 +1416,31 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_D
     return hipGetLastError();
   }
-  if (M.dcol) {  // 16-bit column deltas, lane per row
+  if (M.slot_mask) {  // slot-uniform stencil: R slices per wave, 4R per workgroup
+    const int R = stencil_slices_per_wave();
+    a.sw = M.stencil_w;
+    a.nblocks_pad = (((M.nrows + 63) / 64 + 4 * R - 1) / (4 * R) + 7) / 8 * 8;
+    const dim3 sgrid(a.nblocks_pad);
+#define HVE_S(OPV, CF, RR)                                                                         \
+  if (nt) hipLaunchKernelGGL((k_sell_stencil<OPV, CF, true, RR>), sgrid, block, 0, s, a);         \
+  else hipLaunchKernelGGL((k_sell_stencil<OPV, CF, false, RR>), sgrid, block, 0, s, a);
+#define HVE_SR(OPV, CF) \
+  if (R == 4) { HVE_S(OPV, CF, 4) } else if (R == 1) { HVE_S(OPV, CF, 1) } else { HVE_S(OPV, CF, 2) }
+#define HVE_SL(OPV)                                                 \
+  case OPV:                                                         \
+    if (cfsel) { HVE_SR(OPV, true) } else { HVE_SR(OPV, false) }   \
+    break;
+    switch (op) {
+      HVE_SL(OP_RESID) HVE_SL(OP_MATVEC) HVE_SL(OP_L1JAC) HVE_SL(OP_L1JAC_W) HVE_SL(OP_JAC)
+      HVE_SL(OP_PROLONG) HVE_SL(OP_RESTRICT) HVE_SL(OP_GENERAL) HVE_SL(OP_RESID_L1JAC) HVE_SL(OP_RESTRICT_ZG)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_SL
+#undef HVE_SR
+#undef HVE_S
+    return hipGetLastError();
+  }
+  if (delta_like) {  // 16-bit column deltas, lane per row
     // 16-bit value table: persistent grid of 8 workgroups per CU (the fused
     // residual norm writes one partial per workgroup: sell_nrm_parts)
     const dim3 xgrid(M.vidx16 ? std::min(a.nblocks_pad, 2048) : a.nblocks_pad);
@@ -1454,6 +1620,40 @@ hipError_t launch_stream_read(int64_t n_bytes, int elem_bytes, const void* buf, 
   return hipGetLastError();
 }
 
+// Segmented read: every wave streams its own contiguous 16 KiB segment (the
+// shape of a slice's value block in the row loops: 64 lanes x 8 B per load,
+// 16 loads in flight), or (INTERLEAVE) the 4 waves of a workgroup take turns
+// over 512-B chunks of the workgroup's 64 KiB.  Against the grid-stride
+// stream it measures what many concurrent per-wave streams cost in HBM.
+template <bool INTERLEAVE>
+__global__ void __launch_bounds__(256) k_stream_seg(int64_t n, const double* __restrict__ buf,
+                                                    double* __restrict__ out, int nblocks_pad) {
+  const int lb = xcd_logical_block(blockIdx.x, nblocks_pad);
+  const int64_t base = (int64_t)lb * 8192;
+  if (base >= n) return;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double acc = 0.0;
+  for (int c = 0; c < 2; ++c) {
+    double v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t idx = INTERLEAVE ? base + ((int64_t)(c * 16 + q) * 4 + w) * 64 + lane
+                                     : base + (int64_t)w * 2048 + (int64_t)(c * 16 + q) * 64 + lane;
+      v[q] = idx < n ? __builtin_nontemporal_load(buf + idx) : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc += v[q];
+  }
+  if (acc == 12345.678) out[0] = acc;
+}
+hipError_t launch_stream_seg(int64_t n, bool interleave, const double* buf, double* out, hipStream_t st) {
+  const int nb = (int)((n + 8191) / 8192);
+  const int nbp = (nb + 7) / 8 * 8;
+  if (interleave) hipLaunchKernelGGL(k_stream_seg<true>, dim3(nbp), dim3(256), 0, st, n, buf, out, nbp);
+  else hipLaunchKernelGGL(k_stream_seg<false>, dim3(nbp), dim3(256), 0, st, n, buf, out, nbp);
+  return hipGetLastError();
+}
+
 // Read/write mix: y[i] = sum of R streams (doubles), R reads + 1 write per
 // element, grid-stride; the ceiling for kernels that read ~R bytes per byte
 // written (the finest residual reads ~4.8 for each one it writes).
@@ -1531,7 +1731,20 @@ int dot_num_parts(int n) {
   int b = blocks_for(n);
   return b < 1024 ? (b < 1 ? 1 : b) : 1024;
 }
+// Slices per wave of the stencil loop (k_sell_stencil): HVE_STENCIL_R=1|2|4.
+int stencil_slices_per_wave() {
+  static const int r = [] {
+    const char* e = getenv("HVE_STENCIL_R");
+    const int v = e ? atoi(e) : 2;
+    return (v == 1 || v == 2 || v == 4) ? v : 2;
+  }();
+  return r;
+}
 int sell_nrm_parts(const SellView& M) {
+  if (M.slot_mask) {
+    const int R = stencil_slices_per_wave();
+    return std::max(8, (((std::max(M.nrows, 1) + 63) / 64 + 4 * R - 1) / (4 * R) + 7) / 8 * 8);
+  }
   const int nb = blocks_pad8(std::max(M.nrows, 1));
   return M.vidx16 ? std::min(nb, 2048) : nb;
 }

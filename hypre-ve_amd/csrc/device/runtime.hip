@@ -50,7 +50,7 @@ static int sell_valtab_env() {
 void DevSell::set_block_order(const std::vector<int>& stored_to_local, const std::vector<int64_t>& key) {
   if (key.empty() || nrows <= 0) return;
   // the row block one workgroup of the chosen loop runs (kernels.hip launch_sell)
-  const int unit = col16 ? 64 * dict_group : (dcol || vidx16) ? 256 : (wide && !rowlen) ? 64 : 256;
+  const int unit = col16 ? 64 * dict_group : slot_mask ? 256 * stencil_slices_per_wave() : (delta_like() || vidx16) ? 256 : (wide && !rowlen) ? 64 : 256;
   const int nb = (nrows + unit - 1) / unit;
   std::vector<int64_t> bk(nb);
   for (int b = 0; b < nb; ++b) {
@@ -155,7 +155,47 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
   const bool delta_before_dict = policy == 0 && use_dict && !jag && !wide && delta_env != 0 && sigma_env == 0 &&
                                  sell_valtab_env() != 0;
   bool use_delta = (A.nnz() > 0 && !wide && !jag && !use_dict && delta_env != 0 && sigma_env == 0) || delta_before_dict;
-  if (policy != 0) use_delta = (policy == 6 || policy == 7) && A.nnz() > 0;
+  if (policy != 0) use_delta = (policy == 6 || policy == 7 || policy == 11) && A.nnz() > 0;
+  // A constant-coefficient stencil (every slot of a slice one neighbour offset
+  // and one value for all its lanes) takes the slot-uniform layout: nothing
+  // stored per entry, so an application streams only the vectors.
+  // HVE_SELL_STENCIL=0 turns it off; policy 11 forces it where it builds.
+  static const int stencil_env = [] {
+    const char* e = getenv("HVE_SELL_STENCIL");
+    return e ? atoi(e) : 1;
+  }();
+  if (use_delta && !short_rows && ((policy == 0 && stencil_env != 0) || policy == 11)) {
+    std::vector<int> so, svi;
+    std::vector<uint64_t> sm;
+    std::vector<double> tab;
+    int sw = 0;
+    if (build_sell_stencil_host(A, 64, sw, so, svi, sm, tab)) {
+      nrows = A.nrows;
+      ncols = A.ncols;
+      nslices = (A.nrows + 63) / 64;
+      nnz = A.nnz();
+      nnz_pad = (int64_t)nslices * 64 * sw;
+      stencil_w = sw;
+      batch = 8;
+      pipe = 0;
+      wide = 0;
+      pw = 0;
+      slot_base = dupload(so.data(), so.size());
+      slot_vi = dupload(svi.data(), svi.size());
+      slot_mask = dupload(sm.data(), sm.size());
+      vtab = dupload(tab.data(), tab.size());
+      nvtab = (int)tab.size();
+      if (!rowmap_h.empty()) {
+        bool ident = true;
+        for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
+        if (!ident) rowmap = dupload(rowmap_h.data(), rowmap_h.size());
+      }
+      stored_map = rowmap_h;
+      if (key) set_block_order(rowmap_h, *key);
+      return;
+    }
+    sp.clear();
+  }
   if (use_delta) {
     std::vector<short> dc;
     std::vector<int> sb;
@@ -415,12 +455,15 @@ void DevSell::release() {
   if (vidx) (void)hipFree(vidx);
   if (vidx16) (void)hipFree(vidx16);
   if (vtab) (void)hipFree(vtab);
+  if (slot_vi) (void)hipFree(slot_vi);
+  if (slot_mask) (void)hipFree(slot_mask);
   if (blk_map) (void)hipFree(blk_map);
   blk_map = nullptr;
   nblk = 0;
   stored_map.clear();
   stored_map.shrink_to_fit();
   dcol = nullptr; slot_base = nullptr; vidx = nullptr; vidx16 = nullptr; vtab = nullptr; nvtab = 0;
+  slot_vi = nullptr; slot_mask = nullptr; stencil_w = 0;
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
   col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1; dict_ranges = 0; ndict = 0;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;
@@ -655,7 +698,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       D.hv.upload(L.hv);
     }
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
-    D.l1_fly = !L.l1.empty() && l1_on_the_fly(L.A, L.l1) && D.A.in.dcol && (D.A.bd.nrows == 0 || D.A.bd.dcol);
+    D.l1_fly = !L.l1.empty() && l1_on_the_fly(L.A, L.l1) && D.A.in.delta_like() && (D.A.bd.nrows == 0 || D.A.bd.delta_like());
     if (!L.cf.empty()) D.cf = dupload(L.cf.data(), L.cf.size());
     if (!L.cf.empty() && prm.relax_order == 1 && (prm.relax_type[1] == 18 || prm.relax_type[2] == 18)) {
       std::vector<int> m(L.cf.begin(), L.cf.begin() + std::min<size_t>(L.cf.size(), (size_t)L.n_loc));
@@ -832,7 +875,7 @@ void DevAMG::fine_apply(int op, const double* x, const double* b, double* y, dou
 // layout (partials summed afterwards), else the matvec and the dot kernel.
 void DevAMG::fine_matvec_dot(const double* p, double* sv, double* dot_out, hipStream_t s) {
   DevLevel& L = lev_[0];
-  const bool fused = L.A.in.dcol && (L.A.bd.nrows == 0 || L.A.bd.dcol) && nrm_fusion_ && !x0_buf_;
+  const bool fused = L.A.in.delta_like() && (L.A.bd.nrows == 0 || L.A.bd.delta_like()) && nrm_fusion_ && !x0_buf_;
   if (!fused) {
     fine_apply(K_MATVEC, p, nullptr, sv, 1.0, 0.0, s);
     dot(L.n, sv, p, dot_out, s);
@@ -1181,7 +1224,7 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
   // Norms then reduce in another order than the dot kernel's (as the oracle's
   // differs from both); iterates are unchanged.
   const DevLevel& L0 = lev_[0];
-  const bool fuse_nrm = fuse && L0.A.in.dcol && (L0.A.bd.nrows == 0 || L0.A.bd.dcol) && nrm_fusion_;
+  const bool fuse_nrm = fuse && L0.A.in.delta_like() && (L0.A.bd.nrows == 0 || L0.A.bd.delta_like()) && nrm_fusion_;
   double resid_sq = 0.0;
   // r = f - A u, and with fusion the first sweep of the next cycle
   auto residual = [&](bool initial) {

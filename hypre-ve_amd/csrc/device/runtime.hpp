@@ -43,6 +43,9 @@ struct DevSell {
   short* dcol = nullptr;   // delta layout: 16-bit column deltas
   int* slot_base = nullptr;
   unsigned char* vidx = nullptr;  // delta layout with a value table
+  int* slot_vi = nullptr;            // stencil layout: value index per (slice, slot)
+  uint64_t* slot_mask = nullptr;     // stencil layout: lanes present per (slice, slot)
+  int stencil_w = 0;                 // stencil layout: slots per slice
   unsigned short* vidx16 = nullptr;
   double* vtab = nullptr;
   int nvtab = 0;
@@ -58,6 +61,7 @@ struct DevSell {
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
     v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group; v.dict_ranges = dict_ranges;
     v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vidx16 = vidx16; v.vtab = vtab; v.nvtab = nvtab;
+    v.slot_vi = slot_vi; v.slot_mask = slot_mask; v.stencil_w = stencil_w;
     v.blk_map = blk_map; v.nblk = nblk;
     return v;
   }
@@ -75,7 +79,12 @@ struct DevSell {
   // per stored slot its column (32-bit, 16-bit delta or 16-bit local column)
   // and value (8 B, or an 8/16-bit index into the LDS value table), plus slice
   // pointers, slot bases, dictionaries, row maps and row lengths.
+  // delta or stencil layout: columns as offsets from the row, lane per row,
+  // the finest-level fusions (residual norm, l1 on the fly) available
+  bool delta_like() const { return dcol != nullptr || slot_mask != nullptr; }
   size_t bytes() const {
+    if (slot_mask)  // stencil layout: per (slice, slot) offset, value index, lane mask
+      return (size_t)nslices * stencil_w * 16 + (rowmap ? (size_t)nrows * 4 : 0);
     const size_t colb = dcol || col16 ? 2 : 4;
     const size_t valb = vidx ? 1 : vidx16 ? 2 : 8;
     size_t b = (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * (colb + valb);

@@ -159,6 +159,113 @@ bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vecto
   return ok != 0;
 }
 
+// Slot-uniform SELL-64 (the "stencil" layout).  A constant-coefficient stencil
+// operator repeats one (column offset, value) pair in each slot of a slice: slot
+// k holds, for every lane that has it, the neighbour at row + off_k with value
+// val_k.  The slots of a slice are a shortest common supersequence of its rows'
+// (offset, value) sequences, merged row by row through their longest common
+// subsequence; each row is then matched greedily, in entry order, into the
+// slots (a missing neighbour -- grid boundary -- leaves its lane's bit clear),
+// with its first entry in slot 0.  Nothing is stored per entry: per (slice,
+// slot) a 32-bit offset, an index into the table of the slot values (<= 256
+// distinct) and the 64-bit lane mask, every slice padded to the operator's
+// widest (empty slots: mask 0), so slot k of slice s sits at s * width + k.
+// Each row still sums its entries in stored order.  false when the slots would
+// exceed max_width or the values 256 (the operator then takes the per-entry
+// delta layout).
+namespace {
+struct SlotKey {
+  int64_t off;
+  uint64_t bits;
+  bool operator==(const SlotKey& o) const { return off == o.off && bits == o.bits; }
+};
+bool is_subseq(const std::vector<SlotKey>& s, const std::vector<SlotKey>& t) {
+  size_t k = 0;
+  for (const SlotKey& e : s) {
+    while (k < t.size() && !(t[k] == e)) ++k;
+    if (k == t.size()) return false;
+    ++k;
+  }
+  return true;
+}
+// shortest common supersequence of a and b (through their LCS)
+std::vector<SlotKey> scs(const std::vector<SlotKey>& a, const std::vector<SlotKey>& b) {
+  const size_t m = a.size(), n = b.size();
+  std::vector<int> L((m + 1) * (n + 1), 0);
+  for (size_t i = m; i-- > 0;)
+    for (size_t j = n; j-- > 0;)
+      L[i * (n + 1) + j] = a[i] == b[j] ? L[(i + 1) * (n + 1) + j + 1] + 1
+                                        : std::max(L[(i + 1) * (n + 1) + j], L[i * (n + 1) + j + 1]);
+  std::vector<SlotKey> out;
+  size_t i = 0, j = 0;
+  while (i < m && j < n) {
+    if (a[i] == b[j]) { out.push_back(a[i]); ++i; ++j; }
+    else if (L[(i + 1) * (n + 1) + j] >= L[i * (n + 1) + j + 1]) out.push_back(a[i++]);
+    else out.push_back(b[j++]);
+  }
+  while (i < m) out.push_back(a[i++]);
+  while (j < n) out.push_back(b[j++]);
+  return out;
+}
+}  // namespace
+
+bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vector<int>& slot_off,
+                             std::vector<int>& slot_vi, std::vector<uint64_t>& slot_mask, std::vector<double>& tab) {
+  const int n = A.nrows;
+  const int ns = (n + 63) / 64;
+  std::vector<std::vector<SlotKey>> T(ns);
+  int ok = 1, wmax = 0;
+#pragma omp parallel for schedule(static) reduction(min : ok) reduction(max : wmax)
+  for (int s = 0; s < ns; ++s) {
+    if (!ok) continue;
+    std::vector<SlotKey> seq;
+    for (int r = s * 64; r < std::min(n, (s + 1) * 64); ++r) {
+      seq.clear();
+      for (int e = A.i[r]; e < A.i[r + 1]; ++e) {
+        SlotKey k{(int64_t)A.j[e] - r, 0};
+        std::memcpy(&k.bits, &A.a[e], 8);
+        seq.push_back(k);
+      }
+      if (!is_subseq(seq, T[s])) T[s] = scs(T[s], seq);
+      if ((int)T[s].size() > max_width) { ok = 0; break; }
+    }
+    for (const SlotKey& k : T[s])
+      if (k.off < INT_MIN || k.off > INT_MAX) ok = 0;
+    wmax = std::max(wmax, (int)T[s].size());
+  }
+  if (!ok) return false;
+  width = wmax;
+  const size_t ns_pad = (size_t)ns + 8;  // a wave's last slices and batch past the end read padding
+  const size_t nslots = ns_pad * (size_t)width;
+  slot_off.assign(nslots + 16, 0);
+  slot_mask.assign(nslots + 16, 0);
+  std::vector<double> sval(nslots + 16, 0.0);
+#pragma omp parallel for schedule(static) reduction(min : ok)
+  for (int s = 0; s < ns; ++s) {
+    if (!ok) continue;
+    const size_t s0 = (size_t)s * width;
+    for (size_t k = 0; k < T[s].size(); ++k) {
+      slot_off[s0 + k] = (int)T[s][k].off;
+      std::memcpy(&sval[s0 + k], &T[s][k].bits, 8);
+    }
+    const int w = (int)T[s].size();
+    for (int r = s * 64; r < std::min(n, (s + 1) * 64) && ok; ++r) {
+      int k = 0;
+      for (int e = A.i[r]; e < A.i[r + 1]; ++e, ++k) {
+        const int64_t off = (int64_t)A.j[e] - r;
+        while (k < w && !(slot_off[s0 + k] == off && std::memcmp(&sval[s0 + k], &A.a[e], 8) == 0)) ++k;
+        if (k == w || (e == A.i[r] && k != 0)) { ok = 0; break; }
+        slot_mask[s0 + k] |= 1ull << (r & 63);
+      }
+    }
+  }
+  if (!ok) return false;
+  std::vector<unsigned char> vi;
+  if (!build_value_table(sval, 256, vi, tab)) return false;
+  slot_vi.assign(vi.begin(), vi.end());
+  return true;
+}
+
 // Value table (value-indexed storage, lossless): when the stored values take
 // at most maxv distinct bit patterns (constant-coefficient stencils: 2-4),
 // each entry keeps an 8-bit index into the ascending-by-bits table instead of

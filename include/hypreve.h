@@ -253,8 +253,11 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands,
  * indices into a table of the operator's distinct values (where at most 256
  * occur), 8 padded and 9 jagged, each with 16-bit value indices (where at
  * most 4096 distinct values occur), 10 jagged with an LDS x-tile made of at
- * most 63 contiguous column ranges (range dictionary).  All give identical
- * bits; the forced settings exist for parity tests and experiments. */
+ * most 63 contiguous column ranges (range dictionary), 11 slot-uniform
+ * stencil layout (per slice and slot one column offset, one value and a lane
+ * mask; nothing stored per entry) where an operator is a constant-coefficient
+ * stencil, else as 7.  All give identical bits; the forced settings exist for
+ * parity tests and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* One GPU runs the hybrid Gauss-Seidel smoothers with the row blocks of an
  * N-rank run whose level-0 rows start at starts[0..nranks] (num_blocks blocks
@@ -332,7 +335,7 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver solver, HYPRE_Real *byte
  * 0 padded SELL-64, 1 jagged, 2 workgroup-per-slice, 3 jagged wave-product,
  * 4 dictionary, 5 16-bit column deltas, 6 deltas + 8-bit value table,
  * 7 deltas + 16-bit value table, 8 padded + 16-bit value table, 9 jagged +
- * 16-bit value table. */
+ * 16-bit value table, 10 range dictionary, 11 slot-uniform stencil. */
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int *kind);
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
@@ -348,7 +351,9 @@ HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver solver, HYPRE_Int level, 
 /* Read-only streaming kernel (elem_bytes 2, 4, 8 or 16): FETCH_SIZE calibration.
  * elem_bytes -1 / -2 / -5: a read/write mix, R = 1, 2 or 5 streams of n doubles
  * read and one written per element (the achievable bandwidth of a kernel that
- * reads R bytes for each byte it writes). */
+ * reads R bytes for each byte it writes).  elem_bytes -8: n doubles read as
+ * per-wave contiguous 16 KiB segments (the row loops' access shape); -9: the
+ * same with the 4 waves of a workgroup interleaved over 512-B chunks. */
 HYPRE_Int hypreve_BenchStream(HYPRE_Int elem_bytes, int64_t n, HYPRE_Int reps, HYPRE_Real *avg_ms);
 HYPRE_Int hypreve_DeviceSynchronize(void);
 const char *hypreve_BuildInfo(void);

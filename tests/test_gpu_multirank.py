@@ -189,3 +189,21 @@ def test_loopback_aggressive_bitwise(hv, nranks):
     xN, itN, rrN, nlN = _solve_nranks(hv, 16, 16, 18, kw, nranks)
     assert nlN == nl1 and all(i == it1 for i in itN)
     assert np.array_equal(x1, xN)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+@pytest.mark.parametrize("stencil,relax", [(7, 18), (7, 0), (27, 18)])
+def test_loopback_stencil_layout_bitwise(hv, nranks, stencil, relax):
+    """The slot-uniform stencil layout (policy 11) on the interior and boundary
+    rows of every rank's finest operator: offsets are taken from the stored
+    row, so a rank's interior rows (one plane in) keep one offset per slot.
+    The N-rank iterates equal the one-rank ones, and both use the layout."""
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=relax, tol=1e-8, max_iter=60,
+              sell_policy=11)
+    if relax == 0:
+        kw.update(relax_wt=0.6)
+    x1, it1, rr1, nl1 = _solve_1rank(hv, 14, 13, 16, kw, stencil=stencil)
+    xN, itN, rrN, nlN = _solve_nranks(hv, 14, 13, 16, kw, nranks, stencil=stencil)
+    assert nlN == nl1 and all(i == it1 for i in itN)
+    assert np.array_equal(x1, xN)

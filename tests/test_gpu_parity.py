@@ -99,13 +99,14 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen, wt):
     assert np.array_equal(x.get(), xo)
 
 
-@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
 def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
     workgroup-per-slice, jagged wave-product-parallel, jagged with an LDS
     x-tile, padded with 16-bit column deltas, the same with a value table,
-    padded / jagged with 16-bit value indices) forced on every
+    padded / jagged with 16-bit value indices, the slot-uniform stencil
+    layout where an operator is a constant-coefficient stencil) forced on every
     operator of the hierarchy: the same bits as the oracle.  The automatic
     choice only uses jagged and wide loops on operators too large for the
     other tests, so this is where those loops meet the oracle."""
@@ -132,7 +133,7 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     assert np.array_equal(x.get(), xo)
 
 
-@pytest.mark.parametrize("policy", [6, 7])
+@pytest.mark.parametrize("policy", [6, 7, 11])
 def test_delta_layout_wide_stride_bitwise(gpu, orc, policy):
     """16-bit column deltas where the z-neighbour is 36000 rows away: the
     per-slot base carries the stride, and the z = 0 / z = last planes (one
@@ -147,6 +148,8 @@ def test_delta_layout_wide_stride_bitwise(gpu, orc, policy):
     u0 = rng.standard_normal(n)
     f = hv.ParVector(n, f_h)
     u = hv.ParVector(n, u0)
+    if policy == 11:
+        assert amg.level_layout(0, 0) == "stencil"
     amg.cycle(f, u)
     uo = u0.copy()
     O.cycle(f_h, uo)

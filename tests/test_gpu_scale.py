@@ -1,7 +1,7 @@
 """GPU against the CPU oracle at the bench's own sizes and layouts.
 
-The automatic layouts the bench runs (A0: 16-bit column deltas + 8-bit value
-table; P0/R0: 16-bit value indices; A1/R1/A2: LDS x-tile dictionaries with
+The automatic layouts the bench runs (A0: the slot-uniform stencil layout;
+P0/R0: 16-bit value indices; A1/R1/A2: LDS x-tile dictionaries with
 thousands of distinct columns per workgroup) only appear on large operators,
 so here they meet the oracle at 256^3 (configs[1]) and on the 27-point
 operator (configs[3]'s stencil) at 96^3.  Iterates are compared bit for bit;
@@ -64,21 +64,38 @@ def test_bench_size_256_bitwise(gpu, orc):
     amg.setup(A)
     layouts = {(l, w): amg.level_layout(l, w) for l in range(3) for w in range(3)}
     print("layouts", layouts)
-    assert layouts[(0, 0)] == "delta+vt8"
+    assert layouts[(0, 0)] == "stencil"
     assert layouts[(1, 0)] == "dict"
     cycle_and_solve_bitwise(hv, orc, A, amg, 101, 3)
 
 
 def test_27pt_96_bitwise(gpu, orc):
     """configs[3]'s 27-point operator at 96^3 (885k rows): A0 takes the
-    delta + 8-bit value table layout ahead of the dictionary; one V-cycle and
-    a short solve equal the oracle's bits."""
+    slot-uniform stencil layout ahead of the dictionary; one V-cycle and a
+    short solve equal the oracle's bits."""
     hv = gpu
     A = hv.ParCSRMatrix.laplacian27(96, 96, 96)
     amg = bench_amg(hv)
     amg.setup(A)
-    assert amg.level_layout(0, 0) == "delta+vt8"
+    assert amg.level_layout(0, 0) == "stencil"
     cycle_and_solve_bitwise(hv, orc, A, amg, 202, 4)
+
+
+@pytest.mark.parametrize("coef", [(0.001, 1.0, 1.0)])
+def test_aniso_stencil_128_bitwise(gpu, orc, coef):
+    """configs[4]'s anisotropic operator at 128^3 (2M rows, automatic layouts:
+    three slot values) and the delta + 8-bit value table it replaced, forced
+    off through policy 7: both equal the oracle's bits."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(128, 128, 128, cx=coef[0], cy=coef[1], cz=coef[2])
+    amg = bench_amg(hv)
+    amg.setup(A)
+    assert amg.level_layout(0, 0) == "stencil"
+    cycle_and_solve_bitwise(hv, orc, A, amg, 303, 3)
+    amg7 = bench_amg(hv, sell_policy=7)
+    amg7.setup(A)
+    assert amg7.level_layout(0, 0) == "delta+vt8"
+    cycle_and_solve_bitwise(hv, orc, A, amg7, 304, 3)
 
 
 def test_gpu_boomer_out14(gpu):
