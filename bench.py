@@ -32,7 +32,7 @@ PROFILE_DIR = os.path.join(ROOT, "profiles")
 # hypreve_BoomerAMGGetLevelLayout name -> (residual kernel instantiation as
 # rocprofv3 names it, minus the batch width: "<prefix>B<suffix>"; description)
 KERNEL_OF_LAYOUT = {
-    "stencil": ("k_sell_delta<0, false, |, true, 3>(hve::SpArgs)",
+    "stencil": ("k_sell_stencil<0, false, true, |>(hve::SpArgs)",
                 "slot-uniform SELL-64 (per slice and slot one column offset, one value and a lane mask; "
                 "nothing stored per entry)"),
     "delta+vt8": ("k_sell_delta<0, false, |, true, 1>(hve::SpArgs)",

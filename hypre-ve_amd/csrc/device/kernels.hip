@@ -703,7 +703,12 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
       row_store<OP, NT>(p, gg, false, t[r], uo[r], d[r]);
     }
   }
-  if ((OP == OP_RESID_L1JAC || OP == OP_MATVEC) && p.nrm) wg_sum_store(acc, p.nrm + blockIdx.x);
+  if ((OP == OP_RESID_L1JAC || OP == OP_MATVEC) && p.nrm) {
+    // one partial per wave, in a fixed order (no workgroup barrier: these
+    // workgroups are short-lived and a barrier at their end holds them resident)
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if (lane == 0) p.nrm[blockIdx.x * 4 + (threadIdx.x >> 6)] = acc;
+  }
 }
 
 // Row blocks of 256 rows; gridDim.x (a multiple of 8) workgroups, each XCD's
@@ -1742,9 +1747,9 @@ int stencil_slices_per_wave() {
   return r;
 }
 int sell_nrm_parts(const SellView& M) {
-  if (M.slot_mask) {
+  if (M.slot_mask) {  // one per wave
     const int R = stencil_slices_per_wave();
-    return std::max(8, (((std::max(M.nrows, 1) + 63) / 64 + 4 * R - 1) / (4 * R) + 7) / 8 * 8);
+    return 4 * std::max(8, (((std::max(M.nrows, 1) + 63) / 64 + 4 * R - 1) / (4 * R) + 7) / 8 * 8);
   }
   const int nb = blocks_pad8(std::max(M.nrows, 1));
   return M.vidx16 ? std::min(nb, 2048) : nb;

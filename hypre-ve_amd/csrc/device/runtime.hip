@@ -577,8 +577,9 @@ void DevAMG::init_workspace(int n, DevComm* comm) {
   comm_ = (comm && comm->size() > 1) ? comm : nullptr;
   init_common(&stream_, &comm_stream_, &ev_packed_, &ev_halo_);
   dot_part_ = dalloc<double>(1024);
-  // fused norms / dots: one partial per row block (delta kernels) or per workgroup (PCG update)
-  nrm_part_ = dalloc<double>(std::max<size_t>(2 * ((size_t)n / 256 + 16), 4096));
+  // fused norms / dots: one partial per row block (delta kernels), per wave
+  // (stencil kernel) or per workgroup (PCG update)
+  nrm_part_ = dalloc<double>(std::max<size_t>(4 * ((size_t)n / 256 + 32), 4096));
   dscal_ = dalloc<double>(16);
   HVE_HIP(hipMemset(dscal_, 0, 16 * sizeof(double)));
   HVE_HIP(hipHostMalloc((void**)&hscal_, 16 * sizeof(double), hipHostMallocDefault));

@@ -39,3 +39,8 @@ if [[ $WHAT == all || $WHAT == pmc ]]; then
   python scripts/pmc_summary.py $OUT 60000 > $OUT/pmc_summary.txt 2>&1
 fi
 echo "=== done"
+if [[ $WHAT == rsweep ]]; then
+  for R in 2 4; do
+    HVE_STENCIL_R=$R step ops${N}_R$R 500 python scripts/ops_time.py $N
+  done
+fi

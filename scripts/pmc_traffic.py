@@ -17,7 +17,7 @@ import os
 import sys
 
 
-PREFIXES = ("hve::k_sell<0,", "hve::k_sell_delta<0,")
+PREFIXES = ("hve::k_sell<0,", "hve::k_sell_delta<0,", "hve::k_sell_stencil<0,")
 
 
 def mean_counter(path, counter, grid, prefixes=PREFIXES, names=None):
@@ -54,7 +54,7 @@ def main():
     write, nw = mean_counter(os.path.join(root, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE", grid)
     if fetch is None or write is None:
         raise SystemExit("no matching dispatches")
-    out = {"kernel": "k_sell / k_sell_delta <OP_RESID> finest level", "kernel_names": sorted(names),
+    out = {"kernel": "k_sell / k_sell_delta / k_sell_stencil <OP_RESID> finest level", "kernel_names": sorted(names),
            "grid": grid, "dispatches": [nf, nw],
            "fetch_kib": fetch, "write_kib": write,
            "traffic_bytes": 2.0 * fetch * 1024 + write * 1024,
