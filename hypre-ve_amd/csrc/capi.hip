@@ -1355,6 +1355,43 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver s, HYPRE_Int num_blocks)
   API_END
 }
 
+// Host check of the slot-uniform stencil layout of a level's A: every row's
+// (column, value) sequence rebuilt from its slice's pattern equals the CSR row
+// entry for entry (bit patterns of the values included).  *width = 0 when the
+// operator is not a constant-coefficient stencil (the layout does not build).
+HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int* width,
+                                              HYPRE_Int* npatterns) {
+  CHECK_ARG(s && s->kind == KIND_AMG && !s->H.lev.empty(), 1);
+  CHECK_ARG(level >= 0 && level < (HYPRE_Int)s->H.lev.size(), 2);
+  API_BEGIN
+  const CSR& A = s->H.lev[level].A;
+  std::vector<int> pat, off, vi;
+  std::vector<uint64_t> mask;
+  std::vector<double> tab;
+  int W = 0;
+  if (width) *width = 0;
+  if (npatterns) *npatterns = 0;
+  if (!build_sell_stencil_host(A, 64, W, pat, off, vi, mask, tab)) return g_error;
+  for (int r = 0; r < A.nrows; ++r) {
+    const size_t p0 = (size_t)pat[r >> 6] * W;
+    int e = A.i[r];
+    for (int k = 0; k < W; ++k) {
+      if (!((mask[p0 + k] >> (r & 63)) & 1)) continue;
+      if (e >= A.i[r + 1] || (int64_t)A.j[e] - r != off[p0 + k] ||
+          std::memcmp(&tab[vi[p0 + k]], &A.a[e], 8) != 0)
+        throw std::runtime_error("stencil layout: row " + std::to_string(r) + " differs at its entry " +
+                                 std::to_string(e - A.i[r]));
+      ++e;
+    }
+    if (e != A.i[r + 1]) throw std::runtime_error("stencil layout: row " + std::to_string(r) + " loses entries");
+    if (A.i[r + 1] > A.i[r] && !(mask[p0] >> (r & 63) & 1))
+      throw std::runtime_error("stencil layout: row " + std::to_string(r) + " does not start in slot 0");
+  }
+  if (width) *width = W;
+  if (npatterns) *npatterns = (HYPRE_Int)((off.size() - 16) / std::max(W, 1));
+  API_END
+}
+
 // Average time of one application of a level operator (which: 0 = A_l as the
 // residual r = f - A u, 1 = P_l as prolongation u_l += P u_{l+1}, 2 = R_l as
 // restriction f_{l+1} = R r_l) with its algorithmic bytes: every stored

@@ -30,7 +30,8 @@ struct SellView {
   const double* vtab = nullptr;         // the operator's distinct values
   const int* slot_vi = nullptr;         // stencil layout (no per-entry data): value index,
   const uint64_t* slot_mask = nullptr;  // lanes present, offset (slot_base) per (slice, slot)
-  int stencil_w = 0;                    // stencil layout: slots per slice
+  int stencil_w = 0;                    // stencil layout: slots per pattern
+  const int* slice_pat = nullptr;       // stencil layout: slot pattern of each slice
   int nvtab = 0;
   // Traversal order of the workgroup row blocks (logical block -> stored row
   // block, nullptr = identity): blocks are visited so that each XCD streams a
@@ -81,6 +82,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const
                             hipStream_t st);
 int sell_batch_override();
 int stencil_slices_per_wave();
+int stencil_grid(int nrows);
 int sell_pipe_override();
 bool sell_nt();
 bool sell_pw();

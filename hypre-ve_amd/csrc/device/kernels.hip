@@ -78,7 +78,8 @@ struct SpArgs {
   int nvtab;
   const int* __restrict__ slot_vi;           // stencil layout: value index per (slice, slot)
   const uint64_t* __restrict__ slot_mask;    // stencil layout: lanes present per (slice, slot)
-  int sw;                                    // stencil layout: slots per slice
+  int sw;                                    // stencil layout: slots per pattern
+  const int* __restrict__ slice_pat;         // stencil layout: slot pattern of each slice
   const int* __restrict__ blk_map;           // logical -> stored row block (nullptr: identity)
   int nblk;                                  // entries of blk_map
   double* __restrict__ y;         // output
@@ -573,10 +574,11 @@ __device__ __forceinline__ void wg_sum_store(double v, double* out) {
 // ---------------------------------------------------------------------------
 // Slot-uniform SELL-64 (host: build_sell_stencil_host), for constant-
 // coefficient stencils: slot k of a slice is one neighbour offset and one value
-// for all its lanes, so nothing is streamed per entry.  Every slice has W slots
-// (slot k of slice s at s*W + k: no slice pointer to chase); a slot's offset,
-// value index and lane mask are wave-uniform scalar loads, and so is its value
-// from the table.  Each wave runs R consecutive slices with all
+// for all its lanes, so nothing is streamed per entry.  Slices with the same
+// slot sequence share a pattern of W slots (slot k of slice s at
+// slice_pat[s]*W + k); a slot's offset, value index and lane mask are
+// wave-uniform scalar loads from the few-KiB pattern table, and so is its
+// value from the value table.  Each wave runs R consecutive slices with all
 // their loads of a batch in flight together: per row only x (gathered at
 // row + off: consecutive rows, one offset, coalesced), b and y move, so R
 // slices per wave keep enough bytes in flight to cover HBM latency.  Each row
@@ -595,6 +597,9 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
   const bool fly = (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC) && p.l1 == nullptr;
   double acc = 0.0;
   if (slice0 * kWave < p.nrows) {
+    int pat[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) pat[r] = __builtin_amdgcn_readfirstlane(p.slice_pat[slice0 + r]);
     int row[R], g[R];
     bool act[R];
     double t[R], uo[R], d[R], s1[R];
@@ -621,8 +626,9 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
       // the diagonal is every row's first entry, in slot 0 (the host checks it)
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const uint64_t m0 = p.slot_mask[(size_t)(slice0 + r) * W];
-        const double d0 = p.vtab[__builtin_amdgcn_readfirstlane(p.slot_vi[(size_t)(slice0 + r) * W])];
+        const size_t s0 = (size_t)pat[r] * W;
+        const uint64_t m0 = p.slot_mask[s0];
+        const double d0 = p.vtab[__builtin_amdgcn_readfirstlane(p.slot_vi[s0])];
         if (act[r]) {
           uo[r] = p.x[g[r]];
           d[r] = ((m0 >> lane) & 1) ? d0 : 0.0;
@@ -637,7 +643,7 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
         // the tail padding and are dropped)
         // (readfirstlane keeps every load of the batch unconditional and scalar:
         // the compiler would otherwise sink each one into its lane-masked use)
-        const size_t sb = (size_t)(slice0 + r) * W + k;
+        const size_t sb = (size_t)pat[r] * W + k;
         int off[B], vi[B];
         uint32_t mlo[B], mhi[B];
 #pragma unroll
@@ -1424,8 +1430,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   if (M.slot_mask) {  // slot-uniform stencil: R slices per wave, 4R per workgroup
     const int R = stencil_slices_per_wave();
     a.sw = M.stencil_w;
+    a.slice_pat = M.slice_pat;
     a.nblocks_pad = (((M.nrows + 63) / 64 + 4 * R - 1) / (4 * R) + 7) / 8 * 8;
-    const dim3 sgrid(a.nblocks_pad);
+    const dim3 sgrid(stencil_grid(M.nrows));
 #define HVE_S(OPV, CF, RR)                                                                         \
   if (nt) hipLaunchKernelGGL((k_sell_stencil<OPV, CF, true, RR>), sgrid, block, 0, s, a);         \
   else hipLaunchKernelGGL((k_sell_stencil<OPV, CF, false, RR>), sgrid, block, 0, s, a);
@@ -1746,11 +1753,16 @@ int stencil_slices_per_wave() {
   }();
   return r;
 }
+// Grid of the stencil loop: one workgroup per block of 4R slices, whole XCD
+// rounds.  (A persistent grid that fetched each next block's traversal entry
+// and patterns ahead measured slower: 512^3 A0 1.60-1.68 ms against 0.87.)
+int stencil_grid(int nrows) {
+  const int R = stencil_slices_per_wave();
+  const int nlb = ((std::max(nrows, 1) + 63) / 64 + 4 * R - 1) / (4 * R);
+  return std::max(8, (nlb + 7) / 8 * 8);
+}
 int sell_nrm_parts(const SellView& M) {
-  if (M.slot_mask) {  // one per wave
-    const int R = stencil_slices_per_wave();
-    return 4 * std::max(8, (((std::max(M.nrows, 1) + 63) / 64 + 4 * R - 1) / (4 * R) + 7) / 8 * 8);
-  }
+  if (M.slot_mask) return 4 * stencil_grid(M.nrows);  // one per wave
   const int nb = blocks_pad8(std::max(M.nrows, 1));
   return M.vidx16 ? std::min(nb, 2048) : nb;
 }

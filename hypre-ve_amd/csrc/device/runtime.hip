@@ -168,8 +168,9 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
     std::vector<int> so, svi;
     std::vector<uint64_t> sm;
     std::vector<double> tab;
+    std::vector<int> spat;
     int sw = 0;
-    if (build_sell_stencil_host(A, 64, sw, so, svi, sm, tab)) {
+    if (build_sell_stencil_host(A, 64, sw, spat, so, svi, sm, tab)) {
       nrows = A.nrows;
       ncols = A.ncols;
       nslices = (A.nrows + 63) / 64;
@@ -180,6 +181,10 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       pipe = 0;
       wide = 0;
       pw = 0;
+      slice_pat = dupload(spat.data(), spat.size());
+      npat = (int)((so.size() - 16) / std::max(sw, 1));
+      if (getenv("HVE_LAYOUT_LOG"))
+        fprintf(stderr, "[layout] stencil rows=%d width=%d patterns=%d values=%zu\n", A.nrows, sw, npat, tab.size());
       slot_base = dupload(so.data(), so.size());
       slot_vi = dupload(svi.data(), svi.size());
       slot_mask = dupload(sm.data(), sm.size());
@@ -457,13 +462,14 @@ void DevSell::release() {
   if (vtab) (void)hipFree(vtab);
   if (slot_vi) (void)hipFree(slot_vi);
   if (slot_mask) (void)hipFree(slot_mask);
+  if (slice_pat) (void)hipFree(slice_pat);
   if (blk_map) (void)hipFree(blk_map);
   blk_map = nullptr;
   nblk = 0;
   stored_map.clear();
   stored_map.shrink_to_fit();
   dcol = nullptr; slot_base = nullptr; vidx = nullptr; vidx16 = nullptr; vtab = nullptr; nvtab = 0;
-  slot_vi = nullptr; slot_mask = nullptr; stencil_w = 0;
+  slot_vi = nullptr; slot_mask = nullptr; stencil_w = 0; slice_pat = nullptr; npat = 0;
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
   col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1; dict_ranges = 0; ndict = 0;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;

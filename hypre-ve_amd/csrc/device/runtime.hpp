@@ -45,7 +45,9 @@ struct DevSell {
   unsigned char* vidx = nullptr;  // delta layout with a value table
   int* slot_vi = nullptr;            // stencil layout: value index per (slice, slot)
   uint64_t* slot_mask = nullptr;     // stencil layout: lanes present per (slice, slot)
-  int stencil_w = 0;                 // stencil layout: slots per slice
+  int stencil_w = 0;                 // stencil layout: slots per pattern
+  int* slice_pat = nullptr;          // stencil layout: pattern of each slice
+  int npat = 0;
   unsigned short* vidx16 = nullptr;
   double* vtab = nullptr;
   int nvtab = 0;
@@ -61,7 +63,7 @@ struct DevSell {
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
     v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group; v.dict_ranges = dict_ranges;
     v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vidx16 = vidx16; v.vtab = vtab; v.nvtab = nvtab;
-    v.slot_vi = slot_vi; v.slot_mask = slot_mask; v.stencil_w = stencil_w;
+    v.slot_vi = slot_vi; v.slot_mask = slot_mask; v.stencil_w = stencil_w; v.slice_pat = slice_pat;
     v.blk_map = blk_map; v.nblk = nblk;
     return v;
   }
@@ -84,7 +86,7 @@ struct DevSell {
   bool delta_like() const { return dcol != nullptr || slot_mask != nullptr; }
   size_t bytes() const {
     if (slot_mask)  // stencil layout: per (slice, slot) offset, value index, lane mask
-      return (size_t)nslices * stencil_w * 16 + (rowmap ? (size_t)nrows * 4 : 0);
+      return (size_t)nslices * 4 + (size_t)npat * stencil_w * 16 + (rowmap ? (size_t)nrows * 4 : 0);
     const size_t colb = dcol || col16 ? 2 : 4;
     const size_t valb = vidx ? 1 : vidx16 ? 2 : 8;
     size_t b = (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * (colb + valb);

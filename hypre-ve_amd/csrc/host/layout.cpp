@@ -4,6 +4,7 @@
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
+#include <unordered_map>
 #include <unordered_set>
 
 #include "hve_host.hpp"
@@ -199,8 +200,12 @@ std::vector<SlotKey> scs(const std::vector<SlotKey>& a, const std::vector<SlotKe
   std::vector<SlotKey> out;
   size_t i = 0, j = 0;
   while (i < m && j < n) {
+    const int la = L[(i + 1) * (n + 1) + j], lb = L[i * (n + 1) + j + 1];
     if (a[i] == b[j]) { out.push_back(a[i]); ++i; ++j; }
-    else if (L[(i + 1) * (n + 1) + j] >= L[i * (n + 1) + j + 1]) out.push_back(a[i++]);
+    // ties go to the smaller (offset, value) first: rows stored in ascending
+    // column order (after the diagonal) then merge into that same order
+    else if (la > lb || (la == lb && (a[i].off < b[j].off || (a[i].off == b[j].off && a[i].bits < b[j].bits))))
+      out.push_back(a[i++]);
     else out.push_back(b[j++]);
   }
   while (i < m) out.push_back(a[i++]);
@@ -209,8 +214,9 @@ std::vector<SlotKey> scs(const std::vector<SlotKey>& a, const std::vector<SlotKe
 }
 }  // namespace
 
-bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vector<int>& slot_off,
-                             std::vector<int>& slot_vi, std::vector<uint64_t>& slot_mask, std::vector<double>& tab) {
+bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vector<int>& slice_pat,
+                             std::vector<int>& slot_off, std::vector<int>& slot_vi, std::vector<uint64_t>& slot_mask,
+                             std::vector<double>& tab) {
   const int n = A.nrows;
   const int ns = (n + 63) / 64;
   std::vector<std::vector<SlotKey>> T(ns);
@@ -262,7 +268,58 @@ bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vecto
   if (!ok) return false;
   std::vector<unsigned char> vi;
   if (!build_value_table(sval, 256, vi, tab)) return false;
-  slot_vi.assign(vi.begin(), vi.end());
+  // Slices with the same slot sequence (offsets, values and lane masks: the
+  // interior of a stencil, and each kind of boundary slice) share one
+  // pattern; a slice keeps only its pattern's index, so the slot data of a
+  // launch is a few KiB that stay in cache instead of a stream.
+  const int W = width;
+  std::vector<uint64_t> h(ns);
+#pragma omp parallel for schedule(static)
+  for (int s = 0; s < ns; ++s) {
+    uint64_t x = 1469598103934665603ull;
+    for (int k = 0; k < W; ++k) {
+      const size_t i = (size_t)s * W + k;
+      for (uint64_t v : {(uint64_t)(uint32_t)slot_off[i], (uint64_t)vi[i], slot_mask[i]}) {
+        x ^= v + 0x9e3779b97f4a7c15ull + (x << 6) + (x >> 2);
+      }
+    }
+    h[s] = x;
+  }
+  std::unordered_map<uint64_t, std::vector<int>> seen;  // hash -> patterns
+  std::vector<int> po, pv;
+  std::vector<uint64_t> pm;
+  slice_pat.assign((size_t)ns + 8, 0);
+  auto same = [&](int s, int pt) {
+    for (int k = 0; k < W; ++k) {
+      const size_t i = (size_t)s * W + k, j = (size_t)pt * W + k;
+      if (slot_off[i] != po[j] || (int)vi[i] != pv[j] || slot_mask[i] != pm[j]) return false;
+    }
+    return true;
+  };
+  for (int s = 0; s < ns; ++s) {
+    std::vector<int>& cand = seen[h[s]];
+    int found = -1;
+    for (int pt : cand)
+      if (same(s, pt)) { found = pt; break; }
+    if (found < 0) {
+      found = (int)(po.size() / (size_t)std::max(W, 1));
+      for (int k = 0; k < W; ++k) {
+        const size_t i = (size_t)s * W + k;
+        po.push_back(slot_off[i]);
+        pv.push_back(vi[i]);
+        pm.push_back(slot_mask[i]);
+      }
+      cand.push_back(found);
+    }
+    slice_pat[s] = found;
+  }
+  // a batch reads up to 8 slots past a pattern's last: 16 slots of tail
+  po.resize(po.size() + 16, 0);
+  pv.resize(pv.size() + 16, 0);
+  pm.resize(pm.size() + 16, 0);
+  slot_off.swap(po);
+  slot_vi.swap(pv);
+  slot_mask.swap(pm);
   return true;
 }
 

@@ -21,13 +21,15 @@ constexpr short kDeltaPad = -32768;
 bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vector<int>& slot_base,
                            std::vector<short>& dcol, std::vector<double>& val);
 // Slot-uniform SELL-64 for constant-coefficient stencils: no per-entry data.
-// Every slice has `width` slots; slot k of slice s (index s * width + k)
-// holds column row + slot_off, value tab[slot_vi] for the lanes set in
-// slot_mask (0 for a slice's unused slots).  The arrays cover 8 slices past
-// the last and 16 slots of tail.  false when a slice needs more than
-// max_width slots or more than 256 distinct values occur (layout.cpp).
-bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vector<int>& slot_off,
-                             std::vector<int>& slot_vi, std::vector<uint64_t>& slot_mask, std::vector<double>& tab);
+// Slices with identical slot sequences share a pattern: slice s uses pattern
+// slice_pat[s], whose `width` slots k (index pattern * width + k) hold column
+// row + slot_off, value tab[slot_vi] for the lanes set in slot_mask (0 for
+// unused slots).  slice_pat covers 8 slices past the last, the slot arrays 16
+// slots of tail.  false when a slice needs more than max_width slots or more
+// than 256 distinct values occur (layout.cpp).
+bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vector<int>& slice_pat,
+                             std::vector<int>& slot_off, std::vector<int>& slot_vi, std::vector<uint64_t>& slot_mask,
+                             std::vector<double>& tab);
 // Lossless value table: idx[i] indexes tab (ascending by bit pattern) with
 // tab[idx[i]] bitwise equal to val[i]; false when more than maxv (<= 256)
 // distinct values occur.

@@ -191,6 +191,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGSetGsRankStarts", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGSetRankEmulation", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
+    ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchLevelOpStoredBytes", _i, [_p, _i, _i, _pd]),
     ("hypreve_BenchStream", _i, [_i, C.c_int64, _i, _pd]),
@@ -538,6 +539,14 @@ class BoomerAMG:
 
     def gs_schedule_check(self, num_blocks):
         check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
+
+    def stencil_layout_check(self, level=0):
+        """(slots per pattern, patterns) of level's A in the stencil layout,
+        checked row by row against the CSR on the host; (0, 0) when the
+        operator is not a constant-coefficient stencil."""
+        w, npat = C.c_int(), C.c_int()
+        check(lib().hypreve_BoomerAMGStencilLayoutCheck(self.h, level, C.byref(w), C.byref(npat)), "StencilLayoutCheck")
+        return w.value, npat.value
 
     def bench_level_op(self, level, which=0, reps=20):
         """(avg_ms, algorithmic bytes, padded entries) of A_l (0), P_l (1) or R_l (2)."""

@@ -340,6 +340,12 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, 
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
 HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_blocks);
+/* Host check of the slot-uniform stencil layout of level's A (after
+ * hypreve_BoomerAMGSetupHost or Setup): every row rebuilt from its slice's
+ * slot pattern equals the CSR row entry for entry.  *width = 0 (and
+ * *npatterns = 0) when the operator is not a constant-coefficient stencil. */
+HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int *width,
+                                              HYPRE_Int *npatterns);
 /* One level operator (which 0 = A as residual, 1 = P as prolongation, 2 = R
  * as restriction): average ms over reps, algorithmic bytes, padded entries. */
 HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,

@@ -213,3 +213,30 @@ def test_chebyshev_setup(hv, scale):
         den = de * de - 2 * th * th
         ref = [-4 * th / den, 2 / den, 0.0]
         assert np.allclose(co, ref, rtol=1e-13, atol=0)
+
+
+@pytest.mark.parametrize("gen,dims,width", [("7", (200, 180, 3), 7), ("7", (10, 10, 10), 7), ("27", (13, 12, 15), 27),
+                                             ("aniso", (28, 26, 24), 7), ("7", (1, 1, 70), 3)])
+def test_stencil_layout_rebuilds_rows(hv, gen, dims, width):
+    """The slot-uniform stencil layout (A0 of constant-coefficient operators):
+    every row rebuilt from its slice's slot pattern equals the CSR row entry
+    for entry, values bit for bit, the diagonal in slot 0.  (200, 180, 3)
+    has slices with no full row (y = 0 and y = 179 lines in one slice: the
+    slots are a common supersequence of all its rows); (1, 1, 70) is a 1-D
+    chain.  The
+    Galerkin level 1 is no stencil: the layout does not build there."""
+    if gen == "27":
+        A = hv.ParCSRMatrix.laplacian27(*dims)
+    elif gen == "aniso":
+        A = hv.ParCSRMatrix.laplacian(*dims, cx=0.001, cy=1.0, cz=1.0)
+    else:
+        A = hv.ParCSRMatrix.laplacian(*dims)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup_host(A)
+    w, npat = amg.stencil_layout_check(0)
+    assert w == width  # rows in ascending column order merge into the stencil's own slots
+    assert 1 <= npat <= (A.n + 63) // 64
+    if amg.num_levels() > 2:
+        assert amg.stencil_layout_check(1) == (0, 0)
