@@ -602,8 +602,11 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
     for (int r = 0; r < R; ++r) pat[r] = __builtin_amdgcn_readfirstlane(p.slice_pat[slice0 + r]);
     int row[R], g[R];
     bool act[R];
-    double t[R], uo[R], d[R], s1[R];
+    double t[R], uo[R], d[R], s1[R], xg[R], l1g[R];
     bool neg[R], seen[R];
+    // the smoothers' own x_g and l1_g go out with b, not after the row sum
+    // (a late load would add a dependent round trip to every workgroup)
+    constexpr bool SMOOTH = OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       row[r] = (slice0 + r) * kWave + lane;
@@ -615,6 +618,8 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
         sstore<NT>(p.y + g[r], p.x[g[r]]);
       act[r] = ex && !skip;
       t[r] = act[r] ? row_init<OP, NT>(p, g[r]) : 0.0;
+      xg[r] = (SMOOTH && act[r]) ? p.x[g[r]] : 0.0;
+      l1g[r] = (SMOOTH && act[r] && !fly) ? mload<NT>(p.l1 + g[r]) : 1.0;
       uo[r] = 0.0;
       d[r] = 0.0;
       s1[r] = 0.0;
@@ -690,19 +695,28 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
         if (OP == OP_RESID_L1JAC) {
           if (p.y) sstore<NT>(p.y + gg, t[r]);
           if (p.nrm) acc += t[r] * t[r];
-          sstore<NT>(p.y2 + gg, p.x[gg] + t[r] / l1v);
+          sstore<NT>(p.y2 + gg, xg[r] + t[r] / l1v);
         } else if (OP == OP_L1JAC) {
-          sstore<NT>(p.y + gg, p.x[gg] + t[r] / l1v);
+          sstore<NT>(p.y + gg, xg[r] + t[r] / l1v);
         } else if (OP == OP_L1JAC_W) {
           const double v = (-p.w) * t[r];
-          sstore<NT>(p.y + gg, p.x[gg] + v / l1v);
+          sstore<NT>(p.y + gg, xg[r] + v / l1v);
         }
         continue;
       }
       if (OP == OP_RESID_L1JAC) {
         if (p.y) sstore<NT>(p.y + gg, t[r]);
         if (p.nrm) acc += t[r] * t[r];
-        sstore<NT>(p.y2 + gg, p.x[gg] + t[r] / mload<NT>(p.l1 + gg));
+        sstore<NT>(p.y2 + gg, xg[r] + t[r] / l1g[r]);
+        continue;
+      }
+      if (OP == OP_L1JAC) {
+        sstore<NT>(p.y + gg, xg[r] + t[r] / l1g[r]);
+        continue;
+      }
+      if (OP == OP_L1JAC_W) {
+        const double v = (-p.w) * t[r];
+        sstore<NT>(p.y + gg, xg[r] + v / l1g[r]);
         continue;
       }
       if (OP == OP_MATVEC && p.nrm) acc += p.x[gg] * t[r];
