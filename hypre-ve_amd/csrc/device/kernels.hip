@@ -299,6 +299,11 @@ __device__ __forceinline__ void sell_row_op(const SpArgs& p, const double* vt, i
     return;
   }
   const int llen = skip ? 0 : blen;
+  // the epilogue's own x_g and l1_g go out before the row loop, not after it
+  constexpr bool XG = OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC;
+  constexpr bool LG = XG || OP == OP_RESTRICT_ZG;
+  const double xg = (XG && !skip) ? p.x[g] : 0.0;
+  const double l1g = (LG && !skip) ? mload<NT>(p.l1 + g) : 1.0;
 #define HVE_ROW(SUBV, K0, T0) row_sum<SUBV, B, PIPE, NT, JAG>(cp, vl, K0, width, blen, llen, p.x, T0)
 
   if (OP == OP_RESID || OP == OP_L1JAC || OP == OP_RESID_L1JAC) {
@@ -309,19 +314,19 @@ __device__ __forceinline__ void sell_row_op(const SpArgs& p, const double* vt, i
     }
     if (OP == OP_RESID_L1JAC) {
       sstore<NT>(p.y + g, t);
-      sstore<NT>(p.y2 + g, p.x[g] + t / mload<NT>(p.l1 + g));
+      sstore<NT>(p.y2 + g, xg + t / l1g);
     } else if (OP == OP_RESID) sstore<NT>(p.y + g, t);
-    else sstore<NT>(p.y + g, p.x[g] + t / mload<NT>(p.l1 + g));
+    else sstore<NT>(p.y + g, xg + t / l1g);
   } else if (OP == OP_L1JAC_W) {
     const double t = HVE_ROW(false, 0, skip ? 0.0 : -mload<NT>(p.b + g));
     if (skip) { sstore<NT>(p.y + g, p.x[g]); return; }
     const double v = (-p.w) * t;
-    sstore<NT>(p.y + g, p.x[g] + v / mload<NT>(p.l1 + g));
+    sstore<NT>(p.y + g, xg + v / l1g);
   } else if (OP == OP_MATVEC || OP == OP_RESTRICT || OP == OP_RESTRICT_ZG) {
     const double t = HVE_ROW(false, 0, 0.0);
     if (!skip) {
       sstore<NT>(p.y + g, t);
-      if (OP == OP_RESTRICT_ZG) sstore<NT>(p.y2 + g, 0.0 + t / mload<NT>(p.l1 + g));
+      if (OP == OP_RESTRICT_ZG) sstore<NT>(p.y2 + g, 0.0 + t / l1g);
     }
   } else if (OP == OP_PROLONG) {
     const double t = HVE_ROW(false, 0, skip ? 0.0 : mload<NT>(p.y + g));
@@ -441,6 +446,40 @@ __device__ __forceinline__ void row_store(const SpArgs& p, int g, bool skip, dou
     const double alpha = p.w;
     const bool neg = (alpha == -1.0);
     sstore<NT>(p.y + g, (alpha == 1.0 || neg) ? t : alpha * t);
+  }
+}
+
+// Row epilogue with the smoother's x_g and l1_g loaded early (row_preload).
+struct RowPre {
+  double xg = 0.0, l1g = 1.0;
+};
+template <int OP, bool NT>
+__device__ __forceinline__ RowPre row_preload(const SpArgs& p, int g) {
+  RowPre r;
+  if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC) r.xg = p.x[g];
+  if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC || OP == OP_RESTRICT_ZG) r.l1g = mload<NT>(p.l1 + g);
+  return r;
+}
+template <int OP, bool NT>
+__device__ __forceinline__ void row_store_pre(const SpArgs& p, int g, bool skip, double t, double uo, double d,
+                                              const RowPre& pre) {
+  if (skip) {
+    if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) sstore<NT>(p.y + g, p.x[g]);
+    return;
+  }
+  if (OP == OP_RESID_L1JAC) {
+    sstore<NT>(p.y + g, t);
+    sstore<NT>(p.y2 + g, pre.xg + t / pre.l1g);
+  } else if (OP == OP_L1JAC) {
+    sstore<NT>(p.y + g, pre.xg + t / pre.l1g);
+  } else if (OP == OP_L1JAC_W) {
+    const double v = (-p.w) * t;
+    sstore<NT>(p.y + g, pre.xg + v / pre.l1g);
+  } else if (OP == OP_RESTRICT_ZG) {
+    sstore<NT>(p.y + g, t);
+    sstore<NT>(p.y2 + g, 0.0 + t / pre.l1g);
+  } else {
+    row_store<OP, NT>(p, g, false, t, uo, d);
   }
 }
 
@@ -954,10 +993,12 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   int g = 0;
   bool skip = false;
   double t = 0.0, uo = 0.0, d = 0.0;
+  RowPre pre;
   if (own) {
     g = p.rowmap ? mload<NT>(p.rowmap + row) : row;
     if (CFSEL) skip = p.cf[g] != p.relax_points;
     t = row_init<OP, NT>(p, g);
+    if (!skip) pre = row_preload<OP, NT>(p, g);
     if (OP == OP_JAC) {
       uo = p.x[g];
       d = blen > 0 ? p.val[beg + lane] : 0.0;  // diagonal stored first
@@ -1050,7 +1091,7 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
 #pragma unroll
     for (int q = 0; q < B; ++q) { c[q] = cn[q]; a[q] = an[q]; }
   }
-  if (own) row_store<OP, NT>(p, g, skip, t, uo, d);
+  if (own) row_store_pre<OP, NT>(p, g, skip, t, uo, d, pre);
 }
 
 // ---------------------------------------------------------------------------
