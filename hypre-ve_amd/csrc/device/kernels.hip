@@ -1799,7 +1799,9 @@ int dot_num_parts(int n) {
   return b < 1024 ? (b < 1 ? 1 : b) : 1024;
 }
 // Slices per wave of the stencil loop (k_sell_stencil): HVE_STENCIL_R=1|2|4.
-// Measured on MI355X (256^3 A0): 1 / 2 / 4 slices 0.105 / 0.107 / 0.113 ms.
+// Measured on MI355X (256^3 A0): 1 / 2 / 4 slices 0.105 / 0.107 / 0.113 ms;
+// 512^3 with slot patterns: 0.877 / 0.897 / 0.898 ms, 15.6 / 17.0 / 17.9 ms
+// per solve iteration.
 int stencil_slices_per_wave() {
   static const int r = [] {
     const char* e = getenv("HVE_STENCIL_R");
