@@ -1,16 +1,19 @@
 """BoomerAMG V-cycle throughput on MI355X (BASELINE.json metric).
 
-Workload: 3-D 7-point Laplacian, 512^3 rows per GPU (configs[2]'s grid, the
-north-star size), BoomerAMG with PMIS coarsening, extended+i interpolation
-(P_max_elmts 4), l1-Jacobi down/up smoothing, Gaussian elimination on the
-coarsest level.  On one GPU the 256^3 problem (configs[1]) is measured after
-it into "secondary".
+Workload: 3-D 7-point Laplacian 512^3 (configs[2]'s grid, the north-star
+size), BoomerAMG with PMIS coarsening, extended+i interpolation (P_max_elmts
+4), l1-Jacobi down/up smoothing, Gaussian elimination on the coarsest level.
+On one GPU the 256^3 problem (configs[1]) is measured after it into
+"secondary", and the CPU oracle's iterate after its sample is compared with
+the GPU's bit for bit ("parity").
 A step = one BoomerAMG solve iteration (hypre_BoomerAMGSolve loop body): one
 V-cycle plus the fine-grid residual and its norm.  Inputs are resident in HBM
 before the timed region; the host setup phase is not timed.
 
-Multi-GPU: one process per GPU (torch.distributed.run); weak scaling with
-n^3 rows per GPU (global grid n x n x n*N, row blocks by z-slab).
+Multi-GPU: one process per GPU (torch.distributed.run).  Strong scaling by
+default: the global 512^3 problem (ij -n is the global size, ij.c:1780) in
+z-slab row blocks, as configs[3]/[4] state it; --weak keeps n^3 rows per GPU.
+configs[3]: --stencil 27; configs[4]: --coef 0.001,1,1 --agg 1.
 """
 import argparse
 import json
@@ -104,8 +107,10 @@ class heartbeat:
 def oracle_cpu_baseline(amg, nrows, n, pcg, args):
     """The reference's CPU solve path, restated in C (oracle/oracle.c, the
     parity checker) and run with OpenMP over rows on this host's cores, on the
-    hierarchy `amg` (one-process setup) with rhs = ones.  Sample sized to
-    about args.cpu_seconds of CPU work."""
+    hierarchy `amg` (one-process setup) with rhs = ones, from x = 0.  Sample
+    sized to about args.cpu_seconds of CPU work.  Returns (cpu_baseline dict,
+    the oracle's iterate, iterations): the bench then runs the GPU for the same
+    iterations from the same start and compares the iterates bit for bit."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
 
@@ -129,10 +134,40 @@ def oracle_cpu_baseline(amg, nrows, n, pcg, args):
     threads = oracle_py.num_threads()
     what = "PCG iterations (one V-cycle preconditioner each)" if pcg else "solve iterations (V-cycle + residual norm)"
     cpu = {"value": round(nrows * done / tcpu, 1), "unit": "DOF/s", "cores": threads, "kind": "port",
-           "sample": f"{done} {what} of the same {n}^3 hierarchy by the C oracle (oracle/oracle.c), "
+           "sample": f"{done} {what} of the same {n} hierarchy by the C oracle (oracle/oracle.c), "
                      f"OpenMP {threads} threads, {tcpu:.1f}s"}
     log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({done} iterations, {tcpu:.1f}s, {threads} threads)")
-    return cpu
+    del O
+    return cpu, u, done
+
+
+def gpu_parity(hv, amg, krylov, A, b, x, u_oracle, iters, pcg):
+    """The GPU solve from x = 0 for the oracle's iterations, compared with the
+    oracle's iterate: every row sum keeps the reference's order, so a V-cycle
+    solve must agree bit for bit (PCG's dot products reduce in another order:
+    its iterate is compared at a stated tolerance instead)."""
+    x.fill(0.0)
+    if pcg:
+        krylov.set(max_iter=iters)
+        krylov.solve(A, b, x)
+    else:
+        amg.set(max_iter=iters)
+        amg.solve(A, b, x)
+    xg = x.get()
+    if not pcg:
+        same = bool(np.array_equal(xg, u_oracle))
+        diff = 0.0 if same else float(np.max(np.abs(xg - u_oracle)))
+        res = {"kind": "bitwise", "equal": same, "iterations": iters, "rows": int(xg.size),
+               "max_abs_diff": diff}
+        tag = "bitwise" if same else "MISMATCH"
+    else:
+        rel = float(np.linalg.norm(xg - u_oracle) / max(np.linalg.norm(u_oracle), 1e-300))
+        ok = rel <= 1e-9
+        res = {"kind": "rtol 1e-9 (PCG reductions reorder)", "equal": ok, "iterations": iters,
+               "rows": int(xg.size), "rel_diff": rel}
+        tag = "rtol1e-9" if ok else "MISMATCH"
+    log(f"[bench] parity: GPU vs oracle after {iters} iterations from x = 0 on {xg.size} rows: {tag}")
+    return tag, res
 
 
 def amg_settings(hv, pcg, agg=0, relax=18, coarsen=8):
@@ -156,30 +191,54 @@ def smoother_name(relax):
     return f"relax {relax} down/up"
 
 
-def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light=False):
+def global_grid(args, world):
+    """(nx, ny, nz) of the global problem.  Strong (the default): --grid, or
+    n^3, split over the ranks in z-slabs (ij -n is the global size, ij.c:1780;
+    hypre_GeneratePartitioning gives the first nz % N slabs one plane more).
+    --weak: n x n x (n N), n^3 rows per rank."""
+    if args.grid:
+        nx, ny, nz = (int(v) for v in args.grid.split(","))
+    else:
+        nx = ny = nz = args.n
+    if args.weak:
+        nz *= world
+    return nx, ny, nz
+
+
+def peak_rss_gb():
+    import resource
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6
+
+
+def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=None, light=False):
     """One rank's part of the bench; returns the JSON dict on rank 0.  light:
     a secondary size (no CPU baseline, no stream calibration)."""
     import torch
 
-    n = args.n if n is None else n
     t0 = time.time()
     cx, cy, cz = (float(v) for v in args.coef.split(","))
+    if n is None:
+        nx, ny, nz = global_grid(args, world)
+    else:
+        nx = ny = nz = n
 
-    def gen(nz, **part):
+    def gen(**part):
         if args.stencil == 27:
-            return hv.ParCSRMatrix.laplacian27(n, n, nz, **part)
-        return hv.ParCSRMatrix.laplacian(n, n, nz, cx=cx, cy=cy, cz=cz, **part)
+            return hv.ParCSRMatrix.laplacian27(nx, ny, nz, **part)
+        return hv.ParCSRMatrix.laplacian(nx, ny, nz, cx=cx, cy=cy, cz=cz, **part)
 
     if comm is not None:
-        # weak scaling: n x n x (n * world) grid, rank r owns z-slab r
-        A = gen(n * world, comm=comm, P=1, Q=1, R=world, p=0, q=0, r=rank)
+        # rank r owns z-slab r of the P x Q x R = 1 x 1 x world process grid
+        A = gen(comm=comm, P=1, Q=1, R=world, p=0, q=0, r=rank)
     else:
-        A = gen(n)
+        A = gen()
     nrows = A.n
+    gn = nx * ny * nz
     pcg = args.solver == "pcg"
     first = A.first if comm is not None else 0
-    b = hv.ParVector(nrows, np.ones(nrows), comm=comm, first=first, global_n=nrows * world)
-    x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=nrows * world)
+    b = hv.ParVector(nrows, np.ones(nrows), comm=comm, first=first, global_n=gn)
+    x = hv.ParVector(nrows, np.zeros(nrows), comm=comm, first=first, global_n=gn)
+    krylov = None
     if pcg:
         # ij -solver 1: PCG (two-norm) preconditioned by one BoomerAMG V-cycle
         amg = hv.BoomerAMG(**amg_settings(hv, True, args.agg, args.relax, args.coarsen))
@@ -194,10 +253,11 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
         with heartbeat(f"rank {rank} setup"):
             amg.setup(A)
     t_setup = time.time() - t0
+    rss_setup = peak_rss_gb()
     g, o, c = amg.complexities()
     if rank == 0:
-        log(f"[bench] ranks={world} n={n}^3/rank rows/rank={nrows} levels={amg.num_levels()} grid={g:.4f} "
-            f"op={o:.4f} setup={t_setup:.1f}s")
+        log(f"[bench] ranks={world} grid={nx}x{ny}x{nz} rows/rank={nrows} levels={amg.num_levels()} grid={g:.4f} "
+            f"op={o:.4f} setup={t_setup:.1f}s peak RSS {rss_setup:.1f} GB")
     # warmup (also instantiates the cycle hipGraph)
     if args.warmup > 0:
         if pcg:
@@ -220,15 +280,14 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
     elapsed = max_over_ranks(time.perf_counter() - t_start)
     assert it == args.steps, (it, args.steps)
     ms_per_step = elapsed / args.steps * 1e3
-    value = nrows * world * args.steps / elapsed
+    value = gn * args.steps / elapsed
     if rank == 0:
         log(f"[bench] {args.steps} steps in {elapsed*1e3:.2f} ms -> {ms_per_step:.3f} ms/step, rel.res {rr:.3e}")
 
     # roofline: finest-level SpMV (the dominant kernel), HIP events on the solver stream.
-    # achieved = the bytes its stored layout must move (every stored slot once:
-    # 16-bit column delta + 8-bit value index with the value table, 16-bit
-    # delta + 8-B value without; slot bases; x, b, y once) / launch time.  The
-    # CSR-equivalent rate (12 B a nonzero) is reported beside it.
+    # achieved = the bytes its stored layout must move per launch / launch time
+    # (hypreve_BenchFineSpMVStoredBytes); the CSR-equivalent rate (12 B a
+    # nonzero) is reported beside it.
     spmv_ms, csr_bytes = amg.bench_fine_spmv(args.spmv_reps)
     stored_bytes = amg.fine_spmv_stored_bytes()
     achieved = stored_bytes / (spmv_ms * 1e-3) / 1e9
@@ -239,7 +298,7 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
     kname, kdesc = KERNEL_OF_LAYOUT[layout0]
     # the committed PMC summary (scripts/pmc_traffic.py) measured the default
     # operator's finest residual kernel at this size; reported only for the same kernel
-    traffic = committed_traffic(n, kname) if default_op else None
+    traffic = committed_traffic(nx, kname) if (default_op and world == 1 and nx == ny == nz) else None
     # every large operator of the cycle, each timed alone with HIP events (bytes
     # of its stored layout + vectors per launch)
     per_kernel = []
@@ -262,7 +321,6 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
     stream_n = (1 << 31) // 8
     stream_gbs = stream_n * 8 / (hv.bench_stream(8, stream_n, 3 if light else 10) * 1e-3) / 1e9
     # and its read/write mix: 5 double streams read and one written per element
-    # (48 B; the finest residual reads ~4.8 bytes for each one it writes)
     mix_n = (1 << 27)
     mix_gbs = mix_n * 48 / (hv.bench_stream(-5, mix_n, 3 if light else 10) * 1e-3) / 1e9
     if args.calib:
@@ -278,37 +336,34 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
             "stream_mix_gbs": round(mix_gbs, 1), "frac_of_mix_stream": round(achieved / mix_gbs, 4),
             "per_kernel": per_kernel}
     if rank == 0:
-        import resource
         log(f"[bench] read stream {stream_gbs:.0f} GB/s, 5:1 read/write mix {mix_gbs:.0f} GB/s; "
             f"fine SpMV at {achieved / stream_gbs:.3f} / {achieved / mix_gbs:.3f} of them")
         log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {stored_bytes/1e9:.3f} GB stored -> {achieved:.1f} GB/s "
-            f"(CSR-equivalent {csr_gbs:.1f} GB/s); "
-            f"host peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1e6:.1f} GB")
+            f"(CSR-equivalent {csr_gbs:.1f} GB/s); host peak RSS {peak_rss_gb():.1f} GB")
 
-    cpu = None
-    if rank == 0 and not light and args.cpu_cycles > 0:
-        if world == 1 and not args.dist:
-            cpu = oracle_cpu_baseline(amg, nrows, n, pcg, args)
-        else:
-            # The partitioned hierarchy keeps no whole level matrices on the
-            # host: rank 0 times the same CPU path on a one-process hierarchy of
-            # args.cpu_n^3 rows (DOF/s of the host path is size-independent in
-            # this range: 1.1-1.3e8 at 256^3, 1.1e8 at 512^3 on 16 threads).
-            ncpu = args.cpu_n
-            Ac = hv.ParCSRMatrix.laplacian27(ncpu, ncpu, ncpu) if args.stencil == 27 else \
-                hv.ParCSRMatrix.laplacian(ncpu, ncpu, ncpu, cx=cx, cy=cy, cz=cz)
-            ac = hv.BoomerAMG(**amg_settings(hv, pcg, args.agg, args.relax, args.coarsen))
-            ac.setup(Ac)
-            cpu = oracle_cpu_baseline(ac, Ac.n, ncpu, pcg, args)
-            cpu["sample"] += f" (one-process {ncpu}^3 stand-in for the {world}-rank problem: per-rank equivalent)"
-            ac.destroy()
-            Ac.destroy()
+    cpu, parity, parity_detail = None, None, None
+    if rank == 0 and not light and args.cpu_cycles > 0 and world == 1 and comm is None:
+        cpu, u_orc, iters = oracle_cpu_baseline(amg, nrows, f"{nx}x{ny}x{nz}", pcg, args)
+        parity, parity_detail = gpu_parity(hv, amg, krylov, A, b, x, u_orc, iters, pcg)
+        del u_orc
+    elif rank == 0 and not light and world > 1:
+        # bench contract: the CPU baseline is timed at N = 1 only.  Under strong
+        # scaling the N = 1 line runs this same global problem, so its
+        # cpu_baseline is this line's too; N-rank iterates equal the 1-rank
+        # iterates bit for bit (tests/test_gpu_multirank.py, loopback + RCCL).
+        parity = "bitwise vs 1 rank (tests/test_gpu_multirank.py)"
+    stats = gather({"rank": rank, "rows": nrows, "setup_s": round(t_setup, 1), "setup_peak_rss_gb": round(rss_setup, 1),
+                    "peak_rss_gb": round(peak_rss_gb(), 1), "omp_threads": int(os.environ.get("OMP_NUM_THREADS", "0"))})
     nlev = amg.num_levels()
     for obj in ((krylov,) if pcg else ()) + (amg, A, b, x):
         obj.destroy()  # release host and device memory before a secondary size runs
     if rank != 0:
         return None
-    return {
+    strong = not args.weak
+    split = f"{world} z-slab row blocks" if world > 1 else "one row block"
+    scaled = "global problem, fixed as N grows" if strong else f"{nx}x{ny}x{nz // world} per GPU"
+    opname = f"{'anisotropic diffusion (' + args.coef + ')' if aniso else 'Laplacian'}"
+    out = {
         "metric": "BoomerAMG V-cycle DOF/s + finest-level SpMV GB/s vs HBM peak, 1/2/4/8 GPU",
         "value": round(value, 1),
         "unit": "DOF/s",
@@ -317,23 +372,44 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, n=None, light
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": f"synthetic ({'GenerateLaplacian27pt' if args.stencil == 27 else 'GenerateLaplacian 7-point'}"
                 f"{'' if default_op else ', coefficients ' + args.coef}, rhs = ones)",
-        "config": {"workload": f"3D {args.stencil}-point {'anisotropic diffusion (' + args.coef + ')' if aniso else 'Laplacian'}"
-                               f" {n}^3 per GPU ({n}x{n}x{n * world} global, z-slab row "
-                               f"blocks), {'BoomerAMG-PCG (one V-cycle per PCG iteration)' if pcg else 'BoomerAMG V-cycle'}"
+        "config": {"workload": f"3D {args.stencil}-point {opname} {nx}x{ny}x{nz} ({scaled}; {split})"
+                               f", {'BoomerAMG-PCG (one V-cycle per PCG iteration)' if pcg else 'BoomerAMG V-cycle'}"
                                f", {'HMIS' if args.coarsen == 10 else 'PMIS'} + ext+i (Pmx 4)"
                                f"{f', {args.agg} aggressive level(s) (multipass)' if args.agg else ''}"
                                f", {smoother_name(args.relax)}, Gaussian elimination coarsest",
-                   "rows_per_gpu": nrows, "levels": nlev, "grid_complexity": round(g, 6),
+                   "global_rows": gn, "rows_per_gpu": nrows, "levels": nlev, "grid_complexity": round(g, 6),
                    "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
-                   "parallelism": f"rows{world}"},
+                   "per_rank": stats,
+                   "parallelism": f"rows{world}, {'strong' if strong else 'weak'}"},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "parity": parity,
     }
+    if parity_detail is not None:
+        out["parity_detail"] = parity_detail
+    if world > 1:
+        out["cpu_baseline_note"] = ("timed at N = 1 only (bench contract); strong scaling: the N = 1 line runs "
+                                    "the same global problem") if strong else "timed at N = 1 only (bench contract)"
+    return out
+
+
+def rank_threads():
+    """OpenMP threads of this rank's host setup: the host cores this process may
+    use, shared by the ranks of the node (LOCAL_WORLD_SIZE), and no more than an
+    OMP_NUM_THREADS the launcher set.  Set before the OpenMP runtime loads."""
+    lw = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    share = len(os.sched_getaffinity(0))
+    per = max(1, share // max(1, lw))
+    env = os.environ.get("OMP_NUM_THREADS", "")
+    if env.isdigit() and int(env) > 0:
+        per = min(per, int(env))
+    os.environ["OMP_NUM_THREADS"] = str(per)
+    return per
 
 
 def main():
@@ -342,11 +418,15 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=512,
-                    help="grid edge per GPU (n^3 rows per GPU); 512: configs[2]'s 512^3, the north-star size")
+                    help="grid edge of the global n^3 problem (512: configs[2]-[4]'s 512^3, the north-star size), "
+                         "split over the ranks in z-slabs; with --weak n^3 rows per GPU")
+    ap.add_argument("--grid", default="",
+                    help="nx,ny,nz of the global grid instead of n^3 (e.g. 512,512,64: one rank's share of the "
+                         "8-GPU 512^3 problem, for a one-GPU rehearsal)")
+    ap.add_argument("--weak", action="store_true",
+                    help="weak scaling: n^3 rows per GPU (n x n x n*N global) instead of the global n^3")
     ap.add_argument("--secondary-n", type=int, default=256,
                     help="one GPU: also measure this size (configs[1]'s 256^3) into 'secondary' (0 = skip)")
-    ap.add_argument("--cpu-n", type=int, default=256,
-                    help="N > 1: grid edge of the one-process hierarchy rank 0 times the CPU baseline on")
     ap.add_argument("--stencil", type=int, choices=[7, 27], default=7,
                     help="7: GenerateLaplacian (configs[1], the bench line); 27: GenerateLaplacian27pt (configs[3])")
     ap.add_argument("--coef", default="1,1,1",
@@ -372,6 +452,7 @@ def main():
     ap.add_argument("--loopback", type=int, default=0,
                     help="rehearsal only: N virtual ranks (threads) sharing this process's GPU")
     args = ap.parse_args()
+    omp = rank_threads()
 
     import torch  # loads the HIP runtime the library then shares
 
@@ -392,13 +473,22 @@ def main():
         times = [0.0] * nv
         results, errs = [None] * nv, [None] * nv
 
+        slots = [None] * nv
+
         def worker(r):
             def max_fn(t):
                 times[r] = t
                 bar.wait()
                 return max(times)
+
+            def gather_fn(obj):
+                slots[r] = obj
+                bar.wait()
+                out = list(slots)
+                bar.wait()
+                return out
             try:
-                results[r] = run_rank(hv, args, comms[r], r, nv, bar.wait, max_fn)
+                results[r] = run_rank(hv, args, comms[r], r, nv, bar.wait, max_fn, gather_fn)
             except BaseException as e:
                 errs[r] = e
                 bar.abort()
@@ -443,9 +533,18 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         return float(tt.item())
 
-    out = run_rank(hv, args, comm, rank, world, barrier, max_over_ranks)
-    if out is not None and world == 1 and comm is None and args.secondary_n > 0 and args.secondary_n != args.n:
-        sec = run_rank(hv, args, None, 0, 1, barrier, max_over_ranks, n=args.secondary_n, light=True)
+    def gather(obj):
+        if not dist:
+            return [obj]
+        out = [None] * world
+        dist.all_gather_object(out, obj)
+        return out
+
+    log(f"[bench] rank {rank}/{world}: OpenMP {omp} host threads for the setup")
+    out = run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather)
+    if out is not None and world == 1 and comm is None and args.secondary_n > 0 and args.secondary_n != args.n \
+            and not args.grid:
+        sec = run_rank(hv, args, None, 0, 1, barrier, max_over_ranks, gather, n=args.secondary_n, light=True)
         out["secondary"] = {k: sec[k] for k in ("value", "unit", "ms_per_step", "steps")}
         out["secondary"]["config"] = sec["config"]
         out["secondary"]["roofline"] = {k: sec["roofline"][k] for k in ("achieved", "frac", "avg_ms", "kernel",

@@ -98,8 +98,21 @@ static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A);
 // Automatic hybrid Gauss-Seidel block count (num_blocks 0): one block of about
 // kAutoBlockRows rows each, so a large level's sweep runs on thousands of
 // workgroups while every block keeps hypre's exact in-block GS order.
-static constexpr int kAutoBlockRows = 4096;
-static int auto_num_blocks(int local_rows) { return std::max(1, (local_rows + kAutoBlockRows - 1) / kAutoBlockRows); }
+// The count is chosen per level and per rank from that level's own rows
+// (AMGParams::blocks_for), so coarse levels keep blocks of about that size too.
+// HVE_AUTO_BLOCK_ROWS overrides the block size (tuning).
+static int auto_block_rows() {
+  static const int v = [] {
+    const char* e = getenv("HVE_AUTO_BLOCK_ROWS");
+    const int r = e ? atoi(e) : 0;
+    return r > 0 ? r : 4096;
+  }();
+  return v;
+}
+static void resolve_blocks(hypre_Solver_struct* s, int local_rows) {
+  s->prm.auto_block_rows = s->auto_blocks ? auto_block_rows() : 0;
+  if (s->auto_blocks) s->prm.num_blocks = s->prm.blocks_for(local_rows);  // level 0 (reported)
+}
 
 // ---------------------------------------------------------------------------
 // error state (utilities/hypre_error.c semantics)
@@ -851,7 +864,7 @@ HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(A, 2);
   API_BEGIN
-  if (s->auto_blocks) s->prm.num_blocks = auto_num_blocks(A->n);
+  resolve_blocks(s, A->n);
   setup_one_process(s, A);
   API_END
 }
@@ -1092,6 +1105,11 @@ static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
     amg_setup(A->diag, prm, s->H, &s->rank_emul);
   }
   gs_rank_blocks_host(s->H, s->gs_rank_starts, s->gs_blocks_host, s->gs_l1_host);
+  if (s->gs_blocks_host.empty() && s->prm.auto_block_rows > 0) {
+    // per-level automatic blocks: exported for the introspection calls (the
+    // l1 norms of L.l1 already follow them)
+    for (const Level& L : s->H.lev) s->gs_blocks_host.push_back(hypre_block_starts(L.A.nrows, s->prm.blocks_for(L.A.nrows)));
+  }
 }
 
 extern "C" {
@@ -1101,7 +1119,7 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
   CHECK_ARG(A, 2);
   API_BEGIN
   s->comm = A->comm;
-  if (s->auto_blocks) s->prm.num_blocks = auto_num_blocks(A->n);
+  resolve_blocks(s, A->n);
   if (A->multi()) {
     if (use_dist_setup(s->prm)) setup_dist(s, A);
     else setup_multi(s, A);
@@ -1371,7 +1389,8 @@ HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver s, HYPRE_Int level, H
   int W = 0;
   if (width) *width = 0;
   if (npatterns) *npatterns = 0;
-  if (!build_sell_stencil_host(A, 64, W, pat, off, vi, mask, tab)) return g_error;
+  // not a constant-coefficient stencil: success with width 0 (not the sticky error flag)
+  if (!build_sell_stencil_host(A, 64, W, pat, off, vi, mask, tab)) return 0;
   for (int r = 0; r < A.nrows; ++r) {
     const size_t p0 = (size_t)pat[r >> 6] * W;
     int e = A.i[r];

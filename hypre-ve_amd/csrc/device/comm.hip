@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <deque>
@@ -320,11 +321,24 @@ class ShmComm final : public DevComm {
     } else {
       for (int tries = 0; tries < 60000 && hdr_->magic.load(std::memory_order_acquire) != kShmMagic; ++tries)
         ::usleep(1000);
-      if (hdr_->magic.load(std::memory_order_acquire) != kShmMagic || hdr_->size.load() != size)
+      if (hdr_->magic.load(std::memory_order_acquire) != kShmMagic || hdr_->size.load() != size) {
+        unmap();
         throw std::runtime_error("shm comm: segment not initialised by rank 0");
+      }
     }
     hdr_->attached.fetch_add(1);
-    while (hdr_->attached.load() < size) ::usleep(100);  // every rank is mapped
+    // every rank is mapped; a peer that died during startup ends the wait
+    const auto t0 = std::chrono::steady_clock::now();
+    while (hdr_->attached.load() < size) {
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(kShmAttachSeconds)) {
+        const int seen = hdr_->attached.load();
+        unmap();
+        if (rank == 0) ::shm_unlink(name_.c_str());
+        throw std::runtime_error("shm comm: only " + std::to_string(seen) + " of " + std::to_string(size) +
+                                 " ranks attached within " + std::to_string(kShmAttachSeconds) + " s");
+      }
+      ::usleep(100);
+    }
   }
   ~ShmComm() override {
     if (!base_) return;
@@ -333,7 +347,7 @@ class ShmComm final : public DevComm {
       for (int tries = 0; tries < 10000 && hdr_->detached.load() < size_; ++tries) ::usleep(1000);
       ::shm_unlink(name_.c_str());
     }
-    ::munmap(base_, bytes_);
+    unmap();
   }
   const char* kind() const override { return "shm"; }
 
@@ -381,6 +395,14 @@ class ShmComm final : public DevComm {
   }
 
  private:
+  // startup and per-exchange deadlines: a peer that is gone ends the wait with an error
+  static constexpr int kShmAttachSeconds = 60;
+  static constexpr int kShmIdleSeconds = 300;
+  void unmap() {
+    if (base_) ::munmap(base_, bytes_);
+    base_ = nullptr;
+    hdr_ = nullptr;
+  }
   ShmSlot* slot_at(int i) const { return reinterpret_cast<ShmSlot*>(base_ + 4096 + (size_t)i * sizeof(ShmSlot)); }
   ShmSlot* slot(int src, int dst) const { return slot_at(src * size_ + dst); }
   char* data(int src, int dst) const {
@@ -404,6 +426,7 @@ class ShmComm final : public DevComm {
     for (int d : sdone) left += !d;
     for (int d : rdone) left += !d;
     long idle = 0;
+    auto last = std::chrono::steady_clock::now();
     while (left) {
       bool progress = false;
       for (int p = 0; p < size_; ++p) {
@@ -438,8 +461,13 @@ class ShmComm final : public DevComm {
         idle = 0;
       } else if (++idle > 64) {
         ::usleep(idle > 100000 ? 1000 : 20);
-        if (idle > 20000000L) throw std::runtime_error("shm comm: exchange made no progress (peer gone?)");
+        if ((idle & 1023) == 0) {
+          if (std::chrono::steady_clock::now() - last > std::chrono::seconds(kShmIdleSeconds))
+            throw std::runtime_error("shm comm: exchange made no progress for " + std::to_string(kShmIdleSeconds) +
+                                     " s (peer gone?)");
+        }
       }
+      if (progress) last = std::chrono::steady_clock::now();
     }
   }
 

@@ -755,7 +755,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       DevLevel& D = lev_[l];
       if (l == nl - 1 && R.coarse_n > 0) break;  // coarsest level: direct solve
       const CSR rows = merged_rows(L.A, L.n_loc);
-      const std::vector<int> bs = L.gs_blocks.empty() ? hypre_block_starts(L.n_loc, prm.num_blocks) : L.gs_blocks;
+      const std::vector<int> bs = L.gs_blocks.empty() ? hypre_block_starts(L.n_loc, prm.blocks_for(L.n_loc)) : L.gs_blocks;
       if (fwd) D.gs_fwd.upload(rows, bs, true);
       if (bwd) D.gs_bwd.upload(rows, bs, false);
       D.gs_tmp = dalloc<double>(D.n + D.hu.n_halo);

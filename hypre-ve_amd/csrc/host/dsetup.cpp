@@ -924,9 +924,9 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     }
     const std::vector<int>* cfp = use_cf ? &D.cf : nullptr;
     if (j < nl - 1 && (uses_l1_gs(prm.relax_type[1]) || uses_l1_gs(prm.relax_type[2])))
-      l1_dist(D.A, D.first, D.nglob, 4, cfp, &gp, &gcf, prm.num_blocks, D.l1);
+      l1_dist(D.A, D.first, D.nglob, 4, cfp, &gp, &gcf, prm.blocks_for(D.A.nrows), D.l1);
     else if (j == nl - 1 && uses_l1_gs(prm.relax_type[3]))
-      l1_dist(D.A, D.first, D.nglob, 4, nullptr, nullptr, nullptr, prm.num_blocks, D.l1);
+      l1_dist(D.A, D.first, D.nglob, 4, nullptr, nullptr, nullptr, prm.blocks_for(D.A.nrows), D.l1);
     if (j < nl - 1 && (prm.relax_type[1] == 18 || prm.relax_type[2] == 18))
       l1_dist(D.A, D.first, D.nglob, 1, cfp, &gp, &gcf, 1, D.l1);
     else if (j == nl - 1 && prm.relax_type[3] == 18)
@@ -990,7 +990,7 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
       bool cfr = false;
       if (!D.l1.empty() && l1_option_for_level(prm, l, nl, &cfr) == 4)
         compute_l1_norms_blocks(D.A, 4, (cfr && !D.cf.empty()) ? D.cf.data() : nullptr,
-                                hypre_block_starts(D.nglob, std::max(1, prm.num_blocks)), D.l1);
+                                hypre_block_starts(D.nglob, prm.blocks_for(D.nglob)), D.l1);
     }
     for (int l = agg; l < nl; ++l) {
       DLevel& D = L[l];
@@ -1039,7 +1039,7 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     }
     RL.l1 = D.l1;
     RL.cf = D.cf;
-    if (size > 1 && uses_hybrid_gs_any(prm)) RL.gs_blocks = hypre_block_starts(D.nloc, std::max(1, prm.num_blocks));
+    if (size > 1 && uses_hybrid_gs_any(prm)) RL.gs_blocks = hypre_block_starts(D.nloc, prm.blocks_for(D.nloc));
     if (agg >= 0 && l >= agg) {
       RL.hu.n_loc = D.nloc;
       if (l + 1 < nl) RL.hv.n_loc = D.nloc;

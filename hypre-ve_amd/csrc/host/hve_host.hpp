@@ -98,6 +98,18 @@ struct AMGParams {
   // Number of contiguous row blocks for the hybrid (block-Jacobi / in-block GS)
   // smoothers; hypre's CPU path uses num_threads for this (par_relax.c:4387).
   int num_blocks = 1;
+  // > 0: the block count is chosen per level (and per rank) instead, one block
+  // of about auto_block_rows rows (hypreve_BoomerAMGSetNumBlocks(0)); a small
+  // coarse level then keeps a few blocks instead of one row each.
+  int auto_block_rows = 0;
+  // hybrid-GS row blocks of a level (one rank's share) of `rows` rows
+  int blocks_for(int rows) const {
+    if (auto_block_rows > 0) {
+      const long long b = ((long long)rows + auto_block_rows - 1) / auto_block_rows;
+      return b < 1 ? 1 : (int)b;
+    }
+    return num_blocks < 1 ? 1 : num_blocks;
+  }
   // Aggressive coarsening (par_amg.c:153-173 defaults): the first
   // agg_num_levels levels coarsen twice (second pass on S*S + 2S over the C
   // points, num_paths paths needed) and interpolate with agg_interp_type 4

@@ -111,17 +111,17 @@ std::vector<std::vector<int>> rank_gs_blocks(const Hierarchy& H, const std::vect
   const int nl = (int)H.lev.size();
   const auto starts = level_starts(H, starts0, size);
   const int agg = hierarchy_agg_level(H, size);
-  const int nb = std::max(1, H.prm.num_blocks);
   std::vector<std::vector<int>> out(nl);
   for (int l = 0; l < nl; ++l) {
     const int n = H.lev[l].A.nrows;
     if (agg >= 0 && l >= agg) {
-      out[l] = hypre_block_starts(n, nb);
+      out[l] = hypre_block_starts(n, H.prm.blocks_for(n));
       continue;
     }
     out[l].assign(1, 0);
     for (int r = 0; r < size; ++r) {
       const int a = starts[l][r], b = starts[l][r + 1];
+      const int nb = H.prm.blocks_for(b - a);
       const std::vector<int> loc = hypre_block_starts(b - a, nb);
       for (int k = 1; k <= nb; ++k) out[l].push_back(a + loc[k]);
     }
@@ -222,7 +222,7 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
       }
       if (gs_ranks) {
         if (!l1_ranks[l].empty()) RL.l1.assign(l1_ranks[l].begin() + a, l1_ranks[l].begin() + b);
-        RL.gs_blocks = hypre_block_starts(b - a, std::max(1, H.prm.num_blocks));
+        RL.gs_blocks = hypre_block_starts(b - a, H.prm.blocks_for(b - a));
       } else if (!L.l1.empty()) {
         RL.l1.assign(L.l1.begin() + a, L.l1.begin() + b);
       }

@@ -1756,9 +1756,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     Level& L = H.lev[j];
     const int* cfp = (prm.relax_order && !L.cf.empty()) ? L.cf.data() : nullptr;
     if (j < nl - 1 && (uses_l1_gs(prm.relax_type[1]) || uses_l1_gs(prm.relax_type[2])))
-      compute_l1_norms(L.A, 4, cfp, prm.num_blocks, L.l1);
+      compute_l1_norms(L.A, 4, cfp, prm.blocks_for(L.A.nrows), L.l1);
     else if (j == nl - 1 && uses_l1_gs(prm.relax_type[3]))
-      compute_l1_norms(L.A, 4, nullptr, prm.num_blocks, L.l1);
+      compute_l1_norms(L.A, 4, nullptr, prm.blocks_for(L.A.nrows), L.l1);
     if (j < nl - 1 && (prm.relax_type[1] == 18 || prm.relax_type[2] == 18))
       compute_l1_norms(L.A, 1, cfp, 1, L.l1);
     else if (j == nl - 1 && prm.relax_type[3] == 18)
@@ -1798,11 +1798,11 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     // the blocks of hypre's threads, or of every emulated rank (num_blocks each)
     std::vector<int> bs;
     std::vector<double> l1 = L.l1;
-    const int nbk = std::max(1, prm.num_blocks);
     if (!lev_starts.empty()) {
       const std::vector<int>& st = lev_starts[j];
       bs.push_back(0);
       for (size_t r = 0; r + 1 < st.size(); ++r) {
+        const int nbk = prm.blocks_for(st[r + 1] - st[r]);
         const std::vector<int> loc = hypre_block_starts(st[r + 1] - st[r], nbk);
         for (int k = 1; k <= nbk; ++k) bs.push_back(st[r] + loc[k]);
       }
@@ -1810,7 +1810,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       if (!l1.empty() && l1_option_for_level(prm, j, nl, &cfr) == 4)
         compute_l1_norms_blocks(L.A, 4, (cfr && !L.cf.empty()) ? L.cf.data() : nullptr, bs, l1);
     } else {
-      bs = hypre_block_starts(L.A.nrows, nbk);
+      bs = hypre_block_starts(L.A.nrows, prm.blocks_for(L.A.nrows));
     }
     const int rt = prm.relax_type[1];
     if ((rt == 18 || rt == 7 || uses_l1_gs(rt)) && l1.empty()) throw std::runtime_error("l1 norms missing");

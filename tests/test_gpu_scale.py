@@ -119,3 +119,59 @@ def test_gpu_boomer_out14(gpu):
     print(f"grid {g:.6f} operator {o:.6f} iterations {it} rel.res {rr:.6e}")
     assert 19 <= it <= 23, it
     assert rr < 1e-8
+
+
+@pytest.mark.timeout(900)
+def test_gpu_boomer_out5_loopback4(gpu):
+    """TEST_cuda_lassen/gpu_boomer.saved out.5 (gpu_boomer.jobs:24: mpirun -np 4
+    ./ij -n 256 256 128 -P 2 2 1 -27pt -pmis -keepT 1 -rlx 18 -interptype 6
+    -solver 1) on 4 virtual ranks (loopback hub, one host thread each) over the
+    same 2 x 2 x 1 process grid: configs[3]'s 27-point operator on the
+    partitioned path at 8.4M rows.  Saved: grid 1.091816, operator 1.219636,
+    18 PCG iterations, final relative residual 6.742504e-09.  That run used
+    the GPU PMIS (curand), so the check is a band: complexities within 1 %,
+    iterations 18 +- 2."""
+    import threading
+
+    hv = gpu
+    nx, ny, nz, P, Q = 256, 256, 128, 2, 2
+    nr = P * Q
+    comms = hv.Comm.loopback(nr)
+    out, errs = [None] * nr, [None] * nr
+
+    def worker(r):
+        try:
+            c = comms[r]
+            A = hv.ParCSRMatrix.laplacian27(nx, ny, nz, comm=c, P=P, Q=Q, R=1, p=r % P, q=r // P, r=0)
+            kw = hv.ij_amg_defaults(1)
+            kw.update(coarsen_type=8, interp_type=6, relax_type=18)
+            amg = hv.BoomerAMG(**kw)
+            pcg = hv.PCG(tol=1e-8, max_iter=1000, two_norm=1)
+            pcg.set_precond_amg(amg)
+            b = hv.ParVector(A.n, np.ones(A.n), comm=c, first=A.first, global_n=A.global_n)
+            x = hv.ParVector(A.n, np.zeros(A.n), comm=c, first=A.first, global_n=A.global_n)
+            pcg.setup(A, b, x)
+            g, o, _ = amg.complexities()
+            it, rr = pcg.solve(A, b, x)
+            out[r] = (g, o, it, rr)
+            for obj in (pcg, amg, A, b, x):
+                obj.destroy()
+        except Exception as e:  # reported by the main thread
+            errs[r] = e
+
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(nr)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(800)
+    assert not any(t.is_alive() for t in th), "a virtual rank did not finish"
+    for e in errs:
+        if e is not None:
+            raise e
+    g, o, it, rr = out[0]
+    print(f"grid {g:.6f} operator {o:.6f} iterations {it} rel.res {rr:.6e}")
+    assert all(v[2] == it for v in out)
+    assert abs(g - 1.091816) <= 0.01 * 1.091816, g
+    assert abs(o - 1.219636) <= 0.01 * 1.219636, o
+    assert 16 <= it <= 20, it
+    assert rr < 1e-8
