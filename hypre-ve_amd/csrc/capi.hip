@@ -784,7 +784,7 @@ HYPRE_Int hypreve_BoomerAMGSetNumBlocks(HYPRE_Solver s, HYPRE_Int nb) {
 }
 HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver s, HYPRE_Int rows) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  s->prm.agglo_rows = rows < 0 ? 0 : rows;
+  s->prm.agglo_rows = rows < 0 ? -1 : rows;
   return 0;
 }
 // Hybrid Gauss-Seidel on one GPU with the row blocks of an N-rank run whose
@@ -1129,7 +1129,7 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
   }
   if (!s->dev) s->dev.reset(new DevAMG);
   s->dev->build(s->RH, A->multi() ? A->comm->dc.get() : nullptr);
-  s->dev->set_use_graph(s->use_graph && !A->multi());
+  s->dev->set_use_graph(s->use_graph);
   API_END
 }
 
@@ -1416,6 +1416,16 @@ HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver s, HYPRE_Int level, H
 // restriction f_{l+1} = R r_l) with its algorithmic bytes: every stored
 // nonzero once (8 B value + 4 B column), each input vector entry once, each
 // output entry read and/or written once.  Interior rows only on multi-rank.
+HYPRE_Int hypreve_BenchOperator(HYPRE_ParCSRMatrix A, HYPRE_Int op, HYPRE_Int policy, HYPRE_Int nbands,
+                                HYPRE_Int reps, HYPRE_Real* avg_ms, HYPRE_Real* stored_bytes, char* layout, HYPRE_Int len) {
+  CHECK_ARG(A && !A->multi(), 1);
+  CHECK_ARG(op == K_RESID || op == K_MATVEC || op == K_L1JAC || op == K_RESID_L1JAC, 2);
+  CHECK_ARG(reps > 0, 5);
+  API_BEGIN
+  const double ms = bench_operator(A->diag, op, policy, nbands, reps, stored_bytes, layout, len);
+  if (avg_ms) *avg_ms = ms;
+  API_END
+}
 HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,
                                HYPRE_Real* avg_ms, HYPRE_Real* bytes, HYPRE_Real* padded_nnz) {
   CHECK_ARG(s && s->dev && s->dev->built(), 1);

@@ -70,6 +70,7 @@ class RcclComm final : public DevComm {
     if (comm_) (void)ncclCommDestroy(comm_);
   }
   const char* kind() const override { return "rccl"; }
+  bool capturable() const override { return true; }
   void exchange(const std::vector<P2PMsg>& sends, const std::vector<P2PMsg>& recvs, hipStream_t s) override {
     if (sends.empty() && recvs.empty()) return;
     nccl_check(ncclGroupStart(), "ncclGroupStart");

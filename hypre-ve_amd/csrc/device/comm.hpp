@@ -33,6 +33,10 @@ class DevComm {
   int rank() const { return rank_; }
   int size() const { return size_; }
   virtual const char* kind() const = 0;
+  // Whether exchange / allreduce_sum may be recorded into a hipGraph (stream
+  // capture): RCCL's grouped send/recv and all-reduce can; the loopback hub and
+  // the shared-memory transport block on the host and cannot.
+  virtual bool capturable() const { return false; }
   // Grouped exchange on stream s with ncclGroupStart/Send/Recv/GroupEnd
   // semantics: the k-th message this rank sends to p matches p's k-th receive
   // from this rank.  All transfers, sends included, complete in stream order,

@@ -39,6 +39,12 @@ struct SellView {
   // changes, not any row's arithmetic.
   const int* blk_map = nullptr;
   int nblk = 0;
+  // stencil layout, one slice per wave: per logical wave (traversal order)
+  // its stored slice and that slice's pattern, {slice, pattern} pairs (slice
+  // -1: no rows), so a wave finds its slot data with one scalar load instead
+  // of two dependent ones (traversal map, then pattern index)
+  const int* wave_map = nullptr;
+  int nwave = 0;
 };
 
 enum : int {
@@ -83,6 +89,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const
 int sell_batch_override();
 int stencil_slices_per_wave();
 int stencil_grid(int nrows);
+bool stencil_wave_map();
 int sell_pipe_override();
 bool sell_nt();
 bool sell_pw();

@@ -82,6 +82,8 @@ struct SpArgs {
   const int* __restrict__ slice_pat;         // stencil layout: slot pattern of each slice
   const int* __restrict__ blk_map;           // logical -> stored row block (nullptr: identity)
   int nblk;                                  // entries of blk_map
+  const int* __restrict__ wave_map;          // stencil layout, R = 1: {slice, pattern} per logical wave
+  int nwave;
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double* __restrict__ nrm;       // OP_RESID_L1JAC (delta layout): per-workgroup sums of r_i^2 (y may be null)
@@ -627,10 +629,20 @@ __device__ __forceinline__ void wg_sum_store(double v, double* out) {
 template <int OP, bool CFSEL, bool NT, int R>
 __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
   constexpr int B = 8;  // slots per batch and slice
-  const int lb = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
   const int lane = threadIdx.x & (kWave - 1);
   const int W = p.sw;
-  const int slice0 = __builtin_amdgcn_readfirstlane((lb * 4 + (int)(threadIdx.x >> 6)) * R);  // wave-uniform
+  int slice0, pat0 = -1;
+  if (R == 1 && p.wave_map) {
+    // one scalar load gives the wave its slice and pattern (traversal order)
+    const int lw = xcd_logical_block(blockIdx.x, p.nblocks_pad) * 4 + (int)(threadIdx.x >> 6);
+    const int2 m = lw < p.nwave ? reinterpret_cast<const int2*>(p.wave_map)[__builtin_amdgcn_readfirstlane(lw)]
+                                : make_int2(-1, 0);
+    slice0 = __builtin_amdgcn_readfirstlane(m.x < 0 ? (p.nrows + 63) / 64 : m.x);
+    pat0 = __builtin_amdgcn_readfirstlane(m.y);
+  } else {
+    const int lb = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
+    slice0 = __builtin_amdgcn_readfirstlane((lb * 4 + (int)(threadIdx.x >> 6)) * R);  // wave-uniform
+  }
   const bool SUB = op_subtracts<OP>();
   const bool sub = SUB || (OP == OP_GENERAL && p.w == -1.0);
   const bool fly = (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC) && p.l1 == nullptr;
@@ -638,7 +650,8 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
   if (slice0 * kWave < p.nrows) {
     int pat[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) pat[r] = __builtin_amdgcn_readfirstlane(p.slice_pat[slice0 + r]);
+    for (int r = 0; r < R; ++r)
+      pat[r] = (R == 1 && pat0 >= 0) ? pat0 : __builtin_amdgcn_readfirstlane(p.slice_pat[slice0 + r]);
     int row[R], g[R];
     bool act[R];
     double t[R], uo[R], d[R], s1[R], xg[R], l1g[R];
@@ -1486,6 +1499,8 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     const int R = stencil_slices_per_wave();
     a.sw = M.stencil_w;
     a.slice_pat = M.slice_pat;
+    a.wave_map = (R == 1 && stencil_wave_map()) ? M.wave_map : nullptr;
+    a.nwave = M.nwave;
     a.nblocks_pad = (((M.nrows + 63) / 64 + 4 * R - 1) / (4 * R) + 7) / 8 * 8;
     const dim3 sgrid(stencil_grid(M.nrows));
 #define HVE_S(OPV, CF, RR)                                                                         \
@@ -1813,6 +1828,16 @@ int stencil_slices_per_wave() {
 // Grid of the stencil loop: one workgroup per block of 4R slices, whole XCD
 // rounds.  (A persistent grid that fetched each next block's traversal entry
 // and patterns ahead measured slower: 512^3 A0 1.60-1.68 ms against 0.87.)
+// One scalar load of {slice, pattern} per wave (SellView::wave_map) instead of
+// the traversal map and then the slice's pattern; HVE_STENCIL_WMAP=0 keeps the
+// two dependent loads.
+bool stencil_wave_map() {
+  static const bool v = [] {
+    const char* e = getenv("HVE_STENCIL_WMAP");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
+}
 int stencil_grid(int nrows) {
   const int R = stencil_slices_per_wave();
   const int nlb = ((std::max(nrows, 1) + 63) / 64 + 4 * R - 1) / (4 * R);

@@ -67,6 +67,30 @@ void DevSell::set_block_order(const std::vector<int>& stored_to_local, const std
   if (blk_map) (void)hipFree(blk_map);
   blk_map = dupload(ord.data(), ord.size());
   nblk = nb;
+  blk_host = ord;
+  build_wave_map();
+}
+
+// Stencil layout with one slice per wave: {stored slice, pattern} of every
+// logical wave, in the traversal order of blk_map (kernels.hip k_sell_stencil).
+void DevSell::build_wave_map() {
+  if (wave_map) (void)hipFree(wave_map);
+  wave_map = nullptr;
+  nwave = 0;
+  if (!slot_mask || stencil_slices_per_wave() != 1 || pat_host.empty()) return;
+  const int nb = (nslices + 3) / 4;  // row blocks of 4 slices (256 rows)
+  std::vector<int> m((size_t)nb * 4 * 2, 0);
+  for (int lb = 0; lb < nb; ++lb) {
+    const int b = (!blk_host.empty() && lb < (int)blk_host.size()) ? blk_host[lb] : lb;
+    for (int w = 0; w < 4; ++w) {
+      const int s = b * 4 + w;
+      const size_t e = ((size_t)lb * 4 + w) * 2;
+      m[e] = s < nslices ? s : -1;
+      m[e + 1] = s < nslices ? pat_host[s] : 0;
+    }
+  }
+  wave_map = dupload(m.data(), m.size());
+  nwave = nb * 4;
 }
 
 void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy, const std::vector<int64_t>* key) {
@@ -182,6 +206,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       wide = 0;
       pw = 0;
       slice_pat = dupload(spat.data(), spat.size());
+      pat_host = spat;
       npat = (int)((so.size() - 16) / std::max(sw, 1));
       if (getenv("HVE_LAYOUT_LOG"))
         fprintf(stderr, "[layout] stencil rows=%d width=%d patterns=%d values=%zu\n", A.nrows, sw, npat, tab.size());
@@ -197,6 +222,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       }
       stored_map = rowmap_h;
       if (key) set_block_order(rowmap_h, *key);
+      if (!wave_map) build_wave_map();
       return;
     }
     sp.clear();
@@ -466,6 +492,12 @@ void DevSell::release() {
   if (blk_map) (void)hipFree(blk_map);
   blk_map = nullptr;
   nblk = 0;
+  blk_host.clear();
+  pat_host.clear();
+  pat_host.shrink_to_fit();
+  if (wave_map) (void)hipFree(wave_map);
+  wave_map = nullptr;
+  nwave = 0;
   stored_map.clear();
   stored_map.shrink_to_fit();
   dcol = nullptr; slot_base = nullptr; vidx = nullptr; vidx16 = nullptr; vtab = nullptr; nvtab = 0;
@@ -662,6 +694,57 @@ static void locality_keys(const RankHierarchy& R, int agg_level, int nbands, std
   }
 }
 
+// Tuning harness: one operator uploaded alone (layout policy, nbands of the
+// traversal when the grid strides are found), op applied reps times on a
+// private stream, timed with HIP events.  op: K_RESID, K_MATVEC, or the
+// l1-Jacobi forms with the l1 norms formed on the fly (stencil / delta layouts).
+double bench_operator(const CSR& A, int op, int policy, int nbands, int reps, double* stored_bytes, char* layout_msg,
+                      int msg_len) {
+  DevSell M;
+  std::vector<int64_t> key;
+  int64_t plane = 0, line = 0;
+  if (nbands > 0 && grid_strides(A, {}, A.nrows, &plane, &line)) {
+    const int64_t ny = std::max<int64_t>(1, plane / line);
+    key.resize(A.nrows);
+    for (int64_t i = 0; i < A.nrows; ++i)
+      key[i] = std::min<int64_t>(nbands - 1, ((i % plane) / line) * nbands / ny) * A.nrows + i;
+  }
+  M.upload(A, {}, policy, key.empty() ? nullptr : &key);
+  if (stored_bytes) *stored_bytes = (double)M.bytes() + 24.0 * A.nrows;
+  if (layout_msg && msg_len > 0)
+    snprintf(layout_msg, msg_len, "%s w=%d npat=%d wave_map=%d blk_map=%d", M.slot_mask ? "stencil" : M.dcol ? "delta" : "other",
+             M.stencil_w, M.npat, M.wave_map != nullptr, M.blk_map != nullptr);
+  const int n = A.nrows;
+  double *x = dalloc<double>(n), *b = dalloc<double>(n), *y = dalloc<double>(n), *y2 = dalloc<double>(n);
+  double* nrm = dalloc<double>(1 << 22);
+  hipStream_t st;
+  HVE_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HVE_HIP(launch_set(n, 1.0, x, st));
+  HVE_HIP(launch_set(n, 0.5, b, st));
+  auto one = [&]() {
+    if (op == K_RESID_L1JAC)
+      HVE_HIP(launch_sell(op, M.view(), x, b, nullptr, nullptr, 0, nullptr, 1.0, 0.0, st, y2, nrm));
+    else
+      HVE_HIP(launch_sell(op, M.view(), x, b, nullptr, nullptr, 0, y, op == K_RESID ? -1.0 : 1.0, 0.0, st));
+  };
+  for (int w = 0; w < 3; ++w) one();
+  hipEvent_t e0, e1;
+  HVE_HIP(hipEventCreate(&e0));
+  HVE_HIP(hipEventCreate(&e1));
+  HVE_HIP(hipEventRecord(e0, st));
+  for (int r = 0; r < reps; ++r) one();
+  HVE_HIP(hipEventRecord(e1, st));
+  HVE_HIP(hipEventSynchronize(e1));
+  float ms = 0.f;
+  HVE_HIP(hipEventElapsedTime(&ms, e0, e1));
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(st);
+  for (double* p : {x, b, y, y2, nrm}) (void)hipFree(p);
+  M.release();
+  return ms / reps;
+}
+
 void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   const int n0 = R.lev.empty() ? 0 : R.lev[0].n_loc;
   init_workspace(n0, comm);
@@ -781,7 +864,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     HVE_HIP(hipMemset(u0_buf_[1], 0, sizeof(double) * m));
     HVE_HIP(hipMemset(x0_buf_, 0, sizeof(double) * m));
   }
-  if (comm_) use_graph_ = false;  // communication stays outside graph capture in this build
+  set_use_graph(use_graph_);
   HVE_HIP(hipDeviceSynchronize());
 }
 
@@ -801,8 +884,10 @@ void DevAMG::set_block_bands(const RankHierarchy& R, int nbands, int which_mask)
       if (M.blk_map) (void)hipFree(M.blk_map);
       M.blk_map = nullptr;
       M.nblk = 0;
+      M.blk_host.clear();
       if (!k.empty() && M.stored_map.size() == (size_t)M.nrows) M.set_block_order(M.stored_map, k);
       else if (!k.empty() && !M.rowmap) M.set_block_order(map, k);
+      if (M.blk_host.empty()) M.build_wave_map();
     };
     if (which_mask & 1) redo(D.A.in, kl, {});
     if (l < nl - 1) {
@@ -812,6 +897,14 @@ void DevAMG::set_block_bands(const RankHierarchy& R, int nbands, int which_mask)
     (void)L;
   }
   graphs_clear();
+}
+void DevAMG::set_use_graph(bool g) {
+  static const bool multi_ok = [] {
+    const char* e = std::getenv("HVE_GRAPH_MULTI");
+    return !e || std::atoi(e) != 0;
+  }();
+  use_graph_ = g && (!comm_ || (comm_->capturable() && multi_ok));
+  if (!use_graph_) graphs_clear();
 }
 void DevAMG::graphs_clear() {
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
@@ -1182,6 +1275,13 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
   cycle_ops_ = ops;
 }
 
+void DevAMG::capture_failed(const char* why) {
+  fprintf(stderr, "[hypreve] rank %d: cycle capture over %s failed (%s); cycles run eagerly\n", comm_->rank(),
+          comm_->kind(), why);
+  use_graph_ = false;
+  graphs_clear();
+}
+
 void DevAMG::cycle(const double* f, double* u, hipStream_t s, const double* presmoothed, bool zero_u) {
   const bool pre = presmoothed != nullptr;
   if (pre && presmoothed != presmooth_buffer()) throw std::runtime_error("cycle: unexpected presmoothed buffer");
@@ -1193,7 +1293,13 @@ void DevAMG::cycle(const double* f, double* u, hipStream_t s, const double* pres
   auto key = std::make_tuple((const void*)f, (const void*)u, (int)pre + 2 * (int)zero_u);
   auto it = graphs_.find(key);
   if (it == graphs_.end()) {
-    hipGraph_t g;
+    if (comm_ && eager_runs_[key]++ == 0) {
+      // first run of this shape on several ranks: eagerly (RCCL connects its
+      // peers on first use, which must not happen inside a capture)
+      emit_cycle(f, u, s, pre, zero_u);
+      return;
+    }
+    hipGraph_t g = nullptr;
     HVE_HIP(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     try {
       emit_cycle(f, u, s, pre, zero_u);
@@ -1201,12 +1307,25 @@ void DevAMG::cycle(const double* f, double* u, hipStream_t s, const double* pres
       hipGraph_t tmp = nullptr;
       (void)hipStreamEndCapture(s, &tmp);
       if (tmp) (void)hipGraphDestroy(tmp);
-      throw;
+      (void)hipGetLastError();
+      if (!comm_) throw;
+      // nothing captured has run: the cycle runs eagerly from here on (every
+      // rank still issues the same sequence of transfers)
+      capture_failed("emission");
+      emit_cycle(f, u, s, pre, zero_u);
+      return;
     }
-    HVE_HIP(hipStreamEndCapture(s, &g));
-    hipGraphExec_t ge;
-    HVE_HIP(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
-    HVE_HIP(hipGraphDestroy(g));
+    hipError_t ec = hipStreamEndCapture(s, &g);
+    hipGraphExec_t ge = nullptr;
+    if (ec == hipSuccess) ec = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (g) (void)hipGraphDestroy(g);
+    if (ec != hipSuccess) {
+      if (!comm_) check_hip(ec, "cycle graph capture");
+      (void)hipGetLastError();
+      capture_failed(hipGetErrorString(ec));
+      emit_cycle(f, u, s, pre, zero_u);
+      return;
+    }
     if (graphs_.size() > 16) {
       for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
       graphs_.clear();

@@ -57,6 +57,11 @@ struct DevSell {
   int pw = 0;
   int* blk_map = nullptr;  // locality traversal of the workgroup row blocks (SellView::blk_map)
   int nblk = 0;
+  std::vector<int> blk_host;   // host copy of blk_map
+  std::vector<int> pat_host;   // stencil layout: host copy of slice_pat
+  int* wave_map = nullptr;     // stencil layout: SellView::wave_map
+  int nwave = 0;
+  void build_wave_map();
   std::vector<int> stored_map;  // host copy of the stored row -> local row map (empty: identity)
   SellView view() const {
     SellView v;
@@ -64,7 +69,7 @@ struct DevSell {
     v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group; v.dict_ranges = dict_ranges;
     v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vidx16 = vidx16; v.vtab = vtab; v.nvtab = nvtab;
     v.slot_vi = slot_vi; v.slot_mask = slot_mask; v.stencil_w = stencil_w; v.slice_pat = slice_pat;
-    v.blk_map = blk_map; v.nblk = nblk;
+    v.blk_map = blk_map; v.nblk = nblk; v.wave_map = wave_map; v.nwave = nwave;
     return v;
   }
   // rowmap: subset row -> local row; empty or identity -> no map
@@ -194,7 +199,9 @@ class DevAMG {
   const DevLevel& level(int l) const { return lev_[l]; }
   hipStream_t stream() const { return stream_; }
   double* scratch(int i) { return scratch_[i]; }
-  void set_use_graph(bool g) { use_graph_ = g; }
+  // Whole-cycle hipGraphs: one rank always; several ranks when the transport
+  // can be captured (RCCL), unless HVE_GRAPH_MULTI=0.
+  void set_use_graph(bool g);
   double cycle_op_count() const { return cycle_ops_; }
   bool multi_rank() const { return comm_ != nullptr; }
   // Re-key the row-block traversal (tuning; see locality_keys in runtime.hip).
@@ -207,6 +214,7 @@ class DevAMG {
  private:
   void emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed, bool zero_u = false);
   bool can_fuse_presmooth() const;
+  void capture_failed(const char* why);
   double* presmooth_buffer();
   void relax(int level, int relax_type, int relax_points, const double* f, double*& u_cur, double*& u_alt,
              bool zero_guess, hipStream_t s);
@@ -238,6 +246,9 @@ class DevAMG {
   hipEvent_t ev_packed_ = nullptr, ev_halo_ = nullptr;
   DevComm* comm_ = nullptr;  // not owned
   bool use_graph_ = true;
+  // multi-rank: a cycle shape runs eagerly once before it is captured (the
+  // transport sets up its peer connections outside the capture)
+  std::map<std::tuple<const void*, const void*, int>, int> eager_runs_;
   // the solve loop's residual norm summed inside the fused residual + sweep
   // kernel (no r stored); HVE_NRM_FUSE=0 stores r and runs the dot kernel
   bool nrm_fusion_ = [] {
@@ -250,6 +261,10 @@ class DevAMG {
   int agg_level_ = -1;            // first replicated level (RankHierarchy::agg_level)
   std::vector<int> agg_starts_;   // its rows' distributed owners
 };
+
+// Tuning harness (hypreve_BenchOperator): average ms of op on A alone.
+double bench_operator(const CSR& A, int op, int policy, int nbands, int reps, double* stored_bytes, char* layout_msg,
+                      int msg_len);
 
 // PCG (krylov/pcg.c:262).
 struct PCGParams {

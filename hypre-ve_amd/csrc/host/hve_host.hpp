@@ -135,7 +135,9 @@ struct AMGParams {
   double cheby_fraction = 0.3;
   // Multi-rank: levels from the first one with at most agglo_rows global rows
   // down are replicated on every rank (0 = never); see partition.hpp.
-  int agglo_rows = 20000;
+  // -1 (default): automatic, kAggloRowsPerRank rows per rank.
+  int agglo_rows = -1;
+  static constexpr int kAggloRowsPerRank = 12288;
 };
 
 struct Level {

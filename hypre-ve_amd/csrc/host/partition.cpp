@@ -263,9 +263,13 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
 }
 
 int agglomeration_level(const AMGParams& prm, const std::vector<int64_t>& rows, int size) {
-  if (size <= 1 || prm.agglo_rows <= 0) return -1;
+  if (size <= 1 || prm.agglo_rows == 0) return -1;
+  // automatic (-1): a level is replicated once each rank's share is below
+  // kAggloRowsPerRank rows; its operators then take a few microseconds per
+  // application on one GPU, less than one halo exchange's latency
+  const int64_t lim = prm.agglo_rows > 0 ? prm.agglo_rows : (int64_t)AMGParams::kAggloRowsPerRank * size;
   for (size_t l = 1; l < rows.size(); ++l)
-    if (rows[l] <= prm.agglo_rows) return (int)l;
+    if (rows[l] <= lim) return (int)l;
   return -1;
 }
 

@@ -72,7 +72,8 @@ struct RankHierarchy {
   std::vector<int> agg_starts;
 };
 // First replicated level for `size` ranks (rank-independent): the first level
-// l >= 1 with rows[l] <= prm.agglo_rows, or -1.
+// l >= 1 with rows[l] <= prm.agglo_rows (automatic when negative: 12288 rows
+// per rank), or -1.
 int agglomeration_level(const AMGParams& prm, const std::vector<int64_t>& rows, int size);
 
 // starts0: level-0 row starts (size+1 entries).

@@ -194,6 +194,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchLevelOpStoredBytes", _i, [_p, _i, _i, _pd]),
+    ("hypreve_BenchOperator", _i, [_p, _i, _i, _i, _i, _pd, _pd, C.c_char_p, _i]),
     ("hypreve_BenchStream", _i, [_i, C.c_int64, _i, _pd]),
     ("hypreve_DeviceSynchronize", _i, []),
     ("hypreve_BuildInfo", C.c_char_p, []),
@@ -327,6 +328,15 @@ class ParCSRMatrix:
         check(lib().hypreve_ParCSRMatrixCreateFromCSR(None, 0, n, n, _ptr(ip, C.c_int), _ptr(jj, C.c_int),
                                                       _ptr(vv, C.c_double), C.byref(h)), "CreateFromCSR")
         return cls(h, n)
+
+    def bench_operator(self, op=0, policy=0, nbands=8, reps=20):
+        """(avg ms, stored bytes, layout text) of op applied to this matrix
+        alone (hypreve_BenchOperator; tuning)."""
+        ms, by = C.c_double(), C.c_double()
+        buf = C.create_string_buffer(160)
+        check(lib().hypreve_BenchOperator(self.h, op, policy, nbands, reps, C.byref(ms), C.byref(by), buf, 160),
+              "BenchOperator")
+        return ms.value, by.value, buf.value.decode()
 
     def matvec(self, alpha, x, beta, y):
         check(lib().HYPRE_ParCSRMatrixMatvec(alpha, self.h, x.h, beta, y.h), "Matvec")

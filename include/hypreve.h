@@ -283,7 +283,8 @@ HYPRE_Int hypreve_BoomerAMGSetRankEmulation(HYPRE_Solver solver, HYPRE_Int nrank
 /* Multi-rank: coarse levels with at most `rows` global rows (from the first
  * such level down) are held whole by every rank and cycled redundantly, with
  * one all-gather on the way down instead of halo exchanges on every coarse
- * level (same bits).  0 = never; default 20000. */
+ * level (same bits).  0 = never; < 0 (the default): automatic, from the first
+ * level with at most 12288 rows per rank. */
 HYPRE_Int hypreve_BoomerAMGSetAggloRows(HYPRE_Solver solver, HYPRE_Int rows);
 /* Whole-cycle hipGraph capture on/off (default on). */
 HYPRE_Int hypreve_BoomerAMGSetUseGraph(HYPRE_Solver solver, HYPRE_Int use_graph);
@@ -350,6 +351,15 @@ HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver solver, HYPRE_Int lev
  * as restriction): average ms over reps, algorithmic bytes, padded entries. */
 HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,
                                HYPRE_Real *avg_ms, HYPRE_Real *bytes, HYPRE_Real *padded_nnz);
+/* Tuning harness: the matrix's rows uploaded alone in layout `policy` (0 =
+ * automatic, as hypreve_BoomerAMGSetSellPolicy) with an nbands traversal, op
+ * (0 residual, 1 matvec, 2 l1-Jacobi, 8 residual + l1-Jacobi with the norm
+ * partials; the l1 forms take their norms on the fly, stencil / delta layouts)
+ * applied reps times: average ms, bytes of the stored layout + 24 B a row,
+ * and a layout description in layout[0..len). */
+HYPRE_Int hypreve_BenchOperator(HYPRE_ParCSRMatrix A, HYPRE_Int op, HYPRE_Int policy, HYPRE_Int nbands,
+                                HYPRE_Int reps, HYPRE_Real *avg_ms, HYPRE_Real *stored_bytes, char *layout,
+                                HYPRE_Int len);
 /* Bytes the same launch streams in the operator's stored (compressed) layout,
  * vectors included. */
 HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,

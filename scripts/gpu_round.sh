@@ -20,7 +20,7 @@ step() {  # step <name> <seconds> <cmd...>
 WHAT=${1:-all}
 want() { [[ $WHAT == all || ,$WHAT, == *,$1,* ]]; }  # e.g. tests,share,bench
 if want tests; then
-  step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread ${PYTEST_ARGS:-}
+  step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v --timeout 900 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"}
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 fi
 if want multi; then
