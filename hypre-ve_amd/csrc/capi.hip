@@ -827,7 +827,7 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands, HYPRE
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  CHECK_ARG(policy >= 0 && policy <= 11, 2);
+  CHECK_ARG(policy >= 0 && policy <= 12, 2);
   s->prm.sell_policy = policy;
   return 0;
 }
@@ -1338,7 +1338,7 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE
   API_BEGIN
   const DevLevel& L = s->dev->level(level);
   const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
-  *kind = M.slot_mask ? 11
+  *kind = M.code16 ? 12 : M.slot_mask ? 11
          : M.dcol ? (M.vidx16 ? 7 : M.vidx ? 6 : 5)
                  : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? (M.dict_ranges ? 10 : 4) : M.pw ? 3 : M.rowlen ? 1
                  : M.wide ? 2 : 0;
@@ -1411,6 +1411,55 @@ HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver s, HYPRE_Int level, H
   API_END
 }
 
+// Host check of the offset-coded layout of level's P (which 1) or R (which 2):
+// every row decoded from its 16-bit codes (offset and value tables, anchors,
+// fine -> coarse map) equals the CSR row entry for entry, values bitwise.
+HYPRE_Int hypreve_BoomerAMGCodedLayoutCheck(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int* noffsets,
+                                            HYPRE_Int* nvalues) {
+  CHECK_ARG(s && s->kind == KIND_AMG && !s->H.lev.empty(), 1);
+  CHECK_ARG(level >= 0 && level + 1 < (HYPRE_Int)s->H.lev.size(), 2);
+  CHECK_ARG(which == 1 || which == 2, 3);
+  API_BEGIN
+  const auto& L = s->H.lev[level];
+  const CSR& M = which == 1 ? L.P : L.R;
+  if (noffsets) *noffsets = 0;
+  if (nvalues) *nvalues = 0;
+  std::vector<int> fc, cidx(L.A.nrows, -1);
+  for (int i = 0; i < (int)L.cf.size() && i < L.A.nrows; ++i)
+    if (L.cf[i] == 1) {
+      cidx[i] = (int)fc.size();
+      fc.push_back(i);
+    }
+  static const std::vector<int> none;
+  std::vector<int> sp, ot;
+  std::vector<unsigned short> code;
+  std::vector<double> tab;
+  int vb = 0;
+  // not coded (too many offsets or values): success with zero counts
+  if (!build_sell_coded_host(M, none, which == 2 ? fc : none, which == 1 ? fc : none, which == 1 ? cidx : none, sp,
+                             code, ot, tab, vb))
+    return 0;
+  for (int r = 0; r < M.nrows; ++r) {
+    const int s0 = r >> 6, w = (sp[s0 + 1] - sp[s0]) >> 6;
+    const int64_t a = which == 2 ? fc[r] : r;
+    int e = M.i[r];
+    for (int k = 0; k < w; ++k) {
+      const unsigned c = code[(size_t)sp[s0] + (size_t)k * 64 + (r & 63)];
+      if (c == 0xFFFF) break;
+      const int64_t pos = a + ot[c >> vb];
+      const int64_t col = which == 1 ? cidx[pos] : pos;
+      if (e >= M.i[r + 1] || col != M.j[e] || std::memcmp(&tab[c & ((1u << vb) - 1)], &M.a[e], 8) != 0)
+        throw std::runtime_error("coded layout: row " + std::to_string(r) + " differs at its entry " +
+                                 std::to_string(e - M.i[r]));
+      ++e;
+    }
+    if (e != M.i[r + 1]) throw std::runtime_error("coded layout: row " + std::to_string(r) + " loses entries");
+  }
+  if (noffsets) *noffsets = (HYPRE_Int)ot.size();
+  if (nvalues) *nvalues = (HYPRE_Int)tab.size();
+  API_END
+}
+
 // Average time of one application of a level operator (which: 0 = A_l as the
 // residual r = f - A u, 1 = P_l as prolongation u_l += P u_{l+1}, 2 = R_l as
 // restriction f_{l+1} = R r_l) with its algorithmic bytes: every stored
@@ -1463,6 +1512,14 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
              (M.rowmap ? (double)M.nrows * 4.0 : 0.0) + (M.rowlen ? (double)M.nrows * 4.0 : 0.0);
   if (padded_nnz) *padded_nnz = (double)M.nnz_pad;
   API_END
+}
+
+// Tuning knobs read by the launch code (kernels.h set_knob): variants compared
+// in one process on one hierarchy.
+HYPRE_Int hypreve_SetKnob(HYPRE_Int id, HYPRE_Int value) {
+  CHECK_ARG(id >= 0 && id < 16, 1);
+  set_knob(id, value);
+  return 0;
 }
 
 // Bytes one hypreve_BenchLevelOp launch streams in the operator's stored layout

@@ -45,6 +45,16 @@ struct SellView {
   // of two dependent ones (traversal map, then pattern index)
   const int* wave_map = nullptr;
   int nwave = 0;
+  // offset-coded layout (k_sell_code; host: build_sell_coded_host): per entry
+  // one 16-bit code (offset index << vbits | value index into vtab); column =
+  // a + otab[offset index], or cmap[a + otab[..]], a = anc[row] (the row itself
+  // when anc is null)
+  const unsigned short* code16 = nullptr;
+  const int* otab = nullptr;
+  int notab = 0;
+  int vbits = 0;
+  const int* anc = nullptr;
+  const int* cmap = nullptr;
 };
 
 enum : int {
@@ -87,6 +97,10 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const
                             int relax_points, const double* tmp, double* u, double w, double omega,
                             hipStream_t st);
 int sell_batch_override();
+// Tuning knobs read at launch (0 = default): 0 offset-coded row blocks per
+// step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU.
+void set_knob(int id, int v);
+int knob(int id);
 int stencil_slices_per_wave();
 int stencil_grid(int nrows);
 bool stencil_wave_map();

@@ -84,6 +84,12 @@ struct SpArgs {
   int nblk;                                  // entries of blk_map
   const int* __restrict__ wave_map;          // stencil layout, R = 1: {slice, pattern} per logical wave
   int nwave;
+  const unsigned short* __restrict__ code16; // offset-coded layout: (offset index << vbits) | value index
+  const int* __restrict__ otab;              // offset-coded layout: the distinct offsets
+  int notab;
+  int vbits;
+  const int* __restrict__ anc;               // offset-coded layout: row anchors (nullptr: the row)
+  const int* __restrict__ cmap;              // offset-coded layout: position -> column (nullptr: identity)
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double* __restrict__ nrm;       // OP_RESID_L1JAC (delta layout): per-workgroup sums of r_i^2 (y may be null)
@@ -804,6 +810,107 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
   // the solve loop's residual norm, fused: one partial per workgroup (every
   // workgroup writes one, rows or not)
   if ((OP == OP_RESID_L1JAC || OP == OP_MATVEC) && p.nrm) wg_sum_store(acc, p.nrm + blockIdx.x);
+}
+
+// ---------------------------------------------------------------------------
+// Offset-coded SELL-64 (host: build_sell_coded_host), for P_0 and R_0 of a grid
+// hierarchy: one 16-bit code per entry, (offset index << vbits) | value index.
+// The column is the row's anchor plus the offset (R: anchor = the coarse row's
+// fine point, column = a fine point), or cmap of it (P: anchor = the fine row,
+// cmap = fine point -> coarse index).  Offset and value tables sit in LDS, so
+// an entry streams 2 B; the lane walks its row's entries in stored order with
+// the usual rounding, so the sums are bitwise those of every other loop.  The
+// next batch's codes are loaded before this batch's adds (pipelined).
+// ---------------------------------------------------------------------------
+// NR rows per lane at once (rows of NR consecutive row blocks): all their
+// loads of a batch go out together, so a wave keeps NR x B gathers in flight.
+template <int OP, bool CFSEL, int B, bool MAP, int NR>
+__device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, const int* ot, int rb0) {
+  constexpr unsigned PAD = 0xFFFFu;
+  const int vb = p.vbits;
+  const unsigned vm = (1u << vb) - 1u;
+  const bool sub = op_subtracts<OP>() || (OP == OP_GENERAL && p.w == -1.0);
+  int g[NR], a[NR], width[NR];
+  bool act[NR];
+  const unsigned short* cp[NR];
+  RowPre pre[NR];
+  double t[NR];
+  int wmax = 0;
+#pragma unroll
+  for (int r = 0; r < NR; ++r) {
+    const int row = map_block(p, rb0 + r) * 256 + (int)threadIdx.x;
+    act[r] = row < p.nrows;
+    const int slice = __builtin_amdgcn_readfirstlane(act[r] ? row >> 6 : 0);
+    const int beg = p.slice_ptr[slice];
+    width[r] = act[r] ? __builtin_amdgcn_readfirstlane((p.slice_ptr[slice + 1] - beg) >> 6) : 0;
+    g[r] = act[r] ? (p.rowmap ? mload<true>(p.rowmap + row) : row) : 0;
+    cp[r] = p.code16 + beg + (threadIdx.x & (kWave - 1));
+    wmax = max(wmax, width[r]);  // the slice's width: wave-uniform
+    if (CFSEL && act[r] && p.cf[g[r]] != p.relax_points) {
+      if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) sstore<true>(p.y + g[r], p.x[g[r]]);
+      act[r] = false;
+    }
+    if (!act[r]) width[r] = 0;  // this lane loads nothing
+    a[r] = act[r] ? (p.anc ? mload<true>(p.anc + g[r]) : g[r]) : 0;
+    pre[r] = act[r] ? row_preload<OP, true>(p, g[r]) : RowPre{};
+    t[r] = act[r] ? row_init<OP, true>(p, g[r]) : 0.0;
+  }
+  unsigned c[NR][B];
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+#pragma unroll
+    for (int q = 0; q < B; ++q) c[r][q] = q < width[r] ? (unsigned)__builtin_nontemporal_load(cp[r] + q * kWave) : PAD;
+  for (int k = 0; k < wmax; k += B) {
+    double xv[NR][B];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        const int pos = c[r][q] != PAD ? a[r] + ot[c[r][q] >> vb] : 0;
+        const int col = c[r][q] == PAD ? -1 : MAP ? p.cmap[pos] : pos;
+        xv[r][q] = col >= 0 ? p.x[col] : 0.0;
+      }
+    unsigned cn[NR][B];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int q = 0; q < B; ++q)
+        cn[r][q] = (k + B + q) < width[r] ? (unsigned)__builtin_nontemporal_load(cp[r] + (k + B + q) * kWave) : PAD;
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        if (c[r][q] != PAD) {
+          const double pr = vt[c[r][q] & vm] * xv[r][q];
+          t[r] = sub ? t[r] - pr : t[r] + pr;
+        }
+      }
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int q = 0; q < B; ++q) c[r][q] = cn[r][q];
+  }
+#pragma unroll
+  for (int r = 0; r < NR; ++r)
+    if (act[r]) row_store_pre<OP, true>(p, g[r], false, t[r], 0.0, 0.0, pre[r]);
+}
+
+// Persistent grid (the tables are staged once per workgroup); each XCD's
+// workgroups walk its contiguous share of the row blocks, NR consecutive
+// blocks at a time.
+template <int OP, bool CFSEL, int B, bool MAP, int NR>
+__global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
+  extern __shared__ double vt[];  // nvtab doubles, then notab ints
+  int* ot = reinterpret_cast<int*>(vt + p.nvtab);
+  for (int i = threadIdx.x; i < p.nvtab; i += 256) vt[i] = p.vtab[i];
+  for (int i = threadIdx.x; i < p.notab; i += 256) ot[i] = p.otab[i];
+  __syncthreads();
+  const int nrb = (p.nrows + 255) >> 8;
+  const int per_xcd = (nrb + 7) >> 3;
+  const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
+  const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
+  for (int rb = r0 + (int)(blockIdx.x >> 3) * NR; rb < r1; rb += per_wg * NR)
+    code_rows_op<OP, CFSEL, B, MAP, NR>(p, vt, ot, rb);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -1571,6 +1678,43 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_P
     return hipGetLastError();
   }
+  if (M.code16) {  // offset-coded entries (P_0 / R_0 of a grid hierarchy)
+    a.code16 = M.code16;
+    a.otab = M.otab;
+    a.notab = M.notab;
+    a.vbits = M.vbits;
+    a.anc = M.anc;
+    a.cmap = M.cmap;
+    const int wpc = knob(2) > 0 ? knob(2) : 8;  // persistent workgroups per CU
+    const dim3 cgrid(std::min(a.nblocks_pad, 256 * wpc));
+    const size_t lds = (size_t)M.nvtab * sizeof(double) + (size_t)M.notab * sizeof(int);
+    const bool map = M.cmap != nullptr;
+    const int nr = knob(0) > 0 ? knob(0) : 1;   // row blocks per workgroup step
+    const int cb = knob(1) > 0 ? knob(1) : 8;   // codes per batch
+#define HVE_C2(OPV, CF, BB, NRV)                                                                  \
+  if (map) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, true, NRV>), cgrid, block, lds, s, a);  \
+  else hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV>), cgrid, block, lds, s, a);
+#define HVE_C(OPV, CF)                                                    \
+  if (CF) { HVE_C2(OPV, CF, 8, 1) }                                        \
+  else if (nr == 2 && cb == 4) { HVE_C2(OPV, CF, 4, 2) }                  \
+  else if (nr == 2) { HVE_C2(OPV, CF, 8, 2) }                              \
+  else if (nr == 4) { HVE_C2(OPV, CF, 4, 4) }                              \
+  else if (cb == 4) { HVE_C2(OPV, CF, 4, 1) }                              \
+  else if (cb == 16) { HVE_C2(OPV, CF, 16, 1) }                            \
+  else { HVE_C2(OPV, CF, 8, 1) }
+#define HVE_CL(OPV)                                               \
+  case OPV:                                                       \
+    if (cfsel) { HVE_C(OPV, true) } else { HVE_C(OPV, false) }   \
+    break;
+    switch (op) {  // the operators this layout is built for (P, R) and plain products
+      HVE_CL(OP_PROLONG) HVE_CL(OP_RESTRICT) HVE_CL(OP_RESTRICT_ZG) HVE_CL(OP_MATVEC) HVE_CL(OP_GENERAL)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_CL
+#undef HVE_C
+#undef HVE_C2
+    return hipGetLastError();
+  }
   if (M.vidx16) {  // 32-bit columns, 16-bit value indices (padded or jagged)
     const dim3 vgrid(std::min(a.nblocks_pad, 2048));
     const size_t lds = (size_t)M.nvtab * sizeof(double);
@@ -1638,6 +1782,14 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_LN
   return hipGetLastError();
 }
+
+// Tuning knobs (hypreve_SetKnob): read at launch time, so variants can be
+// compared in one process on one hierarchy.  0 = the built-in default.
+static int g_knob[16];
+void set_knob(int id, int v) {
+  if (id >= 0 && id < 16) g_knob[id] = v;
+}
+int knob(int id) { return (id >= 0 && id < 16) ? g_knob[id] : 0; }
 
 // Entries per load batch in the SELL row loop: chosen per operator at upload
 // (SellView::batch); HVE_SELL_BATCH=8|16 overrides it and HVE_SELL_PIPE=1
@@ -1748,8 +1900,27 @@ __global__ void __launch_bounds__(256) k_stream_mix(int64_t n, const double* __r
     __builtin_nontemporal_store(acc, y + i);
   }
 }
+// The same with 16-B accesses (two doubles per lane and access).
+typedef double dbl2 __attribute__((ext_vector_type(2)));
+template <int R>
+__global__ void __launch_bounds__(256) k_stream_mix2(int64_t n2, const dbl2* __restrict__ src, dbl2* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n2; i += (int64_t)gridDim.x * 256) {
+    dbl2 acc = {0.0, 0.0};
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc += __builtin_nontemporal_load(src + (int64_t)r * n2 + i);
+    __builtin_nontemporal_store(acc, y + i);
+  }
+}
 hipError_t launch_stream_mix(int64_t n, int reads, const double* src, double* y, hipStream_t st) {
   const dim3 grid(256 * 16), block(256);
+  if (knob(3) == 2) {  // 16-B accesses (n even)
+    const int64_t n2 = n / 2;
+    if (reads == 1) hipLaunchKernelGGL(k_stream_mix2<1>, grid, block, 0, st, n2, (const dbl2*)src, (dbl2*)y);
+    else if (reads == 2) hipLaunchKernelGGL(k_stream_mix2<2>, grid, block, 0, st, n2, (const dbl2*)src, (dbl2*)y);
+    else if (reads == 5) hipLaunchKernelGGL(k_stream_mix2<5>, grid, block, 0, st, n2, (const dbl2*)src, (dbl2*)y);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (reads == 1) hipLaunchKernelGGL(k_stream_mix<1>, grid, block, 0, st, n, src, y);
   else if (reads == 2) hipLaunchKernelGGL(k_stream_mix<2>, grid, block, 0, st, n, src, y);
   else if (reads == 5) hipLaunchKernelGGL(k_stream_mix<5>, grid, block, 0, st, n, src, y);

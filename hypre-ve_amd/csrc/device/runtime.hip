@@ -50,7 +50,7 @@ static int sell_valtab_env() {
 void DevSell::set_block_order(const std::vector<int>& stored_to_local, const std::vector<int64_t>& key) {
   if (key.empty() || nrows <= 0) return;
   // the row block one workgroup of the chosen loop runs (kernels.hip launch_sell)
-  const int unit = col16 ? 64 * dict_group : slot_mask ? 256 * stencil_slices_per_wave() : (delta_like() || vidx16) ? 256 : (wide && !rowlen) ? 64 : 256;
+  const int unit = col16 ? 64 * dict_group : slot_mask ? 256 * stencil_slices_per_wave() : (delta_like() || vidx16 || code16) ? 256 : (wide && !rowlen) ? 64 : 256;
   const int nb = (nrows + unit - 1) / unit;
   std::vector<int64_t> bk(nb);
   for (int b = 0; b < nb; ++b) {
@@ -93,8 +93,66 @@ void DevSell::build_wave_map() {
   nwave = nb * 4;
 }
 
-void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy, const std::vector<int64_t>* key) {
+void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy, const std::vector<int64_t>* key,
+                     const Coded* coded) {
   release();
+  // Offset-coded layout (P_0 / R_0 of a grid hierarchy: 25 offsets, ~1200
+  // weights, so an entry is one 16-bit code, 2 B instead of 6) where the grid
+  // context is given, the operator is large and the codes build.  Measured on
+  // MI355X (k_sell_code against padded + 16-bit values): R_0 at 512^3 1.46 vs
+  // 1.62 ms, at 256^3 0.160-0.176 vs 0.183; P_0 1.62 vs 1.29 ms and 0.19-0.23
+  // vs 0.156 (its column needs a second dependent gather, through the fine ->
+  // coarse map), so by default only restrictions take it.  Both are bound by
+  // their scattered x gathers, not by the bytes.  HVE_SELL_CODED=0 turns it
+  // off, 2 also on P; policy 12 forces it wherever it builds.
+  static const int coded_env = [] {
+    const char* e = getenv("HVE_SELL_CODED");
+    return e ? atoi(e) : 1;
+  }();
+  const bool coded_auto = coded_env == 2 || (coded_env == 1 && coded && coded->anc);
+  if (coded && A.nnz() > 0 && ((policy == 0 && coded_auto && A.nrows >= (1 << 18)) || policy == 12)) {
+    static const std::vector<int> none;
+    std::vector<int> sp, ot;
+    std::vector<unsigned short> cd;
+    std::vector<double> tab;
+    int vb = 0;
+    if (build_sell_coded_host(A, rowmap_h, coded->anc ? *coded->anc : none, coded->colpos ? *coded->colpos : none,
+                              coded->cmap ? *coded->cmap : none, sp, cd, ot, tab, vb)) {
+      nrows = A.nrows;
+      ncols = A.ncols;
+      nslices = (int)sp.size() - 1;
+      nnz = A.nnz();
+      nnz_pad = (int64_t)sp.back();
+      batch = 8;
+      pipe = 1;
+      slice_ptr = dupload(sp.data(), sp.size());
+      code16 = dupload(cd.data(), cd.size());
+      otab = dupload(ot.data(), ot.size());
+      notab = (int)ot.size();
+      vbits = vb;
+      vtab = dupload(tab.data(), tab.size());
+      nvtab = (int)tab.size();
+      if (coded->anc && !coded->anc->empty()) {
+        anc = dupload(coded->anc->data(), coded->anc->size());
+        anc_n = (int64_t)coded->anc->size();
+      }
+      if (coded->cmap && !coded->cmap->empty()) {
+        cmap = dupload(coded->cmap->data(), coded->cmap->size());
+        cmap_n = (int64_t)coded->cmap->size();
+      }
+      if (getenv("HVE_LAYOUT_LOG"))
+        fprintf(stderr, "[layout] coded rows=%d offsets=%d values=%d vbits=%d pad=%.2f\n", A.nrows, notab, nvtab, vbits,
+                (double)nnz_pad / std::max<int64_t>(1, nnz));
+      if (!rowmap_h.empty()) {
+        bool ident = true;
+        for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
+        if (!ident) rowmap = dupload(rowmap_h.data(), rowmap_h.size());
+      }
+      stored_map = rowmap_h;
+      if (key) set_block_order(rowmap_h, *key);
+      return;
+    }
+  }
   std::vector<int> sp, col, perm;
   std::vector<double> val;
   // Sort rows inside windows (SELL-C-sigma) only where the plain layout pads
@@ -505,6 +563,10 @@ void DevSell::release() {
   slice_ptr = nullptr; col = nullptr; val = nullptr; rowmap = nullptr; rowlen = nullptr;
   col16 = nullptr; dict_ptr = nullptr; dict = nullptr; dmax = 0; dict_group = 1; dict_ranges = 0; ndict = 0;
   nrows = ncols = nslices = 0; nnz = nnz_pad = 0; wide = 0; pw = 0;
+  for (void* q : {(void*)code16, (void*)otab, (void*)anc, (void*)cmap})
+    if (q) (void)hipFree(q);
+  code16 = nullptr; otab = nullptr; anc = nullptr; cmap = nullptr;
+  notab = vbits = 0; anc_n = cmap_n = 0;
 }
 
 void DevGs::upload(const CSR& A, int num_blocks, bool forward) {
@@ -535,8 +597,8 @@ void DevGs::release() {
   max_levels = 0;
 }
 
-void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key) {
-  in.upload(op.interior, op.map_int, policy, key);
+void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key, const DevSell::Coded* coded) {
+  in.upload(op.interior, op.map_int, policy, key, coded);
   bd.upload(op.boundary, op.map_bnd, policy);
   nrows_local = op.nrows_local;
 }
@@ -783,8 +845,28 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     D.A.upload(L.A, prm.sell_policy, kl);
     D.hu.upload(L.hu);
     if (l < nl - 1) {
-      D.P.upload(L.P, prm.sell_policy, kl);
-      D.R.upload(L.R, prm.sell_policy, kc);
+      // grid context of P_l / R_l for the offset-coded layout: the fine point
+      // of each local coarse point (fc) and its inverse (cidx, -1 at F points)
+      std::vector<int> fc, cidx;
+      DevSell::Coded cp, cr;
+      const DevSell::Coded *pc = nullptr, *rc = nullptr;
+      if (!L.cf.empty() && (int)L.cf.size() >= L.n_loc) {
+        cidx.assign(L.n_loc, -1);
+        for (int i = 0; i < L.n_loc; ++i)
+          if (L.cf[i] == 1) {
+            cidx[i] = (int)fc.size();
+            fc.push_back(i);
+          }
+        if ((int)fc.size() == R.lev[l + 1].n_loc) {
+          cp.colpos = &fc;
+          cp.cmap = &cidx;
+          cr.anc = &fc;
+          pc = &cp;
+          rc = &cr;
+        }
+      }
+      D.P.upload(L.P, prm.sell_policy, kl, pc);
+      D.R.upload(L.R, prm.sell_policy, kc, rc);
       D.hv.upload(L.hv);
     }
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());

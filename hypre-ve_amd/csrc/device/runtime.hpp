@@ -63,6 +63,13 @@ struct DevSell {
   int nwave = 0;
   void build_wave_map();
   std::vector<int> stored_map;  // host copy of the stored row -> local row map (empty: identity)
+  // offset-coded layout (P_0 / R_0 of a grid hierarchy; SellView::code16)
+  unsigned short* code16 = nullptr;
+  int* otab = nullptr;
+  int notab = 0, vbits = 0;
+  int* anc = nullptr;
+  int* cmap = nullptr;
+  int64_t anc_n = 0, cmap_n = 0;
   SellView view() const {
     SellView v;
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
@@ -70,13 +77,23 @@ struct DevSell {
     v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vidx16 = vidx16; v.vtab = vtab; v.nvtab = nvtab;
     v.slot_vi = slot_vi; v.slot_mask = slot_mask; v.stencil_w = stencil_w; v.slice_pat = slice_pat;
     v.blk_map = blk_map; v.nblk = nblk; v.wave_map = wave_map; v.nwave = nwave;
+    v.code16 = code16; v.otab = otab; v.notab = notab; v.vbits = vbits; v.anc = anc; v.cmap = cmap;
     return v;
   }
+  // Grid context of an interpolation / restriction operator for the
+  // offset-coded layout (build_sell_coded_host): anchors per local row,
+  // positions per column, position -> column map.
+  struct Coded {
+    const std::vector<int>* anc = nullptr;
+    const std::vector<int>* colpos = nullptr;
+    const std::vector<int>* cmap = nullptr;
+  };
   // rowmap: subset row -> local row; empty or identity -> no map
   // policy: AMGParams::sell_policy
   // key: per local row, the sort key of the locality traversal (nullptr: natural order)
+  // coded: grid context; the offset-coded layout is tried first where it is given
   void upload(const CSR& A, const std::vector<int>& rowmap = {}, int policy = 0,
-              const std::vector<int64_t>* key = nullptr);
+              const std::vector<int64_t>* key = nullptr, const Coded* coded = nullptr);
   // Workgroup row blocks visited in ascending key of their first row
   // (stored_to_local: stored row -> local row, empty = identity).
   void set_block_order(const std::vector<int>& stored_to_local, const std::vector<int64_t>& key);
@@ -92,6 +109,9 @@ struct DevSell {
   size_t bytes() const {
     if (slot_mask)  // stencil layout: per (slice, slot) offset, value index, lane mask
       return (size_t)nslices * 4 + (size_t)npat * stencil_w * 16 + (rowmap ? (size_t)nrows * 4 : 0);
+    if (code16)  // offset-coded: 2 B a slot, the anchors, the position -> column map once
+      return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * 2 + (size_t)(anc_n + cmap_n) * 4 +
+             (rowmap ? (size_t)nrows * 4 : 0);
     const size_t colb = dcol || col16 ? 2 : 4;
     const size_t valb = vidx ? 1 : vidx16 ? 2 : 8;
     size_t b = (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * (colb + valb);
@@ -108,7 +128,9 @@ struct DevOp {
   DevSell in, bd;
   int nrows_local = 0;
   int64_t nnz() const { return in.nnz + bd.nnz; }
-  void upload(const RankOp& op, int policy = 0, const std::vector<int64_t>* key = nullptr);
+  // coded: grid context for the interior rows (DevSell::Coded)
+  void upload(const RankOp& op, int policy = 0, const std::vector<int64_t>* key = nullptr,
+              const DevSell::Coded* coded = nullptr);
   void release() { in.release(); bd.release(); }
 };
 

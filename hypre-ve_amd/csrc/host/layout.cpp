@@ -369,6 +369,91 @@ bool build_value_table16(const std::vector<double>& val, int maxv, std::vector<u
   return value_table_impl(val, std::min(maxv, 65536), idx, tab);
 }
 
+// Offset-coded SELL-64.  Between two levels of a grid hierarchy the fine
+// points an interpolation row or a restriction row touches lie at a few fixed
+// offsets from the row's own grid point (the 7-point hierarchy's P_0 and R_0:
+// the 25 points within distance 2), and their weights take ~1200 distinct
+// values, so (offset, value) packs into 16 bits: 2 B an entry instead of 6
+// (32-bit column + 16-bit value index) or 12.
+bool build_sell_coded_host(const CSR& A, const std::vector<int>& rowmap, const std::vector<int>& anc,
+                           const std::vector<int>& colpos, const std::vector<int>& cmap, std::vector<int>& slice_ptr,
+                           std::vector<unsigned short>& code, std::vector<int>& otab, std::vector<double>& vtab,
+                           int& vbits) {
+  const int n = A.nrows;
+  if (n == 0 || A.nnz() == 0) return false;
+  constexpr int kMaxOff = 256;
+  auto anchor = [&](int i) -> int64_t {
+    const int g = rowmap.empty() ? i : rowmap[i];
+    if (anc.empty()) return g;
+    return (g >= 0 && g < (int)anc.size()) ? anc[g] : INT64_MIN / 4;
+  };
+  auto position = [&](int c) -> int64_t {
+    if (colpos.empty()) return c;
+    return (c >= 0 && c < (int)colpos.size() && colpos[c] >= 0) ? colpos[c] : INT64_MIN / 4;
+  };
+  // distinct offsets, with the decode checked entry by entry
+  std::vector<int64_t> offs;
+  bool bad = false;
+#pragma omp parallel
+  {
+    std::unordered_set<int64_t> mine;
+#pragma omp for schedule(static)
+    for (int i = 0; i < n; ++i) {
+      if (bad) continue;
+      const int64_t a = anchor(i);
+      for (int k = A.i[i]; k < A.i[i + 1]; ++k) {
+        const int64_t pos = position(A.j[k]);
+        const int64_t off = pos - a;
+        const int64_t at = a + off;
+        bool ok = pos > INT64_MIN / 8 && a > INT64_MIN / 8 && off >= INT_MIN && off <= INT_MAX;
+        if (ok && !cmap.empty()) ok = at >= 0 && at < (int64_t)cmap.size() && cmap[at] == A.j[k];
+        if (ok && cmap.empty()) ok = at == A.j[k];
+        if (!ok || (mine.insert(off).second && (int)mine.size() > kMaxOff)) {
+          bad = true;
+          break;
+        }
+      }
+    }
+#pragma omp critical
+    offs.insert(offs.end(), mine.begin(), mine.end());
+  }
+  if (bad) return false;
+  std::sort(offs.begin(), offs.end());
+  offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
+  if ((int)offs.size() > kMaxOff) return false;
+  std::vector<unsigned short> vi;
+  if (!build_value_table16(A.a, 4096, vi, vtab)) return false;
+  vbits = 1;
+  while ((1 << vbits) < (int)vtab.size()) ++vbits;
+  const int obits = 16 - vbits;
+  // the largest offset index stays below 2^obits - 1, so 0xFFFF is never a code
+  if (obits <= 0 || (int64_t)offs.size() >= (1LL << obits)) return false;
+  otab.assign(offs.begin(), offs.end());
+  const int ns = (n + 63) / 64;
+  std::vector<int64_t> sp(ns + 1, 0);
+  for (int s = 0; s < ns; ++s) {
+    int w = 0;
+    for (int r = s * 64; r < std::min(n, (s + 1) * 64); ++r) w = std::max(w, A.i[r + 1] - A.i[r]);
+    sp[s + 1] = sp[s] + (int64_t)w * 64;
+  }
+  if (sp[ns] > 0x7fffffffLL) return false;
+  slice_ptr.assign(ns + 1, 0);
+  for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
+  code.assign((size_t)sp[ns], 0xFFFF);
+#pragma omp parallel for schedule(static)
+  for (int s = 0; s < ns; ++s) {
+    for (int r = s * 64; r < std::min(n, (s + 1) * 64); ++r) {
+      const int64_t a = anchor(r);
+      for (int k = A.i[r]; k < A.i[r + 1]; ++k) {
+        const int64_t off = position(A.j[k]) - a;
+        const int oi = (int)(std::lower_bound(offs.begin(), offs.end(), off) - offs.begin());
+        code[(size_t)sp[s] + (size_t)(k - A.i[r]) * 64 + (r & 63)] = (unsigned short)((oi << vbits) | vi[k]);
+      }
+    }
+  }
+  return true;
+}
+
 // Jagged SELL-64: rows sorted by descending length inside each 64-row slice
 // (stable), entry k stored only for the cnt_k lanes whose row is longer than
 // k, at slice_ptr[s] + (cnt_0 + ... + cnt_{k-1}) + lane.  No padding is

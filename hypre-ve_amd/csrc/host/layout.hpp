@@ -38,6 +38,20 @@ bool build_value_table(const std::vector<double>& val, int maxv, std::vector<uns
 // The same with 16-bit indices (maxv <= 65536).
 bool build_value_table16(const std::vector<double>& val, int maxv, std::vector<unsigned short>& idx,
                          std::vector<double>& tab);
+// Offset-coded SELL-64 (P and R between two levels of a grid hierarchy).  Row
+// i of A (local row g = rowmap[i], identity when empty) has the anchor
+// a = anc[g] (g when anc is empty); column c has the position colpos[c] (c when
+// empty).  Each entry stores one 16-bit code, (offset index << vbits) | value
+// index, where otab[offset index] = position(c) - a and vtab[value index] is
+// bitwise the entry's value; the device recovers the column as a + off, or
+// cmap[a + off] when cmap is not empty.  Padded, natural row order, padding
+// code 0xFFFF.  false (nothing built) when more than 256 distinct offsets or
+// 4096 distinct values occur, the codes do not fit 16 bits, or some column is
+// not recovered exactly.
+bool build_sell_coded_host(const CSR& A, const std::vector<int>& rowmap, const std::vector<int>& anc,
+                           const std::vector<int>& colpos, const std::vector<int>& cmap, std::vector<int>& slice_ptr,
+                           std::vector<unsigned short>& code, std::vector<int>& otab, std::vector<double>& vtab,
+                           int& vbits);
 // Jagged SELL-64 (no stored padding): perm[i] = CSR row at stored position i
 // (rows sorted by descending length inside each slice), rowlen[i] its length
 // (nslices*64 entries, 0 past the last row), entry k of the slice's lane r at

@@ -192,6 +192,8 @@ SIGNATURES = [
     ("hypreve_BoomerAMGSetRankEmulation", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
+    ("hypreve_BoomerAMGCodedLayoutCheck", _i, [_p, _i, _i, _pi, _pi]),
+    ("hypreve_SetKnob", _i, [_i, _i]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchLevelOpStoredBytes", _i, [_p, _i, _i, _pd]),
     ("hypreve_BenchOperator", _i, [_p, _i, _i, _i, _i, _pd, _pd, C.c_char_p, _i]),
@@ -558,6 +560,15 @@ class BoomerAMG:
         check(lib().hypreve_BoomerAMGStencilLayoutCheck(self.h, level, C.byref(w), C.byref(npat)), "StencilLayoutCheck")
         return w.value, npat.value
 
+    def coded_layout_check(self, level=0, which=1):
+        """(distinct offsets, distinct values) of level's P (which 1) or R (2)
+        in the offset-coded layout, checked row by row against the CSR on the
+        host; (0, 0) when the operator does not code in 16 bits."""
+        no, nv = C.c_int(), C.c_int()
+        check(lib().hypreve_BoomerAMGCodedLayoutCheck(self.h, level, which, C.byref(no), C.byref(nv)),
+              "CodedLayoutCheck")
+        return no.value, nv.value
+
     def bench_level_op(self, level, which=0, reps=20):
         """(avg_ms, algorithmic bytes, padded entries) of A_l (0), P_l (1) or R_l (2)."""
         ms, by, pz = C.c_double(), C.c_double(), C.c_double()
@@ -601,7 +612,7 @@ class BoomerAMG:
         check(lib().hypreve_BoomerAMGSetRankEmulation(self.h, len(starts) - 1, arr), "SetRankEmulation")
 
     LAYOUTS = ("padded", "jagged", "wide", "jag-pw", "dict", "delta", "delta+vt8", "delta+vt16", "padded+vt16",
-               "jagged+vt16", "dict-ranges", "stencil")
+               "jagged+vt16", "dict-ranges", "stencil", "coded")
 
     def level_layout(self, level, which=0):
         """Device layout name of A_l (0), P_l (1) or R_l (2) (interior rows)."""
@@ -684,3 +695,8 @@ def ij_amg_defaults(solver_id=0):
     return dict(max_row_sum=1.0, tol=1e-8 if solver_id == 0 else 0.0, max_iter=100 if solver_id == 0 else 1,
                 strong_threshold=0.25, trunc_factor=0.0, P_max_elmts=4, max_coarse_size=9, max_levels=25,
                 cycle_type=1, relax_wt=1.0, outer_wt=1.0)
+
+
+def set_knob(knob_id, value):
+    """Tuning knob read at kernel launch (hypreve_SetKnob; results unchanged)."""
+    check(lib().hypreve_SetKnob(knob_id, value), "SetKnob")

@@ -256,8 +256,10 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands,
  * most 63 contiguous column ranges (range dictionary), 11 slot-uniform
  * stencil layout (per slice and slot one column offset, one value and a lane
  * mask; nothing stored per entry) where an operator is a constant-coefficient
- * stencil, else as 7.  All give identical bits; the forced settings exist for
- * parity tests and experiments. */
+ * stencil, else as 7, 12 offset-coded P and R (one 16-bit code per entry:
+ * offset from the row's grid point and value index) where they build, else
+ * padded.  All give identical bits; the forced settings exist for parity tests
+ * and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* One GPU runs the hybrid Gauss-Seidel smoothers with the row blocks of an
  * N-rank run whose level-0 rows start at starts[0..nranks] (num_blocks blocks
@@ -336,7 +338,8 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver solver, HYPRE_Real *byte
  * 0 padded SELL-64, 1 jagged, 2 workgroup-per-slice, 3 jagged wave-product,
  * 4 dictionary, 5 16-bit column deltas, 6 deltas + 8-bit value table,
  * 7 deltas + 16-bit value table, 8 padded + 16-bit value table, 9 jagged +
- * 16-bit value table, 10 range dictionary, 11 slot-uniform stencil. */
+ * 16-bit value table, 10 range dictionary, 11 slot-uniform stencil,
+ * 12 offset-coded (P, R). */
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int *kind);
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
@@ -347,6 +350,12 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_bl
  * *npatterns = 0) when the operator is not a constant-coefficient stencil. */
 HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int *width,
                                               HYPRE_Int *npatterns);
+/* Host check of the offset-coded layout of level's P (which 1) or R (which 2)
+ * (after hypreve_BoomerAMGSetupHost or Setup): every row decoded from its
+ * 16-bit codes equals the CSR row entry for entry, values bitwise.
+ * *noffsets = *nvalues = 0 when the operator does not code in 16 bits. */
+HYPRE_Int hypreve_BoomerAMGCodedLayoutCheck(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,
+                                            HYPRE_Int *noffsets, HYPRE_Int *nvalues);
 /* One level operator (which 0 = A as residual, 1 = P as prolongation, 2 = R
  * as restriction): average ms over reps, algorithmic bytes, padded entries. */
 HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int reps,
@@ -360,6 +369,10 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int w
 HYPRE_Int hypreve_BenchOperator(HYPRE_ParCSRMatrix A, HYPRE_Int op, HYPRE_Int policy, HYPRE_Int nbands,
                                 HYPRE_Int reps, HYPRE_Real *avg_ms, HYPRE_Real *stored_bytes, char *layout,
                                 HYPRE_Int len);
+/* Tuning knobs read at kernel launch (0 = built-in default): 0 row blocks per
+ * step of the offset-coded loop (1, 2, 4), 1 its codes per batch (4, 8, 16),
+ * 2 its persistent workgroups per CU.  Results are unchanged. */
+HYPRE_Int hypreve_SetKnob(HYPRE_Int id, HYPRE_Int value);
 /* Bytes the same launch streams in the operator's stored (compressed) layout,
  * vectors included. */
 HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,

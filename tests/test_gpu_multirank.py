@@ -207,3 +207,19 @@ def test_loopback_stencil_layout_bitwise(hv, nranks, stencil, relax):
     xN, itN, rrN, nlN = _solve_nranks(hv, 14, 13, 16, kw, nranks, stencil=stencil)
     assert nlN == nl1 and all(i == it1 for i in itN)
     assert np.array_equal(x1, xN)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+@pytest.mark.parametrize("agglo", [0, 20000])
+def test_loopback_coded_layout_bitwise(hv, nranks, agglo):
+    """Offset-coded P and R (policy 12) on every rank's interior rows: anchors
+    and the fine -> coarse map are rank-local, boundary rows and the
+    agglomerated levels keep the other layouts.  The N-rank iterates equal the
+    one-rank ones bit for bit."""
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-8, max_iter=60,
+              sell_policy=12, agglo_rows=agglo)
+    x1, it1, rr1, nl1 = _solve_1rank(hv, 14, 13, 16, kw)
+    xN, itN, rrN, nlN = _solve_nranks(hv, 14, 13, 16, kw, nranks)
+    assert nlN == nl1 and all(i == it1 for i in itN)
+    assert np.array_equal(x1, xN)

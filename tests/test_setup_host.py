@@ -240,3 +240,30 @@ def test_stencil_layout_rebuilds_rows(hv, gen, dims, width):
     assert 1 <= npat <= (A.n + 63) // 64
     if amg.num_levels() > 2:
         assert amg.stencil_layout_check(1) == (0, 0)
+
+
+@pytest.mark.parametrize("gen,dims", [("7", (30, 27, 25)), ("7", (200, 180, 3)), ("27", (13, 12, 15)),
+                                      ("aniso", (28, 26, 24))])
+def test_coded_layout_rebuilds_rows(hv, gen, dims):
+    """Offset-coded P_0 / R_0: every row decoded from its 16-bit codes (offset
+    from the row's grid point, value index; P through the fine -> coarse map)
+    equals the CSR row entry for entry, values bit for bit.  The 7-point
+    hierarchy codes with the 25 offsets within distance 2; operators whose
+    weights do not fit (the 27-point P_0: ~10^5 distinct values) report (0, 0)
+    and keep the other layouts."""
+    if gen == "27":
+        A = hv.ParCSRMatrix.laplacian27(*dims)
+    elif gen == "aniso":
+        A = hv.ParCSRMatrix.laplacian(*dims, cx=0.001, cy=1.0, cz=1.0)
+    else:
+        A = hv.ParCSRMatrix.laplacian(*dims)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup_host(A)
+    for which in (1, 2):
+        no, nv = amg.coded_layout_check(0, which)
+        if gen == "7":
+            assert 1 <= no <= 25 and 1 <= nv <= 2048, (which, no, nv)
+        else:
+            assert (no, nv) == (0, 0) or (no >= 1 and nv >= 1)
