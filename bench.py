@@ -335,6 +335,19 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
             "stream_read_gbs": round(stream_gbs, 1), "frac_of_stream": round(achieved / stream_gbs, 4),
             "stream_mix_gbs": round(mix_gbs, 1), "frac_of_mix_stream": round(achieved / mix_gbs, 4),
             "per_kernel": per_kernel}
+    if world == 1 and comm is None and not light:
+        # the same finest residual through the general per-entry path: the
+        # operator uploaded alone in padded SELL-64 (32-bit column + f64 value
+        # per stored entry, what any variable-coefficient operator streams),
+        # same traversal, HIP events
+        g_ms, g_bytes, _ = A.bench_operator(op=0, policy=1, nbands=8, reps=max(5, args.spmv_reps // 2))
+        roof["general"] = {"layout": "padded SELL-64, 32-bit column + f64 value per entry (policy 1)",
+                           "avg_ms": round(g_ms, 4), "bytes_per_launch": round(g_bytes),
+                           "achieved": round(g_bytes / (g_ms * 1e-3) / 1e9, 1),
+                           "frac": round(g_bytes / (g_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+        if rank == 0:
+            log(f"[bench] general path (padded, f64 values): {g_ms:.4f} ms, {g_bytes / 1e9:.3f} GB -> "
+                f"{roof['general']['achieved']:.0f} GB/s ({roof['general']['frac']:.3f})")
     if rank == 0:
         log(f"[bench] read stream {stream_gbs:.0f} GB/s, 5:1 read/write mix {mix_gbs:.0f} GB/s; "
             f"fine SpMV at {achieved / stream_gbs:.3f} / {achieved / mix_gbs:.3f} of them")

@@ -96,11 +96,14 @@ struct hypre_Solver_struct {
 // coarsening and GS blocks; no agglomeration, which the reference lacks).
 static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A);
 // Automatic hybrid Gauss-Seidel block count (num_blocks 0): one block of about
-// kAutoBlockRows rows each, so a large level's sweep runs on thousands of
-// workgroups while every block keeps hypre's exact in-block GS order.
-// The count is chosen per level and per rank from that level's own rows
-// (AMGParams::blocks_for), so coarse levels keep blocks of about that size too.
-// HVE_AUTO_BLOCK_ROWS overrides the block size (tuning).
+// 4096 rows of the rank's level 0, so a large level's sweep runs on thousands
+// of workgroups while every block keeps hypre's exact in-block GS order.  That
+// count plays hypre's OMP_NUM_THREADS on every level (AMGParams::blocks_for),
+// capped so that a coarse level's blocks keep at least 64 rows.  Measured on
+// MI355X (256^3, relax 13/14): blocks of 4096 rows on every level 45.6 ms a
+// cycle, 1024 rows 38.5 (the coarse Galerkin levels' long in-block dependency
+// chains on few blocks), the level-0 count everywhere (round 2) 11.5.
+// HVE_AUTO_BLOCK_ROWS overrides the level-0 block size (tuning).
 static int auto_block_rows() {
   static const int v = [] {
     const char* e = getenv("HVE_AUTO_BLOCK_ROWS");
@@ -111,7 +114,7 @@ static int auto_block_rows() {
 }
 static void resolve_blocks(hypre_Solver_struct* s, int local_rows) {
   s->prm.auto_block_rows = s->auto_blocks ? auto_block_rows() : 0;
-  if (s->auto_blocks) s->prm.num_blocks = s->prm.blocks_for(local_rows);  // level 0 (reported)
+  if (s->auto_blocks) s->prm.num_blocks = std::max(1, (local_rows + auto_block_rows() - 1) / auto_block_rows());
 }
 
 // ---------------------------------------------------------------------------

@@ -16,6 +16,7 @@
 //   parcsr_ls/par_rap.c:27             hypre_BoomerAMGBuildCoarseOperatorKT
 //   parcsr_ls/ams.c:571,3398           hypre_ParCSRComputeL1Norms(Threads)
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <utility>
@@ -42,6 +43,62 @@ struct CSR {
 struct Pattern {
   int n = 0;
   std::vector<int> i, j;
+};
+
+// Per-row marker map: the reference's P_marker / A_marker arrays (one int per
+// point of the matrix, per thread) restricted to the points one row touches.
+// Open addressing in a power-of-two table sized per row from an upper bound of
+// its entries; a generation stamp per slot empties the table in O(1) between
+// rows.  Lookups cost an L1 hit instead of a cache miss into an array of
+// n ints, and a thread holds kilobytes instead of 4n bytes.
+struct RowMap {
+  std::vector<int> key, val;
+  std::vector<unsigned> gen;
+  unsigned cur = 0, mask = 0;
+  int shift = 32;
+  // start a row that inserts at most `bound` keys
+  void begin(int64_t bound) {
+    size_t cap = 16;
+    while ((int64_t)cap < 2 * bound + 2) cap <<= 1;
+    if (key.size() < cap) {
+      key.assign(cap, 0);
+      val.assign(cap, 0);
+      gen.assign(cap, 0);
+      cur = 0;
+    }
+    mask = (unsigned)cap - 1;
+    shift = 32;
+    for (size_t c = cap; c > 1; c >>= 1) --shift;
+    if (++cur == 0) {  // stamp wrapped: clear once
+      std::fill(gen.begin(), gen.end(), 0u);
+      cur = 1;
+    }
+  }
+  // slot of k (inserted with value v0 when absent; *fresh tells which)
+  int* find_or_insert(int k, int v0, bool* fresh) {
+    unsigned h = ((unsigned)k * 2654435761u) >> shift;
+    for (;; h = (h + 1) & mask) {
+      if (gen[h] != cur) {
+        gen[h] = cur;
+        key[h] = k;
+        val[h] = v0;
+        *fresh = true;
+        return &val[h];
+      }
+      if (key[h] == k) {
+        *fresh = false;
+        return &val[h];
+      }
+    }
+  }
+  // value of k, or dflt when absent
+  int get(int k, int dflt) const {
+    unsigned h = ((unsigned)k * 2654435761u) >> shift;
+    for (;; h = (h + 1) & mask) {
+      if (gen[h] != cur) return dflt;
+      if (key[h] == k) return val[h];
+    }
+  }
 };
 
 // Point types (hypre: C_PT 1, F_PT -1, Z_PT -2, SF_PT -3).
@@ -98,17 +155,21 @@ struct AMGParams {
   // Number of contiguous row blocks for the hybrid (block-Jacobi / in-block GS)
   // smoothers; hypre's CPU path uses num_threads for this (par_relax.c:4387).
   int num_blocks = 1;
-  // > 0: the block count is chosen per level (and per rank) instead, one block
-  // of about auto_block_rows rows (hypreve_BoomerAMGSetNumBlocks(0)); a small
-  // coarse level then keeps a few blocks instead of one row each.
+  // > 0 (hypreve_BoomerAMGSetNumBlocks(0)): num_blocks is the level-0 count,
+  // one block of about auto_block_rows rows (hypre's OMP_NUM_THREADS), used on
+  // every level as hypre does, except that a coarse level never gets blocks of
+  // fewer than auto_block_min rows (there hypre's blocks of 0-1 rows would turn
+  // relax 3/4/6 into unweighted Jacobi and 8/13/14 into l1-Jacobi).
   int auto_block_rows = 0;
+  int auto_block_min = 64;
   // hybrid-GS row blocks of a level (one rank's share) of `rows` rows
   int blocks_for(int rows) const {
+    const int top = num_blocks < 1 ? 1 : num_blocks;
     if (auto_block_rows > 0) {
-      const long long b = ((long long)rows + auto_block_rows - 1) / auto_block_rows;
-      return b < 1 ? 1 : (int)b;
+      const long long cap = ((long long)rows + auto_block_min - 1) / auto_block_min;
+      return (int)std::max(1LL, std::min<long long>(top, cap));
     }
-    return num_blocks < 1 ? 1 : num_blocks;
+    return top;
   }
   // Aggressive coarsening (par_amg.c:153-173 defaults): the first
   // agg_num_levels levels coarsen twice (second pass on S*S + 2S over the C

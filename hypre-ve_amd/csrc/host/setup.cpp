@@ -12,6 +12,8 @@
 #include <cstdio>
 #include <cstring>
 #include <chrono>
+#include <cstdlib>
+#include <cstdio>
 #include <stdexcept>
 #ifdef _OPENMP
 #include <omp.h>
@@ -809,33 +811,47 @@ void truncate_rows(CSR& P, double tol, int max_elmts) {
 // indices (ncoarse in all).
 void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
                 int nrows, int ncoarse, int nuniv, CSR& P) {
-  // Row-parallel restatement.  Each row's P entries depend only on the
-  // markers set while processing that row (stale markers of earlier rows of
-  // the same thread are below jj_begin_row or are other negative stamps), so a
-  // thread-local P_marker processed in increasing row order reproduces the
-  // single-thread result entry for entry.
+  // Row-parallel restatement.  The reference's P_marker (one int per point)
+  // only ever tells, for the row being built, whether a point is in its C-hat
+  // set (marker = the entry's slot, >= jj_begin_row), one of its strong F
+  // neighbours (marker = strong_f_marker) or neither (a stale value of an
+  // earlier row); a per-row map (RowMap) answers the same three ways, so every
+  // row's entries, their order and their sums are unchanged.
+  (void)nuniv;
   const int n = nrows;
+  constexpr int kNone = -1, kStrongF = -2;
   P.resize_rows(n, ncoarse);
   std::vector<int> rowcnt(n, 0);
+  // upper bound of the points a row's C-hat search inserts
+  auto bound = [&](int i) {
+    int64_t b = 1 + (S.i[i + 1] - S.i[i]);
+    for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) b += S.i[S.j[jj] + 1] - S.i[S.j[jj]];
+    return b;
+  };
 #pragma omp parallel
   {
-    std::vector<int> P_marker(nuniv, -1);
+    RowMap M;
 #pragma omp for schedule(static)
     for (int i = 0; i < n; ++i) {
-      // first pass (par_lr_interp.c:1290-1370): |C-hat_i|, stamped by row id
+      // first pass (par_lr_interp.c:1290-1370): |C-hat_i|
       int cnt = 0;
-      const int stamp = i;
       if (cf[i] >= 0) {
         cnt = 1;
       } else if (cf[i] != SF_PT) {
+        M.begin(bound(i));
+        bool fresh;
         for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
           int i1 = S.j[jj];
           if (cf[i1] >= 0) {
-            if (P_marker[i1] != stamp) { P_marker[i1] = stamp; cnt++; }
+            M.find_or_insert(i1, 0, &fresh);
+            cnt += fresh;
           } else if (cf[i1] != SF_PT) {
             for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
               int k1 = S.j[kk];
-              if (cf[k1] >= 0 && P_marker[k1] != stamp) { P_marker[k1] = stamp; cnt++; }
+              if (cf[k1] >= 0) {
+                M.find_or_insert(k1, 0, &fresh);
+                cnt += fresh;
+              }
             }
           }
         }
@@ -849,8 +865,7 @@ void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, cons
   P.a.assign(nnzP, 0.0);
 #pragma omp parallel
   {
-    std::vector<int> P_marker(nuniv, -1);
-    int strong_f_marker = -2;
+    RowMap M;
 #pragma omp for schedule(static)
     for (int i = 0; i < n; ++i) {
       const int jj_begin_row = P.i[i];
@@ -860,19 +875,20 @@ void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, cons
         P.a[jc] = 1.0;
         jc++;
       } else if (cf[i] != SF_PT) {
-        strong_f_marker--;
+        M.begin(bound(i));
+        bool fresh;
         for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
           int i1 = S.j[jj];
           if (cf[i1] >= 0) {
-            if (P_marker[i1] < jj_begin_row) {
-              P_marker[i1] = jc; P.j[jc] = fine_to_coarse[i1]; P.a[jc] = 0.0; jc++;
-            }
+            M.find_or_insert(i1, jc, &fresh);
+            if (fresh) { P.j[jc] = fine_to_coarse[i1]; P.a[jc] = 0.0; jc++; }
           } else if (cf[i1] != SF_PT) {
-            P_marker[i1] = strong_f_marker;
+            *M.find_or_insert(i1, kStrongF, &fresh) = kStrongF;
             for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
               int k1 = S.j[kk];
-              if (cf[k1] >= 0 && P_marker[k1] < jj_begin_row) {
-                P_marker[k1] = jc; P.j[jc] = fine_to_coarse[k1]; P.a[jc] = 0.0; jc++;
+              if (cf[k1] >= 0) {
+                M.find_or_insert(k1, jc, &fresh);
+                if (fresh) { P.j[jc] = fine_to_coarse[k1]; P.a[jc] = 0.0; jc++; }
               }
             }
           }
@@ -881,21 +897,23 @@ void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, cons
         double diagonal = A.a[A.i[i]];
         for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
           int i1 = A.j[jj];
-          if (P_marker[i1] >= jj_begin_row) {
-            P.a[P_marker[i1]] += A.a[jj];
-          } else if (P_marker[i1] == strong_f_marker) {
+          const int m1 = M.get(i1, kNone);
+          if (m1 >= 0) {
+            P.a[m1] += A.a[jj];
+          } else if (m1 == kStrongF) {
             double sum = 0.0;
             int sgn = 1;
             if (A.a[A.i[i1]] < 0) sgn = -1;
             for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
               int i2 = A.j[jj1];
-              if ((P_marker[i2] >= jj_begin_row || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
+              if ((M.get(i2, kNone) >= 0 || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
             }
             if (sum != 0) {
               double distribute = A.a[jj] / sum;
               for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
                 int i2 = A.j[jj1];
-                if (P_marker[i2] >= jj_begin_row && (sgn * A.a[jj1]) < 0) P.a[P_marker[i2]] += distribute * A.a[jj1];
+                const int m2 = M.get(i2, kNone);
+                if (m2 >= 0 && (sgn * A.a[jj1]) < 0) P.a[m2] += distribute * A.a[jj1];
                 if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
               }
             } else {
@@ -909,7 +927,6 @@ void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, cons
           for (int jj = jj_begin_row; jj < jj_end_row; ++jj) P.a[jj] /= -diagonal;
         }
       }
-      strong_f_marker--;
     }
   }
 }
@@ -921,8 +938,12 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
   int coarse_counter = 0;
   for (int i = 0; i < n; ++i)
     if (cf[i] >= 0) fine_to_coarse[i] = coarse_counter++;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  double t0 = now();
   extpi_core(A, S, cf, fine_to_coarse, n, coarse_counter, n, P);
+  double t1 = now();
   if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+  if (getenv("HVE_SETUP_T")) fprintf(stderr, "extpi core %.3f trunc %.3f\n", t1 - t0, now() - t1);
   for (int i = 0; i < n; ++i)
     if (cf[i] == SF_PT) cf[i] = F_PT;
 }
@@ -1013,10 +1034,16 @@ void transpose(const CSR& A, CSR& AT) {
 // coarse-universe points (global coarse indices).
 void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& row_ic,
               const std::vector<int>& coarse_glob, int nfine_univ, int ncoarse_univ, int ncoarse_glob, CSR& C) {
+  // The reference's A_marker / P_marker arrays (per point) answer "position of
+  // this column in the row's touch list, or none" for the row being formed: a
+  // per-row map (RowMap) gives the same answers, so the first-touch order and
+  // every sum are unchanged.
+  (void)nfine_univ;
+  (void)ncoarse_univ;
   const int nc = R.nrows;
   C.resize_rows(nc, ncoarse_glob);
   std::vector<int> rowlen(nc, 0);
-  // Each thread keeps its own markers.  Two passes: sizes, then values.
+  // Two passes: sizes, then values.
   for (int pass = 0; pass < 2; ++pass) {
     if (pass == 1) {
       for (int r = 0; r < nc; ++r) C.i[r + 1] = C.i[r] + rowlen[r];
@@ -1025,7 +1052,7 @@ void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& 
     }
 #pragma omp parallel
     {
-      std::vector<int> A_marker(nfine_univ, -1), P_marker(ncoarse_univ, -1);
+      RowMap AM, PM;
       std::vector<int> ra_j;
       std::vector<double> ra_a;
       ra_j.reserve(4096);
@@ -1037,25 +1064,30 @@ void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& 
         const int ic = row_ic[q];
         ra_j.clear();
         ra_a.clear();
+        int64_t ba = 0;
+        for (int jj1 = R.i[q]; jj1 < R.i[q + 1]; ++jj1) ba += A.i[R.j[jj1] + 1] - A.i[R.j[jj1]];
+        AM.begin(ba);
+        bool fresh;
         for (int jj1 = R.i[q]; jj1 < R.i[q + 1]; ++jj1) {
           const int i1 = R.j[jj1];
           const double r_entry = R.a[jj1];
           for (int jj2 = A.i[i1]; jj2 < A.i[i1 + 1]; ++jj2) {
             const int i2 = A.j[jj2];
-            const int marker = A_marker[i2];
-            if (marker < 0) {
-              A_marker[i2] = (int)ra_j.size();
+            int* m = AM.find_or_insert(i2, (int)ra_j.size(), &fresh);
+            if (fresh) {
               ra_j.push_back(i2);
               ra_a.push_back(r_entry * A.a[jj2]);
             } else {
-              ra_a[marker] += r_entry * A.a[jj2];
+              ra_a[*m] += r_entry * A.a[jj2];
             }
           }
         }
-        for (int i2 : ra_j) A_marker[i2] = -1;
         tj.clear();
         ta.clear();
-        P_marker[ic] = 0;
+        int64_t bp = 1;
+        for (int i1 : ra_j) bp += P.i[i1 + 1] - P.i[i1];
+        PM.begin(bp);
+        PM.find_or_insert(ic, 0, &fresh);
         tj.push_back(ic);
         ta.push_back(0.0);
         for (size_t k = 0; k < ra_j.size(); ++k) {
@@ -1063,17 +1095,15 @@ void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& 
           const double rap_ = ra_a[k];
           for (int jj2 = P.i[i1]; jj2 < P.i[i1 + 1]; ++jj2) {
             const int i2 = P.j[jj2];
-            const int marker = P_marker[i2];
-            if (marker < 0) {
-              P_marker[i2] = (int)tj.size();
+            int* m = PM.find_or_insert(i2, (int)tj.size(), &fresh);
+            if (fresh) {
               tj.push_back(i2);
               ta.push_back(rap_ * P.a[jj2]);
             } else {
-              ta[marker] += rap_ * P.a[jj2];
+              ta[*m] += rap_ * P.a[jj2];
             }
           }
         }
-        for (int c : tj) P_marker[c] = -1;
         if (pass == 0) {
           rowlen[q] = (int)tj.size();
         } else {

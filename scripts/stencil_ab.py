@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--bands", type=int, default=8)
     ap.add_argument("--tag", default="")
+    ap.add_argument("--settings", default="", help="knob settings 'k=v,k=v;k=v' (hypreve_SetKnob), one row each")
     args = ap.parse_args()
     import torch  # noqa: F401
     import hypreve as hv
@@ -31,15 +32,20 @@ def main():
     t = time.time()
     n = args.n
     A = hv.ParCSRMatrix.laplacian27(n, n, n) if args.stencil == 27 else hv.ParCSRMatrix.laplacian(n, n, n)
-    row = {"tag": args.tag, "n": n, "stencil": args.stencil,
-           "env": {k: v for k, v in os.environ.items() if k.startswith("HVE_")}, "gen_s": round(time.time() - t, 1)}
-    for op, name in ((0, "resid"), (2, "l1jac"), (8, "resid_l1jac")):
-        t = time.time()
-        ms, by, lay = A.bench_operator(op=op, policy=0, nbands=args.bands, reps=args.reps)
-        row[name] = {"ms": round(ms, 4), "GBs": round(by / ms / 1e6, 1), "frac": round(by / ms / 1e6 / 8000, 4)}
-        row["layout"] = lay
-        row["upload_s"] = round(time.time() - t, 1)
-    print(json.dumps(row), flush=True)
+    base = {"tag": args.tag, "n": n, "stencil": args.stencil,
+            "env": {k: v for k, v in os.environ.items() if k.startswith("HVE_")}, "gen_s": round(time.time() - t, 1)}
+    for st in args.settings.split(";"):
+        knobs = dict((int(a), int(b)) for a, b in (kv.split("=") for kv in filter(None, st.split(","))))
+        for k in range(16):
+            hv.set_knob(k, knobs.get(k, 0))
+        row = dict(base, knobs=knobs)
+        for op, name in ((0, "resid"), (2, "l1jac"), (8, "resid_l1jac")):
+            t = time.time()
+            ms, by, lay = A.bench_operator(op=op, policy=0, nbands=args.bands, reps=args.reps)
+            row[name] = {"ms": round(ms, 4), "GBs": round(by / ms / 1e6, 1), "frac": round(by / ms / 1e6 / 8000, 4)}
+            row["layout"] = lay
+            row["upload_s"] = round(time.time() - t, 1)
+        print(json.dumps(row), flush=True)
     A.destroy()
 
 

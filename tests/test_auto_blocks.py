@@ -1,8 +1,8 @@
 """Automatic hybrid Gauss-Seidel blocks (hypreve_BoomerAMGSetNumBlocks(0), the
-default): the block count is chosen per level from that level's own rows, one
-block of about 4096 rows, so a coarse level of a few thousand rows keeps a
-real Gauss-Seidel block instead of blocks of 0-1 rows (which would turn relax
-3/4/6 into unweighted Jacobi and relax 8/13/14 into l1-Jacobi).
+default): level 0 gets one block per about 4096 rows, and that count (hypre's
+thread count) is used on every level, capped so that a coarse level keeps
+blocks of at least 64 rows instead of blocks of 0-1 rows (which would turn
+relax 3/4/6 into unweighted Jacobi and relax 8/13/14 into l1-Jacobi).
 
 CPU: the exported blocks and the convergence of relax 3 / 6 / 13 through the
 oracle.  GPU: the same hierarchies, iterates bitwise equal to the oracle.
@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 AUTO = 4096
+MIN_ROWS = 64
 
 
 def amg_auto(hv, relax, **extra):
@@ -27,16 +28,18 @@ def test_auto_blocks_per_level(hv, orc, relax):
     amg.setup_host(A)
     nl = amg.num_levels()
     assert nl >= 4
+    top = -(-A.n // AUTO)
     for l in range(nl):
         n = amg.level_info(l)[0]
         bs = amg.level_vector(l, 3)
-        nb = max(1, -(-n // AUTO))
+        nb = max(1, min(top, -(-n // MIN_ROWS)))
         assert bs.size == nb + 1, (l, n, bs.size)
         assert bs[0] == 0 and bs[-1] == n
         assert np.all(np.diff(bs) >= 1)
-    # level 0 has several blocks, the coarse levels one each
+    # level 0 has several blocks, the small coarse levels blocks of >= 64 rows
     assert amg.level_vector(0, 3).size - 1 == 12
-    assert amg.level_vector(nl - 2, 3).size - 1 == 1
+    assert amg.level_vector(1, 3).size - 1 == 12
+    assert np.all(np.diff(amg.level_vector(nl - 2, 3)) >= MIN_ROWS) or amg.level_vector(nl - 2, 3).size == 2
     O = orc.OracleAMG(amg)
     st = O.solve(np.ones(A.n), np.zeros(A.n), 1e-8, 60)
     assert st["rel_res"] < 1e-8 and st["iterations"] <= 25, st
