@@ -101,6 +101,13 @@ struct RowMap {
   }
 };
 
+// Working storage of one thread's Galerkin rows (rap_row).
+struct RapScratch {
+  RowMap AM, PM;
+  std::vector<int> ra_j, tj;
+  std::vector<double> ra_a, ta;
+};
+
 // Point types (hypre: C_PT 1, F_PT -1, Z_PT -2, SF_PT -3).
 enum { C_PT = 1, F_PT = -1, Z_PT = -2, SF_PT = -3 };
 
@@ -264,6 +271,13 @@ void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, cons
                 int nrows, int ncoarse, int nuniv, CSR& P);
 void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& row_ic,
               const std::vector<int>& coarse_glob, int nfine_univ, int ncoarse_univ, int ncoarse_glob, CSR& C);
+// Their single rows (the device versions finish rows that overflow LDS here).
+int extpi_row_count(const Pattern& S, const std::vector<int>& cf, int i, RowMap& M);
+void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
+                    int i, RowMap& M, CSR& P);
+void rap_row(const CSR& R, const CSR& A, const CSR& P, int q, int ic, RapScratch& W);
+// one row of truncate_rows in its own slots; returns the new length
+int truncate_row(CSR& P, int r, double tol, int max_elmts, std::vector<int>& rj, std::vector<double>& ra);
 double hypre_rand_at(int64_t k, int seed);
 // Chebyshev smoother setup (one process, one thread, as the reference's host
 // path): par_relax_more.c:115 hypre_ParCSRMaxEigEstimateCG (random start

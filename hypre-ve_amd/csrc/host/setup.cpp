@@ -736,6 +736,45 @@ static void qsort2_abs(int* v, double* w, int left, int right) {
   qsort2_abs(v, w, last + 1, right);
 }
 
+int truncate_row(CSR& P, int r, double tol, int max_elmts, std::vector<int>& rj, std::vector<double>& ra) {
+  const int b = P.i[r], e = P.i[r + 1];
+  rj.assign(P.j.begin() + b, P.j.begin() + e);
+  ra.assign(P.a.begin() + b, P.a.begin() + e);
+  if (tol > 0) {
+    double row_nrm = 0;
+    for (double x : ra) row_nrm = (row_nrm < std::fabs(x)) ? std::fabs(x) : row_nrm;
+    const double drop = tol * row_nrm;
+    double row_sum = 0, scale = 0;
+    size_t o = 0;
+    for (size_t k = 0; k < ra.size(); ++k) {
+      row_sum += ra[k];
+      if (!(std::fabs(ra[k]) < drop)) { scale += ra[k]; rj[o] = rj[k]; ra[o] = ra[k]; ++o; }
+    }
+    rj.resize(o);
+    ra.resize(o);
+    if (scale != 0. && scale != row_sum) {
+      scale = row_sum / scale;
+      for (double& x : ra) x *= scale;
+    }
+  }
+  if (max_elmts > 0 && (int)ra.size() > max_elmts) {
+    double row_sum = 0;
+    for (double x : ra) row_sum += x;
+    qsort2_abs(rj.data(), ra.data(), 0, (int)ra.size() - 1);
+    double scale = 0;
+    for (int k = 0; k < max_elmts; ++k) scale += ra[k];
+    rj.resize(max_elmts);
+    ra.resize(max_elmts);
+    if (scale != 0. && scale != row_sum) {
+      scale = row_sum / scale;
+      for (double& x : ra) x *= scale;
+    }
+  }
+  std::copy(rj.begin(), rj.end(), P.j.begin() + b);
+  std::copy(ra.begin(), ra.end(), P.a.begin() + b);
+  return (int)ra.size();
+}
+
 void truncate_rows(CSR& P, double tol, int max_elmts) {
   if (tol <= 0.0 && max_elmts == 0) return;
   const int n = P.nrows;
@@ -746,44 +785,7 @@ void truncate_rows(CSR& P, double tol, int max_elmts) {
     std::vector<int> rj;
     std::vector<double> ra;
 #pragma omp for schedule(static)
-    for (int r = 0; r < n; ++r) {
-      const int b = P.i[r], e = P.i[r + 1];
-      rj.assign(P.j.begin() + b, P.j.begin() + e);
-      ra.assign(P.a.begin() + b, P.a.begin() + e);
-      if (tol > 0) {
-        double row_nrm = 0;
-        for (double x : ra) row_nrm = (row_nrm < std::fabs(x)) ? std::fabs(x) : row_nrm;
-        const double drop = tol * row_nrm;
-        double row_sum = 0, scale = 0;
-        size_t o = 0;
-        for (size_t k = 0; k < ra.size(); ++k) {
-          row_sum += ra[k];
-          if (!(std::fabs(ra[k]) < drop)) { scale += ra[k]; rj[o] = rj[k]; ra[o] = ra[k]; ++o; }
-        }
-        rj.resize(o);
-        ra.resize(o);
-        if (scale != 0. && scale != row_sum) {
-          scale = row_sum / scale;
-          for (double& x : ra) x *= scale;
-        }
-      }
-      if (max_elmts > 0 && (int)ra.size() > max_elmts) {
-        double row_sum = 0;
-        for (double x : ra) row_sum += x;
-        qsort2_abs(rj.data(), ra.data(), 0, (int)ra.size() - 1);
-        double scale = 0;
-        for (int k = 0; k < max_elmts; ++k) scale += ra[k];
-        rj.resize(max_elmts);
-        ra.resize(max_elmts);
-        if (scale != 0. && scale != row_sum) {
-          scale = row_sum / scale;
-          for (double& x : ra) x *= scale;
-        }
-      }
-      std::copy(rj.begin(), rj.end(), P.j.begin() + b);
-      std::copy(ra.begin(), ra.end(), P.a.begin() + b);
-      newlen[r] = (int)ra.size();
-    }
+    for (int r = 0; r < n; ++r) newlen[r] = truncate_row(P, r, tol, max_elmts, rj, ra);
   }
   std::vector<int> ni(n + 1, 0);
   for (int r = 0; r < n; ++r) ni[r + 1] = ni[r] + newlen[r];
@@ -809,55 +811,119 @@ void truncate_rows(CSR& P, double tol, int max_elmts) {
 // are given for every universe point; rows of A and S are needed for the
 // computed rows and their strong F neighbours.  P's columns are global coarse
 // indices (ncoarse in all).
+// One row of extpi_core.  The reference's P_marker (one int per point) only
+// ever tells, for the row being built, whether a point is in its C-hat set
+// (marker = the entry's slot, >= jj_begin_row), one of its strong F
+// neighbours (marker = strong_f_marker) or neither (a stale value of an
+// earlier row); a per-row map (RowMap) answers the same three ways, so every
+// row's entries, their order and their sums are unchanged.
+static int64_t extpi_bound(const Pattern& S, int i) {
+  int64_t b = 1 + (S.i[i + 1] - S.i[i]);
+  for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) b += S.i[S.j[jj] + 1] - S.i[S.j[jj]];
+  return b;
+}
+// first pass (par_lr_interp.c:1290-1370): |C-hat_i|
+int extpi_row_count(const Pattern& S, const std::vector<int>& cf, int i, RowMap& M) {
+  int cnt = 0;
+  if (cf[i] >= 0) {
+    cnt = 1;
+  } else if (cf[i] != SF_PT) {
+    M.begin(extpi_bound(S, i));
+    bool fresh;
+    for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+      int i1 = S.j[jj];
+      if (cf[i1] >= 0) {
+        M.find_or_insert(i1, 0, &fresh);
+        cnt += fresh;
+      } else if (cf[i1] != SF_PT) {
+        for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+          int k1 = S.j[kk];
+          if (cf[k1] >= 0) {
+            M.find_or_insert(k1, 0, &fresh);
+            cnt += fresh;
+          }
+        }
+      }
+    }
+  }
+  return cnt;
+}
+// second pass: row i into P.j / P.a from P.i[i] on
+void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
+                    int i, RowMap& M, CSR& P) {
+  constexpr int kNone = -1, kStrongF = -2;
+  const int jj_begin_row = P.i[i];
+  int jc = jj_begin_row;
+  if (cf[i] >= 0) {
+    P.j[jc] = fine_to_coarse[i];
+    P.a[jc] = 1.0;
+    return;
+  }
+  if (cf[i] == SF_PT) return;
+  M.begin(extpi_bound(S, i));
+  bool fresh;
+  for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+    int i1 = S.j[jj];
+    if (cf[i1] >= 0) {
+      M.find_or_insert(i1, jc, &fresh);
+      if (fresh) { P.j[jc] = fine_to_coarse[i1]; P.a[jc] = 0.0; jc++; }
+    } else if (cf[i1] != SF_PT) {
+      *M.find_or_insert(i1, kStrongF, &fresh) = kStrongF;
+      for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+        int k1 = S.j[kk];
+        if (cf[k1] >= 0) {
+          M.find_or_insert(k1, jc, &fresh);
+          if (fresh) { P.j[jc] = fine_to_coarse[k1]; P.a[jc] = 0.0; jc++; }
+        }
+      }
+    }
+  }
+  const int jj_end_row = jc;
+  double diagonal = A.a[A.i[i]];
+  for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
+    int i1 = A.j[jj];
+    const int m1 = M.get(i1, kNone);
+    if (m1 >= 0) {
+      P.a[m1] += A.a[jj];
+    } else if (m1 == kStrongF) {
+      double sum = 0.0;
+      int sgn = 1;
+      if (A.a[A.i[i1]] < 0) sgn = -1;
+      for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
+        int i2 = A.j[jj1];
+        if ((M.get(i2, kNone) >= 0 || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
+      }
+      if (sum != 0) {
+        double distribute = A.a[jj] / sum;
+        for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
+          int i2 = A.j[jj1];
+          const int m2 = M.get(i2, kNone);
+          if (m2 >= 0 && (sgn * A.a[jj1]) < 0) P.a[m2] += distribute * A.a[jj1];
+          if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
+        }
+      } else {
+        diagonal += A.a[jj];
+      }
+    } else if (cf[i1] != SF_PT) {
+      diagonal += A.a[jj];
+    }
+  }
+  if (diagonal) {
+    for (int jj = jj_begin_row; jj < jj_end_row; ++jj) P.a[jj] /= -diagonal;
+  }
+}
+
 void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
                 int nrows, int ncoarse, int nuniv, CSR& P) {
-  // Row-parallel restatement.  The reference's P_marker (one int per point)
-  // only ever tells, for the row being built, whether a point is in its C-hat
-  // set (marker = the entry's slot, >= jj_begin_row), one of its strong F
-  // neighbours (marker = strong_f_marker) or neither (a stale value of an
-  // earlier row); a per-row map (RowMap) answers the same three ways, so every
-  // row's entries, their order and their sums are unchanged.
   (void)nuniv;
   const int n = nrows;
-  constexpr int kNone = -1, kStrongF = -2;
   P.resize_rows(n, ncoarse);
   std::vector<int> rowcnt(n, 0);
-  // upper bound of the points a row's C-hat search inserts
-  auto bound = [&](int i) {
-    int64_t b = 1 + (S.i[i + 1] - S.i[i]);
-    for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) b += S.i[S.j[jj] + 1] - S.i[S.j[jj]];
-    return b;
-  };
 #pragma omp parallel
   {
     RowMap M;
 #pragma omp for schedule(static)
-    for (int i = 0; i < n; ++i) {
-      // first pass (par_lr_interp.c:1290-1370): |C-hat_i|
-      int cnt = 0;
-      if (cf[i] >= 0) {
-        cnt = 1;
-      } else if (cf[i] != SF_PT) {
-        M.begin(bound(i));
-        bool fresh;
-        for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
-          int i1 = S.j[jj];
-          if (cf[i1] >= 0) {
-            M.find_or_insert(i1, 0, &fresh);
-            cnt += fresh;
-          } else if (cf[i1] != SF_PT) {
-            for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
-              int k1 = S.j[kk];
-              if (cf[k1] >= 0) {
-                M.find_or_insert(k1, 0, &fresh);
-                cnt += fresh;
-              }
-            }
-          }
-        }
-      }
-      rowcnt[i] = cnt;
-    }
+    for (int i = 0; i < n; ++i) rowcnt[i] = extpi_row_count(S, cf, i, M);
   }
   for (int i = 0; i < n; ++i) P.i[i + 1] = P.i[i] + rowcnt[i];
   const int64_t nnzP = P.i[n];
@@ -867,67 +933,7 @@ void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, cons
   {
     RowMap M;
 #pragma omp for schedule(static)
-    for (int i = 0; i < n; ++i) {
-      const int jj_begin_row = P.i[i];
-      int jc = jj_begin_row;
-      if (cf[i] >= 0) {
-        P.j[jc] = fine_to_coarse[i];
-        P.a[jc] = 1.0;
-        jc++;
-      } else if (cf[i] != SF_PT) {
-        M.begin(bound(i));
-        bool fresh;
-        for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
-          int i1 = S.j[jj];
-          if (cf[i1] >= 0) {
-            M.find_or_insert(i1, jc, &fresh);
-            if (fresh) { P.j[jc] = fine_to_coarse[i1]; P.a[jc] = 0.0; jc++; }
-          } else if (cf[i1] != SF_PT) {
-            *M.find_or_insert(i1, kStrongF, &fresh) = kStrongF;
-            for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
-              int k1 = S.j[kk];
-              if (cf[k1] >= 0) {
-                M.find_or_insert(k1, jc, &fresh);
-                if (fresh) { P.j[jc] = fine_to_coarse[k1]; P.a[jc] = 0.0; jc++; }
-              }
-            }
-          }
-        }
-        const int jj_end_row = jc;
-        double diagonal = A.a[A.i[i]];
-        for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
-          int i1 = A.j[jj];
-          const int m1 = M.get(i1, kNone);
-          if (m1 >= 0) {
-            P.a[m1] += A.a[jj];
-          } else if (m1 == kStrongF) {
-            double sum = 0.0;
-            int sgn = 1;
-            if (A.a[A.i[i1]] < 0) sgn = -1;
-            for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
-              int i2 = A.j[jj1];
-              if ((M.get(i2, kNone) >= 0 || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
-            }
-            if (sum != 0) {
-              double distribute = A.a[jj] / sum;
-              for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
-                int i2 = A.j[jj1];
-                const int m2 = M.get(i2, kNone);
-                if (m2 >= 0 && (sgn * A.a[jj1]) < 0) P.a[m2] += distribute * A.a[jj1];
-                if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
-              }
-            } else {
-              diagonal += A.a[jj];
-            }
-          } else if (cf[i1] != SF_PT) {
-            diagonal += A.a[jj];
-          }
-        }
-        if (diagonal) {
-          for (int jj = jj_begin_row; jj < jj_end_row; ++jj) P.a[jj] /= -diagonal;
-        }
-      }
-    }
+    for (int i = 0; i < n; ++i) extpi_row_fill(A, S, cf, fine_to_coarse, i, M, P);
   }
 }
 
@@ -1032,12 +1038,58 @@ void transpose(const CSR& A, CSR& AT) {
 // P's rows fine-universe and columns coarse-universe indices; row q of R is
 // coarse-universe point row_ic[q]; C's columns are coarse_glob[] of the
 // coarse-universe points (global coarse indices).
+// One row q of rap_core: the touch list tj / sums ta of C's row.  The
+// reference's A_marker / P_marker arrays (per point) answer "position of this
+// column in the row's touch list, or none" for the row being formed: a per-row
+// map (RowMap) gives the same answers, so the first-touch order and every sum
+// are unchanged.
+void rap_row(const CSR& R, const CSR& A, const CSR& P, int q, int ic, RapScratch& W) {
+  W.ra_j.clear();
+  W.ra_a.clear();
+  int64_t ba = 0;
+  for (int jj1 = R.i[q]; jj1 < R.i[q + 1]; ++jj1) ba += A.i[R.j[jj1] + 1] - A.i[R.j[jj1]];
+  W.AM.begin(ba);
+  bool fresh;
+  for (int jj1 = R.i[q]; jj1 < R.i[q + 1]; ++jj1) {
+    const int i1 = R.j[jj1];
+    const double r_entry = R.a[jj1];
+    for (int jj2 = A.i[i1]; jj2 < A.i[i1 + 1]; ++jj2) {
+      const int i2 = A.j[jj2];
+      int* m = W.AM.find_or_insert(i2, (int)W.ra_j.size(), &fresh);
+      if (fresh) {
+        W.ra_j.push_back(i2);
+        W.ra_a.push_back(r_entry * A.a[jj2]);
+      } else {
+        W.ra_a[*m] += r_entry * A.a[jj2];
+      }
+    }
+  }
+  W.tj.clear();
+  W.ta.clear();
+  int64_t bp = 1;
+  for (int i1 : W.ra_j) bp += P.i[i1 + 1] - P.i[i1];
+  W.PM.begin(bp);
+  W.PM.find_or_insert(ic, 0, &fresh);
+  W.tj.push_back(ic);
+  W.ta.push_back(0.0);
+  for (size_t k = 0; k < W.ra_j.size(); ++k) {
+    const int i1 = W.ra_j[k];
+    const double rap_ = W.ra_a[k];
+    for (int jj2 = P.i[i1]; jj2 < P.i[i1 + 1]; ++jj2) {
+      const int i2 = P.j[jj2];
+      int* m = W.PM.find_or_insert(i2, (int)W.tj.size(), &fresh);
+      if (fresh) {
+        W.tj.push_back(i2);
+        W.ta.push_back(rap_ * P.a[jj2]);
+      } else {
+        W.ta[*m] += rap_ * P.a[jj2];
+      }
+    }
+  }
+}
+
 void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& row_ic,
               const std::vector<int>& coarse_glob, int nfine_univ, int ncoarse_univ, int ncoarse_glob, CSR& C) {
-  // The reference's A_marker / P_marker arrays (per point) answer "position of
-  // this column in the row's touch list, or none" for the row being formed: a
-  // per-row map (RowMap) gives the same answers, so the first-touch order and
-  // every sum are unchanged.
   (void)nfine_univ;
   (void)ncoarse_univ;
   const int nc = R.nrows;
@@ -1052,65 +1104,17 @@ void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& 
     }
 #pragma omp parallel
     {
-      RowMap AM, PM;
-      std::vector<int> ra_j;
-      std::vector<double> ra_a;
-      ra_j.reserve(4096);
-      ra_a.reserve(4096);
-      std::vector<int> tj;
-      std::vector<double> ta;
+      RapScratch W;
 #pragma omp for schedule(dynamic, 256)
       for (int q = 0; q < nc; ++q) {
-        const int ic = row_ic[q];
-        ra_j.clear();
-        ra_a.clear();
-        int64_t ba = 0;
-        for (int jj1 = R.i[q]; jj1 < R.i[q + 1]; ++jj1) ba += A.i[R.j[jj1] + 1] - A.i[R.j[jj1]];
-        AM.begin(ba);
-        bool fresh;
-        for (int jj1 = R.i[q]; jj1 < R.i[q + 1]; ++jj1) {
-          const int i1 = R.j[jj1];
-          const double r_entry = R.a[jj1];
-          for (int jj2 = A.i[i1]; jj2 < A.i[i1 + 1]; ++jj2) {
-            const int i2 = A.j[jj2];
-            int* m = AM.find_or_insert(i2, (int)ra_j.size(), &fresh);
-            if (fresh) {
-              ra_j.push_back(i2);
-              ra_a.push_back(r_entry * A.a[jj2]);
-            } else {
-              ra_a[*m] += r_entry * A.a[jj2];
-            }
-          }
-        }
-        tj.clear();
-        ta.clear();
-        int64_t bp = 1;
-        for (int i1 : ra_j) bp += P.i[i1 + 1] - P.i[i1];
-        PM.begin(bp);
-        PM.find_or_insert(ic, 0, &fresh);
-        tj.push_back(ic);
-        ta.push_back(0.0);
-        for (size_t k = 0; k < ra_j.size(); ++k) {
-          const int i1 = ra_j[k];
-          const double rap_ = ra_a[k];
-          for (int jj2 = P.i[i1]; jj2 < P.i[i1 + 1]; ++jj2) {
-            const int i2 = P.j[jj2];
-            int* m = PM.find_or_insert(i2, (int)tj.size(), &fresh);
-            if (fresh) {
-              tj.push_back(i2);
-              ta.push_back(rap_ * P.a[jj2]);
-            } else {
-              ta[*m] += rap_ * P.a[jj2];
-            }
-          }
-        }
+        rap_row(R, A, P, q, row_ic[q], W);
         if (pass == 0) {
-          rowlen[q] = (int)tj.size();
+          rowlen[q] = (int)W.tj.size();
         } else {
           int o = C.i[q];
-          for (size_t k = 0; k < tj.size(); ++k, ++o) {
-            C.j[o] = coarse_glob.empty() ? tj[k] : coarse_glob[tj[k]];
-            C.a[o] = ta[k];
+          for (size_t k = 0; k < W.tj.size(); ++k, ++o) {
+            C.j[o] = coarse_glob.empty() ? W.tj[k] : coarse_glob[W.tj[k]];
+            C.a[o] = W.ta[k];
           }
         }
       }
