@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -80,6 +81,8 @@ struct hypre_Solver_struct {
   // local rows, resolved at Setup (hypre's CPU path uses its OpenMP thread
   // count; a single block would run each sweep in one workgroup)
   bool auto_blocks = true;
+  // Setup's ext+i, truncation, R = P^T and RAP on the GPU (hypreve_BoomerAMGSetDeviceSetup)
+  bool device_setup = true;
   std::vector<int> gs_rank_starts;  // one GPU emulating the GS blocks of an N-rank run
   std::vector<int> rank_emul;       // one process emulating a reference N-rank setup (SetRankEmulation)
   // per level: those blocks and their l1 norms (host copies for the introspection calls)
@@ -868,8 +871,21 @@ HYPRE_Int hypreve_BoomerAMGSetupHost(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   CHECK_ARG(A, 2);
   API_BEGIN
   resolve_blocks(s, A->n);
+  s->prm.device_setup = 0;  // host only: the reference functions of the device setup
   setup_one_process(s, A);
   API_END
+}
+
+HYPRE_Int hypreve_BoomerAMGSetDeviceSetup(HYPRE_Solver s, HYPRE_Int on) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  s->device_setup = on != 0;
+  return 0;
+}
+
+HYPRE_Int hypreve_BoomerAMGGetSetupLog(HYPRE_Solver s, char* buf, HYPRE_Int len) {
+  CHECK_ARG(s && s->kind == KIND_AMG && buf && len > 0, 1);
+  snprintf(buf, (size_t)len, "%s", s->H.log.c_str());
+  return 0;
 }
 
 }  // extern "C"
@@ -1123,16 +1139,27 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
   API_BEGIN
   s->comm = A->comm;
   resolve_blocks(s, A->n);
+  s->prm.device_setup = s->device_setup ? 1 : 0;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = now();
   if (A->multi()) {
     if (use_dist_setup(s->prm)) setup_dist(s, A);
     else setup_multi(s, A);
   } else {
     setup_one_process(s, A);
-    single_rank_hierarchy(s->H, s->RH, s->gs_rank_starts.empty() ? nullptr : &s->gs_rank_starts);
   }
+  const double t1 = now();
+  if (!A->multi()) single_rank_hierarchy(s->H, s->RH, s->gs_rank_starts.empty() ? nullptr : &s->gs_rank_starts);
+  const double t2 = now();
   if (!s->dev) s->dev.reset(new DevAMG);
   s->dev->build(s->RH, A->multi() ? A->comm->dc.get() : nullptr);
   s->dev->set_use_graph(s->use_graph);
+  const double t3 = now();
+  char tb[160];
+  snprintf(tb, sizeof tb, "setup: hierarchy %.3fs, rank partition %.3fs, device layouts and upload %.3fs\n", t1 - t0,
+           t2 - t1, t3 - t2);
+  s->H.log += tb;
+  if (s->prm.print_level > 0) fputs(tb, stderr);
   API_END
 }
 
@@ -1219,7 +1246,7 @@ HYPRE_Int hypreve_BoomerAMGGetLevelMatrix(HYPRE_Solver s, HYPRE_Int level, HYPRE
                                           HYPRE_Real* vals) {
   CHECK_ARG(s && level >= 0 && level < (int)s->H.lev.size(), 2);
   const Level& L = s->H.lev[level];
-  const CSR& M = which == 0 ? L.A : L.P;
+  const CSR& M = which == 0 ? L.A : which == 1 ? L.P : L.R;
   if (nrows) *nrows = M.nrows;
   if (ncols) *ncols = M.ncols;
   if (nnz) *nnz = M.nnz();

@@ -98,7 +98,9 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const
                             hipStream_t st);
 int sell_batch_override();
 // Tuning knobs read at launch (0 = default): 0 offset-coded row blocks per
-// step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU.
+// step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU,
+// 3 stream-mix access width (2: 16 B), 7 caps the device setup's LDS tables
+// at 2^v slots (tests of its host fallback).
 void set_knob(int id, int v);
 int knob(int id);
 int stencil_slices_per_wave();

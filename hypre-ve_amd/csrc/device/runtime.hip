@@ -3,6 +3,7 @@
 // arithmetic step runs in a HIP kernel (kernels.hip) -- there is no host path.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdio>
@@ -833,7 +834,10 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   std::vector<std::vector<int64_t>> keys_r;
   if (nbands_r_env != nbands_env) locality_keys(R, agg_level_, nbands_r_env, keys_r);
   const std::vector<std::vector<int64_t>>& kr = nbands_r_env != nbands_env ? keys_r : keys;
+  const bool tlog = getenv("HVE_SETUP_T") != nullptr;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   for (int l = 0; l < nl; ++l) {
+    const double tl0 = now();
     const RankLevel& L = R.lev[l];
     DevLevel& D = lev_[l];
     D.n = L.n_loc;
@@ -900,6 +904,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       D.cheby_o = dalloc<double>(D.n);
       HVE_HIP(hipMemset(D.cheby_t, 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
     }
+    if (tlog) fprintf(stderr, "[build] level %d: %.3fs (A %s)\n", l, now() - tl0, D.A.in.slot_mask ? "stencil" : "");
   }
   // Hybrid Gauss-Seidel schedules for the relax types the cycle uses
   // (num_blocks = hypre's thread count: row blocks of each level).

@@ -1,0 +1,715 @@
+// Device setup kernels: the heavy row loops of the BoomerAMG setup
+// (ext+i interpolation, its truncation, R = P^T and the Galerkin product RAP)
+// run on the GPU, byte for byte what the host functions of host/setup.cpp
+// produce.
+//
+// Each row of ext+i and RAP is an ordered first-touch list with sums formed in
+// a fixed order, so one lane restates the host row function verbatim: one row
+// per wavefront, lane 0 does the row's work, and the per-row marker map (the
+// reference's P_marker / A_marker arrays, host RowMap) is an open-addressing
+// table in the wave's LDS with generation stamps (no clearing between rows).
+// Thousands of rows run at once, each an L1/LDS-latency chain, which is what
+// makes the device versions fast: the host's rows are cache-miss chains into
+// multi-GB arrays.  A row whose table would overflow its LDS capacity is
+// flagged and finished by the host's own row function (setup.cpp), so every
+// row is exact either way.  Truncation (par_csr_matrix.c:2671) runs one row
+// per lane with the row in private memory; the quicksort partitions of
+// qsort2_abs (hypre_qsort.c:367) are replayed from an explicit stack: the
+// subranges are disjoint, so the order they are processed in does not change
+// the result.  R = P^T is a stable radix sort of P's entries by column
+// (rows stay ascending inside a column, as in the counting-sort transpose).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../host/setup_dev.hpp"
+#include "kernels.h"
+
+namespace hve {
+
+namespace {
+
+void ck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("device setup: HIP error '") + hipGetErrorString(e) + "' in " + what);
+}
+#define SDV(x) ck((x), #x)
+
+template <typename T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  DBuf() = default;
+  explicit DBuf(size_t m) { alloc(m); }
+  void alloc(size_t m) {
+    free();
+    n = m;
+    SDV(hipMalloc((void**)&p, std::max<size_t>(1, m) * sizeof(T)));
+  }
+  void up(const std::vector<T>& h) {
+    alloc(h.size());
+    if (!h.empty()) SDV(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
+  }
+  void down(std::vector<T>& h, size_t m) const {
+    h.resize(m);
+    if (m) SDV(hipMemcpy(h.data(), p, m * sizeof(T), hipMemcpyDeviceToHost));
+  }
+  void free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DBuf() { free(); }
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+};
+
+struct DCsr {
+  const int* i;
+  const int* j;
+  const double* a;
+  int n;
+};
+
+struct DevCSR {
+  DBuf<int> i, j;
+  DBuf<double> a;
+  int n = 0, ncols = 0;
+  void up(const CSR& h) {
+    n = h.nrows;
+    ncols = h.ncols;
+    i.up(h.i);
+    j.up(h.j);
+    a.up(h.a);
+  }
+  DCsr view() const { return DCsr{i.p, j.p, a.p, n}; }
+};
+
+long long g_host_rows = 0;
+
+// Open-addressing map in LDS, one per wavefront, used by lane 0 only.
+struct LMap {
+  int* key;
+  int* val;
+  int* gen;
+  unsigned mask;
+  int shift;
+  int cur;
+  int count;
+  int limit;  // at most cap/2 keys: beyond that the row overflows
+  __device__ void init(int* base, int cap, int lg) {
+    key = base;
+    val = base + cap;
+    gen = base + 2 * cap;
+    mask = (unsigned)cap - 1;
+    shift = 32 - lg;
+    cur = 0;
+    limit = cap / 2;
+  }
+  __device__ void begin() {
+    ++cur;
+    count = 0;
+  }
+  // slot of k; inserted with v0 when absent (fresh); nullptr on overflow
+  __device__ int* find_or_insert(int k, int v0, bool& fresh) {
+    unsigned h = ((unsigned)k * 2654435761u) >> shift;
+    for (;; h = (h + 1) & mask) {
+      if (gen[h] != cur) {
+        if (count >= limit) return nullptr;
+        ++count;
+        gen[h] = cur;
+        key[h] = k;
+        val[h] = v0;
+        fresh = true;
+        return &val[h];
+      }
+      if (key[h] == k) {
+        fresh = false;
+        return &val[h];
+      }
+    }
+  }
+  __device__ int get(int k, int dflt) const {
+    unsigned h = ((unsigned)k * 2654435761u) >> shift;
+    for (;; h = (h + 1) & mask) {
+      if (gen[h] != cur) return dflt;
+      if (key[h] == k) return val[h];
+    }
+  }
+};
+
+__device__ __forceinline__ void lds_zero(int* p, int n) {
+  for (int t = threadIdx.x; t < n; t += blockDim.x) p[t] = 0;
+  __syncthreads();
+}
+
+constexpr int kSF = -3;  // SF_PT
+
+// ---------------------------------------------------------------------------
+// Ext+i rows (setup.cpp extpi_row_count / extpi_row_fill, par_lr_interp.c:1041).
+// COUNT: rowcnt[i] = |C-hat_i| (-1: overflow).  FILL: P.j / P.a of rows
+// with rowcnt >= 0, from Pi[i] on.
+// LDS: map (3 x cap ints) + the row's values (cap/2 doubles).
+// ---------------------------------------------------------------------------
+template <bool FILL>
+__global__ void __launch_bounds__(64) k_extpi(DCsr A, DCsr S, const int* __restrict__ cf,
+                                              const int* __restrict__ f2c, int n, int cap, int lg,
+                                              int* __restrict__ rowcnt, const int* __restrict__ Pi,
+                                              int* __restrict__ Pj, double* __restrict__ Pa) {
+  extern __shared__ int lds[];
+  lds_zero(lds + 2 * cap, cap);  // generation stamps
+  if (threadIdx.x != 0) return;
+  LMap M;
+  M.init(lds, cap, lg);
+  double* pa = reinterpret_cast<double*>(lds + 3 * cap);  // cap/2 doubles (8-aligned: cap is a power of 2)
+  constexpr int kNone = -1, kStrongF = -2;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int ci = cf[i];
+    if (!FILL) {
+      int cnt = 0;
+      if (ci >= 0) {
+        cnt = 1;
+      } else if (ci != kSF) {
+        // the same insertions as the fill pass (strong F neighbours too), so a
+        // row that fits here fits there
+        M.begin();
+        bool fresh, ovf = false;
+        for (int jj = S.i[i]; jj < S.i[i + 1] && !ovf; ++jj) {
+          const int i1 = S.j[jj];
+          const int c1 = cf[i1];
+          if (c1 >= 0) {
+            if (!M.find_or_insert(i1, 0, fresh)) ovf = true;
+            else cnt += fresh;
+          } else if (c1 != kSF) {
+            if (!M.find_or_insert(i1, kStrongF, fresh)) { ovf = true; break; }
+            for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+              const int k1 = S.j[kk];
+              if (cf[k1] >= 0) {
+                if (!M.find_or_insert(k1, 0, fresh)) { ovf = true; break; }
+                cnt += fresh;
+              }
+            }
+          }
+        }
+        if (ovf) cnt = -1;
+      }
+      rowcnt[i] = cnt;
+      continue;
+    }
+    if (rowcnt[i] < 0) continue;  // finished on the host
+    const int jb = Pi[i];
+    if (ci >= 0) {
+      Pj[jb] = f2c[i];
+      Pa[jb] = 1.0;
+      continue;
+    }
+    if (ci == kSF) continue;
+    M.begin();
+    int jc = 0;  // slot relative to jb
+    bool fresh;
+    for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+      const int i1 = S.j[jj];
+      const int c1 = cf[i1];
+      if (c1 >= 0) {
+        M.find_or_insert(i1, jc, fresh);  // fits: the count pass saw the same keys
+        if (fresh) { Pj[jb + jc] = f2c[i1]; pa[jc] = 0.0; jc++; }
+      } else if (c1 != kSF) {
+        *M.find_or_insert(i1, kStrongF, fresh) = kStrongF;
+        for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+          const int k1 = S.j[kk];
+          if (cf[k1] >= 0) {
+            M.find_or_insert(k1, jc, fresh);
+            if (fresh) { Pj[jb + jc] = f2c[k1]; pa[jc] = 0.0; jc++; }
+          }
+        }
+      }
+    }
+    const int jend = jc;
+    double diagonal = A.a[A.i[i]];
+    for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
+      const int i1 = A.j[jj];
+      const int m1 = M.get(i1, kNone);
+      if (m1 >= 0) {
+        pa[m1] += A.a[jj];
+      } else if (m1 == kStrongF) {
+        double sum = 0.0;
+        int sgn = 1;
+        if (A.a[A.i[i1]] < 0) sgn = -1;
+        for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
+          const int i2 = A.j[jj1];
+          if ((M.get(i2, kNone) >= 0 || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
+        }
+        if (sum != 0) {
+          const double distribute = A.a[jj] / sum;
+          for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
+            const int i2 = A.j[jj1];
+            const int m2 = M.get(i2, kNone);
+            if (m2 >= 0 && (sgn * A.a[jj1]) < 0) pa[m2] += distribute * A.a[jj1];
+            if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
+          }
+        } else {
+          diagonal += A.a[jj];
+        }
+      } else if (cf[i1] != kSF) {
+        diagonal += A.a[jj];
+      }
+    }
+    if (diagonal) {
+      for (int k = 0; k < jend; ++k) pa[k] /= -diagonal;
+    }
+    for (int k = 0; k < jend; ++k) Pa[jb + k] = pa[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Truncation of one row per lane (setup.cpp truncate_row): in place inside
+// the row's slots, newlen[r] = kept entries (-1: row longer than kTrMax,
+// finished on the host).
+// ---------------------------------------------------------------------------
+constexpr int kTrMax = 64;
+__global__ void __launch_bounds__(256) k_truncate(int n, const int* __restrict__ Pi, int* __restrict__ Pj,
+                                                  double* __restrict__ Pa, double tol, int max_elmts,
+                                                  int* __restrict__ newlen) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  const int b = Pi[r], e = Pi[r + 1];
+  int len = e - b;
+  if (len > kTrMax) {
+    newlen[r] = -1;
+    return;
+  }
+  int rj[kTrMax];
+  double ra[kTrMax];
+  for (int k = 0; k < len; ++k) {
+    rj[k] = Pj[b + k];
+    ra[k] = Pa[b + k];
+  }
+  if (tol > 0) {
+    double row_nrm = 0;
+    for (int k = 0; k < len; ++k) row_nrm = (row_nrm < fabs(ra[k])) ? fabs(ra[k]) : row_nrm;
+    const double drop = tol * row_nrm;
+    double row_sum = 0, scale = 0;
+    int o = 0;
+    for (int k = 0; k < len; ++k) {
+      row_sum += ra[k];
+      if (!(fabs(ra[k]) < drop)) { scale += ra[k]; rj[o] = rj[k]; ra[o] = ra[k]; ++o; }
+    }
+    len = o;
+    if (scale != 0. && scale != row_sum) {
+      scale = row_sum / scale;
+      for (int k = 0; k < len; ++k) ra[k] *= scale;
+    }
+  }
+  if (max_elmts > 0 && len > max_elmts) {
+    double row_sum = 0;
+    for (int k = 0; k < len; ++k) row_sum += ra[k];
+    // qsort2_abs (descending |w|), its partitions replayed from a stack
+    int stk[4 * kTrMax + 4];
+    int sp = 0;
+    stk[sp++] = 0;
+    stk[sp++] = len - 1;
+    while (sp > 0) {
+      const int right = stk[--sp];
+      const int left = stk[--sp];
+      if (left >= right) continue;
+      {
+        const int m = (left + right) / 2;
+        const int tv = rj[left]; rj[left] = rj[m]; rj[m] = tv;
+        const double tw = ra[left]; ra[left] = ra[m]; ra[m] = tw;
+      }
+      int last = left;
+      for (int k = left + 1; k <= right; ++k)
+        if (fabs(ra[k]) > fabs(ra[left])) {
+          ++last;
+          const int tv = rj[last]; rj[last] = rj[k]; rj[k] = tv;
+          const double tw = ra[last]; ra[last] = ra[k]; ra[k] = tw;
+        }
+      {
+        const int tv = rj[left]; rj[left] = rj[last]; rj[last] = tv;
+        const double tw = ra[left]; ra[left] = ra[last]; ra[last] = tw;
+      }
+      stk[sp++] = left;
+      stk[sp++] = last - 1;
+      stk[sp++] = last + 1;
+      stk[sp++] = right;
+    }
+    double scale = 0;
+    for (int k = 0; k < max_elmts; ++k) scale += ra[k];
+    len = max_elmts;
+    if (scale != 0. && scale != row_sum) {
+      scale = row_sum / scale;
+      for (int k = 0; k < len; ++k) ra[k] *= scale;
+    }
+  }
+  for (int k = 0; k < len; ++k) {
+    Pj[b + k] = rj[k];
+    Pa[b + k] = ra[k];
+  }
+  newlen[r] = len;
+}
+
+// compacted copy of the kept entries: row r's newlen[r] first slots
+__global__ void __launch_bounds__(256) k_compact(int n, const int* __restrict__ Pi, const int* __restrict__ Pj,
+                                                 const double* __restrict__ Pa, const int* __restrict__ Ni,
+                                                 int* __restrict__ Nj, double* __restrict__ Na) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  const int b = Pi[r], o = Ni[r], len = Ni[r + 1] - Ni[r];
+  for (int k = 0; k < len; ++k) {
+    Nj[o + k] = Pj[b + k];
+    Na[o + k] = Pa[b + k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Transpose helpers: row of every entry, column counts, gather of values.
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) k_entry_rows(int n, const int* __restrict__ Pi, int* __restrict__ rowof) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  for (int k = Pi[r]; k < Pi[r + 1]; ++k) rowof[k] = r;
+}
+__global__ void __launch_bounds__(256) k_iota(int64_t n, int* __restrict__ v) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < n) v[k] = (int)k;
+}
+__global__ void __launch_bounds__(256) k_col_count(int64_t nnz, const int* __restrict__ Pj, int* __restrict__ cnt) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k < nnz) atomicAdd(&cnt[Pj[k]], 1);
+}
+__global__ void __launch_bounds__(256) k_transpose_fill(int64_t nnz, const int* __restrict__ perm,
+                                                        const int* __restrict__ rowof, const double* __restrict__ Pa,
+                                                        int* __restrict__ Rj, double* __restrict__ Ra) {
+  const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= nnz) return;
+  const int e = perm[k];
+  Rj[k] = rowof[e];
+  Ra[k] = Pa[e];
+}
+
+// ---------------------------------------------------------------------------
+// Galerkin rows (setup.cpp rap_row, par_rap.c:27): C row q from R row q,
+// the RA row (first touch over A's columns) and then RA * P (first touch over
+// P's columns, the diagonal ic = q first).  COUNT: rowlen[q] (-1: overflow);
+// FILL: C.j / C.a from Ci[q].  LDS: map1 (3 x cap1) + RA list (cap1/2 ints +
+// doubles) + map2 (3 x cap2) + the row's values (cap2/2 doubles).
+// ---------------------------------------------------------------------------
+template <bool FILL>
+__global__ void __launch_bounds__(64) k_rap(DCsr R, DCsr A, DCsr P, int cap1, int lg1, int cap2, int lg2,
+                                            int* __restrict__ rowlen, const int* __restrict__ Ci,
+                                            int* __restrict__ Cj, double* __restrict__ Ca) {
+  extern __shared__ int lds[];
+  int* m1 = lds;
+  int* m2 = m1 + 3 * cap1;
+  lds_zero(m1 + 2 * cap1, cap1);
+  lds_zero(m2 + 2 * cap2, cap2);
+  if (threadIdx.x != 0) return;
+  int* raj = m2 + 3 * cap2;                                        // cap1/2 ints
+  double* raa = reinterpret_cast<double*>(raj + cap1 / 2);         // cap1/2 doubles
+  double* ta = raa + cap1 / 2;                                     // cap2/2 doubles
+  LMap M1, M2;
+  M1.init(m1, cap1, lg1);
+  M2.init(m2, cap2, lg2);
+  for (int q = blockIdx.x; q < R.n; q += gridDim.x) {
+    if (FILL && rowlen[q] < 0) continue;  // finished on the host
+    M1.begin();
+    int nra = 0;
+    bool fresh, ovf = false;
+    for (int jj1 = R.i[q]; jj1 < R.i[q + 1] && !ovf; ++jj1) {
+      const int i1 = R.j[jj1];
+      const double r_entry = R.a[jj1];
+      for (int jj2 = A.i[i1]; jj2 < A.i[i1 + 1]; ++jj2) {
+        const int i2 = A.j[jj2];
+        int* m = M1.find_or_insert(i2, nra, fresh);
+        if (!m) { ovf = true; break; }
+        if (fresh) {
+          raj[nra] = i2;
+          if (FILL) raa[nra] = r_entry * A.a[jj2];
+          ++nra;
+        } else if (FILL) {
+          raa[*m] += r_entry * A.a[jj2];
+        }
+      }
+    }
+    int ntj = 0;
+    if (!ovf) {
+      M2.begin();
+      M2.find_or_insert(q, 0, fresh);
+      const int cb = FILL ? Ci[q] : 0;
+      if (FILL) {
+        Cj[cb] = q;
+        ta[0] = 0.0;
+      }
+      ntj = 1;
+      for (int k = 0; k < nra && !ovf; ++k) {
+        const int i1 = raj[k];
+        const double rap_ = FILL ? raa[k] : 0.0;
+        for (int jj2 = P.i[i1]; jj2 < P.i[i1 + 1]; ++jj2) {
+          const int i2 = P.j[jj2];
+          int* m = M2.find_or_insert(i2, ntj, fresh);
+          if (!m) { ovf = true; break; }
+          if (fresh) {
+            if (FILL) {
+              Cj[cb + ntj] = i2;
+              ta[ntj] = rap_ * P.a[jj2];
+            }
+            ++ntj;
+          } else if (FILL) {
+            ta[*m] += rap_ * P.a[jj2];
+          }
+        }
+      }
+      if (FILL)
+        for (int k = 0; k < ntj; ++k) Ca[cb + k] = ta[k];
+    }
+    if (!FILL) rowlen[q] = ovf ? -1 : ntj;
+  }
+}
+
+int lg2_ceil(int64_t v) {
+  int lg = 4;
+  while ((int64_t(1) << lg) < v) ++lg;
+  return lg;
+}
+
+void exclusive_scan(const int* d_in, int* d_out, int n) {
+  size_t tmp = 0;
+  SDV(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, d_in, d_out, n));
+  DBuf<char> t(tmp);
+  SDV(hipcub::DeviceScan::ExclusiveSum(t.p, tmp, d_in, d_out, n));
+}
+
+// Row pointers from per-row counts (device), with the host copy.
+void row_ptr(const DBuf<int>& cnt, int n, DBuf<int>& ptr, std::vector<int>& hptr) {
+  ptr.alloc((size_t)n + 1);
+  std::vector<int> hc;
+  cnt.down(hc, n);
+  hptr.assign((size_t)n + 1, 0);
+  int64_t t = 0;
+  for (int r = 0; r < n; ++r) {
+    hptr[r] = (int)t;
+    t += hc[r];
+  }
+  if (t > 0x7fffffffLL) throw std::runtime_error("device setup: more than 2^31 entries");
+  hptr[n] = (int)t;
+  SDV(hipMemcpy(ptr.p, hptr.data(), hptr.size() * sizeof(int), hipMemcpyHostToDevice));
+}
+
+int grid_rows(int n, int waves_per_cu) { return std::max(1, std::min(n, 256 * waves_per_cu)); }
+
+}  // namespace
+
+long long dev_setup_host_rows() { return g_host_rows; }
+
+void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf,
+                      const std::vector<int>& fine_to_coarse, int ncoarse, double trunc_factor, int max_elmts,
+                      CSR& P) {
+  g_host_rows = 0;
+  const int n = A.nrows;
+  P.resize_rows(n, ncoarse);
+  if (n == 0) return;
+  DevCSR dA;
+  dA.up(A);
+  DBuf<int> Si, Sj, dcf, df2c;
+  Si.up(S.i);
+  Sj.up(S.j);
+  dcf.up(cf);
+  df2c.up(fine_to_coarse);
+  const DCsr dS{Si.p, Sj.p, nullptr, S.n};
+  // table capacity from the largest candidate count of a row (capped; rows
+  // beyond it overflow to the host)
+  const int64_t bmax = extpi_bound_max(S);
+  // <= 2048 slots: 24 KiB + 8 KiB of values (knob 7 lowers the cap: tests of the host fallback)
+  const int lg = std::min(lg2_ceil(2 * bmax + 2), knob(7) > 0 ? std::min(knob(7), 11) : 11);
+  const int cap = 1 << lg;
+  const size_t lds = (size_t)3 * cap * sizeof(int) + (size_t)(cap / 2) * sizeof(double);
+  DBuf<int> cnt(n);
+  const int grid = grid_rows(n, 32);
+  hipLaunchKernelGGL((k_extpi<false>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
+                     nullptr, nullptr, nullptr);
+  SDV(hipGetLastError());
+  // rows that overflowed: counted on the host
+  std::vector<int> hc;
+  cnt.down(hc, n);
+  std::vector<int> ovf;
+  for (int i = 0; i < n; ++i)
+    if (hc[i] < 0) ovf.push_back(i);
+  if (!ovf.empty()) extpi_count_rows(S, cf, ovf, hc);
+  std::vector<int> hp((size_t)n + 1, 0);
+  int64_t t = 0;
+  for (int i = 0; i < n; ++i) {
+    hp[i] = (int)t;
+    t += hc[i];
+  }
+  if (t > 0x7fffffffLL) throw std::runtime_error("device setup: interpolation exceeds 2^31 entries");
+  hp[n] = (int)t;
+  DBuf<int> Pi, Pj((size_t)t);
+  DBuf<double> Pa((size_t)t);
+  Pi.up(hp);
+  // the count buffer keeps -1 on overflow rows: the fill pass skips them
+  hipLaunchKernelGGL((k_extpi<true>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
+                     Pi.p, Pj.p, Pa.p);
+  SDV(hipGetLastError());
+  dA.i.free();
+  dA.j.free();
+  dA.a.free();
+  Si.free();
+  Sj.free();
+  const bool trunc = trunc_factor != 0.0 || max_elmts > 0;
+  if (!trunc) {
+    P.i = hp;
+    Pj.down(P.j, (size_t)t);
+    Pa.down(P.a, (size_t)t);
+    if (!ovf.empty()) extpi_fill_rows(A, S, cf, fine_to_coarse, ovf, P);
+    g_host_rows = (long long)ovf.size();
+    return;
+  }
+  // overflow rows: filled on the host into the device arrays before truncation
+  if (!ovf.empty()) {
+    CSR part;
+    part.resize_rows(n, ncoarse);
+    part.i = hp;
+    part.j.assign((size_t)t, 0);
+    part.a.assign((size_t)t, 0.0);
+    extpi_fill_rows(A, S, cf, fine_to_coarse, ovf, part);
+    for (int i : ovf) {
+      const int b = hp[i], len = hp[i + 1] - hp[i];
+      if (len == 0) continue;
+      SDV(hipMemcpy(Pj.p + b, part.j.data() + b, len * sizeof(int), hipMemcpyHostToDevice));
+      SDV(hipMemcpy(Pa.p + b, part.a.data() + b, len * sizeof(double), hipMemcpyHostToDevice));
+    }
+  }
+  DBuf<int> nl(n);
+  hipLaunchKernelGGL(k_truncate, dim3((n + 255) / 256), dim3(256), 0, 0, n, Pi.p, Pj.p, Pa.p, trunc_factor, max_elmts,
+                     nl.p);
+  SDV(hipGetLastError());
+  std::vector<int> hl;
+  nl.down(hl, n);
+  std::vector<int> longrows;
+  for (int i = 0; i < n; ++i)
+    if (hl[i] < 0) longrows.push_back(i);
+  if (!longrows.empty()) {  // rows longer than the kernel's private arrays
+    CSR part;
+    part.resize_rows(n, ncoarse);
+    part.i = hp;
+    part.j.assign((size_t)t, 0);
+    part.a.assign((size_t)t, 0.0);
+    for (int i : longrows) {
+      const int b = hp[i], len = hp[i + 1] - hp[i];
+      SDV(hipMemcpy(part.j.data() + b, Pj.p + b, len * sizeof(int), hipMemcpyDeviceToHost));
+      SDV(hipMemcpy(part.a.data() + b, Pa.p + b, len * sizeof(double), hipMemcpyDeviceToHost));
+    }
+    truncate_row_list(part, longrows, trunc_factor, max_elmts, hl);
+    for (int i : longrows) {
+      const int b = hp[i], len = hl[i];
+      SDV(hipMemcpy(Pj.p + b, part.j.data() + b, len * sizeof(int), hipMemcpyHostToDevice));
+      SDV(hipMemcpy(Pa.p + b, part.a.data() + b, len * sizeof(double), hipMemcpyHostToDevice));
+    }
+  }
+  std::vector<int> ni((size_t)n + 1, 0);
+  for (int i = 0; i < n; ++i) ni[i + 1] = ni[i] + hl[i];
+  DBuf<int> Ni, Nj((size_t)ni[n]);
+  DBuf<double> Na((size_t)ni[n]);
+  Ni.up(ni);
+  hipLaunchKernelGGL(k_compact, dim3((n + 255) / 256), dim3(256), 0, 0, n, Pi.p, Pj.p, Pa.p, Ni.p, Nj.p, Na.p);
+  SDV(hipGetLastError());
+  P.i = ni;
+  Nj.down(P.j, (size_t)ni[n]);
+  Na.down(P.a, (size_t)ni[n]);
+  g_host_rows = (long long)(ovf.size() + longrows.size());
+}
+
+void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
+  g_host_rows = 0;
+  const int nf = P.nrows, nc = P.ncols;
+  const int64_t nnzp = P.nnz();
+  DevCSR dP, dA;
+  dP.up(P);
+  dA.up(A);
+  // R = P^T: a stable radix sort of the entries by column keeps every
+  // column's rows ascending (transpose's counting sort)
+  DBuf<int> rowof((size_t)nnzp), perm_in((size_t)nnzp), keys_out((size_t)nnzp), perm((size_t)nnzp);
+  hipLaunchKernelGGL(k_entry_rows, dim3((nf + 255) / 256), dim3(256), 0, 0, nf, dP.i.p, rowof.p);
+  hipLaunchKernelGGL(k_iota, dim3((unsigned)((nnzp + 255) / 256)), dim3(256), 0, 0, nnzp, perm_in.p);
+  SDV(hipGetLastError());
+  {
+    int bits = 1;
+    while ((1LL << bits) < (int64_t)std::max(nc, 2)) ++bits;
+    size_t tmp = 0;
+    SDV(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp, dP.j.p, keys_out.p, perm_in.p, perm.p, (int)nnzp, 0, bits));
+    DBuf<char> t(tmp);
+    SDV(hipcub::DeviceRadixSort::SortPairs(t.p, tmp, dP.j.p, keys_out.p, perm_in.p, perm.p, (int)nnzp, 0, bits));
+  }
+  perm_in.free();
+  keys_out.free();
+  DBuf<int> ccnt((size_t)nc + 1), Ri((size_t)nc + 1);
+  SDV(hipMemset(ccnt.p, 0, ((size_t)nc + 1) * sizeof(int)));
+  hipLaunchKernelGGL(k_col_count, dim3((unsigned)((nnzp + 255) / 256)), dim3(256), 0, 0, nnzp, dP.j.p, ccnt.p);
+  exclusive_scan(ccnt.p, Ri.p, nc + 1);
+  DBuf<int> Rj((size_t)nnzp);
+  DBuf<double> Ra((size_t)nnzp);
+  hipLaunchKernelGGL(k_transpose_fill, dim3((unsigned)((nnzp + 255) / 256)), dim3(256), 0, 0, nnzp, perm.p, rowof.p,
+                     dP.a.p, Rj.p, Ra.p);
+  SDV(hipGetLastError());
+  perm.free();
+  rowof.free();
+  ccnt.free();
+  Rh.resize_rows(nc, nf);
+  Ri.down(Rh.i, (size_t)nc + 1);
+  Rj.down(Rh.j, (size_t)nnzp);
+  Ra.down(Rh.a, (size_t)nnzp);
+  // table capacities from the largest products of a row (rows beyond: host)
+  const int64_t b1 = rap_bound_max(Rh, A);
+  int64_t pmax = 1;
+  for (int r = 0; r < nf; ++r) pmax = std::max<int64_t>(pmax, P.i[r + 1] - P.i[r]);
+  const int lgcap = knob(7) > 0 ? knob(7) : 10;
+  const int lg1 = std::min(lg2_ceil(2 * b1 + 2), std::min(lgcap, 10));
+  const int cap1 = 1 << lg1;
+  const int lg2 = std::min(lg2_ceil(2 * (1 + (int64_t)(cap1 / 2) * pmax) + 2), std::min(lgcap, 9));
+  const int cap2 = 1 << lg2;
+  const size_t lds = (size_t)3 * (cap1 + cap2) * sizeof(int) + (size_t)(cap1 / 2) * (sizeof(int) + sizeof(double)) +
+                     (size_t)(cap2 / 2) * sizeof(double);
+  const DCsr dR{Ri.p, Rj.p, Ra.p, nc};
+  DBuf<int> len((size_t)nc);
+  const int grid = grid_rows(nc, 32);
+  hipLaunchKernelGGL((k_rap<false>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
+                     len.p, nullptr, nullptr, nullptr);
+  SDV(hipGetLastError());
+  std::vector<int> hl;
+  len.down(hl, nc);
+  std::vector<int> ovf;
+  for (int q = 0; q < nc; ++q)
+    if (hl[q] < 0) ovf.push_back(q);
+  std::vector<std::vector<int>> oj;
+  std::vector<std::vector<double>> oa;
+  rap_row_list(Rh, A, P, ovf, oj, oa);
+  for (size_t k = 0; k < ovf.size(); ++k) hl[ovf[k]] = (int)oj[k].size();
+  std::vector<int> ci((size_t)nc + 1, 0);
+  for (int q = 0; q < nc; ++q) {
+    if ((int64_t)ci[q] + hl[q] > 0x7fffffffLL) throw std::runtime_error("device setup: RAP exceeds 2^31 entries");
+    ci[q + 1] = ci[q] + hl[q];
+  }
+  DBuf<int> Ci, Cj((size_t)ci[nc]);
+  DBuf<double> Ca((size_t)ci[nc]);
+  Ci.up(ci);
+  hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
+                     len.p, Ci.p, Cj.p, Ca.p);
+  SDV(hipGetLastError());
+  C.resize_rows(nc, nc);
+  C.i = ci;
+  Cj.down(C.j, (size_t)ci[nc]);
+  Ca.down(C.a, (size_t)ci[nc]);
+  for (size_t k = 0; k < ovf.size(); ++k) {
+    std::copy(oj[k].begin(), oj[k].end(), C.j.begin() + ci[ovf[k]]);
+    std::copy(oa[k].begin(), oa[k].end(), C.a.begin() + ci[ovf[k]]);
+  }
+  g_host_rows = (long long)ovf.size();
+}
+
+}  // namespace hve

@@ -169,6 +169,10 @@ struct AMGParams {
   // relax 3/4/6 into unweighted Jacobi and 8/13/14 into l1-Jacobi).
   int auto_block_rows = 0;
   int auto_block_min = 64;
+  // 1: the ext+i interpolation, its truncation, R = P^T and RAP run on the GPU
+  // (device/setup_dev.hip, byte for byte the host result); set by the device
+  // setup path only
+  int device_setup = 0;
   // hybrid-GS row blocks of a level (one rank's share) of `rows` rows
   int blocks_for(int rows) const {
     const int top = num_blocks < 1 ? 1 : num_blocks;
@@ -276,6 +280,16 @@ int extpi_row_count(const Pattern& S, const std::vector<int>& cf, int i, RowMap&
 void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
                     int i, RowMap& M, CSR& P);
 void rap_row(const CSR& R, const CSR& A, const CSR& P, int q, int ic, RapScratch& W);
+// row lists of the device setup's host fallback, and its table bounds
+int64_t extpi_bound_max(const Pattern& S);
+void extpi_count_rows(const Pattern& S, const std::vector<int>& cf, const std::vector<int>& rows,
+                      std::vector<int>& cnt);
+void extpi_fill_rows(const CSR& A, const Pattern& S, const std::vector<int>& cf,
+                     const std::vector<int>& fine_to_coarse, const std::vector<int>& rows, CSR& P);
+void truncate_row_list(CSR& P, const std::vector<int>& rows, double tol, int max_elmts, std::vector<int>& newlen);
+int64_t rap_bound_max(const CSR& R, const CSR& A);
+void rap_row_list(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& rows,
+                  std::vector<std::vector<int>>& oj, std::vector<std::vector<double>>& oa);
 // one row of truncate_rows in its own slots; returns the new length
 int truncate_row(CSR& P, int r, double tol, int max_elmts, std::vector<int>& rj, std::vector<double>& ra);
 double hypre_rand_at(int64_t k, int seed);

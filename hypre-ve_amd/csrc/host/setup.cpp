@@ -5,6 +5,7 @@
 // accumulation order, so that the resulting hierarchy (and therefore the
 // complexities and convergence the reference reports) is reproduced exactly.
 #include "hve_host.hpp"
+#include "setup_dev.hpp"
 #include "layout.hpp"
 
 #include <algorithm>
@@ -913,6 +914,67 @@ void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, 
   }
 }
 
+// Row lists for the device setup's host fallback and its table bounds
+// (OpenMP here; setup_dev.hip is compiled without it).
+int64_t extpi_bound_max(const Pattern& S) {
+  int64_t m = 1;
+#pragma omp parallel for reduction(max : m) schedule(static)
+  for (int i = 0; i < S.n; ++i) m = std::max(m, extpi_bound(S, i));
+  return m;
+}
+void extpi_count_rows(const Pattern& S, const std::vector<int>& cf, const std::vector<int>& rows,
+                      std::vector<int>& cnt) {
+#pragma omp parallel
+  {
+    RowMap M;
+#pragma omp for schedule(dynamic, 64)
+    for (size_t k = 0; k < rows.size(); ++k) cnt[rows[k]] = extpi_row_count(S, cf, rows[k], M);
+  }
+}
+void extpi_fill_rows(const CSR& A, const Pattern& S, const std::vector<int>& cf,
+                     const std::vector<int>& fine_to_coarse, const std::vector<int>& rows, CSR& P) {
+#pragma omp parallel
+  {
+    RowMap M;
+#pragma omp for schedule(dynamic, 64)
+    for (size_t k = 0; k < rows.size(); ++k) extpi_row_fill(A, S, cf, fine_to_coarse, rows[k], M, P);
+  }
+}
+void truncate_row_list(CSR& P, const std::vector<int>& rows, double tol, int max_elmts, std::vector<int>& newlen) {
+#pragma omp parallel
+  {
+    std::vector<int> rj;
+    std::vector<double> ra;
+#pragma omp for schedule(dynamic, 16)
+    for (size_t k = 0; k < rows.size(); ++k) newlen[rows[k]] = truncate_row(P, rows[k], tol, max_elmts, rj, ra);
+  }
+}
+int64_t rap_bound_max(const CSR& R, const CSR& A) {
+  int64_t m = 1;
+#pragma omp parallel for reduction(max : m) schedule(static)
+  for (int q = 0; q < R.nrows; ++q) {
+    int64_t b = 0;
+    for (int jj = R.i[q]; jj < R.i[q + 1]; ++jj) b += A.i[R.j[jj] + 1] - A.i[R.j[jj]];
+    m = std::max(m, b);
+  }
+  return m;
+}
+void rap_row_list(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& rows,
+                  std::vector<std::vector<int>>& oj, std::vector<std::vector<double>>& oa) {
+  oj.assign(rows.size(), {});
+  oa.assign(rows.size(), {});
+#pragma omp parallel
+  {
+    RapScratch W;
+#pragma omp for schedule(dynamic, 16)
+    for (size_t k = 0; k < rows.size(); ++k) {
+      rap_row(R, A, P, rows[k], rows[k], W);
+      oj[k] = W.tj;
+      oa[k] = W.ta;
+    }
+  }
+}
+
 void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
                 int nrows, int ncoarse, int nuniv, CSR& P) {
   (void)nuniv;
@@ -1742,13 +1804,34 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
       rank_order_rows(P, emul, cs);
     }
+    else if (prm.interp_type == 6 && prm.device_setup) {
+      std::vector<int> f2c(cf.size(), -1);
+      int nc = 0;
+      for (size_t i = 0; i < cf.size(); ++i)
+        if (cf[i] >= 0) f2c[i] = nc++;
+      dev_extpi_interp(L.A, S, cf, f2c, nc, prm.trunc_factor, prm.P_max_elmts, P);
+      for (int& v : cf)
+        if (v == SF_PT) v = F_PT;
+      if (dev_setup_host_rows() > 0) {
+        snprintf(buf, sizeof buf, "level %d: %lld interpolation rows on the host\n", level, dev_setup_host_rows());
+        H.log += buf;
+      }
+    }
     else if (prm.interp_type == 6) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));
     double t3 = now();
     t_i += t3 - t2;
-    CSR Ac;
-    rap(P, L.A, Ac);
+    CSR Ac, Rdev;
+    if (prm.device_setup) {
+      dev_rap(P, L.A, Rdev, Ac);
+      if (dev_setup_host_rows() > 0) {
+        snprintf(buf, sizeof buf, "level %d: %lld Galerkin rows on the host\n", level, dev_setup_host_rows());
+        H.log += buf;
+      }
+    } else {
+      rap(P, L.A, Ac);
+    }
     std::vector<int> emul_c;
     if (!emul.empty()) {
       // hypre's RAP keeps each coarse row as diag then offd (par_rap.c)
@@ -1762,7 +1845,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     t_r += t4 - t3;
     L.cf.swap(cf);
     L.P.swap(P);
-    transpose(L.P, L.R);
+    if (prm.device_setup) L.R.swap(Rdev);  // R = P^T came with the device RAP
+    else transpose(L.P, L.R);
     t_t += now() - t4;
     snprintf(buf, sizeof buf, "level %d: rows %d nnz %lld -> coarse %d (P nnz %lld)\n", level, fine_size,
              (long long)L.A.nnz(), coarse_size, (long long)L.P.nnz());
@@ -1783,7 +1867,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   snprintf(buf, sizeof buf, "setup phases: strength %.3fs coarsen %.3fs interp %.3fs rap %.3fs transpose %.3fs\n",
            t_s, t_c, t_i, t_r, t_t);
   H.log += buf;
-  if (prm.print_level > 0) fputs(H.log.c_str(), stderr);
+  const double t_l1 = now();
   const int nl = (int)H.lev.size();
   // l1 norms for the smoothers that need them
   for (int j = 0; j < nl; ++j) {
@@ -1866,6 +1950,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     H.coarse_n = Ac.nrows;
     csr_to_dense(Ac, H.coarse_dense);
   }
+  snprintf(buf, sizeof buf, "setup: smoother data (l1 norms, weights, coarsest factor) %.3fs\n", now() - t_l1);
+  H.log += buf;
+  if (prm.print_level > 0) fputs(H.log.c_str(), stderr);
   double tot_rows = 0, tot_nnz = 0;
   for (auto& L : H.lev) { tot_rows += L.A.nrows; tot_nnz += (double)L.A.nnz(); }
   H.grid_complexity = tot_rows / H.lev[0].A.nrows;

@@ -194,6 +194,8 @@ SIGNATURES = [
     ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
     ("hypreve_BoomerAMGCodedLayoutCheck", _i, [_p, _i, _i, _pi, _pi]),
     ("hypreve_SetKnob", _i, [_i, _i]),
+    ("hypreve_BoomerAMGSetDeviceSetup", _i, [_p, _i]),
+    ("hypreve_BoomerAMGGetSetupLog", _i, [_p, C.c_char_p, _i]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchLevelOpStoredBytes", _i, [_p, _i, _i, _pd]),
     ("hypreve_BenchOperator", _i, [_p, _i, _i, _i, _i, _pd, _pd, C.c_char_p, _i]),
@@ -410,6 +412,7 @@ class BoomerAMG:
         "print_level": ("HYPRE_BoomerAMGSetPrintLevel", int), "converge_type": ("HYPRE_BoomerAMGSetConvergeType", int),
         "num_blocks": ("hypreve_BoomerAMGSetNumBlocks", int), "use_graph": ("hypreve_BoomerAMGSetUseGraph", int),
         "sell_policy": ("hypreve_BoomerAMGSetSellPolicy", int),
+        "device_setup": ("hypreve_BoomerAMGSetDeviceSetup", int),
         "agglo_rows": ("hypreve_BoomerAMGSetAggloRows", int),
         "agg_num_levels": ("HYPRE_BoomerAMGSetAggNumLevels", int), "num_paths": ("HYPRE_BoomerAMGSetNumPaths", int),
         "agg_interp_type": ("HYPRE_BoomerAMGSetAggInterpType", int),
@@ -494,7 +497,7 @@ class BoomerAMG:
         return r.value, a.value, p.value
 
     def level_matrix(self, l, which=0):
-        """(indptr, indices, data, shape) of A_l (which=0) or P_l (which=1)."""
+        """(indptr, indices, data, shape) of A_l (which=0), P_l (1) or R_l = P_l^T (2)."""
         nr, nc, nz = C.c_int(), C.c_int(), C.c_int64()
         L = lib()
         check(L.hypreve_BoomerAMGGetLevelMatrix(self.h, l, which, C.byref(nr), C.byref(nc), C.byref(nz),
@@ -559,6 +562,12 @@ class BoomerAMG:
         w, npat = C.c_int(), C.c_int()
         check(lib().hypreve_BoomerAMGStencilLayoutCheck(self.h, level, C.byref(w), C.byref(npat)), "StencilLayoutCheck")
         return w.value, npat.value
+
+    def setup_log(self):
+        """The setup's log: levels, phase times, rows the device setup left to the host."""
+        buf = C.create_string_buffer(1 << 16)
+        check(lib().hypreve_BoomerAMGGetSetupLog(self.h, buf, 1 << 16), "GetSetupLog")
+        return buf.value.decode()
 
     def coded_layout_check(self, level=0, which=1):
         """(distinct offsets, distinct values) of level's P (which 1) or R (2)

@@ -296,7 +296,7 @@ HYPRE_Int hypreve_BoomerAMGGetComplexities(HYPRE_Solver solver, HYPRE_Real *grid
 HYPRE_Int hypreve_BoomerAMGGetLevelInfo(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int *rows,
                                         int64_t *nnz_A, int64_t *nnz_P);
 /* Export one level of the (host-side) hierarchy for inspection/testing.
- * which: 0 = A, 1 = P.  Pass NULL arrays to query sizes. */
+ * which: 0 = A, 1 = P, 2 = R = P^T.  Pass NULL arrays to query sizes. */
 HYPRE_Int hypreve_BoomerAMGGetLevelMatrix(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which,
                                           HYPRE_Int *nrows, HYPRE_Int *ncols, int64_t *nnz,
                                           HYPRE_Int *row_ptr, HYPRE_Int *cols, HYPRE_Real *vals);
@@ -350,6 +350,14 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_bl
  * *npatterns = 0) when the operator is not a constant-coefficient stencil. */
 HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int *width,
                                               HYPRE_Int *npatterns);
+/* Setup's heavy row loops on the GPU (default 1): ext+i interpolation and its
+ * truncation, R = P^T and the Galerkin product RAP, byte for byte the host
+ * functions' result (device/setup_dev.hip); 0 runs them on the host.  The
+ * distributed setup keeps the host. */
+HYPRE_Int hypreve_BoomerAMGSetDeviceSetup(HYPRE_Solver solver, HYPRE_Int on);
+/* The setup's log (levels, phase times, rows the device setup left to the
+ * host) into buf[0..len). */
+HYPRE_Int hypreve_BoomerAMGGetSetupLog(HYPRE_Solver solver, char *buf, HYPRE_Int len);
 /* Host check of the offset-coded layout of level's P (which 1) or R (which 2)
  * (after hypreve_BoomerAMGSetupHost or Setup): every row decoded from its
  * 16-bit codes equals the CSR row entry for entry, values bitwise.
@@ -371,7 +379,9 @@ HYPRE_Int hypreve_BenchOperator(HYPRE_ParCSRMatrix A, HYPRE_Int op, HYPRE_Int po
                                 HYPRE_Int len);
 /* Tuning knobs read at kernel launch (0 = built-in default): 0 row blocks per
  * step of the offset-coded loop (1, 2, 4), 1 its codes per batch (4, 8, 16),
- * 2 its persistent workgroups per CU.  Results are unchanged. */
+ * 2 its persistent workgroups per CU, 3 the stream-mix access width (2: 16 B),
+ * 7 the device setup's LDS table cap (2^v slots; rows beyond it are finished
+ * on the host).  Results are unchanged. */
 HYPRE_Int hypreve_SetKnob(HYPRE_Int id, HYPRE_Int value);
 /* Bytes the same launch streams in the operator's stored (compressed) layout,
  * vectors included. */
