@@ -599,7 +599,14 @@ void DevGs::release() {
 }
 
 void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key, const DevSell::Coded* coded) {
+  static const bool tlog = getenv("HVE_SETUP_T") != nullptr;
+  auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double t0 = now();
   in.upload(op.interior, op.map_int, policy, key, coded);
+  if (tlog)
+    fprintf(stderr, "[upload] %d rows %lld nnz: %s %.3fs\n", op.interior.nrows, (long long)op.interior.nnz(),
+            in.code16 ? "coded" : in.slot_mask ? "stencil" : in.col16 ? "dict" : in.vidx16 ? "vt16" : in.rowlen ? "jagged"
+            : in.wide ? "wide" : "padded", now() - t0);
   bd.upload(op.boundary, op.map_bnd, policy);
   nrows_local = op.nrows_local;
 }

@@ -22,6 +22,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -92,6 +93,22 @@ struct DevCSR {
 };
 
 long long g_host_rows = 0;
+
+// HVE_SETUP_T: stage times of the device setup on stderr
+struct STimer {
+  bool on = getenv("HVE_SETUP_T") != nullptr;
+  double t = now();
+  static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  void lap(const char* what) {
+    if (!on) return;
+    (void)hipDeviceSynchronize();
+    const double n = now();
+    fprintf(stderr, "[dsetup] %-28s %.3fs\n", what, n - t);
+    t = n;
+  }
+};
 
 // Open-addressing map in LDS, one per wavefront, used by lane 0 only.
 struct LMap {
@@ -514,6 +531,7 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   const int n = A.nrows;
   P.resize_rows(n, ncoarse);
   if (n == 0) return;
+  STimer T;
   DevCSR dA;
   dA.up(A);
   DBuf<int> Si, Sj, dcf, df2c;
@@ -522,6 +540,7 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   dcf.up(cf);
   df2c.up(fine_to_coarse);
   const DCsr dS{Si.p, Sj.p, nullptr, S.n};
+  T.lap("extpi upload");
   // table capacity from the largest candidate count of a row (capped; rows
   // beyond it overflow to the host)
   const int64_t bmax = extpi_bound_max(S);
@@ -534,6 +553,7 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   hipLaunchKernelGGL((k_extpi<false>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
                      nullptr, nullptr, nullptr);
   SDV(hipGetLastError());
+  T.lap("extpi count kernel");
   // rows that overflowed: counted on the host
   std::vector<int> hc;
   cnt.down(hc, n);
@@ -556,6 +576,7 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   hipLaunchKernelGGL((k_extpi<true>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
                      Pi.p, Pj.p, Pa.p);
   SDV(hipGetLastError());
+  T.lap("extpi fill kernel");
   dA.i.free();
   dA.j.free();
   dA.a.free();
@@ -589,6 +610,7 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   hipLaunchKernelGGL(k_truncate, dim3((n + 255) / 256), dim3(256), 0, 0, n, Pi.p, Pj.p, Pa.p, trunc_factor, max_elmts,
                      nl.p);
   SDV(hipGetLastError());
+  T.lap("truncate kernel");
   std::vector<int> hl;
   nl.down(hl, n);
   std::vector<int> longrows;
@@ -619,9 +641,11 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   Ni.up(ni);
   hipLaunchKernelGGL(k_compact, dim3((n + 255) / 256), dim3(256), 0, 0, n, Pi.p, Pj.p, Pa.p, Ni.p, Nj.p, Na.p);
   SDV(hipGetLastError());
+  T.lap("truncate host part");
   P.i = ni;
   Nj.down(P.j, (size_t)ni[n]);
   Na.down(P.a, (size_t)ni[n]);
+  T.lap("P download");
   g_host_rows = (long long)(ovf.size() + longrows.size());
 }
 
@@ -629,9 +653,11 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   g_host_rows = 0;
   const int nf = P.nrows, nc = P.ncols;
   const int64_t nnzp = P.nnz();
+  STimer T;
   DevCSR dP, dA;
   dP.up(P);
   dA.up(A);
+  T.lap("rap upload");
   // R = P^T: a stable radix sort of the entries by column keeps every
   // column's rows ascending (transpose's counting sort)
   DBuf<int> rowof((size_t)nnzp), perm_in((size_t)nnzp), keys_out((size_t)nnzp), perm((size_t)nnzp);
@@ -664,6 +690,7 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   Ri.down(Rh.i, (size_t)nc + 1);
   Rj.down(Rh.j, (size_t)nnzp);
   Ra.down(Rh.a, (size_t)nnzp);
+  T.lap("transpose + R download");
   // table capacities from the largest products of a row (rows beyond: host)
   const int64_t b1 = rap_bound_max(Rh, A);
   int64_t pmax = 1;
@@ -681,6 +708,7 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   hipLaunchKernelGGL((k_rap<false>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
                      len.p, nullptr, nullptr, nullptr);
   SDV(hipGetLastError());
+  T.lap("rap count kernel");
   std::vector<int> hl;
   len.down(hl, nc);
   std::vector<int> ovf;
@@ -701,6 +729,7 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
                      len.p, Ci.p, Cj.p, Ca.p);
   SDV(hipGetLastError());
+  T.lap("rap fill kernel");
   C.resize_rows(nc, nc);
   C.i = ci;
   Cj.down(C.j, (size_t)ci[nc]);
@@ -709,6 +738,7 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
     std::copy(oj[k].begin(), oj[k].end(), C.j.begin() + ci[ovf[k]]);
     std::copy(oa[k].begin(), oa[k].end(), C.a.begin() + ci[ovf[k]]);
   }
+  T.lap("C download");
   g_host_rows = (long long)ovf.size();
 }
 

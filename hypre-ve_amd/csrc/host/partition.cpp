@@ -19,6 +19,7 @@ int owner_of(const std::vector<int>& starts, int g) {
 // Collect the sorted, unique global columns outside [a,b) referenced by rows
 // [r0,r1) of M.
 void halo_cols(const CSR& M, int r0, int r1, int a, int b, std::vector<int>& out) {
+  if (a <= 0 && b >= M.ncols) return;  // every column is local (one rank, or a replicated level)
   for (int r = r0; r < r1; ++r)
     for (int k = M.i[r]; k < M.i[r + 1]; ++k) {
       const int c = M.j[k];
@@ -37,11 +38,13 @@ void make_op(const CSR& M, int r0, int r1, int a, int b, const std::vector<int>&
   const int nrows = r1 - r0;
   op.nrows_local = nrows;
   std::vector<char> bnd(nrows, 0);
+#pragma omp parallel for schedule(static)
   for (int r = r0; r < r1; ++r)
     for (int k = M.i[r]; k < M.i[r + 1]; ++k) {
       const int c = M.j[k];
       if (c < a || c >= b) { bnd[r - r0] = 1; break; }
     }
+  // row copies in parallel (one rank's operators are the whole hierarchy)
   auto build = [&](bool want_bnd, CSR& out, std::vector<int>& map) {
     map.clear();
     for (int r = 0; r < nrows; ++r)
@@ -54,6 +57,7 @@ void make_op(const CSR& M, int r0, int r1, int a, int b, const std::vector<int>&
     }
     out.j.resize(out.i[m]);
     out.a.resize(out.i[m]);
+#pragma omp parallel for schedule(static)
     for (int q = 0; q < m; ++q) {
       const int r = map[q] + r0;
       int o = out.i[q];
@@ -183,7 +187,7 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
       hv(nl, std::vector<std::vector<int>>(size));
   for (int l = 0; l < nl; ++l) {
     const Level& L = H.lev[l];
-#pragma omp parallel for schedule(dynamic)
+#pragma omp parallel for schedule(dynamic) if (size > 1)
     for (int r = 0; r < size; ++r) {
       const int a = lo(l, r), b = hi(l, r);
       std::vector<int> u;
@@ -205,7 +209,8 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
   }
   for (int l = 0; l < nl; ++l) {
     const Level& L = H.lev[l];
-#pragma omp parallel for schedule(dynamic)
+    // one rank: the rank loop stays serial and make_op's row copies run in parallel
+#pragma omp parallel for schedule(dynamic) if (size > 1)
     for (int r = 0; r < size; ++r) {
       RankLevel& RL = out[r].lev[l];
       const int a = lo(l, r), b = hi(l, r);
