@@ -95,7 +95,7 @@ void DevSell::build_wave_map() {
 }
 
 void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy, const std::vector<int64_t>* key,
-                     const Coded* coded) {
+                     const Coded* coded, const std::vector<int64_t>* tile) {
   release();
   // Offset-coded layout (P_0 / R_0 of a grid hierarchy: 25 offsets, ~1200
   // weights, so an entry is one 16-bit code, 2 B instead of 6) where the grid
@@ -351,6 +351,19 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
   }
 dict:
   if (use_dict) {
+    // rows in compact grid tiles (DevAMG::build tile_keys): the groups of
+    // consecutive slices share more of their columns
+    std::vector<int> pre;
+    if (tile && !tile->empty()) {
+      pre.resize(A.nrows);
+      for (int r = 0; r < A.nrows; ++r) pre[r] = r;
+      auto tk = [&](int r) {
+        const int g = rowmap_h.empty() ? r : rowmap_h[r];
+        return g < (int)tile->size() ? (*tile)[g] : (int64_t)g;
+      };
+      std::stable_sort(pre.begin(), pre.end(), [&](int a, int b) { return tk(a) < tk(b); });
+    }
+    const std::vector<int>* prep = pre.empty() ? nullptr : &pre;
     std::vector<unsigned short> c16;
     std::vector<int> dp, dc, rl2;
     int mxd = 0;
@@ -378,20 +391,22 @@ dict:
     bool built = false, ranges = false;
     if (try_ranges) {
       built = build_sell_dict_host(A, group > 1 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd, 63,
-                                   policy == 10 ? 1e30 : 1.5);
+                                   policy == 10 ? 1e30 : 1.5, prep);
       if (!built && group > 1 && group_env == 0) {
         group = 1;
-        built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd, 63, policy == 10 ? 1e30 : 1.5);
+        built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd, 63, policy == 10 ? 1e30 : 1.5,
+                                     prep);
       }
       ranges = built;
       if (!built) group = (group_env == 1 || group_env == 2 || group_env == 4 || group_env == 8) ? group_env
                                                                                           : (A.nrows == A.ncols ? 4 : 1);
     }
     if (!built && policy != 10) {
-      built = build_sell_dict_host(A, group > 1 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd);
+      built = build_sell_dict_host(A, group > 1 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd, 0, 1.5,
+                                   prep);
       if (!built && group > 1 && group_env == 0) {
         group = 1;
-        built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd);
+        built = build_sell_dict_host(A, 4096, 1, perm, sp, rl2, c16, val, dp, dc, mxd, 0, 1.5, prep);
       }
     }
     if (built) {
@@ -598,11 +613,12 @@ void DevGs::release() {
   max_levels = 0;
 }
 
-void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key, const DevSell::Coded* coded) {
+void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key, const DevSell::Coded* coded,
+                   const std::vector<int64_t>* tile) {
   static const bool tlog = getenv("HVE_SETUP_T") != nullptr;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = now();
-  in.upload(op.interior, op.map_int, policy, key, coded);
+  in.upload(op.interior, op.map_int, policy, key, coded, tile);
   if (tlog)
     fprintf(stderr, "[upload] %d rows %lld nnz: %s %.3fs\n", op.interior.nrows, (long long)op.interior.nnz(),
             in.code16 ? "coded" : in.slot_mask ? "stencil" : in.col16 ? "dict" : in.vidx16 ? "vt16" : in.rowlen ? "jagged"
@@ -764,6 +780,58 @@ static void locality_keys(const RankHierarchy& R, int agg_level, int nbands, std
   }
 }
 
+// Compact 3-D tile keys of every coarse level's rows (dictionary layouts).
+// A dictionary group is 4 slices = 256 consecutive rows; in natural order they
+// are a thin strip of one grid line (512^3, level 1: 4095 distinct columns a
+// group, 16 a row), in a compact tile about 3x their count.  The tile of a
+// row is taken from its level-0 grid point f, with sides of about the cube
+// root of the fine points 256 of the level's rows cover (powers of two), and
+// rows are keyed (tile, f).  Only the row order of the layout changes, not any
+// row's sum.  HVE_DICT_TILES=0 keeps the natural order.
+static void tile_keys(const RankHierarchy& R, int agg_level, std::vector<std::vector<int64_t>>& keys) {
+  keys.assign(R.lev.size(), {});
+  static const int on = [] {
+    const char* e = getenv("HVE_DICT_TILES");
+    return e ? atoi(e) : 1;
+  }();
+  if (!on || R.lev.empty()) return;
+  const RankLevel& L0 = R.lev[0];
+  int64_t plane = 0, line = 0;
+  if (!grid_strides(L0.A.interior, L0.A.map_int, L0.n_loc, &plane, &line)) return;
+  const int64_t n0 = L0.n_loc;
+  const int64_t nx = line, ny = std::max<int64_t>(1, plane / line), nz = std::max<int64_t>(1, (n0 + plane - 1) / plane);
+  std::vector<int64_t> f(n0);
+  for (int64_t i = 0; i < n0; ++i) f[i] = i;
+  auto pow2 = [](double v) {
+    int64_t p = 1;
+    while ((double)(p * 2) <= v * 1.41421356) p *= 2;
+    return p;
+  };
+  for (size_t l = 0; l < R.lev.size(); ++l) {
+    if (agg_level >= 0 && (int)l >= agg_level) break;
+    const RankLevel& L = R.lev[l];
+    if ((int64_t)f.size() != L.n_loc) break;
+    if (l > 0 && L.n_loc > 0) {
+      const double vol = 256.0 * (double)n0 / (double)L.n_loc;  // fine points under 256 rows
+      const int64_t tz = std::min(nz, pow2(std::cbrt(vol))), ty = std::min(ny, pow2(std::cbrt(vol)));
+      const int64_t tx = std::min(nx, pow2(vol / (double)(ty * tz)));
+      const int64_t ntx = (nx + tx - 1) / tx, nty = (ny + ty - 1) / ty;
+      std::vector<int64_t>& k = keys[l];
+      k.resize(L.n_loc);
+      for (int i = 0; i < L.n_loc; ++i) {
+        const int64_t x = f[i] % line, y = (f[i] % plane) / line, z = f[i] / plane;
+        k[i] = (((z / tz) * nty + y / ty) * ntx + x / tx) * n0 + f[i];
+      }
+    }
+    if (L.cf.empty()) break;
+    std::vector<int64_t> fc;
+    fc.reserve(L.n_loc / 2);
+    for (int i = 0; i < L.n_loc && i < (int)L.cf.size(); ++i)
+      if (L.cf[i] == 1) fc.push_back(f[i]);
+    f.swap(fc);
+  }
+}
+
 // Tuning harness: one operator uploaded alone (layout policy, nbands of the
 // traversal when the grid strides are found), op applied reps times on a
 // private stream, timed with HIP events.  op: K_RESID, K_MATVEC, or the
@@ -841,6 +909,8 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   std::vector<std::vector<int64_t>> keys_r;
   if (nbands_r_env != nbands_env) locality_keys(R, agg_level_, nbands_r_env, keys_r);
   const std::vector<std::vector<int64_t>>& kr = nbands_r_env != nbands_env ? keys_r : keys;
+  std::vector<std::vector<int64_t>> tiles;
+  tile_keys(R, agg_level_, tiles);
   const bool tlog = getenv("HVE_SETUP_T") != nullptr;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   for (int l = 0; l < nl; ++l) {
@@ -853,7 +923,11 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     // A_l and P_l rows are level-l rows; R_l rows are level-(l+1) rows
     const std::vector<int64_t>* kl = keys[l].empty() ? nullptr : &keys[l];
     const std::vector<int64_t>* kc = (l + 1 < nl && !kr[l + 1].empty()) ? &kr[l + 1] : nullptr;
-    D.A.upload(L.A, prm.sell_policy, kl);
+    // A on level 1 and the restrictions (measured at 512^3: A_1 3.42 -> 3.24 ms,
+    // R_1 0.582 -> 0.560; A_2 0.873 -> 0.936, so A_2 keeps the natural order)
+    const std::vector<int64_t>* tl = (l == 1 && !tiles[l].empty()) ? &tiles[l] : nullptr;
+    const std::vector<int64_t>* tc = (l + 1 < nl && !tiles[l + 1].empty()) ? &tiles[l + 1] : nullptr;
+    D.A.upload(L.A, prm.sell_policy, kl, nullptr, tl);
     D.hu.upload(L.hu);
     if (l < nl - 1) {
       // grid context of P_l / R_l for the offset-coded layout: the fine point
@@ -877,7 +951,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
         }
       }
       D.P.upload(L.P, prm.sell_policy, kl, pc);
-      D.R.upload(L.R, prm.sell_policy, kc, rc);
+      D.R.upload(L.R, prm.sell_policy, kc, rc, tc);
       D.hv.upload(L.hv);
     }
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());

@@ -92,8 +92,11 @@ struct DevSell {
   // policy: AMGParams::sell_policy
   // key: per local row, the sort key of the locality traversal (nullptr: natural order)
   // coded: grid context; the offset-coded layout is tried first where it is given
+  // tile: per local row, a key of compact grid tiles; the dictionary layout
+  // cuts its slices from rows in that order (fewer distinct columns per group)
   void upload(const CSR& A, const std::vector<int>& rowmap = {}, int policy = 0,
-              const std::vector<int64_t>* key = nullptr, const Coded* coded = nullptr);
+              const std::vector<int64_t>* key = nullptr, const Coded* coded = nullptr,
+              const std::vector<int64_t>* tile = nullptr);
   // Workgroup row blocks visited in ascending key of their first row
   // (stored_to_local: stored row -> local row, empty = identity).
   void set_block_order(const std::vector<int>& stored_to_local, const std::vector<int64_t>& key);
@@ -130,7 +133,7 @@ struct DevOp {
   int64_t nnz() const { return in.nnz + bd.nnz; }
   // coded: grid context for the interior rows (DevSell::Coded)
   void upload(const RankOp& op, int policy = 0, const std::vector<int64_t>* key = nullptr,
-              const DevSell::Coded* coded = nullptr);
+              const DevSell::Coded* coded = nullptr, const std::vector<int64_t>* tile = nullptr);
   void release() { in.release(); bd.release(); }
 };
 

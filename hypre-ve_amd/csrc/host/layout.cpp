@@ -14,10 +14,10 @@ namespace hve {
 
 // SELL-64: slices of 64 consecutive rows, padded to the longest row of the
 // slice; entry k of lane r at slice_ptr[s] + 64*k + r; padding col = -1.
-static void sell_order(const CSR& A, int sigma, std::vector<int>& perm) {
+static void sell_order(const CSR& A, int sigma, std::vector<int>& perm, const std::vector<int>* pre = nullptr) {
   const int n = A.nrows;
   perm.resize(n);
-  for (int r = 0; r < n; ++r) perm[r] = r;
+  for (int r = 0; r < n; ++r) perm[r] = pre ? (*pre)[r] : r;
   if (sigma <= 0) return;
 #pragma omp parallel for schedule(static)
   for (int w0 = 0; w0 < n; w0 += sigma) {
@@ -551,13 +551,14 @@ static void cover_ranges(const std::vector<int>& cols, int max_ranges, std::vect
 bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& perm, std::vector<int>& slice_ptr,
                           std::vector<int>& rowlen, std::vector<unsigned short>& col16, std::vector<double>& val,
                           std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct, int max_ranges,
-                          double max_cover) {
+                          double max_cover, const std::vector<int>* pre) {
   if (dmax > 65535) dmax = 65535;
   if (group < 1) group = 1;
   const int n = A.nrows;
   const int ns = (n + 63) / 64;
   const int ng = (ns + group - 1) / group;
-  sell_order(A, 64, perm);
+  if (pre && (int)pre->size() != n) pre = nullptr;
+  sell_order(A, 64, perm, pre);
   // distinct columns of each group of `group` slices (one workgroup)
   auto group_cols = [&](int g, std::vector<int>& cols) {
     cols.clear();

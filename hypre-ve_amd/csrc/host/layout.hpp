@@ -62,6 +62,8 @@ void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<in
 // indices into the slice's ascending list of distinct columns).  false when
 // a slice has more than dmax distinct columns; max_distinct is set either way.
 // group: slices sharing one dictionary (one workgroup of `group` waves).
+// pre: the order rows are cut into slices in (a permutation of the rows;
+// nullptr = natural order), before each slice is sorted by row length.
 // max_ranges > 0: range dictionary instead.  The x-tile of a group is the
 // union of at most max_ranges contiguous column ranges that cover its distinct
 // columns (the largest holes between them left out), staged by coalesced
@@ -73,7 +75,7 @@ void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<in
 bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& perm, std::vector<int>& slice_ptr,
                           std::vector<int>& rowlen, std::vector<unsigned short>& col16, std::vector<double>& val,
                           std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct,
-                          int max_ranges = 0, double max_cover = 1.5);
+                          int max_ranges = 0, double max_cover = 1.5, const std::vector<int>* pre = nullptr);
 // Padded entry count of the SELL-64 layout for a given sigma (0 = no sort).
 int64_t sell_padded_nnz(const CSR& A, int sigma);
 // Level schedule of one hybrid Gauss-Seidel sweep (par_relax.c cases 3/4/6/
