@@ -48,10 +48,19 @@ def stream_calibration(path):
 
 def main():
     root, grid = sys.argv[1], int(sys.argv[2])
+    # the cycle's own finest residual kernel: the first layout family with
+    # dispatches at this grid (bench.py also times the general padded path,
+    # hve::k_sell<0, ...>, on the same grid: it must not be averaged in)
+    fpath = os.path.join(root, "pmc_fetch", "run_counter_collection.csv")
+    wpath = os.path.join(root, "pmc_write", "run_counter_collection.csv")
+    fetch = write = None
     names = set()
-    fetch, nf = mean_counter(os.path.join(root, "pmc_fetch", "run_counter_collection.csv"), "FETCH_SIZE", grid,
-                             names=names)
-    write, nw = mean_counter(os.path.join(root, "pmc_write", "run_counter_collection.csv"), "WRITE_SIZE", grid)
+    for pre in ("hve::k_sell_stencil<0,", "hve::k_sell_delta<0,", "hve::k_sell<0,"):
+        names = set()
+        fetch, nf = mean_counter(fpath, "FETCH_SIZE", grid, prefixes=(pre,), names=names)
+        write, nw = mean_counter(wpath, "WRITE_SIZE", grid, prefixes=(pre,))
+        if fetch is not None and write is not None:
+            break
     if fetch is None or write is None:
         raise SystemExit("no matching dispatches")
     out = {"kernel": "k_sell / k_sell_delta / k_sell_stencil <OP_RESID> finest level", "kernel_names": sorted(names),
