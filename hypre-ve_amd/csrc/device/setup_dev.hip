@@ -284,6 +284,140 @@ __global__ void __launch_bounds__(64) k_extpi(DCsr A, DCsr S, const int* __restr
   }
 }
 
+// LDS writes of one lane visible to the wave's other lanes
+__device__ __forceinline__ void wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Fill pass with the wave's 64 lanes sharing the strong-F distribution loops
+// (par_lr_interp.c's "sum" and "distribute" loops over A's row i1): lane 0
+// builds C-hat in first-touch order as above; then for each entry of A's row i
+// (in order, every lane in step) the lanes look up a chunk of row i1's entries
+// in the LDS map at once.  The sum is still added up by lane 0 in entry order
+// from the staged contributions, each distributed entry updates its own C-hat
+// slot (a row holds a column once, so no two lanes meet), and the diagonal's
+// single contribution of row i1 is added by every lane's copy of the diagonal
+// in the same place as on the host.  Same operations, same order.
+__global__ void __launch_bounds__(64) k_extpi_fill_w(DCsr A, DCsr S, const int* __restrict__ cf,
+                                                     const int* __restrict__ f2c, int n, int cap, int lg,
+                                                     const int* __restrict__ rowcnt, const int* __restrict__ Pi,
+                                                     int* __restrict__ Pj, double* __restrict__ Pa) {
+  extern __shared__ int lds[];
+  lds_zero(lds + 2 * cap, cap);  // generation stamps
+  const int lane = threadIdx.x;
+  LMap M;
+  M.init(lds, cap, lg);
+  double* pa = reinterpret_cast<double*>(lds + 3 * cap);  // cap/2 doubles
+  double* cv = pa + cap / 2;                               // 64 staged contributions
+  int* cfg = reinterpret_cast<int*>(cv + 64);              // 64 flags
+  constexpr int kNone = -1, kStrongF = -2;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    if (rowcnt[i] < 0) continue;  // finished on the host
+    const int ci = cf[i];
+    const int jb = Pi[i];
+    if (ci >= 0) {
+      if (lane == 0) {
+        Pj[jb] = f2c[i];
+        Pa[jb] = 1.0;
+      }
+      continue;
+    }
+    if (ci == kSF) continue;
+    M.begin();  // every lane: the generation stamps stay in step
+    int jend = 0;
+    if (lane == 0) {
+      int jc = 0;
+      bool fresh;
+      for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+        const int i1 = S.j[jj];
+        const int c1 = cf[i1];
+        if (c1 >= 0) {
+          M.find_or_insert(i1, jc, fresh);
+          if (fresh) { Pj[jb + jc] = f2c[i1]; pa[jc] = 0.0; jc++; }
+        } else if (c1 != kSF) {
+          *M.find_or_insert(i1, kStrongF, fresh) = kStrongF;
+          for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+            const int k1 = S.j[kk];
+            if (cf[k1] >= 0) {
+              M.find_or_insert(k1, jc, fresh);
+              if (fresh) { Pj[jb + jc] = f2c[k1]; pa[jc] = 0.0; jc++; }
+            }
+          }
+        }
+      }
+      jend = jc;
+    }
+    jend = __shfl(jend, 0, 64);
+    wsync();
+    double diagonal = A.a[A.i[i]];
+    for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
+      const int i1 = A.j[jj];
+      const double aij = A.a[jj];
+      const int m1 = M.get(i1, kNone);
+      if (m1 >= 0) {
+        if (lane == 0) pa[m1] += aij;
+        wsync();
+      } else if (m1 == kStrongF) {
+        const int b1 = A.i[i1] + 1, e1 = A.i[i1 + 1];
+        const int sgn = (A.a[A.i[i1]] < 0) ? -1 : 1;
+        double sum = 0.0;
+        for (int c0 = b1; c0 < e1; c0 += 64) {
+          const int jj1 = c0 + lane;
+          double v = 0.0;
+          int take = 0;
+          if (jj1 < e1) {
+            const int i2 = A.j[jj1];
+            v = A.a[jj1];
+            take = ((M.get(i2, kNone) >= 0 || i2 == i) && (sgn * v) < 0) ? 1 : 0;
+          }
+          cv[lane] = v;
+          cfg[lane] = take;
+          wsync();
+          if (lane == 0) {
+            const int cnt = min(64, e1 - c0);
+            for (int q = 0; q < cnt; ++q)
+              if (cfg[q]) sum += cv[q];
+          }
+          wsync();
+        }
+        sum = __shfl(sum, 0, 64);
+        if (sum != 0) {
+          const double distribute = aij / sum;
+          double dadd = 0.0;
+          int dhas = 0;
+          for (int c0 = b1; c0 < e1; c0 += 64) {
+            const int jj1 = c0 + lane;
+            if (jj1 < e1) {
+              const int i2 = A.j[jj1];
+              const double a2 = A.a[jj1];
+              const int m2 = M.get(i2, kNone);
+              if (m2 >= 0 && (sgn * a2) < 0) pa[m2] += distribute * a2;
+              if (i2 == i && (sgn * a2) < 0) {
+                dadd = distribute * a2;
+                dhas = 1;
+              }
+            }
+          }
+          const unsigned long long bl = __ballot(dhas);
+          if (bl) diagonal += __shfl(dadd, __ffsll((long long)bl) - 1, 64);
+          wsync();
+        } else {
+          diagonal += aij;
+        }
+      } else if (cf[i1] != kSF) {
+        diagonal += aij;
+      }
+    }
+    for (int k = lane; k < jend; k += 64) {
+      double v = pa[k];
+      if (diagonal) v /= -diagonal;
+      Pa[jb + k] = v;
+    }
+    wsync();
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Truncation of one row per lane (setup.cpp truncate_row): in place inside
 // the row's slots, newlen[r] = kept entries (-1: row longer than kTrMax,
@@ -572,9 +706,16 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   DBuf<int> Pi, Pj((size_t)t);
   DBuf<double> Pa((size_t)t);
   Pi.up(hp);
-  // the count buffer keeps -1 on overflow rows: the fill pass skips them
-  hipLaunchKernelGGL((k_extpi<true>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
-                     Pi.p, Pj.p, Pa.p);
+  // the count buffer keeps -1 on overflow rows: the fill pass skips them.
+  // HVE_EXTPI_SERIAL=1: the one-lane fill (k_extpi<true>) instead of the
+  // wave-shared one
+  static const bool serial_fill = getenv("HVE_EXTPI_SERIAL") && atoi(getenv("HVE_EXTPI_SERIAL")) != 0;
+  if (serial_fill)
+    hipLaunchKernelGGL((k_extpi<true>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
+                       Pi.p, Pj.p, Pa.p);
+  else
+    hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), lds + 64 * (sizeof(double) + sizeof(int)), 0, dA.view(),
+                       dS, dcf.p, df2c.p, n, cap, lg, cnt.p, Pi.p, Pj.p, Pa.p);
   SDV(hipGetLastError());
   T.lap("extpi fill kernel");
   dA.i.free();
