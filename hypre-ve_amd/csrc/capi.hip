@@ -1509,13 +1509,13 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
                                HYPRE_Real* avg_ms, HYPRE_Real* bytes, HYPRE_Real* padded_nnz) {
   CHECK_ARG(s && s->dev && s->dev->built(), 1);
   CHECK_ARG(level >= 0 && level < s->dev->num_levels(), 2);
-  CHECK_ARG(which >= 0 && which <= 2 && (which == 0 || level < s->dev->num_levels() - 1), 3);
+  CHECK_ARG(which >= 0 && which <= 3 && (which == 0 || which == 3 || level < s->dev->num_levels() - 1), 3);
   CHECK_ARG(reps > 0, 4);
   API_BEGIN
   DevAMG& D = *s->dev;
   const DevLevel& L = D.level(level);
-  const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
-  const int op = which == 0 ? K_RESID : which == 1 ? K_PROLONG : K_RESTRICT;
+  const DevSell& M = (which == 0 || which == 3) ? L.A.in : which == 1 ? L.P.in : L.R.in;
+  const int op = which == 0 ? K_RESID : which == 1 ? K_PROLONG : which == 2 ? K_RESTRICT : K_L1JAC;
   hipStream_t st = D.stream();
   double* x = D.scratch(0);
   double* b = D.scratch(1);
@@ -1523,12 +1523,14 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
   HVE_HIP(launch_set(D.ws_n(), 1.0, x, st));
   HVE_HIP(launch_set(D.ws_n(), 0.5, b, st));
   HVE_HIP(launch_set(D.ws_n(), 0.0, y, st));
-  for (int w = 0; w < 3; ++w) HVE_HIP(launch_sell(op, M.view(), x, b, nullptr, nullptr, 0, y, -1.0, 0.0, st));
+  // which 3: A as the l1-Jacobi sweep, with b standing in for the l1 norms
+  const double* l1 = which == 3 ? b : nullptr;
+  for (int w = 0; w < 3; ++w) HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, y, -1.0, 0.0, st));
   hipEvent_t e0, e1;
   HVE_HIP(hipEventCreate(&e0));
   HVE_HIP(hipEventCreate(&e1));
   HVE_HIP(hipEventRecord(e0, st));
-  for (int r = 0; r < reps; ++r) HVE_HIP(launch_sell(op, M.view(), x, b, nullptr, nullptr, 0, y, -1.0, 0.0, st));
+  for (int r = 0; r < reps; ++r) HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, y, -1.0, 0.0, st));
   HVE_HIP(hipEventRecord(e1, st));
   HVE_HIP(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -1558,11 +1560,12 @@ HYPRE_Int hypreve_SetKnob(HYPRE_Int id, HYPRE_Int value) {
 HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Real* bytes) {
   CHECK_ARG(s && s->dev && s->dev->built() && bytes, 1);
   CHECK_ARG(level >= 0 && level < s->dev->num_levels(), 2);
-  CHECK_ARG(which >= 0 && which <= 2 && (which == 0 || level < s->dev->num_levels() - 1), 3);
+  CHECK_ARG(which >= 0 && which <= 3 && (which == 0 || which == 3 || level < s->dev->num_levels() - 1), 3);
   API_BEGIN
   const DevLevel& L = s->dev->level(level);
-  const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
-  const double out_rw = which == 0 ? 16.0 : which == 1 ? 16.0 : 8.0;
+  const DevSell& M = (which == 0 || which == 3) ? L.A.in : which == 1 ? L.P.in : L.R.in;
+  // b read + y write / y rw / y write / f, u_g, l1 read + u' write
+  const double out_rw = which == 0 ? 16.0 : which == 1 ? 16.0 : which == 2 ? 8.0 : 32.0;
   *bytes = (double)M.bytes() + (double)M.nrows * out_rw + (double)M.ncols * 8.0;
   API_END
 }

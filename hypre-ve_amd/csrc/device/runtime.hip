@@ -813,8 +813,34 @@ static void tile_keys(const RankHierarchy& R, int agg_level, std::vector<std::ve
     if ((int64_t)f.size() != L.n_loc) break;
     if (l > 0 && L.n_loc > 0) {
       const double vol = 256.0 * (double)n0 / (double)L.n_loc;  // fine points under 256 rows
-      const int64_t tz = std::min(nz, pow2(std::cbrt(vol))), ty = std::min(ny, pow2(std::cbrt(vol)));
-      const int64_t tx = std::min(nx, pow2(vol / (double)(ty * tz)));
+      // Tiles long in x: the per-row vectors (b, u, l1, y) of a slice stay in a
+      // few cache lines while the dictionary shrinks.  Measured at 512^3
+      // (profiles/r03/08_dict_tiles/tileshape*.log), level 1, A_1 residual /
+      // l1 sweep: natural order 3.42 / -, cube-like 16x8x8 3.15 / 3.29,
+      // 64x4x4 2.97 / 3.02, 128x4x2 2.88 / 2.94, 256x2x2 and longer slower;
+      // the level-2 keys (R_1's rows) best at 64x4x4 (R_1 0.565 -> 0.486).
+      int64_t tx, ty, tz;
+      if (l == 1) {
+        ty = std::min<int64_t>(ny, 4);
+        tz = std::min<int64_t>(nz, 2);
+        tx = std::min(nx, pow2(vol / (double)(ty * tz)));
+      } else {
+        tx = std::min<int64_t>(nx, 64);
+        ty = std::min<int64_t>(ny, 4);
+        tz = std::min<int64_t>(nz, 4);
+      }
+      // "tx,ty,tz" in fine points (tuning): HVE_DICT_TILE for level 1, HVE_DICT_TILE2 beyond
+      static const char* shape1 = getenv("HVE_DICT_TILE");
+      static const char* shape2 = getenv("HVE_DICT_TILE2");
+      const char* shape = l == 1 ? shape1 : shape2;
+      if (shape) {
+        long long a = 0, b = 0, c = 0;
+        if (sscanf(shape, "%lld,%lld,%lld", &a, &b, &c) == 3 && a > 0 && b > 0 && c > 0) {
+          tx = std::min<int64_t>(nx, a);
+          ty = std::min<int64_t>(ny, b);
+          tz = std::min<int64_t>(nz, c);
+        }
+      }
       const int64_t ntx = (nx + tx - 1) / tx, nty = (ny + ty - 1) / ty;
       std::vector<int64_t>& k = keys[l];
       k.resize(L.n_loc);

@@ -20,7 +20,7 @@ amg = hv.BoomerAMG(**kw)
 t = time.time()
 amg.setup(A)
 print(json.dumps({"n": n, "setup_s": round(time.time() - t, 1)}), flush=True)
-which = {"A": 0, "P": 1, "R": 2}
+which = {"A": 0, "P": 1, "R": 2, "J": 3}  # J: A as the l1-Jacobi sweep
 for st in settings:
     knobs = {}
     for kv in filter(None, st.split(",")):
@@ -32,5 +32,6 @@ for st in settings:
     for name in ops:
         l, w = int(name[1:]), which[name[0]]
         ms = min(amg.bench_level_op(l, w, 20)[0] for _ in range(2))
-        row[name] = [amg.level_layout(l, w), round(ms, 4), round(amg.level_op_stored_bytes(l, w) / ms / 1e6, 0)]
+        row[name] = [amg.level_layout(l, w if w < 3 else 0), round(ms, 4),
+                     round(amg.level_op_stored_bytes(l, w) / ms / 1e6, 0)]
     print(json.dumps(row), flush=True)
