@@ -951,7 +951,12 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     const std::vector<int64_t>* kc = (l + 1 < nl && !kr[l + 1].empty()) ? &kr[l + 1] : nullptr;
     // A on level 1 and the restrictions (measured at 512^3: A_1 3.42 -> 3.24 ms,
     // R_1 0.582 -> 0.560; A_2 0.873 -> 0.936, so A_2 keeps the natural order)
-    const std::vector<int64_t>* tl = (l == 1 && !tiles[l].empty()) ? &tiles[l] : nullptr;
+    // HVE_DICT_TILES_A2=1 tiles A_2 too (64x4x4: 0.872 -> 0.932 ms at 512^3)
+    static const int a2_tiles = [] {
+      const char* e = getenv("HVE_DICT_TILES_A2");
+      return e ? atoi(e) : 0;
+    }();
+    const std::vector<int64_t>* tl = ((l == 1 || (l >= 2 && a2_tiles)) && !tiles[l].empty()) ? &tiles[l] : nullptr;
     const std::vector<int64_t>* tc = (l + 1 < nl && !tiles[l + 1].empty()) ? &tiles[l + 1] : nullptr;
     D.A.upload(L.A, prm.sell_policy, kl, nullptr, tl);
     D.hu.upload(L.hu);
