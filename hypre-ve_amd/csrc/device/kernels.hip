@@ -70,6 +70,7 @@ struct SpArgs {
   const int* __restrict__ dict;              // dictionary layout: distinct columns, ascending
                                              // (dict_ranges: (start, offset) pairs of column ranges)
   int dict_ranges;                           // 1: range dictionary (k_sell_dict phase 1 copies ranges)
+  int dmax;                                  // dictionary layout: x-tile doubles (the value table follows)
   const short* __restrict__ dcol;            // delta layout: col - row - slot base
   const int* __restrict__ slot_base;         // delta layout: per (slice, slot) base offset
   const unsigned char* __restrict__ vidx;    // delta layout, value table: entry -> vtab index
@@ -1076,14 +1077,14 @@ __global__ void __launch_bounds__(256) k_sell_pw(SpArgs p) {
 // reads 2-byte local columns and takes x from LDS.  Same entries, same order,
 // same rounding as every other loop: bitwise the same.
 // ---------------------------------------------------------------------------
-template <int B, bool NT>
-__device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp, const double* __restrict__ vp, int& P,
-                                          int k, int blen, int llen, int (&c)[B], double (&a)[B]) {
+template <int B, bool NT, class V>
+__device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp, const V& vl, int& P, int k, int blen,
+                                          int llen, int (&c)[B], typename V::raw (&a)[B]) {
 #pragma unroll
   for (int q = 0; q < B; ++q) {
     const bool in = (k + q) < llen;
     c[q] = in ? (int)mload<NT>(cp + P) : -1;
-    a[q] = in ? mload<NT>(vp + P) : 0.0;
+    a[q] = in ? vl.template load<NT>(P) : V::none();
     P += __popcll(__ballot((k + q) < blen));
   }
 }
@@ -1091,9 +1092,16 @@ __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp,
 #ifndef HVE_DICT_TG
 #define HVE_DICT_TG (G == 4 ? 12 : 16 / G > 4 ? 16 / G : 4)
 #endif
-template <int OP, bool CFSEL, int B, bool NT, int G>
+// V: 8-byte values (ValF64) or 16-bit indices into the operator's value table
+// (ValT16, staged in LDS after the x-tile: the restriction of the 7-point
+// hierarchy, ~1200 distinct weights).
+template <int OP, bool CFSEL, int B, bool NT, int G, class V = ValF64>
 __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   extern __shared__ double xl[];
+  constexpr bool VT = sizeof(typename V::raw) == 4;  // ValT16
+  double* vt = xl + p.dmax;
+  if (VT)
+    for (int i = threadIdx.x; i < p.nvtab; i += 64 * G) vt[i] = p.vtab[i];
   // G waves per workgroup share one dictionary (the distinct columns of G
   // consecutive slices); wave w runs slice group * G + w.
   const int group = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
@@ -1119,20 +1127,21 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
     if (CFSEL) skip = p.cf[g] != p.relax_points;
     t = row_init<OP, NT>(p, g);
     if (!skip) pre = row_preload<OP, NT>(p, g);
-    if (OP == OP_JAC) {
-      uo = p.x[g];
-      d = blen > 0 ? p.val[beg + lane] : 0.0;  // diagonal stored first
-    }
+  }
+  const V vl = V::make(p, vt, beg + lane);
+  typename V::raw draw = V::none();  // diagonal stored first; its value is read after the table is staged
+  if (own && OP == OP_JAC) {
+    uo = p.x[g];
+    if (blen > 0) draw = vl.template load<false>(0);
   }
   const int llen = skip ? 0 : blen;
   const int k0 = (OP == OP_JAC) ? 1 : 0;
   const unsigned short* __restrict__ cp = p.col16 + beg + lane;
-  const double* __restrict__ vp = p.val + beg + lane;
   int P = 0;
   for (int k = 0; k < k0; ++k) P += __popcll(__ballot(k < blen));
   int c[B];
-  double a[B];
-  dict_load<B, NT>(cp, vp, P, k0, blen, llen, c, a);
+  typename V::raw a[B];
+  dict_load<B, NT>(cp, vl, P, k0, blen, llen, c, a);
   // 1. x-tile -> LDS, TG loads in flight per thread
   constexpr int TG = HVE_DICT_TG;
   constexpr int NT_ = 64 * G;
@@ -1195,15 +1204,16 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   }
   __syncthreads();
   if (!wave_live) return;
+  if (OP == OP_JAC && own) d = blen > 0 ? vl.value(draw) : 0.0;
   // 2. jagged row loop over local columns
   for (int k = k0; k < width; k += B) {
     int cn[B];
-    double an[B];
-    dict_load<B, NT>(cp, vp, P, k + B, blen, llen, cn, an);
+    typename V::raw an[B];
+    dict_load<B, NT>(cp, vl, P, k + B, blen, llen, cn, an);
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       if (c[q] >= 0) {
-        const double pr = a[q] * xl[c[q]];
+        const double pr = vl.value(a[q]) * xl[c[q]];
         if (sub) t -= pr;
         else t += pr;
       }
@@ -1572,7 +1582,25 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     const int G = M.dict_group;
     const int ngroups = ((M.nrows + 63) / 64 + G - 1) / G;
     a.nblocks_pad = (ngroups + 7) / 8 * 8;
+    a.dmax = M.dmax;
     const dim3 dgrid(a.nblocks_pad), dblock(64 * G);
+    if (M.vidx16) {  // 16-bit value indices: the table staged after the x-tile (one slice per workgroup)
+      if (G != 1) return hipErrorInvalidValue;
+      const size_t ldsv = (size_t)(M.dmax + M.nvtab) * sizeof(double);
+#define HVE_DV(OPV, BB) hipLaunchKernelGGL((k_sell_dict<OPV, false, BB, true, 1, ValT16>), dgrid, dblock, ldsv, s, a);
+#define HVE_DVL(OPV)                                        \
+  case OPV:                                                 \
+    if (bsel == 16) { HVE_DV(OPV, 16) } else { HVE_DV(OPV, 8) } \
+    break;
+      if (cfsel) return hipErrorInvalidValue;
+      switch (op) {
+        HVE_DVL(OP_RESTRICT) HVE_DVL(OP_RESTRICT_ZG) HVE_DVL(OP_MATVEC) HVE_DVL(OP_PROLONG) HVE_DVL(OP_GENERAL)
+        default: return hipErrorInvalidValue;
+      }
+#undef HVE_DVL
+#undef HVE_DV
+      return hipGetLastError();
+    }
     const size_t lds = (size_t)M.dmax * sizeof(double);
 #define HVE_D(OPV, CF, BB)                                                                             \
   if (G == 4) {                                                                                        \

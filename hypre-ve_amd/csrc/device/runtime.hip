@@ -428,7 +428,26 @@ dict:
       rowlen = dupload(rl2.data(), rl2.size());
       slice_ptr = dupload(sp.data(), sp.size());
       col16 = dupload(c16.data(), c16.size());
-      this->val = dupload(val.data(), val.size());
+      // one-slice dictionaries (restrictions) whose values take at most 4096
+      // bit patterns: 16-bit indices into a table staged in LDS after the
+      // x-tile, 4 B an entry instead of 10.  Measured on R_0 at 512^3 (its
+      // 64-row slices hold 573 distinct fine columns, 9 a row): 3.73 ms
+      // against 1.59 for the offset-coded layout, so it is taken only under
+      // the forced dictionary policy (5, tested bitwise) or HVE_DICT_VT=1.
+      static const int dict_vt_env = [] {
+        const char* e = getenv("HVE_DICT_VT");
+        return e ? atoi(e) : 0;
+      }();
+      std::vector<unsigned short> vi16;
+      std::vector<double> tab;
+      if (group == 1 && !ranges && (dict_vt_env != 0 || policy == 5) && sell_valtab_env() != 0 &&
+          (size_t)(dmax + 4096) * sizeof(double) <= 64 * 1024 && build_value_table16(val, 4096, vi16, tab)) {
+        vidx16 = dupload(vi16.data(), vi16.size());
+        vtab = dupload(tab.data(), tab.size());
+        nvtab = (int)tab.size();
+      } else {
+        this->val = dupload(val.data(), val.size());
+      }
       dict_ptr = dupload(dp.data(), dp.size());
       dict = dupload(dc.data(), std::max<size_t>(1, dc.size()));
       ndict = (int64_t)dc.size();  // ints: distinct columns, or 2 per range pair
