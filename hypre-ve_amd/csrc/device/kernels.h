@@ -55,6 +55,9 @@ struct SellView {
   int vbits = 0;
   const int* anc = nullptr;
   const int* cmap = nullptr;
+  // packed layout (k_sell_code PK; host: pack_sell_codes): per entry one 32-bit
+  // code ((column - slot_base[slice]) << vbits | value index into vtab)
+  const unsigned* code32 = nullptr;
 };
 
 enum : int {

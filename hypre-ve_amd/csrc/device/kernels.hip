@@ -22,6 +22,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace hve {
@@ -91,6 +92,7 @@ struct SpArgs {
   int vbits;
   const int* __restrict__ anc;               // offset-coded layout: row anchors (nullptr: the row)
   const int* __restrict__ cmap;              // offset-coded layout: position -> column (nullptr: identity)
+  const unsigned* __restrict__ code32;       // packed layout: ((col - slice base) << vbits) | value index
   double* __restrict__ y;         // output
   double* __restrict__ y2;        // second output (OP_RESID_L1JAC)
   double* __restrict__ nrm;       // OP_RESID_L1JAC (delta layout): per-workgroup sums of r_i^2 (y may be null)
@@ -825,15 +827,20 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
 // ---------------------------------------------------------------------------
 // NR rows per lane at once (rows of NR consecutive row blocks): all their
 // loads of a batch go out together, so a wave keeps NR x B gathers in flight.
-template <int OP, bool CFSEL, int B, bool MAP, int NR>
+// PK: the packed layout (host: pack_sell_codes) instead, one 32-bit code per
+// entry, ((column - slice base) << vbits) | value index, the base per slice in
+// slot_base: 4 B an entry and the column without a second gather (P_0, whose
+// offset-coded form needs cmap).
+template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK>
 __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, const int* ot, int rb0) {
-  constexpr unsigned PAD = 0xFFFFu;
+  using CT = typename std::conditional<PK, unsigned, unsigned short>::type;
+  constexpr unsigned PAD = PK ? 0xFFFFFFFFu : 0xFFFFu;
   const int vb = p.vbits;
   const unsigned vm = (1u << vb) - 1u;
   const bool sub = op_subtracts<OP>() || (OP == OP_GENERAL && p.w == -1.0);
   int g[NR], a[NR], width[NR];
   bool act[NR];
-  const unsigned short* cp[NR];
+  const CT* cp[NR];
   RowPre pre[NR];
   double t[NR];
   int wmax = 0;
@@ -845,14 +852,16 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
     const int beg = p.slice_ptr[slice];
     width[r] = act[r] ? __builtin_amdgcn_readfirstlane((p.slice_ptr[slice + 1] - beg) >> 6) : 0;
     g[r] = act[r] ? (p.rowmap ? mload<true>(p.rowmap + row) : row) : 0;
-    cp[r] = p.code16 + beg + (threadIdx.x & (kWave - 1));
+    if constexpr (PK) cp[r] = p.code32 + beg + (threadIdx.x & (kWave - 1));
+    else cp[r] = p.code16 + beg + (threadIdx.x & (kWave - 1));
     wmax = max(wmax, width[r]);  // the slice's width: wave-uniform
     if (CFSEL && act[r] && p.cf[g[r]] != p.relax_points) {
       if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) sstore<true>(p.y + g[r], p.x[g[r]]);
       act[r] = false;
     }
     if (!act[r]) width[r] = 0;  // this lane loads nothing
-    a[r] = act[r] ? (p.anc ? mload<true>(p.anc + g[r]) : g[r]) : 0;
+    if (PK) a[r] = p.slot_base[slice];  // the slice's smallest column
+    else a[r] = act[r] ? (p.anc ? mload<true>(p.anc + g[r]) : g[r]) : 0;
     pre[r] = act[r] ? row_preload<OP, true>(p, g[r]) : RowPre{};
     t[r] = act[r] ? row_init<OP, true>(p, g[r]) : 0.0;
   }
@@ -867,8 +876,8 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
     for (int r = 0; r < NR; ++r)
 #pragma unroll
       for (int q = 0; q < B; ++q) {
-        const int pos = c[r][q] != PAD ? a[r] + ot[c[r][q] >> vb] : 0;
-        const int col = c[r][q] == PAD ? -1 : MAP ? p.cmap[pos] : pos;
+        const int pos = c[r][q] != PAD ? a[r] + (PK ? (int)(c[r][q] >> vb) : ot[c[r][q] >> vb]) : 0;
+        const int col = c[r][q] == PAD ? -1 : (MAP && !PK) ? p.cmap[pos] : pos;
         xv[r][q] = col >= 0 ? p.x[col] : 0.0;
       }
     unsigned cn[NR][B];
@@ -899,7 +908,7 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
 // Persistent grid (the tables are staged once per workgroup); each XCD's
 // workgroups walk its contiguous share of the row blocks, NR consecutive
 // blocks at a time.
-template <int OP, bool CFSEL, int B, bool MAP, int NR>
+template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK>
 __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
   extern __shared__ double vt[];  // nvtab doubles, then notab ints
   int* ot = reinterpret_cast<int*>(vt + p.nvtab);
@@ -911,7 +920,7 @@ __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
   const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
   const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
   for (int rb = r0 + (int)(blockIdx.x >> 3) * NR; rb < r1; rb += per_wg * NR)
-    code_rows_op<OP, CFSEL, B, MAP, NR>(p, vt, ot, rb);
+    code_rows_op<OP, CFSEL, B, MAP, NR, PK>(p, vt, ot, rb);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -1706,8 +1715,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_P
     return hipGetLastError();
   }
-  if (M.code16) {  // offset-coded entries (P_0 / R_0 of a grid hierarchy)
+  if (M.code16 || M.code32) {  // offset-coded (P_0 / R_0 of a grid hierarchy) or packed entries
     a.code16 = M.code16;
+    a.code32 = M.code32;
     a.otab = M.otab;
     a.notab = M.notab;
     a.vbits = M.vbits;
@@ -1720,8 +1730,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     const int nr = knob(0) > 0 ? knob(0) : 1;   // row blocks per workgroup step
     const int cb = knob(1) > 0 ? knob(1) : 8;   // codes per batch
 #define HVE_C2(OPV, CF, BB, NRV)                                                                  \
-  if (map) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, true, NRV>), cgrid, block, lds, s, a);  \
-  else hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV>), cgrid, block, lds, s, a);
+  if (M.code32) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, true>), cgrid, block, lds, s, a); \
+  else if (map) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, true, NRV, false>), cgrid, block, lds, s, a); \
+  else hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, false>), cgrid, block, lds, s, a);
 #define HVE_C(OPV, CF)                                                    \
   if (CF) { HVE_C2(OPV, CF, 8, 1) }                                        \
   else if (nr == 2 && cb == 4) { HVE_C2(OPV, CF, 4, 2) }                  \

@@ -51,7 +51,7 @@ static int sell_valtab_env() {
 void DevSell::set_block_order(const std::vector<int>& stored_to_local, const std::vector<int64_t>& key) {
   if (key.empty() || nrows <= 0) return;
   // the row block one workgroup of the chosen loop runs (kernels.hip launch_sell)
-  const int unit = col16 ? 64 * dict_group : slot_mask ? 256 * stencil_slices_per_wave() : (delta_like() || vidx16 || code16) ? 256 : (wide && !rowlen) ? 64 : 256;
+  const int unit = col16 ? 64 * dict_group : slot_mask ? 256 * stencil_slices_per_wave() : (delta_like() || vidx16 || code16 || code32) ? 256 : (wide && !rowlen) ? 64 : 256;
   const int nb = (nrows + unit - 1) / unit;
   std::vector<int64_t> bk(nb);
   for (int b = 0; b < nb; ++b) {
@@ -92,6 +92,36 @@ void DevSell::build_wave_map() {
   }
   wave_map = dupload(m.data(), m.size());
   nwave = nb * 4;
+}
+
+// Packed SELL-64 entries (k_sell_code PK): code = ((col - base[slice]) << vbits)
+// | value index, base = the slice's smallest column, padding 0xFFFFFFFF.  false
+// when some slice's column span does not fit 32 - vbits bits (all-ones span
+// reserved, so no entry equals the padding code).
+static bool pack_sell_codes(const std::vector<int>& sp, const std::vector<int>& col,
+                            const std::vector<unsigned short>& vi, int nv, std::vector<unsigned>& code,
+                            std::vector<int>& base, int& vbits) {
+  int vb = 1;
+  while ((1 << vb) < nv) ++vb;
+  const int ns = (int)sp.size() - 1;
+  const int64_t lim = (int64_t(1) << (32 - vb)) - 1;
+  base.assign(ns + 1, 0);  // one past the last: the kernel's scalar load may run ahead
+  code.assign(col.size(), 0xFFFFFFFFu);
+  int ok = 1;
+#pragma omp parallel for schedule(static) reduction(min : ok)
+  for (int s = 0; s < ns; ++s) {
+    int lo = INT32_MAX, hi = -1;
+    for (int q = sp[s]; q < sp[s + 1]; ++q)
+      if (col[q] >= 0) { lo = std::min(lo, col[q]); hi = std::max(hi, col[q]); }
+    if (hi < 0) continue;
+    if ((int64_t)hi - lo >= lim) { ok = 0; continue; }
+    base[s] = lo;
+    for (int q = sp[s]; q < sp[s + 1]; ++q)
+      if (col[q] >= 0) code[q] = ((unsigned)(col[q] - lo) << vb) | vi[q];
+  }
+  if (!ok) return false;
+  vbits = vb;
+  return true;
 }
 
 void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy, const std::vector<int64_t>* key,
@@ -486,20 +516,39 @@ dict:
   pipe = (jag || batch == 16 || avg_row < 5.0) ? 1 : 0;
   if (jag) rowlen = dupload(rl.data(), rl.size());
   slice_ptr = dupload(sp.data(), sp.size());
-  this->col = dupload(col.data(), col.size());
   // 16-bit indices into the operator's distinct values where at most 4096
   // occur (P and R of the 7-point hierarchy at every size: ~1200), off for the
   // workgroup-per-slice loop of small operators.  HVE_SELL_VALTAB=0 turns it off.
   std::vector<unsigned short> vi16;
   std::vector<double> tab;
-  const bool try_vt16 = policy == 8 || policy == 9 || (policy == 0 && !wide && sell_valtab_env() != 0);
+  const bool try_vt16 = policy == 8 || policy == 9 || policy == 13 || (policy == 0 && !wide && sell_valtab_env() != 0);
   if (try_vt16 && A.nnz() > 0 && build_value_table16(val, 4096, vi16, tab)) {
-    vidx16 = dupload(vi16.data(), vi16.size());
     vtab = dupload(tab.data(), tab.size());
     nvtab = (int)tab.size();
     wide = 0;
     pipe = 1;
+    // Packed 32-bit entries (column - slice base, value index): 4 B instead of
+    // 6 where every slice's column span fits the bits the value index leaves
+    // (P_0: ~1200 values, 21 bits of span).  Measured on MI355X at 512^3:
+    // P_0 1.32 -> 0.99 ms; R_0 1.63 ms, no better than the offset-coded 1.62
+    // (which it takes first).  Interpolation and restriction only (coded
+    // given: the loop has no Jacobi epilogue).  HVE_SELL_PACK=0 turns it off;
+    // policy 13 forces it.
+    static const int pack_env = [] {
+      const char* e = getenv("HVE_SELL_PACK");
+      return e ? atoi(e) : 1;
+    }();
+    std::vector<unsigned> c32;
+    std::vector<int> sbase;
+    if (!jag && coded && (policy == 13 || (policy == 0 && pack_env != 0)) && pack_sell_codes(sp, col, vi16, nvtab, c32, sbase, vbits)) {
+      code32 = dupload(c32.data(), c32.size());
+      slot_base = dupload(sbase.data(), sbase.size());
+    } else {
+      this->col = dupload(col.data(), col.size());
+      vidx16 = dupload(vi16.data(), vi16.size());
+    }
   } else {
+    this->col = dupload(col.data(), col.size());
     this->val = dupload(val.data(), val.size());
   }
   // stored row i -> local output row: subset map composed with the sort order
@@ -576,6 +625,8 @@ void DevSell::release() {
   if (dict) (void)hipFree(dict);
   if (dcol) (void)hipFree(dcol);
   if (slot_base) (void)hipFree(slot_base);
+  if (code32) (void)hipFree(code32);
+  code32 = nullptr;
   if (vidx) (void)hipFree(vidx);
   if (vidx16) (void)hipFree(vidx16);
   if (vtab) (void)hipFree(vtab);
@@ -640,7 +691,7 @@ void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key
   in.upload(op.interior, op.map_int, policy, key, coded, tile);
   if (tlog)
     fprintf(stderr, "[upload] %d rows %lld nnz: %s %.3fs\n", op.interior.nrows, (long long)op.interior.nnz(),
-            in.code16 ? "coded" : in.slot_mask ? "stencil" : in.col16 ? "dict" : in.vidx16 ? "vt16" : in.rowlen ? "jagged"
+            in.code16 ? "coded" : in.code32 ? "packed" : in.slot_mask ? "stencil" : in.col16 ? "dict" : in.vidx16 ? "vt16" : in.rowlen ? "jagged"
             : in.wide ? "wide" : "padded", now() - t0);
   bd.upload(op.boundary, op.map_bnd, policy);
   nrows_local = op.nrows_local;
@@ -983,8 +1034,10 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       // grid context of P_l / R_l for the offset-coded layout: the fine point
       // of each local coarse point (fc) and its inverse (cidx, -1 at F points)
       std::vector<int> fc, cidx;
+      // (given without members where there is no grid context: the operator
+      // is still known to be P / R, which the packed layout is limited to)
       DevSell::Coded cp, cr;
-      const DevSell::Coded *pc = nullptr, *rc = nullptr;
+      const DevSell::Coded *pc = &cp, *rc = &cr;
       if (!L.cf.empty() && (int)L.cf.size() >= L.n_loc) {
         cidx.assign(L.n_loc, -1);
         for (int i = 0; i < L.n_loc; ++i)
@@ -996,8 +1049,6 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
           cp.colpos = &fc;
           cp.cmap = &cidx;
           cr.anc = &fc;
-          pc = &cp;
-          rc = &cr;
         }
       }
       D.P.upload(L.P, prm.sell_policy, kl, pc);

@@ -70,6 +70,9 @@ struct DevSell {
   int* anc = nullptr;
   int* cmap = nullptr;
   int64_t anc_n = 0, cmap_n = 0;
+  // packed layout (SellView::code32): one 32-bit code per slot, the slice
+  // bases in slot_base, the values in vtab
+  unsigned* code32 = nullptr;
   SellView view() const {
     SellView v;
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
@@ -78,6 +81,7 @@ struct DevSell {
     v.slot_vi = slot_vi; v.slot_mask = slot_mask; v.stencil_w = stencil_w; v.slice_pat = slice_pat;
     v.blk_map = blk_map; v.nblk = nblk; v.wave_map = wave_map; v.nwave = nwave;
     v.code16 = code16; v.otab = otab; v.notab = notab; v.vbits = vbits; v.anc = anc; v.cmap = cmap;
+    v.code32 = code32;
     return v;
   }
   // Grid context of an interpolation / restriction operator for the
@@ -115,6 +119,8 @@ struct DevSell {
     if (code16)  // offset-coded: 2 B a slot, the anchors, the position -> column map once
       return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * 2 + (size_t)(anc_n + cmap_n) * 4 +
              (rowmap ? (size_t)nrows * 4 : 0);
+    if (code32)  // packed: 4 B a slot, a base per slice
+      return (size_t)(nslices + 1) * 8 + (size_t)nnz_pad * 4 + (rowmap ? (size_t)nrows * 4 : 0);
     const size_t colb = dcol || col16 ? 2 : 4;
     const size_t valb = vidx ? 1 : vidx16 ? 2 : 8;
     size_t b = (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * (colb + valb);

@@ -258,7 +258,8 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands,
  * mask; nothing stored per entry) where an operator is a constant-coefficient
  * stencil, else as 7, 12 offset-coded P and R (one 16-bit code per entry:
  * offset from the row's grid point and value index) where they build, else
- * padded.  All give identical bits; the forced settings exist for parity tests
+ * padded, 13 packed P and R (one 32-bit code per entry: column less the
+ * slice's smallest column, and value index) where they fit, else as 8.  All give identical bits; the forced settings exist for parity tests
  * and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* One GPU runs the hybrid Gauss-Seidel smoothers with the row blocks of an
@@ -339,7 +340,7 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver solver, HYPRE_Real *byte
  * 4 dictionary, 5 16-bit column deltas, 6 deltas + 8-bit value table,
  * 7 deltas + 16-bit value table, 8 padded + 16-bit value table, 9 jagged +
  * 16-bit value table, 10 range dictionary, 11 slot-uniform stencil,
- * 12 offset-coded (P, R). */
+ * 12 offset-coded (P, R), 13 packed 32-bit codes (P, R). */
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int *kind);
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */

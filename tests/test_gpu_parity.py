@@ -99,7 +99,7 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen, wt):
     assert np.array_equal(x.get(), xo)
 
 
-@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
 def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
@@ -107,7 +107,7 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     x-tile, padded with 16-bit column deltas, the same with a value table,
     padded / jagged with 16-bit value indices, the slot-uniform stencil
     layout where an operator is a constant-coefficient stencil, offset-coded P
-    and R where they build) forced on every
+    and R where they build, packed 32-bit P and R codes) forced on every
     operator of the hierarchy: the same bits as the oracle.  The automatic
     choice only uses jagged and wide loops on operators too large for the
     other tests, so this is where those loops meet the oracle."""
@@ -117,6 +117,8 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     n = A.n
     if policy == 12:  # the layout is really taken (level 0's P and R)
         assert amg.level_layout(0, 1) == "coded" and amg.level_layout(0, 2) == "coded"
+    if policy == 13:
+        assert amg.level_layout(0, 1) == "packed" and amg.level_layout(0, 2) == "packed"
     rng = np.random.default_rng(23 + policy)
     f_h = rng.standard_normal(n)
     u0 = rng.standard_normal(n)
