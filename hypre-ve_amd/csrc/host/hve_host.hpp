@@ -125,7 +125,7 @@ struct AMGParams {
   int coarsen_type = 10;          // 8 PMIS, 9 PMIS(seq rand), 10 HMIS
   int measure_type = 0;
   int coarsen_cut_factor = 0;
-  int interp_type = 6;            // 6 ext+i, 3 direct
+  int interp_type = 6;            // 6 ext+i, 14 ext, 18 ext+e (MM), 3 direct
   int P_max_elmts = 4;
   double trunc_factor = 0.0;
   // grid_relax_type (par_amg.c:218-220, 339-341: [0] keeps the 3 of the
@@ -258,8 +258,12 @@ void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, i
                              std::vector<int>& cf, const int* full_row_len = nullptr);
 void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
                   const std::vector<int>* rs = nullptr);
+// plus_i false: extended interpolation (interp_type 14) instead of ext+i
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
-                        double trunc_factor, int max_elmts, CSR& P);
+                        double trunc_factor, int max_elmts, CSR& P, bool plus_i = true);
+// extended+e in matrix-matrix form (interp_type 18, par_mod_lr_interp.c:1040)
+void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                           int max_elmts, CSR& P);
 void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                          double trunc_factor, int max_elmts, CSR& P);
 void truncate_rows(CSR& P, double tol, int max_elmts);
@@ -272,13 +276,13 @@ void build_multipass_interp(const CSR& A, const std::vector<int>& cf, const Patt
 // Universe-indexed cores of ext+i and RAP shared by the one-process and the
 // distributed setup (see setup.cpp).
 void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
-                int nrows, int ncoarse, int nuniv, CSR& P);
+                int nrows, int ncoarse, int nuniv, CSR& P, bool plus_i = true);
 void rap_core(const CSR& R, const CSR& A, const CSR& P, const std::vector<int>& row_ic,
               const std::vector<int>& coarse_glob, int nfine_univ, int ncoarse_univ, int ncoarse_glob, CSR& C);
 // Their single rows (the device versions finish rows that overflow LDS here).
 int extpi_row_count(const Pattern& S, const std::vector<int>& cf, int i, RowMap& M);
 void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
-                    int i, RowMap& M, CSR& P);
+                    int i, RowMap& M, CSR& P, bool plus_i = true);
 void rap_row(const CSR& R, const CSR& A, const CSR& P, int q, int ic, RapScratch& W);
 // row lists of the device setup's host fallback, and its table bounds
 int64_t extpi_bound_max(const Pattern& S);

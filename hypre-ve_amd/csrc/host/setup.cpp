@@ -850,8 +850,12 @@ int extpi_row_count(const Pattern& S, const std::vector<int>& cf, int i, RowMap&
   return cnt;
 }
 // second pass: row i into P.j / P.a from P.i[i] on
+// plus_i false: extended interpolation (interp_type 14, par_lr_interp.c:4686
+// hypre_BoomerAMGBuildExtInterpHost, weight loop :5194-5262): a strong F
+// neighbour's connection is distributed over C-hat_i only, i itself takes no
+// share, so the sum and the distribution leave out a_{i1,i}.
 void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
-                    int i, RowMap& M, CSR& P) {
+                    int i, RowMap& M, CSR& P, bool plus_i) {
   constexpr int kNone = -1, kStrongF = -2;
   const int jj_begin_row = P.i[i];
   int jc = jj_begin_row;
@@ -892,7 +896,7 @@ void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, 
       if (A.a[A.i[i1]] < 0) sgn = -1;
       for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
         int i2 = A.j[jj1];
-        if ((M.get(i2, kNone) >= 0 || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
+        if ((M.get(i2, kNone) >= 0 || (plus_i && i2 == i)) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
       }
       if (sum != 0) {
         double distribute = A.a[jj] / sum;
@@ -900,7 +904,7 @@ void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, 
           int i2 = A.j[jj1];
           const int m2 = M.get(i2, kNone);
           if (m2 >= 0 && (sgn * A.a[jj1]) < 0) P.a[m2] += distribute * A.a[jj1];
-          if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
+          if (plus_i && i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
         }
       } else {
         diagonal += A.a[jj];
@@ -976,7 +980,7 @@ void rap_row_list(const CSR& R, const CSR& A, const CSR& P, const std::vector<in
 }
 
 void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, const std::vector<int>& fine_to_coarse,
-                int nrows, int ncoarse, int nuniv, CSR& P) {
+                int nrows, int ncoarse, int nuniv, CSR& P, bool plus_i) {
   (void)nuniv;
   const int n = nrows;
   P.resize_rows(n, ncoarse);
@@ -995,12 +999,12 @@ void extpi_core(const CSR& A, const Pattern& S, const std::vector<int>& cf, cons
   {
     RowMap M;
 #pragma omp for schedule(static)
-    for (int i = 0; i < n; ++i) extpi_row_fill(A, S, cf, fine_to_coarse, i, M, P);
+    for (int i = 0; i < n; ++i) extpi_row_fill(A, S, cf, fine_to_coarse, i, M, P, plus_i);
   }
 }
 
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
-                        double trunc_factor, int max_elmts, CSR& P) {
+                        double trunc_factor, int max_elmts, CSR& P, bool plus_i) {
   const int n = A.nrows;
   std::vector<int> fine_to_coarse(n, -1);
   int coarse_counter = 0;
@@ -1008,12 +1012,135 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
     if (cf[i] >= 0) fine_to_coarse[i] = coarse_counter++;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   double t0 = now();
-  extpi_core(A, S, cf, fine_to_coarse, n, coarse_counter, n, P);
+  extpi_core(A, S, cf, fine_to_coarse, n, coarse_counter, n, P, plus_i);
   double t1 = now();
   if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
   if (getenv("HVE_SETUP_T")) fprintf(stderr, "extpi core %.3f trunc %.3f\n", t1 - t0, now() - t1);
   for (int i = 0; i < n; ++i)
     if (cf[i] == SF_PT) cf[i] = F_PT;
+}
+
+// ---------------------------------------------------------------------------
+// Extended+e interpolation in matrix-matrix form (interp_type 18):
+// par_mod_lr_interp.c:1040 hypre_BoomerAMGBuildModExtPEInterpHost, one
+// process.  As_FF / As_FC (F rows; the diagonal, then the strong F resp. C
+// neighbours in S's order, values from A) as gen_fffc.c:19
+// hypre_ParCSRMatrixGenerateFFFC; the diagonal scalings of :1204-1318; W =
+// As_FF As_FC as par_csr_matop.c:277 hypre_ParMatmul (rows in first-touch
+// order, a new entry assigned its first product); P's F rows are W's rows.
+// SF points (-3) count as F and keep their marker (the reference does not
+// reset it here).
+// ---------------------------------------------------------------------------
+void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                           int max_elmts, CSR& P) {
+  const int n = A.nrows;
+  std::vector<int> f2f(n, -1), f2c(n, -1), frow;
+  int nC = 0;
+  for (int i = 0; i < n; ++i) {
+    if (cf[i] > 0) f2c[i] = nC++;
+    else { f2f[i] = (int)frow.size(); frow.push_back(i); }
+  }
+  const int nF = (int)frow.size();
+  // As_FF / As_FC
+  std::vector<int> ffi(nF + 1, 0), fci(nF + 1, 0);
+  for (int r = 0; r < nF; ++r) {
+    const int i = frow[r];
+    int nff = 1, nfc = 0;
+    for (int q = S.i[i]; q < S.i[i + 1]; ++q) (cf[S.j[q]] > 0 ? nfc : nff)++;
+    ffi[r + 1] = ffi[r] + nff;
+    fci[r + 1] = fci[r] + nfc;
+  }
+  std::vector<int> ffj(ffi[nF]), fcj(fci[nF]);
+  std::vector<double> ffa(ffi[nF]), fca(fci[nF]);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r) {
+    const int i = frow[r];
+    int a = ffi[r], c = fci[r];
+    ffj[a] = f2f[A.j[A.i[i]]];
+    ffa[a++] = A.a[A.i[i]];
+    for (int q = S.i[i]; q < S.i[i + 1]; ++q) {
+      const int js = S.j[q];
+      int ja = A.i[i] + 1;
+      while (A.j[ja] != js) ja++;  // gen_fffc.c: the first match after the diagonal
+      if (cf[js] > 0) { fcj[c] = f2c[js]; fca[c++] = A.a[ja]; }
+      else { ffj[a] = f2f[js]; ffa[a++] = A.a[ja]; }
+    }
+  }
+  std::vector<double> lam(nF, 0.0), beta(nF, 0.0), tmp(nF, 0.0), dw(nF, 0.0), tau(nF, 0.0);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r) {
+    for (int q = ffi[r] + 1; q < ffi[r + 1]; ++q) lam[r] += ffa[q];
+    const double number = (double)(ffi[r + 1] - ffi[r] - 1);
+    if (number) lam[r] /= number;
+    for (int q = fci[r]; q < fci[r + 1]; ++q) beta[r] += fca[q];
+    if (lam[r] + beta[r]) tmp[r] = lam[r] / (beta[r] + lam[r]);
+  }
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r) {
+    const int i = frow[r];
+    for (int q = A.i[i]; q < A.i[i + 1]; ++q) dw[r] += A.a[q];
+    for (int q = ffi[r] + 1; q < ffi[r + 1]; ++q) dw[r] -= ffa[q];
+    dw[r] -= beta[r];
+    for (int q = ffi[r] + 1; q < ffi[r + 1]; ++q) tau[r] += ffa[q] * tmp[ffj[q]];
+  }
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r) {
+    double value = dw[r] + tau[r];
+    if (value) value = -1.0 / value;
+    double theta = beta[r] + lam[r];
+    ffa[ffi[r]] = value * theta;
+    if (theta) theta = 1.0 / theta;
+    for (int q = ffi[r] + 1; q < ffi[r + 1]; ++q) ffa[q] *= value;
+    for (int q = fci[r]; q < fci[r + 1]; ++q) fca[q] *= theta;
+  }
+  // W = As_FF As_FC; hypre_ParMatmul seeds each row with a zero diagonal entry
+  // when the product is square (nF == nC)
+  const bool square = nF == nC;
+  std::vector<int> wlen(nF, 0);
+  std::vector<std::vector<int>> wj(nF);
+  std::vector<std::vector<double>> wa(nF);
+#pragma omp parallel
+  {
+    std::vector<int> mark(std::max(nC, 1), -1);
+    std::vector<int> touched;
+#pragma omp for schedule(dynamic, 256)
+    for (int r = 0; r < nF; ++r) {
+      std::vector<int>& rj = wj[r];
+      std::vector<double>& ra = wa[r];
+      touched.clear();
+      if (square) { mark[r] = 0; rj.push_back(r); ra.push_back(0.0); touched.push_back(r); }
+      for (int q = ffi[r]; q < ffi[r + 1]; ++q) {
+        const double ae = ffa[q];
+        const int k = ffj[q];
+        for (int t = fci[k]; t < fci[k + 1]; ++t) {
+          const int c = fcj[t];
+          if (mark[c] < 0) {
+            mark[c] = (int)rj.size();
+            touched.push_back(c);
+            rj.push_back(c);
+            ra.push_back(ae * fca[t]);
+          } else {
+            ra[mark[c]] += ae * fca[t];
+          }
+        }
+      }
+      for (int c : touched) mark[c] = -1;
+      wlen[r] = (int)rj.size();
+    }
+  }
+  P.resize_rows(n, nC);
+  for (int i = 0; i < n; ++i) P.i[i + 1] = P.i[i] + (cf[i] > 0 ? 1 : wlen[f2f[i]]);
+  P.j.resize(P.i[n]);
+  P.a.resize(P.i[n]);
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    const int b = P.i[i];
+    if (cf[i] > 0) { P.j[b] = f2c[i]; P.a[b] = 1.0; continue; }
+    const int r = f2f[i];
+    std::copy(wj[r].begin(), wj[r].end(), P.j.begin() + b);
+    std::copy(wa[r].begin(), wa[r].end(), P.a.begin() + b);
+  }
+  if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
 }
 
 // Direct interpolation (interp_type 3): par_interp.c hypre_BoomerAMGBuildDirInterp
@@ -1715,7 +1842,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   if (rank_starts && rank_starts->size() > 2) {
     emul = *rank_starts;
     if (emul.front() != 0 || emul.back() != A0.nrows) throw std::runtime_error("rank emulation: row starts do not cover A");
-    if (prm.interp_type != 6) throw std::runtime_error("rank emulation: only ext+i interpolation is restated");
+    if (prm.interp_type != 6 && prm.interp_type != 14)
+      throw std::runtime_error("rank emulation: only ext+i and ext interpolation are restated");
     rank_order_rows(H.lev[0].A, emul, emul);
   }
   const std::vector<int>* rs = emul.empty() ? nullptr : &emul;
@@ -1790,7 +1918,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         rank_order_rows(P, emul, cs);
       }
     }
-    else if (prm.interp_type == 6 && !emul.empty()) {
+    else if ((prm.interp_type == 6 || prm.interp_type == 14) && !emul.empty()) {
       // par_csr_matrix.c:2671 truncates the row [P_diag | P_offd] and splits
       // the kept entries back into the two parts in their sorted order
       std::vector<int> cs(emul.size(), 0);
@@ -1799,7 +1927,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] == 1);
         for (size_t r = 0; r < emul.size(); ++r) cs[r] = pref[emul[r]];
       }
-      build_extpi_interp(L.A, cf, S, 0.0, 0, P);
+      build_extpi_interp(L.A, cf, S, 0.0, 0, P, prm.interp_type == 6);
       rank_order_rows(P, emul, cs);
       if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
       rank_order_rows(P, emul, cs);
@@ -1818,6 +1946,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       }
     }
     else if (prm.interp_type == 6) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
+    else if (prm.interp_type == 18) build_modextpe_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
+    else if (prm.interp_type == 14) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P, false);
     else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));
     double t3 = now();

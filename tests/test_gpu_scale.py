@@ -121,6 +121,60 @@ def test_gpu_boomer_out14(gpu):
     assert rr < 1e-8
 
 
+@pytest.mark.timeout(600)
+def test_gpu_boomer_out15_ext_interp(gpu):
+    """TEST_cuda_lassen/gpu_boomer.saved out.15 (gpu_boomer.jobs:56: np 1,
+    -n 256 256 256 -pmis -keepT 1 -rlx 18 -interptype 14 -solver 1): extended
+    interpolation.  Saved: grid 1.363166, operator 2.857169, 22 iterations,
+    4.471627e-09.  Band as out.14 (the saved run used the GPU PMIS)."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(256, 256, 256)
+    kw = hv.ij_amg_defaults(1)
+    kw.update(coarsen_type=8, interp_type=14, relax_type=18)
+    amg = hv.BoomerAMG(**kw)
+    pcg = hv.PCG(tol=1e-8, max_iter=1000, two_norm=1)
+    pcg.set_precond_amg(amg)
+    n = A.n
+    b = hv.ParVector(n, np.ones(n))
+    x = hv.ParVector(n, np.zeros(n))
+    pcg.setup(A, b, x)
+    g, o, _ = amg.complexities()
+    print(f"grid {g:.6f} operator {o:.6f}")
+    assert abs(g - 1.363166) <= 0.01 * 1.363166, g
+    assert abs(o - 2.857169) <= 0.02 * 2.857169, o
+    it, rr = pcg.solve(A, b, x)
+    print(f"iterations {it} rel.res {rr:.6e}")
+    assert 20 <= it <= 24, it
+    assert rr < 1e-8
+
+
+@pytest.mark.timeout(600)
+def test_gpu_boomer_out16_modextpe_interp(gpu):
+    """TEST_cuda_lassen/gpu_boomer.saved out.16 (gpu_boomer.jobs:59: np 1,
+    -n 256 256 256 -pmis -keepT 1 -rlx 18 -interptype 18 -solver 1): ext+e
+    interpolation in matrix-matrix form.  Saved: grid 1.353558, operator
+    2.783221, 21 iterations, 3.802953e-09.  Band as out.14."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(256, 256, 256)
+    kw = hv.ij_amg_defaults(1)
+    kw.update(coarsen_type=8, interp_type=18, relax_type=18)
+    amg = hv.BoomerAMG(**kw)
+    pcg = hv.PCG(tol=1e-8, max_iter=1000, two_norm=1)
+    pcg.set_precond_amg(amg)
+    n = A.n
+    b = hv.ParVector(n, np.ones(n))
+    x = hv.ParVector(n, np.zeros(n))
+    pcg.setup(A, b, x)
+    g, o, _ = amg.complexities()
+    print(f"grid {g:.6f} operator {o:.6f}")
+    assert abs(g - 1.353558) <= 0.01 * 1.353558, g
+    assert abs(o - 2.783221) <= 0.02 * 2.783221, o
+    it, rr = pcg.solve(A, b, x)
+    print(f"iterations {it} rel.res {rr:.6e}")
+    assert 19 <= it <= 23, it
+    assert rr < 1e-8
+
+
 @pytest.mark.timeout(900)
 def test_gpu_boomer_out5_loopback4(gpu):
     """TEST_cuda_lassen/gpu_boomer.saved out.5 (gpu_boomer.jobs:24: mpirun -np 4
