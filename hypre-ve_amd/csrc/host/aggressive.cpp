@@ -84,6 +84,15 @@ void correct_cf_marker(std::vector<int>& cf, const std::vector<int>& new_cf) {
   }
 }
 
+// par_strength.c:2978 (2-stage interpolations): a first-pass C point the
+// second pass makes F becomes -2, every other one 1.
+void correct_cf_marker2(std::vector<int>& cf, const std::vector<int>& new_cf) {
+  int cnt = 0;
+  for (size_t i = 0; i < cf.size(); ++i) {
+    if (cf[i] > 0) cf[i] = new_cf[cnt++] == -1 ? -2 : 1;
+  }
+}
+
 // par_multi_interp.c:16 hypre_BoomerAMGBuildMultipass, num_procs 1, one
 // thread, num_functions 1, weight_option 0.
 //   * pass 0: C points (P row: the point itself, weight 1);

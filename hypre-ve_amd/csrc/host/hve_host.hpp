@@ -271,6 +271,14 @@ void truncate_rows(CSR& P, double tol, int max_elmts);
 // :2957 CorrectCFMarker, par_multi_interp.c:16 BuildMultipass.
 void create_2nd_strength(const Pattern& S, std::vector<int>& cf, int num_paths, Pattern& S2);
 void correct_cf_marker(std::vector<int>& cf, const std::vector<int>& new_cf);
+void correct_cf_marker2(std::vector<int>& cf, const std::vector<int>& new_cf);
+// matrix-matrix interpolations (setup.cpp): ModExt (pe false) / ModExtPE, the
+// 2-stage second stage ModPartialExt, and P = P1 P2 with the aggressive truncation
+void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                         int max_elmts, bool pe, CSR& P);
+void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                                int max_elmts, CSR& P);
+void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P);
 void build_multipass_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                             int max_elmts, CSR& P);
 // Universe-indexed cores of ext+i and RAP shared by the one-process and the

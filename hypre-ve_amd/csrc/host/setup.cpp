@@ -1021,126 +1021,260 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
 }
 
 // ---------------------------------------------------------------------------
-// Extended+e interpolation in matrix-matrix form (interp_type 18):
-// par_mod_lr_interp.c:1040 hypre_BoomerAMGBuildModExtPEInterpHost, one
-// process.  As_FF / As_FC (F rows; the diagonal, then the strong F resp. C
-// neighbours in S's order, values from A) as gen_fffc.c:19
-// hypre_ParCSRMatrixGenerateFFFC; the diagonal scalings of :1204-1318; W =
-// As_FF As_FC as par_csr_matop.c:277 hypre_ParMatmul (rows in first-touch
-// order, a new entry assigned its first product); P's F rows are W's rows.
-// SF points (-3) count as F and keep their marker (the reference does not
-// reset it here).
+// Interpolation in matrix-matrix form (par_mod_lr_interp.c, par_2s_interp.c),
+// one process.  The pieces:
+// * fffc: As_FF / As_FC as gen_fffc.c:19 hypre_ParCSRMatrixGenerateFFFC
+//   (partial = false: rows = F points, CF < 0) or gen_fffc.c:506
+//   hypre_ParCSRMatrixGenerateFFFC3 (partial = true: As_FF rows = the -2
+//   points only, As_FC rows = every F point).  An As_FF row is the diagonal,
+//   then the strong non-C neighbours (columns: index among the non-C points);
+//   an As_FC row the strong C neighbours (columns: coarse index); both in S's
+//   order, values from A (the first match after the diagonal).
+// * matmul_first_touch: hypre_ParMatmul (par_csr_matop.c:277), the CPU
+//   build's product for W = As_FF As_FC and P = P1 P2.
+// SF points (-3) count as F and keep their marker (these builders do not
+// reset it, unlike ext+i).
 // ---------------------------------------------------------------------------
-void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P) {
+static void fffc(const CSR& A, const std::vector<int>& cf, const Pattern& S, bool partial, CSR& FF, CSR& FC,
+                 std::vector<int>& frow, std::vector<int>& ffrow) {
   const int n = A.nrows;
-  std::vector<int> f2f(n, -1), f2c(n, -1), frow;
-  int nC = 0;
+  std::vector<int> f2f(n, -1), f2c(n, -1);
+  int nC = 0, nF = 0;
+  frow.clear();
+  ffrow.clear();
   for (int i = 0; i < n; ++i) {
     if (cf[i] > 0) f2c[i] = nC++;
-    else { f2f[i] = (int)frow.size(); frow.push_back(i); }
+    else f2f[i] = nF++;
+    if (cf[i] < 0) frow.push_back(i);
+    if (partial ? cf[i] == -2 : cf[i] < 0) ffrow.push_back(i);
   }
-  const int nF = (int)frow.size();
-  // As_FF / As_FC
-  std::vector<int> ffi(nF + 1, 0), fci(nF + 1, 0);
-  for (int r = 0; r < nF; ++r) {
+  const int nfr = (int)frow.size(), nff = (int)ffrow.size();
+  FC.resize_rows(nfr, nC);
+  FF.resize_rows(nff, nF);
+  for (int r = 0; r < nfr; ++r) {
     const int i = frow[r];
-    int nff = 1, nfc = 0;
-    for (int q = S.i[i]; q < S.i[i + 1]; ++q) (cf[S.j[q]] > 0 ? nfc : nff)++;
-    ffi[r + 1] = ffi[r] + nff;
-    fci[r + 1] = fci[r] + nfc;
+    int c = 0;
+    for (int q = S.i[i]; q < S.i[i + 1]; ++q) c += cf[S.j[q]] > 0;
+    FC.i[r + 1] = FC.i[r] + c;
   }
-  std::vector<int> ffj(ffi[nF]), fcj(fci[nF]);
-  std::vector<double> ffa(ffi[nF]), fca(fci[nF]);
+  for (int r = 0; r < nff; ++r) {
+    const int i = ffrow[r];
+    int c = 1;
+    for (int q = S.i[i]; q < S.i[i + 1]; ++q) c += cf[S.j[q]] <= 0;
+    FF.i[r + 1] = FF.i[r] + c;
+  }
+  FC.j.resize(FC.i[nfr]);
+  FC.a.resize(FC.i[nfr]);
+  FF.j.resize(FF.i[nff]);
+  FF.a.resize(FF.i[nff]);
+  auto aval = [&](int i, int js) {
+    int ja = A.i[i] + 1;
+    while (A.j[ja] != js) ja++;
+    return A.a[ja];
+  };
 #pragma omp parallel for schedule(static)
-  for (int r = 0; r < nF; ++r) {
+  for (int r = 0; r < nfr; ++r) {
     const int i = frow[r];
-    int a = ffi[r], c = fci[r];
-    ffj[a] = f2f[A.j[A.i[i]]];
-    ffa[a++] = A.a[A.i[i]];
-    for (int q = S.i[i]; q < S.i[i + 1]; ++q) {
-      const int js = S.j[q];
-      int ja = A.i[i] + 1;
-      while (A.j[ja] != js) ja++;  // gen_fffc.c: the first match after the diagonal
-      if (cf[js] > 0) { fcj[c] = f2c[js]; fca[c++] = A.a[ja]; }
-      else { ffj[a] = f2f[js]; ffa[a++] = A.a[ja]; }
+    int c = FC.i[r];
+    for (int q = S.i[i]; q < S.i[i + 1]; ++q)
+      if (cf[S.j[q]] > 0) { FC.j[c] = f2c[S.j[q]]; FC.a[c++] = aval(i, S.j[q]); }
+  }
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nff; ++r) {
+    const int i = ffrow[r];
+    int c = FF.i[r];
+    FF.j[c] = f2f[A.j[A.i[i]]];
+    FF.a[c++] = A.a[A.i[i]];
+    for (int q = S.i[i]; q < S.i[i + 1]; ++q)
+      if (cf[S.j[q]] <= 0) { FF.j[c] = f2f[S.j[q]]; FF.a[c++] = aval(i, S.j[q]); }
+  }
+}
+
+static void matmul_first_touch(const CSR& X, const CSR& Y, CSR& C) {
+  const int nr = X.nrows, nc = Y.ncols;
+  const bool square = nr == nc;  // hypre_ParMatmul's allsquare: a zero diagonal entry first
+  std::vector<std::vector<int>> cj(nr);
+  std::vector<std::vector<double>> ca(nr);
+#pragma omp parallel
+  {
+    std::vector<int> mark(std::max(nc, 1), -1);
+    std::vector<int> touched;
+#pragma omp for schedule(dynamic, 256)
+    for (int r = 0; r < nr; ++r) {
+      std::vector<int>& rj = cj[r];
+      std::vector<double>& ra = ca[r];
+      touched.clear();
+      if (square) { mark[r] = 0; rj.push_back(r); ra.push_back(0.0); touched.push_back(r); }
+      for (int q = X.i[r]; q < X.i[r + 1]; ++q) {
+        const double ae = X.a[q];
+        const int k = X.j[q];
+        for (int t = Y.i[k]; t < Y.i[k + 1]; ++t) {
+          const int c = Y.j[t];
+          if (mark[c] < 0) {
+            mark[c] = (int)rj.size();
+            touched.push_back(c);
+            rj.push_back(c);
+            ra.push_back(ae * Y.a[t]);
+          } else {
+            ra[mark[c]] += ae * Y.a[t];
+          }
+        }
+      }
+      for (int c : touched) mark[c] = -1;
     }
   }
+  C.resize_rows(nr, nc);
+  for (int r = 0; r < nr; ++r) C.i[r + 1] = C.i[r] + (int)cj[r].size();
+  C.j.resize(C.i[nr]);
+  C.a.resize(C.i[nr]);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nr; ++r) {
+    std::copy(cj[r].begin(), cj[r].end(), C.j.begin() + C.i[r]);
+    std::copy(ca[r].begin(), ca[r].end(), C.a.begin() + C.i[r]);
+  }
+}
+
+// P's rows: `rows` (fine points, in order) are C points (cf > 0: injection at
+// their coarse index) or take the next row of W.
+static void assemble_mm_p(const std::vector<int>& cf, const std::vector<int>& rows, const CSR& W, int ncoarse,
+                          CSR& P) {
+  const int n = (int)rows.size();
+  P.resize_rows(n, ncoarse);
+  std::vector<int> wr(n, -1);
+  int c = 0, w = 0;
+  for (int r = 0; r < n; ++r) {
+    if (cf[rows[r]] > 0) { P.i[r + 1] = P.i[r] + 1; ++c; }
+    else { wr[r] = w; P.i[r + 1] = P.i[r] + (W.i[w + 1] - W.i[w]); ++w; }
+  }
+  P.j.resize(P.i[n]);
+  P.a.resize(P.i[n]);
+  c = 0;
+  for (int r = 0; r < n; ++r) {
+    const int b = P.i[r];
+    if (wr[r] < 0) { P.j[b] = c++; P.a[b] = 1.0; continue; }
+    std::copy(W.j.begin() + W.i[wr[r]], W.j.begin() + W.i[wr[r] + 1], P.j.begin() + b);
+    std::copy(W.a.begin() + W.i[wr[r]], W.a.begin() + W.i[wr[r] + 1], P.a.begin() + b);
+  }
+}
+
+// Extended+e (interp_type 18, agg_interp_type 7's first stage):
+// par_mod_lr_interp.c:1040 hypre_BoomerAMGBuildModExtPEInterpHost, the
+// diagonal scalings of :1204-1318.  Extended (agg_interp_type 5's first
+// stage, pe = false): :16 hypre_BoomerAMGBuildModExtInterpHost, :170-245.
+void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                         int max_elmts, bool pe, CSR& P) {
+  CSR FF, FC;
+  std::vector<int> frow, ffrow;
+  fffc(A, cf, S, false, FF, FC, frow, ffrow);
+  const int nF = (int)frow.size();
   std::vector<double> lam(nF, 0.0), beta(nF, 0.0), tmp(nF, 0.0), dw(nF, 0.0), tau(nF, 0.0);
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < nF; ++r) {
-    for (int q = ffi[r] + 1; q < ffi[r + 1]; ++q) lam[r] += ffa[q];
-    const double number = (double)(ffi[r + 1] - ffi[r] - 1);
+    for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) beta[r] += FC.a[q];
+    if (!pe) continue;
+    for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) lam[r] += FF.a[q];
+    const double number = (double)(FF.i[r + 1] - FF.i[r] - 1);
     if (number) lam[r] /= number;
-    for (int q = fci[r]; q < fci[r + 1]; ++q) beta[r] += fca[q];
     if (lam[r] + beta[r]) tmp[r] = lam[r] / (beta[r] + lam[r]);
   }
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < nF; ++r) {
     const int i = frow[r];
     for (int q = A.i[i]; q < A.i[i + 1]; ++q) dw[r] += A.a[q];
-    for (int q = ffi[r] + 1; q < ffi[r + 1]; ++q) dw[r] -= ffa[q];
+    for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) dw[r] -= FF.a[q];
     dw[r] -= beta[r];
-    for (int q = ffi[r] + 1; q < ffi[r + 1]; ++q) tau[r] += ffa[q] * tmp[ffj[q]];
+    if (pe)
+      for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) tau[r] += FF.a[q] * tmp[FF.j[q]];
   }
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < nF; ++r) {
-    double value = dw[r] + tau[r];
-    if (value) value = -1.0 / value;
-    double theta = beta[r] + lam[r];
-    ffa[ffi[r]] = value * theta;
-    if (theta) theta = 1.0 / theta;
-    for (int q = ffi[r] + 1; q < ffi[r + 1]; ++q) ffa[q] *= value;
-    for (int q = fci[r]; q < fci[r + 1]; ++q) fca[q] *= theta;
-  }
-  // W = As_FF As_FC; hypre_ParMatmul seeds each row with a zero diagonal entry
-  // when the product is square (nF == nC)
-  const bool square = nF == nC;
-  std::vector<int> wlen(nF, 0);
-  std::vector<std::vector<int>> wj(nF);
-  std::vector<std::vector<double>> wa(nF);
-#pragma omp parallel
-  {
-    std::vector<int> mark(std::max(nC, 1), -1);
-    std::vector<int> touched;
-#pragma omp for schedule(dynamic, 256)
-    for (int r = 0; r < nF; ++r) {
-      std::vector<int>& rj = wj[r];
-      std::vector<double>& ra = wa[r];
-      touched.clear();
-      if (square) { mark[r] = 0; rj.push_back(r); ra.push_back(0.0); touched.push_back(r); }
-      for (int q = ffi[r]; q < ffi[r + 1]; ++q) {
-        const double ae = ffa[q];
-        const int k = ffj[q];
-        for (int t = fci[k]; t < fci[k + 1]; ++t) {
-          const int c = fcj[t];
-          if (mark[c] < 0) {
-            mark[c] = (int)rj.size();
-            touched.push_back(c);
-            rj.push_back(c);
-            ra.push_back(ae * fca[t]);
-          } else {
-            ra[mark[c]] += ae * fca[t];
-          }
-        }
-      }
-      for (int c : touched) mark[c] = -1;
-      wlen[r] = (int)rj.size();
+    double fscale, cscale;
+    if (pe) {
+      double value = dw[r] + tau[r];
+      if (value) value = -1.0 / value;
+      double theta = beta[r] + lam[r];
+      FF.a[FF.i[r]] = value * theta;
+      if (theta) theta = 1.0 / theta;
+      fscale = value;
+      cscale = theta;
+    } else {
+      const double b = dw[r] ? 1.0 / dw[r] : 1.0;
+      FF.a[FF.i[r]] = b * beta[r];
+      fscale = b;
+      cscale = beta[r] ? -1.0 / beta[r] : 1.0;
     }
+    for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) FF.a[q] *= fscale;
+    for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) FC.a[q] *= cscale;
   }
-  P.resize_rows(n, nC);
-  for (int i = 0; i < n; ++i) P.i[i + 1] = P.i[i] + (cf[i] > 0 ? 1 : wlen[f2f[i]]);
-  P.j.resize(P.i[n]);
-  P.a.resize(P.i[n]);
-#pragma omp parallel for schedule(static)
-  for (int i = 0; i < n; ++i) {
-    const int b = P.i[i];
-    if (cf[i] > 0) { P.j[b] = f2c[i]; P.a[b] = 1.0; continue; }
-    const int r = f2f[i];
-    std::copy(wj[r].begin(), wj[r].end(), P.j.begin() + b);
-    std::copy(wa[r].begin(), wa[r].end(), P.a.begin() + b);
-  }
+  CSR W;
+  matmul_first_touch(FF, FC, W);
+  std::vector<int> all(A.nrows);
+  for (int i = 0; i < A.nrows; ++i) all[i] = i;
+  assemble_mm_p(cf, all, W, FC.ncols, P);
   if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+}
+
+void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                           int max_elmts, CSR& P) {
+  build_modext_interp(A, cf, S, trunc_factor, max_elmts, true, P);
+}
+
+// Second stage of the 2-stage aggressive interpolations (cf: 1 = C of both
+// stages, -2 = C of the first stage only): P2 from the first stage's C
+// points to the second's.  agg_interp_type 5: par_2s_interp.c:15
+// hypre_BoomerAMGBuildModPartialExtInterpHost (:180-330).
+void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                                int max_elmts, CSR& P) {
+  CSR FF, FC;
+  std::vector<int> frow, ffrow;
+  fffc(A, cf, S, true, FF, FC, frow, ffrow);
+  const int nF = (int)frow.size(), nN = (int)ffrow.size();
+  std::vector<int> f2f(A.nrows, -1);
+  {
+    int k = 0;
+    for (int i = 0; i < A.nrows; ++i)
+      if (cf[i] < 0) f2f[i] = k++;
+  }
+  std::vector<double> dq(nF, 0.0), dw(nN, 0.0);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r)
+    for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) dq[r] += FC.a[q];
+  // As_FF's columns index the non-C points; with cf in {1, -1, -2, -3} they
+  // are exactly the F rows (CF < 0), so dq is indexed by them directly
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nN; ++r) {
+    const int i = ffrow[r];
+    for (int q = A.i[i]; q < A.i[i + 1]; ++q) dw[r] += A.a[q];
+    for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q)
+      if (dq[FF.j[q]]) dw[r] -= FF.a[q];
+    dw[r] -= dq[f2f[i]];
+  }
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nN; ++r) {
+    if (!dw[r]) continue;  // the reference leaves such a row unscaled, diagonal included
+    const double b = 1.0 / dw[r];
+    FF.a[FF.i[r]] = b * dq[f2f[ffrow[r]]];
+    for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) FF.a[q] *= b;
+  }
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r) {
+    const double g = dq[r] ? -1.0 / dq[r] : 0.0;
+    for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) FC.a[q] *= g;
+  }
+  CSR W;
+  matmul_first_touch(FF, FC, W);
+  std::vector<int> c1;  // rows of P2: the first stage's C points, in order
+  for (int i = 0; i < A.nrows; ++i)
+    if (cf[i] > 0 || cf[i] == -2) c1.push_back(i);
+  assemble_mm_p(cf, c1, W, FC.ncols, P);
+  if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+}
+
+// P = P1 P2 (par_amg_setup.c:1681 hypre_ParMatmul), then the aggressive
+// truncation (:1685)
+void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P) {
+  matmul_first_touch(P1, P2, P);
+  truncate_rows(P, trunc_factor, max_elmts);
 }
 
 // Direct interpolation (interp_type 3): par_interp.c hypre_BoomerAMGBuildDirInterp
@@ -1829,9 +1963,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
-  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4)
+  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4 && prm.agg_interp_type != 5)
     throw std::runtime_error("aggressive coarsening: agg_interp_type " + std::to_string(prm.agg_interp_type) +
-                             " is not available in this build (4, multipass, is)");
+                             " is not available in this build (4 multipass, 5 2-stage extended MM)");
   if (prm.num_paths < 1) throw std::runtime_error("num_paths must be >= 1");
   int coarsen_type = prm.coarsen_type;
   H.lev.emplace_back();
@@ -1844,6 +1978,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     if (emul.front() != 0 || emul.back() != A0.nrows) throw std::runtime_error("rank emulation: row starts do not cover A");
     if (prm.interp_type != 6 && prm.interp_type != 14)
       throw std::runtime_error("rank emulation: only ext+i and ext interpolation are restated");
+    if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4)
+      throw std::runtime_error("rank emulation: only multipass aggressive interpolation is restated");
     rank_order_rows(H.lev[0].A, emul, emul);
   }
   const std::vector<int>* rs = emul.empty() ? nullptr : &emul;
@@ -1872,6 +2008,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     // par_amg_setup.c:1239-1285: aggressive levels coarsen the C points
     // again on S*S + 2S, and the second marker refines the first
     const bool agg = level < prm.agg_num_levels;
+    std::vector<int> cf1;
     if (agg) {
       Pattern S2;
       create_2nd_strength(S, cf, prm.num_paths, S2);
@@ -1896,7 +2033,12 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       } else {
         throw std::runtime_error("aggressive coarsening with coarsen_type " + std::to_string(coarsen_type));
       }
-      correct_cf_marker(cf, cfn);  // agg_interp_type 4: par_amg_setup.c:1590
+      if (prm.agg_interp_type == 4) {
+        correct_cf_marker(cf, cfn);  // agg_interp_type 4: par_amg_setup.c:1590
+      } else {
+        cf1 = cf;  // the first stage's markers, for P1
+        correct_cf_marker2(cf, cfn);  // par_amg_setup.c:1600 (par_strength.c:2978)
+      }
     }
     int coarse_size = 0;
     for (int v : cf) coarse_size += (v == 1);
@@ -1909,7 +2051,15 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     }
     if (coarse_size < prm.min_coarse_size) break;
     CSR P;
-    if (agg) {
+    if (agg && prm.agg_interp_type != 4) {
+      // 2-stage: P1 to the first stage's C points, P2 from them to the
+      // second's (par_amg_setup.c:1575-1689)
+      CSR P1, P2;
+      build_modext_interp(L.A, cf1, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, false, P1);
+      build_modpartialext_interp(L.A, cf, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, P2);
+      multiply_interp(P1, P2, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
+    }
+    else if (agg) {
       build_multipass_interp(L.A, cf, S, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
       if (!emul.empty()) {  // P_diag | P_offd
         std::vector<int> cs(emul.size(), 0), pref(cf.size() + 1, 0);

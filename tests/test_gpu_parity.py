@@ -370,3 +370,36 @@ def test_aggressive_coarsening_bitwise(gpu, orc, agg, coarsen, relax, coef):
     st = O.solve(f_h, xo, 1e-7, 80)
     assert it == st["iterations"]
     assert np.array_equal(x.get(), xo)
+
+
+@pytest.mark.parametrize("interp,agg,agg_interp", [(14, 0, 4), (18, 0, 4), (6, 1, 5), (6, 2, 5), (18, 1, 5)])
+@pytest.mark.parametrize("order", [0, 1])
+def test_interp_types_bitwise(gpu, orc, interp, agg, agg_interp, order):
+    """Extended (14), ext+e MM (18) and the 2-stage extended MM aggressive
+    interpolation (agg_interp_type 5, whose levels keep -2 markers that C/F
+    relaxation skips): one V-cycle and a solve equal the oracle's bits."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(28, 26, 24, cx=0.01)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=interp, agg_num_levels=agg, agg_interp_type=agg_interp,
+              relax_type=18, relax_order=order, tol=1e-7, max_iter=80)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup(A)
+    O = orc.OracleAMG(amg)
+    n = A.n
+    rng = np.random.default_rng(interp * 7 + agg)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+    b = hv.ParVector(n, f_h)
+    x = hv.ParVector(n, np.zeros(n))
+    it, rr = amg.solve(A, b, x)
+    xo = np.zeros(n)
+    st = O.solve(f_h, xo, 1e-7, 80)
+    assert it == st["iterations"]
+    assert np.array_equal(x.get(), xo)

@@ -206,3 +206,130 @@ def test_modextpe_interp_matches_restatement(hv, coarsen_type, dims):
     for i, (cols, vals) in enumerate(rows):
         assert pj[pi[i]:pi[i + 1]].tolist() == cols, i
         assert np.array_equal(pv[pi[i]:pi[i + 1]], np.array(vals, dtype=np.float64)), i
+
+
+def _fffc(ip, jj, vv, cf, partial):
+    """gen_fffc.c:19 (partial False) / :506 GenerateFFFC3 (partial True) on a
+    matrix whose strength pattern is its off-diagonal pattern."""
+    n = len(ip) - 1
+    f2f, f2c = {}, {}
+    for i in range(n):
+        if cf[i] > 0:
+            f2c[i] = len(f2c)
+        else:
+            f2f[i] = len(f2f)
+    frow = [i for i in range(n) if cf[i] < 0]
+    ffrow = [i for i in range(n) if (cf[i] == -2 if partial else cf[i] < 0)]
+    FC = [[[f2c[jj[q]], vv[q]] for q in range(ip[i] + 1, ip[i + 1]) if cf[jj[q]] > 0] for i in frow]
+    FF = [[[f2f[i], vv[ip[i]]]] + [[f2f[jj[q]], vv[q]] for q in range(ip[i] + 1, ip[i + 1]) if cf[jj[q]] <= 0]
+          for i in ffrow]
+    return FF, FC, frow, ffrow, len(f2c)
+
+
+def _matmul(X, Y, ncols):
+    out = []
+    for r, row in enumerate(X):
+        cols, vals, slot = [], [], {}
+        if len(X) == ncols:
+            slot[r] = 0
+            cols.append(r)
+            vals.append(0.0)
+        for k, a in row:
+            for c, b in Y[k]:
+                if c not in slot:
+                    slot[c] = len(cols)
+                    cols.append(c)
+                    vals.append(a * b)
+                else:
+                    vals[slot[c]] += a * b
+        out.append([[c, v] for c, v in zip(cols, vals)])
+    return out
+
+
+def modext_rows(ip, jj, vv, cf):
+    """par_mod_lr_interp.c:16 hypre_BoomerAMGBuildModExtInterpHost."""
+    FF, FC, frow, _, nC = _fffc(ip, jj, vv, cf, False)
+    for r, i in enumerate(frow):
+        dq = 0.0
+        for _, a in FC[r]:
+            dq += a
+        dw = 0.0
+        for q in range(ip[i], ip[i + 1]):
+            dw += vv[q]
+        for _, a in FF[r][1:]:
+            dw -= a
+        dw -= dq
+        beta = 1.0 / dw if dw else 1.0
+        FF[r][0][1] = beta * dq
+        gamma = -1.0 / dq if dq else 1.0
+        for e in FF[r][1:]:
+            e[1] *= beta
+        for e in FC[r]:
+            e[1] *= gamma
+    W = _matmul(FF, FC, nC)
+    it = iter(W)
+    return [[[c, 1.0]] if cf[i] > 0 else next(it) for i, c in
+            ((i, sum(1 for k in range(i) if cf[k] > 0)) for i in range(len(ip) - 1))]
+
+
+def modpartialext_rows(ip, jj, vv, cf):
+    """par_2s_interp.c:15 hypre_BoomerAMGBuildModPartialExtInterpHost."""
+    FF, FC, frow, ffrow, nC = _fffc(ip, jj, vv, cf, True)
+    fidx = {i: r for r, i in enumerate(frow)}
+    dq = []
+    for row in FC:
+        s = 0.0
+        for _, a in row:
+            s += a
+        dq.append(s)
+    for r, i in enumerate(ffrow):
+        dw = 0.0
+        for q in range(ip[i], ip[i + 1]):
+            dw += vv[q]
+        for c, a in FF[r][1:]:
+            if dq[c]:
+                dw -= a
+        dw -= dq[fidx[i]]
+        if dw:
+            b = 1.0 / dw
+            FF[r][0][1] = b * dq[fidx[i]]
+            for e in FF[r][1:]:
+                e[1] *= b
+    for r in range(len(FC)):
+        g = -1.0 / dq[r] if dq[r] else 0.0
+        for e in FC[r]:
+            e[1] *= g
+    W = _matmul(FF, FC, nC)
+    it = iter(W)
+    rows, c = [], 0
+    for i in range(len(ip) - 1):
+        if cf[i] > 0:
+            rows.append([[c, 1.0]])
+            c += 1
+        elif cf[i] == -2:
+            rows.append(next(it))
+    return rows
+
+
+@pytest.mark.parametrize("coarsen_type", [8, 10])
+def test_two_stage_modext_agg_interp_matches_restatement(hv, coarsen_type):
+    """agg_interp_type 5 (par_amg_setup.c:1575-1689): P = P1 P2 with P1 the
+    extended MM interpolation to the first pass's C points and P2 the partial
+    one from them to the second pass's; no truncation."""
+    A = hv.ParCSRMatrix.laplacian(14, 13, 12)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=coarsen_type, relax_type=18, agg_num_levels=1, agg_interp_type=5,
+            agg_P_max_elmts=0, agg_P12_max_elmts=0, agg_trunc_factor=0.0, agg_P12_trunc_factor=0.0)
+    amg.setup_host(A)
+    ip, jj, vv, _ = amg.level_matrix(0, 0)
+    cf = amg.level_vector(0, 0).astype(np.int64)
+    assert (cf == -2).any() and (cf == 1).any()
+    cf1 = np.where(cf == -2, 1, cf)
+    P1 = modext_rows(ip, jj, vv, cf1)
+    P2 = modpartialext_rows(ip, jj, vv, cf)
+    P = _matmul(P1, P2, int((cf == 1).sum()))
+    pi, pj, pv, _ = amg.level_matrix(0, 1)
+    assert len(P) == len(pi) - 1
+    for i, row in enumerate(P):
+        assert pj[pi[i]:pi[i + 1]].tolist() == [c for c, _ in row], i
+        assert np.array_equal(pv[pi[i]:pi[i + 1]], np.array([v for _, v in row], dtype=np.float64)), i
