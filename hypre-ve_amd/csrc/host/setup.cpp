@@ -1222,9 +1222,12 @@ void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Patte
 // Second stage of the 2-stage aggressive interpolations (cf: 1 = C of both
 // stages, -2 = C of the first stage only): P2 from the first stage's C
 // points to the second's.  agg_interp_type 5: par_2s_interp.c:15
-// hypre_BoomerAMGBuildModPartialExtInterpHost (:180-330).
+// hypre_BoomerAMGBuildModPartialExtInterpHost (:180-330); 7 (pe): :564
+// hypre_BoomerAMGBuildModPartialExtPEInterpHost (:730-900), with D_lambda as
+// gen_fffc.c:1056 hypre_ParCSRMatrixGenerateFFFCD3 forms it (every F row: the
+// mean of its strong non-C connections).
 void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                                int max_elmts, CSR& P) {
+                                int max_elmts, bool pe, CSR& P) {
   CSR FF, FC;
   std::vector<int> frow, ffrow;
   fffc(A, cf, S, true, FF, FC, frow, ffrow);
@@ -1235,15 +1238,37 @@ void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const 
     for (int i = 0; i < A.nrows; ++i)
       if (cf[i] < 0) f2f[i] = k++;
   }
-  std::vector<double> dq(nF, 0.0), dw(nN, 0.0);
+  std::vector<double> dq(nF, 0.0), dw(nN, 0.0), lam(nF, 0.0), dinv(nF, 0.0), tau(nN, 0.0);
 #pragma omp parallel for schedule(static)
-  for (int r = 0; r < nF; ++r)
+  for (int r = 0; r < nF; ++r) {
     for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) dq[r] += FC.a[q];
+    if (!pe) continue;
+    const int i = frow[r];
+    double sum = 0;
+    for (int q = S.i[i]; q < S.i[i + 1]; ++q) {
+      const int js = S.j[q];
+      if (cf[js] > 0) continue;
+      int ja = A.i[i] + 1;
+      while (A.j[ja] != js) ja++;
+      sum += 1;
+      lam[r] += A.a[ja];
+    }
+    if (sum) lam[r] = lam[r] / sum;
+    if (dq[r] + lam[r]) dinv[r] = 1.0 / (dq[r] + lam[r]);
+  }
   // As_FF's columns index the non-C points; with cf in {1, -1, -2, -3} they
   // are exactly the F rows (CF < 0), so dq is indexed by them directly
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < nN; ++r) {
     const int i = ffrow[r];
+    if (pe) {
+      for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) tau[r] += FF.a[q] * lam[FF.j[q]] * dinv[FF.j[q]];
+      for (int q = A.i[i]; q < A.i[i + 1]; ++q) dw[r] += A.a[q];
+      for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q)
+        if (dinv[FF.j[q]]) dw[r] -= FF.a[q];
+      dw[r] += tau[r] - dq[f2f[i]];
+      continue;
+    }
     for (int q = A.i[i]; q < A.i[i + 1]; ++q) dw[r] += A.a[q];
     for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q)
       if (dq[FF.j[q]]) dw[r] -= FF.a[q];
@@ -1252,13 +1277,14 @@ void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const 
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < nN; ++r) {
     if (!dw[r]) continue;  // the reference leaves such a row unscaled, diagonal included
-    const double b = 1.0 / dw[r];
-    FF.a[FF.i[r]] = b * dq[f2f[ffrow[r]]];
+    const int fi = f2f[ffrow[r]];
+    const double b = pe ? -1.0 / dw[r] : 1.0 / dw[r];
+    FF.a[FF.i[r]] = pe ? b * (dq[fi] + lam[fi]) : b * dq[fi];
     for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) FF.a[q] *= b;
   }
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < nF; ++r) {
-    const double g = dq[r] ? -1.0 / dq[r] : 0.0;
+    const double g = pe ? dinv[r] : dq[r] ? -1.0 / dq[r] : 0.0;
     for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) FC.a[q] *= g;
   }
   CSR W;
@@ -1963,9 +1989,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
-  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4 && prm.agg_interp_type != 5)
+  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4 && prm.agg_interp_type != 5 && prm.agg_interp_type != 7)
     throw std::runtime_error("aggressive coarsening: agg_interp_type " + std::to_string(prm.agg_interp_type) +
-                             " is not available in this build (4 multipass, 5 2-stage extended MM)");
+                             " is not available in this build (4 multipass, 5 / 7 2-stage extended / ext+e MM)");
   if (prm.num_paths < 1) throw std::runtime_error("num_paths must be >= 1");
   int coarsen_type = prm.coarsen_type;
   H.lev.emplace_back();
@@ -2055,8 +2081,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       // 2-stage: P1 to the first stage's C points, P2 from them to the
       // second's (par_amg_setup.c:1575-1689)
       CSR P1, P2;
-      build_modext_interp(L.A, cf1, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, false, P1);
-      build_modpartialext_interp(L.A, cf, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, P2);
+      const bool pe = prm.agg_interp_type == 7;
+      build_modext_interp(L.A, cf1, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P1);
+      build_modpartialext_interp(L.A, cf, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P2);
       multiply_interp(P1, P2, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
     }
     else if (agg) {

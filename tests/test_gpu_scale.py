@@ -203,6 +203,34 @@ def test_gpu_boomer_out17_two_stage_agg(gpu):
     assert rr < 1e-8
 
 
+@pytest.mark.timeout(600)
+def test_gpu_boomer_out18_two_stage_agg_pe(gpu):
+    """TEST_cuda_lassen/gpu_boomer.saved out.18 (gpu_boomer.jobs:65: np 4,
+    -n 256 256 128 -pmis -keepT 1 -rlx 7 -w 0.85 -agg_nl 1 -agg_interp 7
+    -agg_P12_mx 4 -solver 1), in one process.  Saved: grid 1.070965, operator
+    1.448836, 20 iterations, 4.969910e-09.  Band as out.14."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(256, 256, 128)
+    kw = hv.ij_amg_defaults(1)
+    kw.update(coarsen_type=8, interp_type=6, relax_type=7, relax_wt=0.85, agg_num_levels=1, agg_interp_type=7,
+              agg_P12_max_elmts=4)
+    amg = hv.BoomerAMG(**kw)
+    pcg = hv.PCG(tol=1e-8, max_iter=1000, two_norm=1)
+    pcg.set_precond_amg(amg)
+    n = A.n
+    b = hv.ParVector(n, np.ones(n))
+    x = hv.ParVector(n, np.zeros(n))
+    pcg.setup(A, b, x)
+    g, o, _ = amg.complexities()
+    print(f"grid {g:.6f} operator {o:.6f}")
+    assert abs(g - 1.070965) <= 0.01 * 1.070965, g
+    assert abs(o - 1.448836) <= 0.02 * 1.448836, o
+    it, rr = pcg.solve(A, b, x)
+    print(f"iterations {it} rel.res {rr:.6e}")
+    assert 18 <= it <= 22, it
+    assert rr < 1e-8
+
+
 @pytest.mark.timeout(900)
 def test_gpu_boomer_out5_loopback4(gpu):
     """TEST_cuda_lassen/gpu_boomer.saved out.5 (gpu_boomer.jobs:24: mpirun -np 4

@@ -272,31 +272,55 @@ def modext_rows(ip, jj, vv, cf):
             ((i, sum(1 for k in range(i) if cf[k] > 0)) for i in range(len(ip) - 1))]
 
 
-def modpartialext_rows(ip, jj, vv, cf):
-    """par_2s_interp.c:15 hypre_BoomerAMGBuildModPartialExtInterpHost."""
+def modpartialext_rows(ip, jj, vv, cf, pe=False):
+    """par_2s_interp.c:15 hypre_BoomerAMGBuildModPartialExtInterpHost; pe:
+    :564 hypre_BoomerAMGBuildModPartialExtPEInterpHost (D_lambda as
+    gen_fffc.c:1056 GenerateFFFCD3)."""
     FF, FC, frow, ffrow, nC = _fffc(ip, jj, vv, cf, True)
     fidx = {i: r for r, i in enumerate(frow)}
-    dq = []
-    for row in FC:
+    dq, lam, dinv = [], [], []
+    for r, row in enumerate(FC):
         s = 0.0
         for _, a in row:
             s += a
         dq.append(s)
+        i = frow[r]
+        lm, cnt = 0.0, 0
+        for q in range(ip[i] + 1, ip[i + 1]):
+            if cf[jj[q]] <= 0:
+                cnt += 1
+                lm += vv[q]
+        if cnt:
+            lm = lm / cnt
+        lam.append(lm)
+        dinv.append(1.0 / (s + lm) if s + lm else 0.0)
     for r, i in enumerate(ffrow):
+        fi = fidx[i]
         dw = 0.0
-        for q in range(ip[i], ip[i + 1]):
-            dw += vv[q]
-        for c, a in FF[r][1:]:
-            if dq[c]:
-                dw -= a
-        dw -= dq[fidx[i]]
+        if pe:
+            tau = 0.0
+            for c, a in FF[r][1:]:
+                tau += a * lam[c] * dinv[c]
+            for q in range(ip[i], ip[i + 1]):
+                dw += vv[q]
+            for c, a in FF[r][1:]:
+                if dinv[c]:
+                    dw -= a
+            dw += tau - dq[fi]
+        else:
+            for q in range(ip[i], ip[i + 1]):
+                dw += vv[q]
+            for c, a in FF[r][1:]:
+                if dq[c]:
+                    dw -= a
+            dw -= dq[fi]
         if dw:
-            b = 1.0 / dw
-            FF[r][0][1] = b * dq[fidx[i]]
+            b = -1.0 / dw if pe else 1.0 / dw
+            FF[r][0][1] = b * (dq[fi] + lam[fi]) if pe else b * dq[fi]
             for e in FF[r][1:]:
                 e[1] *= b
     for r in range(len(FC)):
-        g = -1.0 / dq[r] if dq[r] else 0.0
+        g = dinv[r] if pe else (-1.0 / dq[r] if dq[r] else 0.0)
         for e in FC[r]:
             e[1] *= g
     W = _matmul(FF, FC, nC)
@@ -311,22 +335,26 @@ def modpartialext_rows(ip, jj, vv, cf):
     return rows
 
 
+@pytest.mark.parametrize("agg_interp", [5, 7])
 @pytest.mark.parametrize("coarsen_type", [8, 10])
-def test_two_stage_modext_agg_interp_matches_restatement(hv, coarsen_type):
-    """agg_interp_type 5 (par_amg_setup.c:1575-1689): P = P1 P2 with P1 the
-    extended MM interpolation to the first pass's C points and P2 the partial
-    one from them to the second pass's; no truncation."""
+def test_two_stage_modext_agg_interp_matches_restatement(hv, coarsen_type, agg_interp):
+    """agg_interp_type 5 / 7 (par_amg_setup.c:1575-1689): P = P1 P2 with P1
+    the extended (ext+e) MM interpolation to the first pass's C points and P2
+    the partial one from them to the second pass's; no truncation."""
     A = hv.ParCSRMatrix.laplacian(14, 13, 12)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
-    amg.set(coarsen_type=coarsen_type, relax_type=18, agg_num_levels=1, agg_interp_type=5,
+    amg.set(coarsen_type=coarsen_type, relax_type=18, agg_num_levels=1, agg_interp_type=agg_interp,
             agg_P_max_elmts=0, agg_P12_max_elmts=0, agg_trunc_factor=0.0, agg_P12_trunc_factor=0.0)
     amg.setup_host(A)
     ip, jj, vv, _ = amg.level_matrix(0, 0)
     cf = amg.level_vector(0, 0).astype(np.int64)
     assert (cf == -2).any() and (cf == 1).any()
     cf1 = np.where(cf == -2, 1, cf)
-    P1 = modext_rows(ip, jj, vv, cf1)
-    P2 = modpartialext_rows(ip, jj, vv, cf)
+    if agg_interp == 5:
+        P1 = modext_rows(ip, jj, vv, cf1)
+    else:
+        P1 = [[[c, v] for c, v in zip(*row)] for row in modextpe_rows(ip, jj, vv, cf1)]
+    P2 = modpartialext_rows(ip, jj, vv, cf, pe=agg_interp == 7)
     P = _matmul(P1, P2, int((cf == 1).sum()))
     pi, pj, pv, _ = amg.level_matrix(0, 1)
     assert len(P) == len(pi) - 1
