@@ -125,7 +125,7 @@ struct AMGParams {
   int coarsen_type = 10;          // 8 PMIS, 9 PMIS(seq rand), 10 HMIS
   int measure_type = 0;
   int coarsen_cut_factor = 0;
-  int interp_type = 6;            // 6 ext+i, 14 ext, 18 ext+e (MM), 3 direct
+  int interp_type = 6;            // 6 ext+i, 14 ext, 16/17/18 ext / ext+i / ext+e (MM), 3 direct
   int P_max_elmts = 4;
   double trunc_factor = 0.0;
   // grid_relax_type (par_amg.c:218-220, 339-341: [0] keeps the 3 of the
@@ -261,6 +261,9 @@ void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_fact
 // plus_i false: extended interpolation (interp_type 14) instead of ext+i
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P, bool plus_i = true);
+// extended+i in matrix-matrix form (interp_type 17, par_mod_lr_interp.c:474)
+void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                           int max_elmts, CSR& P);
 // extended+e in matrix-matrix form (interp_type 18, par_mod_lr_interp.c:1040)
 void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                            int max_elmts, CSR& P);

@@ -1219,6 +1219,59 @@ void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Patte
   build_modext_interp(A, cf, S, trunc_factor, max_elmts, true, P);
 }
 
+// Extended+i in matrix-matrix form (interp_type 17): par_mod_lr_interp.c:474
+// hypre_BoomerAMGBuildModExtPIInterpHost (:640-800).  As_FF's off-diagonal
+// a_ij is divided by D_q[j] + a_ji (a_ji from an unmodified copy; D_q[j] alone
+// when j has no strong connection back to i), those a_ji shares form D_theta,
+// the diagonal is 1, and the row is scaled by -1 / (D_theta + D_w); As_FC is
+// used as is.
+void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                           int max_elmts, CSR& P) {
+  CSR FF, FC;
+  std::vector<int> frow, ffrow;
+  fffc(A, cf, S, false, FF, FC, frow, ffrow);
+  const int nF = (int)frow.size();
+  const std::vector<double> orig = FF.a;
+  std::vector<double> dq(nF, 0.0), dw(nF, 0.0), dth(nF, 0.0);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r)
+    for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) dq[r] += FC.a[q];
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r) {
+    const int i = frow[r];
+    for (int q = A.i[i]; q < A.i[i + 1]; ++q) dw[r] += A.a[q];
+    for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) dw[r] -= FF.a[q];
+    dw[r] -= dq[r];
+  }
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < nF; ++r) {
+    for (int q = FF.i[r] + 1; q < FF.i[r + 1]; ++q) {
+      const int jj = FF.j[q];
+      double value = dq[jj];
+      for (int k = FF.i[jj] + 1; k < FF.i[jj + 1]; ++k)
+        if (FF.j[k] == r) {
+          const double value1 = orig[k];
+          value += value1;
+          dth[r] += FF.a[q] * value1 / value;
+          break;
+        }
+      FF.a[q] /= value;
+    }
+    FF.a[FF.i[r]] = 1.0;
+    double theta = dth[r] + dw[r];
+    if (theta) {
+      theta = -1.0 / theta;
+      for (int q = FF.i[r]; q < FF.i[r + 1]; ++q) FF.a[q] *= theta;
+    }
+  }
+  CSR W;
+  matmul_first_touch(FF, FC, W);
+  std::vector<int> all(A.nrows);
+  for (int i = 0; i < A.nrows; ++i) all[i] = i;
+  assemble_mm_p(cf, all, W, FC.ncols, P);
+  if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+}
+
 // Second stage of the 2-stage aggressive interpolations (cf: 1 = C of both
 // stages, -2 = C of the first stage only): P2 from the first stage's C
 // points to the second's.  agg_interp_type 5: par_2s_interp.c:15
@@ -2124,6 +2177,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     }
     else if (prm.interp_type == 6) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else if (prm.interp_type == 18) build_modextpe_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
+    else if (prm.interp_type == 17) build_modextpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
+    else if (prm.interp_type == 16)
+      build_modext_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, false, P);
     else if (prm.interp_type == 14) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P, false);
     else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));

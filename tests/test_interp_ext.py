@@ -361,3 +361,70 @@ def test_two_stage_modext_agg_interp_matches_restatement(hv, coarsen_type, agg_i
     for i, row in enumerate(P):
         assert pj[pi[i]:pi[i + 1]].tolist() == [c for c, _ in row], i
         assert np.array_equal(pv[pi[i]:pi[i + 1]], np.array([v for _, v in row], dtype=np.float64)), i
+
+
+def modextpi_rows(ip, jj, vv, cf):
+    """par_mod_lr_interp.c:474 hypre_BoomerAMGBuildModExtPIInterpHost."""
+    FF, FC, frow, _, nC = _fffc(ip, jj, vv, cf, False)
+    orig = [[e[1] for e in row] for row in FF]
+    dq = []
+    for row in FC:
+        s = 0.0
+        for _, a in row:
+            s += a
+        dq.append(s)
+    dw = []
+    for r, i in enumerate(frow):
+        w = 0.0
+        for q in range(ip[i], ip[i + 1]):
+            w += vv[q]
+        for _, a in FF[r][1:]:
+            w -= a
+        w -= dq[r]
+        dw.append(w)
+    for r in range(len(FF)):
+        th = 0.0
+        for e in FF[r][1:]:
+            c = e[0]
+            value = dq[c]
+            for k in range(1, len(FF[c])):
+                if FF[c][k][0] == r:
+                    value1 = orig[c][k]
+                    value += value1
+                    th += e[1] * value1 / value
+                    break
+            e[1] /= value
+        FF[r][0][1] = 1.0
+        theta = th + dw[r]
+        if theta:
+            theta = -1.0 / theta
+            for e in FF[r]:
+                e[1] *= theta
+    W = _matmul(FF, FC, nC)
+    it = iter(W)
+    rows, c = [], 0
+    for i in range(len(ip) - 1):
+        if cf[i] > 0:
+            rows.append([[c, 1.0]])
+            c += 1
+        else:
+            rows.append(next(it))
+    return rows
+
+
+@pytest.mark.parametrize("interp_type", [16, 17])
+@pytest.mark.parametrize("coarsen_type", [8, 10])
+def test_modext_modextpi_interp_matches_restatement(hv, interp_type, coarsen_type):
+    """interp_type 16 (par_mod_lr_interp.c:16) and 17 (:474), no truncation."""
+    A = hv.ParCSRMatrix.laplacian(11, 10, 9)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=coarsen_type, interp_type=interp_type, relax_type=18, P_max_elmts=0, trunc_factor=0.0)
+    amg.setup_host(A)
+    ip, jj, vv, _ = amg.level_matrix(0, 0)
+    cf = amg.level_vector(0, 0).astype(np.int64)
+    rows = (modext_rows if interp_type == 16 else modextpi_rows)(ip, jj, vv, cf)
+    pi, pj, pv, _ = amg.level_matrix(0, 1)
+    assert len(rows) == len(pi) - 1
+    for i, row in enumerate(rows):
+        assert pj[pi[i]:pi[i + 1]].tolist() == [c for c, _ in row], i
+        assert np.array_equal(pv[pi[i]:pi[i + 1]], np.array([v for _, v in row], dtype=np.float64)), i
