@@ -263,10 +263,10 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P, bool plus_i = true);
 // extended+i in matrix-matrix form (interp_type 17, par_mod_lr_interp.c:474)
 void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P);
+                           int max_elmts, CSR& P, const std::vector<int>* emul = nullptr);
 // extended+e in matrix-matrix form (interp_type 18, par_mod_lr_interp.c:1040)
 void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P);
+                           int max_elmts, CSR& P, const std::vector<int>* emul = nullptr);
 void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                          double trunc_factor, int max_elmts, CSR& P);
 void truncate_rows(CSR& P, double tol, int max_elmts);
@@ -277,8 +277,9 @@ void correct_cf_marker(std::vector<int>& cf, const std::vector<int>& new_cf);
 void correct_cf_marker2(std::vector<int>& cf, const std::vector<int>& new_cf);
 // matrix-matrix interpolations (setup.cpp): ModExt (pe false) / ModExtPE, the
 // 2-stage second stage ModPartialExt, and P = P1 P2 with the aggressive truncation
+// emul: fine row starts of an emulated N-rank run (hypre_ParMatmul's np > 1 order)
 void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                         int max_elmts, bool pe, CSR& P);
+                         int max_elmts, bool pe, CSR& P, const std::vector<int>* emul = nullptr);
 void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                                 int max_elmts, bool pe, CSR& P);
 void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P);

@@ -1,3 +1,4 @@
+#include <memory>
 // BoomerAMG setup phase on the host: strength, PMIS coarsening, extended+i
 // interpolation, truncation and the Galerkin product.  Every routine follows the
 // single-process (num_procs == 1) branch of the cited hypre routine statement for
@@ -1090,35 +1091,92 @@ static void fffc(const CSR& A, const std::vector<int>& cf, const Pattern& S, boo
   }
 }
 
-static void matmul_first_touch(const CSR& X, const CSR& Y, CSR& C) {
+// Owners under N-rank emulation (hypre_BoomerAMGSetRankEmulation): the rank
+// of each row of X, of each column of X (= row of Y) and of each column of Y.
+struct MatmulRanks {
+  std::vector<int> row, xcol, ycol;
+  int nranks = 0;
+};
+// With ranks, the np > 1 order of hypre_ParMatmul (par_csr_matop.c:860-1000):
+// a row's entries in other ranks' columns (A_offd) go first, each through its
+// B row's other-rank columns (B_ext_offd) and then own ones (B_ext_diag); then
+// the own-column entries (A_diag), through B_diag then B_offd; the product row
+// is C_diag's first-touch list followed by C_offd's.
+static void matmul_first_touch(const CSR& X, const CSR& Y, CSR& C, const MatmulRanks* rk = nullptr) {
   const int nr = X.nrows, nc = Y.ncols;
-  const bool square = nr == nc;  // hypre_ParMatmul's allsquare: a zero diagonal entry first
+  bool square = nr == nc;  // hypre_ParMatmul's allsquare: a zero diagonal entry first
+  std::vector<int> lrows, lcols;  // emulated: rows / Y columns per rank (allsquare is local too)
+  if (rk) {
+    lrows.assign(rk->nranks, 0);
+    lcols.assign(rk->nranks, 0);
+    for (int r : rk->row) lrows[r]++;
+    for (int c : rk->ycol) lcols[c]++;
+  }
   std::vector<std::vector<int>> cj(nr);
   std::vector<std::vector<double>> ca(nr);
 #pragma omp parallel
   {
     std::vector<int> mark(std::max(nc, 1), -1);
     std::vector<int> touched;
+    std::vector<int> oj;  // emulated: the C_offd list
+    std::vector<double> oa;
 #pragma omp for schedule(dynamic, 256)
     for (int r = 0; r < nr; ++r) {
       std::vector<int>& rj = cj[r];
       std::vector<double>& ra = ca[r];
       touched.clear();
-      if (square) { mark[r] = 0; rj.push_back(r); ra.push_back(0.0); touched.push_back(r); }
-      for (int q = X.i[r]; q < X.i[r + 1]; ++q) {
-        const double ae = X.a[q];
-        const int k = X.j[q];
-        for (int t = Y.i[k]; t < Y.i[k + 1]; ++t) {
-          const int c = Y.j[t];
-          if (mark[c] < 0) {
-            mark[c] = (int)rj.size();
-            touched.push_back(c);
-            rj.push_back(c);
-            ra.push_back(ae * Y.a[t]);
-          } else {
-            ra[mark[c]] += ae * Y.a[t];
+      if (!rk) {
+        if (square) { mark[r] = 0; rj.push_back(r); ra.push_back(0.0); touched.push_back(r); }
+        for (int q = X.i[r]; q < X.i[r + 1]; ++q) {
+          const double ae = X.a[q];
+          const int k = X.j[q];
+          for (int t = Y.i[k]; t < Y.i[k + 1]; ++t) {
+            const int c = Y.j[t];
+            if (mark[c] < 0) {
+              mark[c] = (int)rj.size();
+              touched.push_back(c);
+              rj.push_back(c);
+              ra.push_back(ae * Y.a[t]);
+            } else {
+              ra[mark[c]] += ae * Y.a[t];
+            }
           }
         }
+      } else {
+        const int R = rk->row[r];
+        oj.clear();
+        oa.clear();
+        if (square && lrows[R] == lcols[R]) {  // C_{i1,i1} at the rank's local diagonal
+          // (never met by the interpolations here: their F and C counts differ)
+          mark[r] = 0; rj.push_back(r); ra.push_back(0.0); touched.push_back(r);
+        }
+        auto add = [&](double ae, int c, double b) {
+          const bool own = rk->ycol[c] == R;
+          std::vector<int>& lj = own ? rj : oj;
+          std::vector<double>& la = own ? ra : oa;
+          if (mark[c] < 0) {
+            mark[c] = (int)lj.size();
+            touched.push_back(c);
+            lj.push_back(c);
+            la.push_back(ae * b);
+          } else {
+            la[mark[c]] += ae * b;
+          }
+        };
+        for (int pass = 0; pass < 2; ++pass)  // 0: A_offd entries, 1: A_diag entries
+          for (int q = X.i[r]; q < X.i[r + 1]; ++q) {
+            const int k = X.j[q];
+            if ((rk->xcol[k] == R) != (pass == 1)) continue;
+            const double ae = X.a[q];
+            for (int half = 0; half < 2; ++half)  // A_offd: B_ext_offd first; A_diag: B_diag first
+              for (int t = Y.i[k]; t < Y.i[k + 1]; ++t) {
+                const bool own = rk->ycol[Y.j[t]] == R;
+                if (own != ((pass == 1) == (half == 0))) continue;
+                add(ae, Y.j[t], Y.a[t]);
+              }
+          }
+        rj.insert(rj.end(), oj.begin(), oj.end());
+        ra.insert(ra.end(), oa.begin(), oa.end());
       }
       for (int c : touched) mark[c] = -1;
     }
@@ -1132,6 +1190,19 @@ static void matmul_first_touch(const CSR& X, const CSR& Y, CSR& C) {
     std::copy(cj[r].begin(), cj[r].end(), C.j.begin() + C.i[r]);
     std::copy(ca[r].begin(), ca[r].end(), C.a.begin() + C.i[r]);
   }
+}
+
+// Owners of W = As_FF As_FC's rows and columns under rank emulation (emul:
+// fine row starts); nullptr without it.
+static std::unique_ptr<MatmulRanks> mm_ranks(const std::vector<int>& cf, const std::vector<int>& ffrow,
+                                             const std::vector<int>* emul) {
+  if (!emul || emul->size() <= 2) return nullptr;
+  auto owner = [&](int i) { return (int)(std::upper_bound(emul->begin(), emul->end(), i) - emul->begin()) - 1; };
+  auto rk = std::make_unique<MatmulRanks>();
+  rk->nranks = (int)emul->size() - 1;
+  for (int i : ffrow) rk->row.push_back(owner(i));
+  for (int i = 0; i < (int)cf.size(); ++i) (cf[i] > 0 ? rk->ycol : rk->xcol).push_back(owner(i));
+  return rk;
 }
 
 // P's rows: `rows` (fine points, in order) are C points (cf > 0: injection at
@@ -1162,7 +1233,7 @@ static void assemble_mm_p(const std::vector<int>& cf, const std::vector<int>& ro
 // diagonal scalings of :1204-1318.  Extended (agg_interp_type 5's first
 // stage, pe = false): :16 hypre_BoomerAMGBuildModExtInterpHost, :170-245.
 void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                         int max_elmts, bool pe, CSR& P) {
+                         int max_elmts, bool pe, CSR& P, const std::vector<int>* emul) {
   CSR FF, FC;
   std::vector<int> frow, ffrow;
   fffc(A, cf, S, false, FF, FC, frow, ffrow);
@@ -1207,7 +1278,8 @@ void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern
     for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) FC.a[q] *= cscale;
   }
   CSR W;
-  matmul_first_touch(FF, FC, W);
+  const auto rk = mm_ranks(cf, ffrow, emul);
+  matmul_first_touch(FF, FC, W, rk.get());
   std::vector<int> all(A.nrows);
   for (int i = 0; i < A.nrows; ++i) all[i] = i;
   assemble_mm_p(cf, all, W, FC.ncols, P);
@@ -1215,8 +1287,8 @@ void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern
 }
 
 void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P) {
-  build_modext_interp(A, cf, S, trunc_factor, max_elmts, true, P);
+                           int max_elmts, CSR& P, const std::vector<int>* emul) {
+  build_modext_interp(A, cf, S, trunc_factor, max_elmts, true, P, emul);
 }
 
 // Extended+i in matrix-matrix form (interp_type 17): par_mod_lr_interp.c:474
@@ -1226,7 +1298,7 @@ void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Patte
 // the diagonal is 1, and the row is scaled by -1 / (D_theta + D_w); As_FC is
 // used as is.
 void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P) {
+                           int max_elmts, CSR& P, const std::vector<int>* emul) {
   CSR FF, FC;
   std::vector<int> frow, ffrow;
   fffc(A, cf, S, false, FF, FC, frow, ffrow);
@@ -1265,7 +1337,8 @@ void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Patte
     }
   }
   CSR W;
-  matmul_first_touch(FF, FC, W);
+  const auto rk = mm_ranks(cf, ffrow, emul);
+  matmul_first_touch(FF, FC, W, rk.get());
   std::vector<int> all(A.nrows);
   for (int i = 0; i < A.nrows; ++i) all[i] = i;
   assemble_mm_p(cf, all, W, FC.ncols, P);
@@ -2055,8 +2128,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   if (rank_starts && rank_starts->size() > 2) {
     emul = *rank_starts;
     if (emul.front() != 0 || emul.back() != A0.nrows) throw std::runtime_error("rank emulation: row starts do not cover A");
-    if (prm.interp_type != 6 && prm.interp_type != 14)
-      throw std::runtime_error("rank emulation: only ext+i and ext interpolation are restated");
+    if (prm.interp_type != 6 && prm.interp_type != 14 && (prm.interp_type < 16 || prm.interp_type > 18))
+      throw std::runtime_error("rank emulation: interp_type " + std::to_string(prm.interp_type) + " is not restated");
     if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4)
       throw std::runtime_error("rank emulation: only multipass aggressive interpolation is restated");
     rank_order_rows(H.lev[0].A, emul, emul);
@@ -2148,7 +2221,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         rank_order_rows(P, emul, cs);
       }
     }
-    else if ((prm.interp_type == 6 || prm.interp_type == 14) && !emul.empty()) {
+    else if ((prm.interp_type == 6 || prm.interp_type == 14 || (prm.interp_type >= 16 && prm.interp_type <= 18)) &&
+             !emul.empty()) {
       // par_csr_matrix.c:2671 truncates the row [P_diag | P_offd] and splits
       // the kept entries back into the two parts in their sorted order
       std::vector<int> cs(emul.size(), 0);
@@ -2157,7 +2231,10 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] == 1);
         for (size_t r = 0; r < emul.size(); ++r) cs[r] = pref[emul[r]];
       }
-      build_extpi_interp(L.A, cf, S, 0.0, 0, P, prm.interp_type == 6);
+      if (prm.interp_type == 16) build_modext_interp(L.A, cf, S, 0.0, 0, false, P, &emul);
+      else if (prm.interp_type == 17) build_modextpi_interp(L.A, cf, S, 0.0, 0, P, &emul);
+      else if (prm.interp_type == 18) build_modextpe_interp(L.A, cf, S, 0.0, 0, P, &emul);
+      else build_extpi_interp(L.A, cf, S, 0.0, 0, P, prm.interp_type == 6);
       rank_order_rows(P, emul, cs);
       if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
       rank_order_rows(P, emul, cs);

@@ -18,7 +18,10 @@ l1 hybrid GS 13/14 (also C/F-ordered and weighted, w = 1.1), hybrid GS 4 up,
 6 and 8 under PCG, Chebyshev (order 2/3, unscaled, variant 1),
 BoomerAMG-PCG, and aggressive coarsening (HMIS second pass on S*S + 2S with
 local measures per rank, multipass interpolation, 1 and 10 aggressive levels,
-7- and 27-point: agg_interp.out.4/8, coarsening.out.7).
+7- and 27-point: agg_interp.out.4/8, coarsening.out.7), and the extended /
+extended+i interpolations in matrix-matrix form (interp.out.7/8), whose
+hypre_ParMatmul products follow its np > 1 entry order (other-rank columns
+first) under the emulation.
 """
 import json
 import os
