@@ -281,7 +281,7 @@ void correct_cf_marker2(std::vector<int>& cf, const std::vector<int>& new_cf);
 void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                          int max_elmts, bool pe, CSR& P, const std::vector<int>* emul = nullptr);
 void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                                int max_elmts, bool pe, CSR& P);
+                                int max_elmts, bool pe, CSR& P, const std::vector<int>* emul = nullptr);
 void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P);
 void build_multipass_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                             int max_elmts, CSR& P);

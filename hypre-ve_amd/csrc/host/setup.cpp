@@ -1112,6 +1112,8 @@ static void matmul_first_touch(const CSR& X, const CSR& Y, CSR& C, const MatmulR
     for (int r : rk->row) lrows[r]++;
     for (int c : rk->ycol) lcols[c]++;
   }
+  std::vector<int> rfirst(lrows.size() + 1, 0), cfirst(lcols.size() + 1, 0);  // rows / columns owned by ranks < R
+  for (size_t q = 0; q < lrows.size(); ++q) { rfirst[q + 1] = rfirst[q] + lrows[q]; cfirst[q + 1] = cfirst[q] + lcols[q]; }
   std::vector<std::vector<int>> cj(nr);
   std::vector<std::vector<double>> ca(nr);
 #pragma omp parallel
@@ -1146,9 +1148,9 @@ static void matmul_first_touch(const CSR& X, const CSR& Y, CSR& C, const MatmulR
         const int R = rk->row[r];
         oj.clear();
         oa.clear();
-        if (square && lrows[R] == lcols[R]) {  // C_{i1,i1} at the rank's local diagonal
-          // (never met by the interpolations here: their F and C counts differ)
-          mark[r] = 0; rj.push_back(r); ra.push_back(0.0); touched.push_back(r);
+        if (square && lrows[R] == lcols[R]) {  // C_{i1,i1}: the rank's local diagonal
+          const int c = cfirst[R] + (r - rfirst[R]);
+          mark[c] = 0; rj.push_back(c); ra.push_back(0.0); touched.push_back(c);
         }
         auto add = [&](double ae, int c, double b) {
           const bool own = rk->ycol[c] == R;
@@ -1353,7 +1355,7 @@ void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Patte
 // gen_fffc.c:1056 hypre_ParCSRMatrixGenerateFFFCD3 forms it (every F row: the
 // mean of its strong non-C connections).
 void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                                int max_elmts, bool pe, CSR& P) {
+                                int max_elmts, bool pe, CSR& P, const std::vector<int>* emul) {
   CSR FF, FC;
   std::vector<int> frow, ffrow;
   fffc(A, cf, S, true, FF, FC, frow, ffrow);
@@ -1414,7 +1416,8 @@ void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const 
     for (int q = FC.i[r]; q < FC.i[r + 1]; ++q) FC.a[q] *= g;
   }
   CSR W;
-  matmul_first_touch(FF, FC, W);
+  const auto rk = mm_ranks(cf, ffrow, emul);
+  matmul_first_touch(FF, FC, W, rk.get());
   std::vector<int> c1;  // rows of P2: the first stage's C points, in order
   for (int i = 0; i < A.nrows; ++i)
     if (cf[i] > 0 || cf[i] == -2) c1.push_back(i);
@@ -2130,8 +2133,6 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     if (emul.front() != 0 || emul.back() != A0.nrows) throw std::runtime_error("rank emulation: row starts do not cover A");
     if (prm.interp_type != 6 && prm.interp_type != 14 && (prm.interp_type < 16 || prm.interp_type > 18))
       throw std::runtime_error("rank emulation: interp_type " + std::to_string(prm.interp_type) + " is not restated");
-    if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4)
-      throw std::runtime_error("rank emulation: only multipass aggressive interpolation is restated");
     rank_order_rows(H.lev[0].A, emul, emul);
   }
   const std::vector<int>* rs = emul.empty() ? nullptr : &emul;
@@ -2208,9 +2209,41 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       // second's (par_amg_setup.c:1575-1689)
       CSR P1, P2;
       const bool pe = prm.agg_interp_type == 7;
-      build_modext_interp(L.A, cf1, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P1);
-      build_modpartialext_interp(L.A, cf, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P2);
-      multiply_interp(P1, P2, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
+      if (emul.empty()) {
+        build_modext_interp(L.A, cf1, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P1);
+        build_modpartialext_interp(L.A, cf, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P2);
+        multiply_interp(P1, P2, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
+      } else {
+        // emulated ranks: every product in hypre_ParMatmul's np > 1 order and
+        // every truncation over [P_diag | P_offd] (as for ext+i below)
+        const int nfine = (int)cf.size();
+        std::vector<int> c1pref(nfine + 1, 0), c2pref(nfine + 1, 0);
+        for (int i = 0; i < nfine; ++i) {
+          c1pref[i + 1] = c1pref[i] + (cf1[i] > 0);
+          c2pref[i + 1] = c2pref[i] + (cf[i] > 0);
+        }
+        std::vector<int> cs1, cs2;
+        for (int v : emul) { cs1.push_back(c1pref[v]); cs2.push_back(c2pref[v]); }
+        auto trunc = [&](CSR& M, const std::vector<int>& rs, const std::vector<int>& cs, double tf, int mx) {
+          rank_order_rows(M, rs, cs);
+          if (tf != 0.0 || mx > 0) truncate_rows(M, tf, mx);
+          rank_order_rows(M, rs, cs);
+        };
+        build_modext_interp(L.A, cf1, S, 0.0, 0, pe, P1, &emul);
+        trunc(P1, emul, cs1, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts);
+        build_modpartialext_interp(L.A, cf, S, 0.0, 0, pe, P2, &emul);
+        trunc(P2, cs1, cs2, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts);
+        MatmulRanks rk;
+        rk.nranks = (int)emul.size() - 1;
+        auto owner = [](const std::vector<int>& st, int i) {
+          return (int)(std::upper_bound(st.begin(), st.end(), i) - st.begin()) - 1;
+        };
+        for (int i = 0; i < P1.nrows; ++i) rk.row.push_back(owner(emul, i));
+        for (int c = 0; c < P1.ncols; ++c) rk.xcol.push_back(owner(cs1, c));
+        for (int c = 0; c < P2.ncols; ++c) rk.ycol.push_back(owner(cs2, c));
+        matmul_first_touch(P1, P2, P, &rk);
+        trunc(P, emul, cs2, prm.agg_trunc_factor, prm.agg_P_max_elmts);
+      }
     }
     else if (agg) {
       build_multipass_interp(L.A, cf, S, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
