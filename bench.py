@@ -137,8 +137,7 @@ def oracle_cpu_baseline(amg, nrows, n, pcg, args):
            "sample": f"{done} {what} of the same {n} hierarchy by the C oracle (oracle/oracle.c), "
                      f"OpenMP {threads} threads, {tcpu:.1f}s"}
     log(f"[bench] cpu oracle: {cpu['value']:.3e} DOF/s ({done} iterations, {tcpu:.1f}s, {threads} threads)")
-    del O
-    return cpu, u, done
+    return cpu, u, done, O
 
 
 def gpu_parity(hv, amg, krylov, A, b, x, u_oracle, iters, pcg):
@@ -168,6 +167,77 @@ def gpu_parity(hv, amg, krylov, A, b, x, u_oracle, iters, pcg):
         tag = "rtol1e-9" if ok else "MISMATCH"
     log(f"[bench] parity: GPU vs oracle after {iters} iterations from x = 0 on {xg.size} rows: {tag}")
     return tag, res
+
+
+def pcg_parity(hv, amg, A, b, x, O, nrows, iters):
+    """configs[2]'s solver on the bench's hierarchy: BoomerAMG-PCG (ij
+    -solver 1: two-norm PCG, krylov/pcg.c:271, one V-cycle per iteration from
+    a cleared z) for `iters` iterations from x = 0 on the GPU and in the C
+    oracle.  PCG's dot products reduce in another order than the oracle's, so
+    the iterate is compared at rtol 1e-9 with equal iteration counts, as the
+    PCG tests do (tests/test_gpu_parity.py)."""
+    amg.set(tol=0.0, max_iter=1)  # the preconditioner: one cycle (ij.c -solver 1)
+    kr = hv.PCG(tol=0.0, max_iter=iters, two_norm=1)
+    kr.set_precond_amg(amg, setup=False)  # the hierarchy is set up already
+    kr.setup(A, b, x)
+    x.fill(0.0)
+    it_g, rr_g = kr.solve(A, b, x)
+    xg = x.get()
+    kr.destroy()
+    u = np.zeros(nrows)
+    it_o, rr_o = O.pcg(np.ones(nrows), u, 0.0, iters, 1)
+    rel = float(np.linalg.norm(xg - u) / max(np.linalg.norm(u), 1e-300))
+    ok = rel <= 1e-9 and it_g == it_o == iters
+    log(f"[bench] parity_pcg: {iters} PCG iterations on {nrows} rows: GPU vs oracle rel. diff {rel:.3e}, "
+        f"final rel. residual {rr_g:.6e} vs {rr_o:.6e}: {'rtol1e-9' if ok else 'MISMATCH'}")
+    return {"kind": "rtol 1e-9 (PCG reductions reorder)", "equal": ok, "iterations": int(it_g),
+            "oracle_iterations": int(it_o), "rows": int(nrows), "rel_diff": rel,
+            "final_rel_res": rr_g, "oracle_final_rel_res": rr_o}
+
+
+def hierarchy_digest(amg):
+    """sha256 over every level's A, P, R (row pointers, columns, value bits),
+    CF marker and l1 norms: one level at a time, so two 256^3 hierarchies can
+    be compared without holding both."""
+    import hashlib
+    h = hashlib.sha256()
+    nl = amg.num_levels()
+    for l in range(nl):
+        for w in (0, 1, 2):
+            if w and l == nl - 1:
+                continue
+            ip, jj, vv, shp = amg.level_matrix(l, w)
+            h.update(np.asarray(shp, dtype=np.int64).tobytes())
+            for arr in (ip, jj, vv):
+                h.update(np.ascontiguousarray(arr).tobytes())
+        for w in (0, 1):
+            h.update(np.ascontiguousarray(amg.level_vector(l, w)).tobytes())
+    return h.hexdigest()
+
+
+def setup_parity(hv, args, n):
+    """The device setup (Setup's default: ext+i, truncation, R = P^T and RAP
+    on the GPU) against the host setup (SetupHost, the restatement pinned to
+    the reference's saved runs) at n^3: every level's bytes must agree."""
+    cx, cy, cz = (float(v) for v in args.coef.split(","))
+    digests = []
+    t0 = time.time()
+    for host in (False, True):
+        A = (hv.ParCSRMatrix.laplacian27(n, n, n) if args.stencil == 27
+             else hv.ParCSRMatrix.laplacian(n, n, n, cx=cx, cy=cy, cz=cz))
+        amg = hv.BoomerAMG(**amg_settings(hv, False, args.agg, args.relax, args.coarsen))
+        if host:
+            amg.setup_host(A)
+        else:
+            amg.setup(A)
+        digests.append((hierarchy_digest(amg), amg.num_levels()))
+        amg.destroy()
+        A.destroy()
+    ok = digests[0] == digests[1]
+    log(f"[bench] setup parity at {n}^3: device setup {'==' if ok else '!='} host setup "
+        f"({digests[0][1]} levels, {time.time() - t0:.1f}s)")
+    return {"kind": "sha256 of every level's A, P, R, CF and l1 bytes", "size": f"{n}^3", "equal": ok,
+            "levels": digests[0][1], "device_digest": digests[0][0], "host_digest": digests[1][0]}
 
 
 def amg_settings(hv, pcg, agg=0, relax=18, coarsen=8):
@@ -354,11 +424,14 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
         log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {stored_bytes/1e9:.3f} GB stored -> {achieved:.1f} GB/s "
             f"(CSR-equivalent {csr_gbs:.1f} GB/s); host peak RSS {peak_rss_gb():.1f} GB")
 
-    cpu, parity, parity_detail = None, None, None
+    cpu, parity, parity_detail, parity_pcg = None, None, None, None
     if rank == 0 and not light and args.cpu_cycles > 0 and world == 1 and comm is None:
-        cpu, u_orc, iters = oracle_cpu_baseline(amg, nrows, f"{nx}x{ny}x{nz}", pcg, args)
+        cpu, u_orc, iters, O = oracle_cpu_baseline(amg, nrows, f"{nx}x{ny}x{nz}", pcg, args)
         parity, parity_detail = gpu_parity(hv, amg, krylov, A, b, x, u_orc, iters, pcg)
         del u_orc
+        if not pcg and args.pcg_iters > 0:
+            parity_pcg = pcg_parity(hv, amg, A, b, x, O, nrows, args.pcg_iters)
+        del O
     elif rank == 0 and not light and world > 1:
         # bench contract: the CPU baseline is timed at N = 1 only.  Under strong
         # scaling the N = 1 line runs this same global problem, so its
@@ -405,6 +478,8 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
     }
     if parity_detail is not None:
         out["parity_detail"] = parity_detail
+    if parity_pcg is not None:
+        out["parity_pcg"] = parity_pcg
     if world > 1:
         out["cpu_baseline_note"] = ("timed at N = 1 only (bench contract); strong scaling: the N = 1 line runs "
                                     "the same global problem") if strong else "timed at N = 1 only (bench contract)"
@@ -454,6 +529,11 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
     ap.add_argument("--cpu-cycles-max", type=int, default=60)
     ap.add_argument("--spmv-reps", type=int, default=50)
+    ap.add_argument("--pcg-iters", type=int, default=4,
+                    help="one GPU: configs[2]'s BoomerAMG-PCG on the bench hierarchy for this many iterations, "
+                         "against the C oracle (parity_pcg; 0 = skip)")
+    ap.add_argument("--setup-parity", type=int, default=1,
+                    help="one GPU: device setup vs host setup at the secondary size (setup_parity; 0 = skip)")
     ap.add_argument("--calib", action="store_true",
                     help="also run 512 MiB read streams of 2/4/8-B elements (PMC FETCH_SIZE calibration)")
     ap.add_argument("--solver", choices=["amg", "pcg"], default="amg",
@@ -562,6 +642,8 @@ def main():
         out["secondary"]["config"] = sec["config"]
         out["secondary"]["roofline"] = {k: sec["roofline"][k] for k in ("achieved", "frac", "avg_ms", "kernel",
                                                                         "bytes_per_launch", "per_kernel")}
+        if args.setup_parity:
+            out["setup_parity"] = setup_parity(hv, args, args.secondary_n)
     if out is not None:
         print(json.dumps(out), flush=True)
     if dist:

@@ -1392,14 +1392,41 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver s, HYPRE_Int num_blocks)
         l1[i] = t;
       }
     }
-    for (int fwd = 0; fwd < 2; ++fwd)
-      for (int use_l1 = 0; use_l1 < 2; ++use_l1) {
-        std::string msg;
-        if (gs_schedule_self_check(A, num_blocks, fwd != 0, use_l1 != 0, l1, msg))
-          throw std::runtime_error("level " + std::to_string(l) + (fwd ? " forward" : " backward") +
-                                   (use_l1 ? " l1" : "") + ": " + msg);
-      }
+    // teams of about 64 rows a step (the default) and of a few rows (many
+    // steps per team level: ring reach and fences exercised)
+    for (int team_rows : {64, 3})
+      for (int fwd = 0; fwd < 2; ++fwd)
+        for (int use_l1 = 0; use_l1 < 2; ++use_l1)
+          for (int wgt = 0; wgt < 2; ++wgt) {
+            std::string msg;
+            if (gs_schedule_self_check(A, num_blocks, fwd != 0, use_l1 != 0, l1, msg, team_rows, wgt != 0))
+              throw std::runtime_error("level " + std::to_string(l) + (fwd ? " forward" : " backward") +
+                                       (use_l1 ? " l1" : "") + (wgt ? " weighted" : "") + " team_rows " +
+                                       std::to_string(team_rows) + ": " + msg);
+          }
   }
+  API_END
+}
+
+// Size of the packed hybrid Gauss-Seidel schedule of a level's A for a block
+// count (host only): out = {nnz, stored entries, steps, teams, longest team
+// (steps), blocks}.
+HYPRE_Int hypreve_BoomerAMGGsScheduleStats(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int forward, HYPRE_Int num_blocks,
+                                           int64_t* out) {
+  CHECK_ARG(s && s->kind == KIND_AMG && !s->H.lev.empty(), 1);
+  CHECK_ARG(level >= 0 && level < (HYPRE_Int)s->H.lev.size(), 2);
+  CHECK_ARG(num_blocks >= 1, 4);
+  CHECK_ARG(out, 5);
+  API_BEGIN
+  const CSR& A = s->H.lev[level].A;
+  GsSchedule S;
+  build_gs_schedule(A, hypre_block_starts(A.nrows, num_blocks), forward != 0, S);
+  out[0] = S.nnz;
+  out[1] = (int64_t)S.code.size();
+  out[2] = S.team_step.back();
+  out[3] = S.nteams;
+  out[4] = S.max_steps;
+  out[5] = num_blocks;
   API_END
 }
 

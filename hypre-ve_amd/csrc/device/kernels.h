@@ -84,21 +84,28 @@ hipError_t launch_cheby(int n, int step, int scale, double c, const double* ds, 
 // op: 0 l1-Jacobi w=1, 1 l1-Jacobi weighted, 2 Jacobi (s = diagonal)
 hipError_t launch_zero_guess(int n, int op, double w, const double* f, const double* s, double* u,
                              hipStream_t st);
-// Device view of a hybrid Gauss-Seidel level schedule (host/layout.hpp GsSchedule).
+// Device view of a packed, step-ordered hybrid Gauss-Seidel schedule
+// (host/layout.hpp GsSchedule).
 struct GsView {
-  const int* block_start = nullptr;
-  const int* block_level = nullptr;
-  const int* level_slice = nullptr;
-  const int* slice_ptr = nullptr;
-  const int* col = nullptr;
+  const int* team_step = nullptr;  // nteams + 1 step ranges
+  const int* step = nullptr;       // 4 per step: entry offset (unsigned), position offset, rows, width
+  const int* code = nullptr;       // per entry: source code (layout.hpp)
   const double* val = nullptr;
-  const int* rowmap = nullptr;
-  int nblocks = 0;
-  int wg = 64;  // workgroup size: 64, or 256 for wide levels
+  const int* tcol = nullptr;       // weighted forms: in-block entries' T position (-1 otherwise)
+  const int* rowmap = nullptr;     // position -> row
+  const double* l1 = nullptr;      // l1 norms by position
+  const int* cf = nullptr;         // CF marker by position
+  int nteams = 0, nrows = 0, max_width = 0;
 };
-hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const double* l1, const int* cf,
-                            int relax_points, const double* tmp, double* u, double w, double omega,
-                            hipStream_t st);
+// The sweep's vectors in its order (layout.hpp GsSchedule): G[k] = tmp[rowmap[k]]
+// (T; u when tmp is null), G[n + k] = u[rowmap[k]] (C), F[k] = f[rowmap[k]],
+// and the off-rank halo of u, u[n .. n + nhalo), into G[3n ..).
+hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp, const double* f, int nhalo,
+                            double* G, double* F, hipStream_t st);
+// One hybrid Gauss-Seidel sweep over S: reads G's T, C and halo parts and F,
+// writes G's U part and u (natural rows).
+hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, const double* F,
+                            double* u, double w, double omega, hipStream_t st);
 int sell_batch_override();
 // Tuning knobs read at launch (0 = default): 0 offset-coded row blocks per
 // step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU,

@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include "kernels.h"
+#include "../host/layout.hpp"
 
 #include <algorithm>
 #include <type_traits>
@@ -832,7 +833,7 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
 // slot_base: 4 B an entry and the column without a second gather (P_0, whose
 // offset-coded form needs cmap).
 template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK>
-__device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, const int* ot, int rb0) {
+__device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, const int* ot, int rb0, int rb1) {
   using CT = typename std::conditional<PK, unsigned, unsigned short>::type;
   constexpr unsigned PAD = PK ? 0xFFFFFFFFu : 0xFFFFu;
   const int vb = p.vbits;
@@ -846,7 +847,9 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
   int wmax = 0;
 #pragma unroll
   for (int r = 0; r < NR; ++r) {
-    const int row = map_block(p, rb0 + r) * 256 + (int)threadIdx.x;
+    // blocks from rb1 on belong to the next XCD's share (NR > 1)
+    const bool own = rb0 + r < rb1;
+    const int row = own ? map_block(p, rb0 + r) * 256 + (int)threadIdx.x : p.nrows;
     act[r] = row < p.nrows;
     const int slice = __builtin_amdgcn_readfirstlane(act[r] ? row >> 6 : 0);
     const int beg = p.slice_ptr[slice];
@@ -920,7 +923,7 @@ __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
   const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
   const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
   for (int rb = r0 + (int)(blockIdx.x >> 3) * NR; rb < r1; rb += per_wg * NR)
-    code_rows_op<OP, CFSEL, B, MAP, NR, PK>(p, vt, ot, rb);
+    code_rows_op<OP, CFSEL, B, MAP, NR, PK>(p, vt, ot, rb, r1);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -1234,124 +1237,300 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// Hybrid Gauss-Seidel sweep over a level schedule (host: build_gs_schedule).
-// One workgroup per hypre thread block [ns, ne); its levels run in order with
-// a workgroup barrier between them, the rows of a level in parallel (lane per
-// row).  In-block columns read the iterate being updated (already relaxed for
-// the rows of earlier levels, not yet relaxed for later ones, exactly as the
-// sequential sweep sees them); out-of-block columns read tmp, the copy taken
-// before the sweep (par_relax.c tmp_data / Vext_data).
+// Hybrid Gauss-Seidel sweep over a packed, step-ordered schedule (host:
+// build_gs_schedule, layout.hpp).  One wavefront per team of consecutive
+// hypre thread blocks [ns, ne); the team's steps run in order.  The sweep
+// works on vectors permuted into its order (launch_gs_gather), so a step's
+// rows are contiguous and so, for a grid operator, are the neighbours they read
+// (the next step's rows, or the same step of the teams of the adjacent planes).
+// A step runs in two phases:
+//   products: every lane takes entries of the step (64 at a time, all loads
+//     issued before the first use): code, value, the source value (C / T / U
+//     in HBM, the LDS ring, or the halo), the product a * x into LDS;
+//   row sums: lane r adds its row's products in CSR order from LDS.
+// Rows wider than the LDS product buffer run in chunks of entries.  In-block
+// columns read the iterate being updated (already relaxed for rows of earlier
+// steps, not yet relaxed for later ones, exactly as the sequential sweep sees
+// them): values computed in the last kGsFence steps from the wave's LDS ring,
+// older ones from U, whose stores the wave fences every kGsFence steps; not
+// yet updated ones from C; off-block columns read T, the copy taken before the
+// sweep (par_relax.c tmp_data / Vext_data).  Only U (the team's own positions)
+// and u (natural rows, read by nobody during the sweep) are written, so teams
+// never wait on each other.
 //   L1 = true : cases 8/13/14, res = f - sum_all a*u, u += res / l1
 //   L1 = false: cases 3/4/6,   res = f - sum_offdiag a*u, u = res / a_ii
 //   WGT (relax_weight w or omega != 1, par_relax.c:1277/4544): the diagonal
 //   entry skipped; in-block res0 -= a*u, res2 += a*Vtemp; off-block
 //   res -= a*tmp; u = u*(1 - w*omega); u += w*(omega*res + res0 + (1-omega)*res2)/d
-//   with d = l1 or a_ii.  Vtemp and tmp are the same pre-sweep copy.
+//   with d = l1 or a_ii.  Vtemp and tmp are the same pre-sweep copy (T).
+// A padding entry (code -1) contributes the product +0, which leaves every
+// value of a subtraction unchanged (signed zeros included).
 // ---------------------------------------------------------------------------
 struct GsArgs {
-  const int* __restrict__ block_start;
-  const int* __restrict__ block_level;
-  const int* __restrict__ level_slice;
-  const int* __restrict__ slice_ptr;
-  const int* __restrict__ col;
+  const int* __restrict__ team_step;
+  const int* __restrict__ step;
+  const int* __restrict__ code;
   const double* __restrict__ val;
+  const int* __restrict__ tcol;
   const int* __restrict__ rowmap;
-  const double* __restrict__ f;
   const double* __restrict__ l1;
   const int* __restrict__ cf;
-  const double* tmp;
+  double* G;  // T | C | U | halo (layout.hpp)
+  const double* __restrict__ F;
   double* u;
-  int relax_points;
+  int n, nteams, relax_points;
   double w, omega;
 };
+static constexpr int kGsWaves = 2;  // teams per workgroup
 
-template <bool L1, bool CFSEL, bool WGT, int WG>
-__global__ void __launch_bounds__(WG) k_hybrid_gs(GsArgs p) {
-  constexpr int B = 8;
-  const int blk = blockIdx.x;
-  const int ns = p.block_start[blk], ne = p.block_start[blk + 1];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
-  constexpr int nwaves = WG / kWave;
-  for (int lv = p.block_level[blk]; lv < p.block_level[blk + 1]; ++lv) {
-    for (int sl = p.level_slice[lv] + wave; sl < p.level_slice[lv + 1]; sl += nwaves) {
-      const int i = p.rowmap[(size_t)sl * kWave + lane];
-      if (i < 0) continue;
-      if (CFSEL && p.cf[i] != p.relax_points) continue;
-      const int beg = p.slice_ptr[sl];
-      const int width = (p.slice_ptr[sl + 1] - beg) >> 6;
-      const int* __restrict__ cp = p.col + beg + lane;
-      const double* __restrict__ vp = p.val + beg + lane;
-      double scale;
-      int k0;
-      if (L1) {
-        scale = p.l1[i];
-        k0 = WGT ? 1 : 0;
-      } else {
-        scale = vp[0];  // diagonal stored first
-        k0 = 1;
+__device__ __forceinline__ void gs_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Per wave LDS: the ring, and the staging of one step (its first chunk of
+// PROD entries: codes, values (overwritten by the products), the weighted
+// forms' Vtemp positions / second products / classes; its rows' map, C, F,
+// l1 and cf).  The staging of step j + 1 is loaded while step j's gathers are
+// in flight (one global latency per step) and written after step j's sums.
+template <int PROD, bool WGT>
+struct GsLds {
+  double ring[kGsRingSlots];
+  double val[PROD];
+  int code[PROD];
+  int tcol[WGT ? PROD : 1];
+  double prod2[WGT ? PROD : 1];
+  unsigned char cls[WGT ? PROD : 1];
+  int row[64], cf[64];
+  double c[64], f[64], l1[64];
+};
+
+// Registers of a prefetched step: entries lane + 64 t of its first chunk.
+template <int PER, bool WGT>
+struct GsPre {
+  int c[PER], tc[WGT ? PER : 1];
+  double a[PER];
+  int row, cf;
+  double cv, fv, l1v;
+};
+
+template <bool L1, bool CFSEL, bool WGT, int PROD>
+__device__ __forceinline__ void gs_prefetch(const GsArgs& p, const int4 m, int lane, GsPre<PROD / 64, WGT>& P) {
+  constexpr int PER = PROD / 64;
+  const int R = m.z, W = m.w;
+  const int KC = PROD / R;
+  const int E = min(KC, W) * R;
+  const unsigned ent = (unsigned)m.x;
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    if (64 * t >= E) break;
+    const int e = lane + 64 * t;
+    const unsigned o = ent + (unsigned)(e < E ? e : 0);
+    P.c[t] = p.code[o];
+    P.a[t] = p.val[o];
+    if (WGT) P.tc[t] = p.tcol[o];
+  }
+  const int kp = m.y + (lane < R ? lane : R - 1);
+  P.row = p.rowmap[kp];
+  P.cv = p.G[p.n + kp];
+  P.fv = p.F[kp];
+  if (L1) P.l1v = p.l1[kp];
+  if (CFSEL) P.cf = p.cf[kp];
+}
+
+template <bool L1, bool CFSEL, bool WGT, int PROD>
+__device__ __forceinline__ void gs_stage(const int4 m, int lane, const GsPre<PROD / 64, WGT>& P,
+                                         GsLds<PROD, WGT>& S) {
+  constexpr int PER = PROD / 64;
+  const int R = m.z, W = m.w;
+  const int E = min(PROD / R, W) * R;
+#pragma unroll
+  for (int t = 0; t < PER; ++t) {
+    if (64 * t >= E) break;
+    const int e = lane + 64 * t;
+    if (e < E) {
+      S.code[e] = P.c[t];
+      S.val[e] = P.a[t];
+      if (WGT) S.tcol[e] = P.tc[t];
+    }
+  }
+  S.row[lane] = P.row;
+  S.c[lane] = P.cv;
+  S.f[lane] = P.fv;
+  if (L1) S.l1[lane] = P.l1v;
+  if (CFSEL) S.cf[lane] = P.cf;
+}
+
+template <bool L1, bool CFSEL, bool WGT, int PROD>
+__global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
+  constexpr int PER = PROD / 64;
+  __shared__ GsLds<PROD, WGT> lds_all[kGsWaves];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int team = blockIdx.x * kGsWaves + wave;
+  if (team >= p.nteams) return;
+  GsLds<PROD, WGT>& S = lds_all[wave];
+  const int s0 = __builtin_amdgcn_readfirstlane(p.team_step[team]);
+  const int ns = __builtin_amdgcn_readfirstlane(p.team_step[team + 1]) - s0;
+  // step metadata through the scalar cache (read-only, constant address space)
+  using cint = const __attribute__((address_space(4))) int;
+  cint* const steps = (cint*)(p.step + 4 * (size_t)s0);
+  auto meta = [&](int j) -> int4 {
+    cint* q = steps + 4 * (j < ns ? j : ns - 1);
+    int4 m;
+    m.x = q[0]; m.y = q[1]; m.z = q[2]; m.w = q[3];
+    return m;
+  };
+  constexpr int k0 = (L1 && !WGT) ? 0 : 1;  // the diagonal (stored first) is skipped unless l1 scales
+  {
+    GsPre<PER, WGT> P;
+    const int4 m = meta(0);
+    gs_prefetch<L1, CFSEL, WGT, PROD>(p, m, lane, P);
+    gs_stage<L1, CFSEL, WGT, PROD>(m, lane, P, S);
+    gs_wave_sync();
+  }
+  for (int j = 0; j < ns; ++j) {
+    const int4 m = meta(j);
+    const unsigned ent = (unsigned)m.x;
+    const int R = m.z, W = m.w;
+    const int r = lane < R ? lane : R - 1;
+    const int KC = PROD / R;
+    double res = 0.0, res0 = 0.0, res2 = 0.0;
+    GsPre<PER, WGT> P;
+    for (int kc = 0; kc < W; kc += KC) {
+      const int kw = min(KC, W - kc), E = kw * R;
+      int c[PER], tc[PER];
+      double a[PER], x[PER], rv[PER], t2[PER];
+      if (kc == 0) {  // the staged first chunk
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+          if (64 * t >= E) break;
+          const int e = lane + 64 * t < E ? lane + 64 * t : 0;
+          c[t] = S.code[e];
+          a[t] = S.val[e];
+          tc[t] = WGT ? S.tcol[e] : -1;
+        }
+      } else {  // later chunks of wide rows: from HBM in place
+        const unsigned base = ent + (unsigned)(kc * R);
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+          if (64 * t >= E) break;
+          const int e = lane + 64 * t;
+          const unsigned o = base + (unsigned)(e < E ? e : 0);
+          c[t] = p.code[o];
+          a[t] = p.val[o];
+          tc[t] = WGT ? p.tcol[o] : -1;
+        }
       }
-      if (scale == 0.0) continue;
-      double res = p.f[i];
-      if (WGT) {
-        double res0 = 0.0, res2 = 0.0;
-        for (int k = k0; k < width; ++k) {
-          const int cc = cp[k * kWave];
-          if (cc < 0) continue;
-          const double a = vp[k * kWave];
-          if (cc >= ns && cc < ne) {
-            res0 -= a * p.u[cc];
-            res2 += a * p.tmp[cc];
-          } else {
-            res -= a * p.tmp[cc];
+      // the next step's staging data, issued with this chunk's gathers (one
+      // wait covers both)
+      if (kc == 0) gs_prefetch<L1, CFSEL, WGT, PROD>(p, meta(j + 1), lane, P);
+#pragma unroll
+      for (int t = 0; t < PER; ++t) {
+        if (64 * t >= E) break;
+        x[t] = p.G[c[t] > 0 ? c[t] : 0];
+        if (WGT) t2[t] = p.G[tc[t] > 0 ? tc[t] : 0];
+      }
+#pragma unroll
+      for (int t = 0; t < PER; ++t) {
+        if (64 * t >= E) break;
+        rv[t] = S.ring[c[t] < -1 ? -2 - c[t] : 0];
+      }
+#pragma unroll
+      for (int t = 0; t < PER; ++t) {
+        if (64 * t >= E) break;
+        const int e = lane + 64 * t;
+        const int cc = c[t];
+        const double xv = cc < -1 ? rv[t] : x[t];
+        const double pv = cc == -1 ? 0.0 : a[t] * xv;
+        if (e < E) {
+          S.val[e] = pv;  // the product replaces the staged value
+          if (WGT) {
+            S.prod2[e] = tc[t] >= 0 ? a[t] * t2[t] : 0.0;
+            S.cls[e] = tc[t] >= 0;
           }
         }
-        double ui = p.u[i];
-        ui *= 1.0 - p.w * p.omega;
-        ui += p.w * (p.omega * res + res0 + (1.0 - p.omega) * res2) / scale;
-        p.u[i] = ui;
-        continue;
       }
-      for (int k = k0; k < width; k += B) {
-        int c[B];
-        double a[B], xv[B];
-#pragma unroll
-        for (int q = 0; q < B; ++q) {
-          const bool in = (k + q) < width;
-          c[q] = in ? cp[(k + q) * kWave] : -1;
-          a[q] = in ? vp[(k + q) * kWave] : 0.0;
+      gs_wave_sync();
+      if (kc == 0) res = S.f[r];
+      for (int kk = 0; kk < kw; ++kk) {
+        if (kc + kk < k0) continue;
+        const int e = kk * R + r;
+        const double pv = S.val[e];
+        if (WGT && S.cls[e]) {
+          res0 -= pv;
+          res2 += S.prod2[e];
+        } else {
+          res -= pv;
         }
-#pragma unroll
-        for (int q = 0; q < B; ++q) {
-          const int cc = c[q];
-          xv[q] = cc < 0 ? 0.0 : ((cc >= ns && cc < ne) ? p.u[cc] : p.tmp[cc]);
-        }
-#pragma unroll
-        for (int q = 0; q < B; ++q)
-          if (c[q] >= 0) res -= a[q] * xv[q];
       }
-      if (L1) p.u[i] += res / scale;
-      else p.u[i] = res / scale;
+      gs_wave_sync();  // the next chunk overwrites the products
     }
-    __syncthreads();  // workgroup-scope release/acquire: the level's updates are visible to the next
+    const int kp = m.y + r;
+    const int i = S.row[r];
+    const double uo = S.c[r];
+    const double sc = L1 ? S.l1[r] : p.val[ent + r];
+    const bool run = lane < R && sc != 0.0 && !(CFSEL && S.cf[r] != p.relax_points);
+    double un = uo;
+    if (WGT) {
+      double ui = un;
+      ui *= 1.0 - p.w * p.omega;
+      ui += p.w * (p.omega * res + res0 + (1.0 - p.omega) * res2) / sc;
+      un = run ? ui : un;
+    } else {
+      const double v = L1 ? un + res / sc : res / sc;
+      un = run ? v : un;
+    }
+    if (lane < R) p.G[2 * p.n + kp] = un;
+    if (run) p.u[i] = un;
+    S.ring[(j % kGsRing) * kWave + lane] = un;
+    gs_stage<L1, CFSEL, WGT, PROD>(meta(j + 1), lane, P, S);
+    gs_wave_sync();  // the ring slot and the next step's staging
+    // the U stores of the last kGsFence steps complete: later steps read them
+    if (j % kGsFence == kGsFence - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
   }
 }
 
-hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, const double* f, const double* l1, const int* cf,
-                            int relax_points, const double* tmp, double* u, double w, double omega,
-                            hipStream_t st) {
-  if (S.nblocks <= 0) return hipSuccess;
+__global__ void k_gs_gather(int n, int nhalo, const int* __restrict__ rowmap, const double* __restrict__ u,
+                            const double* __restrict__ tmp, const double* __restrict__ f, double* __restrict__ G,
+                            double* __restrict__ F) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
+    const int i = rowmap[k];
+    const double v = u[i];
+    G[k] = tmp ? tmp[i] : v;
+    G[n + k] = v;
+    F[k] = f[i];
+  }
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nhalo; k += gridDim.x * blockDim.x) G[3 * n + k] = u[n + k];
+}
+
+hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp, const double* f, int nhalo,
+                            double* G, double* F, hipStream_t st) {
+  if (S.nrows <= 0) return hipSuccess;
+  const int grid = std::min((S.nrows + 255) / 256, 256 * 16);
+  hipLaunchKernelGGL(k_gs_gather, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.rowmap, u, tmp, f, G, F);
+  return hipGetLastError();
+}
+
+hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, const double* F,
+                            double* u, double w, double omega, hipStream_t st) {
+  if (S.nteams <= 0) return hipSuccess;
   GsArgs a;
-  a.block_start = S.block_start; a.block_level = S.block_level; a.level_slice = S.level_slice;
-  a.slice_ptr = S.slice_ptr; a.col = S.col; a.val = S.val; a.rowmap = S.rowmap;
-  a.f = f; a.l1 = l1; a.cf = cf; a.tmp = tmp ? tmp : u; a.u = u; a.relax_points = relax_points;
-  a.w = w; a.omega = omega;
-  const bool cfsel = relax_points != 0 && cf != nullptr;
+  a.team_step = S.team_step; a.step = S.step; a.code = S.code; a.val = S.val; a.tcol = S.tcol; a.rowmap = S.rowmap;
+  a.l1 = S.l1; a.cf = S.cf; a.G = G; a.F = F; a.u = u;
+  a.n = S.nrows; a.nteams = S.nteams; a.relax_points = relax_points; a.w = w; a.omega = omega;
   const bool wgt = w != 1.0 || omega != 1.0;
-  if (wgt && !tmp) return hipErrorInvalidValue;  // the weighted forms read the pre-sweep copy
-  const dim3 grid(S.nblocks);
-#define HVE_G(L1V, CFV, WV)                                                                           \
-  if (S.wg == 256) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, 256>), grid, dim3(256), 0, st, a); \
-  else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, 64>), grid, dim3(64), 0, st, a);
+  if (wgt && !S.tcol) return hipErrorInvalidValue;   // the weighted forms read Vtemp in-block
+  if (use_l1 && !S.l1) return hipErrorInvalidValue;
+  if (cfsel && !S.cf) return hipErrorInvalidValue;
+  const dim3 grid((S.nteams + kGsWaves - 1) / kGsWaves), blk(kGsWaves * kWave);
+#define HVE_G(L1V, CFV, WV)                                                                   \
+  if (S.max_width > 8) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, 1024>), grid, blk, 0, st, a); \
+  else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, 512>), grid, blk, 0, st, a);
 #define HVE_GW(L1V, CFV) \
   if (wgt) { HVE_G(L1V, CFV, true) } else { HVE_G(L1V, CFV, false) }
   if (use_l1) {

@@ -470,7 +470,7 @@ dict:
       }();
       std::vector<unsigned short> vi16;
       std::vector<double> tab;
-      if (group == 1 && !ranges && (dict_vt_env != 0 || policy == 5) && sell_valtab_env() != 0 &&
+      if (group == 1 && !ranges && !relax_ops && (dict_vt_env != 0 || policy == 5) && sell_valtab_env() != 0 &&
           (size_t)(dmax + 4096) * sizeof(double) <= 64 * 1024 && build_value_table16(val, 4096, vi16, tab)) {
         vidx16 = dupload(vi16.data(), vi16.size());
         vtab = dupload(tab.data(), tab.size());
@@ -655,32 +655,45 @@ void DevSell::release() {
   notab = vbits = 0; anc_n = cmap_n = 0;
 }
 
-void DevGs::upload(const CSR& A, int num_blocks, bool forward) {
-  upload(A, hypre_block_starts(A.nrows, num_blocks), forward);
+// Team size of the packed schedule: about this many rows per step
+// (HVE_GS_TEAM_ROWS overrides, tuning).
+static int gs_team_rows() {
+  static const int v = [] {
+    const char* e = getenv("HVE_GS_TEAM_ROWS");
+    const int r = e ? atoi(e) : 0;
+    return r > 0 ? r : 64;
+  }();
+  return v;
 }
-void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forward) {
+void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forward, bool weighted,
+                   const std::vector<double>& l1_rows, const std::vector<int>& cf_rows) {
   release();
   GsSchedule S;
-  build_gs_schedule(A, block_starts, forward, S);
+  build_gs_schedule(A, block_starts, forward, S, gs_team_rows(), weighted, &l1_rows, &cf_rows);
+  nrows = A.nrows;
   nblocks = (int)S.block_start.size() - 1;
-  max_levels = S.max_levels;
-  wg = S.avg_rows_per_level > 96.0 ? 256 : 64;
-  block_start = dupload(S.block_start.data(), S.block_start.size());
-  block_level = dupload(S.block_level.data(), S.block_level.size());
-  level_slice = dupload(S.level_slice.data(), S.level_slice.size());
-  slice_ptr = dupload(S.slice_ptr.data(), S.slice_ptr.size());
-  col = dupload(S.col.data(), std::max<size_t>(1, S.col.size()));
+  nteams = S.nteams;
+  max_steps = S.max_steps;
+  max_width = S.max_width;
+  entries = (int64_t)S.code.size();
+  nnz = S.nnz;
+  team_step = dupload(S.team_step.data(), S.team_step.size());
+  step = dupload(S.step.data(), std::max<size_t>(4, S.step.size()));
+  code = dupload(S.code.data(), std::max<size_t>(1, S.code.size()));
   val = dupload(S.val.data(), std::max<size_t>(1, S.val.size()));
+  if (weighted) tcol = dupload(S.tcol.data(), std::max<size_t>(1, S.tcol.size()));
   rowmap = dupload(S.rowmap.data(), std::max<size_t>(1, S.rowmap.size()));
+  if (!S.l1.empty()) l1 = dupload(S.l1.data(), S.l1.size());
+  if (!S.cf.empty()) cf = dupload(S.cf.data(), S.cf.size());
 }
 void DevGs::release() {
-  for (void* p : {(void*)block_start, (void*)block_level, (void*)level_slice, (void*)slice_ptr, (void*)col,
-                  (void*)val, (void*)rowmap})
+  for (void* p : {(void*)team_step, (void*)step, (void*)code, (void*)val, (void*)tcol, (void*)rowmap, (void*)l1,
+                  (void*)cf})
     if (p) (void)hipFree(p);
-  block_start = block_level = level_slice = slice_ptr = col = rowmap = nullptr;
-  val = nullptr;
-  nblocks = 0;
-  max_levels = 0;
+  team_step = step = code = tcol = rowmap = cf = nullptr;
+  val = l1 = nullptr;
+  nrows = nteams = nblocks = max_steps = max_width = 0;
+  entries = nnz = 0;
 }
 
 void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key, const DevSell::Coded* coded,
@@ -688,6 +701,7 @@ void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key
   static const bool tlog = getenv("HVE_SETUP_T") != nullptr;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = now();
+  in.relax_ops = bd.relax_ops = relax_ops;
   in.upload(op.interior, op.map_int, policy, key, coded, tile);
   if (tlog)
     fprintf(stderr, "[upload] %d rows %lld nnz: %s %.3fs\n", op.interior.nrows, (long long)op.interior.nnz(),
@@ -728,14 +742,13 @@ void DevHalo::release() {
 DevAMG::~DevAMG() { release(); }
 
 void DevAMG::release() {
-  for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
-  graphs_.clear();
+  graphs_clear();
   for (auto& L : lev_) {
     L.A.release(); L.P.release(); L.R.release();
     L.hu.release(); L.hv.release();
     L.gs_fwd.release(); L.gs_bwd.release();
     for (void* p : {(void*)L.l1, (void*)L.cf, (void*)L.cf_l1, (void*)L.F, (void*)L.U[0], (void*)L.U[1], (void*)L.V,
-                    (void*)L.gs_tmp, (void*)L.cheby_ds, (void*)L.cheby_r, (void*)L.cheby_t, (void*)L.cheby_o})
+                    (void*)L.gs_tmp, (void*)L.gs_G, (void*)L.gs_F, (void*)L.cheby_ds, (void*)L.cheby_r, (void*)L.cheby_t, (void*)L.cheby_o})
       if (p) (void)hipFree(p);
   }
   lev_.clear();
@@ -955,11 +968,19 @@ double bench_operator(const CSR& A, int op, int policy, int nbands, int reps, do
   HVE_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   HVE_HIP(launch_set(n, 1.0, x, st));
   HVE_HIP(launch_set(n, 0.5, b, st));
+  // the l1-Jacobi ops: the stencil and delta layouts form the norms from their
+  // entries (as the cycle runs them); every other layout reads a norm vector
+  const bool l1op = op == K_L1JAC || op == K_L1JAC_W || op == K_RESID_L1JAC;
+  double* l1 = nullptr;
+  if (l1op && !M.delta_like()) {
+    l1 = dalloc<double>(n);
+    HVE_HIP(launch_set(n, 8.0, l1, st));
+  }
   auto one = [&]() {
     if (op == K_RESID_L1JAC)
-      HVE_HIP(launch_sell(op, M.view(), x, b, nullptr, nullptr, 0, nullptr, 1.0, 0.0, st, y2, nrm));
+      HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, nullptr, 1.0, 0.0, st, y2, nrm));
     else
-      HVE_HIP(launch_sell(op, M.view(), x, b, nullptr, nullptr, 0, y, op == K_RESID ? -1.0 : 1.0, 0.0, st));
+      HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, y, op == K_RESID ? -1.0 : 1.0, 0.0, st));
   };
   for (int w = 0; w < 3; ++w) one();
   hipEvent_t e0, e1;
@@ -974,7 +995,8 @@ double bench_operator(const CSR& A, int op, int policy, int nbands, int reps, do
   (void)hipEventDestroy(e0);
   (void)hipEventDestroy(e1);
   (void)hipStreamDestroy(st);
-  for (double* p : {x, b, y, y2, nrm}) (void)hipFree(p);
+  for (double* p : {x, b, y, y2, nrm, l1})
+    if (p) (void)hipFree(p);
   M.release();
   return ms / reps;
 }
@@ -1028,6 +1050,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     }();
     const std::vector<int64_t>* tl = ((l == 1 || (l >= 2 && a2_tiles)) && !tiles[l].empty()) ? &tiles[l] : nullptr;
     const std::vector<int64_t>* tc = (l + 1 < nl && !tiles[l + 1].empty()) ? &tiles[l + 1] : nullptr;
+    D.A.relax_ops = true;
     D.A.upload(L.A, prm.sell_policy, kl, nullptr, tl);
     D.hu.upload(L.hu);
     if (l < nl - 1) {
@@ -1108,9 +1131,12 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       if (l == nl - 1 && R.coarse_n > 0) break;  // coarsest level: direct solve
       const CSR rows = merged_rows(L.A, L.n_loc);
       const std::vector<int> bs = L.gs_blocks.empty() ? hypre_block_starts(L.n_loc, prm.blocks_for(L.n_loc)) : L.gs_blocks;
-      if (fwd) D.gs_fwd.upload(rows, bs, true);
-      if (bwd) D.gs_bwd.upload(rows, bs, false);
-      D.gs_tmp = dalloc<double>(D.n + D.hu.n_halo);
+      const bool weighted = prm.wt(l) != 1.0 || prm.omega(l) != 1.0;  // the w / omega forms also read tmp in-block
+      if (fwd) D.gs_fwd.upload(rows, bs, true, weighted, L.l1, L.cf);
+      if (bwd) D.gs_bwd.upload(rows, bs, false, weighted, L.l1, L.cf);
+      D.gs_G = dalloc<double>(3 * (size_t)D.n + D.hu.n_halo + 1);
+      D.gs_F = dalloc<double>((size_t)D.n + 1);
+      if (fwd && bwd) D.gs_tmp = dalloc<double>((size_t)D.n + 1);
     }
   }
   coarse_n_ = R.coarse_n;
@@ -1178,6 +1204,7 @@ void DevAMG::set_use_graph(bool g) {
 void DevAMG::graphs_clear() {
   for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
   graphs_.clear();
+  eager_runs_.clear();  // a new hierarchy or communicator connects its peers again
 }
 
 void DevAMG::dot(int n, const double* x, const double* y, double* out, hipStream_t s) {
@@ -1358,24 +1385,28 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       if (use_l1 && !L.l1) throw std::runtime_error("l1 norms missing for l1 hybrid Gauss-Seidel");
       if ((fw && !L.gs_fwd.built()) || (bw && !L.gs_bwd.built()))
         throw std::runtime_error("hybrid Gauss-Seidel schedule missing on level " + std::to_string(level));
+      if (weighted && ((fw && !L.gs_fwd.tcol) || (bw && !L.gs_bwd.tcol)))
+        throw std::runtime_error("weighted hybrid Gauss-Seidel on level " + std::to_string(level) +
+                                 ": the relaxation weight changed after the setup built the schedule");
       if (zero_guess) HVE_HIP(launch_set(n, 0.0, u_cur, s));
       // off-rank values of u before the sweep (par_relax.c: Vext_data)
-      const bool ex = comm_ && L.hu.active();
-      if (ex) {
+      if (comm_ && L.hu.active()) {
         halo_start(L.hu, u_cur, s);
         halo_finish(s);
       }
-      const int nh = n + L.hu.n_halo;
-      const double* tmp = L.hu.n_halo > 0 ? u_cur : nullptr;  // halo columns: u's halo, untouched by the sweep
-      if (weighted || (L.gs_fwd.built() ? L.gs_fwd.nblocks > 1 : L.gs_bwd.nblocks > 1)) {
-        // tmp_data[i] = u_data[i] (= Vtemp_data of the weighted forms, one copy for both halves of 6/8)
-        HVE_HIP(launch_copy(nh, u_cur, L.gs_tmp, s));
-        tmp = L.gs_tmp;
+      const bool cfsel = relax_points != 0 && L.cf != nullptr;
+      // symmetric sweeps (6, 8): the second half's off-block columns (and the
+      // weighted forms' Vtemp) read u from before the first half (tmp_data),
+      // its in-block ones the first half's result
+      if (fw && bw) HVE_HIP(launch_copy(n, u_cur, L.gs_tmp, s));
+      if (fw) {
+        HVE_HIP(launch_gs_gather(L.gs_fwd.view(), u_cur, nullptr, f, L.hu.n_halo, L.gs_G, L.gs_F, s));
+        HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, cfsel, relax_points, L.gs_G, L.gs_F, u_cur, w, omega, s));
       }
-      if (fw)
-        HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, w, omega, s));
-      if (bw)
-        HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, f, L.l1, L.cf, relax_points, tmp, u_cur, w, omega, s));
+      if (bw) {
+        HVE_HIP(launch_gs_gather(L.gs_bwd.view(), u_cur, fw ? L.gs_tmp : nullptr, f, L.hu.n_halo, L.gs_G, L.gs_F, s));
+        HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, cfsel, relax_points, L.gs_G, L.gs_F, u_cur, w, omega, s));
+      }
       break;
     }
     case 16: {
@@ -1599,9 +1630,47 @@ void DevAMG::cycle(const double* f, double* u, hipStream_t s, const double* pres
       for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
       graphs_.clear();
     }
+    if (comm_ && !graph_replay_matches(ge, f, u, s, pre, zero_u)) {
+      (void)hipGraphExecDestroy(ge);
+      capture_failed("the replayed graph's iterate differs from the eager cycle's");
+      return;  // u holds the eager cycle's result
+    }
     it = graphs_.emplace(key, ge).first;
+    if (comm_) return;  // the validation ran this cycle
   }
   HVE_HIP(hipGraphLaunch(it->second, s));
+}
+
+// Several ranks: a captured cycle is trusted only after one replay has given
+// the eager cycle's iterate bit for bit on every rank (the same inputs run
+// both ways; u then holds that result).  A graph that captures but replays
+// wrongly (a transport whose stream-ordered calls do not record faithfully)
+// turns graphs off for the run.
+bool DevAMG::graph_replay_matches(hipGraphExec_t ge, const double* f, double* u, hipStream_t s, bool pre,
+                                  bool zero_u) {
+  (void)f;
+  const int n = lev_[0].n;
+  double* pb = pre ? presmooth_buffer() : nullptr;
+  const int np = pb ? n + lev_[0].hu.n_halo : 0;
+  double* save = dalloc<double>((size_t)n + np + 1);
+  HVE_HIP(launch_copy(n, u, save, s));
+  if (pb) HVE_HIP(launch_copy(np, pb, save + n, s));
+  HVE_HIP(hipGraphLaunch(ge, s));
+  std::vector<double> hg(n), he(n);
+  HVE_HIP(hipMemcpyAsync(hg.data(), u, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  HVE_HIP(launch_copy(n, save, u, s));
+  if (pb) HVE_HIP(launch_copy(np, save + n, pb, s));
+  emit_cycle(f, u, s, pre, zero_u);
+  HVE_HIP(hipMemcpyAsync(he.data(), u, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  HVE_HIP(hipStreamSynchronize(s));
+  const double bad = std::memcmp(hg.data(), he.data(), sizeof(double) * n) != 0 ? 1.0 : 0.0;
+  HVE_HIP(hipMemcpyAsync(save, &bad, sizeof(double), hipMemcpyHostToDevice, s));
+  comm_->allreduce_sum(save, 1, s);
+  double any = 0.0;
+  HVE_HIP(hipMemcpyAsync(&any, save, sizeof(double), hipMemcpyDeviceToHost, s));
+  HVE_HIP(hipStreamSynchronize(s));
+  (void)hipFree(save);
+  return any == 0.0;
 }
 
 // par_amg_solve.c:22 hypre_BoomerAMGSolve

@@ -73,6 +73,10 @@ struct DevSell {
   // packed layout (SellView::code32): one 32-bit code per slot, the slice
   // bases in slot_base, the values in vtab
   unsigned* code32 = nullptr;
+  // the operator is also applied by the residual and smoother ops (a level's
+  // A), whose kernels do not take the 16-bit value-table dictionary layout;
+  // configuration, kept across release()
+  bool relax_ops = false;
   SellView view() const {
     SellView v;
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
@@ -135,6 +139,7 @@ struct DevSell {
 // Rows of one operator a rank applies, split by whether they read halo values.
 struct DevOp {
   DevSell in, bd;
+  bool relax_ops = false;  // DevSell::relax_ops of both parts
   int nrows_local = 0;
   int64_t nnz() const { return in.nnz + bd.nnz; }
   // coded: grid context for the interior rows (DevSell::Coded)
@@ -143,25 +148,28 @@ struct DevOp {
   void release() { in.release(); bd.release(); }
 };
 
-// Level schedule of one hybrid Gauss-Seidel sweep direction, in HBM.
+// Packed, step-ordered schedule of one hybrid Gauss-Seidel sweep direction,
+// in HBM (host/layout.hpp GsSchedule).
 struct DevGs {
-  int* block_start = nullptr;
-  int* block_level = nullptr;
-  int* level_slice = nullptr;
-  int* slice_ptr = nullptr;
-  int* col = nullptr;
+  int* team_step = nullptr;
+  int* step = nullptr;
+  int* code = nullptr;
   double* val = nullptr;
+  int* tcol = nullptr;  // only when a weighted form may run
   int* rowmap = nullptr;
-  int nblocks = 0, wg = 64, max_levels = 0;
+  double* l1 = nullptr;  // by position
+  int* cf = nullptr;     // by position
+  int nrows = 0, nteams = 0, nblocks = 0, max_steps = 0, max_width = 0;
+  int64_t entries = 0, nnz = 0;
   bool built() const { return nblocks > 0; }
   GsView view() const {
     GsView v;
-    v.block_start = block_start; v.block_level = block_level; v.level_slice = level_slice;
-    v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.nblocks = nblocks; v.wg = wg;
+    v.team_step = team_step; v.step = step; v.code = code; v.val = val; v.tcol = tcol; v.rowmap = rowmap;
+    v.l1 = l1; v.cf = cf; v.nteams = nteams; v.nrows = nrows; v.max_width = max_width;
     return v;
   }
-  void upload(const CSR& A, int num_blocks, bool forward);
-  void upload(const CSR& A, const std::vector<int>& block_starts, bool forward);
+  void upload(const CSR& A, const std::vector<int>& block_starts, bool forward, bool weighted,
+              const std::vector<double>& l1_rows, const std::vector<int>& cf_rows);
   void release();
 };
 
@@ -191,7 +199,9 @@ struct DevLevel {
   double* U[2] = {nullptr, nullptr};  // n + hu.n_halo each
   double* V = nullptr;                // n + hv.n_halo
   DevGs gs_fwd, gs_bwd;               // hybrid Gauss-Seidel schedules (when a cycle uses them)
-  double* gs_tmp = nullptr;           // pre-sweep copy of u (n + hu.n_halo)
+  double* gs_G = nullptr;             // the sweep's T | C | U | halo vectors (3n + hu.n_halo)
+  double* gs_F = nullptr;             // the sweep's right-hand side (n)
+  double* gs_tmp = nullptr;           // symmetric sweeps: u before the first half (n)
   // Chebyshev (relax 16): ds on the device, coefficients on the host (kernel
   // arguments), work vectors r, tmp (n + halo: A is applied to it), orig
   double* cheby_ds = nullptr;
@@ -246,6 +256,7 @@ class DevAMG {
   void emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed, bool zero_u = false);
   bool can_fuse_presmooth() const;
   void capture_failed(const char* why);
+  bool graph_replay_matches(hipGraphExec_t ge, const double* f, double* u, hipStream_t s, bool pre, bool zero_u);
   double* presmooth_buffer();
   void relax(int level, int relax_type, int relax_points, const double* f, double*& u_cur, double*& u_alt,
              bool zero_guess, hipStream_t s);

@@ -1,6 +1,7 @@
 // Host-side construction of the HBM layouts consumed by the device runtime.
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstdint>
 #include <cstring>
 #include <stdexcept>
@@ -663,13 +664,19 @@ std::vector<int> hypre_block_starts(int n, int nb) {
   return st;
 }
 
-void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool forward, GsSchedule& S) {
-  const int nb = (int)block_start.size() - 1;
-  S.block_start = block_start;
-  // per block: levels of its rows, then rows grouped by level (ascending row
-  // order inside a level, as the reference's stable sort by level leaves them)
-  std::vector<std::vector<int>> lvl_rows_ptr(nb), lvl_rows(nb);
-  std::vector<int> level(A.nrows, 0), floor_(A.nrows, 0);
+namespace {
+// Rows of each block grouped by level (GsSchedule): byl[ns .. ne) holds block
+// b's rows by ascending (level, row), lptr[b] its level boundaries.
+struct GsLevels {
+  std::vector<std::vector<int>> lptr;
+  std::vector<int> byl, nlev;
+};
+void gs_levels(const CSR& A, const std::vector<int>& block_start, bool forward, GsLevels& G) {
+  const int n = A.nrows, nb = (int)block_start.size() - 1;
+  G.lptr.assign(nb, {});
+  G.byl.assign(n, 0);
+  G.nlev.assign(nb, 0);
+  std::vector<int> level(n, 0), floor_(n, 0);
 #pragma omp parallel for schedule(dynamic, 16)
   for (int b = 0; b < nb; ++b) {
     const int ns = block_start[b], ne = block_start[b + 1];
@@ -691,125 +698,305 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
         if ((forward && c > i) || (!forward && c < i)) floor_[c] = std::max(floor_[c], L + 1);
       }
     }
-    auto& ptr = lvl_rows_ptr[b];
-    auto& rows = lvl_rows[b];
-    ptr.assign(nlev + 1, 0);
-    for (int i = ns; i < ne; ++i) ptr[level[i] + 1]++;
-    for (int l = 0; l < nlev; ++l) ptr[l + 1] += ptr[l];
-    rows.resize(ne - ns);
-    std::vector<int> pos(ptr.begin(), ptr.end() - 1);
-    for (int i = ns; i < ne; ++i) rows[pos[level[i]]++] = i;
+    G.nlev[b] = nlev;
+    auto& p = G.lptr[b];
+    p.assign(nlev + 1, 0);
+    for (int i = ns; i < ne; ++i) p[level[i] + 1]++;
+    for (int l = 0; l < nlev; ++l) p[l + 1] += p[l];
+    std::vector<int> pos(p.begin(), p.end() - 1);
+    for (int i = ns; i < ne; ++i) G.byl[ns + pos[level[i]]++] = i;
   }
-  // pack: block -> levels -> slices of 64 rows
-  S.block_level.assign(nb + 1, 0);
-  S.level_slice.assign(1, 0);
-  S.slice_ptr.assign(1, 0);
-  S.rowmap.clear();
-  S.max_levels = 0;
-  int64_t entries = 0;
-  int nslices = 0;
-  for (int b = 0; b < nb; ++b) {
-    const int nlev = (int)lvl_rows_ptr[b].size() - 1;
-    S.max_levels = std::max(S.max_levels, nlev);
-    S.block_level[b + 1] = S.block_level[b] + nlev;
-    for (int l = 0; l < nlev; ++l) {
-      const int r0 = lvl_rows_ptr[b][l], r1 = lvl_rows_ptr[b][l + 1];
-      for (int s0 = r0; s0 < r1; s0 += 64) {
-        int w = 0;
-        for (int t = s0; t < std::min(r1, s0 + 64); ++t) {
-          const int i = lvl_rows[b][t];
-          w = std::max(w, A.i[i + 1] - A.i[i]);
+}
+}  // namespace
+
+void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool forward, GsSchedule& S,
+                       int team_rows, bool with_tcol, const std::vector<double>* l1, const std::vector<int>* cf) {
+  const int n = A.nrows, nb = (int)block_start.size() - 1;
+  if (3 * (int64_t)n + std::max(0, A.ncols - n) >= INT_MAX)
+    throw std::runtime_error("Gauss-Seidel schedule: too many rows or columns");
+  S = GsSchedule();
+  S.block_start = block_start;
+  team_rows = std::max(1, team_rows);
+  GsLevels G;
+  gs_levels(A, block_start, forward, G);
+  // teams of consecutive blocks, about team_rows rows per team level
+  std::vector<int> team_blk(1, 0);
+  for (int b = 0; b < nb;) {
+    int64_t rows = 0;
+    int L = 0, e = b;
+    for (; e < nb; ++e) {
+      const int L2 = std::max(L, G.nlev[e]);
+      const int64_t r2 = rows + (block_start[e + 1] - block_start[e]);
+      if (e > b && r2 > (int64_t)team_rows * L2) break;
+      rows = r2;
+      L = L2;
+    }
+    team_blk.push_back(e);
+    b = e;
+  }
+  const int nt = (int)team_blk.size() - 1;
+  // the steps of team t in order: level by level, each level's rows in block
+  // order, cut into chunks of at most 64
+  auto for_each_step = [&](int t, const auto& fn) {
+    int L = 0;
+    for (int b = team_blk[t]; b < team_blk[t + 1]; ++b) L = std::max(L, G.nlev[b]);
+    std::vector<int> rows;
+    for (int l = 0; l < L; ++l) {
+      rows.clear();
+      for (int b = team_blk[t]; b < team_blk[t + 1]; ++b) {
+        if (l >= G.nlev[b]) continue;
+        const int ns = block_start[b];
+        for (int q = G.lptr[b][l]; q < G.lptr[b][l + 1]; ++q) rows.push_back(G.byl[ns + q]);
+      }
+      for (size_t r0 = 0; r0 < rows.size(); r0 += 64) fn(rows.data() + r0, (int)std::min<size_t>(64, rows.size() - r0));
+    }
+  };
+  auto width_of = [&](const int* rows, int cnt) {
+    int w = 0;
+    for (int r = 0; r < cnt; ++r) w = std::max(w, A.i[rows[r] + 1] - A.i[rows[r]]);
+    return w;
+  };
+  std::vector<int64_t> t_steps(nt + 1, 0), t_ent(nt + 1, 0);
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int t = 0; t < nt; ++t) {
+    int64_t ns = 0, ne = 0;
+    for_each_step(t, [&](const int* rows, int cnt) {
+      ++ns;
+      ne += (int64_t)width_of(rows, cnt) * cnt;
+    });
+    t_steps[t + 1] = ns;
+    t_ent[t + 1] = ne;
+  }
+  for (int t = 0; t < nt; ++t) {
+    S.max_steps = std::max(S.max_steps, (int)t_steps[t + 1]);
+    t_steps[t + 1] += t_steps[t];
+    t_ent[t + 1] += t_ent[t];
+  }
+  const int64_t nsteps = t_steps[nt], nent = t_ent[nt];
+  if (nsteps > INT_MAX / 4) throw std::runtime_error("Gauss-Seidel schedule: too many steps");
+  if (nent >= (int64_t)1 << 32) throw std::runtime_error("Gauss-Seidel schedule exceeds 2^32 entries");
+  S.team_step.assign(nt + 1, 0);
+  for (int t = 0; t <= nt; ++t) S.team_step[t] = (int)t_steps[t];
+  S.step.assign((size_t)nsteps * 4, 0);
+  S.code.assign((size_t)nent, -1);
+  S.val.assign((size_t)nent, 0.0);
+  if (with_tcol) S.tcol.assign((size_t)nent, -1);
+  S.rowmap.assign(n, 0);
+  // per row: its position, step and lane
+  std::vector<int> pos(n, 0), st_of(n, 0), ln_of(n, 0), blk_of(n, 0);
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int t = 0; t < nt; ++t) {
+    for (int b = team_blk[t]; b < team_blk[t + 1]; ++b)
+      for (int i = block_start[b]; i < block_start[b + 1]; ++i) blk_of[i] = b;
+    int64_t s = t_steps[t], e = t_ent[t];
+    int r = block_start[team_blk[t]];  // a team's positions are its blocks' rows
+    for_each_step(t, [&](const int* rows, int cnt) {
+      const int w = width_of(rows, cnt);
+      int* m = &S.step[(size_t)s * 4];
+      m[0] = (int)(uint32_t)e;
+      m[1] = r;
+      m[2] = cnt;
+      m[3] = w;
+      for (int q = 0; q < cnt; ++q) {
+        S.rowmap[r + q] = rows[q];
+        pos[rows[q]] = r + q;
+        st_of[rows[q]] = (int)s;
+        ln_of[rows[q]] = q;
+      }
+      ++s;
+      r += cnt;
+      e += (int64_t)w * cnt;
+    });
+  }
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int t = 0; t < nt; ++t) {
+    const int s0 = (int)t_steps[t];
+    for (int64_t sx = t_steps[t]; sx < t_steps[t + 1]; ++sx) {
+      const int* m = &S.step[(size_t)sx * 4];
+      const size_t base = (uint32_t)m[0];
+      const int cnt = m[2];
+      for (int q = 0; q < cnt; ++q) {
+        const int i = S.rowmap[m[1] + q];
+        const int ns = block_start[blk_of[i]], ne = block_start[blk_of[i] + 1];
+        for (int k = A.i[i]; k < A.i[i + 1]; ++k) {
+          const int c = A.j[k];
+          const size_t p = base + (size_t)(k - A.i[i]) * cnt + q;
+          S.val[p] = A.a[k];
+          if (c >= n) {  // off-rank: the halo
+            S.code[p] = 3 * n + (c - n);
+            continue;
+          }
+          if (c < ns || c >= ne) {  // T
+            S.code[p] = pos[c];
+            continue;
+          }
+          if (with_tcol) S.tcol[p] = pos[c];
+          const int d = (int)sx - st_of[c];
+          if (c == i || d < 1) S.code[p] = n + pos[c];  // C
+          else if (d <= kGsFence) S.code[p] = -2 - (((st_of[c] - s0) % kGsRing) * 64 + ln_of[c]);
+          else S.code[p] = 2 * n + pos[c];  // U
         }
-        entries += (int64_t)w * 64;
-        if (entries > 0x7fffffffLL) throw std::runtime_error("Gauss-Seidel schedule exceeds 2^31 entries");
-        S.slice_ptr.push_back((int)entries);
-        for (int t = 0; t < 64; ++t) S.rowmap.push_back(s0 + t < r1 ? lvl_rows[b][s0 + t] : -1);
-        ++nslices;
-      }
-      S.level_slice.push_back(nslices);
-    }
-  }
-  S.col.assign((size_t)entries, -1);
-  S.val.assign((size_t)entries, 0.0);
-#pragma omp parallel for schedule(static)
-  for (int sl = 0; sl < nslices; ++sl) {
-    for (int lane = 0; lane < 64; ++lane) {
-      const int i = S.rowmap[(size_t)sl * 64 + lane];
-      if (i < 0) continue;
-      for (int k = A.i[i]; k < A.i[i + 1]; ++k) {
-        const size_t p = (size_t)S.slice_ptr[sl] + (size_t)(k - A.i[i]) * 64 + lane;
-        S.col[p] = A.j[k];
-        S.val[p] = A.a[k];
       }
     }
   }
-  const int nlev_total = (int)S.level_slice.size() - 1;
-  S.avg_rows_per_level = nlev_total ? (double)A.nrows / nlev_total : 0.0;
+  if (l1 && !l1->empty()) {
+    S.l1.resize(n);
+    for (int k = 0; k < n; ++k) S.l1[k] = (*l1)[S.rowmap[k]];
+  }
+  if (cf && !cf->empty()) {
+    S.cf.resize(n);
+    for (int k = 0; k < n; ++k) S.cf[k] = (*cf)[S.rowmap[k]];
+  }
+  for (int64_t s = 0; s < nsteps; ++s) S.max_width = std::max(S.max_width, S.step[(size_t)s * 4 + 3]);
+  S.nteams = nt;
+  S.nnz = A.i[n];
+  S.rows_per_step = nsteps ? (double)n / nsteps : 0.0;
 }
 
 int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_l1, const std::vector<double>& l1,
-                           std::string& msg) {
+                           std::string& msg, int team_rows, bool weighted) {
   const int n = A.nrows;
   const std::vector<int> bs = hypre_block_starts(n, num_blocks);
   GsSchedule S;
-  build_gs_schedule(A, bs, forward, S);
-  std::vector<double> f(n), u0(n);
+  build_gs_schedule(A, bs, forward, S, team_rows, weighted, &l1);
+  const double w = 0.7, omega = 1.3;
+  std::vector<double> f(n), u0(n), tmp(n);
   uint64_t st = 0x9e3779b97f4a7c15ULL;
   auto rnd = [&] { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return (double)(st >> 11) / 9007199254740992.0 - 0.5; };
-  for (int i = 0; i < n; ++i) { f[i] = rnd(); u0[i] = rnd(); }
-  auto row_update = [&](int i, int ns, int ne, const std::vector<double>& u, const std::vector<double>& tmp,
-                        bool* skip) {
-    const double scale = use_l1 ? l1[i] : A.a[A.i[i]];
-    *skip = scale == 0.0;
-    if (*skip) return 0.0;
-    double res = f[i];
-    for (int k = A.i[i] + (use_l1 ? 0 : 1); k < A.i[i + 1]; ++k) {
-      const int c = A.j[k];
-      res -= A.a[k] * ((c >= ns && c < ne) ? u[c] : tmp[c]);
-    }
-    return use_l1 ? u[i] + res / scale : res / scale;
-  };
-  // reference: sequential sweep per block (par_relax.c thread loops)
-  std::vector<double> ref = u0, tmp = u0;
-  for (int b = 0; b + 1 < (int)bs.size(); ++b) {
+  for (int i = 0; i < n; ++i) { f[i] = rnd(); u0[i] = rnd(); tmp[i] = rnd(); }
+  if (num_blocks == 1) tmp = u0;  // one block reads no tmp; keep the T and C vectors equal there
+  // reference: sequential sweep per block (par_relax.c thread loops; weighted
+  // forms par_relax.c:4544 / :1277): in-block columns read the iterate being
+  // swept, off-block columns (and the weighted forms' Vtemp) the copy tmp
+  std::vector<double> ref = u0;
+  std::vector<int> blk(n);
+  for (int b = 0; b < num_blocks; ++b)
+    for (int i = bs[b]; i < bs[b + 1]; ++i) blk[i] = b;
+  for (int b = 0; b < num_blocks; ++b) {
     const int ns = bs[b], ne = bs[b + 1];
     for (int q = 0; q < ne - ns; ++q) {
       const int i = forward ? ns + q : ne - 1 - q;
-      bool skip;
-      const double v = row_update(i, ns, ne, ref, tmp, &skip);
-      if (!skip) ref[i] = v;
-    }
-  }
-  // schedule: levels in order, each level reads everything before writing
-  std::vector<double> u = u0;
-  if (S.rowmap.size() != (size_t)(S.slice_ptr.size() - 1) * 64) { msg = "rowmap size"; return 1; }
-  std::vector<int> seen(n, 0);
-  for (int b = 0; b + 1 < (int)bs.size(); ++b) {
-    const int ns = bs[b], ne = bs[b + 1];
-    for (int lv = S.block_level[b]; lv < S.block_level[b + 1]; ++lv) {
-      std::vector<std::pair<int, double>> upd;
-      for (int sl = S.level_slice[lv]; sl < S.level_slice[lv + 1]; ++sl) {
-        for (int lane = 0; lane < 64; ++lane) {
-          const int i = S.rowmap[(size_t)sl * 64 + lane];
-          if (i < 0) continue;
-          if (i < ns || i >= ne) { msg = "row outside its block"; return 1; }
-          seen[i]++;
-          // the stored row must be the CSR row, entry for entry
-          const int w = (S.slice_ptr[sl + 1] - S.slice_ptr[sl]) / 64;
-          for (int k = 0; k < w; ++k) {
-            const size_t p = (size_t)S.slice_ptr[sl] + (size_t)k * 64 + lane;
-            const int kk = A.i[i] + k;
-            if (kk < A.i[i + 1] ? (S.col[p] != A.j[kk] || S.val[p] != A.a[kk]) : S.col[p] != -1) {
-              msg = "stored row differs from the CSR row";
-              return 1;
-            }
-          }
-          bool skip;
-          const double v = row_update(i, ns, ne, u, tmp, &skip);
-          if (!skip) upd.push_back({i, v});
+      const double scale = use_l1 ? l1[i] : A.a[A.i[i]];
+      if (scale == 0.0) continue;
+      double res = f[i], res0 = 0.0, res2 = 0.0;
+      for (int k = A.i[i] + (use_l1 && !weighted ? 0 : 1); k < A.i[i + 1]; ++k) {
+        const int c = A.j[k];
+        const bool in = c >= ns && c < ne;
+        if (weighted && in) {
+          res0 -= A.a[k] * ref[c];
+          res2 += A.a[k] * tmp[c];
+        } else {
+          res -= A.a[k] * (in ? ref[c] : tmp[c]);
         }
       }
-      for (auto& pr : upd) u[pr.first] = pr.second;
+      if (weighted) {
+        double ui = ref[i];
+        ui *= 1.0 - w * omega;
+        ui += w * (omega * res + res0 + (1.0 - omega) * res2) / scale;
+        ref[i] = ui;
+      } else {
+        ref[i] = use_l1 ? ref[i] + res / scale : res / scale;
+      }
+    }
+  }
+  // the kernel's view: C / T / F permuted into the sweep order, U stores
+  // visible at the fences only, the LDS ring keeps the last kGsRing steps
+  std::vector<double> C(n), T(n), F(n), U(n, std::nan(""));
+  std::vector<int> inv(n, -1);
+  for (int k = 0; k < n; ++k) {
+    if (S.rowmap[k] < 0 || S.rowmap[k] >= n || inv[S.rowmap[k]] >= 0) { msg = "rowmap is not a permutation"; return 1; }
+    inv[S.rowmap[k]] = k;
+    C[k] = u0[S.rowmap[k]];
+    T[k] = tmp[S.rowmap[k]];
+    F[k] = f[S.rowmap[k]];
+  }
+  std::vector<double> u = u0;  // the natural iterate (scattered stores)
+  std::vector<int> seen(n, 0);
+  const int k0 = use_l1 && !weighted ? 0 : 1;
+  for (int t = 0; t < S.nteams; ++t) {
+    const int s0 = S.team_step[t];
+    std::vector<double> ring((size_t)kGsRingSlots, std::nan(""));
+    std::vector<std::pair<int, double>> pending;
+    for (int s = s0; s < S.team_step[t + 1]; ++s) {
+      const int* m = &S.step[(size_t)s * 4];
+      const size_t base = (uint32_t)m[0];
+      const int cnt = m[2], width = m[3], j = s - s0;
+      if (cnt < 1 || cnt > 64) { msg = "step rows out of range"; return 1; }
+      std::vector<double> out(cnt);
+      for (int q = 0; q < cnt; ++q) {
+        const int kpos = m[1] + q, i = S.rowmap[kpos];
+        if (i < 0 || i >= n) { msg = "row out of range"; return 1; }
+        seen[i]++;
+        const int ns = bs[blk[i]], ne = bs[blk[i] + 1];
+        // the stored row must decode to the CSR row, entry for entry
+        for (int k = 0; k < width; ++k) {
+          const size_t p = base + (size_t)k * cnt + q;
+          const int code = S.code[p];
+          const int kk = A.i[i] + k;
+          if (kk >= A.i[i + 1]) {
+            if (code != -1) { msg = "padding slot holds a code"; return 1; }
+            continue;
+          }
+          int c;
+          bool in;
+          if (code >= 3 * n) { msg = "halo code on a one-rank operator"; return 1; }
+          else if (code >= n) c = S.rowmap[code % n], in = true;
+          else if (code >= 0) c = S.rowmap[code], in = false;
+          else if (code == -1) { msg = "padding inside a row"; return 1; }
+          else {
+            const int slot = -2 - code, rs = slot / 64, rl = slot % 64;
+            int js = -1;
+            for (int d = 1; d <= kGsFence; ++d)
+              if (j - d >= 0 && (j - d) % kGsRing == rs) js = j - d;
+            if (js < 0) { msg = "ring slot out of reach"; return 1; }
+            const int* ms = &S.step[(size_t)(s0 + js) * 4];
+            if (rl >= ms[2]) { msg = "ring lane out of range"; return 1; }
+            c = S.rowmap[ms[1] + rl];
+            in = true;
+          }
+          if (c != A.j[kk] || S.val[p] != A.a[kk]) { msg = "stored row differs from the CSR row"; return 1; }
+          if (in != (c >= ns && c < ne)) { msg = "source kind disagrees with the block"; return 1; }
+          if (weighted && S.tcol[p] != (in ? inv[c] : -1)) { msg = "tcol"; return 1; }
+        }
+        const double uo = C[kpos];
+        const double scale = use_l1 ? S.l1[kpos] : S.val[base + q];
+        out[q] = uo;
+        if (scale == 0.0) continue;
+        auto src = [&](int code) {
+          if (code >= 2 * n) return U[code - 2 * n];
+          if (code >= n) return C[code - n];
+          if (code >= 0) return T[code];
+          return ring[-2 - code];
+        };
+        double res = F[kpos], res0 = 0.0, res2 = 0.0;
+        for (int k = k0; k < A.i[i + 1] - A.i[i]; ++k) {
+          const size_t p = base + (size_t)k * cnt + q;
+          const double a = S.val[p];
+          if (weighted && S.tcol[p] >= 0) {
+            res0 -= a * src(S.code[p]);
+            res2 += a * T[S.tcol[p]];
+          } else {
+            res -= a * src(S.code[p]);
+          }
+        }
+        if (weighted) {
+          double ui = uo;
+          ui *= 1.0 - w * omega;
+          ui += w * (omega * res + res0 + (1.0 - omega) * res2) / scale;
+          out[q] = ui;
+        } else {
+          out[q] = use_l1 ? uo + res / scale : res / scale;
+        }
+      }
+      for (int q = 0; q < cnt; ++q) {
+        pending.push_back({m[1] + q, out[q]});
+        u[S.rowmap[m[1] + q]] = out[q];
+        ring[(size_t)(j % kGsRing) * 64 + q] = out[q];
+      }
+      if (j % kGsFence == kGsFence - 1) {
+        for (auto& pr : pending) U[pr.first] = pr.second;
+        pending.clear();
+      }
     }
   }
   for (int i = 0; i < n; ++i)
@@ -819,7 +1006,8 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
       msg = "row " + std::to_string(i) + " differs from the sequential sweep";
       return 1;
     }
-  msg = "ok: " + std::to_string(S.level_slice.size() - 1) + " levels, max per block " + std::to_string(S.max_levels);
+  msg = "ok: " + std::to_string(S.nteams) + " teams, " + std::to_string(S.team_step.back()) + " steps, max per team " +
+        std::to_string(S.max_steps);
   return 0;
 }
 

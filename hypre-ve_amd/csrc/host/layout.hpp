@@ -78,32 +78,67 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
                           int max_ranges = 0, double max_cover = 1.5, const std::vector<int>* pre = nullptr);
 // Padded entry count of the SELL-64 layout for a given sigma (0 = no sort).
 int64_t sell_padded_nnz(const CSR& A, int sigma);
-// Level schedule of one hybrid Gauss-Seidel sweep (par_relax.c cases 3/4/6/
-// 8/13/14 with hypre's num_threads row blocks; the level scheduling of the
-// reference's relax-6 path, par_relax.c:2340-2650).  Inside each block rows
-// are grouped into levels: a row's level exceeds that of every in-block
-// neighbour it must see updated (lower rows for a forward sweep), and every
-// in-block neighbour it must see un-updated is pushed strictly above it, so the
-// rows of one level never reference each other and a level is one parallel
-// step.  Each level is stored SELL-64 (lane per row, entries in CSR order, so
-// every row sum is formed in the reference's order).
+// Packed, step-ordered schedule of one hybrid Gauss-Seidel sweep (par_relax.c
+// cases 3/4/6/8/13/14 with hypre's num_threads row blocks; the level
+// scheduling of the reference's relax-6 path, par_relax.c:2340-2650).
+//  * Levels.  Inside each block a row's level exceeds that of every in-block
+//    neighbour it must see updated (lower rows for a forward sweep), and every
+//    in-block neighbour it must see un-updated is pushed strictly above it, so
+//    the rows of one level never reference each other.
+//  * Teams.  Blocks interact only through the pre-sweep copy tmp, so
+//    consecutive blocks are swept together by one wavefront (a team): level l
+//    of the team is level l of each of its blocks.  A team takes blocks while
+//    its rows stay within team_rows x its level count.
+//  * Steps.  A team level is cut into steps of at most 64 rows.  Position k
+//    of the sweep order (rowmap[k] = row) is step s's row offset + lane, and
+//    the sweep works on vectors permuted into that order, so a step reads and
+//    writes its rows contiguously.  They sit in one buffer G of 3n + nhalo
+//    doubles: T = G[0, n) (the pre-sweep copy tmp; u itself unless a symmetric
+//    sweep's second half runs), C = G[n, 2n) (u at the sweep's start),
+//    U = G[2n, 3n) (the values this sweep wrote), then the off-rank halo of u
+//    (multi-rank, natural order); F (the right-hand side) beside it, l1 / cf
+//    permuted here.  Entry k of a step's row r sits at ent(s) + k * rows(s) + r.
+//  * Sources.  Each entry stores a code for the value its product reads:
+//      code >= 0   G[code]: T for an off-block column, C for an in-block one
+//                  not updated yet (the row itself included), U for an
+//                  in-block one updated at least kGsFence + 1 steps earlier
+//                  (the kernel fences its U stores every kGsFence steps), or
+//                  the halo for an off-rank column
+//      -1          padding
+//      <= -2       the team's LDS ring, slot -2 - code: a value an in-block
+//                  row computed at most kGsFence steps earlier
+//    Every row's products are summed in CSR order, so a sweep equals the
+//    sequential per-block sweep bit for bit.
+constexpr int kGsRing = 16;
+constexpr int kGsFence = 15;
+constexpr int kGsRingSlots = kGsRing * 64;
 struct GsSchedule {
   std::vector<int> block_start;  // nb + 1 row boundaries (hypre's ns / ne)
-  std::vector<int> block_level;  // nb + 1: level range of each block
-  std::vector<int> level_slice;  // nlevels + 1: slice range of each level
-  std::vector<int> slice_ptr;    // nslices + 1 entry offsets
-  std::vector<int> col;          // padded, -1 = padding
-  std::vector<double> val;
-  std::vector<int> rowmap;       // nslices * 64: row of each lane, -1 = none
-  int max_levels = 0;            // longest block schedule
-  double avg_rows_per_level = 0;
+  std::vector<int> team_step;    // nteams + 1: step range of each team
+  std::vector<int> step;         // 4 per step: entry offset (unsigned), position offset, rows, width
+  std::vector<int> code;         // per entry (see above)
+  std::vector<double> val;       // per entry, 0 for padding
+  std::vector<int> tcol;         // with_tcol: in-block entries' T offset in G (the weighted forms' Vtemp), else -1
+  std::vector<int> rowmap;       // nrows: row of each position
+  std::vector<double> l1;        // l1 norms by position (when given)
+  std::vector<int> cf;           // CF marker by position (when given)
+  int nteams = 0, max_steps = 0, max_width = 0;
+  int64_t nnz = 0;               // the operator's entries (the stored ones minus padding)
+  double rows_per_step = 0;
 };
-void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool forward, GsSchedule& S);
-// Host check of a schedule: the level-parallel sweep (every read of a level
-// before any of its writes) against the sequential per-block sweep of the
-// reference, on random f / u; returns 0 when bitwise equal.
+// A: the rows swept (columns >= A.nrows are off-rank, read from the halo).
+void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool forward, GsSchedule& S,
+                       int team_rows = 64, bool with_tcol = false, const std::vector<double>* l1 = nullptr,
+                       const std::vector<int>* cf = nullptr);
+// Host check of a schedule: the team-parallel sweep emulated with the
+// kernel's memory semantics (permuted C / T / U vectors; a step reads
+// everything before writing; U stores become visible only at the kernel's
+// fences; ring slots are reused after kGsRing steps) against the sequential
+// per-block sweep of the reference, on random f / u and a different tmp (a
+// symmetric sweep's second half); returns 0 when bitwise equal.  weighted: the
+// w / omega form (par_relax.c:4544) with w = 0.7, omega = 1.3.
 int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_l1, const std::vector<double>& l1,
-                           std::string& msg);
+                           std::string& msg, int team_rows = 64, bool weighted = false);
 // hypre's thread partition of n rows into nb blocks (par_relax.c size / rest).
 std::vector<int> hypre_block_starts(int n, int nb);
 

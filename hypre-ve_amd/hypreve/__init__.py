@@ -191,6 +191,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGSetGsRankStarts", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGSetRankEmulation", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
+    ("hypreve_BoomerAMGGsScheduleStats", _i, [_p, _i, _i, _i, _pi64]),
     ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
     ("hypreve_BoomerAMGCodedLayoutCheck", _i, [_p, _i, _i, _pi, _pi]),
     ("hypreve_SetKnob", _i, [_i, _i]),
@@ -555,6 +556,14 @@ class BoomerAMG:
     def gs_schedule_check(self, num_blocks):
         check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
 
+    def gs_schedule_stats(self, level, forward, num_blocks):
+        """Packed hybrid-GS schedule of level `level`: nnz, stored entries,
+        steps, teams, longest team (steps), blocks."""
+        out = (C.c_int64 * 6)()
+        check(lib().hypreve_BoomerAMGGsScheduleStats(self.h, level, int(forward), num_blocks, out),
+              "GsScheduleStats")
+        return dict(zip(("nnz", "entries", "steps", "teams", "max_steps", "blocks"), list(out)))
+
     def stencil_layout_check(self, level=0):
         """(slots per pattern, patterns) of level's A in the stencil layout,
         checked row by row against the CSR on the host; (0, 0) when the
@@ -658,10 +667,12 @@ class PCG:
         if max_iter is not None:
             check(lib().HYPRE_ParCSRPCGSetMaxIter(self.h, int(max_iter)), "PCGSetMaxIter")
 
-    def set_precond_amg(self, amg: BoomerAMG):
+    def set_precond_amg(self, amg: BoomerAMG, setup=True):
+        """BoomerAMG as the preconditioner; setup=False: PCGSetup leaves an
+        already set-up hierarchy as it is (no precond_setup function)."""
         L = lib()
         solve = C.cast(L.HYPRE_BoomerAMGSolve, C.c_void_p)
-        setup = C.cast(L.HYPRE_BoomerAMGSetup, C.c_void_p)
+        setup = C.cast(L.HYPRE_BoomerAMGSetup, C.c_void_p) if setup else None
         check(L.HYPRE_ParCSRPCGSetPrecond(self.h, solve, setup, amg.h), "PCGSetPrecond")
         self.precond = amg
 

@@ -346,6 +346,11 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, 
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
 HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_blocks);
+/* Size of the packed hybrid Gauss-Seidel schedule of level `level`'s A with
+ * num_blocks blocks (host only, after Setup / SetupHost): out[6] = {nnz, stored
+ * entries, steps, teams, longest team in steps, blocks}. */
+HYPRE_Int hypreve_BoomerAMGGsScheduleStats(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int forward,
+                                           HYPRE_Int num_blocks, int64_t *out);
 /* Host check of the slot-uniform stencil layout of level's A (after
  * hypreve_BoomerAMGSetupHost or Setup): every row rebuilt from its slice's
  * slot pattern equals the CSR row entry for entry.  *width = 0 (and

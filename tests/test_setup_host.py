@@ -267,3 +267,23 @@ def test_coded_layout_rebuilds_rows(hv, gen, dims):
             assert 1 <= no <= 25 and 1 <= nv <= 2048, (which, no, nv)
         else:
             assert (no, nv) == (0, 0) or (no >= 1 and nv >= 1)
+
+
+@pytest.mark.parametrize("forward", [True, False])
+def test_gs_packed_schedule_size(hv, forward):
+    """BoomerAMG's default smoother at the north-star grid width: 4096-row
+    blocks of a 512-wide 7-point grid are 8 x-lines with 519 dependency levels
+    of at most 8 rows; the packed schedule sweeps 8 such blocks per wavefront,
+    so it stores at most 1.3x the operator's entries (the one-level-per-slice
+    layout it replaced padded every level to 64 lanes: about 8x) and needs about
+    one step per level of a block."""
+    A = hv.ParCSRMatrix.laplacian(512, 16, 8)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(max_levels=1, relax_type=13)
+    amg.setup_host(A)
+    nb = 512 * 16 * 8 // 4096
+    st = amg.gs_schedule_stats(0, forward, nb)
+    assert st["entries"] <= 1.3 * st["nnz"], st
+    assert st["teams"] == nb // 8, st
+    assert st["max_steps"] <= 520, st
+    amg.gs_schedule_check(nb)
