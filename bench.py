@@ -438,8 +438,19 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
         # cpu_baseline is this line's too; N-rank iterates equal the 1-rank
         # iterates bit for bit (tests/test_gpu_multirank.py, loopback + RCCL).
         parity = "bitwise vs 1 rank (tests/test_gpu_multirank.py)"
+    comm_stats = None
+    if world > 1:
+        # this rank's communication per V-cycle, per level (the solve loop adds
+        # one level-0 exchange for its residual and one all-reduce for its norm)
+        cc = amg.cycle_comm_stats()
+        comm_stats = {"exchanges": sum(c["exchanges"] for c in cc), "bytes": sum(c["bytes"] for c in cc),
+                      "allgathers": sum(c["allgathers"] for c in cc),
+                      "allgather_bytes": sum(c["allgather_bytes"] for c in cc),
+                      "allreduces": sum(c["allreduces"] for c in cc),
+                      "per_level": [[c["exchanges"], c["bytes"]] for c in cc]}
     stats = gather({"rank": rank, "rows": nrows, "setup_s": round(t_setup, 1), "setup_peak_rss_gb": round(rss_setup, 1),
-                    "peak_rss_gb": round(peak_rss_gb(), 1), "omp_threads": int(os.environ.get("OMP_NUM_THREADS", "0"))})
+                    "peak_rss_gb": round(peak_rss_gb(), 1), "omp_threads": int(os.environ.get("OMP_NUM_THREADS", "0")),
+                    "cycle_comm": comm_stats})
     nlev = amg.num_levels()
     for obj in ((krylov,) if pcg else ()) + (amg, A, b, x):
         obj.destroy()  # release host and device memory before a secondary size runs
@@ -545,6 +556,23 @@ def main():
     ap.add_argument("--loopback", type=int, default=0,
                     help="rehearsal only: N virtual ranks (threads) sharing this process's GPU")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.loopback <= 1:
+        # one process per GPU: start the ranks under torch.distributed.run as a
+        # child process (nothing here has touched the GPU) and exit with its code
+        import subprocess
+        import torch
+        ndev = torch.cuda.device_count()  # counts devices without initialising one
+        if ndev < args.gpus:
+            log(f"[bench] --gpus {args.gpus} needs {args.gpus} GPUs on this node, found {ndev}")
+            sys.exit(2)
+        import socket
+        with socket.socket() as so:
+            so.bind(("127.0.0.1", 0))
+            port = so.getsockname()[1]
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        log(f"[bench] launching {args.gpus} ranks: {' '.join(cmd)}")
+        sys.exit(subprocess.call(cmd))
     omp = rank_threads()
 
     import torch  # loads the HIP runtime the library then shares
@@ -552,6 +580,9 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.loopback <= 1 and world != args.gpus:
+        log(f"[bench] --gpus {args.gpus} but the launcher started {world} rank(s)")
+        sys.exit(2)
 
     import hypreve as hv
 

@@ -1408,6 +1408,25 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver s, HYPRE_Int num_blocks)
   API_END
 }
 
+// This rank's communication in one V-cycle (the last cycle the solver emitted):
+// out = {halo exchanges, bytes they send, all-gathers, all-gather bytes sent,
+// all-reduces} on level `level`; zeros on one rank.
+HYPRE_Int hypreve_BoomerAMGGetCycleCommStats(HYPRE_Solver s, HYPRE_Int level, int64_t* out) {
+  CHECK_ARG(s && s->kind == KIND_AMG && s->dev, 1);
+  CHECK_ARG(out, 3);
+  API_BEGIN
+  const auto& cc = s->dev->cycle_comm();
+  for (int k = 0; k < 5; ++k) out[k] = 0;
+  if (level >= 0 && level < (HYPRE_Int)cc.size()) {
+    out[0] = cc[level].exchanges;
+    out[1] = cc[level].bytes;
+    out[2] = cc[level].allgathers;
+    out[3] = cc[level].allgather_bytes;
+    out[4] = cc[level].allreduces;
+  }
+  API_END
+}
+
 // Size of the packed hybrid Gauss-Seidel schedule of a level's A for a block
 // count (host only): out = {nnz, stored entries, steps, teams, longest team
 // (steps), blocks}.

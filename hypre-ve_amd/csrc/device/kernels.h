@@ -93,6 +93,7 @@ struct GsView {
   const double* val = nullptr;
   const int* tcol = nullptr;       // weighted forms: in-block entries' T position (-1 otherwise)
   const int* rowmap = nullptr;     // position -> row
+  const int* pos = nullptr;        // row -> position
   const double* l1 = nullptr;      // l1 norms by position
   const int* cf = nullptr;         // CF marker by position
   int nteams = 0, nrows = 0, max_width = 0;
@@ -103,9 +104,10 @@ struct GsView {
 hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp, const double* f, int nhalo,
                             double* G, double* F, hipStream_t st);
 // One hybrid Gauss-Seidel sweep over S: reads G's T, C and halo parts and F,
-// writes G's U part and u (natural rows).
-hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, const double* F,
-                            double* u, double w, double omega, hipStream_t st);
+// writes G's U part, then scatters it into u (natural rows).  G (3n + nhalo
+// doubles) must stay below 4 GiB.
+hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, int nhalo,
+                            const double* F, double* u, double w, double omega, hipStream_t st);
 int sell_batch_override();
 // Tuning knobs read at launch (0 = default): 0 offset-coded row blocks per
 // step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU,

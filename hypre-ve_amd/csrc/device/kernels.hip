@@ -1254,9 +1254,9 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
 // them): values computed in the last kGsFence steps from the wave's LDS ring,
 // older ones from U, whose stores the wave fences every kGsFence steps; not
 // yet updated ones from C; off-block columns read T, the copy taken before the
-// sweep (par_relax.c tmp_data / Vext_data).  Only U (the team's own positions)
-// and u (natural rows, read by nobody during the sweep) are written, so teams
-// never wait on each other.
+// sweep (par_relax.c tmp_data / Vext_data).  Only U (the team's own
+// positions) is written, so teams never wait on each other; a scatter after
+// the sweep puts U back into u's natural order.
 //   L1 = true : cases 8/13/14, res = f - sum_all a*u, u += res / l1
 //   L1 = false: cases 3/4/6,   res = f - sum_offdiag a*u, u = res / a_ii
 //   WGT (relax_weight w or omega != 1, par_relax.c:1277/4544): the diagonal
@@ -1279,9 +1279,32 @@ struct GsArgs {
   const double* __restrict__ F;
   double* u;
   int n, nteams, relax_points;
+  unsigned gbytes;  // G's size in bytes (< 4 GiB: 32-bit buffer offsets)
   double w, omega;
 };
-static constexpr int kGsWaves = 2;  // teams per workgroup
+static constexpr int kGsWaves = 4;           // teams per workgroup
+static constexpr int kGsProd = 512;          // LDS products per wave and chunk
+static constexpr int kGsPer = kGsProd / 64;  // entries per lane and chunk
+// U stores leave the ring in batches of kGsBatch steps: on CDNA a load waits
+// for every older vector-memory operation, stores included, so a store per
+// step would put a store's completion on every step's critical path.  A batch
+// is fenced before the next one is issued (kGsBatch steps later), so a value
+// reaches U at most 2 kGsBatch - 1 <= kGsFence steps after it was computed.
+static constexpr int kGsBatch = 8;
+static_assert(2 * kGsBatch - 1 <= kGsFence && kGsFence < kGsRing, "ring reach");
+
+// Buffer loads with 32-bit offsets from wave-uniform bases: no 64-bit address
+// arithmetic in VGPRs (whose register reuse otherwise made the compiler wait
+// for every load in flight before a step's first entry load).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gs_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double gs_ld64(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ int gs_ld32(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
+}
 
 __device__ __forceinline__ void gs_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1289,189 +1312,108 @@ __device__ __forceinline__ void gs_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Per wave LDS: the ring, and the staging of one step (its first chunk of
-// PROD entries: codes, values (overwritten by the products), the weighted
-// forms' Vtemp positions / second products / classes; its rows' map, C, F,
-// l1 and cf).  The staging of step j + 1 is loaded while step j's gathers are
-// in flight (one global latency per step) and written after step j's sums.
-template <int PROD, bool WGT>
-struct GsLds {
-  double ring[kGsRingSlots];
-  double val[PROD];
-  int code[PROD];
-  int tcol[WGT ? PROD : 1];
-  double prod2[WGT ? PROD : 1];
-  unsigned char cls[WGT ? PROD : 1];
-  int row[64], cf[64];
-  double c[64], f[64], l1[64];
-};
-
-// Registers of a prefetched step: entries lane + 64 t of its first chunk.
-template <int PER, bool WGT>
-struct GsPre {
-  int c[PER], tc[WGT ? PER : 1];
-  double a[PER];
-  int row, cf;
-  double cv, fv, l1v;
-};
-
-template <bool L1, bool CFSEL, bool WGT, int PROD>
-__device__ __forceinline__ void gs_prefetch(const GsArgs& p, const int4 m, int lane, GsPre<PROD / 64, WGT>& P) {
-  constexpr int PER = PROD / 64;
-  const int R = m.z, W = m.w;
-  const int KC = PROD / R;
-  const int E = min(KC, W) * R;
-  const unsigned ent = (unsigned)m.x;
-#pragma unroll
-  for (int t = 0; t < PER; ++t) {
-    if (64 * t >= E) break;
-    const int e = lane + 64 * t;
-    const unsigned o = ent + (unsigned)(e < E ? e : 0);
-    P.c[t] = p.code[o];
-    P.a[t] = p.val[o];
-    if (WGT) P.tc[t] = p.tcol[o];
-  }
-  const int kp = m.y + (lane < R ? lane : R - 1);
-  P.row = p.rowmap[kp];
-  P.cv = p.G[p.n + kp];
-  P.fv = p.F[kp];
-  if (L1) P.l1v = p.l1[kp];
-  if (CFSEL) P.cf = p.cf[kp];
-}
-
-template <bool L1, bool CFSEL, bool WGT, int PROD>
-__device__ __forceinline__ void gs_stage(const int4 m, int lane, const GsPre<PROD / 64, WGT>& P,
-                                         GsLds<PROD, WGT>& S) {
-  constexpr int PER = PROD / 64;
-  const int R = m.z, W = m.w;
-  const int E = min(PROD / R, W) * R;
-#pragma unroll
-  for (int t = 0; t < PER; ++t) {
-    if (64 * t >= E) break;
-    const int e = lane + 64 * t;
-    if (e < E) {
-      S.code[e] = P.c[t];
-      S.val[e] = P.a[t];
-      if (WGT) S.tcol[e] = P.tc[t];
-    }
-  }
-  S.row[lane] = P.row;
-  S.c[lane] = P.cv;
-  S.f[lane] = P.fv;
-  if (L1) S.l1[lane] = P.l1v;
-  if (CFSEL) S.cf[lane] = P.cf;
-}
-
-template <bool L1, bool CFSEL, bool WGT, int PROD>
+template <bool L1, bool CFSEL, bool WGT>
 __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
-  constexpr int PER = PROD / 64;
-  __shared__ GsLds<PROD, WGT> lds_all[kGsWaves];
+  __shared__ double ring_all[kGsWaves][kGsRingSlots];
+  __shared__ double prod_all[kGsWaves][kGsProd];
+  __shared__ double prod2_all[kGsWaves][WGT ? kGsProd : 1];
+  __shared__ unsigned char cls_all[kGsWaves][WGT ? kGsProd : 1];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & (kWave - 1);
   const int team = blockIdx.x * kGsWaves + wave;
   if (team >= p.nteams) return;
-  GsLds<PROD, WGT>& S = lds_all[wave];
+  double* ring = ring_all[wave];
+  double* prod = prod_all[wave];
+  double* prod2 = prod2_all[wave];
+  unsigned char* cls = cls_all[wave];
   const int s0 = __builtin_amdgcn_readfirstlane(p.team_step[team]);
   const int ns = __builtin_amdgcn_readfirstlane(p.team_step[team + 1]) - s0;
   // step metadata through the scalar cache (read-only, constant address space)
   using cint = const __attribute__((address_space(4))) int;
   cint* const steps = (cint*)(p.step + 4 * (size_t)s0);
-  auto meta = [&](int j) -> int4 {
-    cint* q = steps + 4 * (j < ns ? j : ns - 1);
-    int4 m;
-    m.x = q[0]; m.y = q[1]; m.z = q[2]; m.w = q[3];
-    return m;
-  };
   constexpr int k0 = (L1 && !WGT) ? 0 : 1;  // the diagonal (stored first) is skipped unless l1 scales
-  {
-    GsPre<PER, WGT> P;
-    const int4 m = meta(0);
-    gs_prefetch<L1, CFSEL, WGT, PROD>(p, m, lane, P);
-    gs_stage<L1, CFSEL, WGT, PROD>(m, lane, P, S);
-    gs_wave_sync();
-  }
+  double* const Ub = p.G + 2 * (size_t)p.n;
+  const auto rG = gs_rsrc(p.G, p.gbytes);                   // T | C | U | halo
+  const auto rC = gs_rsrc(p.G + p.n, (unsigned)p.n * 8u);   // C by position
+  const auto rF = gs_rsrc(p.F, (unsigned)p.n * 8u);
+  const auto rL = gs_rsrc(L1 ? p.l1 : p.F, (unsigned)p.n * 8u);
+  const auto rCF = gs_rsrc(CFSEL ? (const void*)p.cf : (const void*)p.F, (unsigned)p.n * 4u);
   for (int j = 0; j < ns; ++j) {
-    const int4 m = meta(j);
-    const unsigned ent = (unsigned)m.x;
-    const int R = m.z, W = m.w;
+    const unsigned ent = (unsigned)steps[4 * j];
+    const int roff = steps[4 * j + 1], R = steps[4 * j + 2], W = steps[4 * j + 3];
     const int r = lane < R ? lane : R - 1;
-    const int KC = PROD / R;
-    double res = 0.0, res0 = 0.0, res2 = 0.0;
-    GsPre<PER, WGT> P;
-    for (int kc = 0; kc < W; kc += KC) {
+    const int kp = roff + r;
+    // this step's entries: bases in SGPRs, 32-bit offsets
+    const auto rc = gs_rsrc(p.code + ent, 0x7fffffffu);
+    const auto rv8 = gs_rsrc(p.val + ent, 0x7fffffffu);
+    const auto rt = gs_rsrc(WGT ? (const void*)(p.tcol + ent) : (const void*)(p.code + ent), 0x7fffffffu);
+    const double uo = gs_ld64(rC, (int)((unsigned)kp * 8u));
+    const double fv = gs_ld64(rF, (int)((unsigned)kp * 8u));
+    const double sc = L1 ? gs_ld64(rL, (int)((unsigned)kp * 8u)) : gs_ld64(rv8, r * 8);
+    const int cfv = CFSEL ? gs_ld32(rCF, kp * 4) : 0;
+    double res = fv, res0 = 0.0, res2 = 0.0;
+    const int KC = kGsProd / R;
+    // one chunk of entries [kc, kc + KC) of every row of the step; the first
+    // chunk runs straight after the row loads (the loop is for wide rows only,
+    // so no loop merge makes the compiler wait for the row loads first)
+    auto chunk = [&](int kc) {
       const int kw = min(KC, W - kc), E = kw * R;
-      int c[PER], tc[PER];
-      double a[PER], x[PER], rv[PER], t2[PER];
-      if (kc == 0) {  // the staged first chunk
+      const int base = kc * R;
+      int c[kGsPer], tc[kGsPer];
+      double a[kGsPer], x[kGsPer], rv[kGsPer], t2[kGsPer];
 #pragma unroll
-        for (int t = 0; t < PER; ++t) {
-          if (64 * t >= E) break;
-          const int e = lane + 64 * t < E ? lane + 64 * t : 0;
-          c[t] = S.code[e];
-          a[t] = S.val[e];
-          tc[t] = WGT ? S.tcol[e] : -1;
-        }
-      } else {  // later chunks of wide rows: from HBM in place
-        const unsigned base = ent + (unsigned)(kc * R);
-#pragma unroll
-        for (int t = 0; t < PER; ++t) {
-          if (64 * t >= E) break;
-          const int e = lane + 64 * t;
-          const unsigned o = base + (unsigned)(e < E ? e : 0);
-          c[t] = p.code[o];
-          a[t] = p.val[o];
-          tc[t] = WGT ? p.tcol[o] : -1;
-        }
-      }
-      // the next step's staging data, issued with this chunk's gathers (one
-      // wait covers both)
-      if (kc == 0) gs_prefetch<L1, CFSEL, WGT, PROD>(p, meta(j + 1), lane, P);
-#pragma unroll
-      for (int t = 0; t < PER; ++t) {
+      for (int t = 0; t < kGsPer; ++t) {
         if (64 * t >= E) break;
-        x[t] = p.G[c[t] > 0 ? c[t] : 0];
-        if (WGT) t2[t] = p.G[tc[t] > 0 ? tc[t] : 0];
+        const int e = lane + 64 * t;
+        const int o = base + (e < E ? e : 0);
+        c[t] = gs_ld32(rc, o * 4);
+        a[t] = gs_ld64(rv8, o * 8);
+        tc[t] = WGT ? gs_ld32(rt, o * 4) : -1;
       }
 #pragma unroll
-      for (int t = 0; t < PER; ++t) {
+      for (int t = 0; t < kGsPer; ++t) {
         if (64 * t >= E) break;
-        rv[t] = S.ring[c[t] < -1 ? -2 - c[t] : 0];
+        // unsigned byte offsets: G may exceed 2 GiB (< 4 GiB)
+        x[t] = gs_ld64(rG, (int)((unsigned)(c[t] > 0 ? c[t] : 0) * 8u));
+        if (WGT) t2[t] = gs_ld64(rG, (int)((unsigned)(tc[t] > 0 ? tc[t] : 0) * 8u));
       }
 #pragma unroll
-      for (int t = 0; t < PER; ++t) {
+      for (int t = 0; t < kGsPer; ++t) {
+        if (64 * t >= E) break;
+        rv[t] = ring[c[t] < -1 ? -2 - c[t] : 0];
+      }
+#pragma unroll
+      for (int t = 0; t < kGsPer; ++t) {
         if (64 * t >= E) break;
         const int e = lane + 64 * t;
         const int cc = c[t];
         const double xv = cc < -1 ? rv[t] : x[t];
         const double pv = cc == -1 ? 0.0 : a[t] * xv;
         if (e < E) {
-          S.val[e] = pv;  // the product replaces the staged value
+          prod[e] = pv;
           if (WGT) {
-            S.prod2[e] = tc[t] >= 0 ? a[t] * t2[t] : 0.0;
-            S.cls[e] = tc[t] >= 0;
+            prod2[e] = tc[t] >= 0 ? a[t] * t2[t] : 0.0;
+            cls[e] = tc[t] >= 0;
           }
         }
       }
       gs_wave_sync();
-      if (kc == 0) res = S.f[r];
       for (int kk = 0; kk < kw; ++kk) {
         if (kc + kk < k0) continue;
         const int e = kk * R + r;
-        const double pv = S.val[e];
-        if (WGT && S.cls[e]) {
+        const double pv = prod[e];
+        if (WGT && cls[e]) {
           res0 -= pv;
-          res2 += S.prod2[e];
+          res2 += prod2[e];
         } else {
           res -= pv;
         }
       }
       gs_wave_sync();  // the next chunk overwrites the products
-    }
-    const int kp = m.y + r;
-    const int i = S.row[r];
-    const double uo = S.c[r];
-    const double sc = L1 ? S.l1[r] : p.val[ent + r];
-    const bool run = lane < R && sc != 0.0 && !(CFSEL && S.cf[r] != p.relax_points);
+    };
+    chunk(0);
+    for (int kc = KC; kc < W; kc += KC) chunk(kc);
+    const bool run = lane < R && sc != 0.0 && !(CFSEL && cfv != p.relax_points);
     double un = uo;
     if (WGT) {
       double ui = un;
@@ -1482,24 +1424,40 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
       const double v = L1 ? un + res / sc : res / sc;
       un = run ? v : un;
     }
-    if (lane < R) p.G[2 * p.n + kp] = un;
-    if (run) p.u[i] = un;
-    S.ring[(j % kGsRing) * kWave + lane] = un;
-    gs_stage<L1, CFSEL, WGT, PROD>(meta(j + 1), lane, P, S);
-    gs_wave_sync();  // the ring slot and the next step's staging
-    // the U stores of the last kGsFence steps complete: later steps read them
-    if (j % kGsFence == kGsFence - 1) {
+    ring[(j % kGsRing) * kWave + lane] = un;
+    gs_wave_sync();  // the next steps' lanes read the ring slot
+    if (j % kGsBatch == kGsBatch - 1 || j == ns - 1) {
+      // the previous batch is complete (issued kGsBatch steps ago) and
+      // visible to this wave's later U loads; then this batch leaves the ring
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      for (int q = j - j % kGsBatch; q <= j; ++q) {
+        const int rq = steps[4 * q + 2];
+        if (lane < rq) Ub[steps[4 * q + 1] + lane] = ring[(q % kGsRing) * kWave + lane];
+      }
     }
   }
 }
 
-__global__ void k_gs_gather(int n, int nhalo, const int* __restrict__ rowmap, const double* __restrict__ u,
+// u[rowmap[k]] = U[k]: the sweep's result back in natural row order (NAT:
+// u[i] = U[pos[i]], rows in order).
+template <bool NAT>
+__global__ void k_gs_scatter(int n, const int* __restrict__ map, const double* __restrict__ U,
+                             double* __restrict__ u) {
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    if (NAT) u[q] = U[map[q]];
+    else u[map[q]] = U[q];
+  }
+}
+
+// NAT = false: positions in order, rows gathered (rowmap); NAT = true: rows in
+// natural order (coalesced reads), positions scattered (pos = rowmap^-1).
+template <bool NAT>
+__global__ void k_gs_gather(int n, int nhalo, const int* __restrict__ map, const double* __restrict__ u,
                             const double* __restrict__ tmp, const double* __restrict__ f, double* __restrict__ G,
                             double* __restrict__ F) {
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < n; k += gridDim.x * blockDim.x) {
-    const int i = rowmap[k];
+  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+    const int i = NAT ? q : map[q], k = NAT ? map[q] : q;
     const double v = u[i];
     G[k] = tmp ? tmp[i] : v;
     G[n + k] = v;
@@ -1508,29 +1466,41 @@ __global__ void k_gs_gather(int n, int nhalo, const int* __restrict__ rowmap, co
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nhalo; k += gridDim.x * blockDim.x) G[3 * n + k] = u[n + k];
 }
 
+static int gs_natural_order() {
+  static const int v = [] {
+    const char* e = getenv("HVE_GS_NAT");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp, const double* f, int nhalo,
                             double* G, double* F, hipStream_t st) {
   if (S.nrows <= 0) return hipSuccess;
   const int grid = std::min((S.nrows + 255) / 256, 256 * 16);
-  hipLaunchKernelGGL(k_gs_gather, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.rowmap, u, tmp, f, G, F);
+  if (gs_natural_order() & 1)
+    hipLaunchKernelGGL(k_gs_gather<true>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.pos, u, tmp, f, G, F);
+  else
+    hipLaunchKernelGGL(k_gs_gather<false>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.rowmap, u, tmp, f, G, F);
   return hipGetLastError();
 }
 
-hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, const double* F,
-                            double* u, double w, double omega, hipStream_t st) {
+hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, int nhalo,
+                            const double* F, double* u, double w, double omega, hipStream_t st) {
   if (S.nteams <= 0) return hipSuccess;
   GsArgs a;
   a.team_step = S.team_step; a.step = S.step; a.code = S.code; a.val = S.val; a.tcol = S.tcol; a.rowmap = S.rowmap;
   a.l1 = S.l1; a.cf = S.cf; a.G = G; a.F = F; a.u = u;
   a.n = S.nrows; a.nteams = S.nteams; a.relax_points = relax_points; a.w = w; a.omega = omega;
+  const uint64_t gbytes = (3 * (uint64_t)S.nrows + (uint64_t)nhalo) * sizeof(double);
+  if (gbytes > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit buffer offsets (about 178M rows a GPU)
+  a.gbytes = (unsigned)gbytes;
   const bool wgt = w != 1.0 || omega != 1.0;
   if (wgt && !S.tcol) return hipErrorInvalidValue;   // the weighted forms read Vtemp in-block
   if (use_l1 && !S.l1) return hipErrorInvalidValue;
   if (cfsel && !S.cf) return hipErrorInvalidValue;
   const dim3 grid((S.nteams + kGsWaves - 1) / kGsWaves), blk(kGsWaves * kWave);
-#define HVE_G(L1V, CFV, WV)                                                                   \
-  if (S.max_width > 8) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, 1024>), grid, blk, 0, st, a); \
-  else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, 512>), grid, blk, 0, st, a);
+#define HVE_G(L1V, CFV, WV) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV>), grid, blk, 0, st, a);
 #define HVE_GW(L1V, CFV) \
   if (wgt) { HVE_G(L1V, CFV, true) } else { HVE_G(L1V, CFV, false) }
   if (use_l1) {
@@ -1540,6 +1510,12 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   }
 #undef HVE_GW
 #undef HVE_G
+  const int sgrid = std::min((S.nrows + 255) / 256, 256 * 16);
+  if (gs_natural_order() & 2)
+    hipLaunchKernelGGL(k_gs_scatter<true>, dim3(sgrid), dim3(256), 0, st, S.nrows, S.pos, G + 2 * (size_t)S.nrows, u);
+  else
+    hipLaunchKernelGGL(k_gs_scatter<false>, dim3(sgrid), dim3(256), 0, st, S.nrows, S.rowmap, G + 2 * (size_t)S.nrows,
+                       u);
   return hipGetLastError();
 }
 

@@ -655,21 +655,33 @@ void DevSell::release() {
   notab = vbits = 0; anc_n = cmap_n = 0;
 }
 
-// Team size of the packed schedule: about this many rows per step
-// (HVE_GS_TEAM_ROWS overrides, tuning).
-static int gs_team_rows() {
-  static const int v = [] {
+// Team size of the packed schedule: about this many rows per step.  A wide
+// operator (Galerkin levels, rows of 20-100 entries) spends a step on its
+// products, so its teams are small: more of them run at once and a step fits
+// one LDS chunk.  Measured at 256^3 (relax 13/14): level 0 (7 entries a row)
+// 0.70 ms a sweep with 64 rows against 1.01 with 16; level 1 (29 a row) 1.12
+// ms with 16 against 2.34 with 64.  HVE_GS_TEAM_ROWS / HVE_GS_TEAM_ROWS_WIDE
+// override (tuning).
+static int gs_team_rows(const CSR& A) {
+  static const int narrow = [] {
     const char* e = getenv("HVE_GS_TEAM_ROWS");
     const int r = e ? atoi(e) : 0;
     return r > 0 ? r : 64;
   }();
-  return v;
+  static const int wide = [] {
+    const char* e = getenv("HVE_GS_TEAM_ROWS_WIDE");
+    const int r = e ? atoi(e) : 0;
+    return r > 0 ? r : 16;
+  }();
+  int w = 0;
+  for (int i = 0; i < A.nrows; ++i) w = std::max(w, A.i[i + 1] - A.i[i]);
+  return w > 8 ? wide : narrow;
 }
 void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forward, bool weighted,
                    const std::vector<double>& l1_rows, const std::vector<int>& cf_rows) {
   release();
   GsSchedule S;
-  build_gs_schedule(A, block_starts, forward, S, gs_team_rows(), weighted, &l1_rows, &cf_rows);
+  build_gs_schedule(A, block_starts, forward, S, gs_team_rows(A), weighted, &l1_rows, &cf_rows);
   nrows = A.nrows;
   nblocks = (int)S.block_start.size() - 1;
   nteams = S.nteams;
@@ -683,14 +695,19 @@ void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forw
   val = dupload(S.val.data(), std::max<size_t>(1, S.val.size()));
   if (weighted) tcol = dupload(S.tcol.data(), std::max<size_t>(1, S.tcol.size()));
   rowmap = dupload(S.rowmap.data(), std::max<size_t>(1, S.rowmap.size()));
+  {
+    std::vector<int> inv(S.rowmap.size());
+    for (size_t k = 0; k < S.rowmap.size(); ++k) inv[S.rowmap[k]] = (int)k;
+    pos = dupload(inv.data(), std::max<size_t>(1, inv.size()));
+  }
   if (!S.l1.empty()) l1 = dupload(S.l1.data(), S.l1.size());
   if (!S.cf.empty()) cf = dupload(S.cf.data(), S.cf.size());
 }
 void DevGs::release() {
-  for (void* p : {(void*)team_step, (void*)step, (void*)code, (void*)val, (void*)tcol, (void*)rowmap, (void*)l1,
-                  (void*)cf})
+  for (void* p : {(void*)team_step, (void*)step, (void*)code, (void*)val, (void*)tcol, (void*)rowmap, (void*)pos,
+                  (void*)l1, (void*)cf})
     if (p) (void)hipFree(p);
-  team_step = step = code = tcol = rowmap = cf = nullptr;
+  team_step = step = code = tcol = rowmap = pos = cf = nullptr;
   val = l1 = nullptr;
   nrows = nteams = nblocks = max_steps = max_width = 0;
   entries = nnz = 0;
@@ -1221,6 +1238,13 @@ double DevAMG::dot_host(int n, const double* x, const double* y, hipStream_t s) 
 // ParCSR halo exchange (par_csr_communication.c hypre_ParCSRCommHandleCreate,
 // job 1) as gather -> grouped RCCL send/recv on the side stream.
 void DevAMG::halo_start(const DevHalo& h, double* x, hipStream_t s) {
+  if (comm_level_ >= 0) {
+    for (size_t l = 0; l < lev_.size(); ++l)
+      if (&lev_[l].hu == &h || &lev_[l].hv == &h) {
+        cycle_comm_[l].exchanges++;
+        cycle_comm_[l].bytes += (int64_t)h.n_send * (int64_t)sizeof(double);
+      }
+  }
   HVE_HIP(launch_gather(h.n_send, h.d_send_idx, x, h.d_sendbuf, s));
   HVE_HIP(hipEventRecord(ev_packed_, s));
   HVE_HIP(hipStreamWaitEvent(comm_stream_, ev_packed_, 0));
@@ -1307,6 +1331,10 @@ void DevAMG::pcg_update(int n, const double* alpha_p, const double* p, const dou
 // share and receives the others' (one grouped exchange).
 void DevAMG::allgather_rows(double* v, const std::vector<int>& starts, hipStream_t s) {
   const int me = comm_->rank(), n = comm_->size();
+  if (comm_level_ >= 0 && agg_level_ >= 0) {
+    cycle_comm_[agg_level_].allgathers++;
+    cycle_comm_[agg_level_].allgather_bytes += (int64_t)(starts[me + 1] - starts[me]) * (n - 1) * (int64_t)sizeof(double);
+  }
   std::vector<P2PMsg> sends, recvs;
   const size_t mine = (size_t)(starts[me + 1] - starts[me]) * sizeof(double);
   for (int p = 0; p < n; ++p) {
@@ -1328,6 +1356,7 @@ void DevAMG::coarse_solve(int level, const double* f, double* u, hipStream_t s) 
   // hypre_GaussElimSolve gathers f on every rank and solves redundantly
   HVE_HIP(launch_set(coarse_n_, 0.0, coarse_f_, s));
   HVE_HIP(launch_copy(L.n, f, coarse_f_ + L.first, s));
+  if (comm_level_ >= 0) cycle_comm_[level].allreduces++;
   comm_->allreduce_sum(coarse_f_, coarse_n_, s);
   HVE_HIP(launch_coarse(coarse_n_, coarse_L_, coarse_mask_, coarse_U_, coarse_f_, coarse_u_, s));
   HVE_HIP(launch_copy(L.n, coarse_u_ + L.first, u, s));
@@ -1401,11 +1430,13 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       if (fw && bw) HVE_HIP(launch_copy(n, u_cur, L.gs_tmp, s));
       if (fw) {
         HVE_HIP(launch_gs_gather(L.gs_fwd.view(), u_cur, nullptr, f, L.hu.n_halo, L.gs_G, L.gs_F, s));
-        HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, cfsel, relax_points, L.gs_G, L.gs_F, u_cur, w, omega, s));
+        HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, cfsel, relax_points, L.gs_G, L.hu.n_halo, L.gs_F, u_cur, w, omega,
+                                         s));
       }
       if (bw) {
         HVE_HIP(launch_gs_gather(L.gs_bwd.view(), u_cur, fw ? L.gs_tmp : nullptr, f, L.hu.n_halo, L.gs_G, L.gs_F, s));
-        HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, cfsel, relax_points, L.gs_G, L.gs_F, u_cur, w, omega, s));
+        HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, cfsel, relax_points, L.gs_G, L.hu.n_halo, L.gs_F, u_cur, w, omega,
+                                         s));
       }
       break;
     }
@@ -1455,6 +1486,12 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
 // neither cleared nor read.
 void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmoothed, bool zero_u) {
   const int nl = (int)lev_.size();
+  cycle_comm_.assign(nl, CycleComm());
+  comm_level_ = 0;
+  struct CountOff {
+    int& l;
+    ~CountOff() { l = -1; }
+  } count_off{comm_level_};
   std::vector<int> lev_counter(nl, prm.cycle_type);
   std::vector<double*> ucur(nl), ualt(nl);
   std::vector<const double*> fl(nl);

@@ -157,6 +157,7 @@ struct DevGs {
   double* val = nullptr;
   int* tcol = nullptr;  // only when a weighted form may run
   int* rowmap = nullptr;
+  int* pos = nullptr;    // rowmap^-1
   double* l1 = nullptr;  // by position
   int* cf = nullptr;     // by position
   int nrows = 0, nteams = 0, nblocks = 0, max_steps = 0, max_width = 0;
@@ -165,7 +166,7 @@ struct DevGs {
   GsView view() const {
     GsView v;
     v.team_step = team_step; v.step = step; v.code = code; v.val = val; v.tcol = tcol; v.rowmap = rowmap;
-    v.l1 = l1; v.cf = cf; v.nteams = nteams; v.nrows = nrows; v.max_width = max_width;
+    v.pos = pos; v.l1 = l1; v.cf = cf; v.nteams = nteams; v.nrows = nrows; v.max_width = max_width;
     return v;
   }
   void upload(const CSR& A, const std::vector<int>& block_starts, bool forward, bool weighted,
@@ -244,6 +245,13 @@ class DevAMG {
   // can be captured (RCCL), unless HVE_GRAPH_MULTI=0.
   void set_use_graph(bool g);
   double cycle_op_count() const { return cycle_ops_; }
+  // This rank's communication in one V-cycle (the last one emitted), per level:
+  // halo exchanges and the bytes they send, all-gathers into the replicated
+  // levels, all-reduces (the coarsest right-hand side).
+  struct CycleComm {
+    int64_t exchanges = 0, bytes = 0, allgathers = 0, allgather_bytes = 0, allreduces = 0;
+  };
+  const std::vector<CycleComm>& cycle_comm() const { return cycle_comm_; }
   bool multi_rank() const { return comm_ != nullptr; }
   // Re-key the row-block traversal (tuning; see locality_keys in runtime.hip).
   // which_mask: bit 0 the A operators, bit 1 P, bit 2 R
@@ -298,6 +306,8 @@ class DevAMG {
     return !e || std::atoi(e) != 0;
   }();
   double cycle_ops_ = 0;
+  std::vector<CycleComm> cycle_comm_;
+  int comm_level_ = -1;  // level whose exchanges are being counted (emit_cycle), -1 = none
   int ws_n_ = 0;
   std::map<std::tuple<const void*, const void*, int>, hipGraphExec_t> graphs_;  // (f, u, presmoothed + 2 zero_u)
   int agg_level_ = -1;            // first replicated level (RankHierarchy::agg_level)

@@ -192,6 +192,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGSetRankEmulation", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BoomerAMGGsScheduleStats", _i, [_p, _i, _i, _i, _pi64]),
+    ("hypreve_BoomerAMGGetCycleCommStats", _i, [_p, _i, _pi64]),
     ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
     ("hypreve_BoomerAMGCodedLayoutCheck", _i, [_p, _i, _i, _pi, _pi]),
     ("hypreve_SetKnob", _i, [_i, _i]),
@@ -555,6 +556,16 @@ class BoomerAMG:
 
     def gs_schedule_check(self, num_blocks):
         check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
+
+    def cycle_comm_stats(self):
+        """This rank's communication in one V-cycle, per level: halo exchanges,
+        bytes sent, all-gathers, all-gather bytes, all-reduces."""
+        out = []
+        for l in range(self.num_levels()):
+            v = (C.c_int64 * 5)()
+            check(lib().hypreve_BoomerAMGGetCycleCommStats(self.h, l, v), "GetCycleCommStats")
+            out.append(dict(zip(("exchanges", "bytes", "allgathers", "allgather_bytes", "allreduces"), list(v))))
+        return out
 
     def gs_schedule_stats(self, level, forward, num_blocks):
         """Packed hybrid-GS schedule of level `level`: nnz, stored entries,

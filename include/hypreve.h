@@ -346,6 +346,10 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, 
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
 HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_blocks);
+/* This rank's communication in one V-cycle (the last one run), level `level`:
+ * out[5] = {halo exchanges, bytes they send, all-gathers into the replicated
+ * levels, their bytes sent, all-reduces}; zeros on one rank. */
+HYPRE_Int hypreve_BoomerAMGGetCycleCommStats(HYPRE_Solver solver, HYPRE_Int level, int64_t *out);
 /* Size of the packed hybrid Gauss-Seidel schedule of level `level`'s A with
  * num_blocks blocks (host only, after Setup / SetupHost): out[6] = {nnz, stored
  * entries, steps, teams, longest team in steps, blocks}. */
