@@ -1290,7 +1290,7 @@ static constexpr int kGsPer = kGsProd / 64;  // entries per lane and chunk
 // step would put a store's completion on every step's critical path.  A batch
 // is fenced before the next one is issued (kGsBatch steps later), so a value
 // reaches U at most 2 kGsBatch - 1 <= kGsFence steps after it was computed.
-static constexpr int kGsBatch = 8;
+static constexpr int kGsBatch = kGsRing / 2;
 static_assert(2 * kGsBatch - 1 <= kGsFence && kGsFence < kGsRing, "ring reach");
 
 // Buffer loads with 32-bit offsets from wave-uniform bases: no 64-bit address

@@ -660,8 +660,9 @@ void DevSell::release() {
 // products, so its teams are small: more of them run at once and a step fits
 // one LDS chunk.  Measured at 256^3 (relax 13/14): level 0 (7 entries a row)
 // 0.70 ms a sweep with 64 rows against 1.01 with 16; level 1 (29 a row) 1.12
-// ms with 16 against 2.34 with 64.  HVE_GS_TEAM_ROWS / HVE_GS_TEAM_ROWS_WIDE
-// override (tuning).
+// ms with 16 against 2.34 with 64; the cycle 8.03 / 8.35 / 9.11 ms with wide
+// teams of 4 / 8 / 16 rows (profiles/r04/gs_tune).  HVE_GS_TEAM_ROWS /
+// HVE_GS_TEAM_ROWS_WIDE override (tuning).
 static int gs_team_rows(const CSR& A) {
   static const int narrow = [] {
     const char* e = getenv("HVE_GS_TEAM_ROWS");
@@ -671,7 +672,7 @@ static int gs_team_rows(const CSR& A) {
   static const int wide = [] {
     const char* e = getenv("HVE_GS_TEAM_ROWS_WIDE");
     const int r = e ? atoi(e) : 0;
-    return r > 0 ? r : 16;
+    return r > 0 ? r : 4;
   }();
   int w = 0;
   for (int i = 0; i < A.nrows; ++i) w = std::max(w, A.i[i + 1] - A.i[i]);

@@ -109,8 +109,11 @@ int64_t sell_padded_nnz(const CSR& A, int sigma);
 //                  row computed at most kGsFence steps earlier
 //    Every row's products are summed in CSR order, so a sweep equals the
 //    sequential per-block sweep bit for bit.
-constexpr int kGsRing = 16;
-constexpr int kGsFence = 15;
+#ifndef HVE_GS_RING
+#define HVE_GS_RING 16
+#endif
+constexpr int kGsRing = HVE_GS_RING;
+constexpr int kGsFence = kGsRing - 1;
 constexpr int kGsRingSlots = kGsRing * 64;
 struct GsSchedule {
   std::vector<int> block_start;  // nb + 1 row boundaries (hypre's ns / ne)
