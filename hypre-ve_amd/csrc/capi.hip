@@ -1427,6 +1427,16 @@ HYPRE_Int hypreve_BoomerAMGGetCycleCommStats(HYPRE_Solver s, HYPRE_Int level, in
   API_END
 }
 
+// Whether the cycle forms level 0's residual and restriction in one pass
+// (k_resid_restrict: single rank, a grid operator on the stencil layout).
+HYPRE_Int hypreve_BoomerAMGGetFusedResidRestrict(HYPRE_Solver s, HYPRE_Int* on) {
+  CHECK_ARG(s && s->kind == KIND_AMG && s->dev, 1);
+  CHECK_ARG(on, 2);
+  API_BEGIN
+  *on = s->dev->fused_rr() ? 1 : 0;
+  API_END
+}
+
 // Size of the packed hybrid Gauss-Seidel schedule of a level's A for a block
 // count (host only): out = {nnz, stored entries, steps, teams, longest team
 // (steps), blocks}.

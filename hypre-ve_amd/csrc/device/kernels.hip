@@ -926,6 +926,172 @@ __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
     code_rows_op<OP, CFSEL, B, MAP, NR, PK>(p, vt, ot, rb, r1);
 }
 
+// ---------------------------------------------------------------------------
+// Level 0's residual fused with its restriction (host: DevAMG::build_rr).
+// One workgroup per tile of kRRTx x kRRTy fine points (x, y) and chunk of zc
+// planes.  It marches z: the residual r = b - A x of plane z over the tile
+// and a two-point margin goes into an LDS ring of six planes, then the R_0
+// rows anchored in plane z - 2 of the tile are summed from the ring.  Every
+// residual is formed by the stencil layout's slot order (as k_sell_stencil
+// does) and every restriction row in its stored order (as k_sell_code does),
+// so F_c (and U_c = 0 + F_c / l1_c) are bitwise the unfused ones.  Six ring
+// slots let one barrier per plane suffice: plane z + 1 overwrites plane z - 5,
+// which the rows of plane z - 2 no longer read.
+// A tile line x0 .. x0 + 63 is exactly one SELL slice (nx % 64 == 0), so its
+// slot data is wave-uniform (scalar); the four margin columns take the slice
+// pattern per lane.
+// ---------------------------------------------------------------------------
+struct RRArgs {
+  RRView v;
+  const double* __restrict__ x;
+  const double* __restrict__ b;
+  double* Fc;
+  double* Uc;
+  const double* __restrict__ l1c;
+  int nblocks_pad;
+};
+
+template <bool ZG>
+__global__ void __launch_bounds__(256) k_resid_restrict(RRArgs a) {
+  constexpr int PX = kRRTx + 4, PY = kRRTy + 4, PL = PX * PY;
+  constexpr int LPW = (PY + 3) / 4;  // lines of a plane per wave
+  constexpr int B = 8;
+  const RRView& p = a.v;
+  extern __shared__ double sm[];
+  double* ring = sm;               // 6 planes of PL
+  double* vt = sm + 6 * PL;        // R_0's values
+  int* oz = reinterpret_cast<int*>(vt + p.nvtabR);
+  int* oxy = oz + p.notab;
+  for (int i = threadIdx.x; i < p.nvtabR; i += 256) vt[i] = p.vtabR[i];
+  for (int i = threadIdx.x; i < p.notab; i += 256) {
+    oz[i] = p.odz[i];
+    oxy[i] = p.odxy[i];
+  }
+  const int lg = xcd_logical_block(blockIdx.x, a.nblocks_pad);
+  if (lg >= p.ntx * p.nty * p.nzc) return;  // the whole workgroup: no barrier reached
+  const int tx = lg % p.ntx, tyi = (lg / p.ntx) % p.nty, zci = lg / (p.ntx * p.nty);
+  const int x0 = tx * kRRTx, y0 = tyi * kRRTy, z0 = zci * p.zc, z1 = min(p.nz, z0 + p.zc);
+  const int ylo = max(0, y0 - 2), yhi = min(p.ny, y0 + kRRTy + 2);
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (kWave - 1);
+  const int W = p.sw;
+  const unsigned vm = (1u << p.vbits) - 1u;
+  __syncthreads();
+  for (int z = max(0, z0 - 2); z < z1 + 2; ++z) {
+    double* rp = ring + (z % 6) * PL;
+    if (z < p.nz) {
+      // tile lines: one slice each, all lines of the wave in flight together
+      int row[LPW], pat[LPW];
+      bool on_line[LPW];
+      double t[LPW];
+#pragma unroll
+      for (int l = 0; l < LPW; ++l) {
+        const int y = ylo + wave + 4 * l;
+        on_line[l] = y < yhi;
+        row[l] = ((z * p.ny + (on_line[l] ? y : ylo)) * p.nx) + x0 + lane;
+        pat[l] = __builtin_amdgcn_readfirstlane(p.slice_pat[row[l] >> 6]);
+        t[l] = a.b[row[l]];
+      }
+      for (int k = 0; k < W; k += B) {
+#pragma unroll
+        for (int l = 0; l < LPW; ++l) {
+          const size_t sb = (size_t)pat[l] * W + k;
+          int off[B], vi[B];
+          uint32_t mlo[B], mhi[B];
+#pragma unroll
+          for (int q = 0; q < B; ++q) {
+            off[q] = __builtin_amdgcn_readfirstlane(p.slot_off[sb + q]);
+            vi[q] = __builtin_amdgcn_readfirstlane(p.slot_vi[sb + q]);
+            const uint64_t m = p.slot_mask[sb + q];
+            mlo[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
+            mhi[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32));
+          }
+          bool on[B];
+          double xv[B], av[B];
+#pragma unroll
+          for (int q = 0; q < B; ++q) {
+            const uint32_t mw = lane < 32 ? mlo[q] : mhi[q];
+            on[q] = ((k + q) < W) && (((mw >> (lane & 31)) & 1u) != 0);
+            xv[q] = a.x[on[q] ? row[l] + off[q] : row[l]];
+          }
+#pragma unroll
+          for (int q = 0; q < B; ++q) av[q] = p.vtabA[vi[q]];
+#pragma unroll
+          for (int q = 0; q < B; ++q) {
+            const double tn = t[l] - av[q] * xv[q];
+            t[l] = on[q] ? tn : t[l];
+          }
+        }
+      }
+#pragma unroll
+      for (int l = 0; l < LPW; ++l)
+        if (on_line[l]) rp[(ylo + wave + 4 * l - y0 + 2) * PX + lane + 2] = t[l];
+      // margin columns x0 - 2, x0 - 1, x0 + 64, x0 + 65 (the slice pattern per lane)
+      for (int q = threadIdx.x; q < 4 * (yhi - ylo); q += 256) {
+        const int y = ylo + q / 4, m = q % 4;
+        const int xx = m < 2 ? x0 - 2 + m : x0 + kRRTx + (m - 2);
+        if (xx < 0 || xx >= p.nx) continue;
+        const int r = (z * p.ny + y) * p.nx + xx;
+        const int pt = p.slice_pat[r >> 6], ln = r & 63;
+        double tt = a.b[r];
+        for (int k = 0; k < W; ++k) {
+          const size_t sk = (size_t)pt * W + k;
+          if ((p.slot_mask[sk] >> ln) & 1ull) tt -= p.vtabA[p.slot_vi[sk]] * a.x[r + p.slot_off[sk]];
+        }
+        rp[(y - y0 + 2) * PX + (xx - x0 + 2)] = tt;
+      }
+    }
+    __syncthreads();
+    const int zr = z - 2;
+    if (zr >= z0 && zr < z1) {
+      const int bk = (tyi * p.ntx + tx) * p.nz + zr;
+      const int r0 = p.bptr[bk], r1 = p.bptr[bk + 1], ent = p.bent[bk];
+      const int* __restrict__ cnt = p.bcnt + p.bcptr[bk];
+      for (int q = r0 + (int)threadIdx.x; q < r1; q += 256) {
+        const int j = q - r0, len = p.blen[q], lb = p.blb[q];
+        double t = 0.0;
+        for (int k = 0; k < len; ++k) {
+          const unsigned c = p.code[ent + cnt[k] + j];
+          const int o = (int)(c >> p.vbits);
+          t += vt[c & vm] * ring[((zr + oz[o]) % 6) * PL + lb + oxy[o]];
+        }
+        const int row = p.brow[q];
+        a.Fc[row] = t;
+        if (ZG) a.Uc[row] = 0.0 + t / a.l1c[row];
+      }
+    }
+  }
+}
+
+hipError_t launch_resid_restrict(const RRView& V, const double* x, const double* b, double* Fc, double* Uc,
+                                 const double* l1c, hipStream_t st) {
+  constexpr int PL = (kRRTx + 4) * (kRRTy + 4);
+  if (V.ty != kRRTy || V.nx % kRRTx) return hipErrorInvalidValue;
+  RRArgs a;
+  a.v = V; a.x = x; a.b = b; a.Fc = Fc; a.Uc = Uc; a.l1c = l1c;
+  const int nwg = V.ntx * V.nty * V.nzc;
+  a.nblocks_pad = (nwg + 7) / 8 * 8;
+  const size_t lds = (size_t)6 * PL * sizeof(double) + (size_t)V.nvtabR * sizeof(double) + (size_t)2 * V.notab * sizeof(int);
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (Uc) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k_resid_restrict<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_resid_restrict<true>, dim3(a.nblocks_pad), dim3(256), lds, st, a);
+  } else {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)k_resid_restrict<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      attr = true;
+    }
+    hipLaunchKernelGGL(k_resid_restrict<false>, dim3(a.nblocks_pad), dim3(256), lds, st, a);
+  }
+  return hipGetLastError();
+}
+
 template <int OP, bool CFSEL, bool NT>
 __global__ void __launch_bounds__(256) k_sell_wide(SpArgs p) {
   constexpr int KCH = 32;       // entries per row and chunk: 64 x 32 products = 16 KiB of LDS

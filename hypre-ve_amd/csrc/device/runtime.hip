@@ -761,6 +761,7 @@ DevAMG::~DevAMG() { release(); }
 
 void DevAMG::release() {
   graphs_clear();
+  rr_.release();
   for (auto& L : lev_) {
     L.A.release(); L.P.release(); L.R.release();
     L.hu.release(); L.hv.release();
@@ -1019,6 +1020,207 @@ double bench_operator(const CSR& A, int op, int policy, int nbands, int reps, do
   return ms / reps;
 }
 
+void DevRR::release() {
+  for (void* p : {(void*)bptr, (void*)bent, (void*)bcptr, (void*)bcnt, (void*)brow, (void*)blb, (void*)blen, (void*)code,
+                  (void*)vtab, (void*)odz, (void*)odxy})
+    if (p) (void)hipFree(p);
+  bptr = bent = bcptr = bcnt = brow = odz = odxy = nullptr;
+  blb = code = nullptr;
+  blen = nullptr;
+  vtab = nullptr;
+  nvtab = notab = vbits = nbuckets = 0;
+  entries = 0;
+}
+
+// Fine grid of level 0 from its operator, read off an interior row: line =
+// its smallest column offset above 1 (plus one when that offset + 1 is also a
+// neighbour: the diagonal neighbours of a 27-point stencil), plane = its
+// largest offset (minus line + 1 for a 27-point stencil); nx = line,
+// ny = plane / line.  Only a guess: build_rr checks every restriction entry
+// against it, and any factorisation that passes gives the same sums.
+static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz) {
+  const int n = A.nrows;
+  if (n < 4096) return false;
+  for (int i : {n / 2, n / 2 + 7, n / 3 + 11}) {
+    std::vector<int64_t> off;
+    for (int k = A.i[i]; k < A.i[i + 1]; ++k)
+      if (A.j[k] > i) off.push_back((int64_t)A.j[k] - i);
+    std::sort(off.begin(), off.end());
+    auto has = [&](int64_t d) { return std::binary_search(off.begin(), off.end(), d); };
+    int64_t line = 0;
+    for (int64_t d : off)
+      if (d > 1) { line = has(d + 1) ? d + 1 : d; break; }
+    if (line < 2 || off.empty()) continue;
+    int64_t plane = off.back();
+    if (has(plane - 1)) plane -= line + 1;
+    if (plane < 2 * line || plane % line || n % plane) continue;
+    *nx = (int)line;
+    *ny = (int)(plane / line);
+    *nz = (int)(n / plane);
+    return true;
+  }
+  return false;
+}
+
+// Level 0's fused residual + restriction (DevRR), when level 0 is a grid
+// operator on the stencil layout held by one rank and every R_0 row reaches
+// at most two points from its coarse point's fine point in each direction.
+// fc: the fine point of each coarse point.  HVE_FUSE_RR=0 turns it off.
+void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
+  static const int env = [] {
+    const char* e = getenv("HVE_FUSE_RR");
+    return e ? atoi(e) : 1;
+  }();
+  static const int zc_env = [] {
+    const char* e = getenv("HVE_RR_ZC");
+    return e ? atoi(e) : 64;
+  }();
+  rr_.release();
+  if (!env || R.lev.size() < 2 || comm_) return;
+  const RankLevel& L = R.lev[0];
+  const DevLevel& D = lev_[0];
+  if (!D.A.in.slot_mask || D.A.bd.nrows || D.A.in.rowmap || D.R.bd.nrows || !L.A.map_int.empty() ||
+      !L.R.map_int.empty() || L.hv.n_halo || L.hu.n_halo)
+    return;
+  const CSR& A = L.A.interior;
+  const CSR& Rm = L.R.interior;
+  int nx, ny, nz;
+  if (!fine_grid(A, &nx, &ny, &nz) || nx % kRRTx || (int)fc.size() != Rm.nrows) return;
+  const int ty = kRRTy, zc = std::max(1, std::min(zc_env, nz));
+  const int ntx = nx / kRRTx, nty = (ny + ty - 1) / ty, nzc = (nz + zc - 1) / zc;
+  const int nb = ntx * nty * nz;
+  const int nc = Rm.nrows;
+  constexpr int PX = kRRTx + 4;
+  // every entry: (dx, dy, dz) from the anchor, each within +-2
+  std::vector<int> okey(125, -1), ocode;  // (dz, dy, dx) + 2 in base 5 -> offset index
+  std::vector<int> bucket(nc);
+  bool ok = true;
+  for (int c = 0; c < nc && ok; ++c) {
+    const int a = fc[c];
+    const int xa = a % nx, ya = (a / nx) % ny, za = a / (nx * ny);
+    bucket[c] = ((ya / ty) * ntx + xa / kRRTx) * nz + za;
+    for (int k = Rm.i[c]; k < Rm.i[c + 1]; ++k) {
+      const int j = Rm.j[k];
+      const int dx = j % nx - xa, dy = (j / nx) % ny - ya, dz = j / (nx * ny) - za;
+      if (std::abs(dx) > 2 || std::abs(dy) > 2 || std::abs(dz) > 2) { ok = false; break; }
+      const int key = ((dz + 2) * 5 + dy + 2) * 5 + dx + 2;
+      if (okey[key] < 0) {
+        okey[key] = (int)ocode.size();
+        ocode.push_back(key);
+      }
+    }
+  }
+  if (!ok) return;
+  std::vector<unsigned short> vi16;
+  std::vector<double> tab;
+  if (!build_value_table16(Rm.a, 4096, vi16, tab)) return;
+  int vbits = 1;
+  while ((1 << vbits) < (int)tab.size()) ++vbits;
+  if ((int)ocode.size() > (1 << (16 - vbits))) return;
+  // buckets: rows by (tile, plane), each bucket's rows by length, descending
+  std::vector<int> bptr(nb + 1, 0);
+  for (int c = 0; c < nc; ++c) bptr[bucket[c] + 1]++;
+  for (int b = 0; b < nb; ++b) bptr[b + 1] += bptr[b];
+  std::vector<int> brow(nc);
+  {
+    std::vector<int> pos(bptr.begin(), bptr.end() - 1);
+    for (int c = 0; c < nc; ++c) brow[pos[bucket[c]]++] = c;
+  }
+  std::vector<int64_t> bent(nb + 1, 0);
+  std::vector<int> bcptr(nb + 1, 0);
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int b = 0; b < nb; ++b) {
+    auto len = [&](int c) { return Rm.i[c + 1] - Rm.i[c]; };
+    std::stable_sort(brow.begin() + bptr[b], brow.begin() + bptr[b + 1],
+                     [&](int p, int q) { return len(p) > len(q); });
+    int64_t e = 0;
+    for (int q = bptr[b]; q < bptr[b + 1]; ++q) e += len(brow[q]);
+    bent[b + 1] = e;
+    bcptr[b + 1] = bptr[b + 1] > bptr[b] ? len(brow[bptr[b]]) + 1 : 0;
+  }
+  for (int b = 0; b < nb; ++b) {
+    bent[b + 1] += bent[b];
+    bcptr[b + 1] += bcptr[b];
+  }
+  if (bent[nb] >= INT_MAX) return;
+  std::vector<int> bcnt(std::max(1, bcptr[nb]));
+  std::vector<unsigned short> code((size_t)std::max<int64_t>(1, bent[nb]));
+  std::vector<unsigned short> blb(nc);
+  std::vector<unsigned char> blen(nc);
+  bool fits = true;
+#pragma omp parallel for schedule(dynamic, 64) reduction(&& : fits)
+  for (int b = 0; b < nb; ++b) {
+    const int r0 = bptr[b], r1 = bptr[b + 1];
+    if (r0 == r1) continue;
+    const int w = Rm.i[brow[r0] + 1] - Rm.i[brow[r0]];
+    int* cnt = &bcnt[bcptr[b]];
+    cnt[0] = 0;
+    for (int k = 0; k < w; ++k) {
+      int nk = 0;
+      while (r0 + nk < r1 && Rm.i[brow[r0 + nk] + 1] - Rm.i[brow[r0 + nk]] > k) ++nk;
+      cnt[k + 1] = cnt[k] + nk;
+    }
+    const int tx0 = ((b / nz) % ntx) * kRRTx, ty0 = ((b / nz) / ntx) * ty;
+    for (int q = r0; q < r1; ++q) {
+      const int c = brow[q];
+      const int a = fc[c];
+      const int xa = a % nx, ya = (a / nx) % ny;
+      const int len = Rm.i[c + 1] - Rm.i[c];
+      if (len > 255) fits = false;
+      blen[q] = (unsigned char)std::min(len, 255);
+      blb[q] = (unsigned short)((ya - ty0 + 2) * PX + (xa - tx0 + 2));
+      for (int k = 0; k < len; ++k) {
+        const int kk = Rm.i[c] + k, j = Rm.j[kk];
+        const int key = ((j / (nx * ny) - a / (nx * ny) + 2) * 5 + (j / nx) % ny - ya + 2) * 5 + j % nx - xa + 2;
+        code[(size_t)bent[b] + cnt[k] + (q - r0)] = (unsigned short)((okey[key] << vbits) | vi16[kk]);
+      }
+    }
+  }
+  if (!fits) return;
+  std::vector<int> odz(ocode.size()), odxy(ocode.size());
+  for (size_t o = 0; o < ocode.size(); ++o) {
+    const int key = ocode[o], dx = key % 5 - 2, dy = (key / 5) % 5 - 2, dz = key / 25 - 2;
+    odz[o] = dz;
+    odxy[o] = dy * PX + dx;
+  }
+  std::vector<int> bent32(nb + 1);
+  for (int b = 0; b <= nb; ++b) bent32[b] = (int)bent[b];
+  rr_.nx = nx; rr_.ny = ny; rr_.nz = nz; rr_.ty = ty; rr_.zc = zc;
+  rr_.ntx = ntx; rr_.nty = nty; rr_.nzc = nzc;
+  rr_.nbuckets = nb;
+  rr_.entries = bent[nb];
+  rr_.bptr = dupload(bptr.data(), bptr.size());
+  rr_.bent = dupload(bent32.data(), bent32.size());
+  rr_.bcptr = dupload(bcptr.data(), bcptr.size());
+  rr_.bcnt = dupload(bcnt.data(), bcnt.size());
+  rr_.brow = dupload(brow.data(), std::max<size_t>(1, brow.size()));
+  rr_.blb = dupload(blb.data(), std::max<size_t>(1, blb.size()));
+  rr_.blen = dupload(blen.data(), std::max<size_t>(1, blen.size()));
+  rr_.code = dupload(code.data(), code.size());
+  rr_.vtab = dupload(tab.data(), tab.size());
+  rr_.nvtab = (int)tab.size();
+  rr_.odz = dupload(odz.data(), odz.size());
+  rr_.odxy = dupload(odxy.data(), odxy.size());
+  rr_.notab = (int)ocode.size();
+  rr_.vbits = vbits;
+  if (getenv("HVE_LAYOUT_LOG"))
+    fprintf(stderr, "[layout] fused residual+restriction: grid %dx%dx%d, tiles %dx%d, %d-plane chunks, %d offsets, "
+            "%d values, %lld entries\n", nx, ny, nz, kRRTx, ty, zc, rr_.notab, rr_.nvtab, (long long)rr_.entries);
+}
+
+RRView DevAMG::rr_view() const {
+  const DevSell& A = lev_[0].A.in;
+  RRView v;
+  v.slice_pat = A.slice_pat; v.slot_off = A.slot_base; v.slot_vi = A.slot_vi; v.slot_mask = A.slot_mask;
+  v.vtabA = A.vtab; v.sw = A.stencil_w;
+  v.nx = rr_.nx; v.ny = rr_.ny; v.nz = rr_.nz; v.ty = rr_.ty; v.zc = rr_.zc;
+  v.ntx = rr_.ntx; v.nty = rr_.nty; v.nzc = rr_.nzc;
+  v.bptr = rr_.bptr; v.bent = rr_.bent; v.bcptr = rr_.bcptr; v.bcnt = rr_.bcnt; v.brow = rr_.brow;
+  v.blb = rr_.blb; v.blen = rr_.blen; v.code = rr_.code; v.vtabR = rr_.vtab; v.odz = rr_.odz; v.odxy = rr_.odxy;
+  v.nvtabR = rr_.nvtab; v.notab = rr_.notab; v.vbits = rr_.vbits;
+  return v;
+}
+
 void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   const int n0 = R.lev.empty() ? 0 : R.lev[0].n_loc;
   init_workspace(n0, comm);
@@ -1049,6 +1251,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   tile_keys(R, agg_level_, tiles);
   const bool tlog = getenv("HVE_SETUP_T") != nullptr;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  std::vector<int> fc0;  // level 0: the fine point of each coarse point
   for (int l = 0; l < nl; ++l) {
     const double tl0 = now();
     const RankLevel& L = R.lev[l];
@@ -1095,6 +1298,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       D.P.upload(L.P, prm.sell_policy, kl, pc);
       D.R.upload(L.R, prm.sell_policy, kc, rc, tc);
       D.hv.upload(L.hv);
+      if (l == 0) fc0 = fc;
     }
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
     D.l1_fly = !L.l1.empty() && l1_on_the_fly(L.A, L.l1) && D.A.in.delta_like() && (D.A.bd.nrows == 0 || D.A.bd.delta_like());
@@ -1157,6 +1361,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       if (fwd && bwd) D.gs_tmp = dalloc<double>((size_t)D.n + 1);
     }
   }
+  build_rr(R, fc0);
   coarse_n_ = R.coarse_n;
   if (coarse_n_ > 0) {
     std::vector<double> Lf, U;
@@ -1569,14 +1774,19 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
     if (lev_counter[level] >= 0 && level != nl - 1) {
       const int fine = level, coarse = level + 1;
       DevLevel& Lf = lev_[fine];
-      // Vtemp = f - A u  (csr_matvec.c, alpha=-1 beta=1);  F_c = P^T Vtemp
-      apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);
       // When the coarse level's first down sweep is l1-Jacobi (weight 1) from
       // the zero guess, u_c = 0 + F_c/l1 is formed by the restriction itself.
       const bool into_agg = agg_level_ >= 0 && coarse == agg_level_;
       const bool fuse_zg = !into_agg && coarse != nl - 1 && prm.num_sweeps[1] >= 1 && prm.relax_order != 1 &&
                            (prm.relax_type[1] == 18 || prm.relax_type[1] == 7) && prm.wt(coarse) == 1.0 &&
                            lev_[coarse].l1 != nullptr;
+      if (fine == 0 && rr_.built() && !into_agg) {
+        // F_c = P^T (f - A u) in one pass: the residual stays in LDS
+        HVE_HIP(launch_resid_restrict(rr_view(), ucur[fine], fl[fine], lev_[coarse].F,
+                                      fuse_zg ? ucur[coarse] : nullptr, fuse_zg ? lev_[coarse].l1 : nullptr, s));
+      } else {
+      // Vtemp = f - A u  (csr_matvec.c, alpha=-1 beta=1);  F_c = P^T Vtemp
+      apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);
       if (fuse_zg) {
         apply(Lf.R, &Lf.hv, K_RESTRICT_ZG, Lf.V, nullptr, lev_[coarse].l1, nullptr, 0, lev_[coarse].F, 1.0, 0.0,
               s, ucur[coarse]);
@@ -1587,6 +1797,7 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
         allgather_rows(lev_[coarse].F, agg_starts_, s);
       } else {
         apply(Lf.R, &Lf.hv, K_RESTRICT, Lf.V, nullptr, nullptr, nullptr, 0, lev_[coarse].F, 1.0, 0.0, s);
+      }
       }
       ++level;
       lev_counter[level] = std::max(lev_counter[level], prm.cycle_type);

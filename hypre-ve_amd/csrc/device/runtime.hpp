@@ -174,6 +174,32 @@ struct DevGs {
   void release();
 };
 
+// Level 0's residual fused with its restriction (k_resid_restrict): the fine
+// grid in tiles of kRRTx x ty points and chunks of zc planes, the residual
+// of a tile's planes (plus a two-point margin) formed into an LDS ring, and
+// the R_0 rows anchored in the tile applied from it, so r never goes to HBM.
+// R_0's rows in buckets (tile, plane), each bucket's rows sorted by length and
+// stored jagged: entry k of bucket row j at ent[b] + cnt[cptr[b] + k] + j, one
+// 16-bit code (offset index << vbits | value index) per entry.
+struct DevRR {
+  int nx = 0, ny = 0, nz = 0, ty = 0, zc = 0, ntx = 0, nty = 0, nzc = 0;
+  int* bptr = nullptr;   // buckets + 1: rows of bucket b = (ty_i * ntx + tx_i) * nz + z
+  int* bent = nullptr;   // per bucket: first entry
+  int* bcptr = nullptr;  // per bucket: its prefix counts in bcnt (width + 1 values)
+  int* bcnt = nullptr;
+  int* brow = nullptr;   // per bucket row: the coarse row
+  unsigned short* blb = nullptr;  // per bucket row: the anchor's LDS index in its plane
+  unsigned char* blen = nullptr;  // per bucket row: entries
+  unsigned short* code = nullptr;
+  double* vtab = nullptr;
+  int* odz = nullptr;    // per offset index: dz
+  int* odxy = nullptr;   // per offset index: dy * (kRRTx + 4) + dx
+  int nvtab = 0, notab = 0, vbits = 0, nbuckets = 0;
+  int64_t entries = 0;
+  bool built() const { return bptr != nullptr; }
+  void release();
+};
+
 struct DevHalo {
   int n_loc = 0, n_halo = 0, n_send = 0;
   std::vector<int> peers, recv_cnt, recv_off, send_cnt, send_off;
@@ -253,6 +279,7 @@ class DevAMG {
   };
   const std::vector<CycleComm>& cycle_comm() const { return cycle_comm_; }
   bool multi_rank() const { return comm_ != nullptr; }
+  bool fused_rr() const { return rr_.built(); }
   // Re-key the row-block traversal (tuning; see locality_keys in runtime.hip).
   // which_mask: bit 0 the A operators, bit 1 P, bit 2 R
   void set_block_bands(const RankHierarchy& R, int nbands, int which_mask = 7);
@@ -310,6 +337,9 @@ class DevAMG {
   int comm_level_ = -1;  // level whose exchanges are being counted (emit_cycle), -1 = none
   int ws_n_ = 0;
   std::map<std::tuple<const void*, const void*, int>, hipGraphExec_t> graphs_;  // (f, u, presmoothed + 2 zero_u)
+  DevRR rr_;                      // level 0's fused residual + restriction (single rank, grid operator)
+  void build_rr(const RankHierarchy& R, const std::vector<int>& fc);
+  RRView rr_view() const;
   int agg_level_ = -1;            // first replicated level (RankHierarchy::agg_level)
   std::vector<int> agg_starts_;   // its rows' distributed owners
 };

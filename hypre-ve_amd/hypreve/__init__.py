@@ -193,6 +193,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BoomerAMGGsScheduleStats", _i, [_p, _i, _i, _i, _pi64]),
     ("hypreve_BoomerAMGGetCycleCommStats", _i, [_p, _i, _pi64]),
+    ("hypreve_BoomerAMGGetFusedResidRestrict", _i, [_p, _pi]),
     ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
     ("hypreve_BoomerAMGCodedLayoutCheck", _i, [_p, _i, _i, _pi, _pi]),
     ("hypreve_SetKnob", _i, [_i, _i]),
@@ -556,6 +557,12 @@ class BoomerAMG:
 
     def gs_schedule_check(self, num_blocks):
         check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
+
+    def fused_resid_restrict(self):
+        """Whether level 0's residual and restriction run as one kernel."""
+        v = C.c_int()
+        check(lib().hypreve_BoomerAMGGetFusedResidRestrict(self.h, C.byref(v)), "GetFusedResidRestrict")
+        return bool(v.value)
 
     def cycle_comm_stats(self):
         """This rank's communication in one V-cycle, per level: halo exchanges,

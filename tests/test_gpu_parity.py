@@ -403,3 +403,44 @@ def test_interp_types_bitwise(gpu, orc, interp, agg, agg_interp, order):
     st = O.solve(f_h, xo, 1e-7, 80)
     assert it == st["iterations"]
     assert np.array_equal(x.get(), xo)
+
+
+@pytest.mark.parametrize("gen,n3,relax", [("7", (64, 40, 36), 18), ("7", (128, 33, 20), 18), ("7", (64, 40, 36), 0),
+                                          ("27", (64, 24, 20), 18), ("aniso", (64, 30, 28), 18),
+                                          ("7", (64, 40, 36), 13)])
+def test_fused_resid_restrict_bitwise(gpu, orc, gen, n3, relax):
+    """Level 0's residual fused with its restriction (k_resid_restrict, the
+    residual kept in an LDS ring of planes, par_cycle.c:549-566): with the
+    coarse zero-guess sweep folded in (relax 18) and without (0, 13), the
+    7-point, 27-point and anisotropic operators, a V-cycle from a random
+    iterate and a 3-iteration solve equal the oracle bit for bit, and the
+    fused kernel is the one that ran."""
+    hv = gpu
+    if gen == "27":
+        A = hv.ParCSRMatrix.laplacian27(*n3)
+    elif gen == "aniso":
+        A = hv.ParCSRMatrix.laplacian(*n3, cx=0.001, cy=1.0, cz=1.0)
+    else:
+        A = hv.ParCSRMatrix.laplacian(*n3)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, relax_type=relax, P_max_elmts=4)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup(A)
+    assert amg.fused_resid_restrict()
+    O = orc.OracleAMG(amg)
+    n = A.n
+    rng = np.random.default_rng(3)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+    amg.set(tol=0.0, max_iter=3)
+    x = hv.ParVector(n, np.zeros(n))
+    amg.solve(A, f, x)
+    xo = np.zeros(n)
+    O.solve(f_h, xo, 0.0, 3)
+    assert np.array_equal(x.get(), xo)
