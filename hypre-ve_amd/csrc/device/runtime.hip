@@ -2015,7 +2015,7 @@ int DevAMG::solve(const double* f, double* u, hipStream_t s, int* iters, double*
   return 0;
 }
 
-// krylov/pcg.c:262 hypre_PCGSolve (two_norm selectable; stop_crit/rel_change
+// krylov/pcg.c:271 hypre_PCGSolve (two_norm selectable; stop_crit/rel_change
 // off; no recompute) with one BoomerAMG cycle on a cleared vector as the
 // preconditioner (HYPRE_BoomerAMGSolve with tol 0, max_iter 1).  Scalars stay
 // on the device; one host read per iteration for the convergence test.

@@ -348,7 +348,7 @@ class DevAMG {
 double bench_operator(const CSR& A, int op, int policy, int nbands, int reps, double* stored_bytes, char* layout_msg,
                       int msg_len);
 
-// PCG (krylov/pcg.c:262).
+// PCG (krylov/pcg.c:271).
 struct PCGParams {
   double tol = 1e-6, atol = 0.0;
   int max_iter = 1000;

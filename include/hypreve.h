@@ -148,8 +148,10 @@ HYPRE_Int HYPRE_BoomerAMGSetCoarsenType(HYPRE_Solver solver, HYPRE_Int coarsen_t
 HYPRE_Int HYPRE_BoomerAMGSetMeasureType(HYPRE_Solver solver, HYPRE_Int measure_type); /* :362 */
 HYPRE_Int HYPRE_BoomerAMGSetAggNumLevels(HYPRE_Solver solver, HYPRE_Int agg_num_levels); /* :369 */
 HYPRE_Int HYPRE_BoomerAMGSetNumPaths(HYPRE_Solver solver, HYPRE_Int num_paths); /* :377 */
-/* Aggressive-level interpolation: 4 (multipass, the default) is available;
- * Setup fails with HYPRE_ERROR_GENERIC for the other types. */
+/* Aggressive-level interpolation: 4 (multipass, the default), 5 (2-stage
+ * extended, matrix-matrix form: par_mod_lr_interp.c:16 then par_2s_interp.c:15)
+ * and 7 (2-stage extended+e: par_mod_lr_interp.c:1040 then par_2s_interp.c:564);
+ * Setup fails with HYPRE_ERROR_ARG for 1-3, 6 and 8. */
 HYPRE_Int HYPRE_BoomerAMGSetAggInterpType(HYPRE_Solver solver, HYPRE_Int agg_interp_type); /* :480 */
 HYPRE_Int HYPRE_BoomerAMGSetAggTruncFactor(HYPRE_Solver solver, HYPRE_Real agg_trunc_factor); /* :488 */
 HYPRE_Int HYPRE_BoomerAMGSetAggP12TruncFactor(HYPRE_Solver solver, HYPRE_Real agg_P12_trunc_factor); /* :496 */
@@ -269,20 +271,22 @@ HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
  * l1 norms to match), so its iterates equal the N-rank iterates. nranks <= 1
  * clears it. Takes effect at Setup. */
 HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver solver, HYPRE_Int nranks, const HYPRE_Int *starts);
+/* The relaxation weight and outer weight (omega) the cycle uses on `level`. */
+HYPRE_Int hypreve_BoomerAMGGetLevelWeights(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Real *relax_weight,
+                                           HYPRE_Real *omega);
 /* One process reproduces the setup and smoothing of a reference N-rank run
  * (mpirun -np N) whose level-0 rows start at starts[0..nranks]: every row in
  * ParCSR order (the rank's own columns, then the others; par_csr_matrix.c),
  * per-rank PMIS random streams (par_indepset.c:25, seed 2747 + rank), per-rank
  * HMIS first passes (par_coarsen.c:874 on S_diag), the CF_marker_offd
- * semantics of par_coarsen.c:2296/2348, ext+i truncation over [P_diag | P_offd]
+ * semantics of par_coarsen.c:2296/2348, truncation over [P_diag | P_offd]
  * (par_csr_matrix.c:2671), and the hybrid GS blocks of SetGsRankStarts.
  * Coarse-level agglomeration is off (the reference has none).  This pins the
  * product to the reference's own np > 1 saved outputs.  nranks <= 1 clears it.
- * Aggressive levels: the second pass per rank as well, multipass rows in
- * P_diag | P_offd order.  Takes effect at Setup; ext+i (interp_type 6). */
-/* The relaxation weight and outer weight (omega) the cycle uses on `level`. */
-HYPRE_Int hypreve_BoomerAMGGetLevelWeights(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Real *relax_weight,
-                                           HYPRE_Real *omega);
+ * Interpolation: ext+i (6) and ext (14) per rank, the matrix-matrix forms
+ * (16 / 17 / 18) with hypre_ParMatmul's np > 1 entry order; aggressive levels:
+ * the second pass per rank as well, multipass rows in P_diag | P_offd order,
+ * and the 2-stage types 5 / 7.  Takes effect at Setup. */
 HYPRE_Int hypreve_BoomerAMGSetRankEmulation(HYPRE_Solver solver, HYPRE_Int nranks, const HYPRE_Int *starts);
 /* Multi-rank: coarse levels with at most `rows` global rows (from the first
  * such level down) are held whole by every rank and cycled redundantly, with

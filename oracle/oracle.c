@@ -470,7 +470,7 @@ int orc_amg_solve(const orc_amg *amg, const double *f, double *u, double tol,
   return err;
 }
 
-/* ---- krylov/pcg.c:262 hypre_PCGSolve (stop_crit 0, rel_change 0, no
+/* ---- krylov/pcg.c:271 hypre_PCGSolve (stop_crit 0, rel_change 0, no
  * recompute, cf_tol 0) with BoomerAMG preconditioning: HYPRE_BoomerAMGSolve
  * with tol 0 and max_iter 1 performs exactly one cycle on a cleared vector. ---- */
 int orc_pcg_amg(const orc_amg *amg, const double *b, double *x, double tol,

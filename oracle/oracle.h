@@ -87,7 +87,7 @@ int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count);
 int orc_amg_solve(const orc_amg *amg, const double *f, double *u, double tol,
                   int min_iter, int max_iter, int converge_type, double *stats);
 
-/* krylov/pcg.c:262 hypre_PCGSolve with BoomerAMG (1 V-cycle, tol 0) as
+/* krylov/pcg.c:271 hypre_PCGSolve with BoomerAMG (1 V-cycle, tol 0) as
  * preconditioner (two_norm selectable).  stats[0]=iterations, [1]=rel. res. */
 int orc_pcg_amg(const orc_amg *amg, const double *b, double *x, double tol,
                 int max_iter, int two_norm, double *stats);
