@@ -129,7 +129,8 @@ struct RRView {
   const unsigned short* blb = nullptr;
   const unsigned char* blen = nullptr;
   const unsigned short* code = nullptr;
-  const double* vtabR = nullptr;
+  const double* vtabR = nullptr;  // the weights, indexed by the code's low vbits, or
+  const double* bval = nullptr;   // one weight per entry (vbits 0)
   const int* odz = nullptr;
   const int* odxy = nullptr;
   int nvtabR = 0, notab = 0, vbits = 0;
@@ -142,7 +143,8 @@ int sell_batch_override();
 // Tuning knobs read at launch (0 = default): 0 offset-coded row blocks per
 // step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU,
 // 3 stream-mix access width (2: 16 B), 7 caps the device setup's LDS tables
-// at 2^v slots (tests of its host fallback).
+// at 2^v slots (tests of its host fallback), 8 the fused level-0 residual +
+// restriction at the next Setup (1 on, -1 off, 0 HVE_FUSE_RR).
 void set_knob(int id, int v);
 int knob(int id);
 int stencil_slices_per_wave();

@@ -951,7 +951,7 @@ struct RRArgs {
   int nblocks_pad;
 };
 
-template <bool ZG>
+template <bool ZG, bool VT>
 __global__ void __launch_bounds__(256) k_resid_restrict(RRArgs a) {
   constexpr int PX = kRRTx + 4, PY = kRRTy + 4, PL = PX * PY;
   constexpr int LPW = (PY + 3) / 4;  // lines of a plane per wave
@@ -1050,9 +1050,11 @@ __global__ void __launch_bounds__(256) k_resid_restrict(RRArgs a) {
         const int j = q - r0, len = p.blen[q], lb = p.blb[q];
         double t = 0.0;
         for (int k = 0; k < len; ++k) {
-          const unsigned c = p.code[ent + cnt[k] + j];
+          const int e = ent + cnt[k] + j;
+          const unsigned c = p.code[e];
           const int o = (int)(c >> p.vbits);
-          t += vt[c & vm] * ring[((zr + oz[o]) % 6) * PL + lb + oxy[o]];
+          const double w = VT ? vt[c & vm] : p.bval[e];
+          t += w * ring[((zr + oz[o]) % 6) * PL + lb + oxy[o]];
         }
         const int row = p.brow[q];
         a.Fc[row] = t;
@@ -1072,23 +1074,23 @@ hipError_t launch_resid_restrict(const RRView& V, const double* x, const double*
   a.nblocks_pad = (nwg + 7) / 8 * 8;
   const size_t lds = (size_t)6 * PL * sizeof(double) + (size_t)V.nvtabR * sizeof(double) + (size_t)2 * V.notab * sizeof(int);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
-  if (Uc) {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)k_resid_restrict<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      attr = true;
-    }
-    hipLaunchKernelGGL(k_resid_restrict<true>, dim3(a.nblocks_pad), dim3(256), lds, st, a);
-  } else {
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)k_resid_restrict<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024);
-      attr = true;
-    }
-    hipLaunchKernelGGL(k_resid_restrict<false>, dim3(a.nblocks_pad), dim3(256), lds, st, a);
+#define HVE_RR(ZGV, VTV)                                                                              \
+  {                                                                                                    \
+    static bool attr = false;                                                                          \
+    if (!attr) {                                                                                       \
+      (void)hipFuncSetAttribute((const void*)k_resid_restrict<ZGV, VTV>,                              \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);               \
+      attr = true;                                                                                     \
+    }                                                                                                  \
+    hipLaunchKernelGGL((k_resid_restrict<ZGV, VTV>), dim3(a.nblocks_pad), dim3(256), lds, st, a);     \
   }
+  const bool vt = V.bval == nullptr;
+  if (Uc) {
+    if (vt) HVE_RR(true, true) else HVE_RR(true, false)
+  } else {
+    if (vt) HVE_RR(false, true) else HVE_RR(false, false)
+  }
+#undef HVE_RR
   return hipGetLastError();
 }
 

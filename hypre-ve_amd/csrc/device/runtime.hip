@@ -1022,12 +1022,12 @@ double bench_operator(const CSR& A, int op, int policy, int nbands, int reps, do
 
 void DevRR::release() {
   for (void* p : {(void*)bptr, (void*)bent, (void*)bcptr, (void*)bcnt, (void*)brow, (void*)blb, (void*)blen, (void*)code,
-                  (void*)vtab, (void*)odz, (void*)odxy})
+                  (void*)vtab, (void*)bval, (void*)odz, (void*)odxy})
     if (p) (void)hipFree(p);
   bptr = bent = bcptr = bcnt = brow = odz = odxy = nullptr;
   blb = code = nullptr;
   blen = nullptr;
-  vtab = nullptr;
+  vtab = bval = nullptr;
   nvtab = notab = vbits = nbuckets = 0;
   entries = 0;
 }
@@ -1065,27 +1065,44 @@ static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz) {
 // Level 0's fused residual + restriction (DevRR), when level 0 is a grid
 // operator on the stencil layout held by one rank and every R_0 row reaches
 // at most two points from its coarse point's fine point in each direction.
-// fc: the fine point of each coarse point.  HVE_FUSE_RR=0 turns it off.
+// fc: the fine point of each coarse point.  HVE_FUSE_RR=1 turns it on (off by
+// default: first measurement 8.35 ms at 512^3 against 0.90 + 1.63 unfused,
+// each plane a chain of dependent loads).
 void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
   static const int env = [] {
     const char* e = getenv("HVE_FUSE_RR");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 0;
   }();
   static const int zc_env = [] {
     const char* e = getenv("HVE_RR_ZC");
     return e ? atoi(e) : 64;
   }();
   rr_.release();
-  if (!env || R.lev.size() < 2 || comm_) return;
+  const int kn = knob(8);  // hypreve_SetKnob(8, 1 / -1) turns it on / off for this setup (tests)
+  if (!(kn > 0 || (kn == 0 && env)) || R.lev.size() < 2 || comm_) return;
   const RankLevel& L = R.lev[0];
   const DevLevel& D = lev_[0];
-  if (!D.A.in.slot_mask || D.A.bd.nrows || D.A.in.rowmap || D.R.bd.nrows || !L.A.map_int.empty() ||
-      !L.R.map_int.empty() || L.hv.n_halo || L.hu.n_halo)
-    return;
+  auto identity = [](const std::vector<int>& m, int n) {
+    if (m.empty()) return true;
+    if ((int)m.size() != n) return false;
+    for (int i = 0; i < n; ++i)
+      if (m[i] != i) return false;
+    return true;
+  };
+  const bool log = getenv("HVE_LAYOUT_LOG") != nullptr;
+  auto decline = [&](const char* why) {
+    if (log) fprintf(stderr, "[layout] no fused residual+restriction: %s\n", why);
+  };
+  if (!D.A.in.slot_mask) return decline("level 0's operator is not on the stencil layout");
+  if (D.A.bd.nrows || D.A.in.rowmap || D.R.bd.nrows || L.hv.n_halo || L.hu.n_halo)
+    return decline("level 0 is not a one-rank operator in natural order");
+  if (!identity(L.A.map_int, L.A.interior.nrows) || !identity(L.R.map_int, L.R.interior.nrows))
+    return decline("rows are not in natural order");
   const CSR& A = L.A.interior;
   const CSR& Rm = L.R.interior;
   int nx, ny, nz;
-  if (!fine_grid(A, &nx, &ny, &nz) || nx % kRRTx || (int)fc.size() != Rm.nrows) return;
+  if (!fine_grid(A, &nx, &ny, &nz) || nx % kRRTx || (int)fc.size() != Rm.nrows)
+    return decline("no grid with a multiple of 64 points a line");
   const int ty = kRRTy, zc = std::max(1, std::min(zc_env, nz));
   const int ntx = nx / kRRTx, nty = (ny + ty - 1) / ty, nzc = (nz + zc - 1) / zc;
   const int nb = ntx * nty * nz;
@@ -1110,13 +1127,17 @@ void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
       }
     }
   }
-  if (!ok) return;
+  if (!ok) return decline("a restriction row reaches beyond two points");
+  // the weights as a value table (16-bit codes: offset index << vbits | value
+  // index), or, with more than 4096 of them (the 27-point hierarchy), one f64
+  // per entry beside a code that is the offset index alone
   std::vector<unsigned short> vi16;
   std::vector<double> tab;
-  if (!build_value_table16(Rm.a, 4096, vi16, tab)) return;
-  int vbits = 1;
-  while ((1 << vbits) < (int)tab.size()) ++vbits;
-  if ((int)ocode.size() > (1 << (16 - vbits))) return;
+  const bool vt = build_value_table16(Rm.a, 4096, vi16, tab);
+  int vbits = 0;
+  if (vt)
+    while ((1 << vbits) < (int)tab.size()) ++vbits;
+  if ((int)ocode.size() > (1 << (16 - vbits))) return decline("codes do not fit 16 bits");
   // buckets: rows by (tile, plane), each bucket's rows by length, descending
   std::vector<int> bptr(nb + 1, 0);
   for (int c = 0; c < nc; ++c) bptr[bucket[c] + 1]++;
@@ -1142,9 +1163,10 @@ void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
     bent[b + 1] += bent[b];
     bcptr[b + 1] += bcptr[b];
   }
-  if (bent[nb] >= INT_MAX) return;
+  if (bent[nb] >= INT_MAX) return decline("too many entries");
   std::vector<int> bcnt(std::max(1, bcptr[nb]));
   std::vector<unsigned short> code((size_t)std::max<int64_t>(1, bent[nb]));
+  std::vector<double> bval(vt ? 0 : (size_t)std::max<int64_t>(1, bent[nb]));
   std::vector<unsigned short> blb(nc);
   std::vector<unsigned char> blen(nc);
   bool fits = true;
@@ -1172,11 +1194,17 @@ void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
       for (int k = 0; k < len; ++k) {
         const int kk = Rm.i[c] + k, j = Rm.j[kk];
         const int key = ((j / (nx * ny) - a / (nx * ny) + 2) * 5 + (j / nx) % ny - ya + 2) * 5 + j % nx - xa + 2;
-        code[(size_t)bent[b] + cnt[k] + (q - r0)] = (unsigned short)((okey[key] << vbits) | vi16[kk]);
+        const size_t e = (size_t)bent[b] + cnt[k] + (q - r0);
+        if (vt) {
+          code[e] = (unsigned short)((okey[key] << vbits) | vi16[kk]);
+        } else {
+          code[e] = (unsigned short)okey[key];
+          bval[e] = Rm.a[kk];
+        }
       }
     }
   }
-  if (!fits) return;
+  if (!fits) return decline("a restriction row longer than 255");
   std::vector<int> odz(ocode.size()), odxy(ocode.size());
   for (size_t o = 0; o < ocode.size(); ++o) {
     const int key = ocode[o], dx = key % 5 - 2, dy = (key / 5) % 5 - 2, dz = key / 25 - 2;
@@ -1197,15 +1225,20 @@ void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
   rr_.blb = dupload(blb.data(), std::max<size_t>(1, blb.size()));
   rr_.blen = dupload(blen.data(), std::max<size_t>(1, blen.size()));
   rr_.code = dupload(code.data(), code.size());
-  rr_.vtab = dupload(tab.data(), tab.size());
-  rr_.nvtab = (int)tab.size();
+  if (vt) {
+    rr_.vtab = dupload(tab.data(), tab.size());
+    rr_.nvtab = (int)tab.size();
+  } else {
+    rr_.bval = dupload(bval.data(), bval.size());
+  }
   rr_.odz = dupload(odz.data(), odz.size());
   rr_.odxy = dupload(odxy.data(), odxy.size());
   rr_.notab = (int)ocode.size();
   rr_.vbits = vbits;
   if (getenv("HVE_LAYOUT_LOG"))
     fprintf(stderr, "[layout] fused residual+restriction: grid %dx%dx%d, tiles %dx%d, %d-plane chunks, %d offsets, "
-            "%d values, %lld entries\n", nx, ny, nz, kRRTx, ty, zc, rr_.notab, rr_.nvtab, (long long)rr_.entries);
+            "%s, %lld entries\n", nx, ny, nz, kRRTx, ty, zc, rr_.notab, vt ? "16-bit value table" : "f64 values",
+            (long long)rr_.entries);
 }
 
 RRView DevAMG::rr_view() const {
@@ -1217,7 +1250,7 @@ RRView DevAMG::rr_view() const {
   v.ntx = rr_.ntx; v.nty = rr_.nty; v.nzc = rr_.nzc;
   v.bptr = rr_.bptr; v.bent = rr_.bent; v.bcptr = rr_.bcptr; v.bcnt = rr_.bcnt; v.brow = rr_.brow;
   v.blb = rr_.blb; v.blen = rr_.blen; v.code = rr_.code; v.vtabR = rr_.vtab; v.odz = rr_.odz; v.odxy = rr_.odxy;
-  v.nvtabR = rr_.nvtab; v.notab = rr_.notab; v.vbits = rr_.vbits;
+  v.nvtabR = rr_.nvtab; v.notab = rr_.notab; v.vbits = rr_.vbits; v.bval = rr_.bval;
   return v;
 }
 

@@ -191,7 +191,8 @@ struct DevRR {
   unsigned short* blb = nullptr;  // per bucket row: the anchor's LDS index in its plane
   unsigned char* blen = nullptr;  // per bucket row: entries
   unsigned short* code = nullptr;
-  double* vtab = nullptr;
+  double* vtab = nullptr;  // the weights (16-bit codes), or
+  double* bval = nullptr;  // one weight per entry (codes: the offset index alone)
   int* odz = nullptr;    // per offset index: dz
   int* odxy = nullptr;   // per offset index: dy * (kRRTx + 4) + dx
   int nvtab = 0, notab = 0, vbits = 0, nbuckets = 0;
