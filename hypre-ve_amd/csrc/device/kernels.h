@@ -119,7 +119,7 @@ struct RRView {
   const int* slot_vi = nullptr;
   const uint64_t* slot_mask = nullptr;
   const double* vtabA = nullptr;
-  int sw = 0;
+  int sw = 0, npat = 0;
   int nx = 0, ny = 0, nz = 0, ty = 0, zc = 0, ntx = 0, nty = 0, nzc = 0;
   const int* bptr = nullptr;
   const int* bent = nullptr;

@@ -955,14 +955,24 @@ template <bool ZG, bool VT>
 __global__ void __launch_bounds__(256) k_resid_restrict(RRArgs a) {
   constexpr int PX = kRRTx + 4, PY = kRRTy + 4, PL = PX * PY;
   constexpr int LPW = (PY + 3) / 4;  // lines of a plane per wave
-  constexpr int B = 8;
+  constexpr int B = 8;               // slots per batch
+  constexpr int KP = 16;             // restriction codes prefetched per row
   const RRView& p = a.v;
+  const int W = p.sw;
   extern __shared__ double sm[];
-  double* ring = sm;               // 6 planes of PL
-  double* vt = sm + 6 * PL;        // R_0's values
-  int* oz = reinterpret_cast<int*>(vt + p.nvtabR);
+  double* ring = sm;                                         // 6 planes of PL
+  double* vt = sm + 6 * PL;                                  // R_0's values
+  double* pva = vt + p.nvtabR;                               // A_0's slot values, per pattern slot
+  uint64_t* pmask = reinterpret_cast<uint64_t*>(pva + p.npat * W);
+  int* poff = reinterpret_cast<int*>(pmask + p.npat * W);
+  int* oz = poff + p.npat * W;
   int* oxy = oz + p.notab;
   for (int i = threadIdx.x; i < p.nvtabR; i += 256) vt[i] = p.vtabR[i];
+  for (int i = threadIdx.x; i < p.npat * W; i += 256) {
+    pva[i] = p.vtabA[p.slot_vi[i]];
+    pmask[i] = p.slot_mask[i];
+    poff[i] = p.slot_off[i];
+  }
   for (int i = threadIdx.x; i < p.notab; i += 256) {
     oz[i] = p.odz[i];
     oxy[i] = p.odxy[i];
@@ -973,90 +983,113 @@ __global__ void __launch_bounds__(256) k_resid_restrict(RRArgs a) {
   const int x0 = tx * kRRTx, y0 = tyi * kRRTy, z0 = zci * p.zc, z1 = min(p.nz, z0 + p.zc);
   const int ylo = max(0, y0 - 2), yhi = min(p.ny, y0 + kRRTy + 2);
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (kWave - 1);
-  const int W = p.sw;
   const unsigned vm = (1u << p.vbits) - 1u;
+  // margin points of a line: lanes 0, 1 take x0 - 2, x0 - 1; lanes 2, 3 take
+  // x0 + 64, x0 + 65 (in the neighbouring slices, patterns per lane)
+  const int mx = lane < 2 ? x0 - 2 + lane : x0 + kRRTx + (lane - 2);
+  const bool mlane = lane < 4 && mx >= 0 && mx < p.nx;
   __syncthreads();
   for (int z = max(0, z0 - 2); z < z1 + 2; ++z) {
+    const int zr = z - 2;
+    const bool rphase = zr >= z0 && zr < z1;
+    // this plane's restriction rows: the first row's codes go out now and land
+    // during the residual phase
+    int bk = 0, r0 = 0, r1 = 0, ent = 0, cbase = 0;
+    int len0 = 0, lb0 = 0, row0 = 0;
+    unsigned short c0[KP];
+    double w0[VT ? 1 : KP];
+    if (rphase) {
+      bk = (tyi * p.ntx + tx) * p.nz + zr;
+      r0 = p.bptr[bk];
+      r1 = p.bptr[bk + 1];
+      ent = p.bent[bk];
+      cbase = p.bcptr[bk];
+      const int q = r0 + (int)threadIdx.x;
+      if (q < r1) {
+        len0 = p.blen[q];
+        lb0 = p.blb[q];
+        row0 = p.brow[q];
+#pragma unroll
+        for (int k = 0; k < KP; ++k) {
+          const int e = k < len0 ? ent + p.bcnt[cbase + k] + (q - r0) : ent;
+          c0[k] = p.code[e];
+          if (!VT) w0[k] = p.bval[e];
+        }
+      }
+    }
     double* rp = ring + (z % 6) * PL;
     if (z < p.nz) {
-      // tile lines: one slice each, all lines of the wave in flight together
-      int row[LPW], pat[LPW];
+      // the wave's lines (one slice each) and their margin points, every load in flight together
+      int row[LPW], pat[LPW], mrow[LPW], mpat[LPW];
       bool on_line[LPW];
-      double t[LPW];
+      double t[LPW], tm[LPW];
 #pragma unroll
       for (int l = 0; l < LPW; ++l) {
         const int y = ylo + wave + 4 * l;
         on_line[l] = y < yhi;
-        row[l] = ((z * p.ny + (on_line[l] ? y : ylo)) * p.nx) + x0 + lane;
-        pat[l] = __builtin_amdgcn_readfirstlane(p.slice_pat[row[l] >> 6]);
+        const int base = (z * p.ny + (on_line[l] ? y : ylo)) * p.nx;
+        row[l] = base + x0 + lane;
+        pat[l] = __builtin_amdgcn_readfirstlane(p.slice_pat[(base + x0) >> 6]);
+        mrow[l] = base + (mlane ? mx : x0);
+        mpat[l] = p.slice_pat[mrow[l] >> 6];
         t[l] = a.b[row[l]];
+        tm[l] = a.b[mrow[l]];
       }
       for (int k = 0; k < W; k += B) {
 #pragma unroll
         for (int l = 0; l < LPW; ++l) {
-          const size_t sb = (size_t)pat[l] * W + k;
-          int off[B], vi[B];
-          uint32_t mlo[B], mhi[B];
+          bool on[B], mon[B];
+          double xv[B], xm[B];
 #pragma unroll
           for (int q = 0; q < B; ++q) {
-            off[q] = __builtin_amdgcn_readfirstlane(p.slot_off[sb + q]);
-            vi[q] = __builtin_amdgcn_readfirstlane(p.slot_vi[sb + q]);
-            const uint64_t m = p.slot_mask[sb + q];
-            mlo[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)m);
-            mhi[q] = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(m >> 32));
-          }
-          bool on[B];
-          double xv[B], av[B];
-#pragma unroll
-          for (int q = 0; q < B; ++q) {
-            const uint32_t mw = lane < 32 ? mlo[q] : mhi[q];
-            on[q] = ((k + q) < W) && (((mw >> (lane & 31)) & 1u) != 0);
-            xv[q] = a.x[on[q] ? row[l] + off[q] : row[l]];
+            const int sk = pat[l] * W + min(k + q, W - 1), mk = mpat[l] * W + min(k + q, W - 1);
+            on[q] = (k + q) < W && ((pmask[sk] >> lane) & 1ull);
+            mon[q] = (k + q) < W && mlane && ((pmask[mk] >> (mrow[l] & 63)) & 1ull);
+            xv[q] = a.x[on[q] ? row[l] + poff[sk] : row[l]];
+            xm[q] = a.x[mon[q] ? mrow[l] + poff[mk] : mrow[l]];
           }
 #pragma unroll
-          for (int q = 0; q < B; ++q) av[q] = p.vtabA[vi[q]];
-#pragma unroll
           for (int q = 0; q < B; ++q) {
-            const double tn = t[l] - av[q] * xv[q];
+            const int sk = pat[l] * W + min(k + q, W - 1), mk = mpat[l] * W + min(k + q, W - 1);
+            const double tn = t[l] - pva[sk] * xv[q];
             t[l] = on[q] ? tn : t[l];
+            const double mn = tm[l] - pva[mk] * xm[q];
+            tm[l] = mon[q] ? mn : tm[l];
           }
         }
       }
 #pragma unroll
-      for (int l = 0; l < LPW; ++l)
-        if (on_line[l]) rp[(ylo + wave + 4 * l - y0 + 2) * PX + lane + 2] = t[l];
-      // margin columns x0 - 2, x0 - 1, x0 + 64, x0 + 65 (the slice pattern per lane)
-      for (int q = threadIdx.x; q < 4 * (yhi - ylo); q += 256) {
-        const int y = ylo + q / 4, m = q % 4;
-        const int xx = m < 2 ? x0 - 2 + m : x0 + kRRTx + (m - 2);
-        if (xx < 0 || xx >= p.nx) continue;
-        const int r = (z * p.ny + y) * p.nx + xx;
-        const int pt = p.slice_pat[r >> 6], ln = r & 63;
-        double tt = a.b[r];
-        for (int k = 0; k < W; ++k) {
-          const size_t sk = (size_t)pt * W + k;
-          if ((p.slot_mask[sk] >> ln) & 1ull) tt -= p.vtabA[p.slot_vi[sk]] * a.x[r + p.slot_off[sk]];
-        }
-        rp[(y - y0 + 2) * PX + (xx - x0 + 2)] = tt;
+      for (int l = 0; l < LPW; ++l) {
+        if (!on_line[l]) continue;
+        const int yy = ylo + wave + 4 * l - y0 + 2;
+        rp[yy * PX + lane + 2] = t[l];
+        if (mlane) rp[yy * PX + (mx - x0 + 2)] = tm[l];
       }
     }
     __syncthreads();
-    const int zr = z - 2;
-    if (zr >= z0 && zr < z1) {
-      const int bk = (tyi * p.ntx + tx) * p.nz + zr;
-      const int r0 = p.bptr[bk], r1 = p.bptr[bk + 1], ent = p.bent[bk];
-      const int* __restrict__ cnt = p.bcnt + p.bcptr[bk];
+    if (rphase) {
       for (int q = r0 + (int)threadIdx.x; q < r1; q += 256) {
-        const int j = q - r0, len = p.blen[q], lb = p.blb[q];
+        const int j = q - r0;
+        const bool first = q == r0 + (int)threadIdx.x;
+        const int len = first ? len0 : p.blen[q], lb = first ? lb0 : p.blb[q];
         double t = 0.0;
         for (int k = 0; k < len; ++k) {
-          const int e = ent + cnt[k] + j;
-          const unsigned c = p.code[e];
+          int e = 0;
+          unsigned c;
+          double w;
+          if (first && k < KP) {
+            c = c0[k];
+            w = VT ? 0.0 : w0[k];
+          } else {
+            e = ent + p.bcnt[cbase + k] + j;
+            c = p.code[e];
+            w = VT ? 0.0 : p.bval[e];
+          }
           const int o = (int)(c >> p.vbits);
-          const double w = VT ? vt[c & vm] : p.bval[e];
+          if (VT) w = vt[c & vm];
           t += w * ring[((zr + oz[o]) % 6) * PL + lb + oxy[o]];
         }
-        const int row = p.brow[q];
+        const int row = first ? row0 : p.brow[q];
         a.Fc[row] = t;
         if (ZG) a.Uc[row] = 0.0 + t / a.l1c[row];
       }
@@ -1072,7 +1105,9 @@ hipError_t launch_resid_restrict(const RRView& V, const double* x, const double*
   a.v = V; a.x = x; a.b = b; a.Fc = Fc; a.Uc = Uc; a.l1c = l1c;
   const int nwg = V.ntx * V.nty * V.nzc;
   a.nblocks_pad = (nwg + 7) / 8 * 8;
-  const size_t lds = (size_t)6 * PL * sizeof(double) + (size_t)V.nvtabR * sizeof(double) + (size_t)2 * V.notab * sizeof(int);
+  const size_t lds = (size_t)6 * PL * sizeof(double) + (size_t)V.nvtabR * sizeof(double) +
+                     (size_t)V.npat * V.sw * (sizeof(double) + sizeof(uint64_t) + sizeof(int)) +
+                     (size_t)2 * V.notab * sizeof(int);
   if (lds > 160 * 1024) return hipErrorInvalidValue;
 #define HVE_RR(ZGV, VTV)                                                                              \
   {                                                                                                    \

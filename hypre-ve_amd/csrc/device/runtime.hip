@@ -1245,7 +1245,7 @@ RRView DevAMG::rr_view() const {
   const DevSell& A = lev_[0].A.in;
   RRView v;
   v.slice_pat = A.slice_pat; v.slot_off = A.slot_base; v.slot_vi = A.slot_vi; v.slot_mask = A.slot_mask;
-  v.vtabA = A.vtab; v.sw = A.stencil_w;
+  v.vtabA = A.vtab; v.sw = A.stencil_w; v.npat = A.npat;
   v.nx = rr_.nx; v.ny = rr_.ny; v.nz = rr_.nz; v.ty = rr_.ty; v.zc = rr_.zc;
   v.ntx = rr_.ntx; v.nty = rr_.nty; v.nzc = rr_.nzc;
   v.bptr = rr_.bptr; v.bent = rr_.bent; v.bcptr = rr_.bcptr; v.bcnt = rr_.bcnt; v.brow = rr_.brow;
