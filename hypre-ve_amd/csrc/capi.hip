@@ -1368,7 +1368,7 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE
   API_BEGIN
   const DevLevel& L = s->dev->level(level);
   const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
-  *kind = M.code32 ? 13 : M.code16 ? 12 : M.slot_mask ? 11
+  *kind = M.code32 ? 13 : M.code16 ? 12 : M.slot_mask ? (grid_stencil_on(M.view()) ? 14 : 11)
          : M.dcol ? (M.vidx16 ? 7 : M.vidx ? 6 : 5)
                  : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? (M.dict_ranges ? 10 : 4) : M.pw ? 3 : M.rowlen ? 1
                  : M.wide ? 2 : 0;

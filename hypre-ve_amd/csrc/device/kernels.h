@@ -4,6 +4,17 @@
 
 namespace hve {
 
+// Grid form of a stencil-layout slot (k_grid_stencil): lanes present, value,
+// and the neighbour as a plane step dz in {-1, 0, 1} and an in-plane step
+// dxy = dy * (64 + 2) + dx in the LDS tile.  32 B: one scalar load.
+struct GSlot {
+  uint64_t mask;
+  double val;
+  int dz, dxy, pad0, pad1;
+};
+// Lines of the x-tile a grid-stencil workgroup computes per plane (4 waves).
+constexpr int kGTy = 16;
+
 // Device view of one SELL-64 operator, padded or jagged (see kernels.hip).
 struct SellView {
   const int* slice_ptr = nullptr;  // nslices + 1 offsets (in entries)
@@ -58,6 +69,11 @@ struct SellView {
   // packed layout (k_sell_code PK; host: pack_sell_codes): per entry one 32-bit
   // code ((column - slot_base[slice]) << vbits | value index into vtab)
   const unsigned* code32 = nullptr;
+  // stencil layout over the points of a gnx x gny x gnz grid in natural order
+  // (k_grid_stencil: LDS x-tile, gzc planes per workgroup); gslot per
+  // (pattern, slot), nullptr = the per-slice loop
+  const GSlot* gslot = nullptr;
+  int gnx = 0, gny = 0, gnz = 0, gzc = 0;
 };
 
 enum : int {
@@ -144,11 +160,14 @@ int sell_batch_override();
 // step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU,
 // 3 stream-mix access width (2: 16 B), 7 caps the device setup's LDS tables
 // at 2^v slots (tests of its host fallback), 8 the fused level-0 residual +
-// restriction at the next Setup (1 on, -1 off, 0 HVE_FUSE_RR).
+// restriction at the next Setup (1 on, -1 off, 0 HVE_FUSE_RR), 9 the planes a
+// grid-stencil workgroup marches (k_grid_stencil) at the next Setup.
 void set_knob(int id, int v);
 int knob(int id);
 int stencil_slices_per_wave();
 int stencil_grid(int nrows);
+bool grid_stencil_on(const SellView& M);
+int grid_stencil_blocks(const SellView& M);
 bool stencil_wave_map();
 int sell_pipe_override();
 bool sell_nt();

@@ -100,6 +100,8 @@ struct SpArgs {
   double w;                       // relax weight / alpha
   double temp;                    // beta/alpha for OP_GENERAL
   int relax_points;
+  const GSlot* __restrict__ gslot;           // grid stencil (k_grid_stencil)
+  int gnx, gny, gnz, gzc;
 };
 
 // Logical workgroup block -> stored row block (SpArgs::blk_map): the
@@ -128,6 +130,17 @@ template <bool NT, typename T>
 __device__ __forceinline__ void sstore(T* p, T v) {
   if (NT) __builtin_nontemporal_store(v, p);
   else *p = v;
+}
+
+// Raw buffer loads (32-bit byte offsets; an offset past `bytes` reads 0).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gs_rsrc(const void* base, unsigned bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ double gs_ld64(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+__device__ __forceinline__ int gs_ld32(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
 }
 
 // Value streams of the row loops: 8-byte values (ValF64) or 16-bit indices
@@ -788,6 +801,244 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
   if ((OP == OP_RESID_L1JAC || OP == OP_MATVEC) && p.nrm) {
     // one partial per wave, in a fixed order (no workgroup barrier: these
     // workgroups are short-lived and a barrier at their end holds them resident)
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if (lane == 0) p.nrm[blockIdx.x * 4 + (threadIdx.x >> 6)] = acc;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Grid stencil loop with an LDS x-tile, for an operator on the stencil layout
+// whose rows are the points of a gnx x gny x gnz grid in natural order (gnx a
+// multiple of 64) and whose slots reach at most one point in each direction
+// (7- and 27-point stencils; host check: DevSell::build_grid).  A workgroup
+// owns 64 x kGTy points in (x, y) and marches gzc planes in z, keeping planes
+// z-1, z, z+1 of its tile plus a one-point margin in a 4-plane LDS ring: each
+// x value leaves memory once per tile in coalesced 512-B lines instead of once
+// per slot, and plane z+2's loads (and plane z+1's right-hand side) are in
+// flight while plane z is computed.  One barrier a plane.  A row adds its
+// present slots in slot order with k_sell_stencil's rounding: bitwise the same.
+// ---------------------------------------------------------------------------
+// Starting value of a row sum (row_init) for the grid loop, from the loaded b.
+template <int OP>
+__device__ __forceinline__ double grid_init(double bv, double alpha, double temp) {
+  if (OP == OP_RESID || OP == OP_L1JAC || OP == OP_RESID_L1JAC) return bv;
+  if (OP == OP_L1JAC_W) return -bv;
+  if (OP == OP_GENERAL) {
+    const bool neg = (alpha == -1.0);
+    if (temp == 0.0) return 0.0;
+    if (temp == -1.0) return neg ? bv : -bv;
+    if (temp == 1.0) return neg ? -bv : bv;
+    return neg ? -bv * temp : bv * temp;
+  }
+  return 0.0;
+}
+
+// NL lines of one plane sharing the slot pattern `pat`: the slot data is read
+// once (scalar) for all of them and their sums run as NL independent chains.
+// lrow: LDS position of the first line's row (lane), g: its row; the lines
+// are PX apart in LDS and nx apart in the vectors.
+template <int OP, bool NT, int NL>
+__device__ __forceinline__ void grid_lines(const GSlot* __restrict__ gslot, int pat, int W, const double* ring,
+                                           int b0, int b1, int b2, int lrow, int g, int nx, const double* t0,
+                                           const double* l1v, double* __restrict__ y, double* __restrict__ y2,
+                                           bool want_nrm, double w, bool sub, bool fly, double& acc) {
+  constexpr int B = 4;  // slots per batch
+  constexpr int PX = kWave + 2;
+  constexpr bool SMOOTH = OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC;
+  const int lane = threadIdx.x & (kWave - 1);
+  using cgs = const __attribute__((address_space(4))) GSlot;  // scalar cache, read-only
+  cgs* sp = (cgs*)(gslot + (size_t)pat * W);
+  double t[NL];
+#pragma unroll
+  for (int i = 0; i < NL; ++i) t[i] = t0[i];
+  double s1 = 0.0;
+  bool neg = false, seen = false;
+  for (int k = 0; k < W; k += B) {
+    bool on[B];
+    double a[B], xv[B][NL];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      cgs& gs = sp[k + q];  // (the table has a tail past the last pattern)
+      const uint64_t m = gs.mask;
+      const int dz = gs.dz, dxy = gs.dxy;
+      a[q] = gs.val;
+      const uint32_t mw = lane < 32 ? (uint32_t)m : (uint32_t)(m >> 32);
+      on[q] = ((k + q) < W) & (((mw >> (lane & 31)) & 1u) != 0);
+      const int pb = (dz < 0 ? b0 : (dz > 0 ? b2 : b1)) + dxy;
+#pragma unroll
+      for (int i = 0; i < NL; ++i) xv[q][i] = ring[pb + lrow + i * PX];
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q)
+#pragma unroll
+      for (int i = 0; i < NL; ++i) {
+        const double pr = a[q] * xv[q][i];
+        const double tn = sub ? t[i] - pr : t[i] + pr;
+        t[i] = on[q] ? tn : t[i];
+      }
+    if (fly) {
+#pragma unroll
+      for (int q = 0; q < B; ++q) {
+        if (on[q] && !seen) { neg = a[q] < 0.0; seen = true; }
+        s1 = on[q] ? s1 + fabs(a[q]) : s1;
+      }
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NL; ++i) {
+    const int gi = g + i * nx;
+    const double xg = (SMOOTH || OP == OP_MATVEC) ? ring[b1 + lrow + i * PX] : 0.0;
+    const double l1g = fly ? (neg ? -s1 : s1) : l1v[i];
+    if (OP == OP_RESID_L1JAC) {
+      if (y) sstore<NT>(y + gi, t[i]);
+      if (want_nrm) acc += t[i] * t[i];
+      sstore<NT>(y2 + gi, xg + t[i] / l1g);
+    } else if (OP == OP_L1JAC) {
+      sstore<NT>(y + gi, xg + t[i] / l1g);
+    } else if (OP == OP_L1JAC_W) {
+      const double v = (-w) * t[i];
+      sstore<NT>(y + gi, xg + v / l1g);
+    } else if (OP == OP_GENERAL) {
+      sstore<NT>(y + gi, (w == 1.0 || w == -1.0) ? t[i] : w * t[i]);
+    } else {  // OP_RESID, OP_MATVEC
+      if (OP == OP_MATVEC && want_nrm) acc += xg * t[i];
+      sstore<NT>(y + gi, t[i]);
+    }
+  }
+}
+
+template <int OP, bool NT>
+__global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
+  constexpr int PX = kWave + 2, PY = kGTy + 2, PL = PX * PY;
+  constexpr int LPW = kGTy / 4;    // lines of a plane per wave
+  static_assert(LPW == 4, "the shared-pattern test below reads four lines");
+  constexpr int JL = (PY + 3) / 4; // tile lines (margin included) loaded per wave
+  constexpr bool SMOOTH = OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC;
+  __shared__ double ring[4 * PL];
+  const double* __restrict__ xp = p.x;
+  const double* __restrict__ bp = p.b;
+  const double* __restrict__ l1p = p.l1;
+  using cint = const __attribute__((address_space(4))) int;  // slice patterns: scalar cache
+  cint* const spat = (cint*)p.slice_pat;
+  const int nx = p.gnx, ny = p.gny, nz = p.gnz, zc = p.gzc, W = p.sw;
+  const int ntx = nx >> 6, nty = (ny + kGTy - 1) / kGTy;
+  const int ntiles = ntx * nty * ((nz + zc - 1) / zc);
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int lane = threadIdx.x & (kWave - 1);
+  const bool sub = op_subtracts<OP>() || (OP == OP_GENERAL && p.w == -1.0);
+  const bool fly = SMOOTH && l1p == nullptr;
+  const bool want_nrm = p.nrm != nullptr;
+  double acc = 0.0;
+  if (lb < ntiles) {
+    const int tx = lb % ntx, tyi = (lb / ntx) % nty, zci = lb / (ntx * nty);
+    const int x0 = tx * kWave, y0 = tyi * kGTy, z0 = zci * zc, z1 = min(nz, z0 + zc);
+    const int yw = y0 + wave * LPW;  // the wave's first line
+    // plane loads: tile line wave + 4j (y0 - 1 + that), its 64 points by lane;
+    // the margin points (x0 - 1, x0 + 64) of line t / 2 by the first 2 PY
+    // threads.  Points outside the grid read zeros: buffer loads whose offset
+    // is past the vector (unconditional, no branches around the loads).
+    const unsigned nb8 = (unsigned)p.nrows * 8u;
+    const auto rx = gs_rsrc(xp, nb8);
+    const auto rb = gs_rsrc((OP == OP_MATVEC || !bp) ? xp : bp, nb8);
+    const auto rl = gs_rsrc((SMOOTH && !fly) ? l1p : xp, nb8);
+    constexpr int kOut = (int)0xFFFFFFF0u;
+    const int mt = threadIdx.x, mli = mt >> 1;
+    const int mx = (mt & 1) ? x0 + kWave : x0 - 1;
+    const bool mlane = mt < 2 * PY && mx >= 0 && mx < nx && y0 - 1 + mli >= 0 && y0 - 1 + mli < ny;
+    int loff[JL];
+    bool lok[JL];
+#pragma unroll
+    for (int j = 0; j < JL; ++j) {
+      const int li = wave + 4 * j, yy = y0 - 1 + li;
+      lok[j] = li < PY && yy >= 0 && yy < ny;
+      loff[j] = (lok[j] ? yy : 0) * nx + x0 + lane;
+    }
+    const int moff = mlane ? (y0 - 1 + mli) * nx + mx : 0;
+#define HVE_GRID_LD(zz, V, VM)                                                        \
+    {                                                                                 \
+      const int zq = (zz);                                                            \
+      const bool zin = zq >= 0 && zq < nz;                                            \
+      const int zb = zq * nx * ny;                                                    \
+      _Pragma("unroll") for (int j = 0; j < JL; ++j)                                  \
+        V[j] = gs_ld64(rx, (zin && lok[j]) ? (int)((unsigned)(zb + loff[j]) * 8u) : kOut); \
+      VM = gs_ld64(rx, (zin && mlane) ? (int)((unsigned)(zb + moff) * 8u) : kOut);    \
+    }
+#define HVE_GRID_ST(zz, V, VM)                                               \
+    {                                                                        \
+      double* r = ring + ((zz) & 3) * PL;                                    \
+      _Pragma("unroll") for (int j = 0; j < JL; ++j) {                       \
+        const int li = wave + 4 * j;                                         \
+        if (li < PY) r[li * PX + 1 + lane] = V[j];                           \
+      }                                                                      \
+      if (mt < 2 * PY) r[mli * PX + ((mt & 1) ? PX - 1 : 0)] = VM;           \
+    }
+    // the right-hand side (row_init), l1 and slot pattern of the wave's lines
+    // of plane zz (nothing past z1)
+    double t0[LPW], l1v[LPW];
+    int pat[LPW];
+#define HVE_GRID_ROWS(zz, TT, LL, PP)                                                  \
+    {                                                                                  \
+      const int zq = (zz);                                                             \
+      _Pragma("unroll") for (int l = 0; l < LPW; ++l) {                                \
+        const bool ok = zq < z1 && yw + l < ny;                                        \
+        const int base = ok ? (zq * ny + yw + l) * nx + x0 : 0;                        \
+        const int bo = ok ? (int)((unsigned)(base + lane) * 8u) : kOut;                \
+        TT[l] = OP == OP_MATVEC ? 0.0 : grid_init<OP>(gs_ld64(rb, bo), p.w, p.temp);   \
+        LL[l] = (SMOOTH && !fly) ? gs_ld64(rl, bo) : 1.0;                              \
+        PP[l] = spat[base >> 6];                                                       \
+      }                                                                                \
+    }
+    HVE_GRID_ROWS(z0, t0, l1v, pat)
+    {
+      double v0[JL], v1[JL], v2[JL], m0, m1, m2;
+      HVE_GRID_LD(z0 - 1, v0, m0)
+      HVE_GRID_LD(z0, v1, m1)
+      HVE_GRID_LD(z0 + 1, v2, m2)
+      HVE_GRID_ST(z0 - 1, v0, m0)
+      HVE_GRID_ST(z0, v1, m1)
+      HVE_GRID_ST(z0 + 1, v2, m2)
+    }
+    __syncthreads();
+    for (int z = z0; z < z1; ++z) {
+      // the next plane's rows first, then plane z+2: waiting for the plane
+      // (before its LDS store) then leaves no row load in flight across the
+      // barrier, so plane z's sums wait for nothing issued in this iteration
+      double nt0[LPW], nl1[LPW];
+      int npt[LPW];
+      HVE_GRID_ROWS(z + 1, nt0, nl1, npt)
+      double nv[JL], nvm;
+      HVE_GRID_LD(z + 2, nv, nvm)
+      const int b0 = ((z - 1) & 3) * PL, b1 = (z & 3) * PL, b2 = ((z + 1) & 3) * PL;
+      const int lrow = (wave * LPW + 1) * PX + 1 + lane;
+      const int g = (z * ny + yw) * nx + x0 + lane;
+      // the wave's lines share a pattern away from the y faces of the grid
+      if (yw + LPW <= ny && pat[0] == pat[1] && pat[1] == pat[2] && pat[2] == pat[3]) {
+        grid_lines<OP, NT, LPW>(p.gslot, pat[0], W, ring, b0, b1, b2, lrow, g, nx, t0, l1v, p.y, p.y2, want_nrm,
+                                p.w, sub, fly, acc);
+      } else {
+#pragma unroll
+        for (int l = 0; l < LPW; ++l)
+          if (yw + l < ny)
+            grid_lines<OP, NT, 1>(p.gslot, pat[l], W, ring, b0, b1, b2, lrow + l * PX, g + l * nx, nx, t0 + l,
+                                  l1v + l, p.y, p.y2, want_nrm, p.w, sub, fly, acc);
+      }
+      // plane z+2 goes into the slot plane z-2 had: every wave finished with it
+      // before the previous barrier
+      HVE_GRID_ST(z + 2, nv, nvm)
+#pragma unroll
+      for (int l = 0; l < LPW; ++l) {
+        t0[l] = nt0[l];
+        l1v[l] = nl1[l];
+        pat[l] = npt[l];
+      }
+      __syncthreads();
+    }
+#undef HVE_GRID_LD
+#undef HVE_GRID_ST
+#undef HVE_GRID_ROWS
+  }
+  if ((OP == OP_RESID_L1JAC || OP == OP_MATVEC) && want_nrm) {
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
     if (lane == 0) p.nrm[blockIdx.x * 4 + (threadIdx.x >> 6)] = acc;
   }
@@ -1499,16 +1750,6 @@ static_assert(2 * kGsBatch - 1 <= kGsFence && kGsFence < kGsRing, "ring reach");
 // Buffer loads with 32-bit offsets from wave-uniform bases: no 64-bit address
 // arithmetic in VGPRs (whose register reuse otherwise made the compiler wait
 // for every load in flight before a step's first entry load).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t gs_rsrc(const void* base, unsigned bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, (int)bytes, 0x00020000);
-}
-__device__ __forceinline__ double gs_ld64(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
-}
-__device__ __forceinline__ int gs_ld32(__amdgpu_buffer_rsrc_t r, int off) {
-  return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
-}
-
 __device__ __forceinline__ void gs_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -1997,6 +2238,26 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_D
     return hipGetLastError();
   }
+  a.gslot = M.gslot;
+  a.gnx = M.gnx; a.gny = M.gny; a.gnz = M.gnz; a.gzc = M.gzc;
+  if (M.slot_mask && grid_stencil_on(M) && !cfsel &&
+      (op == OP_RESID || op == OP_MATVEC || op == OP_L1JAC || op == OP_L1JAC_W || op == OP_RESID_L1JAC ||
+       op == OP_GENERAL)) {
+    a.sw = M.stencil_w;
+    a.slice_pat = M.slice_pat;
+    const dim3 ggrid(grid_stencil_blocks(M));
+#define HVE_G(OPV)                                                                         \
+  case OPV:                                                                                \
+    if (nt) hipLaunchKernelGGL((k_grid_stencil<OPV, true>), ggrid, block, 0, s, a);       \
+    else hipLaunchKernelGGL((k_grid_stencil<OPV, false>), ggrid, block, 0, s, a);         \
+    break;
+    switch (op) {
+      HVE_G(OP_RESID) HVE_G(OP_MATVEC) HVE_G(OP_L1JAC) HVE_G(OP_L1JAC_W) HVE_G(OP_RESID_L1JAC) HVE_G(OP_GENERAL)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_G
+    return hipGetLastError();
+  }
   if (M.slot_mask) {  // slot-uniform stencil: R slices per wave, 4R per workgroup
     const int R = stencil_slices_per_wave();
     a.sw = M.stencil_w;
@@ -2411,7 +2672,22 @@ int stencil_grid(int nrows) {
   const int nlb = ((std::max(nrows, 1) + 63) / 64 + 4 * R - 1) / (4 * R);
   return std::max(8, (nlb + 7) / 8 * 8);
 }
+// Grid stencil loop (k_grid_stencil) wherever the layout has its grid form;
+// HVE_GRID_STENCIL=0 keeps the per-slice loop.
+bool grid_stencil_on(const SellView& M) {
+  static const bool v = [] {
+    const char* e = getenv("HVE_GRID_STENCIL");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v && M.gslot != nullptr && M.gnx > 0 && M.gzc > 0;
+}
+// One workgroup per (x, y) tile and chunk of gzc planes, whole XCD rounds.
+int grid_stencil_blocks(const SellView& M) {
+  const int nt = (M.gnx / kWave) * ((M.gny + kGTy - 1) / kGTy) * ((M.gnz + M.gzc - 1) / M.gzc);
+  return std::max(8, (nt + 7) / 8 * 8);
+}
 int sell_nrm_parts(const SellView& M) {
+  if (M.slot_mask && grid_stencil_on(M)) return 4 * grid_stencil_blocks(M);  // one per wave
   if (M.slot_mask) return 4 * stencil_grid(M.nrows);  // one per wave
   const int nb = blocks_pad8(std::max(M.nrows, 1));
   return M.vidx16 ? std::min(nb, 2048) : nb;

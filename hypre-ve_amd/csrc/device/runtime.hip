@@ -94,6 +94,68 @@ void DevSell::build_wave_map() {
   nwave = nb * 4;
 }
 
+static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz);
+
+// Grid form of the stencil layout (k_grid_stencil) when the operator's rows
+// are the points of a grid in natural order with 64 | nx: every used slot
+// offset is dz * nx * ny + dy * nx + dx with steps of at most one point, and
+// no present lane's neighbour leaves the grid (so none wraps into another
+// line or plane: the tile position of row + offset is the neighbour's).
+// HVE_GRID_ZC (or knob 9, tests) sets the planes per workgroup (default:
+// about 2048 workgroups).
+bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::vector<int>& svi,
+                         const std::vector<uint64_t>& sm, const std::vector<double>& tab) {
+  int nx, ny, nz;
+  if (A.ncols != A.nrows || !fine_grid(A, &nx, &ny, &nz)) return false;
+  if (nx % 64 || ny < 3 || nz < 3 || (int64_t)nx * ny * nz != A.nrows) return false;
+  const int W = stencil_w;
+  const int64_t P = (int64_t)nx * ny;
+  std::vector<GSlot> gs((size_t)npat * W + 16);
+  for (auto& g : gs) g = GSlot{0, 0.0, 0, 0, 0, 0};
+  for (int pt = 0; pt < npat; ++pt)
+    for (int k = 0; k < W; ++k) {
+      const size_t e = (size_t)pt * W + k;
+      if (!sm[e]) continue;
+      bool found = false;
+      for (int dz = -1; dz <= 1 && !found; ++dz)
+        for (int dy = -1; dy <= 1 && !found; ++dy)
+          for (int dx = -1; dx <= 1 && !found; ++dx)
+            if (dz * P + (int64_t)dy * nx + dx == so[e]) {
+              gs[e] = GSlot{sm[e], tab[svi[e]], dz, dy * (64 + 2) + dx, 0, 0};
+              found = true;
+            }
+      if (!found) return false;
+    }
+  int ok = 1;
+#pragma omp parallel for schedule(static) reduction(min : ok)
+  for (int s = 0; s < nslices; ++s) {
+    const int r0 = s * 64, x0 = r0 % nx, y = (int)((r0 / nx) % ny), z = (int)(r0 / P);
+    const int pt = pat_host[s];
+    for (int k = 0; k < W; ++k) {
+      const GSlot& g = gs[(size_t)pt * W + k];
+      if (!g.mask) continue;
+      const int dx = ((g.dxy + 67) % 66) - 1, dy = (g.dxy - dx) / 66;
+      if (z + g.dz < 0 || z + g.dz >= nz || y + dy < 0 || y + dy >= ny) ok = 0;
+      if (dx < 0 && x0 == 0 && (g.mask & 1ull)) ok = 0;
+      if (dx > 0 && x0 + 64 == nx && (g.mask >> 63)) ok = 0;
+    }
+  }
+  if (!ok) return false;
+  static const int zc_env = [] {
+    const char* e = getenv("HVE_GRID_ZC");
+    return e ? atoi(e) : 0;
+  }();
+  const int64_t txy = (int64_t)(nx / 64) * ((ny + kGTy - 1) / kGTy);
+  const int zc = knob(9) > 0 ? knob(9) : zc_env > 0 ? zc_env
+               : (int)std::max<int64_t>(2, std::min<int64_t>(64, nz * txy / 2048));
+  gslot = dupload(gs.data(), gs.size());
+  gnx = nx; gny = ny; gnz = nz; gzc = std::min(zc, nz);
+  if (getenv("HVE_LAYOUT_LOG"))
+    fprintf(stderr, "[layout] grid stencil %dx%dx%d, %d planes a workgroup, %d workgroups\n", nx, ny, nz, gzc,
+            grid_stencil_blocks(view()));
+  return true;
+}
+
 // Packed SELL-64 entries (k_sell_code PK): code = ((col - base[slice]) << vbits)
 // | value index, base = the slice's smallest column, padding 0xFFFFFFFF.  false
 // when some slice's column span does not fit 32 - vbits bits (all-ones span
@@ -309,6 +371,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
         for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
         if (!ident) rowmap = dupload(rowmap_h.data(), rowmap_h.size());
       }
+      if (!rowmap) build_grid(A, so, svi, sm, tab);
       stored_map = rowmap_h;
       if (key) set_block_order(rowmap_h, *key);
       if (!wave_map) build_wave_map();
@@ -653,6 +716,9 @@ void DevSell::release() {
     if (q) (void)hipFree(q);
   code16 = nullptr; otab = nullptr; anc = nullptr; cmap = nullptr;
   notab = vbits = 0; anc_n = cmap_n = 0;
+  if (gslot) (void)hipFree(gslot);
+  gslot = nullptr;
+  gnx = gny = gnz = gzc = 0;
 }
 
 // Team size of the packed schedule: about this many rows per step.  A wide

@@ -73,6 +73,11 @@ struct DevSell {
   // packed layout (SellView::code32): one 32-bit code per slot, the slice
   // bases in slot_base, the values in vtab
   unsigned* code32 = nullptr;
+  // stencil layout over a grid in natural order (SellView::gslot, k_grid_stencil)
+  GSlot* gslot = nullptr;
+  int gnx = 0, gny = 0, gnz = 0, gzc = 0;
+  bool build_grid(const CSR& A, const std::vector<int>& so, const std::vector<int>& svi,
+                  const std::vector<uint64_t>& sm, const std::vector<double>& tab);
   // the operator is also applied by the residual and smoother ops (a level's
   // A), whose kernels do not take the 16-bit value-table dictionary layout;
   // configuration, kept across release()
@@ -86,6 +91,7 @@ struct DevSell {
     v.blk_map = blk_map; v.nblk = nblk; v.wave_map = wave_map; v.nwave = nwave;
     v.code16 = code16; v.otab = otab; v.notab = notab; v.vbits = vbits; v.anc = anc; v.cmap = cmap;
     v.code32 = code32;
+    v.gslot = gslot; v.gnx = gnx; v.gny = gny; v.gnz = gnz; v.gzc = gzc;
     return v;
   }
   // Grid context of an interpolation / restriction operator for the

@@ -345,7 +345,8 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver solver, HYPRE_Real *byte
  * 4 dictionary, 5 16-bit column deltas, 6 deltas + 8-bit value table,
  * 7 deltas + 16-bit value table, 8 padded + 16-bit value table, 9 jagged +
  * 16-bit value table, 10 range dictionary, 11 slot-uniform stencil,
- * 12 offset-coded (P, R), 13 packed 32-bit codes (P, R). */
+ * 12 offset-coded (P, R), 13 packed 32-bit codes (P, R), 14 slot-uniform
+ * stencil over a grid in natural order (k_grid_stencil: LDS x-tile). */
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int *kind);
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */

@@ -450,3 +450,55 @@ def test_fused_resid_restrict_bitwise(gpu, orc, gen, n3, relax):
     xo = np.zeros(n)
     O.solve(f_h, xo, 0.0, 3)
     assert np.array_equal(x.get(), xo)
+
+
+# grids with 64 | nx and from 2^18 rows up (the stencil layout); ny and nz not
+# multiples of the tile (16 lines) or of the planes a workgroup marches
+@pytest.mark.parametrize("gen,n3,relax,wt,zc", [("7", (64, 64, 64), 18, 1.0, 0), ("27", (64, 66, 64), 18, 1.0, 7),
+                                                ("aniso", (128, 40, 52), 18, 1.0, 0), ("7", (192, 50, 30), 18, 0.8, 5),
+                                                ("27", (128, 37, 60), 0, 1.0, 0), ("7", (64, 64, 70), 13, 1.0, 64)])
+def test_grid_stencil_bitwise(gpu, orc, gen, n3, relax, wt, zc):
+    """The grid-stencil loop (k_grid_stencil: x staged in an LDS ring of tile
+    planes) on level 0: a V-cycle from a random iterate and a 3-iteration
+    solve (the fused residual + first sweep, its norm) equal the oracle bit
+    for bit with l1-Jacobi (weight 1 and 0.8), Jacobi and hybrid GS, and the
+    layout is really the grid form.  zc: planes a workgroup marches (knob 9;
+    0 = automatic)."""
+    hv = gpu
+    if gen == "27":
+        A = hv.ParCSRMatrix.laplacian27(*n3)
+    elif gen == "aniso":
+        A = hv.ParCSRMatrix.laplacian(*n3, cx=0.001, cy=1.0, cz=1.0)
+    else:
+        A = hv.ParCSRMatrix.laplacian(*n3)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, relax_type=relax, relax_wt=wt, P_max_elmts=4)
+    amg = hv.BoomerAMG(**kw)
+    hv.set_knob(9, zc)
+    try:
+        amg.setup(A)
+    finally:
+        hv.set_knob(9, 0)
+    assert amg.level_layout(0, 0) == "grid-stencil"
+    O = orc.OracleAMG(amg)
+    n = A.n
+    rng = np.random.default_rng(29)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+    amg.set(tol=0.0, max_iter=3)
+    x = hv.ParVector(n, np.zeros(n))
+    it, rr = amg.solve(A, f, x)
+    xo = np.zeros(n)
+    st = O.solve(f_h, xo, 0.0, 3)
+    assert np.array_equal(x.get(), xo)
+    assert abs(rr - st["rel_res"]) <= RTOL_NORM * st["rel_res"]
+    for alpha, beta in [(1.0, 0.0), (-1.0, 1.0), (2.5, 0.5)]:
+        xv, yv = hv.ParVector(n, u0), hv.ParVector(n, f_h)
+        A.matvec(alpha, xv, beta, yv)
+        assert np.array_equal(yv.get(), O.matvec(0, alpha, u0, beta, f_h)), (alpha, beta)
