@@ -1433,7 +1433,7 @@ HYPRE_Int hypreve_BoomerAMGGetFusedResidRestrict(HYPRE_Solver s, HYPRE_Int* on) 
   CHECK_ARG(s && s->kind == KIND_AMG && s->dev, 1);
   CHECK_ARG(on, 2);
   API_BEGIN
-  *on = s->dev->fused_rr() ? 1 : 0;
+  *on = s->dev->fused_rr();
   API_END
 }
 
@@ -1581,12 +1581,18 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
   HVE_HIP(launch_set(D.ws_n(), 0.0, y, st));
   // which 3: A as the l1-Jacobi sweep, with b standing in for the l1 norms
   const double* l1 = which == 3 ? b : nullptr;
-  for (int w = 0; w < 3; ++w) HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, y, -1.0, 0.0, st));
+  // R_0 as the cycle runs it: the tiled restriction where it is built
+  const bool tiled = which == 2 && level == 0 && D.fused_rr() == 2;
+  auto launch = [&] {
+    if (tiled) HVE_HIP(launch_tile_restrict(D.rr_view(), D.rr_fine_rows(), x, y, nullptr, nullptr, st));
+    else HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, y, -1.0, 0.0, st));
+  };
+  for (int w = 0; w < 3; ++w) launch();
   hipEvent_t e0, e1;
   HVE_HIP(hipEventCreate(&e0));
   HVE_HIP(hipEventCreate(&e1));
   HVE_HIP(hipEventRecord(e0, st));
-  for (int r = 0; r < reps; ++r) HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, y, -1.0, 0.0, st));
+  for (int r = 0; r < reps; ++r) launch();
   HVE_HIP(hipEventRecord(e1, st));
   HVE_HIP(hipEventSynchronize(e1));
   float ms = 0.f;
@@ -1623,6 +1629,7 @@ HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver s, HYPRE_Int level, HYPRE
   // b read + y write / y rw / y write / f, u_g, l1 read + u' write
   const double out_rw = which == 0 ? 16.0 : which == 1 ? 16.0 : which == 2 ? 8.0 : 32.0;
   *bytes = (double)M.bytes() + (double)M.nrows * out_rw + (double)M.ncols * 8.0;
+  if (which == 2 && level == 0 && s->dev->fused_rr() == 2) *bytes = s->dev->rr_tile_bytes(L.R.nrows_local);
   API_END
 }
 

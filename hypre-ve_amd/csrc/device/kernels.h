@@ -150,18 +150,25 @@ struct RRView {
   const int* odz = nullptr;
   const int* odxy = nullptr;
   int nvtabR = 0, notab = 0, vbits = 0;
+  int64_t entries = 0;  // restriction entries (codes)
 };
 // Fc = R_0 (b - A_0 x) without storing the residual; with l1c, also
 // Uc = 0 + Fc / l1c (the coarse zero-guess l1-Jacobi sweep, OP_RESTRICT_ZG).
 hipError_t launch_resid_restrict(const RRView& V, const double* x, const double* b, double* Fc, double* Uc,
                                  const double* l1c, hipStream_t st);
+// Fc = R_0 r over the same tiles, r (nfine doubles) read from memory into an
+// LDS ring of planes; with l1c, also Uc = 0 + Fc / l1c.
+hipError_t launch_tile_restrict(const RRView& V, int nfine, const double* r, double* Fc, double* Uc,
+                                const double* l1c, hipStream_t st);
 int sell_batch_override();
 // Tuning knobs read at launch (0 = default): 0 offset-coded row blocks per
 // step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU,
 // 3 stream-mix access width (2: 16 B), 7 caps the device setup's LDS tables
 // at 2^v slots (tests of its host fallback), 8 the fused level-0 residual +
 // restriction at the next Setup (1 on, -1 off, 0 HVE_FUSE_RR), 9 the planes a
-// grid-stencil workgroup marches (k_grid_stencil) at the next Setup.
+// grid-stencil workgroup marches (k_grid_stencil) at the next Setup, 10 the
+// tiled level-0 restriction (k_tile_restrict) at the next Setup (1 on, -1
+// off, 0 HVE_TILE_R, default off).
 void set_knob(int id, int v);
 int knob(int id);
 int stencil_slices_per_wave();

@@ -1128,12 +1128,15 @@ static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz) {
   return false;
 }
 
-// Level 0's fused residual + restriction (DevRR), when level 0 is a grid
-// operator on the stencil layout held by one rank and every R_0 row reaches
-// at most two points from its coarse point's fine point in each direction.
-// fc: the fine point of each coarse point.  HVE_FUSE_RR=1 turns it on (off by
-// default: first measurement 8.35 ms at 512^3 against 0.90 + 1.63 unfused,
-// each plane a chain of dependent loads).
+// Level 0's fused residual + restriction (DevRR mode 1) or tiled restriction
+// (mode 2, k_tile_restrict), when level 0 is a grid operator on the stencil
+// layout held by one rank and every R_0 row reaches at most two points from
+// its coarse point's fine point in each direction.  Both off by default:
+// measured at 512^3 the tiled restriction took 3.46 ms against 1.59 for the
+// offset-coded rows (each bucket round waits on its code loads; 2 workgroups
+// a CU), the fused kernel 8.35 ms (HVE_TILE_R=1 / knob 10, HVE_FUSE_RR=1 /
+// knob 8 turn them on; profiles/r04/07_tile_restrict).
+// fc: the fine point of each coarse point.
 void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
   static const int env = [] {
     const char* e = getenv("HVE_FUSE_RR");
@@ -1143,9 +1146,16 @@ void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
     const char* e = getenv("HVE_RR_ZC");
     return e ? atoi(e) : 64;
   }();
+  static const int tile_env = [] {
+    const char* e = getenv("HVE_TILE_R");
+    return e ? atoi(e) : 0;
+  }();
   rr_.release();
-  const int kn = knob(8);  // hypreve_SetKnob(8, 1 / -1) turns it on / off for this setup (tests)
-  if (!(kn > 0 || (kn == 0 && env)) || R.lev.size() < 2 || comm_) return;
+  const int kn = knob(8);   // hypreve_SetKnob(8, 1 / -1) turns it on / off for this setup (tests)
+  const int kt = knob(10);  // the same for the tiled restriction (k_tile_restrict)
+  const bool fused = kn > 0 || (kn == 0 && env);
+  const bool tiled = !fused && (kt > 0 || (kt == 0 && tile_env));
+  if (!(fused || tiled) || R.lev.size() < 2 || comm_) return;
   const RankLevel& L = R.lev[0];
   const DevLevel& D = lev_[0];
   auto identity = [](const std::vector<int>& m, int n) {
@@ -1230,6 +1240,9 @@ void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
     bcptr[b + 1] += bcptr[b];
   }
   if (bent[nb] >= INT_MAX) return decline("too many entries");
+  // the tiled kernel's 32-bit buffer offsets (codes, f64 weights, r)
+  if (tiled && (bent[nb] * (vt ? 2 : 8) >= ((int64_t)1 << 32) || (int64_t)A.nrows * 8 >= ((int64_t)1 << 32)))
+    return decline("restriction or residual past 4 GiB");
   std::vector<int> bcnt(std::max(1, bcptr[nb]));
   std::vector<unsigned short> code((size_t)std::max<int64_t>(1, bent[nb]));
   std::vector<double> bval(vt ? 0 : (size_t)std::max<int64_t>(1, bent[nb]));
@@ -1283,6 +1296,7 @@ void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
   rr_.ntx = ntx; rr_.nty = nty; rr_.nzc = nzc;
   rr_.nbuckets = nb;
   rr_.entries = bent[nb];
+  rr_.mode = fused ? 1 : 2;
   rr_.bptr = dupload(bptr.data(), bptr.size());
   rr_.bent = dupload(bent32.data(), bent32.size());
   rr_.bcptr = dupload(bcptr.data(), bcptr.size());
@@ -1316,7 +1330,7 @@ RRView DevAMG::rr_view() const {
   v.ntx = rr_.ntx; v.nty = rr_.nty; v.nzc = rr_.nzc;
   v.bptr = rr_.bptr; v.bent = rr_.bent; v.bcptr = rr_.bcptr; v.bcnt = rr_.bcnt; v.brow = rr_.brow;
   v.blb = rr_.blb; v.blen = rr_.blen; v.code = rr_.code; v.vtabR = rr_.vtab; v.odz = rr_.odz; v.odxy = rr_.odxy;
-  v.nvtabR = rr_.nvtab; v.notab = rr_.notab; v.vbits = rr_.vbits; v.bval = rr_.bval;
+  v.nvtabR = rr_.nvtab; v.notab = rr_.notab; v.vbits = rr_.vbits; v.bval = rr_.bval; v.entries = rr_.entries;
   return v;
 }
 
@@ -1879,10 +1893,15 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       const bool fuse_zg = !into_agg && coarse != nl - 1 && prm.num_sweeps[1] >= 1 && prm.relax_order != 1 &&
                            (prm.relax_type[1] == 18 || prm.relax_type[1] == 7) && prm.wt(coarse) == 1.0 &&
                            lev_[coarse].l1 != nullptr;
-      if (fine == 0 && rr_.built() && !into_agg) {
+      if (fine == 0 && rr_.built() && rr_.mode == 1 && !into_agg) {
         // F_c = P^T (f - A u) in one pass: the residual stays in LDS
         HVE_HIP(launch_resid_restrict(rr_view(), ucur[fine], fl[fine], lev_[coarse].F,
                                       fuse_zg ? ucur[coarse] : nullptr, fuse_zg ? lev_[coarse].l1 : nullptr, s));
+      } else if (fine == 0 && rr_.built() && !into_agg) {
+        // Vtemp = f - A u, then F_c = P^T Vtemp over grid tiles (Vtemp staged in LDS)
+        apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);
+        HVE_HIP(launch_tile_restrict(rr_view(), Lf.n, Lf.V, lev_[coarse].F, fuse_zg ? ucur[coarse] : nullptr,
+                                     fuse_zg ? lev_[coarse].l1 : nullptr, s));
       } else {
       // Vtemp = f - A u  (csr_matvec.c, alpha=-1 beta=1);  F_c = P^T Vtemp
       apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);

@@ -203,6 +203,7 @@ struct DevRR {
   int* odxy = nullptr;   // per offset index: dy * (kRRTx + 4) + dx
   int nvtab = 0, notab = 0, vbits = 0, nbuckets = 0;
   int64_t entries = 0;
+  int mode = 0;  // 1: fused residual + restriction (k_resid_restrict), 2: tiled restriction (k_tile_restrict)
   bool built() const { return bptr != nullptr; }
   void release();
 };
@@ -286,7 +287,16 @@ class DevAMG {
   };
   const std::vector<CycleComm>& cycle_comm() const { return cycle_comm_; }
   bool multi_rank() const { return comm_ != nullptr; }
-  bool fused_rr() const { return rr_.built(); }
+  int fused_rr() const { return rr_.built() ? rr_.mode : 0; }
+  RRView rr_view() const;
+  int rr_fine_rows() const { return rr_.nx * rr_.ny * rr_.nz; }
+  // bytes one tiled restriction streams: codes (+ f64 weights), the bucket
+  // rows' anchor / length / row, the value and offset tables, r once, F_c
+  double rr_tile_bytes(int ncoarse) const {
+    return (double)rr_.entries * (rr_.bval ? 10.0 : 2.0) + (double)ncoarse * (2 + 1 + 4 + 8) +
+           (double)rr_.nvtab * 8 + (double)rr_.notab * 8 + (double)(rr_.nbuckets + 1) * 12 +
+           (double)rr_fine_rows() * 8;
+  }
   // Re-key the row-block traversal (tuning; see locality_keys in runtime.hip).
   // which_mask: bit 0 the A operators, bit 1 P, bit 2 R
   void set_block_bands(const RankHierarchy& R, int nbands, int which_mask = 7);
@@ -344,9 +354,8 @@ class DevAMG {
   int comm_level_ = -1;  // level whose exchanges are being counted (emit_cycle), -1 = none
   int ws_n_ = 0;
   std::map<std::tuple<const void*, const void*, int>, hipGraphExec_t> graphs_;  // (f, u, presmoothed + 2 zero_u)
-  DevRR rr_;                      // level 0's fused residual + restriction (single rank, grid operator)
+  DevRR rr_;                      // level 0's fused residual + restriction or tiled restriction (single rank, grid operator)
   void build_rr(const RankHierarchy& R, const std::vector<int>& fc);
-  RRView rr_view() const;
   int agg_level_ = -1;            // first replicated level (RankHierarchy::agg_level)
   std::vector<int> agg_starts_;   // its rows' distributed owners
 };

@@ -559,10 +559,11 @@ class BoomerAMG:
         check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
 
     def fused_resid_restrict(self):
-        """Whether level 0's residual and restriction run as one kernel."""
+        """Level 0's restriction kernel: 1 fused with the residual, 2 over
+        LDS-staged grid tiles of the stored residual, 0 the per-row loop."""
         v = C.c_int()
         check(lib().hypreve_BoomerAMGGetFusedResidRestrict(self.h, C.byref(v)), "GetFusedResidRestrict")
-        return bool(v.value)
+        return v.value
 
     def cycle_comm_stats(self):
         """This rank's communication in one V-cycle, per level: halo exchanges,

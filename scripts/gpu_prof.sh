@@ -20,7 +20,7 @@ step() {  # step <name> <seconds> <cmd...>
     *) echo "=== stopping after $name (rc=$rc)"; exit $rc ;;
   esac
 }
-BENCH="bench.py --n $N --secondary-n 0 --cpu-cycles 0"
+BENCH="bench.py --n $N --secondary-n 0 --cpu-cycles 0 --pcg-iters 0 --setup-parity 0"
 WHAT=${1:-all}
 if [[ $WHAT == all || $WHAT == trace ]]; then
   step trace 600 rocprofv3 --kernel-trace --stats -d $OUT/trace -o run --output-format csv -- python $BENCH --steps 10 --warmup 2

@@ -23,7 +23,7 @@ PREFIXES = ("hve::k_sell<0,", "hve::k_sell_delta<0,", "hve::k_sell_stencil<0,")
 def mean_counter(path, counter, grid, prefixes=PREFIXES, names=None):
     vals = []
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != counter or int(r["Grid_Size"]) != grid:
+        if r["Counter_Name"] != counter or (grid is not None and int(r["Grid_Size"]) != grid):
             continue
         nm = r["Kernel_Name"].replace("void ", "")
         if nm.startswith(prefixes):
@@ -55,15 +55,18 @@ def main():
     wpath = os.path.join(root, "pmc_write", "run_counter_collection.csv")
     fetch = write = None
     names = set()
-    for pre in ("hve::k_sell_stencil<0,", "hve::k_sell_delta<0,", "hve::k_sell<0,"):
+    # (the grid-stencil loop launches one workgroup per tile and plane chunk,
+    # not per row block: any grid size; only level 0 has the grid layout)
+    for pre in ("hve::k_grid_stencil<0,", "hve::k_sell_stencil<0,", "hve::k_sell_delta<0,", "hve::k_sell<0,"):
         names = set()
-        fetch, nf = mean_counter(fpath, "FETCH_SIZE", grid, prefixes=(pre,), names=names)
-        write, nw = mean_counter(wpath, "WRITE_SIZE", grid, prefixes=(pre,))
+        g = None if pre.startswith("hve::k_grid") else grid
+        fetch, nf = mean_counter(fpath, "FETCH_SIZE", g, prefixes=(pre,), names=names)
+        write, nw = mean_counter(wpath, "WRITE_SIZE", g, prefixes=(pre,))
         if fetch is not None and write is not None:
             break
     if fetch is None or write is None:
         raise SystemExit("no matching dispatches")
-    out = {"kernel": "k_sell / k_sell_delta / k_sell_stencil <OP_RESID> finest level", "kernel_names": sorted(names),
+    out = {"kernel": "k_grid_stencil / k_sell_stencil / k_sell_delta / k_sell <OP_RESID> finest level", "kernel_names": sorted(names),
            "grid": grid, "dispatches": [nf, nw],
            "fetch_kib": fetch, "write_kib": write,
            "traffic_bytes": 2.0 * fetch * 1024 + write * 1024,
