@@ -74,6 +74,7 @@ struct SellView {
   // (pattern, slot), nullptr = the per-slice loop
   const GSlot* gslot = nullptr;
   int gnx = 0, gny = 0, gnz = 0, gzc = 0;
+  int gz0 = 0, gz1 = 0;  // the stored rows: planes gz0 .. gz1 - 1 (row i = grid point i + gz0 * gnx * gny)
 };
 
 enum : int {

@@ -101,7 +101,7 @@ struct SpArgs {
   double temp;                    // beta/alpha for OP_GENERAL
   int relax_points;
   const GSlot* __restrict__ gslot;           // grid stencil (k_grid_stencil)
-  int gnx, gny, gnz, gzc;
+  int gnx, gny, gnz, gzc, gz0, gz1;
 };
 
 // Logical workgroup block -> stored row block (SpArgs::blk_map): the
@@ -922,7 +922,8 @@ __global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
   cint* const spat = (cint*)p.slice_pat;
   const int nx = p.gnx, ny = p.gny, nz = p.gnz, zc = p.gzc, W = p.sw;
   const int ntx = nx >> 6, nty = (ny + kGTy - 1) / kGTy;
-  const int ntiles = ntx * nty * ((nz + zc - 1) / zc);
+  const int ntiles = ntx * nty * ((p.gz1 - p.gz0 + zc - 1) / zc);
+  const int shift = p.gz0 * nx * ny;  // stored row = grid point - shift (slice patterns)
   const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int lane = threadIdx.x & (kWave - 1);
@@ -932,13 +933,13 @@ __global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
   double acc = 0.0;
   if (lb < ntiles) {
     const int tx = lb % ntx, tyi = (lb / ntx) % nty, zci = lb / (ntx * nty);
-    const int x0 = tx * kWave, y0 = tyi * kGTy, z0 = zci * zc, z1 = min(nz, z0 + zc);
+    const int x0 = tx * kWave, y0 = tyi * kGTy, z0 = p.gz0 + zci * zc, z1 = min(p.gz1, z0 + zc);
     const int yw = y0 + wave * LPW;  // the wave's first line
     // plane loads: tile line wave + 4j (y0 - 1 + that), its 64 points by lane;
     // the margin points (x0 - 1, x0 + 64) of line t / 2 by the first 2 PY
     // threads.  Points outside the grid read zeros: buffer loads whose offset
     // is past the vector (unconditional, no branches around the loads).
-    const unsigned nb8 = (unsigned)p.nrows * 8u;
+    const unsigned nb8 = (unsigned)(nx * ny * nz) * 8u;  // the grid's points (x, b, l1 by grid point)
     const auto rx = gs_rsrc(xp, nb8);
     const auto rb = gs_rsrc((OP == OP_MATVEC || !bp) ? xp : bp, nb8);
     const auto rl = gs_rsrc((SMOOTH && !fly) ? l1p : xp, nb8);
@@ -986,7 +987,7 @@ __global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
         const int bo = ok ? (int)((unsigned)(base + lane) * 8u) : kOut;                \
         TT[l] = OP == OP_MATVEC ? 0.0 : grid_init<OP>(gs_ld64(rb, bo), p.w, p.temp);   \
         LL[l] = (SMOOTH && !fly) ? gs_ld64(rl, bo) : 1.0;                              \
-        PP[l] = spat[base >> 6];                                                       \
+        PP[l] = spat[(ok ? base - shift : 0) >> 6];                                    \
       }                                                                                \
     }
     HVE_GRID_ROWS(z0, t0, l1v, pat)
@@ -2431,7 +2432,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     return hipGetLastError();
   }
   a.gslot = M.gslot;
-  a.gnx = M.gnx; a.gny = M.gny; a.gnz = M.gnz; a.gzc = M.gzc;
+  a.gnx = M.gnx; a.gny = M.gny; a.gnz = M.gnz; a.gzc = M.gzc; a.gz0 = M.gz0; a.gz1 = M.gz1;
   if (M.slot_mask && grid_stencil_on(M) && !cfsel &&
       (op == OP_RESID || op == OP_MATVEC || op == OP_L1JAC || op == OP_L1JAC_W || op == OP_RESID_L1JAC ||
        op == OP_GENERAL)) {
@@ -2875,7 +2876,7 @@ bool grid_stencil_on(const SellView& M) {
 }
 // One workgroup per (x, y) tile and chunk of gzc planes, whole XCD rounds.
 int grid_stencil_blocks(const SellView& M) {
-  const int nt = (M.gnx / kWave) * ((M.gny + kGTy - 1) / kGTy) * ((M.gnz + M.gzc - 1) / M.gzc);
+  const int nt = (M.gnx / kWave) * ((M.gny + kGTy - 1) / kGTy) * ((M.gz1 - M.gz0 + M.gzc - 1) / M.gzc);
   return std::max(8, (nt + 7) / 8 * 8);
 }
 int sell_nrm_parts(const SellView& M) {

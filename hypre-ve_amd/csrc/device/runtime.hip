@@ -94,22 +94,28 @@ void DevSell::build_wave_map() {
   nwave = nb * 4;
 }
 
-static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz);
+static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz, int shift = 0);
 
 // Grid form of the stencil layout (k_grid_stencil) when the operator's rows
-// are the points of a grid in natural order with 64 | nx: every used slot
-// offset is dz * nx * ny + dy * nx + dx with steps of at most one point, and
-// no present lane's neighbour leaves the grid (so none wraps into another
-// line or plane: the tile position of row + offset is the neighbour's).
-// HVE_GRID_ZC (or knob 9, tests) sets the planes per workgroup (default:
-// about 2048 workgroups).
+// are consecutive points of a grid in natural order with 64 | nx: stored row
+// i is grid point i + shift (shift: whole planes; a rank's interior rows start
+// one plane in), and the columns are the nlocal grid points.  Every used slot
+// offset is shift + dz * nx * ny + dy * nx + dx with steps of at most one
+// point, and no present lane's neighbour leaves the grid (so none wraps into
+// another line or plane: the tile position of a point + offset is the
+// neighbour's).  HVE_GRID_ZC (or knob 9, tests) sets the planes per workgroup
+// (default: about 2048 workgroups).
 bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::vector<int>& svi,
-                         const std::vector<uint64_t>& sm, const std::vector<double>& tab) {
-  int nx, ny, nz;
-  if (A.ncols != A.nrows || !fine_grid(A, &nx, &ny, &nz)) return false;
-  if (nx % 64 || ny < 3 || nz < 3 || (int64_t)nx * ny * nz != A.nrows) return false;
-  const int W = stencil_w;
+                         const std::vector<uint64_t>& sm, const std::vector<double>& tab, int shift, int nlocal) {
+  int nx, ny, nzs;
+  if (!fine_grid(A, &nx, &ny, &nzs, shift)) return false;
   const int64_t P = (int64_t)nx * ny;
+  if (nx % 64 || ny < 3 || nlocal % P || shift % P || (int64_t)nx * ny * nzs != A.nrows) return false;
+  const int nz = (int)(nlocal / P);
+  if (nz < 3 || shift / P + nzs > nz) return false;
+  for (int64_t k = 0; k < A.nnz(); ++k)
+    if (A.j[k] >= nlocal) return false;  // a halo column
+  const int W = stencil_w;
   std::vector<GSlot> gs((size_t)npat * W + 16);
   for (auto& g : gs) g = GSlot{0, 0.0, 0, 0, 0, 0};
   for (int pt = 0; pt < npat; ++pt)
@@ -120,7 +126,7 @@ bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::ve
       for (int dz = -1; dz <= 1 && !found; ++dz)
         for (int dy = -1; dy <= 1 && !found; ++dy)
           for (int dx = -1; dx <= 1 && !found; ++dx)
-            if (dz * P + (int64_t)dy * nx + dx == so[e]) {
+            if (shift + dz * P + (int64_t)dy * nx + dx == so[e]) {
               gs[e] = GSlot{sm[e], tab[svi[e]], dz, dy * (64 + 2) + dx, 0, 0};
               found = true;
             }
@@ -129,7 +135,8 @@ bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::ve
   int ok = 1;
 #pragma omp parallel for schedule(static) reduction(min : ok)
   for (int s = 0; s < nslices; ++s) {
-    const int r0 = s * 64, x0 = r0 % nx, y = (int)((r0 / nx) % ny), z = (int)(r0 / P);
+    const int64_t r0 = (int64_t)s * 64 + shift;
+    const int x0 = (int)(r0 % nx), y = (int)((r0 / nx) % ny), z = (int)(r0 / P);
     const int pt = pat_host[s];
     for (int k = 0; k < W; ++k) {
       const GSlot& g = gs[(size_t)pt * W + k];
@@ -147,12 +154,14 @@ bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::ve
   }();
   const int64_t txy = (int64_t)(nx / 64) * ((ny + kGTy - 1) / kGTy);
   const int zc = knob(9) > 0 ? knob(9) : zc_env > 0 ? zc_env
-               : (int)std::max<int64_t>(2, std::min<int64_t>(64, nz * txy / 2048));
+               : (int)std::max<int64_t>(2, std::min<int64_t>(64, nzs * txy / 2048));
   gslot = dupload(gs.data(), gs.size());
-  gnx = nx; gny = ny; gnz = nz; gzc = std::min(zc, nz);
+  gnx = nx; gny = ny; gnz = nz; gzc = std::min(zc, nzs);
+  gz0 = (int)(shift / P);
+  gz1 = gz0 + nzs;
   if (getenv("HVE_LAYOUT_LOG"))
-    fprintf(stderr, "[layout] grid stencil %dx%dx%d, %d planes a workgroup, %d workgroups\n", nx, ny, nz, gzc,
-            grid_stencil_blocks(view()));
+    fprintf(stderr, "[layout] grid stencil %dx%dx%d (planes %d..%d), %d planes a workgroup, %d workgroups\n", nx, ny,
+            nz, gz0, gz1 - 1, gzc, grid_stencil_blocks(view()));
   return true;
 }
 
@@ -366,12 +375,18 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       slot_mask = dupload(sm.data(), sm.size());
       vtab = dupload(tab.data(), tab.size());
       nvtab = (int)tab.size();
+      // the grid form also where the rows are a run of whole planes (a
+      // rank's interior rows): stored row i = local row i + shift
+      int shift = 0;
+      bool affine = true;
       if (!rowmap_h.empty()) {
         bool ident = true;
         for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
         if (!ident) rowmap = dupload(rowmap_h.data(), rowmap_h.size());
+        shift = A.nrows > 0 ? rowmap_h[0] : 0;
+        for (int i = 0; i < A.nrows && affine; ++i) affine = rowmap_h[i] == i + shift;
       }
-      if (!rowmap) build_grid(A, so, svi, sm, tab);
+      if (affine) build_grid(A, so, svi, sm, tab, shift, grid_nlocal > 0 ? grid_nlocal : A.nrows);
       stored_map = rowmap_h;
       if (key) set_block_order(rowmap_h, *key);
       if (!wave_map) build_wave_map();
@@ -718,7 +733,7 @@ void DevSell::release() {
   notab = vbits = 0; anc_n = cmap_n = 0;
   if (gslot) (void)hipFree(gslot);
   gslot = nullptr;
-  gnx = gny = gnz = gzc = 0;
+  gnx = gny = gnz = gzc = gz0 = gz1 = 0;
 }
 
 // Team size of the packed schedule: about this many rows per step.  A wide
@@ -786,6 +801,7 @@ void DevOp::upload(const RankOp& op, int policy, const std::vector<int64_t>* key
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   const double t0 = now();
   in.relax_ops = bd.relax_ops = relax_ops;
+  in.grid_nlocal = bd.grid_nlocal = op.nrows_local;
   in.upload(op.interior, op.map_int, policy, key, coded, tile);
   if (tlog)
     fprintf(stderr, "[upload] %d rows %lld nnz: %s %.3fs\n", op.interior.nrows, (long long)op.interior.nnz(),
@@ -1098,19 +1114,20 @@ void DevRR::release() {
   entries = 0;
 }
 
-// Fine grid of level 0 from its operator, read off an interior row: line =
+// Fine grid of level 0 from its operator (row i is grid point i + shift),
+// read off an interior row: line =
 // its smallest column offset above 1 (plus one when that offset + 1 is also a
 // neighbour: the diagonal neighbours of a 27-point stencil), plane = its
 // largest offset (minus line + 1 for a 27-point stencil); nx = line,
 // ny = plane / line.  Only a guess: build_rr checks every restriction entry
 // against it, and any factorisation that passes gives the same sums.
-static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz) {
+static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz, int shift) {
   const int n = A.nrows;
   if (n < 4096) return false;
   for (int i : {n / 2, n / 2 + 7, n / 3 + 11}) {
     std::vector<int64_t> off;
     for (int k = A.i[i]; k < A.i[i + 1]; ++k)
-      if (A.j[k] > i) off.push_back((int64_t)A.j[k] - i);
+      if (A.j[k] > i + shift) off.push_back((int64_t)A.j[k] - i - shift);
     std::sort(off.begin(), off.end());
     auto has = [&](int64_t d) { return std::binary_search(off.begin(), off.end(), d); };
     int64_t line = 0;

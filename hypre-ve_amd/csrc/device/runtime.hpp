@@ -75,9 +75,10 @@ struct DevSell {
   unsigned* code32 = nullptr;
   // stencil layout over a grid in natural order (SellView::gslot, k_grid_stencil)
   GSlot* gslot = nullptr;
-  int gnx = 0, gny = 0, gnz = 0, gzc = 0;
+  int gnx = 0, gny = 0, gnz = 0, gzc = 0, gz0 = 0, gz1 = 0;
+  int grid_nlocal = 0;  // the rank's local rows (columns below it are grid points); configuration
   bool build_grid(const CSR& A, const std::vector<int>& so, const std::vector<int>& svi,
-                  const std::vector<uint64_t>& sm, const std::vector<double>& tab);
+                  const std::vector<uint64_t>& sm, const std::vector<double>& tab, int shift, int nlocal);
   // the operator is also applied by the residual and smoother ops (a level's
   // A), whose kernels do not take the 16-bit value-table dictionary layout;
   // configuration, kept across release()
@@ -91,7 +92,7 @@ struct DevSell {
     v.blk_map = blk_map; v.nblk = nblk; v.wave_map = wave_map; v.nwave = nwave;
     v.code16 = code16; v.otab = otab; v.notab = notab; v.vbits = vbits; v.anc = anc; v.cmap = cmap;
     v.code32 = code32;
-    v.gslot = gslot; v.gnx = gnx; v.gny = gny; v.gnz = gnz; v.gzc = gzc;
+    v.gslot = gslot; v.gnx = gnx; v.gny = gny; v.gnz = gnz; v.gzc = gzc; v.gz0 = gz0; v.gz1 = gz1;
     return v;
   }
   // Grid context of an interpolation / restriction operator for the

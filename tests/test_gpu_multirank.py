@@ -223,3 +223,49 @@ def test_loopback_coded_layout_bitwise(hv, nranks, agglo):
     xN, itN, rrN, nlN = _solve_nranks(hv, 14, 13, 16, kw, nranks)
     assert nlN == nl1 and all(i == it1 for i in itN)
     assert np.array_equal(x1, xN)
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+@pytest.mark.parametrize("stencil,relax", [(7, 18), (27, 18), (7, 0)])
+def test_loopback_grid_stencil_bitwise(hv, nranks, stencil, relax):
+    """The grid-stencil loop (k_grid_stencil) on every rank's interior rows:
+    a run of whole planes one plane in from the slab's faces, read as grid
+    points shifted by that plane.  The N-rank iterates equal the one-rank ones
+    bit for bit, and every rank's interior operator takes the grid form."""
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=relax, tol=1e-8, max_iter=60,
+              sell_policy=11)
+    if relax == 0:
+        kw.update(relax_wt=0.6)
+    x1, it1, rr1, nl1 = _solve_1rank(hv, 64, 20, 24, kw, stencil=stencil)
+    comms = hv.Comm.loopback(nranks)
+    layouts, out, errs = [None] * nranks, [None] * nranks, [None] * nranks
+
+    def worker(r):
+        try:
+            c = comms[r]
+            A = _gen(hv, stencil, 64, 20, 24, comm=c, P=1, Q=1, R=nranks, p=0, q=0, r=r)
+            amg = hv.BoomerAMG(**kw)
+            amg.setup(A)
+            layouts[r] = amg.level_layout(0, 0)
+            b = hv.ParVector(A.n, np.ones(A.n), comm=c, first=A.first, global_n=A.global_n)
+            x = hv.ParVector(A.n, np.zeros(A.n), comm=c, first=A.first, global_n=A.global_n)
+            it, rr = amg.solve(A, b, x)
+            out[r] = (A.first, x.get(), it)
+        except Exception as e:  # reported by the main thread
+            errs[r] = e
+
+    th = [threading.Thread(target=worker, args=(r,), daemon=True) for r in range(nranks)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(300)
+    assert not any(t.is_alive() for t in th), "a virtual rank did not finish"
+    for e in errs:
+        if e is not None:
+            raise e
+    assert all(lay == "grid-stencil" for lay in layouts), layouts
+    out.sort(key=lambda o: o[0])
+    xN = np.concatenate([o[1] for o in out])
+    assert all(o[2] == it1 for o in out)
+    assert np.array_equal(x1, xN)
