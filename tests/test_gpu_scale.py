@@ -64,7 +64,7 @@ def test_bench_size_256_bitwise(gpu, orc):
     amg.setup(A)
     layouts = {(l, w): amg.level_layout(l, w) for l in range(3) for w in range(3)}
     print("layouts", layouts)
-    assert layouts[(0, 0)] == "stencil"
+    assert layouts[(0, 0)] == "grid-stencil"  # the stencil layout's grid form (64 | nx)
     assert layouts[(1, 0)] == "dict"
     cycle_and_solve_bitwise(hv, orc, A, amg, 101, 3)
 
@@ -90,7 +90,7 @@ def test_aniso_stencil_128_bitwise(gpu, orc, coef):
     A = hv.ParCSRMatrix.laplacian(128, 128, 128, cx=coef[0], cy=coef[1], cz=coef[2])
     amg = bench_amg(hv)
     amg.setup(A)
-    assert amg.level_layout(0, 0) == "stencil"
+    assert amg.level_layout(0, 0) == "grid-stencil"
     cycle_and_solve_bitwise(hv, orc, A, amg, 303, 3)
     amg7 = bench_amg(hv, sell_policy=7)
     amg7.setup(A)
