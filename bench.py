@@ -35,7 +35,7 @@ PROFILE_DIR = os.path.join(ROOT, "profiles")
 # hypreve_BoomerAMGGetLevelLayout name -> (residual kernel instantiation as
 # rocprofv3 names it, minus the batch width: "<prefix>B<suffix>"; description)
 KERNEL_OF_LAYOUT = {
-    "grid-stencil": ("k_grid_stencil<0, true>|(hve::SpArgs)",
+    "grid-stencil": ("k_grid_stencil<0, true, |>(hve::SpArgs)",
                      "slot-uniform SELL-64 over the grid, x staged in an LDS ring of tile planes "
                      "(nothing stored per entry)"),
     "stencil": ("k_sell_stencil<0, false, true, |>(hve::SpArgs)",
@@ -401,7 +401,7 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
             hv.bench_stream(eb, (1 << 29) // eb, 1)
     roof = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-            "kernel": f"{kname.replace('|', '' if layout0 == 'grid-stencil' else 'B').split('(')[0]} finest level (r = b - A x), {kdesc}",
+            "kernel": f"{kname.replace('|', 'NW' if layout0 == 'grid-stencil' else 'B').split('(')[0]} finest level (r = b - A x), {kdesc}",
             "layout": layout0,
             "avg_ms": round(spmv_ms, 4), "bytes_per_launch": stored_bytes,
             "csr_bytes_per_launch": csr_bytes, "csr_equivalent_gbs": round(csr_gbs, 1),

@@ -12,8 +12,6 @@ struct GSlot {
   double val;
   int dz, dxy, pad0, pad1;
 };
-// Lines of the x-tile a grid-stencil workgroup computes per plane (4 waves).
-constexpr int kGTy = 16;
 
 // Device view of one SELL-64 operator, padded or jagged (see kernels.hip).
 struct SellView {
@@ -176,6 +174,8 @@ int stencil_slices_per_wave();
 int stencil_grid(int nrows);
 bool grid_stencil_on(const SellView& M);
 int grid_stencil_blocks(const SellView& M);
+int grid_stencil_waves();  // waves per workgroup (tiles of 64 x 4 waves lines)
+int grid_stencil_ty();
 bool stencil_wave_map();
 int sell_pipe_override();
 bool sell_nt();

@@ -811,7 +811,7 @@ __global__ void __launch_bounds__(256) k_sell_stencil(SpArgs p) {
 // whose rows are the points of a gnx x gny x gnz grid in natural order (gnx a
 // multiple of 64) and whose slots reach at most one point in each direction
 // (7- and 27-point stencils; host check: DevSell::build_grid).  A workgroup
-// owns 64 x kGTy points in (x, y) and marches gzc planes in z, keeping planes
+// owns 64 x 4 NW points in (x, y) and marches gzc planes in z, keeping planes
 // z-1, z, z+1 of its tile plus a one-point margin in a 4-plane LDS ring: each
 // x value leaves memory once per tile in coalesced 512-B lines instead of once
 // per slot, and plane z+2's loads (and plane z+1's right-hand side) are in
@@ -907,21 +907,22 @@ __device__ __forceinline__ void grid_lines(const GSlot* __restrict__ gslot, int 
   }
 }
 
-template <int OP, bool NT>
-__global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
-  constexpr int PX = kWave + 2, PY = kGTy + 2, PL = PX * PY;
-  constexpr int LPW = kGTy / 4;    // lines of a plane per wave
-  static_assert(LPW == 4, "the shared-pattern test below reads four lines");
-  constexpr int JL = (PY + 3) / 4; // tile lines (margin included) loaded per wave
+// NW waves a workgroup, four lines each: tiles of 64 x 4 NW points.
+template <int OP, bool NT, int NW>
+__global__ void __launch_bounds__(64 * NW) k_grid_stencil(SpArgs p) {
+  constexpr int TY = 4 * NW;       // tile lines
+  constexpr int PX = kWave + 2, PY = TY + 2, PL = PX * PY;
+  constexpr int LPW = 4;           // lines of a plane per wave
+  constexpr int JL = (PY + NW - 1) / NW;  // tile lines (margin included) loaded per wave
   constexpr bool SMOOTH = OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_RESID_L1JAC;
-  __shared__ double ring[4 * PL];
+  extern __shared__ double ring[];  // 4 * PL
   const double* __restrict__ xp = p.x;
   const double* __restrict__ bp = p.b;
   const double* __restrict__ l1p = p.l1;
   using cint = const __attribute__((address_space(4))) int;  // slice patterns: scalar cache
   cint* const spat = (cint*)p.slice_pat;
   const int nx = p.gnx, ny = p.gny, nz = p.gnz, zc = p.gzc, W = p.sw;
-  const int ntx = nx >> 6, nty = (ny + kGTy - 1) / kGTy;
+  const int ntx = nx >> 6, nty = (ny + TY - 1) / TY;
   const int ntiles = ntx * nty * ((p.gz1 - p.gz0 + zc - 1) / zc);
   const int shift = p.gz0 * nx * ny;  // stored row = grid point - shift (slice patterns)
   const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
@@ -933,9 +934,9 @@ __global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
   double acc = 0.0;
   if (lb < ntiles) {
     const int tx = lb % ntx, tyi = (lb / ntx) % nty, zci = lb / (ntx * nty);
-    const int x0 = tx * kWave, y0 = tyi * kGTy, z0 = p.gz0 + zci * zc, z1 = min(p.gz1, z0 + zc);
+    const int x0 = tx * kWave, y0 = tyi * TY, z0 = p.gz0 + zci * zc, z1 = min(p.gz1, z0 + zc);
     const int yw = y0 + wave * LPW;  // the wave's first line
-    // plane loads: tile line wave + 4j (y0 - 1 + that), its 64 points by lane;
+    // plane loads: tile line wave + NW j (y0 - 1 + that), its 64 points by lane;
     // the margin points (x0 - 1, x0 + 64) of line t / 2 by the first 2 PY
     // threads.  Points outside the grid read zeros: buffer loads whose offset
     // is past the vector (unconditional, no branches around the loads).
@@ -951,7 +952,7 @@ __global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
     bool lok[JL];
 #pragma unroll
     for (int j = 0; j < JL; ++j) {
-      const int li = wave + 4 * j, yy = y0 - 1 + li;
+      const int li = wave + NW * j, yy = y0 - 1 + li;
       lok[j] = li < PY && yy >= 0 && yy < ny;
       loff[j] = (lok[j] ? yy : 0) * nx + x0 + lane;
     }
@@ -969,7 +970,7 @@ __global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
     {                                                                        \
       double* r = ring + ((zz) & 3) * PL;                                    \
       _Pragma("unroll") for (int j = 0; j < JL; ++j) {                       \
-        const int li = wave + 4 * j;                                         \
+        const int li = wave + NW * j;                                         \
         if (li < PY) r[li * PX + 1 + lane] = V[j];                           \
       }                                                                      \
       if (mt < 2 * PY) r[mli * PX + ((mt & 1) ? PX - 1 : 0)] = VM;           \
@@ -1041,7 +1042,7 @@ __global__ void __launch_bounds__(256) k_grid_stencil(SpArgs p) {
   }
   if ((OP == OP_RESID_L1JAC || OP == OP_MATVEC) && want_nrm) {
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
-    if (lane == 0) p.nrm[blockIdx.x * 4 + (threadIdx.x >> 6)] = acc;
+    if (lane == 0) p.nrm[blockIdx.x * NW + (threadIdx.x >> 6)] = acc;
   }
 }
 
@@ -2439,16 +2440,29 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     a.sw = M.stencil_w;
     a.slice_pat = M.slice_pat;
     const dim3 ggrid(grid_stencil_blocks(M));
+    const int nw = grid_stencil_waves();
+    const size_t glds = (size_t)4 * (kWave + 2) * (4 * nw + 2) * sizeof(double);
+#define HVE_GW(OPV, NTV, NWV)                                                                          \
+  {                                                                                                    \
+    static bool attr = false;                                                                          \
+    if (!attr) {                                                                                       \
+      (void)hipFuncSetAttribute((const void*)k_grid_stencil<OPV, NTV, NWV>,                           \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);               \
+      attr = true;                                                                                     \
+    }                                                                                                  \
+    hipLaunchKernelGGL((k_grid_stencil<OPV, NTV, NWV>), ggrid, dim3(64 * NWV), glds, s, a);          \
+  }
 #define HVE_G(OPV)                                                                         \
   case OPV:                                                                                \
-    if (nt) hipLaunchKernelGGL((k_grid_stencil<OPV, true>), ggrid, block, 0, s, a);       \
-    else hipLaunchKernelGGL((k_grid_stencil<OPV, false>), ggrid, block, 0, s, a);         \
+    if (nw == 8) { if (nt) HVE_GW(OPV, true, 8) else HVE_GW(OPV, false, 8) }              \
+    else { if (nt) HVE_GW(OPV, true, 4) else HVE_GW(OPV, false, 4) }                      \
     break;
     switch (op) {
       HVE_G(OP_RESID) HVE_G(OP_MATVEC) HVE_G(OP_L1JAC) HVE_G(OP_L1JAC_W) HVE_G(OP_RESID_L1JAC) HVE_G(OP_GENERAL)
       default: return hipErrorInvalidValue;
     }
 #undef HVE_G
+#undef HVE_GW
     return hipGetLastError();
   }
   if (M.slot_mask) {  // slot-uniform stencil: R slices per wave, 4R per workgroup
@@ -2874,13 +2888,27 @@ bool grid_stencil_on(const SellView& M) {
   }();
   return v && M.gslot != nullptr && M.gnx > 0 && M.gzc > 0;
 }
+// Waves per grid-stencil workgroup (tiles of 64 x 4 NW points): HVE_GRID_WAVES=4|8.
+// Measured at 512^3 on one box (profiles/r04/13_waves/): the 7-point residual
+// 0.622 ms with 4 waves (64 x 16 tiles, 38 KiB) against 0.585 with 8 (64 x 32,
+// 72 KiB: less tile halo re-read per point); the 27-point share 0.145 / 0.144.
+int grid_stencil_waves() {
+  static const int v = [] {
+    const char* e = getenv("HVE_GRID_WAVES");
+    const int w = e ? atoi(e) : 8;
+    return w == 4 ? 4 : 8;
+  }();
+  return v;
+}
+int grid_stencil_ty() { return 4 * grid_stencil_waves(); }
 // One workgroup per (x, y) tile and chunk of gzc planes, whole XCD rounds.
 int grid_stencil_blocks(const SellView& M) {
-  const int nt = (M.gnx / kWave) * ((M.gny + kGTy - 1) / kGTy) * ((M.gz1 - M.gz0 + M.gzc - 1) / M.gzc);
+  const int ty = grid_stencil_ty();
+  const int nt = (M.gnx / kWave) * ((M.gny + ty - 1) / ty) * ((M.gz1 - M.gz0 + M.gzc - 1) / M.gzc);
   return std::max(8, (nt + 7) / 8 * 8);
 }
 int sell_nrm_parts(const SellView& M) {
-  if (M.slot_mask && grid_stencil_on(M)) return 4 * grid_stencil_blocks(M);  // one per wave
+  if (M.slot_mask && grid_stencil_on(M)) return grid_stencil_waves() * grid_stencil_blocks(M);  // one per wave
   if (M.slot_mask) return 4 * stencil_grid(M.nrows);  // one per wave
   const int nb = blocks_pad8(std::max(M.nrows, 1));
   return M.vidx16 ? std::min(nb, 2048) : nb;

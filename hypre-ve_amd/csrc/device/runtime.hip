@@ -152,7 +152,7 @@ bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::ve
     const char* e = getenv("HVE_GRID_ZC");
     return e ? atoi(e) : 0;
   }();
-  const int64_t txy = (int64_t)(nx / 64) * ((ny + kGTy - 1) / kGTy);
+  const int64_t txy = (int64_t)(nx / 64) * ((ny + grid_stencil_ty() - 1) / grid_stencil_ty());
   const int zc = knob(9) > 0 ? knob(9) : zc_env > 0 ? zc_env
                : (int)std::max<int64_t>(2, std::min<int64_t>(64, nzs * txy / 2048));
   gslot = dupload(gs.data(), gs.size());
