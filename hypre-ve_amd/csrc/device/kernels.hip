@@ -2455,6 +2455,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #define HVE_G(OPV)                                                                         \
   case OPV:                                                                                \
     if (nw == 8) { if (nt) HVE_GW(OPV, true, 8) else HVE_GW(OPV, false, 8) }              \
+    else if (nw == 16) { if (nt) HVE_GW(OPV, true, 16) else HVE_GW(OPV, false, 16) }      \
     else { if (nt) HVE_GW(OPV, true, 4) else HVE_GW(OPV, false, 4) }                      \
     break;
     switch (op) {
@@ -2888,15 +2889,16 @@ bool grid_stencil_on(const SellView& M) {
   }();
   return v && M.gslot != nullptr && M.gnx > 0 && M.gzc > 0;
 }
-// Waves per grid-stencil workgroup (tiles of 64 x 4 NW points): HVE_GRID_WAVES=4|8.
+// Waves per grid-stencil workgroup (tiles of 64 x 4 NW points): HVE_GRID_WAVES=4|8|16.
 // Measured at 512^3 on one box (profiles/r04/13_waves/): the 7-point residual
 // 0.622 ms with 4 waves (64 x 16 tiles, 38 KiB) against 0.585 with 8 (64 x 32,
-// 72 KiB: less tile halo re-read per point); the 27-point share 0.145 / 0.144.
+// 72 KiB: less tile halo re-read per point); the 27-point share 0.145 / 0.144;
+// 16 waves (64 x 64, 139 KiB, one workgroup a CU) 0.642 against 0.584.
 int grid_stencil_waves() {
   static const int v = [] {
     const char* e = getenv("HVE_GRID_WAVES");
     const int w = e ? atoi(e) : 8;
-    return w == 4 ? 4 : 8;
+    return (w == 4 || w == 16) ? w : 8;
   }();
   return v;
 }
