@@ -107,13 +107,67 @@ class heartbeat:
         self.stop.set()
 
 
+def slab_rows(nx, ny, nz, world):
+    """[(first_row, rows)] of each rank's z-slab when GenerateLaplacian[27pt]
+    splits nx x ny x nz over a 1 x 1 x world process grid: the planes by
+    hypre_GeneratePartitioning (seq_mv/genpart.c:18: the first nz % world
+    slabs one plane more), each slab's rows in natural order after the
+    previous slab's (par_laplace.c:363 hypre_map with P = Q = 1)."""
+    size, rest = divmod(nz, world)
+    out, z0 = [], 0
+    for r in range(world):
+        nzl = size + (1 if r < rest else 0)
+        out.append((z0 * nx * ny, nzl * nx * ny))
+        z0 += nzl
+    return out
+
+
+def sha256_f64(v):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(v, dtype="<f8").tobytes()).hexdigest()
+
+
+def slab_digests_of(x, nx, ny, nz, worlds=(2, 4, 8)):
+    """sha256 of the whole iterate and of its z-slabs as an N-rank run would
+    own them, for each N in worlds: an N-rank line's per-rank digests must
+    equal the N-column here (the N-rank iterate equals the 1-rank iterate bit
+    for bit)."""
+    out = {"1": [sha256_f64(x)]}
+    for w in worlds:
+        if w <= nz:
+            out[str(w)] = [sha256_f64(x[f:f + c]) for f, c in slab_rows(nx, ny, nz, w)]
+    return out
+
+
+GOLDEN_DIGESTS = os.path.join(ROOT, "tests", "golden", "slab_digests.json")
+
+
+def digest_key(args, nx, ny, nz, iters):
+    """The workload a slab digest belongs to: grid, operator, method, the
+    parity iterations from x = 0 with rhs = ones."""
+    return (f"{nx}x{ny}x{nz} stencil{args.stencil} coef{args.coef} agg{args.agg} relax{args.relax} "
+            f"coarsen{args.coarsen} solver{args.solver} iters{iters}")
+
+
+def golden_slab_digests(key):
+    """The committed one-GPU digests of workload `key` (tests/golden/
+    slab_digests.json: N = 1 bench lines, the iterate bitwise equal to the C
+    oracle's), or None."""
+    try:
+        with open(GOLDEN_DIGESTS) as f:
+            return json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+
+
 def oracle_cpu_baseline(amg, nrows, n, pcg, args):
     """The reference's CPU solve path, restated in C (oracle/oracle.c, the
     parity checker) and run with OpenMP over rows on this host's cores, on the
-    hierarchy `amg` (one-process setup) with rhs = ones, from x = 0.  Sample
-    sized to about args.cpu_seconds of CPU work.  Returns (cpu_baseline dict,
-    the oracle's iterate, iterations): the bench then runs the GPU for the same
-    iterations from the same start and compares the iterates bit for bit."""
+    hierarchy `amg` (one-process setup) with rhs = ones, from x = 0, for
+    args.parity_iters iterations (the sample; about 10 s at 512^3 on 16
+    threads).  Returns (cpu_baseline dict, the oracle's iterate, iterations):
+    the bench then runs the GPU for the same iterations from the same start
+    and compares the iterates bit for bit."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
 
@@ -127,10 +181,7 @@ def oracle_cpu_baseline(amg, nrows, n, pcg, args):
             return O.pcg(bh, u, 0.0, k, 1)[0]
         return O.solve(bh, u, 1e-300, k)["iterations"]
 
-    tc = time.perf_counter()
-    cpu_run(1)
-    t1 = time.perf_counter() - tc
-    iters = int(max(2, min(args.cpu_cycles_max, round(args.cpu_seconds / max(t1, 1e-3)))))
+    iters = args.parity_iters
     tc = time.perf_counter()
     done = cpu_run(iters)
     tcpu = time.perf_counter() - tc
@@ -427,20 +478,51 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
         log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {stored_bytes/1e9:.3f} GB stored -> {achieved:.1f} GB/s "
             f"(CSR-equivalent {csr_gbs:.1f} GB/s); host peak RSS {peak_rss_gb():.1f} GB")
 
-    cpu, parity, parity_detail, parity_pcg = None, None, None, None
+    cpu, parity, parity_detail, parity_pcg, slab = None, None, None, None, None
     if rank == 0 and not light and args.cpu_cycles > 0 and world == 1 and comm is None:
         cpu, u_orc, iters, O = oracle_cpu_baseline(amg, nrows, f"{nx}x{ny}x{nz}", pcg, args)
         parity, parity_detail = gpu_parity(hv, amg, krylov, A, b, x, u_orc, iters, pcg)
+        if not pcg:
+            # the oracle-equal iterate, cut where an N-rank run's slabs end
+            key = digest_key(args, nx, ny, nz, iters)
+            slab = {"iterations": iters, "key": key, "equal_to_oracle": parity_detail["equal"],
+                    "digests": slab_digests_of(u_orc, nx, ny, nz)}
+            log(f"[bench] slab digests ({key}): whole {slab['digests']['1'][0][:16]}...")
         del u_orc
         if not pcg and args.pcg_iters > 0:
             parity_pcg = pcg_parity(hv, amg, A, b, x, O, nrows, args.pcg_iters)
         del O
-    elif rank == 0 and not light and world > 1:
+    if not light and world > 1 and args.parity_iters > 0 and not pcg:
         # bench contract: the CPU baseline is timed at N = 1 only.  Under strong
-        # scaling the N = 1 line runs this same global problem, so its
-        # cpu_baseline is this line's too; N-rank iterates equal the 1-rank
-        # iterates bit for bit (tests/test_gpu_multirank.py, loopback + RCCL).
-        parity = "bitwise vs 1 rank (tests/test_gpu_multirank.py)"
+        # scaling the N = 1 line runs this same global problem and prints the
+        # digests of its oracle-equal iterate cut at the N-rank slab
+        # boundaries; here every rank solves the same iterations from x = 0 and
+        # rank 0 compares the gathered 32-byte digests of the rank iterates
+        # (the halo exchange of par_csr_communication.c:298 is on this path)
+        x.fill(0.0)
+        amg.set(max_iter=args.parity_iters)
+        amg.solve(A, b, x)
+        mine = (A.first, sha256_f64(x.get()))
+        got = sorted(gather(mine))
+        if rank == 0:
+            key = digest_key(args, nx, ny, nz, args.parity_iters)
+            ref = golden_slab_digests(key)
+            cuts = slab_rows(nx, ny, nz, world)
+            dig = [d for _, d in got]
+            same_cut = [f for f, _ in got] == [f for f, _ in cuts]
+            # hybrid GS blocks follow the ranks (par_relax.c: each process's
+            # threads sweep its own rows), so its N-rank iterate is not the
+            # 1-rank one and has no N = 1 reference
+            want = (ref or {}).get(str(world)) if args.relax >= 0 else None
+            equal = (dig == want and same_cut) if want is not None else None
+            parity = {"kind": "slab sha256 vs N=1", "equal": equal, "iterations": args.parity_iters,
+                      "key": key, "rank_digests": dig, "rank_first_rows": [f for f, _ in got],
+                      "reference": ("tests/golden/slab_digests.json (N = 1 bench line; its iterate is bitwise "
+                                    "equal to the C oracle's)") if want is not None else
+                      "no committed N = 1 digests for this workload: compare rank_digests with the N = 1 line's "
+                      "slab_digests"}
+            log(f"[bench] slab parity vs N=1 after {args.parity_iters} iterations: "
+                f"{'bitwise' if equal else ('MISMATCH' if equal is False else 'no reference')}")
     comm_stats = None
     if world > 1:
         # this rank's communication per V-cycle, per level (the solve loop adds
@@ -494,6 +576,8 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
         out["parity_detail"] = parity_detail
     if parity_pcg is not None:
         out["parity_pcg"] = parity_pcg
+    if slab is not None:
+        out["slab_digests"] = slab
     if world > 1:
         out["cpu_baseline_note"] = ("timed at N = 1 only (bench contract); strong scaling: the N = 1 line runs "
                                     "the same global problem") if strong else "timed at N = 1 only (bench contract)"
@@ -540,8 +624,10 @@ def main():
                          "Gauss-Seidel 13/14 with the automatic block count")
     ap.add_argument("--coarsen", type=int, choices=[8, 10], default=8, help="8: PMIS (the bench line), 10: HMIS")
     ap.add_argument("--cpu-cycles", type=int, default=1, help="run the CPU baseline (0 = skip)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target length of the CPU baseline sample")
-    ap.add_argument("--cpu-cycles-max", type=int, default=60)
+    ap.add_argument("--parity-iters", type=int, default=8,
+                    help="solve iterations from x = 0 that the CPU baseline times and the parity checks compare "
+                         "(N = 1: GPU vs the C oracle, bitwise, plus the slab digests; N > 1: the rank slabs' "
+                         "sha256 against the N = 1 digests)")
     ap.add_argument("--spmv-reps", type=int, default=50)
     ap.add_argument("--pcg-iters", type=int, default=4,
                     help="one GPU: configs[2]'s BoomerAMG-PCG on the bench hierarchy for this many iterations, "

@@ -1463,6 +1463,9 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleStats(HYPRE_Solver s, HYPRE_Int level, HYPR
 // (column, value) sequence rebuilt from its slice's pattern equals the CSR row
 // entry for entry (bit patterns of the values included).  *width = 0 when the
 // operator is not a constant-coefficient stencil (the layout does not build).
+HYPRE_Int hypreve_GridStencilAddressable(HYPRE_BigInt nx, HYPRE_BigInt ny, HYPRE_BigInt nz) {
+  return grid_stencil_addressable(nx, ny, nz) ? 1 : 0;
+}
 HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int* width,
                                               HYPRE_Int* npatterns) {
   CHECK_ARG(s && s->kind == KIND_AMG && !s->H.lev.empty(), 1);

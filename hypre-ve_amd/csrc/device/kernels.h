@@ -83,6 +83,9 @@ enum : int {
 // nrm (K_RESID_L1JAC on the delta layout only): the residual's squares summed
 // per workgroup into nrm[0 .. sell_nrm_parts(M)) (y may then be null: r not stored).
 int sell_nrm_parts(const SellView& M);
+// The grid-stencil loop's 32-bit byte offsets reach every point of an
+// nx x ny x nz grid (DevSell::build_grid refuses the grid form otherwise).
+bool grid_stencil_addressable(int64_t nx, int64_t ny, int64_t nz);
 hipError_t launch_sell(int op, const SellView& M, const double* x, const double* b, const double* l1,
                        const int* cf, int relax_points, double* y, double w, double temp, hipStream_t s,
                        double* y2 = nullptr, double* nrm = nullptr);

@@ -1933,13 +1933,12 @@ struct GsArgs {
 static constexpr int kGsWaves = 4;           // teams per workgroup
 static constexpr int kGsProd = 512;          // LDS products per wave and chunk
 static constexpr int kGsPer = kGsProd / 64;  // entries per lane and chunk
-// U stores leave the ring in batches of kGsBatch steps: on CDNA a load waits
-// for every older vector-memory operation, stores included, so a store per
-// step would put a store's completion on every step's critical path.  A batch
-// is fenced before the next one is issued (kGsBatch steps later), so a value
-// reaches U at most 2 kGsBatch - 1 <= kGsFence steps after it was computed.
-static constexpr int kGsBatch = kGsRing / 2;
-static_assert(2 * kGsBatch - 1 <= kGsFence && kGsFence < kGsRing, "ring reach");
+// U stores leave the ring in batches of kGsBatch steps (host/layout.hpp): on
+// CDNA a load waits for every older vector-memory operation, stores included,
+// so a store per step would put a store's completion on every step's critical
+// path.  A batch is fenced before the next one is issued (kGsBatch steps
+// later), so a value reaches U at most 2 kGsBatch - 1 <= kGsFence steps after
+// it was computed; gs_schedule_self_check emulates exactly this rule.
 
 // Buffer loads with 32-bit offsets from wave-uniform bases: no 64-bit address
 // arithmetic in VGPRs (whose register reuse otherwise made the compiler wait
@@ -2908,6 +2907,12 @@ int grid_stencil_blocks(const SellView& M) {
   const int ty = grid_stencil_ty();
   const int nt = (M.gnx / kWave) * ((M.gny + ty - 1) / ty) * ((M.gz1 - M.gz0 + M.gzc - 1) / M.gzc);
   return std::max(8, (nt + 7) / 8 * 8);
+}
+// k_grid_stencil forms 32-bit buffer byte offsets into x, b and l1 (grid
+// points * 8) and keeps 0xFFFFFFF0 as the off-grid offset, and its row indices
+// are 32-bit: the grid must stay below 2^29 - 2 points.
+bool grid_stencil_addressable(int64_t nx, int64_t ny, int64_t nz) {
+  return nx > 0 && ny > 0 && nz > 0 && nx * ny * nz * 8 < (int64_t)0xFFFFFFF0ll;
 }
 int sell_nrm_parts(const SellView& M) {
   if (M.slot_mask && grid_stencil_on(M)) return grid_stencil_waves() * grid_stencil_blocks(M);  // one per wave

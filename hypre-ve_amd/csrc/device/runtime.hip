@@ -113,6 +113,7 @@ bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::ve
   if (nx % 64 || ny < 3 || nlocal % P || shift % P || (int64_t)nx * ny * nzs != A.nrows) return false;
   const int nz = (int)(nlocal / P);
   if (nz < 3 || shift / P + nzs > nz) return false;
+  if (!grid_stencil_addressable(nx, ny, nz)) return false;  // the per-slice loop takes it
   for (int64_t k = 0; k < A.nnz(); ++k)
     if (A.j[k] >= nlocal) return false;  // a halo column
   const int W = stencil_w;
@@ -860,6 +861,7 @@ void DevAMG::release() {
   u0_buf_[0] = u0_buf_[1] = nullptr; x0_buf_ = nullptr; dot_part_ = nullptr; dscal_ = nullptr;
   if (nrm_part_) (void)hipFree(nrm_part_);
   nrm_part_ = nullptr;
+  nrm_cap_ = 0;
   if (hscal_) (void)hipHostFree(hscal_);
   hscal_ = nullptr;
   for (auto& s : scratch_) { if (s) (void)hipFree(s); s = nullptr; }
@@ -887,12 +889,33 @@ void DevAMG::init_workspace(int n, DevComm* comm) {
   dot_part_ = dalloc<double>(1024);
   // fused norms / dots: one partial per row block (delta kernels), per wave
   // (stencil kernel) or per workgroup (PCG update)
-  nrm_part_ = dalloc<double>(std::max<size_t>(4 * ((size_t)n / 256 + 32), 4096));
+  nrm_cap_ = std::max<size_t>(std::max<size_t>(4 * ((size_t)n / 256 + 32), 4096), (size_t)pcg_xr_parts());
+  nrm_part_ = dalloc<double>(nrm_cap_);
   dscal_ = dalloc<double>(16);
   HVE_HIP(hipMemset(dscal_, 0, 16 * sizeof(double)));
   HVE_HIP(hipHostMalloc((void**)&hscal_, 16 * sizeof(double), hipHostMallocDefault));
   for (auto& s : scratch_) s = dalloc<double>(n);
   ws_n_ = n;
+}
+
+// The fused level-0 norms / dots (OP_RESID_L1JAC with a norm, the PCG
+// matvec-dot) write sell_nrm_parts(in) + sell_nrm_parts(bd) partials: one per
+// wave on the grid-stencil loop, which a thin grid (ny of a few points: every
+// tile mostly empty rows) makes far more than the rows / 64 the workspace
+// starts with.
+void DevAMG::size_nrm_parts() {
+  if (lev_.empty()) return;
+  const DevLevel& L = lev_[0];
+  size_t need = (size_t)pcg_xr_parts();
+  if (L.A.in.nrows > 0 || L.A.bd.nrows > 0) {
+    size_t np = L.A.in.nrows > 0 ? (size_t)sell_nrm_parts(L.A.in.view()) : 0;
+    if (L.A.bd.nrows > 0) np += (size_t)sell_nrm_parts(L.A.bd.view());
+    need = std::max(need, np);
+  }
+  if (need <= nrm_cap_) return;
+  if (nrm_part_) (void)hipFree(nrm_part_);
+  nrm_part_ = dalloc<double>(need);
+  nrm_cap_ = need;
 }
 
 // Plane and line strides of a structured-grid operator, read off its column
@@ -1484,6 +1507,11 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       const CSR rows = merged_rows(L.A, L.n_loc);
       const std::vector<int> bs = L.gs_blocks.empty() ? hypre_block_starts(L.n_loc, prm.blocks_for(L.n_loc)) : L.gs_blocks;
       const bool weighted = prm.wt(l) != 1.0 || prm.omega(l) != 1.0;  // the w / omega forms also read tmp in-block
+      // k_hybrid_gs addresses G (T | C | U | halo) with 32-bit buffer offsets
+      if ((3 * (uint64_t)D.n + (uint64_t)D.hu.n_halo) * sizeof(double) > 0xffffffffull)
+        throw std::runtime_error("hybrid Gauss-Seidel (relax 3/4/6/8/13/14): level " + std::to_string(l) + " has " +
+                                 std::to_string(D.n) + " rows on this rank; the sweep's vectors (3 n + halo doubles) "
+                                 "must stay below 4 GiB (about 178M rows a GPU): use more ranks or relax 18");
       if (fwd) D.gs_fwd.upload(rows, bs, true, weighted, L.l1, L.cf);
       if (bwd) D.gs_bwd.upload(rows, bs, false, weighted, L.l1, L.cf);
       D.gs_G = dalloc<double>(3 * (size_t)D.n + D.hu.n_halo + 1);
@@ -1492,6 +1520,7 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     }
   }
   build_rr(R, fc0);
+  size_nrm_parts();
   coarse_n_ = R.coarse_n;
   if (coarse_n_ > 0) {
     std::vector<double> Lf, U;

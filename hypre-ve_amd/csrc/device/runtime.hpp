@@ -333,6 +333,9 @@ class DevAMG {
   double* x0_buf_ = nullptr;                // fine_apply input with halo space
   double* dot_part_ = nullptr;
   double* nrm_part_ = nullptr;
+  size_t nrm_cap_ = 0;  // doubles in nrm_part_
+  // grow nrm_part_ to hold the partials of level 0's fused norms / dots
+  void size_nrm_parts();
   double* dscal_ = nullptr;  // device scalars
   double* hscal_ = nullptr;  // pinned host scalars
   double* scratch_[4] = {nullptr, nullptr, nullptr, nullptr};

@@ -709,6 +709,8 @@ void gs_levels(const CSR& A, const std::vector<int>& block_start, bool forward, 
 }
 }  // namespace
 
+int knob(int id);  // kernels.hip (tests' knobs)
+
 void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool forward, GsSchedule& S,
                        int team_rows, bool with_tcol, const std::vector<double>* l1, const std::vector<int>* cf) {
   const int n = A.nrows, nb = (int)block_start.size() - 1;
@@ -717,6 +719,11 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
   S = GsSchedule();
   S.block_start = block_start;
   team_rows = std::max(1, team_rows);
+  // ring reach: values computed up to kGsFence steps earlier come from the LDS
+  // ring, older ones from U.  Knob 11 (tests only) shortens it, which hands U
+  // values out before the kernel's fences publish them: gs_schedule_self_check
+  // must then refuse the schedule.
+  const int reach = kGsFence - std::max(0, std::min(kGsFence - 1, knob(11)));
   GsLevels G;
   gs_levels(A, block_start, forward, G);
   // teams of consecutive blocks, about team_rows rows per team level
@@ -833,7 +840,7 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
           if (with_tcol) S.tcol[p] = pos[c];
           const int d = (int)sx - st_of[c];
           if (c == i || d < 1) S.code[p] = n + pos[c];  // C
-          else if (d <= kGsFence) S.code[p] = -2 - (((st_of[c] - s0) % kGsRing) * 64 + ln_of[c]);
+          else if (d <= reach) S.code[p] = -2 - (((st_of[c] - s0) % kGsRing) * 64 + ln_of[c]);
           else S.code[p] = 2 * n + pos[c];  // U
         }
       }
@@ -900,7 +907,9 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
     }
   }
   // the kernel's view: C / T / F permuted into the sweep order, U stores
-  // visible at the fences only, the LDS ring keeps the last kGsRing steps
+  // visible only as k_hybrid_gs makes them (a batch's stores are issued at its
+  // last step and completed by the fence at the next batch's last step), the
+  // LDS ring keeps the last kGsRing steps
   std::vector<double> C(n), T(n), F(n), U(n, std::nan(""));
   std::vector<int> inv(n, -1);
   for (int k = 0; k < n; ++k) {
@@ -916,7 +925,7 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
   for (int t = 0; t < S.nteams; ++t) {
     const int s0 = S.team_step[t];
     std::vector<double> ring((size_t)kGsRingSlots, std::nan(""));
-    std::vector<std::pair<int, double>> pending;
+    std::vector<std::pair<int, double>> batch, issued;  // this batch's values; stores issued, not fenced
     for (int s = s0; s < S.team_step[t + 1]; ++s) {
       const int* m = &S.step[(size_t)s * 4];
       const size_t base = (uint32_t)m[0];
@@ -989,13 +998,14 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
         }
       }
       for (int q = 0; q < cnt; ++q) {
-        pending.push_back({m[1] + q, out[q]});
+        batch.push_back({m[1] + q, out[q]});
         u[S.rowmap[m[1] + q]] = out[q];
         ring[(size_t)(j % kGsRing) * 64 + q] = out[q];
       }
-      if (j % kGsFence == kGsFence - 1) {
-        for (auto& pr : pending) U[pr.first] = pr.second;
-        pending.clear();
+      if (j % kGsBatch == kGsBatch - 1 || s + 1 == S.team_step[t + 1]) {
+        for (auto& pr : issued) U[pr.first] = pr.second;  // the fence completes the previous batch
+        issued.swap(batch);                                // then this batch's stores are issued
+        batch.clear();
       }
     }
   }

@@ -115,6 +115,13 @@ int64_t sell_padded_nnz(const CSR& A, int sigma);
 constexpr int kGsRing = HVE_GS_RING;
 constexpr int kGsFence = kGsRing - 1;
 constexpr int kGsRingSlots = kGsRing * 64;
+// U stores leave the ring in batches of kGsBatch steps (k_hybrid_gs): at the
+// end of a batch the wave fences, which completes the previous batch's stores,
+// then issues this batch's.  A value computed at step q is therefore visible
+// in U from step (q / kGsBatch + 2) * kGsBatch on, at most 2 kGsBatch steps
+// later: U codes need a distance of kGsFence + 1 >= 2 kGsBatch steps.
+constexpr int kGsBatch = kGsRing / 2;
+static_assert(2 * kGsBatch <= kGsFence + 1 && kGsFence < kGsRing, "ring reach");
 struct GsSchedule {
   std::vector<int> block_start;  // nb + 1 row boundaries (hypre's ns / ne)
   std::vector<int> team_step;    // nteams + 1: step range of each team

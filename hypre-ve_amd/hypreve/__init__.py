@@ -195,6 +195,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGGetCycleCommStats", _i, [_p, _i, _pi64]),
     ("hypreve_BoomerAMGGetFusedResidRestrict", _i, [_p, _pi]),
     ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
+    ("hypreve_GridStencilAddressable", _i, [_i, _i, _i]),
     ("hypreve_BoomerAMGCodedLayoutCheck", _i, [_p, _i, _i, _pi, _pi]),
     ("hypreve_SetKnob", _i, [_i, _i]),
     ("hypreve_BoomerAMGSetDeviceSetup", _i, [_p, _i]),

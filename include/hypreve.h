@@ -372,6 +372,10 @@ HYPRE_Int hypreve_BoomerAMGGsScheduleStats(HYPRE_Solver solver, HYPRE_Int level,
  * *npatterns = 0) when the operator is not a constant-coefficient stencil. */
 HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int *width,
                                               HYPRE_Int *npatterns);
+/* 1 when the grid-stencil loop (k_grid_stencil: 32-bit buffer byte offsets)
+ * can address an nx x ny x nz grid on one rank, else 0: a larger rank share
+ * keeps the per-slice stencil loop (no GPU needed). */
+HYPRE_Int hypreve_GridStencilAddressable(HYPRE_BigInt nx, HYPRE_BigInt ny, HYPRE_BigInt nz);
 /* Setup's heavy row loops on the GPU (default 1): ext+i interpolation and its
  * truncation, R = P^T and the Galerkin product RAP, byte for byte the host
  * functions' result (device/setup_dev.hip); 0 runs them on the host.  The

@@ -14,5 +14,5 @@ step() {
   case $rc in 0|1|2|5) return 0 ;; *) echo "=== stopping after $name (rc=$rc)"; exit $rc ;; esac
 }
 step pcg512 500 python bench.py --solver pcg --n 512 --secondary-n 0 --steps 10 --warmup 2 --cpu-cycles 0
-step aniso_agg512 500 python bench.py --coef 0.001,1,1 --agg 1 --n 512 --secondary-n 0 --steps 10 --warmup 2 --cpu-seconds 6
+step aniso_agg512 500 python bench.py --coef 0.001,1,1 --agg 1 --n 512 --secondary-n 0 --steps 10 --warmup 2
 echo "=== done"

@@ -13,7 +13,7 @@ step() {
   echo "=== $name rc=$rc"; tail -2 "$OUT/$name.log"
   case $rc in 0|1|2|5) return 0 ;; *) echo "=== stopping after $name (rc=$rc)"; exit $rc ;; esac
 }
-step hybrid_gs_256 400 python bench.py --n 256 --secondary-n 0 --relax -1 --steps 10 --warmup 2 --cpu-seconds 5
-step hmis_256 400 python bench.py --n 256 --secondary-n 0 --coarsen 10 --steps 10 --warmup 2 --cpu-seconds 5
-step stencil27_256 400 python bench.py --n 256 --secondary-n 0 --stencil 27 --steps 10 --warmup 2 --cpu-seconds 5
+step hybrid_gs_256 400 python bench.py --n 256 --secondary-n 0 --relax -1 --steps 10 --warmup 2
+step hmis_256 400 python bench.py --n 256 --secondary-n 0 --coarsen 10 --steps 10 --warmup 2
+step stencil27_256 400 python bench.py --n 256 --secondary-n 0 --stencil 27 --steps 10 --warmup 2
 echo "=== done"

@@ -6,6 +6,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "hypre-ve_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, ROOT)  # bench.py (slab digests)
 
 
 def pytest_configure(config):

@@ -22,6 +22,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "hypre-ve_amd"))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (slab cut and digests of the bench's N-rank parity)
 
 
 def gen(hv, stencil, nx, ny, nz, **part):
@@ -68,7 +70,8 @@ def main():
         b = hv.ParVector(A.n, b_glob[A.first:A.first + A.n], comm=comm, first=A.first, global_n=N)
         x = hv.ParVector(A.n, np.zeros(A.n), comm=comm, first=A.first, global_n=N)
         it, rr = amg.solve(A, b, x)
-        part = (A.first, x.get(), it, rr, amg.num_levels())
+        xl = x.get()
+        part = (A.first, xl, it, rr, amg.num_levels(), bench.sha256_f64(xl))
         gathered = [None] * world
         dist.all_gather_object(gathered, part)
         if rank == 0:
@@ -83,14 +86,21 @@ def main():
             b1 = hv.ParVector(N, b_glob)
             x1 = hv.ParVector(N, np.zeros(N))
             it1, rr1 = a1.solve(A1, b1, x1)
-            same = bool(np.array_equal(x1.get(), xN))
+            x1h = x1.get()
+            same = bool(np.array_equal(x1h, xN))
+            # bench.py's N-rank parity: each rank's sha256 against the 1-rank
+            # iterate cut at GenerateLaplacian's slab boundaries
+            cut = bench.slab_rows(nx, ny, nz, world)
+            digests_ok = [o[0] for o in gathered] == [f for f, _ in cut] and \
+                [o[5] for o in gathered] == [bench.sha256_f64(x1h[f:f + c]) for f, c in cut]
+            same = same and digests_ok
             its = [o[2] for o in gathered]
             good = same and all(i == it1 for i in its) and all(abs(o[3] - rr1) <= 1e-10 * rr1 for o in gathered) \
                 and gathered[0][4] == a1.num_levels()
             ok = ok and good
             results.append({"stencil": stencil, "grid": [nx, ny, nz], "relax": relax, "agglo_rows": agglo,
                             "num_blocks": nb, "iters": its, "iters_1rank": it1, "rel_res": rr1,
-                            "levels": a1.num_levels(), "bitwise": same, "ok": good})
+                            "levels": a1.num_levels(), "bitwise": same, "slab_digests": digests_ok, "ok": good})
             for o in (a1, A1, b1, x1):
                 o.destroy()
         for o in (amg, A, b, x):

@@ -35,3 +35,18 @@ def test_no_gpu_init_fails_loudly(hv):
     rc = hv.lib().HYPRE_Init()
     assert rc != 0
     hv.lib().HYPRE_ClearAllErrors()
+
+
+def test_grid_stencil_size_guard(hv):
+    """k_grid_stencil's 32-bit buffer byte offsets (kernels.hip, off-grid
+    offset 0xFFFFFFF0): DevSell::build_grid takes the grid form only below
+    2^29 - 2 points a rank and keeps the per-slice loop above, instead of
+    wrapping the offsets and reading zeros."""
+    f = hv.lib().hypreve_GridStencilAddressable
+    assert f(512, 512, 512) == 1          # the headline grid, one rank
+    assert f(512, 512, 2047) == 1         # 2^29 - 2^18 points
+    assert f(512, 512, 2048) == 0         # 2^29 points: offsets wrap
+    assert f(1024, 1024, 512) == 0
+    assert f(64, 8192, 1023) == 1
+    assert f(64, 8192, 1024) == 0
+    assert f(0, 4, 4) == 0

@@ -506,3 +506,77 @@ def test_grid_stencil_bitwise(gpu, orc, gen, n3, relax, wt, zc):
         xv, yv = hv.ParVector(n, u0), hv.ParVector(n, f_h)
         A.matvec(alpha, xv, beta, yv)
         assert np.array_equal(yv.get(), O.matvec(0, alpha, u0, beta, f_h)), (alpha, beta)
+
+
+def test_grid_stencil_thin_grid_norm_parts(gpu, orc):
+    """A thin grid (ny = 3: one line of tiles, every tile mostly empty lines)
+    on the grid-stencil loop gives far more per-wave norm partials (2048 tiles
+    x 8 waves) than rows / 64: the fused residual + first sweep with its norm
+    and the PCG matvec-dot must fit the workspace (DevAMG::size_nrm_parts) and
+    equal the oracle (solve: bitwise; norms and PCG: rtol)."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian(64, 3, 4096)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, relax_type=18, P_max_elmts=4)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup(A)
+    assert amg.level_layout(0, 0) == "grid-stencil"
+    O = orc.OracleAMG(amg)
+    n = A.n
+    rng = np.random.default_rng(5)
+    f_h = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    amg.set(tol=0.0, max_iter=3)
+    x = hv.ParVector(n, np.zeros(n))
+    it, rr = amg.solve(A, f, x)
+    xo = np.zeros(n)
+    st = O.solve(f_h, xo, 0.0, 3)
+    assert np.array_equal(x.get(), xo)
+    assert abs(rr - st["rel_res"]) <= RTOL_NORM * st["rel_res"]
+    # BoomerAMG-PCG on the same hierarchy: s = A p with <s, p> fused
+    amg.set(tol=0.0, max_iter=1)
+    kr = hv.PCG(tol=0.0, max_iter=4, two_norm=1)
+    kr.set_precond_amg(amg, setup=False)
+    kr.setup(A, f, x)
+    x.fill(0.0)
+    it_g, rr_g = kr.solve(A, f, x)
+    kr.destroy()
+    u = np.zeros(n)
+    it_o, rr_o = O.pcg(f_h, u, 0.0, 4, 1)
+    assert it_g == it_o == 4
+    assert np.linalg.norm(x.get() - u) <= 1e-9 * np.linalg.norm(u)
+
+
+@pytest.mark.parametrize("cycle_type,num_sweeps,relax", [(2, 1, 18), (2, 2, 18), (1, 2, 18), (2, 2, 13), (2, 1, 0)])
+def test_w_cycle_sweeps_bitwise(gpu, orc, cycle_type, num_sweeps, relax):
+    """cycle_type 2 (W-cycle: lev_counter, par_cycle.c:246-250 / :683-700) and
+    num_sweeps 2 on every level but the coarsest: a cycle from a random
+    iterate and a 4-iteration solve equal the oracle bit for bit, on a
+    hierarchy deep enough (64^3 and 24^3 levels below) that the W-cycle's
+    repeated coarse visits differ from the V-cycle (control below)."""
+    hv = gpu
+    A, amg, O = setup_pair(hv, orc, (48, 44, 40), coarsen_type=8, relax_type=relax, P_max_elmts=4,
+                           cycle_type=cycle_type, num_sweeps=num_sweeps)
+    info = amg.relax_info()
+    assert info["cycle_type"] == cycle_type
+    n = A.n
+    rng = np.random.default_rng(41)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    amg.cycle(f, u)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+    amg.set(tol=0.0, max_iter=4)
+    x = hv.ParVector(n, np.zeros(n))
+    amg.solve(A, f, x)
+    xo = np.zeros(n)
+    O.solve(f_h, xo, 0.0, 4)
+    assert np.array_equal(x.get(), xo)
+    if cycle_type == 2:
+        O.s.cycle_type = 1
+        uv = u0.copy()
+        O.cycle(f_h, uv)
+        assert not np.array_equal(uv, uo)
