@@ -584,6 +584,31 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
     return out
 
 
+def visible_gpus():
+    """GPUs this process may use, counted without loading the HIP runtime: the
+    KFD topology nodes with SIMDs (the GPUs; CPU nodes have none), limited by
+    a *_VISIBLE_DEVICES list when the launcher set one.  The launcher parent
+    then starts torch.distributed.run with nothing of the GPU initialised."""
+    topo = "/sys/class/kfd/kfd/topology/nodes"
+    n = 0
+    try:
+        for node in os.listdir(topo):
+            try:
+                with open(os.path.join(topo, node, "properties")) as f:
+                    props = dict(ln.split()[:2] for ln in f if len(ln.split()) >= 2)
+                if int(props.get("simd_count", "0")) > 0:
+                    n += 1
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([t for t in v.split(",") if t.strip()]))
+    return n
+
+
 def rank_threads():
     """OpenMP threads of this rank's host setup: the host cores this process may
     use, shared by the ranks of the node (LOCAL_WORLD_SIZE), and no more than an
@@ -649,8 +674,7 @@ def main():
         # one process per GPU: start the ranks under torch.distributed.run as a
         # child process (nothing here has touched the GPU) and exit with its code
         import subprocess
-        import torch
-        ndev = torch.cuda.device_count()  # counts devices without initialising one
+        ndev = visible_gpus()
         if ndev < args.gpus:
             log(f"[bench] --gpus {args.gpus} needs {args.gpus} GPUs on this node, found {ndev}")
             sys.exit(2)

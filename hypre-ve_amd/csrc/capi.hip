@@ -85,6 +85,7 @@ struct hypre_Solver_struct {
   bool device_setup = true;
   std::vector<int> gs_rank_starts;  // one GPU emulating the GS blocks of an N-rank run
   std::vector<int> rank_emul;       // one process emulating a reference N-rank setup (SetRankEmulation)
+  std::vector<int> coarsen_starts;  // one process coarsening HMIS as N ranks do (SetCoarsenRankStarts)
   // per level: those blocks and their l1 norms (host copies for the introspection calls)
   std::vector<std::vector<int>> gs_blocks_host;
   std::vector<std::vector<double>> gs_l1_host;
@@ -807,6 +808,20 @@ HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver s, HYPRE_Int nranks, con
   }
   return 0;
 }
+// HMIS on one process as the distributed setup of an N-rank run coarsens it
+// (each rank's Ruge first pass, per-rank random streams; dsetup.cpp
+// hmis_dist), everything else the one-process setup: with
+// SetGsRankStarts-free relax types the iterates then equal the N-rank ones.
+HYPRE_Int hypreve_BoomerAMGSetCoarsenRankStarts(HYPRE_Solver s, HYPRE_Int nranks, const HYPRE_Int* starts) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  CHECK_ARG(nranks <= 1 || starts, 3);
+  s->coarsen_starts.clear();
+  if (nranks > 1) {
+    for (int r = 0; r < nranks; ++r) CHECK_ARG(starts[r] <= starts[r + 1] && starts[0] == 0, 3);
+    s->coarsen_starts.assign(starts, starts + nranks + 1);
+  }
+  return 0;
+}
 HYPRE_Int hypreve_BoomerAMGSetRankEmulation(HYPRE_Solver s, HYPRE_Int nranks, const HYPRE_Int* starts) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(nranks <= 1 || starts, 3);
@@ -972,7 +987,7 @@ static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
       }
       for (int q = 0; q < (int)all[3 * r]; ++q) G.i[starts0[r] + q + 1] = (int)(nnzoff[r] + li[q + 1]);
     }
-    amg_setup(G, s->prm, s->H);
+    amg_setup(G, s->prm, s->H, nullptr, &starts0);  // HMIS per rank, as the distributed setup
     { CSR().swap(G); }  // the gathered matrix is level 0 of H now
     bufs.resize(size);
     std::vector<RankHierarchy> parts;
@@ -1117,7 +1132,7 @@ static void setup_dist(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
 
 static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   if (s->rank_emul.empty()) {
-    amg_setup(A->diag, s->prm, s->H);
+    amg_setup(A->diag, s->prm, s->H, nullptr, s->coarsen_starts.empty() ? nullptr : &s->coarsen_starts);
   } else {
     AMGParams prm = s->prm;
     prm.agglo_rows = 0;

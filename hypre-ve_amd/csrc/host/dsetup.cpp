@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <stdexcept>
 #include <thread>
 
@@ -146,9 +147,16 @@ void map_cols(CSR& M, const Universe& U) {
 // cf_init 3 (the aggressive second pass, setup.cpp coarsen_pmis(S2, 3)):
 // rows without strong connections become C points, and the first pass skips
 // the independent-set selection (only F points are decided there: order-free).
+// cf_init 1 (HMIS's second stage, hmis_dist): cf holds this rank's Ruge first
+// pass; the random measures come from one stream per rank (seed 2747 + rank
+// from the rank's first row, par_indepset.c:25 as hypre runs it on N
+// processes), rows with an off-rank strong connection restart undecided
+// (par_coarsen.c:2296), and the seeded first sweep reads only own-rank
+// markers (CF_marker_offd is still 0 there, :2348): it runs in row order on
+// each rank alone, as setup.cpp coarsen_pmis does with rank starts.
 void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& starts, HostComm& comm,
                std::vector<int>& cf, int cf_init = 0) {
-  const int size = comm.size();
+  const int size = comm.size(), rank = comm.rank();
   std::vector<int> mcount(n, 0);
   std::vector<std::vector<int>> contrib(size), got;
   for (int c : S.j) {
@@ -161,7 +169,8 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
   std::vector<double> measure(n);
   for (int r = 0; r < n; ++r) {
     measure[r] = (double)mcount[r];
-    measure[r] += hypre_rand_at((int64_t)first + r, 2747);  // par_indepset.c:25 at the global row
+    if (cf_init == 1) measure[r] += hypre_rand_at(r, 2747 + rank);  // the rank's own stream
+    else measure[r] += hypre_rand_at((int64_t)first + r, 2747);  // par_indepset.c:25 at the global row
   }
   std::vector<int> off;
   for (int c : S.j)
@@ -174,14 +183,33 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
     const int c = S.j[k];
     sidx[k] = (c >= first && c < first + n) ? c - first : -1 - gp.find(c);
   }
-  cf.assign(n, 0);
   std::vector<int> graph, graph2;
-  for (int r = 0; r < n; ++r) {
-    if (S.i[r + 1] - S.i[r] == 0) {
-      cf[r] = cf_init == 3 ? C_PT : SF_PT;
-      measure[r] = 0;
-    } else {
-      graph.push_back(r);
+  if (cf_init == 1) {
+    // the first pass's C points keep 1, the others restart (setup.cpp coarsen_pmis)
+    for (int r = 0; r < n; ++r) {
+      if (cf[r] == SF_PT) {
+        measure[r] = 0;
+        continue;
+      }
+      bool offd = false;
+      for (int k = S.i[r]; k < S.i[r + 1] && !offd; ++k) offd = sidx[k] < 0;
+      if (cf[r] == F_PT || offd) cf[r] = 0;
+      if (cf[r] == Z_PT) {
+        if (measure[r] >= 1.0 || S.i[r + 1] - S.i[r] > 0) { cf[r] = 0; graph.push_back(r); }
+        else cf[r] = F_PT;
+      } else {
+        graph.push_back(r);
+      }
+    }
+  } else {
+    cf.assign(n, 0);
+    for (int r = 0; r < n; ++r) {
+      if (S.i[r + 1] - S.i[r] == 0) {
+        cf[r] = cf_init == 3 ? C_PT : SF_PT;
+        measure[r] = 0;
+      } else {
+        graph.push_back(r);
+      }
     }
   }
   std::vector<double> gmeas;
@@ -224,6 +252,20 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
     }
     gp.push(gdem, cf.data(), [](int cur, int flag) { return flag ? 0 : cur; }, comm);
     gp.pull(cf.data(), gcf, comm);
+    if (cf_init == 1 && iter == 1) {
+      // the seeded sweep: row order, own-rank markers only (a neighbour j < i
+      // already holds its new marker)
+      for (int ig = 0; ig < gs; ++ig) {
+        const int i = graph[ig];
+        if (measure[i] < 1) cf[i] = F_PT;
+        if (cf[i] > 0) {
+          cf[i] = C_PT;
+        } else {
+          for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+            if (sidx[k] >= 0 && cf[sidx[k]] > 0) { cf[i] = F_PT; break; }
+        }
+      }
+    } else
 #pragma omp parallel for schedule(static)
     for (int ig = 0; ig < gs; ++ig) {
       const int i = graph[ig];
@@ -252,6 +294,33 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
     }
     graph.swap(graph2);
   }
+}
+
+// ---------------------------------------------------------------------------
+// HMIS (coarsen_type 10, hypre's default), distributed: par_coarsen.c:2774 as
+// hypre runs it on N processes.  Each rank's Ruge first pass (par_coarsen.c:874)
+// sees only the strong connections it owns (S_diag, local measures) with the
+// empty-row test over the whole row, then PMIS seeded with those C points
+// (pmis_dist cf_init 1).  setup.cpp coarsen_hmis with rank starts is the
+// one-process statement of the same thing (amg_setup's coarsen_starts).
+// measure_type 3: the aggressive second pass (agg_2: empty rows become C).
+// ---------------------------------------------------------------------------
+void hmis_dist(const Pattern& S, int first, int n, const std::vector<int>& starts, HostComm& comm, int measure_type,
+               std::vector<int>& cf) {
+  if (measure_type != 0 && measure_type != 3)
+    throw std::runtime_error("distributed HMIS needs local measures (measure_type 0)");
+  Pattern Sl;
+  Sl.n = n;
+  Sl.i.assign(n + 1, 0);
+  std::vector<int> full(n);
+  for (int i = 0; i < n; ++i) {
+    full[i] = S.i[i + 1] - S.i[i];
+    for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+      if (S.j[k] >= first && S.j[k] < first + n) Sl.j.push_back(S.j[k] - first);
+    Sl.i[i + 1] = (int)Sl.j.size();
+  }
+  coarsen_ruge_first_pass(Sl, nullptr, measure_type, 0, cf, full.data());
+  pmis_dist(S, first, n, starts, comm, cf, 1);
 }
 
 // ---------------------------------------------------------------------------
@@ -531,17 +600,32 @@ void multipass_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, 
 }
 
 // ---------------------------------------------------------------------------
-// Ext+i rows of the owned fine points (extpi_core over owned + ghost points).
+// A rank's ghost universe for the interpolations: its owned points, their
+// off-rank neighbours G1 (A rows fetched, S rows recomputed from them:
+// strength is row-local) and the points the G1 rows reach (G2: markers
+// only).  The rows of owned and G1 points are complete, so a row function of
+// an owned point, and of a G1 point it reads, sees exactly what it sees in
+// one process (ext+i, ext, and the matrix-matrix forms 16-18 / 2-stage).
 // ---------------------------------------------------------------------------
-void extpi_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, int first, int n,
-                const std::vector<int>& starts, const std::vector<int>& cstarts, double strong_threshold,
-                double max_row_sum, HostComm& comm, CSR& P) {
-  const int rank = comm.rank(), size = comm.size();
-  std::vector<int> f2c(n, -1);
-  int cc = cstarts[rank];
-  for (int i = 0; i < n; ++i)
-    if (cf[i] >= 0) f2c[i] = cc++;
-  // G1: off-rank neighbours of owned rows (their A and S rows are read)
+struct GhostUniverse {
+  Universe U;
+  CSR A;      // universe rows (G2-only points empty), universe columns
+  Pattern S;
+  GhostPlan gp;  // owned values -> the ghost part (gp.want == U.ghosts)
+  // owned values followed by the pulled ghost values: universe-indexed
+  std::vector<int> extend(const std::vector<int>& owned, HostComm& c) const {
+    std::vector<int> g, out(owned);
+    gp.pull(owned.data(), g, c);
+    out.insert(out.end(), g.begin(), g.end());
+    return out;
+  }
+};
+
+// diag_rows: G2-only points get a row holding a unit diagonal (the
+// whole-matrix builders read every F row's diagonal; no owned row reads them).
+void build_ghost_universe(const CSR& A, const Pattern& S, int first, int n, const std::vector<int>& starts,
+                          double strong_threshold, double max_row_sum, HostComm& comm, GhostUniverse& G,
+                          bool diag_rows = false) {
   std::vector<int> g1;
   for (int c : A.j)
     if (c < first || c >= first + n) g1.push_back(c);
@@ -549,63 +633,190 @@ void extpi_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, int 
   CSR AG1 = fetch_rows(A, first, starts, g1, comm);
   Pattern SG1;
   create_strength(AG1, strong_threshold, max_row_sum, SG1);
-  // G2: off-rank points the G1 rows reference
   std::vector<int> gh = g1;
   for (int c : AG1.j)
     if (c < first || c >= first + n) gh.push_back(c);
   sort_unique(gh);
-  Universe U;
-  U.first = first;
-  U.n = n;
-  U.ghosts = gh;
-  GhostPlan gp;
-  gp.build(gh, first, n, starts, comm);
-  std::vector<int> gcf, gf2c;
-  gp.pull(cf.data(), gcf, comm);
-  gp.pull(f2c.data(), gf2c, comm);
-  const int nU = U.size();
-  std::vector<int> cfU(nU), f2cU(nU);
-  for (int i = 0; i < n; ++i) { cfU[i] = cf[i]; f2cU[i] = f2c[i]; }
-  for (size_t k = 0; k < gh.size(); ++k) { cfU[n + k] = gcf[k]; f2cU[n + k] = gf2c[k]; }
-  // A and S over the universe: rows of owned points and of G1, others empty
-  CSR AU;
+  G.U.first = first;
+  G.U.n = n;
+  G.U.ghosts = gh;
+  G.gp.build(gh, first, n, starts, comm);
+  const int nU = G.U.size();
+  CSR& AU = G.A;
+  Pattern& SU = G.S;
   AU.resize_rows(nU, nU);
-  Pattern SU;
   SU.n = nU;
   SU.i.assign(nU + 1, 0);
   std::vector<int> g1pos(g1.size());
-  for (size_t k = 0; k < g1.size(); ++k) g1pos[k] = U.loc(g1[k]);
-  {
-    std::vector<int> rowlenA(nU, 0), rowlenS(nU, 0);
-    for (int i = 0; i < n; ++i) { rowlenA[i] = A.i[i + 1] - A.i[i]; rowlenS[i] = S.i[i + 1] - S.i[i]; }
-    for (size_t k = 0; k < g1.size(); ++k) {
-      rowlenA[g1pos[k]] = AG1.i[k + 1] - AG1.i[k];
-      rowlenS[g1pos[k]] = SG1.i[k + 1] - SG1.i[k];
-    }
-    for (int u = 0; u < nU; ++u) { AU.i[u + 1] = AU.i[u] + rowlenA[u]; SU.i[u + 1] = SU.i[u] + rowlenS[u]; }
-    AU.j.resize(AU.i[nU]);
-    AU.a.resize(AU.i[nU]);
-    SU.j.resize(SU.i[nU]);
-    for (int i = 0; i < n; ++i) {
-      std::copy(A.j.begin() + A.i[i], A.j.begin() + A.i[i + 1], AU.j.begin() + AU.i[i]);
-      std::copy(A.a.begin() + A.i[i], A.a.begin() + A.i[i + 1], AU.a.begin() + AU.i[i]);
-      std::copy(S.j.begin() + S.i[i], S.j.begin() + S.i[i + 1], SU.j.begin() + SU.i[i]);
-    }
-    for (size_t k = 0; k < g1.size(); ++k) {
-      const int u = g1pos[k];
-      std::copy(AG1.j.begin() + AG1.i[k], AG1.j.begin() + AG1.i[k + 1], AU.j.begin() + AU.i[u]);
-      std::copy(AG1.a.begin() + AG1.i[k], AG1.a.begin() + AG1.i[k + 1], AU.a.begin() + AU.i[u]);
-      std::copy(SG1.j.begin() + SG1.i[k], SG1.j.begin() + SG1.i[k + 1], SU.j.begin() + SU.i[u]);
-    }
+  for (size_t k = 0; k < g1.size(); ++k) g1pos[k] = G.U.loc(g1[k]);
+  std::vector<int> rowlenA(nU, diag_rows ? 1 : 0), rowlenS(nU, 0);
+  for (int i = 0; i < n; ++i) { rowlenA[i] = A.i[i + 1] - A.i[i]; rowlenS[i] = S.i[i + 1] - S.i[i]; }
+  for (size_t k = 0; k < g1.size(); ++k) {
+    rowlenA[g1pos[k]] = AG1.i[k + 1] - AG1.i[k];
+    rowlenS[g1pos[k]] = SG1.i[k + 1] - SG1.i[k];
   }
-  map_cols(AU, U);
+  for (int u = 0; u < nU; ++u) { AU.i[u + 1] = AU.i[u] + rowlenA[u]; SU.i[u + 1] = SU.i[u] + rowlenS[u]; }
+  AU.j.resize(AU.i[nU]);
+  AU.a.resize(AU.i[nU]);
+  SU.j.resize(SU.i[nU]);
+  for (int i = 0; i < n; ++i) {
+    std::copy(A.j.begin() + A.i[i], A.j.begin() + A.i[i + 1], AU.j.begin() + AU.i[i]);
+    std::copy(A.a.begin() + A.i[i], A.a.begin() + A.i[i + 1], AU.a.begin() + AU.i[i]);
+    std::copy(S.j.begin() + S.i[i], S.j.begin() + S.i[i + 1], SU.j.begin() + SU.i[i]);
+  }
+  std::vector<char> filled(nU, 0);
+  for (size_t k = 0; k < g1.size(); ++k) {
+    const int u = g1pos[k];
+    filled[u] = 1;
+    std::copy(AG1.j.begin() + AG1.i[k], AG1.j.begin() + AG1.i[k + 1], AU.j.begin() + AU.i[u]);
+    std::copy(AG1.a.begin() + AG1.i[k], AG1.a.begin() + AG1.i[k + 1], AU.a.begin() + AU.i[u]);
+    std::copy(SG1.j.begin() + SG1.i[k], SG1.j.begin() + SG1.i[k + 1], SU.j.begin() + SU.i[u]);
+  }
+  if (diag_rows)
+    for (int u = n; u < nU; ++u)
+      if (!filled[u]) { AU.j[AU.i[u]] = G.U.glob(u); AU.a[AU.i[u]] = 1.0; }
+  map_cols(AU, G.U);
   for (auto& c : SU.j) {
-    const int l = U.loc(c);
+    const int l = G.U.loc(c);
     if (l < 0) throw std::runtime_error("distributed setup: strength column outside the ghost universe");
     c = l;
   }
-  int64_t ncoarse = cstarts[size];
-  extpi_core(AU, SU, cfU, f2cU, n, (int)ncoarse, nU, P);
+}
+
+// Global index of each owned point of class `sel` (cf > 0 by default) from
+// `cstart` on; -1 elsewhere.
+std::vector<int> class_index(const std::vector<int>& cf, int cstart, bool (*sel)(int)) {
+  std::vector<int> f2c(cf.size(), -1);
+  int cc = cstart;
+  for (size_t i = 0; i < cf.size(); ++i)
+    if (sel(cf[i])) f2c[i] = cc++;
+  return f2c;
+}
+bool is_c(int v) { return v > 0; }
+
+// Rows [0, nrows) of a universe product P (columns: the universe's points of
+// the column class in universe order, as fffc / extpi number them) with
+// global column indices: gidxU holds every universe point's global index in
+// that class (-1 outside it).
+CSR owned_rows_global_cols(const CSR& Pu, int nrows, const std::vector<int>& gidxU, int ncols_glob) {
+  std::vector<int> uc2g;
+  for (int v : gidxU)
+    if (v >= 0) uc2g.push_back(v);
+  CSR P;
+  P.resize_rows(nrows, ncols_glob);
+  for (int r = 0; r < nrows; ++r) P.i[r + 1] = Pu.i[r + 1];
+  P.j.assign(Pu.j.begin(), Pu.j.begin() + Pu.i[nrows]);
+  P.a.assign(Pu.a.begin(), Pu.a.begin() + Pu.i[nrows]);
+  for (int& c : P.j) c = uc2g.at(c);
+  return P;
+}
+
+// ---------------------------------------------------------------------------
+// Ext+i (plus_i) or ext (interp_type 14, par_lr_interp.c:4686) rows of the
+// owned fine points (extpi_core over the ghost universe).
+// ---------------------------------------------------------------------------
+void extpi_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, int first, int n,
+                const std::vector<int>& starts, const std::vector<int>& cstarts, double strong_threshold,
+                double max_row_sum, HostComm& comm, CSR& P, bool plus_i) {
+  const int rank = comm.rank(), size = comm.size();
+  std::vector<int> f2c(n, -1);
+  int cc = cstarts[rank];
+  for (int i = 0; i < n; ++i)
+    if (cf[i] >= 0) f2c[i] = cc++;
+  GhostUniverse G;
+  build_ghost_universe(A, S, first, n, starts, strong_threshold, max_row_sum, comm, G);
+  const std::vector<int> cfU = G.extend(cf, comm), f2cU = G.extend(f2c, comm);
+  extpi_core(G.A, G.S, cfU, f2cU, n, (int)cstarts[size], G.U.size(), P, plus_i);
+}
+
+// ---------------------------------------------------------------------------
+// The matrix-matrix interpolations over the ghost universe (setup.cpp:
+// par_mod_lr_interp.c's ModExt 16 / ModExtPI 17 / ModExtPE 18, and the
+// 2-stage agg_interp_type 5 / 7 of par_amg_setup.c:1575-1689): the one-process
+// builders run on the universe, and the owned rows are kept.  Every owned row
+// reads only owned and G1 rows (its F neighbours' As_FF / As_FC rows and their
+// scalings), so it is the one-process row.  hypre_ParMatmul's allsquare is
+// decided by the global sizes; a square product (a zero diagonal at the
+// row's own index) is refused.
+// ---------------------------------------------------------------------------
+int64_t L0_rows_glob(HostComm& comm, int n) { return comm.allreduce_sum((int64_t)n); }
+
+int mm_square_global(int64_t rows_glob, int64_t cols_glob) {
+  if (rows_glob == cols_glob)
+    throw std::runtime_error("distributed setup: square interpolation product (hypre_ParMatmul allsquare)");
+  return 0;
+}
+
+void mm_interp_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, int first, int n,
+                    const std::vector<int>& starts, const std::vector<int>& cstarts, const AMGParams& prm,
+                    HostComm& comm, CSR& P) {
+  const int rank = comm.rank(), size = comm.size();
+  GhostUniverse G;
+  build_ghost_universe(A, S, first, n, starts, prm.strong_threshold, prm.max_row_sum, comm, G, true);
+  const std::vector<int> cfU = G.extend(cf, comm);
+  const std::vector<int> gcU = G.extend(class_index(cf, cstarts[rank], is_c), comm);
+  int64_t nf = 0;
+  for (int v : cf) nf += v < 0;
+  const int sq = mm_square_global(comm.allreduce_sum(nf), cstarts[size]);
+  CSR Pu;
+  if (prm.interp_type == 16) build_modext_interp(G.A, cfU, G.S, prm.trunc_factor, prm.P_max_elmts, false, Pu, nullptr, sq);
+  else if (prm.interp_type == 17) build_modextpi_interp(G.A, cfU, G.S, prm.trunc_factor, prm.P_max_elmts, Pu, nullptr, sq);
+  else build_modextpe_interp(G.A, cfU, G.S, prm.trunc_factor, prm.P_max_elmts, Pu, nullptr, sq);
+  P = owned_rows_global_cols(Pu, n, gcU, cstarts[size]);
+}
+
+// 2-stage aggressive interpolation: cf1 the first stage's markers (> 0: its C
+// points, numbered by c1starts), cf the corrected ones (1: C of both stages,
+// -2: C of the first only).  P1 (fine -> first-stage C) and P2 (first-stage C
+// -> C) over the universe, each truncated by the P12 limits; P = P1 P2 with
+// the P2 rows of off-rank first-stage C points fetched, then the aggressive
+// truncation.
+void twostage_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf1, const std::vector<int>& cf, int first,
+                   int n, const std::vector<int>& starts, const std::vector<int>& c1starts,
+                   const std::vector<int>& cstarts, const AMGParams& prm, HostComm& comm, CSR& P) {
+  const int rank = comm.rank(), size = comm.size();
+  const bool pe = prm.agg_interp_type == 7;
+  GhostUniverse G;
+  build_ghost_universe(A, S, first, n, starts, prm.strong_threshold, prm.max_row_sum, comm, G, true);
+  const std::vector<int> cf1U = G.extend(cf1, comm), cfU = G.extend(cf, comm);
+  const std::vector<int> g1U = G.extend(class_index(cf1, c1starts[rank], is_c), comm);
+  const std::vector<int> g2U = G.extend(class_index(cf, cstarts[rank], is_c), comm);
+  int64_t nf1 = 0, nc1 = 0;
+  for (int v : cf1) { nf1 += v < 0; nc1 += v > 0; }
+  CSR P1u, P2u;
+  build_modext_interp(G.A, cf1U, G.S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P1u, nullptr,
+                      mm_square_global(comm.allreduce_sum(nf1), c1starts[size]));
+  int64_t nf2 = 0;  // As_FF's rows in the partial form: the first stage's C points only (-2)
+  for (int v : cf) nf2 += v == -2;
+  build_modpartialext_interp(G.A, cfU, G.S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P2u, nullptr,
+                             mm_square_global(comm.allreduce_sum(nf2), cstarts[size]));
+  const CSR P1 = owned_rows_global_cols(P1u, n, g1U, c1starts[size]);
+  // P2's rows are the universe's first-stage C points in universe order: the owned ones first
+  const CSR P2 = owned_rows_global_cols(P2u, (int)nc1, g2U, cstarts[size]);
+  // P1's columns -> rows of [owned P2 rows | fetched P2 rows]
+  const int c1first = c1starts[rank];
+  std::vector<int> want;
+  for (int c : P1.j)
+    if (c < c1first || c >= c1first + (int)nc1) want.push_back(c);
+  sort_unique(want);
+  const CSR P2g = fetch_rows(P2, c1first, c1starts, want, comm);
+  CSR Y;
+  Y.resize_rows((int)nc1 + P2g.nrows, cstarts[size]);
+  for (int r = 0; r < (int)nc1; ++r) Y.i[r + 1] = P2.i[r + 1];
+  for (int r = 0; r < P2g.nrows; ++r) Y.i[nc1 + r + 1] = P2.i[nc1] + P2g.i[r + 1];
+  Y.j = P2.j;
+  Y.a = P2.a;
+  Y.j.insert(Y.j.end(), P2g.j.begin(), P2g.j.end());
+  Y.a.insert(Y.a.end(), P2g.a.begin(), P2g.a.end());
+  CSR X = P1;
+  X.ncols = Y.nrows;
+  for (int& c : X.j) {
+    if (c >= c1first && c < c1first + (int)nc1) c -= c1first;
+    else c = (int)nc1 + (int)(std::lower_bound(want.begin(), want.end(), c) - want.begin());
+  }
+  multiply_interp(X, Y, prm.agg_trunc_factor, prm.agg_P_max_elmts, P,
+                  mm_square_global(L0_rows_glob(comm, n), cstarts[size]));
+  P.ncols = cstarts[size];
 }
 
 // ---------------------------------------------------------------------------
@@ -764,6 +975,121 @@ void l1_dist(const CSR& A, int first, int nglob, int option, const std::vector<i
     if (A.a[A.i[i]] < 0.0) l1[i] = -l1[i];
 }
 
+// ---------------------------------------------------------------------------
+// Chebyshev smoother data (relax 16) with the one-process result, distributed:
+// par_relax_more.c:115 hypre_ParCSRMaxEigEstimateCG's start vector takes
+// hypre_Rand at the global row (the one-process stream), the matvec reads the
+// ghost values of its vector, and every inner product is formed as the
+// one-process loop forms it: a running sum handed from rank to rank in rank
+// order, each rank adding its rows to it.  The Lanczos tridiagonal, its
+// eigenvalues and the coefficients (par_cheby.c:36) are then the one-process
+// ones bit for bit.  par_relax_more.c:25's inf-norm bound is a max over rows.
+// ---------------------------------------------------------------------------
+double chain_dot(const std::vector<double>& x, const std::vector<double>& y, HostComm& comm) {
+  const int size = comm.size(), rank = comm.rank();
+  double s = 0.0;
+  for (int q = 0; q < size; ++q) {
+    int64_t bits = 0;
+    if (rank == q) {
+      for (size_t i = 0; i < x.size(); ++i) s += y[i] * x[i];  // hypre_SeqVectorInnerProd: y_i * x_i
+      std::memcpy(&bits, &s, sizeof bits);
+    }
+    const auto all = comm.allgather(bits);
+    std::memcpy(&s, &all[q], sizeof s);
+  }
+  return s;
+}
+
+void max_eig_cg_dist(const CSR& A, int first, int n, const std::vector<int>& starts, int scale, int max_iter,
+                     HostComm& comm, double* max_eig, double* min_eig) {
+  const int nglob = starts.back();
+  if (nglob < max_iter) max_iter = nglob;
+  std::vector<int> off;
+  for (int c : A.j)
+    if (c < first || c >= first + n) off.push_back(c);
+  GhostPlan gp;
+  gp.build(off, first, n, starts, comm);
+  std::vector<int> lc(A.j.size());
+  for (size_t k = 0; k < A.j.size(); ++k) {
+    const int c = A.j[k];
+    lc[k] = (c >= first && c < first + n) ? c - first : n + gp.find(c);
+  }
+  std::vector<double> r(n), p(n, 0.0), s(n, 0.0), ds(n), u(n, 0.0), xg, xfull;
+  std::vector<double> tridiag(max_iter + 1, 0.0), trioffd(max_iter + 1, 0.0);
+  for (int i = 0; i < n; ++i) r[i] = 2.0 * hypre_rand_at((int64_t)first + i, 1) - 1.0;
+  for (int i = 0; i < n; ++i) ds[i] = scale ? 1 / std::sqrt(A.a[A.i[i]]) : 1.0;
+  auto matvec = [&](const std::vector<double>& x, std::vector<double>& y) {
+    gp.pull(x.data(), xg, comm);
+    xfull = x;
+    xfull.insert(xfull.end(), xg.begin(), xg.end());
+    for (int row = 0; row < n; ++row) {
+      double t = 0.0;
+      for (int k = A.i[row]; k < A.i[row + 1]; ++k) t += A.a[k] * xfull[lc[k]];
+      y[row] = t;
+    }
+  };
+  double gamma = chain_dot(r, p, comm), gamma_old, beta = 1.0, alpha, alphainv;
+  int i = 0;
+  while (i < max_iter) {
+    s = r;
+    gamma_old = gamma;
+    gamma = chain_dot(r, s, comm);
+    if (i == 0) {
+      beta = 1.0;
+      p = s;
+    } else {
+      beta = gamma / gamma_old;
+      for (int k = 0; k < n; ++k) p[k] = s[k] + beta * p[k];
+    }
+    if (scale) {
+      for (int k = 0; k < n; ++k) u[k] = ds[k] * p[k];
+      matvec(u, s);
+      for (int k = 0; k < n; ++k) s[k] = ds[k] * s[k];
+    } else {
+      matvec(p, s);
+    }
+    const double sdotp = chain_dot(s, p, comm);
+    alpha = gamma / sdotp;
+    alphainv = 1.0 / alpha;
+    tridiag[i + 1] = alphainv;
+    tridiag[i] *= beta;
+    tridiag[i] += alphainv;
+    trioffd[i + 1] = alphainv;
+    trioffd[i] *= std::sqrt(beta);
+    for (int k = 0; k < n; ++k) r[k] += (-alpha) * s[k];
+    i++;
+  }
+  linpack_tql1(i, tridiag.data(), trioffd.data());
+  *max_eig = tridiag[i - 1];
+  *min_eig = tridiag[0];
+}
+
+void max_eig_norm_dist(const CSR& A, int scale, HostComm& comm, double* max_eig) {
+  double max_norm = 0.0;
+  int64_t pos_diag = 0, neg_diag = 0;
+  for (int i = 0; i < A.nrows; ++i) {
+    double diag_value = A.a[A.i[i]];
+    if (diag_value > 0) pos_diag++;
+    if (diag_value < 0) { neg_diag++; diag_value = -diag_value; }
+    double row_sum = diag_value;
+    for (int j = A.i[i] + 1; j < A.i[i + 1]; ++j) row_sum += std::fabs(A.a[j]);
+    if (scale && diag_value != 0.0) row_sum = row_sum / diag_value;
+    if (row_sum > max_norm) max_norm = row_sum;
+  }
+  int64_t bits;
+  std::memcpy(&bits, &max_norm, sizeof bits);
+  double m = 0.0;
+  for (int64_t b : comm.allgather(bits)) {
+    double v;
+    std::memcpy(&v, &b, sizeof v);
+    if (v > m) m = v;
+  }
+  pos_diag = comm.allreduce_sum(pos_diag);
+  neg_diag = comm.allreduce_sum(neg_diag);
+  if (pos_diag == 0 && neg_diag > 0) m = -m;
+  *max_eig = m;
+}
+
 bool uses_l1_gs(int t) { return t == 8 || t == 13 || t == 14; }
 bool uses_hybrid_gs_any(const AMGParams& prm) {
   for (int c = 0; c < 4; ++c) {
@@ -777,6 +1103,7 @@ struct DLevel {
   CSR A, P, R;  // owned rows, global columns
   std::vector<int> cf;
   std::vector<double> l1;
+  std::vector<double> cheby_ds, cheby_coefs;  // relax 16 (owned rows; coefficients replicated)
   std::vector<int> starts;  // row starts of this level over the ranks
   int first = 0, nloc = 0, nglob = 0;
   int64_t nnz_glob = 0;
@@ -815,11 +1142,13 @@ void offrank_cols(const CSR& M, int a, int b, std::vector<int>& out) {
 
 bool dist_setup_supported(const AMGParams& prm, std::string* why) {
   auto no = [&](const char* w) { if (why) *why = w; return false; };
-  if (prm.coarsen_type != 8) return no("coarsen_type != 8 (PMIS)");
-  if (prm.interp_type != 6) return no("interp_type != 6 (ext+i)");
-  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4) return no("aggressive coarsening with agg_interp_type != 4");
-  for (int k = 0; k < 4; ++k)  // its eigenvalue estimate reduces over all rows in one order
-    if (prm.relax_type[k] == 16) return no("Chebyshev smoother (relax 16)");
+  if (prm.coarsen_type != 8 && prm.coarsen_type != 10) return no("coarsen_type not 8 (PMIS) or 10 (HMIS)");
+  if (prm.coarsen_type == 10 && (prm.measure_type != 0 || prm.coarsen_cut_factor != 0))
+    return no("HMIS with global measures or a cut factor");
+  if (prm.interp_type != 6 && prm.interp_type != 14 && (prm.interp_type < 16 || prm.interp_type > 18))
+    return no("interp_type not 6, 14, 16, 17 or 18");
+  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4 && prm.agg_interp_type != 5 && prm.agg_interp_type != 7)
+    return no("aggressive coarsening with agg_interp_type not 4, 5 or 7");
   return true;
 }
 
@@ -847,16 +1176,24 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     Pattern S;
     create_strength(L[level].A, prm.strong_threshold, prm.max_row_sum, S);
     std::vector<int> cf;
-    pmis_dist(S, first, n, L[level].starts, comm, cf);
+    if (prm.coarsen_type == 10) hmis_dist(S, first, n, L[level].starts, comm, prm.measure_type, cf);
+    else pmis_dist(S, first, n, L[level].starts, comm, cf);
     // aggressive level: PMIS again on S*S + 2S of the C points, and the second
     // marker refines the first (setup.cpp amg_setup, par_amg_setup.c:1239)
     const bool agg_lvl = level < prm.agg_num_levels;
+    std::vector<int> c1starts, cf1;
     if (agg_lvl) {
       Pattern S2;
-      std::vector<int> c1starts, cfn;
+      std::vector<int> cfn;
       second_strength_dist(S, cf, first, n, L[level].starts, prm.num_paths, comm, c1starts, S2);
-      pmis_dist(S2, c1starts[rank], S2.n, c1starts, comm, cfn, 3);
-      correct_cf_marker(cf, cfn);
+      if (prm.coarsen_type == 10) hmis_dist(S2, c1starts[rank], S2.n, c1starts, comm, prm.measure_type + 3, cfn);
+      else pmis_dist(S2, c1starts[rank], S2.n, c1starts, comm, cfn, 3);
+      if (prm.agg_interp_type == 4) {
+        correct_cf_marker(cf, cfn);
+      } else {
+        cf1 = cf;  // the first stage's markers, for P1
+        correct_cf_marker2(cf, cfn);
+      }
     }
     int64_t nc_loc = 0;
     for (int v : cf) nc_loc += (v == C_PT);
@@ -874,12 +1211,16 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     std::vector<int> cstarts(size + 1, 0);
     for (int p = 0; p < size; ++p) cstarts[p + 1] = cstarts[p] + (int)ncs[p];
     CSR P;
-    if (agg_lvl) {
+    if (agg_lvl && prm.agg_interp_type != 4) {
+      twostage_dist(L[level].A, S, cf1, cf, first, n, L[level].starts, c1starts, cstarts, prm, comm, P);
+    } else if (agg_lvl) {
       multipass_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm.agg_trunc_factor, prm.agg_P_max_elmts,
                      comm, P);
+    } else if (prm.interp_type >= 16 && prm.interp_type <= 18) {
+      mm_interp_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm, comm, P);
     } else {
       extpi_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm.strong_threshold, prm.max_row_sum, comm,
-                 P);
+                 P, prm.interp_type == 6);
       if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
       for (int i = 0; i < n; ++i)
         if (cf[i] == SF_PT) cf[i] = F_PT;
@@ -931,6 +1272,16 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
       l1_dist(D.A, D.first, D.nglob, 1, cfp, &gp, &gcf, 1, D.l1);
     else if (j == nl - 1 && prm.relax_type[3] == 18)
       l1_dist(D.A, D.first, D.nglob, 1, nullptr, nullptr, nullptr, 1, D.l1);
+    // par_amg_setup.c:3139: Chebyshev (relax 16) eigenvalue estimate and coefficients
+    if (prm.relax_type[1] == 16 || prm.relax_type[2] == 16 || (prm.relax_type[3] == 16 && j == nl - 1)) {
+      double max_eig = 0.0, min_eig = 0.0;
+      if (prm.cheby_eig_est)
+        max_eig_cg_dist(D.A, D.first, D.nloc, D.starts, prm.cheby_scale, prm.cheby_eig_est, comm, &max_eig, &min_eig);
+      else
+        max_eig_norm_dist(D.A, prm.cheby_scale, comm, &max_eig);
+      cheby_setup(D.A, max_eig, min_eig, prm.cheby_fraction, prm.cheby_order, prm.cheby_scale, prm.cheby_variant,
+                  D.cheby_coefs, D.cheby_ds);
+    }
     if (prm.relax_type[1] == 7 || prm.relax_type[2] == 7 || (prm.relax_type[3] == 7 && j == nl - 1)) {
       D.l1.resize(D.nloc);
       for (int r = 0; r < D.nloc; ++r) {
@@ -985,6 +1336,7 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
       }
       D.cf = comm.allgatherv(D.cf);
       D.l1 = comm.allgatherv(D.l1);
+      D.cheby_ds = comm.allgatherv(D.cheby_ds);
       // a replicated level is swept as one rank's rows: its hybrid-GS l1
       // norms over num_blocks blocks of the whole level
       bool cfr = false;
@@ -1039,6 +1391,8 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     }
     RL.l1 = D.l1;
     RL.cf = D.cf;
+    RL.cheby_ds = D.cheby_ds;
+    RL.cheby_coefs = D.cheby_coefs;
     if (size > 1 && uses_hybrid_gs_any(prm)) RL.gs_blocks = hypre_block_starts(D.nloc, prm.blocks_for(D.nloc));
     if (agg >= 0 && l >= agg) {
       RL.hu.n_loc = D.nloc;
@@ -1053,10 +1407,11 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
 
 int dist_setup_self_check(const CSR& A, const AMGParams& prm, int size, std::string& msg) {
   Hierarchy H;
-  amg_setup(A, prm, H);
   const int n0 = A.nrows;
   std::vector<int> s0(size + 1);
   for (int r = 0; r <= size; ++r) s0[r] = (int)((int64_t)n0 * r / size);
+  // HMIS: its first pass per rank (the one-process statement: coarsen_starts)
+  amg_setup(A, prm, H, nullptr, &s0);
   std::vector<RankHierarchy> ref;
   partition_hierarchy_all(H, s0, size, ref);
   auto comms = make_thread_host_comms(size);

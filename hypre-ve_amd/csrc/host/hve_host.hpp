@@ -263,10 +263,10 @@ void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P, bool plus_i = true);
 // extended+i in matrix-matrix form (interp_type 17, par_mod_lr_interp.c:474)
 void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P, const std::vector<int>* emul = nullptr);
+                           int max_elmts, CSR& P, const std::vector<int>* emul = nullptr, int mm_square = -1);
 // extended+e in matrix-matrix form (interp_type 18, par_mod_lr_interp.c:1040)
 void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P, const std::vector<int>* emul = nullptr);
+                           int max_elmts, CSR& P, const std::vector<int>* emul = nullptr, int mm_square = -1);
 void build_direct_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                          double trunc_factor, int max_elmts, CSR& P);
 void truncate_rows(CSR& P, double tol, int max_elmts);
@@ -278,11 +278,15 @@ void correct_cf_marker2(std::vector<int>& cf, const std::vector<int>& new_cf);
 // matrix-matrix interpolations (setup.cpp): ModExt (pe false) / ModExtPE, the
 // 2-stage second stage ModPartialExt, and P = P1 P2 with the aggressive truncation
 // emul: fine row starts of an emulated N-rank run (hypre_ParMatmul's np > 1 order)
+// mm_square: hypre_ParMatmul's allsquare decided by global sizes (0 / 1) rather
+// than by the product's own (-1): the distributed setup multiplies a rank's
+// ghost universe, whose sizes are not the matrix's
 void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                         int max_elmts, bool pe, CSR& P, const std::vector<int>* emul = nullptr);
+                         int max_elmts, bool pe, CSR& P, const std::vector<int>* emul = nullptr, int mm_square = -1);
 void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                                int max_elmts, bool pe, CSR& P, const std::vector<int>* emul = nullptr);
-void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P);
+                                int max_elmts, bool pe, CSR& P, const std::vector<int>* emul = nullptr,
+                                int mm_square = -1);
+void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P, int mm_square = -1);
 void build_multipass_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                             int max_elmts, CSR& P);
 // Universe-indexed cores of ext+i and RAP shared by the one-process and the
@@ -335,7 +339,14 @@ int l1_option_for_level(const AMGParams& prm, int j, int nl, bool* cf_restricted
 // rank_starts (optional, N+1 level-0 row starts): build the hierarchy an N-rank
 // hypre run builds (rows in ParCSR diag/offd order on every level, per-rank
 // coarsening); the solve path is unchanged.
-int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H, const std::vector<int>* rank_starts = nullptr);
+// coarsen_starts (optional, N+1 level-0 row starts): HMIS (coarsen_type 10)
+// as an N-process run coarsens, each rank's Ruge first pass over the strong
+// connections it owns and per-rank random streams in the PMIS stage, rank r
+// owning the C points of its rows on the next level; nothing else changes
+// (entry order, interpolation, RAP stay the one-process ones).  This is what
+// the distributed setup computes (dsetup.cpp hmis_dist); PMIS ignores it.
+int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H, const std::vector<int>* rank_starts = nullptr,
+              const std::vector<int>* coarsen_starts = nullptr);
 
 
 }  // namespace hve

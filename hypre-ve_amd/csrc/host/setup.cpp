@@ -1102,9 +1102,13 @@ struct MatmulRanks {
 // B row's other-rank columns (B_ext_offd) and then own ones (B_ext_diag); then
 // the own-column entries (A_diag), through B_diag then B_offd; the product row
 // is C_diag's first-touch list followed by C_offd's.
-static void matmul_first_touch(const CSR& X, const CSR& Y, CSR& C, const MatmulRanks* rk = nullptr) {
+// square_mode: -1 the product's own sizes decide hypre_ParMatmul's allsquare
+// (a zero diagonal entry first); 0 / 1 the caller's global sizes (the
+// distributed setup multiplies a rank's universe, not the whole matrix).
+static void matmul_first_touch(const CSR& X, const CSR& Y, CSR& C, const MatmulRanks* rk = nullptr,
+                               int square_mode = -1) {
   const int nr = X.nrows, nc = Y.ncols;
-  bool square = nr == nc;  // hypre_ParMatmul's allsquare: a zero diagonal entry first
+  bool square = square_mode < 0 ? nr == nc : square_mode != 0;
   std::vector<int> lrows, lcols;  // emulated: rows / Y columns per rank (allsquare is local too)
   if (rk) {
     lrows.assign(rk->nranks, 0);
@@ -1235,7 +1239,7 @@ static void assemble_mm_p(const std::vector<int>& cf, const std::vector<int>& ro
 // diagonal scalings of :1204-1318.  Extended (agg_interp_type 5's first
 // stage, pe = false): :16 hypre_BoomerAMGBuildModExtInterpHost, :170-245.
 void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                         int max_elmts, bool pe, CSR& P, const std::vector<int>* emul) {
+                         int max_elmts, bool pe, CSR& P, const std::vector<int>* emul, int mm_square) {
   CSR FF, FC;
   std::vector<int> frow, ffrow;
   fffc(A, cf, S, false, FF, FC, frow, ffrow);
@@ -1281,7 +1285,7 @@ void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern
   }
   CSR W;
   const auto rk = mm_ranks(cf, ffrow, emul);
-  matmul_first_touch(FF, FC, W, rk.get());
+  matmul_first_touch(FF, FC, W, rk.get(), mm_square);
   std::vector<int> all(A.nrows);
   for (int i = 0; i < A.nrows; ++i) all[i] = i;
   assemble_mm_p(cf, all, W, FC.ncols, P);
@@ -1289,8 +1293,8 @@ void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern
 }
 
 void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P, const std::vector<int>* emul) {
-  build_modext_interp(A, cf, S, trunc_factor, max_elmts, true, P, emul);
+                           int max_elmts, CSR& P, const std::vector<int>* emul, int mm_square) {
+  build_modext_interp(A, cf, S, trunc_factor, max_elmts, true, P, emul, mm_square);
 }
 
 // Extended+i in matrix-matrix form (interp_type 17): par_mod_lr_interp.c:474
@@ -1300,7 +1304,7 @@ void build_modextpe_interp(const CSR& A, const std::vector<int>& cf, const Patte
 // the diagonal is 1, and the row is scaled by -1 / (D_theta + D_w); As_FC is
 // used as is.
 void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                           int max_elmts, CSR& P, const std::vector<int>* emul) {
+                           int max_elmts, CSR& P, const std::vector<int>* emul, int mm_square) {
   CSR FF, FC;
   std::vector<int> frow, ffrow;
   fffc(A, cf, S, false, FF, FC, frow, ffrow);
@@ -1340,7 +1344,7 @@ void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Patte
   }
   CSR W;
   const auto rk = mm_ranks(cf, ffrow, emul);
-  matmul_first_touch(FF, FC, W, rk.get());
+  matmul_first_touch(FF, FC, W, rk.get(), mm_square);
   std::vector<int> all(A.nrows);
   for (int i = 0; i < A.nrows; ++i) all[i] = i;
   assemble_mm_p(cf, all, W, FC.ncols, P);
@@ -1355,7 +1359,7 @@ void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Patte
 // gen_fffc.c:1056 hypre_ParCSRMatrixGenerateFFFCD3 forms it (every F row: the
 // mean of its strong non-C connections).
 void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
-                                int max_elmts, bool pe, CSR& P, const std::vector<int>* emul) {
+                                int max_elmts, bool pe, CSR& P, const std::vector<int>* emul, int mm_square) {
   CSR FF, FC;
   std::vector<int> frow, ffrow;
   fffc(A, cf, S, true, FF, FC, frow, ffrow);
@@ -1417,7 +1421,7 @@ void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const 
   }
   CSR W;
   const auto rk = mm_ranks(cf, ffrow, emul);
-  matmul_first_touch(FF, FC, W, rk.get());
+  matmul_first_touch(FF, FC, W, rk.get(), mm_square);
   std::vector<int> c1;  // rows of P2: the first stage's C points, in order
   for (int i = 0; i < A.nrows; ++i)
     if (cf[i] > 0 || cf[i] == -2) c1.push_back(i);
@@ -1427,8 +1431,8 @@ void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const 
 
 // P = P1 P2 (par_amg_setup.c:1681 hypre_ParMatmul), then the aggressive
 // truncation (:1685)
-void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P) {
-  matmul_first_touch(P1, P2, P);
+void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P, int mm_square) {
+  matmul_first_touch(P1, P2, P, nullptr, mm_square);
   truncate_rows(P, trunc_factor, max_elmts);
 }
 
@@ -2114,7 +2118,8 @@ static void rank_order_rows(CSR& M, const std::vector<int>& rs, const std::vecto
   }
 }
 
-int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::vector<int>* rank_starts) {
+int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::vector<int>* rank_starts,
+              const std::vector<int>* coarsen_starts) {
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
@@ -2136,6 +2141,13 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     rank_order_rows(H.lev[0].A, emul, emul);
   }
   const std::vector<int>* rs = emul.empty() ? nullptr : &emul;
+  // HMIS per rank without the rest of the emulation (the distributed setup's
+  // coarsening): this level's rank starts
+  std::vector<int> crs;
+  if (!rs && coarsen_starts && coarsen_starts->size() > 2 && coarsen_type == 10) {
+    crs = *coarsen_starts;
+    if (crs.front() != 0 || crs.back() != A0.nrows) throw std::runtime_error("coarsen_starts do not cover A");
+  }
   std::vector<std::vector<int>> lev_starts;  // emulated ranks: row starts of every level
   if (rs) lev_starts.push_back(emul);
   char buf[256];
@@ -2154,7 +2166,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     std::vector<int> cf;
     if (coarsen_type == 8) coarsen_pmis(S, 0, cf, rs);
     else if (coarsen_type == 9) coarsen_pmis(S, 2, cf, rs);
-    else if (coarsen_type == 10) coarsen_hmis(S, &L.A, prm.measure_type, prm.coarsen_cut_factor, cf, rs);
+    else if (coarsen_type == 10)
+      coarsen_hmis(S, &L.A, prm.measure_type, prm.coarsen_cut_factor, cf, rs ? rs : (crs.empty() ? nullptr : &crs));
     else throw std::runtime_error("unsupported coarsen_type " + std::to_string(coarsen_type));
     double t2 = now();
     t_c += t2 - t1;
@@ -2167,12 +2180,13 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       create_2nd_strength(S, cf, prm.num_paths, S2);
       // emulated ranks: S2's rows (the first pass's C points) split as the fine rows
       std::vector<int> rs2;
-      if (rs) {
+      const std::vector<int>* lrs = rs ? rs : (crs.empty() ? nullptr : &crs);
+      if (lrs) {
         std::vector<int> pref(cf.size() + 1, 0);
         for (size_t i = 0; i < cf.size(); ++i) pref[i + 1] = pref[i] + (cf[i] > 0);
-        for (int v : *rs) rs2.push_back(pref[v]);
+        for (int v : *lrs) rs2.push_back(pref[v]);
       }
-      const std::vector<int>* rsc = rs ? &rs2 : nullptr;
+      const std::vector<int>* rsc = lrs ? &rs2 : nullptr;
       std::vector<int> cfn;
       if (coarsen_type == 8) coarsen_pmis(S2, 3, cfn, rsc);
       else if (coarsen_type == 9) coarsen_pmis(S2, 4, cfn, rsc);
@@ -2324,6 +2338,12 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     snprintf(buf, sizeof buf, "level %d: rows %d nnz %lld -> coarse %d (P nnz %lld)\n", level, fine_size,
              (long long)L.A.nnz(), coarse_size, (long long)L.P.nnz());
     H.log += buf;
+    if (!crs.empty()) {
+      // rank r owns the C points of its rows on the next level
+      std::vector<int> pref(L.cf.size() + 1, 0);
+      for (size_t i = 0; i < L.cf.size(); ++i) pref[i + 1] = pref[i] + (L.cf[i] == 1);
+      for (int& v : crs) v = pref[v];
+    }
     H.lev.emplace_back();
     H.lev[level + 1].A.swap(Ac);
     if (!emul.empty()) {

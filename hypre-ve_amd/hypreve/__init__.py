@@ -190,6 +190,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGGetLevelLayout", _i, [_p, _i, _i, _pi]),
     ("hypreve_BoomerAMGSetGsRankStarts", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGSetRankEmulation", _i, [_p, _i, _pi]),
+    ("hypreve_BoomerAMGSetCoarsenRankStarts", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BoomerAMGGsScheduleStats", _i, [_p, _i, _i, _i, _pi64]),
     ("hypreve_BoomerAMGGetCycleCommStats", _i, [_p, _i, _pi64]),
@@ -648,6 +649,16 @@ class BoomerAMG:
             return
         arr = (C.c_int * len(starts))(*[int(v) for v in starts])
         check(lib().hypreve_BoomerAMGSetRankEmulation(self.h, len(starts) - 1, arr), "SetRankEmulation")
+
+    def set_coarsen_rank_starts(self, starts):
+        """HMIS coarsened as an N-rank run's distributed setup does it (level-0
+        row starts, N+1 entries; hypreve_BoomerAMGSetCoarsenRankStarts), the
+        rest of the setup one-process; None clears it.  Takes effect at setup."""
+        if starts is None or len(starts) <= 2:
+            check(lib().hypreve_BoomerAMGSetCoarsenRankStarts(self.h, 0, None), "SetCoarsenRankStarts")
+            return
+        arr = (C.c_int * len(starts))(*[int(v) for v in starts])
+        check(lib().hypreve_BoomerAMGSetCoarsenRankStarts(self.h, len(starts) - 1, arr), "SetCoarsenRankStarts")
 
     LAYOUTS = ("padded", "jagged", "wide", "jag-pw", "dict", "delta", "delta+vt8", "delta+vt16", "padded+vt16",
                "jagged+vt16", "dict-ranges", "stencil", "coded", "packed", "grid-stencil")

@@ -274,6 +274,14 @@ HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver solver, HYPRE_Int nranks
 /* The relaxation weight and outer weight (omega) the cycle uses on `level`. */
 HYPRE_Int hypreve_BoomerAMGGetLevelWeights(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Real *relax_weight,
                                            HYPRE_Real *omega);
+/* HMIS (coarsen_type 10) on one process as an N-rank run's setup coarsens
+ * it: each rank's Ruge first pass over the strong connections it owns and a
+ * random stream per rank in the PMIS stage (par_coarsen.c:2774 on N
+ * processes), rank r owning level-0 rows starts[r] .. starts[r+1]-1 and the
+ * C points of its rows below.  The rest of the setup stays the one-process
+ * one, so the iterates equal those of the distributed setup on N ranks.
+ * nranks <= 1 clears it; other coarsenings ignore it.  Takes effect at Setup. */
+HYPRE_Int hypreve_BoomerAMGSetCoarsenRankStarts(HYPRE_Solver solver, HYPRE_Int nranks, const HYPRE_Int *starts);
 /* One process reproduces the setup and smoothing of a reference N-rank run
  * (mpirun -np N) whose level-0 rows start at starts[0..nranks]: every row in
  * ParCSR order (the rank's own columns, then the others; par_csr_matrix.c),

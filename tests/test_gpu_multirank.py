@@ -269,3 +269,31 @@ def test_loopback_grid_stencil_bitwise(hv, nranks, stencil, relax):
     xN = np.concatenate([o[1] for o in out])
     assert all(o[2] == it1 for o in out)
     assert np.array_equal(x1, xN)
+
+
+@pytest.mark.parametrize("nranks,nx,nz", [(2, 16, 16), (3, 14, 20)])
+@pytest.mark.parametrize("relax,interp,agg", [(18, 6, 0), (13, 6, 0), (18, 14, 0), (18, 6, 1)])
+def test_loopback_hmis_bitwise(hv, nranks, nx, nz, relax, interp, agg):
+    """HMIS (hypre's default coarsening) set up distributed across the ranks
+    (each rank's Ruge first pass, PMIS with per-rank streams; dsetup.cpp
+    hmis_dist) and solved: one GPU given the same rank starts for the
+    coarsening (hypreve_BoomerAMGSetCoarsenRankStarts; hybrid GS: the rank
+    blocks too) reproduces the N-rank iterates bit for bit."""
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=10, interp_type=interp, P_max_elmts=4, relax_type=relax, tol=1e-8, max_iter=40,
+              agg_num_levels=agg)
+    xN, itN, rrN, nlN = _solve_nranks(hv, nx, nx, nz, kw, nranks)
+    starts = _solve_nranks.starts
+    A = _gen(hv, 7, nx, nx, nz)
+    amg = hv.BoomerAMG(**kw)
+    amg.set_coarsen_rank_starts(starts)
+    if relax == 13:
+        amg.set_gs_rank_starts(starts)
+    amg.setup(A)
+    b = hv.ParVector(A.n, np.ones(A.n))
+    x = hv.ParVector(A.n, np.zeros(A.n))
+    it1, rr1 = amg.solve(A, b, x)
+    x1 = x.get()
+    assert nlN == amg.num_levels()
+    assert all(i == it1 for i in itN), (it1, itN)
+    assert np.array_equal(x1, xN), f"max |diff| {np.max(np.abs(x1 - xN))}"

@@ -308,3 +308,75 @@ def test_gs_self_check_models_the_kernel_fences(hv):
     finally:
         hv.set_knob(11, 0)
     amg.gs_schedule_check(1)
+
+
+@pytest.mark.parametrize("size", [2, 3, 5, 8])
+@pytest.mark.parametrize("stencil,relax,interp,agg", [(7, 18, 6, 0), (27, 13, 6, 0), (7, 13, 14, 0), (7, 18, 6, 1),
+                                                      (7, 18, 14, 2)])
+def test_distributed_hmis_matches_rank_coarsening(hv, size, stencil, relax, interp, agg):
+    """HMIS (coarsen_type 10, hypre's default) and extended interpolation (14)
+    in the distributed setup: each rank's Ruge first pass over the strong
+    connections it owns, then PMIS seeded with its C points with one random
+    stream per rank (par_coarsen.c:2774 on N processes; dsetup.cpp hmis_dist).
+    Every rank's part of every level equals the one-process setup that
+    coarsens HMIS with the same rank starts (amg_setup's coarsen_starts) byte
+    for byte, with aggressive levels (the second pass per rank too)."""
+    if stencil == 27:
+        A = hv.ParCSRMatrix.laplacian27(17, 15, 19)
+    else:
+        A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=1.0 if agg == 0 else 0.3)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=10, interp_type=interp, relax_type=relax, P_max_elmts=4, agg_num_levels=agg)
+    amg.dist_setup_check(A, size)
+
+
+def test_hmis_rank_coarsening_has_teeth(hv):
+    """The per-rank HMIS differs from the one-process HMIS (first pass over the
+    whole graph), so the check above compares against the right hierarchy."""
+    A = hv.ParCSRMatrix.laplacian(19, 17, 23)
+    sizes = []
+    for starts in (None, [0, A.n // 3, 2 * A.n // 3, A.n]):
+        amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+        amg.set(coarsen_type=10, interp_type=6, relax_type=18, P_max_elmts=4)
+        amg.set_coarsen_rank_starts(starts)
+        amg.setup_host(A)
+        sizes.append([amg.level_matrix(l, 0)[3][0] for l in range(amg.num_levels())])
+        cf = amg.level_vector(0, 0)
+        sizes[-1].append(cf.tobytes())
+        amg.destroy()
+    assert sizes[0] != sizes[1]
+
+
+@pytest.mark.parametrize("size", [2, 3, 5, 8])
+@pytest.mark.parametrize("coarsen,interp,agg,agg_interp,pmx", [(8, 16, 0, 4, 4), (8, 17, 0, 4, 4), (8, 18, 0, 4, 0),
+                                                                (10, 17, 0, 4, 4), (8, 6, 1, 5, 4), (8, 6, 1, 7, 4),
+                                                                (10, 6, 2, 5, 4), (10, 18, 1, 7, 0)])
+def test_distributed_mm_interp_matches_one_process(hv, size, coarsen, interp, agg, agg_interp, pmx):
+    """The matrix-matrix interpolations (16 ext, 17 ext+i, 18 ext+e:
+    par_mod_lr_interp.c) and the 2-stage aggressive ones (agg_interp_type 5 /
+    7: par_2s_interp.c, P = P1 P2) in the distributed setup: each rank runs the
+    one-process builders over its ghost universe (owned points, off-rank
+    neighbours with fetched A rows, the points those reach) and keeps its
+    rows; P2's off-rank rows are fetched for the product.  Every rank's part
+    equals the one-process hierarchy byte for byte (HMIS: coarsened per rank)."""
+    A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=1.0, cy=0.8, cz=1.0)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=coarsen, interp_type=interp, relax_type=18, P_max_elmts=pmx, agg_num_levels=agg,
+            agg_interp_type=agg_interp, agg_P12_max_elmts=4 if agg_interp == 7 else 0, agg_P_max_elmts=4)
+    amg.dist_setup_check(A, size)
+
+
+@pytest.mark.parametrize("size", [2, 3, 5, 8])
+@pytest.mark.parametrize("coarsen,order,scale,variant,eig", [(8, 2, 1, 0, 10), (8, 3, 0, 1, 10), (10, 2, 1, 0, 10),
+                                                             (8, 2, 1, 0, 0)])
+def test_distributed_chebyshev_matches_one_process(hv, size, coarsen, order, scale, variant, eig):
+    """Chebyshev (relax 16) in the distributed setup: the eigenvalue estimate's
+    CG (par_relax_more.c:115) draws its start vector at the global rows, and
+    every inner product is a running sum handed from rank to rank in rank
+    order, so the coefficients and the scaling equal the one-process ones
+    byte for byte; eig 0: the inf-norm bound (par_relax_more.c:25)."""
+    A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=1.0, cy=0.5, cz=1.0)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=coarsen, interp_type=6, relax_type=16, P_max_elmts=4, cheby_order=order,
+            cheby_scale=scale, cheby_variant=variant, cheby_eig_est=eig)
+    amg.dist_setup_check(A, size)
