@@ -842,7 +842,16 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands, HYPRE
   CHECK_ARG(nbands >= 0, 2);
   CHECK_ARG(which_mask >= 0 && which_mask <= 7, 3);
   API_BEGIN
-  s->dev->set_block_bands(s->RH, nbands, which_mask ? which_mask : 7);
+  // a one-rank hierarchy lent its matrices for the build only: lend them again
+  const bool lent = s->RH.size == 1 && !s->RH.lev.empty() && s->RH.lev[0].A.interior.nrows == 0 &&
+                    lend_single_rank(s->H, s->RH, s->gs_rank_starts.empty() ? nullptr : &s->gs_rank_starts);
+  try {
+    s->dev->set_block_bands(s->RH, nbands, which_mask ? which_mask : 7);
+  } catch (...) {
+    if (lent) give_back_single_rank(s->H, s->RH);
+    throw;
+  }
+  if (lent) give_back_single_rank(s->H, s->RH);
   HVE_HIP(hipDeviceSynchronize());
   API_END
 }
@@ -1164,10 +1173,23 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
     setup_one_process(s, A);
   }
   const double t1 = now();
-  if (!A->multi()) single_rank_hierarchy(s->H, s->RH, s->gs_rank_starts.empty() ? nullptr : &s->gs_rank_starts);
+  // one rank: the device build reads the hierarchy's own matrices (lent, no
+  // copy: 11 s and ~45 GB of host memory at 512^3) and they go back to H after
+  bool lent = false;
+  const std::vector<int>* gsr = s->gs_rank_starts.empty() ? nullptr : &s->gs_rank_starts;
+  if (!A->multi()) {
+    lent = lend_single_rank(s->H, s->RH, gsr);
+    if (!lent) single_rank_hierarchy(s->H, s->RH, gsr);
+  }
   const double t2 = now();
   if (!s->dev) s->dev.reset(new DevAMG);
-  s->dev->build(s->RH, A->multi() ? A->comm->dc.get() : nullptr);
+  try {
+    s->dev->build(s->RH, A->multi() ? A->comm->dc.get() : nullptr);
+  } catch (...) {
+    if (lent) give_back_single_rank(s->H, s->RH);
+    throw;
+  }
+  if (lent) give_back_single_rank(s->H, s->RH);
   s->dev->set_use_graph(s->use_graph);
   const double t3 = now();
   char tb[160];

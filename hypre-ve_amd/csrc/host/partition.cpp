@@ -405,6 +405,88 @@ void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out, const std::ve
   }
 }
 
+bool lend_single_rank(Hierarchy& H, RankHierarchy& out, const std::vector<int>* gs_rank_starts) {
+  const int nl = (int)H.lev.size();
+  if (nl == 0) return false;
+  for (int l = 0; l < nl; ++l) {  // make_op's shapes: columns local to the one rank
+    const Level& L = H.lev[l];
+    if (L.A.ncols != L.A.nrows) return false;
+    if (l + 1 < nl && (L.P.nrows != L.A.nrows || L.P.ncols != H.lev[l + 1].A.nrows ||
+                       L.R.nrows != H.lev[l + 1].A.nrows || L.R.ncols != L.A.nrows))
+      return false;
+  }
+  out = RankHierarchy();
+  out.rank = 0;
+  out.size = 1;
+  out.prm = H.prm;
+  out.lev.resize(nl);
+  out.coarse_n = H.coarse_n;
+  out.coarse_dense = H.coarse_dense;
+  out.grid_complexity = H.grid_complexity;
+  out.operator_complexity = H.operator_complexity;
+  for (int l = 0; l < nl; ++l) {
+    out.nnz_A.push_back(H.lev[l].A.nnz());
+    out.rows.push_back(H.lev[l].A.nrows);
+  }
+  out.agg_level = -1;
+  // the GS emulation reads H's matrices: before they move
+  std::vector<std::vector<int>> blocks;
+  std::vector<std::vector<double>> l1b;
+  if (gs_rank_starts && gs_rank_starts->size() > 2 && uses_hybrid_gs(H.prm)) {
+    blocks = rank_gs_blocks(H, *gs_rank_starts, (int)gs_rank_starts->size() - 1);
+    l1b = l1_for_blocks(H, blocks);
+  }
+  auto lend = [](CSR& M, RankOp& op) {
+    op.nrows_local = M.nrows;
+    op.map_int.resize(M.nrows);
+    for (int r = 0; r < M.nrows; ++r) op.map_int[r] = r;
+    op.map_bnd.clear();
+    op.boundary = CSR();
+    op.boundary.resize_rows(0, M.ncols);
+    op.interior.swap(M);
+  };
+  for (int l = 0; l < nl; ++l) {
+    Level& L = H.lev[l];
+    RankLevel& RL = out.lev[l];
+    const int n = L.A.nrows;
+    RL.n_loc = n;
+    RL.first = 0;
+    RL.n_glob = n;
+    RL.l1 = blocks.empty() ? L.l1 : l1b[l];
+    if (!blocks.empty()) RL.gs_blocks = blocks[l];
+    RL.cf = L.cf;
+    RL.cheby_ds = L.cheby_ds;
+    RL.cheby_coefs = L.cheby_coefs;
+    RL.hu = RankHalo();
+    RL.hu.n_loc = n;
+    RL.hv = RankHalo();
+    if (l + 1 < nl) RL.hv.n_loc = n;
+    lend(L.A, RL.A);
+    if (l + 1 < nl) {
+      lend(L.P, RL.P);
+      lend(L.R, RL.R);
+    }
+  }
+  return true;
+}
+
+void give_back_single_rank(Hierarchy& H, RankHierarchy& out) {
+  const int nl = (int)std::min(H.lev.size(), out.lev.size());
+  for (int l = 0; l < nl; ++l) {
+    Level& L = H.lev[l];
+    RankLevel& RL = out.lev[l];
+    if (L.A.nrows == 0 && RL.A.interior.nrows > 0) L.A.swap(RL.A.interior);
+    if (l + 1 < nl) {
+      if (L.P.nrows == 0 && RL.P.interior.nrows > 0) L.P.swap(RL.P.interior);
+      if (L.R.nrows == 0 && RL.R.interior.nrows > 0) L.R.swap(RL.R.interior);
+    }
+    for (RankOp* op : {&RL.A, &RL.P, &RL.R}) {
+      op->interior = CSR();
+      std::vector<int>().swap(op->map_int);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // serialization (flat little-endian bytes; both ends are this library)
 // ---------------------------------------------------------------------------

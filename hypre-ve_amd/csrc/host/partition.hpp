@@ -93,6 +93,15 @@ void partition_hierarchy_all(const Hierarchy& H, const std::vector<int>& starts0
 // on every level (num_blocks per rank, l1 norms to match), so that one GPU
 // reproduces the N-rank iterates.
 void single_rank_hierarchy(const Hierarchy& H, RankHierarchy& out, const std::vector<int>* gs_rank_starts = nullptr);
+// One rank without copies: every row of a one-rank partition is an interior
+// row and every column local, so the rank's operators are the hierarchy's own
+// matrices.  lend moves them into `out` (the rest as single_rank_hierarchy
+// builds it) and leaves H's level matrices empty until give_back returns them
+// (call it after the device build, also when the build throws).  Returns
+// false (nothing moved) where a matrix's shape does not allow it; the caller
+// then uses single_rank_hierarchy.
+bool lend_single_rank(Hierarchy& H, RankHierarchy& out, const std::vector<int>* gs_rank_starts = nullptr);
+void give_back_single_rank(Hierarchy& H, RankHierarchy& out);
 // The hybrid-GS row blocks and option-4 l1 norms of every level that
 // single_rank_hierarchy gives the device for gs_rank_starts (empty when the
 // emulation is off): exported so the CPU oracle sweeps the same blocks.

@@ -26,6 +26,7 @@ dur = defaultdict(list)
 
 
 def kname(s):
+    s = s.replace("(anonymous namespace)::", "")
     s = re.sub(r"\(.*", "", s).replace("void hve::", "").replace("hve::", "")
     return s[:44]
 
@@ -35,13 +36,17 @@ for f in glob.glob(os.path.join(root, "pmc_*", "**", "run_counter_collection.csv
         vals[(kname(r["Kernel_Name"]), int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for f in glob.glob(os.path.join(root, "trace", "**", "run_kernel_trace.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
-        dur[(kname(r["Kernel_Name"]), int(r["Grid_Size"]))].append(
+        dur[(kname(r["Kernel_Name"]), int(r.get("Grid_Size") or r["Grid_Size_X"]))].append(
             (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
 
 
 def m(v, c):
     x = v.get(c)
     return sum(x) / len(x) if x else float("nan")
+
+
+def q(a, b):
+    return a / b if b else float("nan")
 
 
 cols = ["us", "traffic_GB", "L2hit%", "dram%", "L2lat", "TAbusy%", "wait%", "vmem/wave", "lds/wave"]
@@ -51,12 +56,12 @@ for k in sorted(keys, key=lambda k: -m(vals[k], "FETCH_SIZE") if vals[k].get("FE
     v = vals[k]
     d = sum(dur[k]) / len(dur[k]) if dur.get(k) else float("nan")
     row = [d, (2 * m(v, "FETCH_SIZE") + m(v, "WRITE_SIZE")) * 1024 / 1e9,
-           100 * m(v, "TCC_HIT_sum") / (m(v, "TCC_HIT_sum") + m(v, "TCC_MISS_sum")),
-           100 * m(v, "TCC_EA0_RDREQ_DRAM_sum") / m(v, "TCC_EA0_RDREQ_sum"),
-           m(v, "TCP_TCC_READ_REQ_LATENCY_sum") / m(v, "TCP_TCC_READ_REQ_sum"),
-           100 * m(v, "TA_TA_BUSY_sum") / (m(v, "GRBM_GUI_ACTIVE") * 32),
-           100 * m(v, "SQ_WAIT_ANY") / m(v, "SQ_WAVE_CYCLES"),
-           m(v, "SQ_INSTS_VMEM_RD") / m(v, "SQ_WAVES"), m(v, "SQ_INSTS_LDS") / m(v, "SQ_WAVES")]
+           100 * q(m(v, "TCC_HIT_sum"), m(v, "TCC_HIT_sum") + m(v, "TCC_MISS_sum")),
+           100 * q(m(v, "TCC_EA0_RDREQ_DRAM_sum"), m(v, "TCC_EA0_RDREQ_sum")),
+           q(m(v, "TCP_TCC_READ_REQ_LATENCY_sum"), m(v, "TCP_TCC_READ_REQ_sum")),
+           100 * q(m(v, "TA_TA_BUSY_sum"), m(v, "GRBM_GUI_ACTIVE") * 32),
+           100 * q(m(v, "SQ_WAIT_ANY"), m(v, "SQ_WAVE_CYCLES")),
+           q(m(v, "SQ_INSTS_VMEM_RD"), m(v, "SQ_WAVES")), q(m(v, "SQ_INSTS_LDS"), m(v, "SQ_WAVES"))]
     print(f"{k[0]:44s} {k[1]:10d} " + " ".join(f"{x:10.3f}" for x in row))
 print("\nraw means per dispatch:")
 for k in sorted(keys):
