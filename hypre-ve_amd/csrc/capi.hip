@@ -1464,16 +1464,6 @@ HYPRE_Int hypreve_BoomerAMGGetCycleCommStats(HYPRE_Solver s, HYPRE_Int level, in
   API_END
 }
 
-// Whether the cycle forms level 0's residual and restriction in one pass
-// (k_resid_restrict: single rank, a grid operator on the stencil layout).
-HYPRE_Int hypreve_BoomerAMGGetFusedResidRestrict(HYPRE_Solver s, HYPRE_Int* on) {
-  CHECK_ARG(s && s->kind == KIND_AMG && s->dev, 1);
-  CHECK_ARG(on, 2);
-  API_BEGIN
-  *on = s->dev->fused_rr();
-  API_END
-}
-
 // Size of the packed hybrid Gauss-Seidel schedule of a level's A for a block
 // count (host only): out = {nnz, stored entries, steps, teams, longest team
 // (steps), blocks}.
@@ -1621,12 +1611,7 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
   HVE_HIP(launch_set(D.ws_n(), 0.0, y, st));
   // which 3: A as the l1-Jacobi sweep, with b standing in for the l1 norms
   const double* l1 = which == 3 ? b : nullptr;
-  // R_0 as the cycle runs it: the tiled restriction where it is built
-  const bool tiled = which == 2 && level == 0 && D.fused_rr() == 2;
-  auto launch = [&] {
-    if (tiled) HVE_HIP(launch_tile_restrict(D.rr_view(), D.rr_fine_rows(), x, y, nullptr, nullptr, st));
-    else HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, y, -1.0, 0.0, st));
-  };
+  auto launch = [&] { HVE_HIP(launch_sell(op, M.view(), x, b, l1, nullptr, 0, y, -1.0, 0.0, st)); };
   for (int w = 0; w < 3; ++w) launch();
   hipEvent_t e0, e1;
   HVE_HIP(hipEventCreate(&e0));
@@ -1669,7 +1654,6 @@ HYPRE_Int hypreve_BenchLevelOpStoredBytes(HYPRE_Solver s, HYPRE_Int level, HYPRE
   // b read + y write / y rw / y write / f, u_g, l1 read + u' write
   const double out_rw = which == 0 ? 16.0 : which == 1 ? 16.0 : which == 2 ? 8.0 : 32.0;
   *bytes = (double)M.bytes() + (double)M.nrows * out_rw + (double)M.ncols * 8.0;
-  if (which == 2 && level == 0 && s->dev->fused_rr() == 2) *bytes = s->dev->rr_tile_bytes(L.R.nrows_local);
   API_END
 }
 

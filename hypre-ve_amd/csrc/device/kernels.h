@@ -126,51 +126,13 @@ hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp,
 // doubles) must stay below 4 GiB.
 hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, int nhalo,
                             const double* F, double* u, double w, double omega, hipStream_t st);
-// Level 0's residual fused with its restriction (runtime.hpp DevRR): tiles of
-// kRRTx x ty fine points (x, y) marching zc planes in z.
-constexpr int kRRTx = 64;
-constexpr int kRRTy = 16;
-struct RRView {
-  // A_0 on the stencil layout (SellView fields of the same name)
-  const int* slice_pat = nullptr;
-  const int* slot_off = nullptr;
-  const int* slot_vi = nullptr;
-  const uint64_t* slot_mask = nullptr;
-  const double* vtabA = nullptr;
-  int sw = 0, npat = 0;
-  int nx = 0, ny = 0, nz = 0, ty = 0, zc = 0, ntx = 0, nty = 0, nzc = 0;
-  const int* bptr = nullptr;
-  const int* bent = nullptr;
-  const int* bcptr = nullptr;
-  const int* bcnt = nullptr;
-  const int* brow = nullptr;
-  const unsigned short* blb = nullptr;
-  const unsigned char* blen = nullptr;
-  const unsigned short* code = nullptr;
-  const double* vtabR = nullptr;  // the weights, indexed by the code's low vbits, or
-  const double* bval = nullptr;   // one weight per entry (vbits 0)
-  const int* odz = nullptr;
-  const int* odxy = nullptr;
-  int nvtabR = 0, notab = 0, vbits = 0;
-  int64_t entries = 0;  // restriction entries (codes)
-};
-// Fc = R_0 (b - A_0 x) without storing the residual; with l1c, also
-// Uc = 0 + Fc / l1c (the coarse zero-guess l1-Jacobi sweep, OP_RESTRICT_ZG).
-hipError_t launch_resid_restrict(const RRView& V, const double* x, const double* b, double* Fc, double* Uc,
-                                 const double* l1c, hipStream_t st);
-// Fc = R_0 r over the same tiles, r (nfine doubles) read from memory into an
-// LDS ring of planes; with l1c, also Uc = 0 + Fc / l1c.
-hipError_t launch_tile_restrict(const RRView& V, int nfine, const double* r, double* Fc, double* Uc,
-                                const double* l1c, hipStream_t st);
 int sell_batch_override();
 // Tuning knobs read at launch (0 = default): 0 offset-coded row blocks per
 // step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU,
 // 3 stream-mix access width (2: 16 B), 7 caps the device setup's LDS tables
-// at 2^v slots (tests of its host fallback), 8 the fused level-0 residual +
-// restriction at the next Setup (1 on, -1 off, 0 HVE_FUSE_RR), 9 the planes a
-// grid-stencil workgroup marches (k_grid_stencil) at the next Setup, 10 the
-// tiled level-0 restriction (k_tile_restrict) at the next Setup (1 on, -1
-// off, 0 HVE_TILE_R, default off).
+// at 2^v slots (tests of its host fallback), 9 the planes a grid-stencil
+// workgroup marches (k_grid_stencil) at the next Setup, 11 shortens the
+// hybrid-GS ring reach (tests of gs_schedule_self_check).
 void set_knob(int id, int v);
 int knob(int id);
 int stencil_slices_per_wave();

@@ -1179,401 +1179,6 @@ __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
     code_rows_op<OP, CFSEL, B, MAP, NR, PK>(p, vt, ot, rb, r1);
 }
 
-// ---------------------------------------------------------------------------
-// Level 0's residual fused with its restriction (host: DevAMG::build_rr).
-// One workgroup per tile of kRRTx x kRRTy fine points (x, y) and chunk of zc
-// planes.  It marches z: the residual r = b - A x of plane z over the tile
-// and a two-point margin goes into an LDS ring of six planes, then the R_0
-// rows anchored in plane z - 2 of the tile are summed from the ring.  Every
-// residual is formed by the stencil layout's slot order (as k_sell_stencil
-// does) and every restriction row in its stored order (as k_sell_code does),
-// so F_c (and U_c = 0 + F_c / l1_c) are bitwise the unfused ones.  Six ring
-// slots let one barrier per plane suffice: plane z + 1 overwrites plane z - 5,
-// which the rows of plane z - 2 no longer read.
-// A tile line x0 .. x0 + 63 is exactly one SELL slice (nx % 64 == 0), so its
-// slot data is wave-uniform (scalar); the four margin columns take the slice
-// pattern per lane.
-// ---------------------------------------------------------------------------
-struct RRArgs {
-  RRView v;
-  const double* __restrict__ x;
-  const double* __restrict__ b;
-  double* Fc;
-  double* Uc;
-  const double* __restrict__ l1c;
-  int nblocks_pad;
-};
-
-template <bool ZG, bool VT>
-__global__ void __launch_bounds__(256) k_resid_restrict(RRArgs a) {
-  constexpr int PX = kRRTx + 4, PY = kRRTy + 4, PL = PX * PY;
-  constexpr int LPW = (PY + 3) / 4;  // lines of a plane per wave
-  constexpr int B = 8;               // slots per batch
-  constexpr int KP = 16;             // restriction codes prefetched per row
-  const RRView& p = a.v;
-  const int W = p.sw;
-  extern __shared__ double sm[];
-  double* ring = sm;                                         // 6 planes of PL
-  double* vt = sm + 6 * PL;                                  // R_0's values
-  double* pva = vt + p.nvtabR;                               // A_0's slot values, per pattern slot
-  uint64_t* pmask = reinterpret_cast<uint64_t*>(pva + p.npat * W);
-  int* poff = reinterpret_cast<int*>(pmask + p.npat * W);
-  int* oz = poff + p.npat * W;
-  int* oxy = oz + p.notab;
-  for (int i = threadIdx.x; i < p.nvtabR; i += 256) vt[i] = p.vtabR[i];
-  for (int i = threadIdx.x; i < p.npat * W; i += 256) {
-    pva[i] = p.vtabA[p.slot_vi[i]];
-    pmask[i] = p.slot_mask[i];
-    poff[i] = p.slot_off[i];
-  }
-  for (int i = threadIdx.x; i < p.notab; i += 256) {
-    oz[i] = p.odz[i];
-    oxy[i] = p.odxy[i];
-  }
-  const int lg = xcd_logical_block(blockIdx.x, a.nblocks_pad);
-  if (lg >= p.ntx * p.nty * p.nzc) return;  // the whole workgroup: no barrier reached
-  const int tx = lg % p.ntx, tyi = (lg / p.ntx) % p.nty, zci = lg / (p.ntx * p.nty);
-  const int x0 = tx * kRRTx, y0 = tyi * kRRTy, z0 = zci * p.zc, z1 = min(p.nz, z0 + p.zc);
-  const int ylo = max(0, y0 - 2), yhi = min(p.ny, y0 + kRRTy + 2);
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & (kWave - 1);
-  const unsigned vm = (1u << p.vbits) - 1u;
-  // margin points of a line: lanes 0, 1 take x0 - 2, x0 - 1; lanes 2, 3 take
-  // x0 + 64, x0 + 65 (in the neighbouring slices, patterns per lane)
-  const int mx = lane < 2 ? x0 - 2 + lane : x0 + kRRTx + (lane - 2);
-  const bool mlane = lane < 4 && mx >= 0 && mx < p.nx;
-  __syncthreads();
-  for (int z = max(0, z0 - 2); z < z1 + 2; ++z) {
-    const int zr = z - 2;
-    const bool rphase = zr >= z0 && zr < z1;
-    // this plane's restriction rows: the first row's codes go out now and land
-    // during the residual phase
-    int bk = 0, r0 = 0, r1 = 0, ent = 0, cbase = 0;
-    int len0 = 0, lb0 = 0, row0 = 0;
-    unsigned short c0[KP];
-    double w0[VT ? 1 : KP];
-    if (rphase) {
-      bk = (tyi * p.ntx + tx) * p.nz + zr;
-      r0 = p.bptr[bk];
-      r1 = p.bptr[bk + 1];
-      ent = p.bent[bk];
-      cbase = p.bcptr[bk];
-      const int q = r0 + (int)threadIdx.x;
-      if (q < r1) {
-        len0 = p.blen[q];
-        lb0 = p.blb[q];
-        row0 = p.brow[q];
-#pragma unroll
-        for (int k = 0; k < KP; ++k) {
-          const int e = k < len0 ? ent + p.bcnt[cbase + k] + (q - r0) : ent;
-          c0[k] = p.code[e];
-          if (!VT) w0[k] = p.bval[e];
-        }
-      }
-    }
-    double* rp = ring + (z % 6) * PL;
-    if (z < p.nz) {
-      // the wave's lines (one slice each) and their margin points, every load in flight together
-      int row[LPW], pat[LPW], mrow[LPW], mpat[LPW];
-      bool on_line[LPW];
-      double t[LPW], tm[LPW];
-#pragma unroll
-      for (int l = 0; l < LPW; ++l) {
-        const int y = ylo + wave + 4 * l;
-        on_line[l] = y < yhi;
-        const int base = (z * p.ny + (on_line[l] ? y : ylo)) * p.nx;
-        row[l] = base + x0 + lane;
-        pat[l] = __builtin_amdgcn_readfirstlane(p.slice_pat[(base + x0) >> 6]);
-        mrow[l] = base + (mlane ? mx : x0);
-        mpat[l] = p.slice_pat[mrow[l] >> 6];
-        t[l] = a.b[row[l]];
-        tm[l] = a.b[mrow[l]];
-      }
-      for (int k = 0; k < W; k += B) {
-#pragma unroll
-        for (int l = 0; l < LPW; ++l) {
-          bool on[B], mon[B];
-          double xv[B], xm[B];
-#pragma unroll
-          for (int q = 0; q < B; ++q) {
-            const int sk = pat[l] * W + min(k + q, W - 1), mk = mpat[l] * W + min(k + q, W - 1);
-            on[q] = (k + q) < W && ((pmask[sk] >> lane) & 1ull);
-            mon[q] = (k + q) < W && mlane && ((pmask[mk] >> (mrow[l] & 63)) & 1ull);
-            xv[q] = a.x[on[q] ? row[l] + poff[sk] : row[l]];
-            xm[q] = a.x[mon[q] ? mrow[l] + poff[mk] : mrow[l]];
-          }
-#pragma unroll
-          for (int q = 0; q < B; ++q) {
-            const int sk = pat[l] * W + min(k + q, W - 1), mk = mpat[l] * W + min(k + q, W - 1);
-            const double tn = t[l] - pva[sk] * xv[q];
-            t[l] = on[q] ? tn : t[l];
-            const double mn = tm[l] - pva[mk] * xm[q];
-            tm[l] = mon[q] ? mn : tm[l];
-          }
-        }
-      }
-#pragma unroll
-      for (int l = 0; l < LPW; ++l) {
-        if (!on_line[l]) continue;
-        const int yy = ylo + wave + 4 * l - y0 + 2;
-        rp[yy * PX + lane + 2] = t[l];
-        if (mlane) rp[yy * PX + (mx - x0 + 2)] = tm[l];
-      }
-    }
-    __syncthreads();
-    if (rphase) {
-      for (int q = r0 + (int)threadIdx.x; q < r1; q += 256) {
-        const int j = q - r0;
-        const bool first = q == r0 + (int)threadIdx.x;
-        const int len = first ? len0 : p.blen[q], lb = first ? lb0 : p.blb[q];
-        double t = 0.0;
-        for (int k = 0; k < len; ++k) {
-          int e = 0;
-          unsigned c;
-          double w;
-          if (first && k < KP) {
-            c = c0[k];
-            w = VT ? 0.0 : w0[k];
-          } else {
-            e = ent + p.bcnt[cbase + k] + j;
-            c = p.code[e];
-            w = VT ? 0.0 : p.bval[e];
-          }
-          const int o = (int)(c >> p.vbits);
-          if (VT) w = vt[c & vm];
-          t += w * ring[((zr + oz[o]) % 6) * PL + lb + oxy[o]];
-        }
-        const int row = first ? row0 : p.brow[q];
-        a.Fc[row] = t;
-        if (ZG) a.Uc[row] = 0.0 + t / a.l1c[row];
-      }
-    }
-  }
-}
-
-hipError_t launch_resid_restrict(const RRView& V, const double* x, const double* b, double* Fc, double* Uc,
-                                 const double* l1c, hipStream_t st) {
-  constexpr int PL = (kRRTx + 4) * (kRRTy + 4);
-  if (V.ty != kRRTy || V.nx % kRRTx) return hipErrorInvalidValue;
-  RRArgs a;
-  a.v = V; a.x = x; a.b = b; a.Fc = Fc; a.Uc = Uc; a.l1c = l1c;
-  const int nwg = V.ntx * V.nty * V.nzc;
-  a.nblocks_pad = (nwg + 7) / 8 * 8;
-  const size_t lds = (size_t)6 * PL * sizeof(double) + (size_t)V.nvtabR * sizeof(double) +
-                     (size_t)V.npat * V.sw * (sizeof(double) + sizeof(uint64_t) + sizeof(int)) +
-                     (size_t)2 * V.notab * sizeof(int);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-#define HVE_RR(ZGV, VTV)                                                                              \
-  {                                                                                                    \
-    static bool attr = false;                                                                          \
-    if (!attr) {                                                                                       \
-      (void)hipFuncSetAttribute((const void*)k_resid_restrict<ZGV, VTV>,                              \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);               \
-      attr = true;                                                                                     \
-    }                                                                                                  \
-    hipLaunchKernelGGL((k_resid_restrict<ZGV, VTV>), dim3(a.nblocks_pad), dim3(256), lds, st, a);     \
-  }
-  const bool vt = V.bval == nullptr;
-  if (Uc) {
-    if (vt) HVE_RR(true, true) else HVE_RR(true, false)
-  } else {
-    if (vt) HVE_RR(false, true) else HVE_RR(false, false)
-  }
-#undef HVE_RR
-  return hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------
-// Level 0's restriction F_c = R_0 r over tiles of the fine grid (host:
-// DevAMG::build_rr, the buckets of the fused kernel above), reading the fine
-// residual r in natural order: one workgroup per tile of kRRTx x kRRTy fine
-// points and chunk of zc planes marches z with planes z-2 .. z+2 of r over the
-// tile and a two-point margin in an LDS ring of six planes (plane z+3 is in
-// flight while plane z's rows are summed), so each r value leaves memory about
-// once instead of once per restriction entry that reads it (a fine point sits
-// in ~8 R_0 rows).  The rows anchored in plane z of the tile sum their entries
-// in stored order from the ring: bitwise the rows of k_sell_code.
-// A bucket's rows are jagged (sorted by length; entry k of its row j at
-// ent + bcnt[k] + j), so a batch of k reads coalesced codes across threads.
-// ---------------------------------------------------------------------------
-struct TRArgs {
-  RRView v;
-  const double* __restrict__ r;
-  double* Fc;
-  double* Uc;
-  const double* __restrict__ l1c;
-  int nrows;  // fine rows (r's length)
-  int nblocks_pad;
-  int64_t entries;  // restriction entries (codes)
-};
-
-template <bool ZG, bool VT>
-__global__ void __launch_bounds__(256) k_tile_restrict(TRArgs a) {
-  constexpr int PX = kRRTx + 4, PY = kRRTy + 4, PL = PX * PY;
-  constexpr int LPW = PY / 4;  // ring lines loaded per wave
-  static_assert(PY % 4 == 0, "four waves load the ring lines");
-  constexpr int B = 8;         // restriction entries per batch
-  const RRView& p = a.v;
-  extern __shared__ double sm[];
-  double* ring = sm;                 // 6 planes of PL
-  double* vt = sm + 6 * PL;          // R_0's values (VT)
-  int* oz = reinterpret_cast<int*>(vt + (VT ? p.nvtabR : 0));
-  int* oxy = oz + p.notab;
-  for (int i = threadIdx.x; i < (VT ? p.nvtabR : 0); i += 256) vt[i] = p.vtabR[i];
-  for (int i = threadIdx.x; i < p.notab; i += 256) {
-    oz[i] = p.odz[i];
-    oxy[i] = p.odxy[i];
-  }
-  const int lg = xcd_logical_block(blockIdx.x, a.nblocks_pad);
-  if (lg >= p.ntx * p.nty * p.nzc) return;  // the whole workgroup: no barrier reached
-  const int nx = p.nx, ny = p.ny, nz = p.nz;
-  const int tx = lg % p.ntx, tyi = (lg / p.ntx) % p.nty, zci = lg / (p.ntx * p.nty);
-  const int x0 = tx * kRRTx, y0 = tyi * kRRTy, z0 = zci * p.zc, z1 = min(nz, z0 + p.zc);
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)), lane = threadIdx.x & (kWave - 1);
-  const unsigned vm = (1u << p.vbits) - 1u;
-  // ring loads: line wave * LPW + l (y0 - 2 + that), 64 points by lane; the
-  // margins (x0 - 2, x0 - 1, x0 + 64, x0 + 65) of line t / 4 by the first
-  // 4 PY threads; points off the grid read zeros (buffer loads past the end)
-  const auto rr = gs_rsrc(a.r, (unsigned)a.nrows * 8u);
-  constexpr int kOut = (int)0xFFFFFFF0u;
-  const int mt = threadIdx.x, mli = mt >> 2, ms = mt & 3;
-  const int mx = ms < 2 ? x0 - 2 + ms : x0 + kRRTx + (ms - 2);
-  const int my = y0 - 2 + mli;
-  const bool mok = mt < 4 * PY && mx >= 0 && mx < nx && my >= 0 && my < ny;
-  const int mpos = mli * PX + (ms < 2 ? ms : kRRTx + ms);
-  int loff[LPW];
-  bool lok[LPW];
-#pragma unroll
-  for (int l = 0; l < LPW; ++l) {
-    const int yy = y0 - 2 + wave * LPW + l;
-    lok[l] = yy >= 0 && yy < ny;
-    loff[l] = (lok[l] ? yy : 0) * nx + x0 + lane;
-  }
-  const int moff = mok ? my * nx + mx : 0;
-#define HVE_TR_LD(zz, V, VM)                                                                 \
-  {                                                                                          \
-    const int zq = (zz);                                                                     \
-    const bool zin = zq >= 0 && zq < nz;                                                     \
-    const int zb = zq * nx * ny;                                                             \
-    _Pragma("unroll") for (int l = 0; l < LPW; ++l)                                          \
-      V[l] = gs_ld64(rr, (zin && lok[l]) ? (int)((unsigned)(zb + loff[l]) * 8u) : kOut);     \
-    VM = gs_ld64(rr, (zin && mok) ? (int)((unsigned)(zb + moff) * 8u) : kOut);               \
-  }
-#define HVE_TR_ST(zz, V, VM)                                                                 \
-  {                                                                                          \
-    double* rp = ring + (((zz) + 12) % 6) * PL;                                              \
-    _Pragma("unroll") for (int l = 0; l < LPW; ++l) rp[(wave * LPW + l) * PX + 2 + lane] = V[l]; \
-    if (mt < 4 * PY) rp[mpos] = VM;                                                          \
-  }
-  {
-    double v0[LPW], v1[LPW], v2[LPW], v3[LPW], v4[LPW], m0, m1, m2, m3, m4;
-    HVE_TR_LD(z0 - 2, v0, m0)
-    HVE_TR_LD(z0 - 1, v1, m1)
-    HVE_TR_LD(z0, v2, m2)
-    HVE_TR_LD(z0 + 1, v3, m3)
-    HVE_TR_LD(z0 + 2, v4, m4)
-    HVE_TR_ST(z0 - 2, v0, m0)
-    HVE_TR_ST(z0 - 1, v1, m1)
-    HVE_TR_ST(z0, v2, m2)
-    HVE_TR_ST(z0 + 1, v3, m3)
-    HVE_TR_ST(z0 + 2, v4, m4)
-  }
-  __syncthreads();
-  using cint = const __attribute__((address_space(4))) int;  // bucket metadata: scalar cache
-  cint* const bptr = (cint*)p.bptr;
-  cint* const bent = (cint*)p.bent;
-  cint* const bcptr = (cint*)p.bcptr;
-  cint* const bcnt = (cint*)p.bcnt;
-  const auto rc = gs_rsrc(p.code, (unsigned)(a.entries * 2));
-  const auto rw = gs_rsrc(VT ? (const void*)p.code : (const void*)p.bval, (unsigned)(a.entries * (VT ? 2 : 8)));
-  for (int z = z0; z < z1; ++z) {
-    double nv[LPW], nvm;
-    HVE_TR_LD(z + 3, nv, nvm)
-    const int bk = (tyi * p.ntx + tx) * nz + z;
-    const int r0 = bptr[bk], r1 = bptr[bk + 1], ent = bent[bk], cb = bcptr[bk];
-    const int wmax = bcptr[bk + 1] - cb - 1;  // the bucket's longest row (its first)
-    // ring slot base of plane z + dz, dz = -2 .. 2
-    int zs[5];
-#pragma unroll
-    for (int d = 0; d < 5; ++d) zs[d] = ((z + d - 2 + 12) % 6) * PL;
-    for (int base = r0; base < r1; base += 256) {
-      if (base + (wave << 6) >= r1) continue;  // (wave-uniform) no rows left for this wave
-      const int q = base + (int)threadIdx.x;
-      const bool on_row = q < r1;
-      const int qc = on_row ? q : r1 - 1;
-      const int j = q - r0;
-      const int len = on_row ? (int)p.blen[qc] : 0, lb = p.blb[qc];
-      double t = 0.0;
-      for (int k = 0; k < wmax; k += B) {
-        unsigned c[B];
-        double w[B];
-        // every load of the batch unconditional (buffer loads: an entry past
-        // the array reads 0); entries past the row are dropped below
-#pragma unroll
-        for (int i = 0; i < B; ++i) {
-          const int e = ent + bcnt[cb + min(k + i, wmax - 1)] + j;
-          c[i] = (unsigned)__builtin_amdgcn_raw_buffer_load_b16(rc, (int)((unsigned)e * 2u), 0, 0);
-          if (!VT) w[i] = gs_ld64(rw, (int)((unsigned)e * 8u));
-        }
-#pragma unroll
-        for (int i = 0; i < B; ++i) {
-          const bool in = k + i < len;
-          const unsigned ci = in ? c[i] : 0u;
-          const int o = (int)(ci >> p.vbits);
-          const double wi = VT ? vt[ci & vm] : w[i];
-          const int dz = oz[o];
-          const int zb = dz == -2 ? zs[0] : dz == -1 ? zs[1] : dz == 0 ? zs[2] : dz == 1 ? zs[3] : zs[4];
-          const double tn = t + wi * ring[zb + lb + oxy[o]];
-          t = in ? tn : t;
-        }
-      }
-      if (on_row) {
-        const int row = p.brow[q];
-        a.Fc[row] = t;
-        if (ZG) a.Uc[row] = 0.0 + t / a.l1c[row];
-      }
-    }
-    // plane z+3 into the slot of plane z-3, which no row of plane z reads
-    HVE_TR_ST(z + 3, nv, nvm)
-    __syncthreads();
-  }
-#undef HVE_TR_LD
-#undef HVE_TR_ST
-}
-
-hipError_t launch_tile_restrict(const RRView& V, int nfine, const double* r, double* Fc, double* Uc,
-                                const double* l1c, hipStream_t st) {
-  constexpr int PL = (kRRTx + 4) * (kRRTy + 4);
-  if (V.ty != kRRTy || V.nx % kRRTx || (int64_t)V.nx * V.ny * V.nz != nfine) return hipErrorInvalidValue;
-  TRArgs a;
-  a.v = V; a.r = r; a.Fc = Fc; a.Uc = Uc; a.l1c = l1c; a.nrows = nfine; a.entries = V.entries;
-  // 32-bit buffer offsets: codes, f64 weights and r below 4 GiB (DevAMG::build_rr checks)
-  if (V.entries * (V.bval ? 8 : 2) >= ((int64_t)1 << 32) || (int64_t)nfine * 8 >= ((int64_t)1 << 32))
-    return hipErrorInvalidValue;
-  const int nwg = V.ntx * V.nty * V.nzc;
-  a.nblocks_pad = (nwg + 7) / 8 * 8;
-  const bool vt = V.bval == nullptr;
-  const size_t lds = (size_t)6 * PL * sizeof(double) + (vt ? (size_t)V.nvtabR * sizeof(double) : 0) +
-                     (size_t)2 * V.notab * sizeof(int);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-#define HVE_TR(ZGV, VTV)                                                                              \
-  {                                                                                                    \
-    static bool attr = false;                                                                          \
-    if (!attr) {                                                                                       \
-      (void)hipFuncSetAttribute((const void*)k_tile_restrict<ZGV, VTV>,                               \
-                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);               \
-      attr = true;                                                                                     \
-    }                                                                                                  \
-    hipLaunchKernelGGL((k_tile_restrict<ZGV, VTV>), dim3(a.nblocks_pad), dim3(256), lds, st, a);      \
-  }
-  if (Uc) {
-    if (vt) HVE_TR(true, true) else HVE_TR(true, false)
-  } else {
-    if (vt) HVE_TR(false, true) else HVE_TR(false, false)
-  }
-#undef HVE_TR
-  return hipGetLastError();
-}
-
 template <int OP, bool CFSEL, bool NT>
 __global__ void __launch_bounds__(256) k_sell_wide(SpArgs p) {
   constexpr int KCH = 32;       // entries per row and chunk: 64 x 32 products = 16 KiB of LDS

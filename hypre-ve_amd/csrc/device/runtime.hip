@@ -844,7 +844,6 @@ DevAMG::~DevAMG() { release(); }
 
 void DevAMG::release() {
   graphs_clear();
-  rr_.release();
   for (auto& L : lev_) {
     L.A.release(); L.P.release(); L.R.release();
     L.hu.release(); L.hv.release();
@@ -1125,25 +1124,13 @@ double bench_operator(const CSR& A, int op, int policy, int nbands, int reps, do
   return ms / reps;
 }
 
-void DevRR::release() {
-  for (void* p : {(void*)bptr, (void*)bent, (void*)bcptr, (void*)bcnt, (void*)brow, (void*)blb, (void*)blen, (void*)code,
-                  (void*)vtab, (void*)bval, (void*)odz, (void*)odxy})
-    if (p) (void)hipFree(p);
-  bptr = bent = bcptr = bcnt = brow = odz = odxy = nullptr;
-  blb = code = nullptr;
-  blen = nullptr;
-  vtab = bval = nullptr;
-  nvtab = notab = vbits = nbuckets = 0;
-  entries = 0;
-}
-
 // Fine grid of level 0 from its operator (row i is grid point i + shift),
 // read off an interior row: line =
 // its smallest column offset above 1 (plus one when that offset + 1 is also a
 // neighbour: the diagonal neighbours of a 27-point stencil), plane = its
 // largest offset (minus line + 1 for a 27-point stencil); nx = line,
-// ny = plane / line.  Only a guess: build_rr checks every restriction entry
-// against it, and any factorisation that passes gives the same sums.
+// ny = plane / line.  Only a guess: DevSell::build_grid checks every slot
+// offset against it, and any factorisation that passes gives the same sums.
 static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz, int shift) {
   const int n = A.nrows;
   if (n < 4096) return false;
@@ -1166,212 +1153,6 @@ static bool fine_grid(const CSR& A, int* nx, int* ny, int* nz, int shift) {
     return true;
   }
   return false;
-}
-
-// Level 0's fused residual + restriction (DevRR mode 1) or tiled restriction
-// (mode 2, k_tile_restrict), when level 0 is a grid operator on the stencil
-// layout held by one rank and every R_0 row reaches at most two points from
-// its coarse point's fine point in each direction.  Both off by default:
-// measured at 512^3 the tiled restriction took 3.46 ms against 1.59 for the
-// offset-coded rows (each bucket round waits on its code loads; 2 workgroups
-// a CU), the fused kernel 8.35 ms (HVE_TILE_R=1 / knob 10, HVE_FUSE_RR=1 /
-// knob 8 turn them on; profiles/r04/07_tile_restrict).
-// fc: the fine point of each coarse point.
-void DevAMG::build_rr(const RankHierarchy& R, const std::vector<int>& fc) {
-  static const int env = [] {
-    const char* e = getenv("HVE_FUSE_RR");
-    return e ? atoi(e) : 0;
-  }();
-  static const int zc_env = [] {
-    const char* e = getenv("HVE_RR_ZC");
-    return e ? atoi(e) : 64;
-  }();
-  static const int tile_env = [] {
-    const char* e = getenv("HVE_TILE_R");
-    return e ? atoi(e) : 0;
-  }();
-  rr_.release();
-  const int kn = knob(8);   // hypreve_SetKnob(8, 1 / -1) turns it on / off for this setup (tests)
-  const int kt = knob(10);  // the same for the tiled restriction (k_tile_restrict)
-  const bool fused = kn > 0 || (kn == 0 && env);
-  const bool tiled = !fused && (kt > 0 || (kt == 0 && tile_env));
-  if (!(fused || tiled) || R.lev.size() < 2 || comm_) return;
-  const RankLevel& L = R.lev[0];
-  const DevLevel& D = lev_[0];
-  auto identity = [](const std::vector<int>& m, int n) {
-    if (m.empty()) return true;
-    if ((int)m.size() != n) return false;
-    for (int i = 0; i < n; ++i)
-      if (m[i] != i) return false;
-    return true;
-  };
-  const bool log = getenv("HVE_LAYOUT_LOG") != nullptr;
-  auto decline = [&](const char* why) {
-    if (log) fprintf(stderr, "[layout] no fused residual+restriction: %s\n", why);
-  };
-  if (!D.A.in.slot_mask) return decline("level 0's operator is not on the stencil layout");
-  if (D.A.bd.nrows || D.A.in.rowmap || D.R.bd.nrows || L.hv.n_halo || L.hu.n_halo)
-    return decline("level 0 is not a one-rank operator in natural order");
-  if (!identity(L.A.map_int, L.A.interior.nrows) || !identity(L.R.map_int, L.R.interior.nrows))
-    return decline("rows are not in natural order");
-  const CSR& A = L.A.interior;
-  const CSR& Rm = L.R.interior;
-  int nx, ny, nz;
-  if (!fine_grid(A, &nx, &ny, &nz) || nx % kRRTx || (int)fc.size() != Rm.nrows)
-    return decline("no grid with a multiple of 64 points a line");
-  const int ty = kRRTy, zc = std::max(1, std::min(zc_env, nz));
-  const int ntx = nx / kRRTx, nty = (ny + ty - 1) / ty, nzc = (nz + zc - 1) / zc;
-  const int nb = ntx * nty * nz;
-  const int nc = Rm.nrows;
-  constexpr int PX = kRRTx + 4;
-  // every entry: (dx, dy, dz) from the anchor, each within +-2
-  std::vector<int> okey(125, -1), ocode;  // (dz, dy, dx) + 2 in base 5 -> offset index
-  std::vector<int> bucket(nc);
-  bool ok = true;
-  for (int c = 0; c < nc && ok; ++c) {
-    const int a = fc[c];
-    const int xa = a % nx, ya = (a / nx) % ny, za = a / (nx * ny);
-    bucket[c] = ((ya / ty) * ntx + xa / kRRTx) * nz + za;
-    for (int k = Rm.i[c]; k < Rm.i[c + 1]; ++k) {
-      const int j = Rm.j[k];
-      const int dx = j % nx - xa, dy = (j / nx) % ny - ya, dz = j / (nx * ny) - za;
-      if (std::abs(dx) > 2 || std::abs(dy) > 2 || std::abs(dz) > 2) { ok = false; break; }
-      const int key = ((dz + 2) * 5 + dy + 2) * 5 + dx + 2;
-      if (okey[key] < 0) {
-        okey[key] = (int)ocode.size();
-        ocode.push_back(key);
-      }
-    }
-  }
-  if (!ok) return decline("a restriction row reaches beyond two points");
-  // the weights as a value table (16-bit codes: offset index << vbits | value
-  // index), or, with more than 4096 of them (the 27-point hierarchy), one f64
-  // per entry beside a code that is the offset index alone
-  std::vector<unsigned short> vi16;
-  std::vector<double> tab;
-  const bool vt = build_value_table16(Rm.a, 4096, vi16, tab);
-  int vbits = 0;
-  if (vt)
-    while ((1 << vbits) < (int)tab.size()) ++vbits;
-  if ((int)ocode.size() > (1 << (16 - vbits))) return decline("codes do not fit 16 bits");
-  // buckets: rows by (tile, plane), each bucket's rows by length, descending
-  std::vector<int> bptr(nb + 1, 0);
-  for (int c = 0; c < nc; ++c) bptr[bucket[c] + 1]++;
-  for (int b = 0; b < nb; ++b) bptr[b + 1] += bptr[b];
-  std::vector<int> brow(nc);
-  {
-    std::vector<int> pos(bptr.begin(), bptr.end() - 1);
-    for (int c = 0; c < nc; ++c) brow[pos[bucket[c]]++] = c;
-  }
-  std::vector<int64_t> bent(nb + 1, 0);
-  std::vector<int> bcptr(nb + 1, 0);
-#pragma omp parallel for schedule(dynamic, 64)
-  for (int b = 0; b < nb; ++b) {
-    auto len = [&](int c) { return Rm.i[c + 1] - Rm.i[c]; };
-    std::stable_sort(brow.begin() + bptr[b], brow.begin() + bptr[b + 1],
-                     [&](int p, int q) { return len(p) > len(q); });
-    int64_t e = 0;
-    for (int q = bptr[b]; q < bptr[b + 1]; ++q) e += len(brow[q]);
-    bent[b + 1] = e;
-    bcptr[b + 1] = bptr[b + 1] > bptr[b] ? len(brow[bptr[b]]) + 1 : 0;
-  }
-  for (int b = 0; b < nb; ++b) {
-    bent[b + 1] += bent[b];
-    bcptr[b + 1] += bcptr[b];
-  }
-  if (bent[nb] >= INT_MAX) return decline("too many entries");
-  // the tiled kernel's 32-bit buffer offsets (codes, f64 weights, r)
-  if (tiled && (bent[nb] * (vt ? 2 : 8) >= ((int64_t)1 << 32) || (int64_t)A.nrows * 8 >= ((int64_t)1 << 32)))
-    return decline("restriction or residual past 4 GiB");
-  std::vector<int> bcnt(std::max(1, bcptr[nb]));
-  std::vector<unsigned short> code((size_t)std::max<int64_t>(1, bent[nb]));
-  std::vector<double> bval(vt ? 0 : (size_t)std::max<int64_t>(1, bent[nb]));
-  std::vector<unsigned short> blb(nc);
-  std::vector<unsigned char> blen(nc);
-  bool fits = true;
-#pragma omp parallel for schedule(dynamic, 64) reduction(&& : fits)
-  for (int b = 0; b < nb; ++b) {
-    const int r0 = bptr[b], r1 = bptr[b + 1];
-    if (r0 == r1) continue;
-    const int w = Rm.i[brow[r0] + 1] - Rm.i[brow[r0]];
-    int* cnt = &bcnt[bcptr[b]];
-    cnt[0] = 0;
-    for (int k = 0; k < w; ++k) {
-      int nk = 0;
-      while (r0 + nk < r1 && Rm.i[brow[r0 + nk] + 1] - Rm.i[brow[r0 + nk]] > k) ++nk;
-      cnt[k + 1] = cnt[k] + nk;
-    }
-    const int tx0 = ((b / nz) % ntx) * kRRTx, ty0 = ((b / nz) / ntx) * ty;
-    for (int q = r0; q < r1; ++q) {
-      const int c = brow[q];
-      const int a = fc[c];
-      const int xa = a % nx, ya = (a / nx) % ny;
-      const int len = Rm.i[c + 1] - Rm.i[c];
-      if (len > 255) fits = false;
-      blen[q] = (unsigned char)std::min(len, 255);
-      blb[q] = (unsigned short)((ya - ty0 + 2) * PX + (xa - tx0 + 2));
-      for (int k = 0; k < len; ++k) {
-        const int kk = Rm.i[c] + k, j = Rm.j[kk];
-        const int key = ((j / (nx * ny) - a / (nx * ny) + 2) * 5 + (j / nx) % ny - ya + 2) * 5 + j % nx - xa + 2;
-        const size_t e = (size_t)bent[b] + cnt[k] + (q - r0);
-        if (vt) {
-          code[e] = (unsigned short)((okey[key] << vbits) | vi16[kk]);
-        } else {
-          code[e] = (unsigned short)okey[key];
-          bval[e] = Rm.a[kk];
-        }
-      }
-    }
-  }
-  if (!fits) return decline("a restriction row longer than 255");
-  std::vector<int> odz(ocode.size()), odxy(ocode.size());
-  for (size_t o = 0; o < ocode.size(); ++o) {
-    const int key = ocode[o], dx = key % 5 - 2, dy = (key / 5) % 5 - 2, dz = key / 25 - 2;
-    odz[o] = dz;
-    odxy[o] = dy * PX + dx;
-  }
-  std::vector<int> bent32(nb + 1);
-  for (int b = 0; b <= nb; ++b) bent32[b] = (int)bent[b];
-  rr_.nx = nx; rr_.ny = ny; rr_.nz = nz; rr_.ty = ty; rr_.zc = zc;
-  rr_.ntx = ntx; rr_.nty = nty; rr_.nzc = nzc;
-  rr_.nbuckets = nb;
-  rr_.entries = bent[nb];
-  rr_.mode = fused ? 1 : 2;
-  rr_.bptr = dupload(bptr.data(), bptr.size());
-  rr_.bent = dupload(bent32.data(), bent32.size());
-  rr_.bcptr = dupload(bcptr.data(), bcptr.size());
-  rr_.bcnt = dupload(bcnt.data(), bcnt.size());
-  rr_.brow = dupload(brow.data(), std::max<size_t>(1, brow.size()));
-  rr_.blb = dupload(blb.data(), std::max<size_t>(1, blb.size()));
-  rr_.blen = dupload(blen.data(), std::max<size_t>(1, blen.size()));
-  rr_.code = dupload(code.data(), code.size());
-  if (vt) {
-    rr_.vtab = dupload(tab.data(), tab.size());
-    rr_.nvtab = (int)tab.size();
-  } else {
-    rr_.bval = dupload(bval.data(), bval.size());
-  }
-  rr_.odz = dupload(odz.data(), odz.size());
-  rr_.odxy = dupload(odxy.data(), odxy.size());
-  rr_.notab = (int)ocode.size();
-  rr_.vbits = vbits;
-  if (getenv("HVE_LAYOUT_LOG"))
-    fprintf(stderr, "[layout] fused residual+restriction: grid %dx%dx%d, tiles %dx%d, %d-plane chunks, %d offsets, "
-            "%s, %lld entries\n", nx, ny, nz, kRRTx, ty, zc, rr_.notab, vt ? "16-bit value table" : "f64 values",
-            (long long)rr_.entries);
-}
-
-RRView DevAMG::rr_view() const {
-  const DevSell& A = lev_[0].A.in;
-  RRView v;
-  v.slice_pat = A.slice_pat; v.slot_off = A.slot_base; v.slot_vi = A.slot_vi; v.slot_mask = A.slot_mask;
-  v.vtabA = A.vtab; v.sw = A.stencil_w; v.npat = A.npat;
-  v.nx = rr_.nx; v.ny = rr_.ny; v.nz = rr_.nz; v.ty = rr_.ty; v.zc = rr_.zc;
-  v.ntx = rr_.ntx; v.nty = rr_.nty; v.nzc = rr_.nzc;
-  v.bptr = rr_.bptr; v.bent = rr_.bent; v.bcptr = rr_.bcptr; v.bcnt = rr_.bcnt; v.brow = rr_.brow;
-  v.blb = rr_.blb; v.blen = rr_.blen; v.code = rr_.code; v.vtabR = rr_.vtab; v.odz = rr_.odz; v.odxy = rr_.odxy;
-  v.nvtabR = rr_.nvtab; v.notab = rr_.notab; v.vbits = rr_.vbits; v.bval = rr_.bval; v.entries = rr_.entries;
-  return v;
 }
 
 void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
@@ -1404,7 +1185,6 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   tile_keys(R, agg_level_, tiles);
   const bool tlog = getenv("HVE_SETUP_T") != nullptr;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
-  std::vector<int> fc0;  // level 0: the fine point of each coarse point
   for (int l = 0; l < nl; ++l) {
     const double tl0 = now();
     const RankLevel& L = R.lev[l];
@@ -1451,7 +1231,6 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       D.P.upload(L.P, prm.sell_policy, kl, pc);
       D.R.upload(L.R, prm.sell_policy, kc, rc, tc);
       D.hv.upload(L.hv);
-      if (l == 0) fc0 = fc;
     }
     if (!L.l1.empty()) D.l1 = dupload(L.l1.data(), L.l1.size());
     D.l1_fly = !L.l1.empty() && l1_on_the_fly(L.A, L.l1) && D.A.in.delta_like() && (D.A.bd.nrows == 0 || D.A.bd.delta_like());
@@ -1519,7 +1298,6 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       if (fwd && bwd) D.gs_tmp = dalloc<double>((size_t)D.n + 1);
     }
   }
-  build_rr(R, fc0);
   size_nrm_parts();
   coarse_n_ = R.coarse_n;
   if (coarse_n_ > 0) {
@@ -1939,16 +1717,6 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       const bool fuse_zg = !into_agg && coarse != nl - 1 && prm.num_sweeps[1] >= 1 && prm.relax_order != 1 &&
                            (prm.relax_type[1] == 18 || prm.relax_type[1] == 7) && prm.wt(coarse) == 1.0 &&
                            lev_[coarse].l1 != nullptr;
-      if (fine == 0 && rr_.built() && rr_.mode == 1 && !into_agg) {
-        // F_c = P^T (f - A u) in one pass: the residual stays in LDS
-        HVE_HIP(launch_resid_restrict(rr_view(), ucur[fine], fl[fine], lev_[coarse].F,
-                                      fuse_zg ? ucur[coarse] : nullptr, fuse_zg ? lev_[coarse].l1 : nullptr, s));
-      } else if (fine == 0 && rr_.built() && !into_agg) {
-        // Vtemp = f - A u, then F_c = P^T Vtemp over grid tiles (Vtemp staged in LDS)
-        apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);
-        HVE_HIP(launch_tile_restrict(rr_view(), Lf.n, Lf.V, lev_[coarse].F, fuse_zg ? ucur[coarse] : nullptr,
-                                     fuse_zg ? lev_[coarse].l1 : nullptr, s));
-      } else {
       // Vtemp = f - A u  (csr_matvec.c, alpha=-1 beta=1);  F_c = P^T Vtemp
       apply(Lf.A, &Lf.hu, K_RESID, ucur[fine], fl[fine], nullptr, nullptr, 0, Lf.V, -1.0, 0.0, s);
       if (fuse_zg) {
@@ -1961,7 +1729,6 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
         allgather_rows(lev_[coarse].F, agg_starts_, s);
       } else {
         apply(Lf.R, &Lf.hv, K_RESTRICT, Lf.V, nullptr, nullptr, nullptr, 0, lev_[coarse].F, 1.0, 0.0, s);
-      }
       }
       ++level;
       lev_counter[level] = std::max(lev_counter[level], prm.cycle_type);

@@ -181,34 +181,6 @@ struct DevGs {
   void release();
 };
 
-// Level 0's residual fused with its restriction (k_resid_restrict): the fine
-// grid in tiles of kRRTx x ty points and chunks of zc planes, the residual
-// of a tile's planes (plus a two-point margin) formed into an LDS ring, and
-// the R_0 rows anchored in the tile applied from it, so r never goes to HBM.
-// R_0's rows in buckets (tile, plane), each bucket's rows sorted by length and
-// stored jagged: entry k of bucket row j at ent[b] + cnt[cptr[b] + k] + j, one
-// 16-bit code (offset index << vbits | value index) per entry.
-struct DevRR {
-  int nx = 0, ny = 0, nz = 0, ty = 0, zc = 0, ntx = 0, nty = 0, nzc = 0;
-  int* bptr = nullptr;   // buckets + 1: rows of bucket b = (ty_i * ntx + tx_i) * nz + z
-  int* bent = nullptr;   // per bucket: first entry
-  int* bcptr = nullptr;  // per bucket: its prefix counts in bcnt (width + 1 values)
-  int* bcnt = nullptr;
-  int* brow = nullptr;   // per bucket row: the coarse row
-  unsigned short* blb = nullptr;  // per bucket row: the anchor's LDS index in its plane
-  unsigned char* blen = nullptr;  // per bucket row: entries
-  unsigned short* code = nullptr;
-  double* vtab = nullptr;  // the weights (16-bit codes), or
-  double* bval = nullptr;  // one weight per entry (codes: the offset index alone)
-  int* odz = nullptr;    // per offset index: dz
-  int* odxy = nullptr;   // per offset index: dy * (kRRTx + 4) + dx
-  int nvtab = 0, notab = 0, vbits = 0, nbuckets = 0;
-  int64_t entries = 0;
-  int mode = 0;  // 1: fused residual + restriction (k_resid_restrict), 2: tiled restriction (k_tile_restrict)
-  bool built() const { return bptr != nullptr; }
-  void release();
-};
-
 struct DevHalo {
   int n_loc = 0, n_halo = 0, n_send = 0;
   std::vector<int> peers, recv_cnt, recv_off, send_cnt, send_off;
@@ -288,16 +260,6 @@ class DevAMG {
   };
   const std::vector<CycleComm>& cycle_comm() const { return cycle_comm_; }
   bool multi_rank() const { return comm_ != nullptr; }
-  int fused_rr() const { return rr_.built() ? rr_.mode : 0; }
-  RRView rr_view() const;
-  int rr_fine_rows() const { return rr_.nx * rr_.ny * rr_.nz; }
-  // bytes one tiled restriction streams: codes (+ f64 weights), the bucket
-  // rows' anchor / length / row, the value and offset tables, r once, F_c
-  double rr_tile_bytes(int ncoarse) const {
-    return (double)rr_.entries * (rr_.bval ? 10.0 : 2.0) + (double)ncoarse * (2 + 1 + 4 + 8) +
-           (double)rr_.nvtab * 8 + (double)rr_.notab * 8 + (double)(rr_.nbuckets + 1) * 12 +
-           (double)rr_fine_rows() * 8;
-  }
   // Re-key the row-block traversal (tuning; see locality_keys in runtime.hip).
   // which_mask: bit 0 the A operators, bit 1 P, bit 2 R
   void set_block_bands(const RankHierarchy& R, int nbands, int which_mask = 7);
@@ -358,8 +320,6 @@ class DevAMG {
   int comm_level_ = -1;  // level whose exchanges are being counted (emit_cycle), -1 = none
   int ws_n_ = 0;
   std::map<std::tuple<const void*, const void*, int>, hipGraphExec_t> graphs_;  // (f, u, presmoothed + 2 zero_u)
-  DevRR rr_;                      // level 0's fused residual + restriction or tiled restriction (single rank, grid operator)
-  void build_rr(const RankHierarchy& R, const std::vector<int>& fc);
   int agg_level_ = -1;            // first replicated level (RankHierarchy::agg_level)
   std::vector<int> agg_starts_;   // its rows' distributed owners
 };

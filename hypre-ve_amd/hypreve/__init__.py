@@ -194,7 +194,6 @@ SIGNATURES = [
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BoomerAMGGsScheduleStats", _i, [_p, _i, _i, _i, _pi64]),
     ("hypreve_BoomerAMGGetCycleCommStats", _i, [_p, _i, _pi64]),
-    ("hypreve_BoomerAMGGetFusedResidRestrict", _i, [_p, _pi]),
     ("hypreve_BoomerAMGStencilLayoutCheck", _i, [_p, _i, _pi, _pi]),
     ("hypreve_GridStencilAddressable", _i, [_i, _i, _i]),
     ("hypreve_BoomerAMGCodedLayoutCheck", _i, [_p, _i, _i, _pi, _pi]),
@@ -559,13 +558,6 @@ class BoomerAMG:
 
     def gs_schedule_check(self, num_blocks):
         check(lib().hypreve_BoomerAMGGsScheduleCheck(self.h, num_blocks), "GsScheduleCheck")
-
-    def fused_resid_restrict(self):
-        """Level 0's restriction kernel: 1 fused with the residual, 2 over
-        LDS-staged grid tiles of the stored residual, 0 the per-row loop."""
-        v = C.c_int()
-        check(lib().hypreve_BoomerAMGGetFusedResidRestrict(self.h, C.byref(v)), "GetFusedResidRestrict")
-        return v.value
 
     def cycle_comm_stats(self):
         """This rank's communication in one V-cycle, per level: halo exchanges,

@@ -359,12 +359,6 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, 
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
 HYPRE_Int hypreve_BoomerAMGGsScheduleCheck(HYPRE_Solver solver, HYPRE_Int num_blocks);
-/* *on = 1 when the cycle forms level 0's residual and its restriction in one
- * pass (the residual never stored: a single rank, level 0 a grid operator on
- * the stencil layout, R_0 within two points of each coarse point), 2 when it
- * restricts the stored residual over grid tiles staged in LDS (same
- * conditions), 0 otherwise. */
-HYPRE_Int hypreve_BoomerAMGGetFusedResidRestrict(HYPRE_Solver solver, HYPRE_Int *on);
 /* This rank's communication in one V-cycle (the last one run), level `level`:
  * out[5] = {halo exchanges, bytes they send, all-gathers into the replicated
  * levels, their bytes sent, all-reduces}; zeros on one rank. */

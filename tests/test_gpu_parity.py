@@ -405,57 +405,6 @@ def test_interp_types_bitwise(gpu, orc, interp, agg, agg_interp, order):
     assert np.array_equal(x.get(), xo)
 
 
-# sizes from 2^18 rows up: smaller finest operators take the wide layout, not
-# the stencil layout the fused kernel reads A_0 from
-@pytest.mark.parametrize("mode", [1, 2])
-@pytest.mark.parametrize("gen,n3,relax", [("7", (128, 64, 40), 18), ("7", (64, 72, 64), 18), ("7", (128, 64, 40), 0),
-                                          ("27", (64, 66, 64), 18), ("aniso", (64, 66, 64), 18),
-                                          ("7", (128, 64, 40), 13)])
-def test_fused_resid_restrict_bitwise(gpu, orc, gen, n3, relax, mode):
-    """Level 0's residual fused with its restriction (mode 1:
-    k_resid_restrict, the residual kept in an LDS ring of planes,
-    par_cycle.c:549-566) and the tiled restriction of the stored residual
-    (mode 2: k_tile_restrict, the residual staged in an LDS ring of tile
-    planes): with the coarse zero-guess sweep folded in (relax 18) and
-    without (0, 13), the 7-point, 27-point and anisotropic operators, a
-    V-cycle from a random iterate and a 3-iteration solve equal the oracle bit
-    for bit, and the kernel asked for is the one that ran."""
-    hv = gpu
-    if gen == "27":
-        A = hv.ParCSRMatrix.laplacian27(*n3)
-    elif gen == "aniso":
-        A = hv.ParCSRMatrix.laplacian(*n3, cx=0.001, cy=1.0, cz=1.0)
-    else:
-        A = hv.ParCSRMatrix.laplacian(*n3)
-    kw = hv.ij_amg_defaults(0)
-    kw.update(coarsen_type=8, relax_type=relax, P_max_elmts=4)
-    amg = hv.BoomerAMG(**kw)
-    hv.set_knob(8 if mode == 1 else 10, 1)  # the kernel for this setup
-    try:
-        amg.setup(A)
-    finally:
-        hv.set_knob(8, 0)
-        hv.set_knob(10, 0)
-    assert amg.fused_resid_restrict() == mode
-    O = orc.OracleAMG(amg)
-    n = A.n
-    rng = np.random.default_rng(3)
-    f_h = rng.standard_normal(n)
-    u0 = rng.standard_normal(n)
-    f = hv.ParVector(n, f_h)
-    u = hv.ParVector(n, u0)
-    amg.cycle(f, u)
-    uo = u0.copy()
-    O.cycle(f_h, uo)
-    assert np.array_equal(u.get(), uo)
-    amg.set(tol=0.0, max_iter=3)
-    x = hv.ParVector(n, np.zeros(n))
-    amg.solve(A, f, x)
-    xo = np.zeros(n)
-    O.solve(f_h, xo, 0.0, 3)
-    assert np.array_equal(x.get(), xo)
-
-
 # grids with 64 | nx and from 2^18 rows up (the stencil layout); ny and nz not
 # multiples of the tile (16 lines) or of the planes a workgroup marches
 @pytest.mark.parametrize("gen,n3,relax,wt,zc", [("7", (64, 64, 64), 18, 1.0, 0), ("27", (64, 66, 64), 18, 1.0, 7),
