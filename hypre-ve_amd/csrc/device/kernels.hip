@@ -102,6 +102,7 @@ struct SpArgs {
   int relax_points;
   const GSlot* __restrict__ gslot;           // grid stencil (k_grid_stencil)
   int gnx, gny, gnz, gzc, gz0, gz1;
+  int dexp;  // timing-only builds (-DHVE_DICT_EXP): phases of k_sell_dict left out (knob 12)
 };
 
 // Logical workgroup block -> stored row block (SpArgs::blk_map): the
@@ -1344,12 +1345,19 @@ __global__ void __launch_bounds__(256) k_sell_pw(SpArgs p) {
 // ---------------------------------------------------------------------------
 template <int B, bool NT, class V>
 __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp, const V& vl, int& P, int k, int blen,
-                                          int llen, int (&c)[B], typename V::raw (&a)[B]) {
+                                          int llen, int (&c)[B], typename V::raw (&a)[B], int dexp = 0) {
 #pragma unroll
   for (int q = 0; q < B; ++q) {
     const bool in = (k + q) < llen;
+#ifdef HVE_DICT_EXP
+    // timing only: 2 leaves out the column loads, 4 the value loads
+    c[q] = in ? ((dexp & 2) ? (int)((threadIdx.x + q) & 255) : (int)mload<NT>(cp + P)) : -1;
+    a[q] = in ? ((dexp & 4) ? typename V::raw(1) : vl.template load<NT>(P)) : V::none();
+#else
+    (void)dexp;
     c[q] = in ? (int)mload<NT>(cp + P) : -1;
     a[q] = in ? vl.template load<NT>(P) : V::none();
+#endif
     P += __popcll(__ballot((k + q) < blen));
   }
 }
@@ -1406,10 +1414,14 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   for (int k = 0; k < k0; ++k) P += __popcll(__ballot(k < blen));
   int c[B];
   typename V::raw a[B];
-  dict_load<B, NT>(cp, vl, P, k0, blen, llen, c, a);
+  dict_load<B, NT>(cp, vl, P, k0, blen, llen, c, a, p.dexp);
   // 1. x-tile -> LDS, TG loads in flight per thread
   constexpr int TG = HVE_DICT_TG;
   constexpr int NT_ = 64 * G;
+#ifdef HVE_DICT_EXP
+  if (p.dexp & 1) {  // timing only: no x-tile gather
+  } else
+#endif
   if (p.dict_ranges) {
     // Range dictionary: the tile is the concatenation of at most 63 column
     // ranges; lane k of every wave holds pair k (start, offset; the terminal
@@ -1474,7 +1486,7 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   for (int k = k0; k < width; k += B) {
     int cn[B];
     typename V::raw an[B];
-    dict_load<B, NT>(cp, vl, P, k + B, blen, llen, cn, an);
+    dict_load<B, NT>(cp, vl, P, k + B, blen, llen, cn, an, p.dexp);
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       if (c[q] >= 0) {
@@ -1984,6 +1996,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   const bool pipe = sell_pipe_override() >= 0 ? sell_pipe_override() == 1 : M.pipe != 0;
   const bool nt = sell_nt();
   const bool jag = M.rowlen != nullptr;
+  a.dexp = knob(12);
   if (M.col16) {  // dictionary layout: G waves per workgroup share an x-tile in LDS
     const int G = M.dict_group;
     const int ngroups = ((M.nrows + 63) / 64 + G - 1) / G;
