@@ -1362,6 +1362,10 @@ __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp,
   }
 }
 
+// The dictionary loop's long-row batch (compile-time experiments: 12)
+#ifndef HVE_DICT_B16
+#define HVE_DICT_B16 16
+#endif
 #ifndef HVE_DICT_TG
 #define HVE_DICT_TG (G == 4 ? 12 : 16 / G > 4 ? 16 / G : 4)
 #endif
@@ -2034,7 +2038,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     else hipLaunchKernelGGL((k_sell_dict<OPV, CF, BB, false, 1>), dgrid, dblock, lds, s, a);          \
   }
 #define HVE_DB(OPV, CF) \
-  if (bsel == 16) { HVE_D(OPV, CF, 16) } else { HVE_D(OPV, CF, 8) }
+  if (bsel == 16) { HVE_D(OPV, CF, HVE_DICT_B16) } else { HVE_D(OPV, CF, 8) }
 #define HVE_DL(OPV)                                                 \
   case OPV:                                                         \
     if (cfsel) { HVE_DB(OPV, true) } else { HVE_DB(OPV, false) }   \
