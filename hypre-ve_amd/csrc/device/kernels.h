@@ -115,7 +115,10 @@ struct GsView {
   const double* l1 = nullptr;      // l1 norms by position
   const int* cf = nullptr;         // CF marker by position
   int nteams = 0, nrows = 0, max_width = 0;
+  bool one_chunk = false;  // every step's rows x width fits one product chunk (k_hybrid_gs_pipe)
 };
+// entries of one product chunk of the hybrid-GS kernels (LDS per wave)
+int gs_chunk_entries();
 // The sweep's vectors in its order (layout.hpp GsSchedule): G[k] = tmp[rowmap[k]]
 // (T; u when tmp is null), G[n + k] = u[rowmap[k]] (C), F[k] = f[rowmap[k]],
 // and the off-rank halo of u, u[n .. n + nhalo), into G[3n ..).

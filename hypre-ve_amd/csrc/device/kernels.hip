@@ -1554,6 +1554,7 @@ struct GsArgs {
 static constexpr int kGsWaves = 4;           // teams per workgroup
 static constexpr int kGsProd = 512;          // LDS products per wave and chunk
 static constexpr int kGsPer = kGsProd / 64;  // entries per lane and chunk
+int gs_chunk_entries() { return kGsProd; }
 // U stores leave the ring in batches of kGsBatch steps (host/layout.hpp): on
 // CDNA a load waits for every older vector-memory operation, stores included,
 // so a store per step would put a store's completion on every step's critical
@@ -1697,6 +1698,153 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
   }
 }
 
+// The same sweep, software-pipelined across steps (every step of the
+// operator fits one chunk: rows x width <= kGsProd).  Only the LDS ring
+// carries a dependence from one step to the next, so a step's loads need not
+// wait for the previous step: while step j is summed, step j + 1's source
+// values (C, T, U and halo gathers through its codes) and step j + 2's codes,
+// values and row data are in flight.  Each step then costs its LDS work, not
+// two dependent global-memory round trips.  The U gathers of step j + 1 are
+// issued during step j, after the fence of step j - 1; the schedule's U codes
+// reach back at least kGsFence + 1 = 16 steps and a value computed at step q
+// is fenced at the end of step q - q % kGsBatch + 2 kGsBatch - 1 (kGsBatch 4),
+// so every U value a gather reads was published before it was issued
+// (gs_schedule_self_check emulates this: U read for step j visible only from
+// fences of steps <= j - 2).  Every row is summed as in k_hybrid_gs.
+// ---------------------------------------------------------------------------
+struct GsStage {
+  int c[kGsPer], tc[kGsPer];
+  double a[kGsPer];
+  double uo, fv, sc;
+  int cfv, R, W, roff;
+};
+
+template <bool L1, bool CFSEL, bool WGT>
+__global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
+  __shared__ double ring_all[kGsWaves][kGsRingSlots];
+  __shared__ double prod_all[kGsWaves][kGsProd];
+  __shared__ double prod2_all[kGsWaves][WGT ? kGsProd : 1];
+  __shared__ unsigned char cls_all[kGsWaves][WGT ? kGsProd : 1];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int team = blockIdx.x * kGsWaves + wave;
+  if (team >= p.nteams) return;
+  double* ring = ring_all[wave];
+  double* prod = prod_all[wave];
+  double* prod2 = prod2_all[wave];
+  unsigned char* cls = cls_all[wave];
+  const int s0 = __builtin_amdgcn_readfirstlane(p.team_step[team]);
+  const int ns = __builtin_amdgcn_readfirstlane(p.team_step[team + 1]) - s0;
+  using cint = const __attribute__((address_space(4))) int;
+  cint* const steps = (cint*)(p.step + 4 * (size_t)s0);
+  constexpr int k0 = (L1 && !WGT) ? 0 : 1;
+  double* const Ub = p.G + 2 * (size_t)p.n;
+  const auto rG = gs_rsrc(p.G, p.gbytes);
+  const auto rC = gs_rsrc(p.G + p.n, (unsigned)p.n * 8u);
+  const auto rF = gs_rsrc(p.F, (unsigned)p.n * 8u);
+  const auto rL = gs_rsrc(L1 ? p.l1 : p.F, (unsigned)p.n * 8u);
+  const auto rCF = gs_rsrc(CFSEL ? (const void*)p.cf : (const void*)p.F, (unsigned)p.n * 4u);
+  // step j's codes, values and row data (never written during the sweep);
+  // every lane loads kGsPer entries (those past the step's read entry 0)
+  auto load_a = [&](int j, GsStage& S) {
+    const unsigned ent = (unsigned)steps[4 * j];
+    S.roff = steps[4 * j + 1];
+    S.R = steps[4 * j + 2];
+    S.W = steps[4 * j + 3];
+    const int r = lane < S.R ? lane : S.R - 1;
+    const int kp = S.roff + r;
+    const auto rc = gs_rsrc(p.code + ent, 0x7fffffffu);
+    const auto rv8 = gs_rsrc(p.val + ent, 0x7fffffffu);
+    const auto rt = gs_rsrc(WGT ? (const void*)(p.tcol + ent) : (const void*)(p.code + ent), 0x7fffffffu);
+    S.uo = gs_ld64(rC, (int)((unsigned)kp * 8u));
+    S.fv = gs_ld64(rF, (int)((unsigned)kp * 8u));
+    S.sc = L1 ? gs_ld64(rL, (int)((unsigned)kp * 8u)) : gs_ld64(rv8, r * 8);
+    S.cfv = CFSEL ? gs_ld32(rCF, kp * 4) : 0;
+    const int E = S.W * S.R;
+#pragma unroll
+    for (int t = 0; t < kGsPer; ++t) {
+      const int e = lane + 64 * t;
+      const int o = e < E ? e : 0;
+      S.c[t] = gs_ld32(rc, o * 4);
+      S.a[t] = gs_ld64(rv8, o * 8);
+      S.tc[t] = WGT ? gs_ld32(rt, o * 4) : -1;
+    }
+  };
+  // step j's source values from G (ring and padding codes read G[0], unused)
+  auto load_b = [&](const GsStage& S, double (&x)[kGsPer], double (&t2)[kGsPer]) {
+#pragma unroll
+    for (int t = 0; t < kGsPer; ++t) {
+      x[t] = gs_ld64(rG, (int)((unsigned)(S.c[t] > 0 ? S.c[t] : 0) * 8u));
+      t2[t] = WGT ? gs_ld64(rG, (int)((unsigned)(S.tc[t] > 0 ? S.tc[t] : 0) * 8u)) : 0.0;
+    }
+  };
+  GsStage S0, S1, S2;
+  double x0[kGsPer], x1[kGsPer], u0[kGsPer], u1[kGsPer];
+  if (ns > 0) load_a(0, S0);
+  if (ns > 1) load_a(1, S1);
+  if (ns > 0) load_b(S0, x0, u0);
+  for (int j = 0; j < ns; ++j) {
+    if (j + 2 < ns) load_a(j + 2, S2);
+    if (j + 1 < ns) load_b(S1, x1, u1);
+    const int R = S0.R, W = S0.W, E = W * R;
+    const int r = lane < R ? lane : R - 1;
+    double res = S0.fv, res0 = 0.0, res2 = 0.0;
+    double rv[kGsPer];
+#pragma unroll
+    for (int t = 0; t < kGsPer; ++t) rv[t] = ring[S0.c[t] < -1 ? -2 - S0.c[t] : 0];
+#pragma unroll
+    for (int t = 0; t < kGsPer; ++t) {
+      const int e = lane + 64 * t;
+      const int cc = S0.c[t];
+      const double xv = cc < -1 ? rv[t] : x0[t];
+      const double pv = cc == -1 ? 0.0 : S0.a[t] * xv;
+      if (e < E) {
+        prod[e] = pv;
+        if (WGT) {
+          prod2[e] = S0.tc[t] >= 0 ? S0.a[t] * u0[t] : 0.0;
+          cls[e] = S0.tc[t] >= 0;
+        }
+      }
+    }
+    gs_wave_sync();
+    for (int kk = k0; kk < W; ++kk) {
+      const int e = kk * R + r;
+      const double pv = prod[e];
+      if (WGT && cls[e]) {
+        res0 -= pv;
+        res2 += prod2[e];
+      } else {
+        res -= pv;
+      }
+    }
+    const bool run = lane < R && S0.sc != 0.0 && !(CFSEL && S0.cfv != p.relax_points);
+    double un = S0.uo;
+    if (WGT) {
+      double ui = un;
+      ui *= 1.0 - p.w * p.omega;
+      ui += p.w * (p.omega * res + res0 + (1.0 - p.omega) * res2) / S0.sc;
+      un = run ? ui : un;
+    } else {
+      const double v = L1 ? un + res / S0.sc : res / S0.sc;
+      un = run ? v : un;
+    }
+    ring[(j % kGsRing) * kWave + lane] = un;
+    gs_wave_sync();  // the next steps' lanes read the ring slot; the next products overwrite prod
+    if (j % kGsBatch == kGsBatch - 1 || j == ns - 1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      for (int q = j - j % kGsBatch; q <= j; ++q) {
+        const int rq = steps[4 * q + 2];
+        if (lane < rq) Ub[steps[4 * q + 1] + lane] = ring[(q % kGsRing) * kWave + lane];
+      }
+    }
+    S0 = S1;
+    S1 = S2;
+#pragma unroll
+    for (int t = 0; t < kGsPer; ++t) { x0[t] = x1[t]; u0[t] = u1[t]; }
+  }
+}
+
 // u[rowmap[k]] = U[k]: the sweep's result back in natural row order (NAT:
 // u[i] = U[pos[i]], rows in order).
 template <bool NAT>
@@ -1758,7 +1906,15 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   if (use_l1 && !S.l1) return hipErrorInvalidValue;
   if (cfsel && !S.cf) return hipErrorInvalidValue;
   const dim3 grid((S.nteams + kGsWaves - 1) / kGsWaves), blk(kGsWaves * kWave);
-#define HVE_G(L1V, CFV, WV) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV>), grid, blk, 0, st, a);
+  // the pipelined sweep where every step fits one chunk; HVE_GS_PIPE=0 keeps k_hybrid_gs
+  static const bool pipe_env = [] {
+    const char* e = getenv("HVE_GS_PIPE");
+    return e ? atoi(e) != 0 : true;
+  }();
+  const bool pipe = pipe_env && S.one_chunk;
+#define HVE_G(L1V, CFV, WV)                                                          \
+  if (pipe) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV>), grid, blk, 0, st, a); \
+  else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV>), grid, blk, 0, st, a);
 #define HVE_GW(L1V, CFV) \
   if (wgt) { HVE_G(L1V, CFV, true) } else { HVE_G(L1V, CFV, false) }
   if (use_l1) {

@@ -196,8 +196,26 @@ static bool pack_sell_codes(const std::vector<int>& sp, const std::vector<int>& 
   return true;
 }
 
+// HVE_SETUP_T: host stages of an operator's layout construction and upload
+namespace {
+struct SetupLap {
+  bool on = getenv("HVE_SETUP_T") != nullptr;
+  double t = now();
+  static double now() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+  }
+  void operator()(const char* what) {
+    if (!on) return;
+    const double n = now();
+    fprintf(stderr, "[upload]   %-32s %.3fs\n", what, n - t);
+    t = n;
+  }
+};
+}  // namespace
+
 void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy, const std::vector<int64_t>* key,
                      const Coded* coded, const std::vector<int64_t>* tile) {
+  SetupLap lap;
   release();
   // Offset-coded layout (P_0 / R_0 of a grid hierarchy: 25 offsets, ~1200
   // weights, so an entry is one 16-bit code, 2 B instead of 6) where the grid
@@ -280,6 +298,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
     return e ? atoi(e) : -1;
   }();
   const int64_t pad0 = A.nnz() > 0 ? sell_padded_nnz(A, 0) : 0;
+  lap("padding count");
   // Small operators (coarse levels) run one workgroup per slice with the
   // products formed in parallel (k_sell_wide): in the lane-per-row loop they
   // are latency-bound.  Measured on MI355X (256^3): every operator below 2^18
@@ -316,6 +335,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
     std::vector<unsigned short> probe;
     std::vector<double> probe_tab;
     if (build_value_table16(A.a, 4096, probe, probe_tab)) jag = false;
+    lap("value-table probe");
   }
   if (policy != 0) {  // forced (tests): every loop gives the same bits
     wide = policy == 3 ? 1 : 0;
@@ -471,6 +491,7 @@ dict:
         return g < (int)tile->size() ? (*tile)[g] : (int64_t)g;
       };
       std::stable_sort(pre.begin(), pre.end(), [&](int a, int b) { return tk(a) < tk(b); });
+      lap("dict tile order");
     }
     const std::vector<int>* prep = pre.empty() ? nullptr : &pre;
     std::vector<unsigned short> c16;
@@ -519,6 +540,7 @@ dict:
       }
     }
     if (built) {
+      lap("dict build");
       dict_group = group;
       dict_ranges = ranges ? 1 : 0;
       nrows = A.nrows;
@@ -567,6 +589,7 @@ dict:
       if (!ident) rowmap = dupload(map.data(), map.size());
       if (!ident) stored_map = map;
       if (key) set_block_order(map, *key);
+      lap("dict upload + row map");
       return;
     }
     perm.clear();  // a slice has too many distinct columns: fall back
@@ -578,6 +601,7 @@ dict:
     const int sigma = (sigma_env > 0 && A.nnz() > 0 && pad0 > A.nnz() + A.nnz() / 20) ? sigma_env : 0;
     build_sell_host(A, sigma, perm, sp, col, val);
   }
+  lap(jag ? "jagged build" : "padded build");
   nrows = A.nrows;
   ncols = A.ncols;
   nslices = (int)sp.size() - 1;
@@ -601,7 +625,9 @@ dict:
   std::vector<unsigned short> vi16;
   std::vector<double> tab;
   const bool try_vt16 = policy == 8 || policy == 9 || policy == 13 || (policy == 0 && !wide && sell_valtab_env() != 0);
-  if (try_vt16 && A.nnz() > 0 && build_value_table16(val, 4096, vi16, tab)) {
+  const bool vt_ok = try_vt16 && A.nnz() > 0 && build_value_table16(val, 4096, vi16, tab);
+  lap("value table");
+  if (vt_ok) {
     vtab = dupload(tab.data(), tab.size());
     nvtab = (int)tab.size();
     wide = 0;
@@ -641,6 +667,7 @@ dict:
   if (!ident) rowmap = dupload(map.data(), map.size());
   if (!ident) stored_map = map;
   if (key) set_block_order(map, *key);
+  lap("pack / upload / row map");
 }
 // A rank operator's rows in local order (interior and boundary merged, each
 // row's entries in stored order, columns in the [local | halo] space).
@@ -770,6 +797,9 @@ void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forw
   nteams = S.nteams;
   max_steps = S.max_steps;
   max_width = S.max_width;
+  one_chunk = true;  // k_hybrid_gs_pipe: every step's entries in one product chunk
+  for (size_t q = 0; q + 3 < S.step.size() && one_chunk; q += 4)
+    one_chunk = (int64_t)S.step[q + 2] * S.step[q + 3] <= gs_chunk_entries();
   entries = (int64_t)S.code.size();
   nnz = S.nnz;
   team_step = dupload(S.team_step.data(), S.team_step.size());
@@ -793,6 +823,7 @@ void DevGs::release() {
   team_step = step = code = tcol = rowmap = pos = cf = nullptr;
   val = l1 = nullptr;
   nrows = nteams = nblocks = max_steps = max_width = 0;
+  one_chunk = false;
   entries = nnz = 0;
 }
 

@@ -168,12 +168,14 @@ struct DevGs {
   double* l1 = nullptr;  // by position
   int* cf = nullptr;     // by position
   int nrows = 0, nteams = 0, nblocks = 0, max_steps = 0, max_width = 0;
+  bool one_chunk = false;
   int64_t entries = 0, nnz = 0;
   bool built() const { return nblocks > 0; }
   GsView view() const {
     GsView v;
     v.team_step = team_step; v.step = step; v.code = code; v.val = val; v.tcol = tcol; v.rowmap = rowmap;
     v.pos = pos; v.l1 = l1; v.cf = cf; v.nteams = nteams; v.nrows = nrows; v.max_width = max_width;
+    v.one_chunk = one_chunk;
     return v;
   }
   void upload(const CSR& A, const std::vector<int>& block_starts, bool forward, bool weighted,

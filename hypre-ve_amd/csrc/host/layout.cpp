@@ -908,9 +908,12 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
   }
   // the kernel's view: C / T / F permuted into the sweep order, U stores
   // visible only as k_hybrid_gs makes them (a batch's stores are issued at its
-  // last step and completed by the fence at the next batch's last step), the
-  // LDS ring keeps the last kGsRing steps
+  // last step and completed by the fence at the next batch's last step; the
+  // pipelined sweep gathers step j's U values during step j - 1, so they must
+  // have been fenced by the end of step j - 2), the LDS ring keeps the last
+  // kGsRing steps
   std::vector<double> C(n), T(n), F(n), U(n, std::nan(""));
+  std::vector<int> U_fenced(n, INT_MAX);  // the step whose end fence published U[k]
   std::vector<int> inv(n, -1);
   for (int k = 0; k < n; ++k) {
     if (S.rowmap[k] < 0 || S.rowmap[k] >= n || inv[S.rowmap[k]] >= 0) { msg = "rowmap is not a permutation"; return 1; }
@@ -972,7 +975,7 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
         out[q] = uo;
         if (scale == 0.0) continue;
         auto src = [&](int code) {
-          if (code >= 2 * n) return U[code - 2 * n];
+          if (code >= 2 * n) return U_fenced[code - 2 * n] <= j - 2 ? U[code - 2 * n] : std::nan("");
           if (code >= n) return C[code - n];
           if (code >= 0) return T[code];
           return ring[-2 - code];
@@ -1003,7 +1006,10 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
         ring[(size_t)(j % kGsRing) * 64 + q] = out[q];
       }
       if (j % kGsBatch == kGsBatch - 1 || s + 1 == S.team_step[t + 1]) {
-        for (auto& pr : issued) U[pr.first] = pr.second;  // the fence completes the previous batch
+        for (auto& pr : issued) {  // the fence completes the previous batch
+          U[pr.first] = pr.second;
+          U_fenced[pr.first] = j;
+        }
         issued.swap(batch);                                // then this batch's stores are issued
         batch.clear();
       }

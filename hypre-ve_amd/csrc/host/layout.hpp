@@ -119,9 +119,12 @@ constexpr int kGsRingSlots = kGsRing * 64;
 // end of a batch the wave fences, which completes the previous batch's stores,
 // then issues this batch's.  A value computed at step q is therefore visible
 // in U from step (q / kGsBatch + 2) * kGsBatch on, at most 2 kGsBatch steps
-// later: U codes need a distance of kGsFence + 1 >= 2 kGsBatch steps.
-constexpr int kGsBatch = kGsRing / 2;
-static_assert(2 * kGsBatch <= kGsFence + 1 && kGsFence < kGsRing, "ring reach");
+// later.  The pipelined sweep (k_hybrid_gs_pipe) issues step j's U gathers
+// during step j - 1, after the fence of step j - 2, so U codes need a distance
+// of 2 kGsBatch + 1 <= kGsFence + 1 steps; gs_schedule_self_check emulates
+// the stricter rule (a U read of step j sees fences of steps <= j - 2).
+constexpr int kGsBatch = 4;
+static_assert(2 * kGsBatch + 1 <= kGsFence + 1 && kGsFence < kGsRing, "ring reach");
 struct GsSchedule {
   std::vector<int> block_start;  // nb + 1 row boundaries (hypre's ns / ne)
   std::vector<int> team_step;    // nteams + 1: step range of each team

@@ -290,24 +290,31 @@ def test_gs_packed_schedule_size(hv, forward):
 
 
 def test_gs_self_check_models_the_kernel_fences(hv):
-    """gs_schedule_self_check emulates k_hybrid_gs's U publication (a batch
-    of kGsBatch = 8 steps is stored at its last step and fenced at the next
-    batch's last step: visible at most 16 steps after it was computed).  A
-    schedule that reads U one step early (knob 11 = 1: U codes from a distance
-    of 15 steps) is refused; a check that published U every 15 steps (the
-    round-4 emulator) passed it."""
+    """gs_schedule_self_check emulates the sweeps' U publication: a batch of
+    kGsBatch = 4 steps is stored at its last step and fenced at the next
+    batch's last step, and the pipelined sweep gathers step j's U values
+    during step j - 1, so they must have been fenced by the end of step j - 2:
+    a value is readable 9 steps after it was computed at the latest.  A
+    schedule whose U codes reach back only 8 steps (knob 11 = 8 shortens the
+    ring reach from 15 to 7) reads one step early and is refused."""
     A = hv.ParCSRMatrix.laplacian(14, 12, 11)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
     amg.set(coarsen_type=8, relax_type=13, P_max_elmts=4)
     amg.setup_host(A)
     amg.gs_schedule_check(1)
-    hv.set_knob(11, 1)
+    hv.set_knob(11, 6)  # U from 10 steps back: still published in time
+    try:
+        amg.gs_schedule_check(1)
+    finally:
+        hv.set_knob(11, 0)
+    hv.set_knob(11, 8)
     try:
         with pytest.raises(Exception, match="differs from the sequential sweep"):
             amg.gs_schedule_check(1)
     finally:
         hv.set_knob(11, 0)
     amg.gs_schedule_check(1)
+
 
 
 @pytest.mark.parametrize("size", [2, 3, 5, 8])
