@@ -1548,7 +1548,7 @@ HYPRE_Int hypreve_BoomerAMGCodedLayoutCheck(HYPRE_Solver s, HYPRE_Int level, HYP
     }
   static const std::vector<int> none;
   std::vector<int> sp, ot;
-  std::vector<unsigned short> code;
+  hvec<unsigned short> code;
   std::vector<double> tab;
   int vb = 0;
   // not coded (too many offsets or values): success with zero counts

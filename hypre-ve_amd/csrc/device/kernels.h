@@ -108,7 +108,10 @@ struct GsView {
   const int* team_step = nullptr;  // nteams + 1 step ranges
   const int* step = nullptr;       // 4 per step: entry offset (unsigned), position offset, rows, width
   const int* code = nullptr;       // per entry: source code (layout.hpp)
-  const double* val = nullptr;
+  const double* val = nullptr;     // null when vidx8 is set
+  const unsigned char* vidx8 = nullptr;  // 8-bit indices into vtab (k_hybrid_gs_pipe only)
+  const double* vtab = nullptr;
+  int nvtab = 0;
   const int* tcol = nullptr;       // weighted forms: in-block entries' T position (-1 otherwise)
   const int* rowmap = nullptr;     // position -> row
   const int* pos = nullptr;        // row -> position
@@ -119,6 +122,8 @@ struct GsView {
 };
 // entries of one product chunk of the hybrid-GS kernels (LDS per wave)
 int gs_chunk_entries();
+// whether launch_hybrid_gs takes the pipelined sweep for a schedule
+bool gs_uses_pipe(bool one_chunk);
 // The sweep's vectors in its order (layout.hpp GsSchedule): G[k] = tmp[rowmap[k]]
 // (T; u when tmp is null), G[n + k] = u[rowmap[k]] (C), F[k] = f[rowmap[k]],
 // and the off-rank halo of u, u[n .. n + nhalo), into G[3n ..).

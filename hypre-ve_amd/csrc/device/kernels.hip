@@ -143,6 +143,9 @@ __device__ __forceinline__ double gs_ld64(__amdgpu_buffer_rsrc_t r, int off) {
 __device__ __forceinline__ int gs_ld32(__amdgpu_buffer_rsrc_t r, int off) {
   return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0);
 }
+__device__ __forceinline__ int gs_ld8(__amdgpu_buffer_rsrc_t r, int off) {
+  return (int)__builtin_amdgcn_raw_buffer_load_b8(r, off, 0, 0);
+}
 
 // Value streams of the row loops: 8-byte values (ValF64) or 16-bit indices
 // into the operator's table of distinct values staged in LDS (ValT16; the
@@ -1540,6 +1543,9 @@ struct GsArgs {
   const int* __restrict__ step;
   const int* __restrict__ code;
   const double* __restrict__ val;
+  const unsigned char* __restrict__ vidx;  // k_hybrid_gs_pipe VT: 8-bit indices into vtab instead of val
+  const double* __restrict__ vtab;
+  int nvtab;
   const int* __restrict__ tcol;
   const int* __restrict__ rowmap;
   const double* __restrict__ l1;
@@ -1555,6 +1561,16 @@ static constexpr int kGsWaves = 4;           // teams per workgroup
 static constexpr int kGsProd = 512;          // LDS products per wave and chunk
 static constexpr int kGsPer = kGsProd / 64;  // entries per lane and chunk
 int gs_chunk_entries() { return kGsProd; }
+// The pipelined sweep (k_hybrid_gs_pipe): HVE_GS_PIPE 1 (default) = every
+// schedule, 2 = only where every step fits one chunk, 0 = k_hybrid_gs
+// (except schedules stored with 8-bit value indices, which only it reads).
+bool gs_uses_pipe(bool one_chunk) {
+  static const int pipe_env = [] {
+    const char* e = getenv("HVE_GS_PIPE");
+    return e ? atoi(e) : 1;
+  }();
+  return pipe_env == 1 || (pipe_env == 2 && one_chunk);
+}
 // U stores leave the ring in batches of kGsBatch steps (host/layout.hpp): on
 // CDNA a load waits for every older vector-memory operation, stores included,
 // so a store per step would put a store's completion on every step's critical
@@ -1579,7 +1595,9 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
   __shared__ unsigned char cls_all[kGsWaves][WGT ? kGsProd : 1];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & (kWave - 1);
-  const int team = blockIdx.x * kGsWaves + wave;
+  // consecutive teams (adjacent rows of the grid, which read each other's T
+  // values) on one XCD: the grid is padded to a multiple of 8
+  const int team = xcd_logical_block(blockIdx.x, gridDim.x) * kGsWaves + wave;
   if (team >= p.nteams) return;
   double* ring = ring_all[wave];
   double* prod = prod_all[wave];
@@ -1698,36 +1716,52 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
   }
 }
 
-// The same sweep, software-pipelined across steps (every step of the
-// operator fits one chunk: rows x width <= kGsProd).  Only the LDS ring
-// carries a dependence from one step to the next, so a step's loads need not
-// wait for the previous step: while step j is summed, step j + 1's source
-// values (C, T, U and halo gathers through its codes) and step j + 2's codes,
-// values and row data are in flight.  Each step then costs its LDS work, not
-// two dependent global-memory round trips.  The U gathers of step j + 1 are
-// issued during step j, after the fence of step j - 1; the schedule's U codes
-// reach back at least kGsFence + 1 = 16 steps and a value computed at step q
-// is fenced at the end of step q - q % kGsBatch + 2 kGsBatch - 1 (kGsBatch 4),
-// so every U value a gather reads was published before it was issued
-// (gs_schedule_self_check emulates this: U read for step j visible only from
-// fences of steps <= j - 2).  Every row is summed as in k_hybrid_gs.
+// The same sweep, software-pipelined across chunks of steps.  A unit is one
+// chunk of one step (entries [kc, kc + kw) of its rows, at most kGsProd
+// entries; a step of rows x width <= kGsProd is one unit).  Only the LDS ring
+// carries a dependence from one step to the next, so a unit's loads need not
+// wait for the units before it: while unit u is summed, unit u + 1's source
+// values (C, T, U and halo gathers through its codes) and unit u + 2's codes,
+// values and row data are in flight, and each unit costs its LDS work instead
+// of two dependent global-memory round trips (512^3, level 0: 5.3 -> 3.7 ms a
+// sweep).  The U gathers of a step's first unit are issued while the previous
+// step's last unit is summed, after the fence of the step before it; the
+// schedule's U codes reach back at least kGsFence + 1 = 16 steps and a value
+// computed at step q is fenced at the end of step q - q % kGsBatch +
+// 2 kGsBatch - 1 (kGsBatch 4), so every U value a gather reads was published
+// before it was issued (gs_schedule_self_check emulates this: U read for step j
+// visible only from fences of steps <= j - 2).  Every row is summed as in
+// k_hybrid_gs: chunk by chunk, entries in CSR order.
 // ---------------------------------------------------------------------------
+// VT: the values as 8-bit indices into the operator's table of distinct
+// values (level 0 of a constant-coefficient stencil: 2), staged in LDS; a
+// stage keeps the raw index and the table is read when the unit is summed.
+template <bool VT>
 struct GsStage {
+  using A = typename std::conditional<VT, int, double>::type;
   int c[kGsPer], tc[kGsPer];
-  double a[kGsPer];
+  A a[kGsPer];  // VT: the index
   double uo, fv, sc;
-  int cfv, R, W, roff;
+  int sci;      // VT and !L1: the diagonal's index (sc unused)
+  int cfv, R, kc, kw, roff, j, first, last;
 };
 
-template <bool L1, bool CFSEL, bool WGT>
+template <bool L1, bool CFSEL, bool WGT, bool VT>
 __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
   __shared__ double ring_all[kGsWaves][kGsRingSlots];
   __shared__ double prod_all[kGsWaves][kGsProd];
   __shared__ double prod2_all[kGsWaves][WGT ? kGsProd : 1];
   __shared__ unsigned char cls_all[kGsWaves][WGT ? kGsProd : 1];
+  __shared__ double vt_lds[VT ? 256 : 1];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & (kWave - 1);
-  const int team = blockIdx.x * kGsWaves + wave;
+  if (VT) {
+    for (int i = threadIdx.x; i < p.nvtab; i += kGsWaves * kWave) vt_lds[i] = p.vtab[i];
+    __syncthreads();
+  }
+  // consecutive teams (adjacent rows of the grid, which read each other's T
+  // values) on one XCD: the grid is padded to a multiple of 8
+  const int team = xcd_logical_block(blockIdx.x, gridDim.x) * kGsWaves + wave;
   if (team >= p.nteams) return;
   double* ring = ring_all[wave];
   double* prod = prod_all[wave];
@@ -1744,70 +1778,117 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
   const auto rF = gs_rsrc(p.F, (unsigned)p.n * 8u);
   const auto rL = gs_rsrc(L1 ? p.l1 : p.F, (unsigned)p.n * 8u);
   const auto rCF = gs_rsrc(CFSEL ? (const void*)p.cf : (const void*)p.F, (unsigned)p.n * 4u);
-  // step j's codes, values and row data (never written during the sweep);
-  // every lane loads kGsPer entries (those past the step's read entry 0)
-  auto load_a = [&](int j, GsStage& S) {
+  // unit (j, c): chunk c of step j; the next one, j = ns at the end
+  auto next_unit = [&](int& j, int& c) {
+    const int R = steps[4 * j + 2], W = steps[4 * j + 3];
+    const int KC = kGsProd / R;
+    if ((c + 1) * KC < W) {
+      ++c;
+    } else {
+      ++j;
+      c = 0;
+    }
+  };
+  // the unit's codes, values (never written during the sweep) and, for a
+  // step's first unit, its row data; every lane loads kGsPer entries (those
+  // past the unit read its entry 0)
+  auto load_a = [&](int j, int c, GsStage<VT>& S) {
     const unsigned ent = (unsigned)steps[4 * j];
     S.roff = steps[4 * j + 1];
     S.R = steps[4 * j + 2];
-    S.W = steps[4 * j + 3];
+    const int W = steps[4 * j + 3];
+    const int KC = kGsProd / S.R;
+    S.j = j;
+    S.kc = c * KC;
+    S.kw = min(KC, W - S.kc);
+    S.first = c == 0;
+    S.last = S.kc + KC >= W;
     const int r = lane < S.R ? lane : S.R - 1;
     const int kp = S.roff + r;
     const auto rc = gs_rsrc(p.code + ent, 0x7fffffffu);
-    const auto rv8 = gs_rsrc(p.val + ent, 0x7fffffffu);
+    const auto rv8 = VT ? gs_rsrc(p.vidx + ent, 0x7fffffffu) : gs_rsrc(p.val + ent, 0x7fffffffu);
     const auto rt = gs_rsrc(WGT ? (const void*)(p.tcol + ent) : (const void*)(p.code + ent), 0x7fffffffu);
-    S.uo = gs_ld64(rC, (int)((unsigned)kp * 8u));
-    S.fv = gs_ld64(rF, (int)((unsigned)kp * 8u));
-    S.sc = L1 ? gs_ld64(rL, (int)((unsigned)kp * 8u)) : gs_ld64(rv8, r * 8);
-    S.cfv = CFSEL ? gs_ld32(rCF, kp * 4) : 0;
-    const int E = S.W * S.R;
+    if (c == 0) {
+      S.uo = gs_ld64(rC, (int)((unsigned)kp * 8u));
+      S.fv = gs_ld64(rF, (int)((unsigned)kp * 8u));
+      if (L1) S.sc = gs_ld64(rL, (int)((unsigned)kp * 8u));
+      else if (VT) S.sci = gs_ld8(rv8, r);
+      else S.sc = gs_ld64(rv8, r * 8);
+      S.cfv = CFSEL ? gs_ld32(rCF, kp * 4) : 0;
+    }
+    const int E = S.kw * S.R, base = S.kc * S.R;
 #pragma unroll
     for (int t = 0; t < kGsPer; ++t) {
       const int e = lane + 64 * t;
-      const int o = e < E ? e : 0;
+      const int o = base + (e < E ? e : 0);
       S.c[t] = gs_ld32(rc, o * 4);
-      S.a[t] = gs_ld64(rv8, o * 8);
+      if (VT) S.a[t] = gs_ld8(rv8, o);
+      else S.a[t] = gs_ld64(rv8, o * 8);
       S.tc[t] = WGT ? gs_ld32(rt, o * 4) : -1;
     }
   };
-  // step j's source values from G (ring and padding codes read G[0], unused)
-  auto load_b = [&](const GsStage& S, double (&x)[kGsPer], double (&t2)[kGsPer]) {
+  // the unit's source values from G (ring and padding codes read G[0], unused)
+  auto load_b = [&](const GsStage<VT>& S, double (&x)[kGsPer], double (&t2)[kGsPer]) {
 #pragma unroll
     for (int t = 0; t < kGsPer; ++t) {
       x[t] = gs_ld64(rG, (int)((unsigned)(S.c[t] > 0 ? S.c[t] : 0) * 8u));
       t2[t] = WGT ? gs_ld64(rG, (int)((unsigned)(S.tc[t] > 0 ? S.tc[t] : 0) * 8u)) : 0.0;
     }
   };
-  GsStage S0, S1, S2;
+  GsStage<VT> S0, S1, S2;
   double x0[kGsPer], x1[kGsPer], u0[kGsPer], u1[kGsPer];
-  if (ns > 0) load_a(0, S0);
-  if (ns > 1) load_a(1, S1);
+  int j1 = 0, c1 = 0, j2 = 0, c2 = 0;
+  if (ns > 0) {
+    load_a(0, 0, S0);
+    next_unit(j1, c1);
+  }
+  if (j1 < ns) {
+    load_a(j1, c1, S1);
+    j2 = j1;
+    c2 = c1;
+    next_unit(j2, c2);
+  }
   if (ns > 0) load_b(S0, x0, u0);
-  for (int j = 0; j < ns; ++j) {
-    if (j + 2 < ns) load_a(j + 2, S2);
-    if (j + 1 < ns) load_b(S1, x1, u1);
-    const int R = S0.R, W = S0.W, E = W * R;
+  double res = 0.0, res0 = 0.0, res2 = 0.0, uo = 0.0, sc = 0.0;
+  int cfv = 0;
+  bool more = ns > 0;
+  while (more) {
+    const bool have1 = j1 < ns, have2 = j2 < ns;
+    if (have2) load_a(j2, c2, S2);
+    if (have1) load_b(S1, x1, u1);
+    const int R = S0.R, E = S0.kw * R;
     const int r = lane < R ? lane : R - 1;
-    double res = S0.fv, res0 = 0.0, res2 = 0.0;
-    double rv[kGsPer];
+    if (S0.first) {
+      res = S0.fv;
+      res0 = 0.0;
+      res2 = 0.0;
+      uo = S0.uo;
+      sc = (VT && !L1) ? vt_lds[S0.sci] : S0.sc;
+      cfv = S0.cfv;
+    }
+    double rv[kGsPer], av[kGsPer];
 #pragma unroll
-    for (int t = 0; t < kGsPer; ++t) rv[t] = ring[S0.c[t] < -1 ? -2 - S0.c[t] : 0];
+    for (int t = 0; t < kGsPer; ++t) {
+      rv[t] = ring[S0.c[t] < -1 ? -2 - S0.c[t] : 0];
+      av[t] = VT ? vt_lds[(int)S0.a[t]] : (double)S0.a[t];
+    }
 #pragma unroll
     for (int t = 0; t < kGsPer; ++t) {
       const int e = lane + 64 * t;
       const int cc = S0.c[t];
       const double xv = cc < -1 ? rv[t] : x0[t];
-      const double pv = cc == -1 ? 0.0 : S0.a[t] * xv;
+      const double pv = cc == -1 ? 0.0 : av[t] * xv;
       if (e < E) {
         prod[e] = pv;
         if (WGT) {
-          prod2[e] = S0.tc[t] >= 0 ? S0.a[t] * u0[t] : 0.0;
+          prod2[e] = S0.tc[t] >= 0 ? av[t] * u0[t] : 0.0;
           cls[e] = S0.tc[t] >= 0;
         }
       }
     }
     gs_wave_sync();
-    for (int kk = k0; kk < W; ++kk) {
+    for (int kk = 0; kk < S0.kw; ++kk) {
+      if (S0.kc + kk < k0) continue;
       const int e = kk * R + r;
       const double pv = prod[e];
       if (WGT && cls[e]) {
@@ -1817,40 +1898,65 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
         res -= pv;
       }
     }
-    const bool run = lane < R && S0.sc != 0.0 && !(CFSEL && S0.cfv != p.relax_points);
-    double un = S0.uo;
-    if (WGT) {
-      double ui = un;
-      ui *= 1.0 - p.w * p.omega;
-      ui += p.w * (p.omega * res + res0 + (1.0 - p.omega) * res2) / S0.sc;
-      un = run ? ui : un;
-    } else {
-      const double v = L1 ? un + res / S0.sc : res / S0.sc;
-      un = run ? v : un;
-    }
-    ring[(j % kGsRing) * kWave + lane] = un;
-    gs_wave_sync();  // the next steps' lanes read the ring slot; the next products overwrite prod
-    if (j % kGsBatch == kGsBatch - 1 || j == ns - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      for (int q = j - j % kGsBatch; q <= j; ++q) {
-        const int rq = steps[4 * q + 2];
-        if (lane < rq) Ub[steps[4 * q + 1] + lane] = ring[(q % kGsRing) * kWave + lane];
+    if (S0.last) {
+      const int j = S0.j;
+      const bool run = lane < R && sc != 0.0 && !(CFSEL && cfv != p.relax_points);
+      double un = uo;
+      if (WGT) {
+        double ui = un;
+        ui *= 1.0 - p.w * p.omega;
+        ui += p.w * (p.omega * res + res0 + (1.0 - p.omega) * res2) / sc;
+        un = run ? ui : un;
+      } else {
+        const double v = L1 ? un + res / sc : res / sc;
+        un = run ? v : un;
       }
+      ring[(j % kGsRing) * kWave + lane] = un;
+      gs_wave_sync();  // the next steps' lanes read the ring slot; the next products overwrite prod
+      if (j % kGsBatch == kGsBatch - 1 || j == ns - 1) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        for (int q = j - j % kGsBatch; q <= j; ++q) {
+          const int rq = steps[4 * q + 2];
+          if (lane < rq) Ub[steps[4 * q + 1] + lane] = ring[(q % kGsRing) * kWave + lane];
+        }
+      }
+    } else {
+      gs_wave_sync();  // the next chunk overwrites the products
     }
+    more = have1;
     S0 = S1;
     S1 = S2;
 #pragma unroll
     for (int t = 0; t < kGsPer; ++t) { x0[t] = x1[t]; u0[t] = u1[t]; }
+    j1 = j2;
+    c1 = c2;
+    if (have2) next_unit(j2, c2);
   }
+}
+
+// Permutes of the sweep (gather before, scatter after): one contiguous range
+// of positions per workgroup, the ranges of an XCD's workgroups (b % 8)
+// adjacent.  A step's 64 rows lie on 64 lines of u that the next 15 steps
+// read again (the 7-point level 0: a diagonal moving one point a step), so
+// those 16 steps must meet in one L2: with a grid-stride loop they were spread
+// over 4 XCDs, which fetched every line 4 times (512^3: gather 3.95 ms).
+// gridDim.x is a multiple of 8.
+__device__ __forceinline__ void gs_perm_range(int n, int& q0, int& q1) {
+  const int per = (int)(((int64_t)n + gridDim.x - 1) / gridDim.x + 255) & ~255;
+  const int lb = xcd_logical_block(blockIdx.x, gridDim.x);
+  q0 = (int)min<int64_t>((int64_t)lb * per, n);
+  q1 = (int)min<int64_t>((int64_t)q0 + per, n);
 }
 
 // u[rowmap[k]] = U[k]: the sweep's result back in natural row order (NAT:
 // u[i] = U[pos[i]], rows in order).
 template <bool NAT>
-__global__ void k_gs_scatter(int n, const int* __restrict__ map, const double* __restrict__ U,
-                             double* __restrict__ u) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+__global__ void __launch_bounds__(256) k_gs_scatter(int n, const int* __restrict__ map, const double* __restrict__ U,
+                                                    double* __restrict__ u) {
+  int q0, q1;
+  gs_perm_range(n, q0, q1);
+  for (int q = q0 + threadIdx.x; q < q1; q += 256) {
     if (NAT) u[q] = U[map[q]];
     else u[map[q]] = U[q];
   }
@@ -1859,10 +1965,13 @@ __global__ void k_gs_scatter(int n, const int* __restrict__ map, const double* _
 // NAT = false: positions in order, rows gathered (rowmap); NAT = true: rows in
 // natural order (coalesced reads), positions scattered (pos = rowmap^-1).
 template <bool NAT>
-__global__ void k_gs_gather(int n, int nhalo, const int* __restrict__ map, const double* __restrict__ u,
-                            const double* __restrict__ tmp, const double* __restrict__ f, double* __restrict__ G,
-                            double* __restrict__ F) {
-  for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+__global__ void __launch_bounds__(256) k_gs_gather(int n, int nhalo, const int* __restrict__ map,
+                                                   const double* __restrict__ u, const double* __restrict__ tmp,
+                                                   const double* __restrict__ f, double* __restrict__ G,
+                                                   double* __restrict__ F) {
+  int q0, q1;
+  gs_perm_range(n, q0, q1);
+  for (int q = q0 + threadIdx.x; q < q1; q += 256) {
     const int i = NAT ? q : map[q], k = NAT ? map[q] : q;
     const double v = u[i];
     G[k] = tmp ? tmp[i] : v;
@@ -1883,7 +1992,7 @@ static int gs_natural_order() {
 hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp, const double* f, int nhalo,
                             double* G, double* F, hipStream_t st) {
   if (S.nrows <= 0) return hipSuccess;
-  const int grid = std::min((S.nrows + 255) / 256, 256 * 16);
+  const int grid = std::min((S.nrows + 255) / 256 + 7, 256 * 16) & ~7;
   if (gs_natural_order() & 1)
     hipLaunchKernelGGL(k_gs_gather<true>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.pos, u, tmp, f, G, F);
   else
@@ -1896,6 +2005,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   if (S.nteams <= 0) return hipSuccess;
   GsArgs a;
   a.team_step = S.team_step; a.step = S.step; a.code = S.code; a.val = S.val; a.tcol = S.tcol; a.rowmap = S.rowmap;
+  a.vidx = S.vidx8; a.vtab = S.vtab; a.nvtab = S.nvtab;
   a.l1 = S.l1; a.cf = S.cf; a.G = G; a.F = F; a.u = u;
   a.n = S.nrows; a.nteams = S.nteams; a.relax_points = relax_points; a.w = w; a.omega = omega;
   const uint64_t gbytes = (3 * (uint64_t)S.nrows + (uint64_t)nhalo) * sizeof(double);
@@ -1905,15 +2015,12 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   if (wgt && !S.tcol) return hipErrorInvalidValue;   // the weighted forms read Vtemp in-block
   if (use_l1 && !S.l1) return hipErrorInvalidValue;
   if (cfsel && !S.cf) return hipErrorInvalidValue;
-  const dim3 grid((S.nteams + kGsWaves - 1) / kGsWaves), blk(kGsWaves * kWave);
-  // the pipelined sweep where every step fits one chunk; HVE_GS_PIPE=0 keeps k_hybrid_gs
-  static const bool pipe_env = [] {
-    const char* e = getenv("HVE_GS_PIPE");
-    return e ? atoi(e) != 0 : true;
-  }();
-  const bool pipe = pipe_env && S.one_chunk;
-#define HVE_G(L1V, CFV, WV)                                                          \
-  if (pipe) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV>), grid, blk, 0, st, a); \
+  const dim3 grid(((S.nteams + kGsWaves - 1) / kGsWaves + 7) & ~7), blk(kGsWaves * kWave);
+  const bool pipe = gs_uses_pipe(S.one_chunk) || S.vidx8;
+  if (!S.vidx8 && !S.val) return hipErrorInvalidValue;
+#define HVE_G(L1V, CFV, WV)                                                                           \
+  if (S.vidx8) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, true>), grid, blk, 0, st, a);        \
+  else if (pipe) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false>), grid, blk, 0, st, a);    \
   else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV>), grid, blk, 0, st, a);
 #define HVE_GW(L1V, CFV) \
   if (wgt) { HVE_G(L1V, CFV, true) } else { HVE_G(L1V, CFV, false) }
@@ -1924,7 +2031,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   }
 #undef HVE_GW
 #undef HVE_G
-  const int sgrid = std::min((S.nrows + 255) / 256, 256 * 16);
+  const int sgrid = std::min((S.nrows + 255) / 256 + 7, 256 * 16) & ~7;
   if (gs_natural_order() & 2)
     hipLaunchKernelGGL(k_gs_scatter<true>, dim3(sgrid), dim3(256), 0, st, S.nrows, S.pos, G + 2 * (size_t)S.nrows, u);
   else

@@ -114,8 +114,7 @@ bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::ve
   const int nz = (int)(nlocal / P);
   if (nz < 3 || shift / P + nzs > nz) return false;
   if (!grid_stencil_addressable(nx, ny, nz)) return false;  // the per-slice loop takes it
-  for (int64_t k = 0; k < A.nnz(); ++k)
-    if (A.j[k] >= nlocal) return false;  // a halo column
+  if (csr_max_col(A) >= nlocal) return false;  // a halo column
   const int W = stencil_w;
   std::vector<GSlot> gs((size_t)npat * W + 16);
   for (auto& g : gs) g = GSlot{0, 0.0, 0, 0, 0, 0};
@@ -166,36 +165,6 @@ bool DevSell::build_grid(const CSR& A, const std::vector<int>& so, const std::ve
   return true;
 }
 
-// Packed SELL-64 entries (k_sell_code PK): code = ((col - base[slice]) << vbits)
-// | value index, base = the slice's smallest column, padding 0xFFFFFFFF.  false
-// when some slice's column span does not fit 32 - vbits bits (all-ones span
-// reserved, so no entry equals the padding code).
-static bool pack_sell_codes(const std::vector<int>& sp, const std::vector<int>& col,
-                            const std::vector<unsigned short>& vi, int nv, std::vector<unsigned>& code,
-                            std::vector<int>& base, int& vbits) {
-  int vb = 1;
-  while ((1 << vb) < nv) ++vb;
-  const int ns = (int)sp.size() - 1;
-  const int64_t lim = (int64_t(1) << (32 - vb)) - 1;
-  base.assign(ns + 1, 0);  // one past the last: the kernel's scalar load may run ahead
-  code.assign(col.size(), 0xFFFFFFFFu);
-  int ok = 1;
-#pragma omp parallel for schedule(static) reduction(min : ok)
-  for (int s = 0; s < ns; ++s) {
-    int lo = INT32_MAX, hi = -1;
-    for (int q = sp[s]; q < sp[s + 1]; ++q)
-      if (col[q] >= 0) { lo = std::min(lo, col[q]); hi = std::max(hi, col[q]); }
-    if (hi < 0) continue;
-    if ((int64_t)hi - lo >= lim) { ok = 0; continue; }
-    base[s] = lo;
-    for (int q = sp[s]; q < sp[s + 1]; ++q)
-      if (col[q] >= 0) code[q] = ((unsigned)(col[q] - lo) << vb) | vi[q];
-  }
-  if (!ok) return false;
-  vbits = vb;
-  return true;
-}
-
 // HVE_SETUP_T: host stages of an operator's layout construction and upload
 namespace {
 struct SetupLap {
@@ -234,7 +203,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
   if (coded && A.nnz() > 0 && ((policy == 0 && coded_auto && A.nrows >= (1 << 18)) || policy == 12)) {
     static const std::vector<int> none;
     std::vector<int> sp, ot;
-    std::vector<unsigned short> cd;
+    hvec<unsigned short> cd;
     std::vector<double> tab;
     int vb = 0;
     if (build_sell_coded_host(A, rowmap_h, coded->anc ? *coded->anc : none, coded->colpos ? *coded->colpos : none,
@@ -274,8 +243,9 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       return;
     }
   }
-  std::vector<int> sp, col, perm;
-  std::vector<double> val;
+  std::vector<int> sp, perm;
+  hvec<int> col;
+  hvec<double> val;
   // Sort rows inside windows (SELL-C-sigma) only where the plain layout pads
   // noticeably: the Galerkin levels' rows range over 7..150 entries, the
   // finest 7-point operator is nearly uniform and keeps contiguous rows.
@@ -325,16 +295,18 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
     const char* e = getenv("HVE_SELL_DICT");
     return e ? atoi(e) : -1;
   }();
+  // configs[4] (anisotropic, aggressive coarsening, 256^3): A_1 has 15.9
+  // entries a row, 0.093 ms as a dictionary against 0.105 jagged.
   bool use_dict = A.nnz() > 0 &&
-                  (dict_env < 0 ? (A.nrows >= (1 << 18) && avg_len >= 16.0)
+                  (dict_env < 0 ? (A.nrows >= (1 << 18) && avg_len >= 12.0)
                                 : ((dict_env >= 1 && jag) || (dict_env >= 2 && wide)));
   // With 16-bit value indices a padding slot costs 6 B instead of 12, and the
   // padded layout's natural row order gathers x better than the sorted jagged
   // one: R_0 at 256^3 187 us padded+vt16 against 197 jagged+vt16 (202 jagged).
   if (policy == 0 && jag && !pw && sell_valtab_env() != 0) {
-    std::vector<unsigned short> probe;
+    hvec<unsigned short> probe;
     std::vector<double> probe_tab;
-    if (build_value_table16(A.a, 4096, probe, probe_tab)) jag = false;
+    if (build_value_table16(A.a.data(), A.a.size(), 4096, probe, probe_tab)) jag = false;
     lap("value-table probe");
   }
   if (policy != 0) {  // forced (tests): every loop gives the same bits
@@ -416,12 +388,12 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
     sp.clear();
   }
   if (use_delta) {
-    std::vector<short> dc;
+    hvec<short> dc;
     std::vector<int> sb;
-    std::vector<unsigned char> vi_probe;
+    hvec<unsigned char> vi_probe;
     std::vector<double> tab_probe;
     bool delta_ok = build_sell_delta_host(A, sp, sb, dc, val);
-    if (delta_ok && delta_before_dict && !build_value_table(val, 256, vi_probe, tab_probe)) delta_ok = false;
+    if (delta_ok && delta_before_dict && !build_value_table(val.data(), val.size(), 256, vi_probe, tab_probe)) delta_ok = false;
     if (!delta_ok && delta_before_dict) {
       sp.clear();
       val.clear();
@@ -446,13 +418,13 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       const int vt_env = sell_valtab_env();
       // Up to 4096 distinct values (P of the 7-point hierarchy: ~1200): 16-bit
       // indices, the table (<= 32 KiB) in LDS.
-      std::vector<unsigned char> vi;
-      std::vector<unsigned short> vi16;
+      hvec<unsigned char> vi;
+      hvec<unsigned short> vi16;
       std::vector<double> tab;
       const bool try_vt = (vt_env != 0 || policy == 7) && policy != 6;
-      if (try_vt && build_value_table(val, 256, vi, tab)) {
+      if (try_vt && build_value_table(val.data(), val.size(), 256, vi, tab)) {
         vidx = dupload(vi.data(), vi.size());
-      } else if (try_vt && build_value_table16(val, 4096, vi16, tab)) {
+      } else if (try_vt && build_value_table16(val.data(), val.size(), 4096, vi16, tab)) {
         vidx16 = dupload(vi16.data(), vi16.size());
       } else if (short_rows && policy == 0) {
         release();  // no gain without a value table: plain layout
@@ -484,17 +456,17 @@ dict:
     // consecutive slices share more of their columns
     std::vector<int> pre;
     if (tile && !tile->empty()) {
-      pre.resize(A.nrows);
-      for (int r = 0; r < A.nrows; ++r) pre[r] = r;
-      auto tk = [&](int r) {
+      std::vector<int64_t> tk(A.nrows);
+#pragma omp parallel for schedule(static)
+      for (int r = 0; r < A.nrows; ++r) {
         const int g = rowmap_h.empty() ? r : rowmap_h[r];
-        return g < (int)tile->size() ? (*tile)[g] : (int64_t)g;
-      };
-      std::stable_sort(pre.begin(), pre.end(), [&](int a, int b) { return tk(a) < tk(b); });
+        tk[r] = g < (int)tile->size() ? (*tile)[g] : (int64_t)g;
+      }
+      sort_rows_by_key(tk, pre);
       lap("dict tile order");
     }
     const std::vector<int>* prep = pre.empty() ? nullptr : &pre;
-    std::vector<unsigned short> c16;
+    hvec<unsigned short> c16;
     std::vector<int> dp, dc, rl2;
     int mxd = 0;
     // Square operators: one dictionary per workgroup of 4 slices
@@ -569,10 +541,10 @@ dict:
         const char* e = getenv("HVE_DICT_VT");
         return e ? atoi(e) : 0;
       }();
-      std::vector<unsigned short> vi16;
+      hvec<unsigned short> vi16;
       std::vector<double> tab;
       if (group == 1 && !ranges && !relax_ops && (dict_vt_env != 0 || policy == 5) && sell_valtab_env() != 0 &&
-          (size_t)(dmax + 4096) * sizeof(double) <= 64 * 1024 && build_value_table16(val, 4096, vi16, tab)) {
+          (size_t)(dmax + 4096) * sizeof(double) <= 64 * 1024 && build_value_table16(val.data(), val.size(), 4096, vi16, tab)) {
         vidx16 = dupload(vi16.data(), vi16.size());
         vtab = dupload(tab.data(), tab.size());
         nvtab = (int)tab.size();
@@ -622,10 +594,10 @@ dict:
   // 16-bit indices into the operator's distinct values where at most 4096
   // occur (P and R of the 7-point hierarchy at every size: ~1200), off for the
   // workgroup-per-slice loop of small operators.  HVE_SELL_VALTAB=0 turns it off.
-  std::vector<unsigned short> vi16;
+  hvec<unsigned short> vi16;
   std::vector<double> tab;
   const bool try_vt16 = policy == 8 || policy == 9 || policy == 13 || (policy == 0 && !wide && sell_valtab_env() != 0);
-  const bool vt_ok = try_vt16 && A.nnz() > 0 && build_value_table16(val, 4096, vi16, tab);
+  const bool vt_ok = try_vt16 && A.nnz() > 0 && build_value_table16(val.data(), val.size(), 4096, vi16, tab);
   lap("value table");
   if (vt_ok) {
     vtab = dupload(tab.data(), tab.size());
@@ -643,7 +615,7 @@ dict:
       const char* e = getenv("HVE_SELL_PACK");
       return e ? atoi(e) : 1;
     }();
-    std::vector<unsigned> c32;
+    hvec<unsigned> c32;
     std::vector<int> sbase;
     if (!jag && coded && (policy == 13 || (policy == 0 && pack_env != 0)) && pack_sell_codes(sp, col, vi16, nvtab, c32, sbase, vbits)) {
       code32 = dupload(c32.data(), c32.size());
@@ -704,20 +676,7 @@ static bool l1_on_the_fly(const RankOp& op, const std::vector<double>& l1) {
     return e && atoi(e) == 0;
   }();
   if (off) return false;
-  int ok = 1;
-  for (int part = 0; part < 2; ++part) {
-    const CSR& A = part == 0 ? op.interior : op.boundary;
-    const std::vector<int>& map = part == 0 ? op.map_int : op.map_bnd;
-#pragma omp parallel for schedule(static) reduction(min : ok)
-    for (int i = 0; i < A.nrows; ++i) {
-      double s = 0.0;
-      for (int q = A.i[i]; q < A.i[i + 1]; ++q) s += std::fabs(A.a[q]);
-      if (A.i[i + 1] > A.i[i] && A.a[A.i[i]] < 0.0) s = -s;
-      const int g = map.empty() ? i : map[i];
-      if (g < 0 || g >= (int)l1.size() || std::memcmp(&s, &l1[g], sizeof(double)) != 0) ok = 0;
-    }
-  }
-  return ok != 0;
+  return l1_rows_match(op.interior, op.map_int, l1) && l1_rows_match(op.boundary, op.map_bnd, l1);
 }
 
 void DevSell::release() {
@@ -805,7 +764,25 @@ void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forw
   team_step = dupload(S.team_step.data(), S.team_step.size());
   step = dupload(S.step.data(), std::max<size_t>(4, S.step.size()));
   code = dupload(S.code.data(), std::max<size_t>(1, S.code.size()));
-  val = dupload(S.val.data(), std::max<size_t>(1, S.val.size()));
+  // At most 256 distinct values (level 0 of a constant-coefficient stencil):
+  // 8-bit indices into a table, 1 B an entry instead of 8, read only by the
+  // pipelined sweep.  HVE_GS_VT=0 keeps the values.
+  static const int vt_env = [] {
+    const char* e = getenv("HVE_GS_VT");
+    return e ? atoi(e) : 1;
+  }();
+  {
+    hvec<unsigned char> vi;
+    std::vector<double> tab;
+    if (vt_env != 0 && gs_uses_pipe(one_chunk) && !S.val.empty() &&
+        build_value_table(S.val.data(), S.val.size(), 256, vi, tab)) {
+      vidx8 = dupload(vi.data(), vi.size());
+      vtab = dupload(tab.data(), tab.size());
+      nvtab = (int)tab.size();
+    } else {
+      val = dupload(S.val.data(), std::max<size_t>(1, S.val.size()));
+    }
+  }
   if (weighted) tcol = dupload(S.tcol.data(), std::max<size_t>(1, S.tcol.size()));
   rowmap = dupload(S.rowmap.data(), std::max<size_t>(1, S.rowmap.size()));
   {
@@ -818,10 +795,12 @@ void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forw
 }
 void DevGs::release() {
   for (void* p : {(void*)team_step, (void*)step, (void*)code, (void*)val, (void*)tcol, (void*)rowmap, (void*)pos,
-                  (void*)l1, (void*)cf})
+                  (void*)l1, (void*)cf, (void*)vidx8, (void*)vtab})
     if (p) (void)hipFree(p);
   team_step = step = code = tcol = rowmap = pos = cf = nullptr;
-  val = l1 = nullptr;
+  val = l1 = vtab = nullptr;
+  vidx8 = nullptr;
+  nvtab = 0;
   nrows = nteams = nblocks = max_steps = max_width = 0;
   one_chunk = false;
   entries = nnz = 0;

@@ -161,7 +161,10 @@ struct DevGs {
   int* team_step = nullptr;
   int* step = nullptr;
   int* code = nullptr;
-  double* val = nullptr;
+  double* val = nullptr;          // null when vidx8 holds the values
+  unsigned char* vidx8 = nullptr;  // 8-bit indices into vtab (<= 256 distinct values)
+  double* vtab = nullptr;
+  int nvtab = 0;
   int* tcol = nullptr;  // only when a weighted form may run
   int* rowmap = nullptr;
   int* pos = nullptr;    // rowmap^-1
@@ -176,6 +179,7 @@ struct DevGs {
     v.team_step = team_step; v.step = step; v.code = code; v.val = val; v.tcol = tcol; v.rowmap = rowmap;
     v.pos = pos; v.l1 = l1; v.cf = cf; v.nteams = nteams; v.nrows = nrows; v.max_width = max_width;
     v.one_chunk = one_chunk;
+    v.vidx8 = vidx8; v.vtab = vtab; v.nvtab = nvtab;
     return v;
   }
   void upload(const CSR& A, const std::vector<int>& block_starts, bool forward, bool weighted,

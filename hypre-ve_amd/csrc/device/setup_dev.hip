@@ -53,11 +53,13 @@ struct DBuf {
     n = m;
     SDV(hipMalloc((void**)&p, std::max<size_t>(1, m) * sizeof(T)));
   }
-  void up(const std::vector<T>& h) {
+  template <typename Al>
+  void up(const std::vector<T, Al>& h) {
     alloc(h.size());
     if (!h.empty()) SDV(hipMemcpy(p, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice));
   }
-  void down(std::vector<T>& h, size_t m) const {
+  template <typename Al>
+  void down(std::vector<T, Al>& h, size_t m) const {
     h.resize(m);
     if (m) SDV(hipMemcpy(h.data(), p, m * sizeof(T), hipMemcpyDeviceToHost));
   }
@@ -281,6 +283,157 @@ __global__ void __launch_bounds__(64) k_extpi(DCsr A, DCsr S, const int* __restr
       for (int k = 0; k < jend; ++k) pa[k] /= -diagonal;
     }
     for (int k = 0; k < jend; ++k) Pa[jb + k] = pa[k];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Wave-parallel count passes.  A row's count is the number of distinct keys
+// its candidates insert, which does not depend on the insertion order, so the
+// 64 lanes insert at once into an LDS set of (generation, key) words claimed
+// by 64-bit compare-and-swap.  A row overflows (-1: the host finishes it)
+// exactly when it has more than cap/2 distinct keys, as in the one-lane
+// passes, so the fill passes see the same rows.
+// ---------------------------------------------------------------------------
+struct LSet {
+  unsigned long long* t;
+  unsigned mask;
+  int shift;
+  unsigned cap;
+  __device__ void init(unsigned long long* base, int c, int lg) {
+    t = base;
+    cap = (unsigned)c;
+    mask = (unsigned)c - 1;
+    shift = 32 - lg;
+  }
+  // 1: inserted (fresh), 0: present, -1: no free slot found (the row overflows)
+  __device__ int insert(int k, unsigned cur) const {
+    unsigned h = ((unsigned)k * 2654435761u) >> shift;
+    const unsigned long long want = ((unsigned long long)cur << 32) | (unsigned)k;
+    for (unsigned probes = 0; probes < cap;) {
+      const unsigned long long w = __hip_atomic_load(&t[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      if ((unsigned)(w >> 32) == cur) {
+        if ((unsigned)w == (unsigned)k) return 0;
+        h = (h + 1) & mask;
+        ++probes;
+        continue;
+      }
+      unsigned long long exp = w;
+      if (__hip_atomic_compare_exchange_strong(&t[h], &exp, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WAVEFRONT))
+        return 1;
+      // another lane claimed the slot: look at it again
+    }
+    return -1;
+  }
+};
+
+__device__ __forceinline__ int wave_sum(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// ext+i count (k_extpi<false>): |C-hat_i|, strong F neighbours taking table
+// slots as in the fill pass.  LDS: cap 64-bit words.
+__global__ void __launch_bounds__(64) k_extpi_count_w(DCsr S, const int* __restrict__ cf, int n, int cap, int lg,
+                                                      int* __restrict__ rowcnt) {
+  extern __shared__ unsigned long long lds64[];
+  for (int t = threadIdx.x; t < cap; t += 64) lds64[t] = 0ull;
+  __syncthreads();
+  const int lane = threadIdx.x;
+  LSet M;
+  M.init(lds64, cap, lg);
+  const int limit = cap / 2;
+  unsigned cur = 0;
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int ci = cf[i];
+    if (ci >= 0 || ci == kSF) {
+      if (lane == 0) rowcnt[i] = ci >= 0 ? 1 : 0;
+      continue;
+    }
+    ++cur;
+    int cntc = 0, keys = 0, bad = 0;
+    for (int jj = S.i[i] + lane; jj < S.i[i + 1] && !bad; jj += 64) {
+      const int i1 = S.j[jj];
+      const int c1 = cf[i1];
+      if (c1 >= 0) {
+        const int r = M.insert(i1, cur);
+        if (r < 0) bad = 1;
+        cntc += r > 0;
+        keys += r > 0;
+      } else if (c1 != kSF) {
+        const int r = M.insert(i1, cur);
+        if (r < 0) bad = 1;
+        keys += r > 0;
+        for (int kk = S.i[i1]; kk < S.i[i1 + 1] && !bad; ++kk) {
+          const int k1 = S.j[kk];
+          if (cf[k1] >= 0) {
+            const int r2 = M.insert(k1, cur);
+            if (r2 < 0) bad = 1;
+            cntc += r2 > 0;
+            keys += r2 > 0;
+          }
+        }
+      }
+    }
+    const int tk = wave_sum(keys), tc = wave_sum(cntc), tb = wave_sum(bad);
+    if (lane == 0) rowcnt[i] = (tb || tk > limit) ? -1 : tc;
+  }
+}
+
+// Galerkin count (k_rap<false>): distinct columns of C row q (q itself
+// first).  LDS: cap1 + cap2 64-bit words and the RA list (cap1 / 2 ints).
+__global__ void __launch_bounds__(64) k_rap_count_w(DCsr R, DCsr A, DCsr P, int cap1, int lg1, int cap2, int lg2,
+                                                    int* __restrict__ rowlen) {
+  extern __shared__ unsigned long long lds64[];
+  for (int t = threadIdx.x; t < cap1 + cap2; t += 64) lds64[t] = 0ull;
+  int* ra = reinterpret_cast<int*>(lds64 + cap1 + cap2);
+  __shared__ int nra_s;
+  __syncthreads();
+  const int lane = threadIdx.x;
+  LSet M1, M2;
+  M1.init(lds64, cap1, lg1);
+  M2.init(lds64 + cap1, cap2, lg2);
+  const int lim1 = cap1 / 2, lim2 = cap2 / 2;
+  unsigned cur = 0;
+  for (int q = blockIdx.x; q < R.n; q += gridDim.x) {
+    ++cur;
+    if (lane == 0) nra_s = 0;
+    __syncthreads();
+    int bad = 0;
+    for (int jj1 = R.i[q] + lane; jj1 < R.i[q + 1] && !bad; jj1 += 64) {
+      const int i1 = R.j[jj1];
+      for (int jj2 = A.i[i1]; jj2 < A.i[i1 + 1]; ++jj2) {
+        const int i2 = A.j[jj2];
+        const int r = M1.insert(i2, cur);
+        if (r < 0) { bad = 1; break; }
+        if (r > 0) {
+          const int at = atomicAdd(&nra_s, 1);
+          if (at < lim1) ra[at] = i2;
+        }
+      }
+    }
+    __syncthreads();
+    const int nra = nra_s;
+    int keys = 0;
+    bad = wave_sum(bad);
+    if (!bad && nra <= lim1) {
+      if (lane == 0) keys += M2.insert(q, cur) > 0;
+      __syncthreads();
+      for (int t = lane; t < nra && !bad; t += 64) {
+        const int i1 = ra[t];
+        for (int jj2 = P.i[i1]; jj2 < P.i[i1 + 1]; ++jj2) {
+          const int r = M2.insert(P.j[jj2], cur);
+          if (r < 0) { bad = 1; break; }
+          keys += r > 0;
+        }
+      }
+      bad = wave_sum(bad);
+      keys = wave_sum(keys);
+    } else {
+      bad = 1;
+    }
+    if (lane == 0) rowlen[q] = (bad || keys > lim2) ? -1 : keys;
+    __syncthreads();
   }
 }
 
@@ -684,8 +837,13 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   const size_t lds = (size_t)3 * cap * sizeof(int) + (size_t)(cap / 2) * sizeof(double);
   DBuf<int> cnt(n);
   const int grid = grid_rows(n, 32);
-  hipLaunchKernelGGL((k_extpi<false>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
-                     nullptr, nullptr, nullptr);
+  // HVE_DSETUP_PCOUNT=0: the one-lane count passes
+  static const int pcount = getenv("HVE_DSETUP_PCOUNT") ? atoi(getenv("HVE_DSETUP_PCOUNT")) : 1;
+  if (pcount)
+    hipLaunchKernelGGL(k_extpi_count_w, dim3(grid), dim3(64), (size_t)cap * 8, 0, dS, dcf.p, n, cap, lg, cnt.p);
+  else
+    hipLaunchKernelGGL((k_extpi<false>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
+                       nullptr, nullptr, nullptr);
   SDV(hipGetLastError());
   T.lap("extpi count kernel");
   // rows that overflowed: counted on the host
@@ -850,8 +1008,13 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   const DCsr dR{Ri.p, Rj.p, Ra.p, nc};
   DBuf<int> len((size_t)nc);
   const int grid = grid_rows(nc, 32);
-  hipLaunchKernelGGL((k_rap<false>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
-                     len.p, nullptr, nullptr, nullptr);
+  static const int pcount = getenv("HVE_DSETUP_PCOUNT") ? atoi(getenv("HVE_DSETUP_PCOUNT")) : 1;
+  if (pcount)
+    hipLaunchKernelGGL(k_rap_count_w, dim3(grid), dim3(64), (size_t)(cap1 + cap2) * 8 + (size_t)(cap1 / 2) * 4, 0, dR,
+                       dA.view(), dP.view(), cap1, lg1, cap2, lg2, len.p);
+  else
+    hipLaunchKernelGGL((k_rap<false>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
+                       len.p, nullptr, nullptr, nullptr);
   SDV(hipGetLastError());
   T.lap("rap count kernel");
   std::vector<int> hl;

@@ -335,13 +335,13 @@ Pattern fetch_pattern_rows(const Pattern& S, int first, const std::vector<int>& 
   CSR M;
   M.resize_rows(S.n, 0);
   M.i = S.i;
-  M.j = S.j;
+  M.j.assign(S.j.begin(), S.j.end());
   M.a.assign(S.j.size(), 1.0);
   CSR G = fetch_rows(M, first, starts, rows, c);
   Pattern P;
   P.n = G.nrows;
   P.i = G.i;
-  P.j.swap(G.j);
+  P.j.assign(G.j.begin(), G.j.end());
   return P;
 }
 
@@ -1304,8 +1304,8 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     CSR G;
     G.resize_rows(nglob_rows, M.ncols);
     for (int r = 0; r < nglob_rows; ++r) G.i[r + 1] = G.i[r] + alen[r];
-    G.j.swap(acol);
-    G.a.swap(aval);
+    G.j.assign(acol.begin(), acol.end());
+    G.a.assign(aval.begin(), aval.end());
     return G;
   };
   // coarsest-level direct solve: the coarsest operator gathered on every rank

@@ -55,9 +55,9 @@ class HostComm {
     }
   }
   // every rank's vector, concatenated in rank order
-  template <typename T>
-  std::vector<T> allgatherv(const std::vector<T>& mine) {
-    std::vector<std::vector<T>> send(size_, mine), recv;
+  template <typename T, typename Al>
+  std::vector<T> allgatherv(const std::vector<T, Al>& mine) {
+    std::vector<std::vector<T>> send(size_, std::vector<T>(mine.begin(), mine.end())), recv;
     exchange(send, recv);
     std::vector<T> out;
     for (auto& v : recv) out.insert(out.end(), v.begin(), v.end());

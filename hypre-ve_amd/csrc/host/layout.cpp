@@ -7,6 +7,7 @@
 #include <stdexcept>
 #include <unordered_map>
 #include <unordered_set>
+#include <parallel/algorithm>
 
 #include "hve_host.hpp"
 #include "layout.hpp"
@@ -42,7 +43,7 @@ int64_t sell_padded_nnz(const CSR& A, int sigma) {
 }
 
 void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vector<int>& slice_ptr,
-                     std::vector<int>& col, std::vector<double>& val) {
+                     hvec<int>& col, hvec<double>& val) {
   const int n = A.nrows;
   const int ns = (n + 63) / 64;
   sell_order(A, sigma, perm);
@@ -56,11 +57,15 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
   }
   if (sp[ns] > 0x7fffffffLL) throw std::runtime_error("padded operator exceeds 2^31 entries on one GPU");
   for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
-  col.assign((size_t)sp[ns], -1);
-  val.assign((size_t)sp[ns], 0.0);
+  col.clear();
+  val.clear();
+  col.resize((size_t)sp[ns]);
+  val.resize((size_t)sp[ns]);
 #pragma omp parallel for schedule(static)
   for (int s = 0; s < ns; ++s) {
     const int r1 = std::min(n, (s + 1) * 64);
+    std::fill(col.begin() + slice_ptr[s], col.begin() + slice_ptr[s + 1], -1);
+    std::fill(val.begin() + slice_ptr[s], val.begin() + slice_ptr[s + 1], 0.0);
     for (int r = s * 64; r < r1; ++r) {
       const int lane = r & 63, src = perm[r];
       for (int k = A.i[src]; k < A.i[src + 1]; ++k) {
@@ -87,7 +92,7 @@ void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vecto
 // its column offsets span less than 64K.  Returns false when some row
 // does not fit its slice's slots (the operator then keeps 32-bit columns).
 bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vector<int>& slot_base,
-                           std::vector<short>& dcol, std::vector<double>& val) {
+                           hvec<short>& dcol, hvec<double>& val) {
   const int n = A.nrows;
   const int ns = (n + 63) / 64;
   slice_ptr.assign(ns + 1, 0);
@@ -104,8 +109,8 @@ bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vecto
   if (sp[ns] > 0x7fffffffLL) return false;
   for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
   slot_base.assign((size_t)(sp[ns] / 64), 0);
-  dcol.assign((size_t)sp[ns], kDeltaPad);
-  val.assign((size_t)sp[ns], 0.0);
+  par_assign(dcol, (size_t)sp[ns], kDeltaPad);
+  par_assign(val, (size_t)sp[ns], 0.0);
   int ok = 1;
 #pragma omp parallel for schedule(static) reduction(min : ok)
   for (int s = 0; s < ns; ++s) {
@@ -267,8 +272,8 @@ bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vecto
     }
   }
   if (!ok) return false;
-  std::vector<unsigned char> vi;
-  if (!build_value_table(sval, 256, vi, tab)) return false;
+  hvec<unsigned char> vi;
+  if (!build_value_table(sval.data(), sval.size(), 256, vi, tab)) return false;
   // Slices with the same slot sequence (offsets, values and lane masks: the
   // interior of a stencil, and each kind of boundary slice) share one
   // pattern; a slice keeps only its pattern's index, so the slot data of a
@@ -329,18 +334,22 @@ bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vecto
 // each entry keeps an 8-bit index into the ascending-by-bits table instead of
 // its 8-byte value.  Padding entries index their own (+0.0) pattern.
 template <typename I>
-static bool value_table_impl(const std::vector<double>& val, int maxv, std::vector<I>& idx, std::vector<double>& tab) {
-  const size_t n = val.size();
+static bool value_table_impl(const double* val, size_t n, int maxv, hvec<I>& idx, std::vector<double>& tab) {
   std::vector<uint64_t> all;
   bool over = false;
 #pragma omp parallel
   {
     std::unordered_set<uint64_t> mine;
+    uint64_t last = 0;
+    bool have = false;
 #pragma omp for schedule(static)
     for (size_t i = 0; i < n; ++i) {
       if (over) continue;
       uint64_t b;
       std::memcpy(&b, &val[i], 8);
+      if (have && b == last) continue;  // runs of one value (padding, stencil slots)
+      last = b;
+      have = true;
       if (mine.insert(b).second && (int)mine.size() > maxv) over = true;
     }
 #pragma omp critical
@@ -352,7 +361,8 @@ static bool value_table_impl(const std::vector<double>& val, int maxv, std::vect
   if ((int)all.size() > maxv) return false;
   tab.resize(all.size());
   for (size_t t = 0; t < all.size(); ++t) std::memcpy(&tab[t], &all[t], 8);
-  idx.assign(n, 0);
+  idx.clear();
+  idx.resize(n);
 #pragma omp parallel for schedule(static)
   for (size_t i = 0; i < n; ++i) {
     uint64_t b;
@@ -361,13 +371,12 @@ static bool value_table_impl(const std::vector<double>& val, int maxv, std::vect
   }
   return true;
 }
-bool build_value_table(const std::vector<double>& val, int maxv, std::vector<unsigned char>& idx,
-                       std::vector<double>& tab) {
-  return value_table_impl(val, std::min(maxv, 256), idx, tab);
+bool build_value_table(const double* val, size_t n, int maxv, hvec<unsigned char>& idx, std::vector<double>& tab) {
+  return value_table_impl(val, n, std::min(maxv, 256), idx, tab);
 }
-bool build_value_table16(const std::vector<double>& val, int maxv, std::vector<unsigned short>& idx,
+bool build_value_table16(const double* val, size_t n, int maxv, hvec<unsigned short>& idx,
                          std::vector<double>& tab) {
-  return value_table_impl(val, std::min(maxv, 65536), idx, tab);
+  return value_table_impl(val, n, std::min(maxv, 65536), idx, tab);
 }
 
 // Offset-coded SELL-64.  Between two levels of a grid hierarchy the fine
@@ -378,7 +387,7 @@ bool build_value_table16(const std::vector<double>& val, int maxv, std::vector<u
 // (32-bit column + 16-bit value index) or 12.
 bool build_sell_coded_host(const CSR& A, const std::vector<int>& rowmap, const std::vector<int>& anc,
                            const std::vector<int>& colpos, const std::vector<int>& cmap, std::vector<int>& slice_ptr,
-                           std::vector<unsigned short>& code, std::vector<int>& otab, std::vector<double>& vtab,
+                           hvec<unsigned short>& code, std::vector<int>& otab, std::vector<double>& vtab,
                            int& vbits) {
   const int n = A.nrows;
   if (n == 0 || A.nnz() == 0) return false;
@@ -422,8 +431,8 @@ bool build_sell_coded_host(const CSR& A, const std::vector<int>& rowmap, const s
   std::sort(offs.begin(), offs.end());
   offs.erase(std::unique(offs.begin(), offs.end()), offs.end());
   if ((int)offs.size() > kMaxOff) return false;
-  std::vector<unsigned short> vi;
-  if (!build_value_table16(A.a, 4096, vi, vtab)) return false;
+  hvec<unsigned short> vi;
+  if (!build_value_table16(A.a.data(), A.a.size(), 4096, vi, vtab)) return false;
   vbits = 1;
   while ((1 << vbits) < (int)vtab.size()) ++vbits;
   const int obits = 16 - vbits;
@@ -440,9 +449,11 @@ bool build_sell_coded_host(const CSR& A, const std::vector<int>& rowmap, const s
   if (sp[ns] > 0x7fffffffLL) return false;
   slice_ptr.assign(ns + 1, 0);
   for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
-  code.assign((size_t)sp[ns], 0xFFFF);
+  code.clear();
+  code.resize((size_t)sp[ns]);
 #pragma omp parallel for schedule(static)
   for (int s = 0; s < ns; ++s) {
+    std::fill(code.begin() + sp[s], code.begin() + sp[s + 1], (unsigned short)0xFFFF);
     for (int r = s * 64; r < std::min(n, (s + 1) * 64); ++r) {
       const int64_t a = anchor(r);
       for (int k = A.i[r]; k < A.i[r + 1]; ++k) {
@@ -461,7 +472,7 @@ bool build_sell_coded_host(const CSR& A, const std::vector<int>& rowmap, const s
 // stored; the device recovers each offset from a wave ballot of
 // (k < rowlen[lane]).
 void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<int>& slice_ptr,
-                            std::vector<int>& rowlen, std::vector<int>& col, std::vector<double>& val) {
+                            std::vector<int>& rowlen, hvec<int>& col, hvec<double>& val) {
   const int n = A.nrows;
   const int ns = (n + 63) / 64;
   sell_order(A, 64, perm);
@@ -476,8 +487,10 @@ void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<in
   }
   if (sp[ns] > 0x7fffffffLL) throw std::runtime_error("operator exceeds 2^31 entries on one GPU");
   for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
-  col.assign((size_t)sp[ns], -1);
-  val.assign((size_t)sp[ns], 0.0);
+  col.clear();  // every entry is written below
+  val.clear();
+  col.resize((size_t)sp[ns]);
+  val.resize((size_t)sp[ns]);
 #pragma omp parallel for schedule(static)
   for (int s = 0; s < ns; ++s) {
     const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
@@ -549,8 +562,19 @@ static void cover_ranges(const std::vector<int>& cols, int max_ranges, std::vect
   rs.push_back(off);
 }
 
+void sort_rows_by_key(const std::vector<int64_t>& key, std::vector<int>& order) {
+  // ties broken by row, so any correct sort gives the stable order: libstdc++'s
+  // parallel sort on the OpenMP team (41M rows at 512^3: 3.0 s serial)
+  const int n = (int)key.size();
+  order.resize(n);
+#pragma omp parallel for schedule(static)
+  for (int r = 0; r < n; ++r) order[r] = r;
+  __gnu_parallel::sort(order.begin(), order.end(),
+                       [&](int a, int b) { return key[a] < key[b] || (key[a] == key[b] && a < b); });
+}
+
 bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& perm, std::vector<int>& slice_ptr,
-                          std::vector<int>& rowlen, std::vector<unsigned short>& col16, std::vector<double>& val,
+                          std::vector<int>& rowlen, hvec<unsigned short>& col16, hvec<double>& val,
                           std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct, int max_ranges,
                           double max_cover, const std::vector<int>* pre) {
   if (dmax > 65535) dmax = 65535;
@@ -560,34 +584,47 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
   const int ng = (ns + group - 1) / group;
   if (pre && (int)pre->size() != n) pre = nullptr;
   sell_order(A, 64, perm, pre);
-  // distinct columns of each group of `group` slices (one workgroup)
-  auto group_cols = [&](int g, std::vector<int>& cols) {
+  // distinct columns of each group of `group` slices (one workgroup), found
+  // through a per-thread hash (RowMap) and kept for the fill pass
+  std::vector<std::vector<int>> gcols(ng);
+  auto group_cols = [&](int g, RowMap& M, std::vector<int>& cols) {
     cols.clear();
     const int r0 = g * group * 64, r1 = std::min(n, (g + 1) * group * 64);
+    int64_t ent = 0;
+    for (int r = r0; r < r1; ++r) ent += A.i[perm[r] + 1] - A.i[perm[r]];
+    M.begin(std::min<int64_t>(ent, A.ncols));
+    bool fresh;
     for (int r = r0; r < r1; ++r)
-      for (int k = A.i[perm[r]]; k < A.i[perm[r] + 1]; ++k) cols.push_back(A.j[k]);
+      for (int k = A.i[perm[r]]; k < A.i[perm[r] + 1]; ++k) {
+        M.find_or_insert(A.j[k], 0, &fresh);
+        if (fresh) cols.push_back(A.j[k]);
+      }
     std::sort(cols.begin(), cols.end());
-    cols.erase(std::unique(cols.begin(), cols.end()), cols.end());
   };
   const bool ranges = max_ranges > 0;
   std::vector<int64_t> dcount(ng, 0);
   int mx = 0;
   int64_t tot_distinct = 0, tot_cover = 0;
-#pragma omp parallel for schedule(static) reduction(max : mx) reduction(+ : tot_distinct, tot_cover)
-  for (int g = 0; g < ng; ++g) {
-    std::vector<int> cols, rs;
-    group_cols(g, cols);
-    int cover = (int)cols.size();
-    if (ranges) {
-      cover_ranges(cols, max_ranges, rs);
-      cover = rs.back();
-      dcount[g] = (int64_t)rs.size() / 2;  // pairs, terminal included
-    } else {
-      dcount[g] = (int64_t)cols.size();
+#pragma omp parallel reduction(max : mx) reduction(+ : tot_distinct, tot_cover)
+  {
+    RowMap M;
+    std::vector<int> rs;
+#pragma omp for schedule(dynamic, 64)
+    for (int g = 0; g < ng; ++g) {
+      std::vector<int>& cols = gcols[g];
+      group_cols(g, M, cols);
+      int cover = (int)cols.size();
+      if (ranges) {
+        cover_ranges(cols, max_ranges, rs);
+        cover = rs.back();
+        dcount[g] = (int64_t)rs.size() / 2;  // pairs, terminal included
+      } else {
+        dcount[g] = (int64_t)cols.size();
+      }
+      tot_distinct += (int64_t)cols.size();
+      tot_cover += cover;
+      mx = std::max(mx, cover);
     }
-    tot_distinct += (int64_t)cols.size();
-    tot_cover += cover;
-    mx = std::max(mx, cover);
   }
   max_distinct = mx;
   if (mx > dmax) return false;
@@ -606,53 +643,116 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
   for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
   for (int g = 0; g <= ng; ++g) dict_ptr[g] = (int)dp[g];
   rowlen.assign((size_t)ns * 64, 0);
-  col16.assign((size_t)sp[ns], 0xFFFF);
-  val.assign((size_t)sp[ns], 0.0);
+  col16.clear();  // every entry is written below
+  val.clear();
+  col16.resize((size_t)sp[ns]);
+  val.resize((size_t)sp[ns]);
   dict.assign((size_t)dp[ng] * (ranges ? 2 : 1), 0);
-#pragma omp parallel for schedule(static)
-  for (int g = 0; g < ng; ++g) {
-    std::vector<int> cols, rs;
-    group_cols(g, cols);
-    if (ranges) {
-      cover_ranges(cols, max_ranges, rs);
-      std::copy(rs.begin(), rs.end(), dict.begin() + 2 * (size_t)dict_ptr[g]);
-    } else {
-      std::copy(cols.begin(), cols.end(), dict.begin() + dict_ptr[g]);
-    }
-    const int nrg = (int)rs.size() / 2 - 1;
-    // position of column c in the group's x-tile
-    auto local = [&](int c) -> int {
-      if (!ranges) return (int)(std::lower_bound(cols.begin(), cols.end(), c) - cols.begin());
-      int lo = 0, hi = nrg - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) / 2;
-        if (rs[2 * mid] <= c) lo = mid;
-        else hi = mid - 1;
+#pragma omp parallel
+  {
+    RowMap M;
+    std::vector<int> rs;
+#pragma omp for schedule(dynamic, 64)
+    for (int g = 0; g < ng; ++g) {
+      std::vector<int> cols;
+      cols.swap(gcols[g]);
+      if (ranges) {
+        cover_ranges(cols, max_ranges, rs);
+        std::copy(rs.begin(), rs.end(), dict.begin() + 2 * (size_t)dict_ptr[g]);
+      } else {
+        std::copy(cols.begin(), cols.end(), dict.begin() + dict_ptr[g]);
+        M.begin((int64_t)cols.size());
+        bool fresh;
+        for (int t = 0; t < (int)cols.size(); ++t) *M.find_or_insert(cols[t], t, &fresh) = t;
       }
-      return rs[2 * lo + 1] + (c - rs[2 * lo]);
-    };
-    for (int s = g * group; s < std::min(ns, (g + 1) * group); ++s) {
-      const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
-      int len[64] = {0};
-      for (int r = r0; r < r1; ++r) {
-        len[r - r0] = A.i[perm[r] + 1] - A.i[perm[r]];
-        rowlen[r] = len[r - r0];
-      }
-      size_t pos = (size_t)slice_ptr[s];
-      for (int k = 0; k < len[0]; ++k) {
-        int cnt = 0;
-        while (cnt < r1 - r0 && len[cnt] > k) ++cnt;  // lanes sorted by descending length
-        for (int l = 0; l < cnt; ++l) {
-          const int src = perm[r0 + l];
-          const int c = A.j[A.i[src] + k];
-          col16[pos + l] = (unsigned short)local(c);
-          val[pos + l] = A.a[A.i[src] + k];
+      const int nrg = (int)rs.size() / 2 - 1;
+      // position of column c in the group's x-tile
+      auto local = [&](int c) -> int {
+        if (!ranges) return M.get(c, 0);
+        int lo = 0, hi = nrg - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) / 2;
+          if (rs[2 * mid] <= c) lo = mid;
+          else hi = mid - 1;
         }
-        pos += cnt;
+        return rs[2 * lo + 1] + (c - rs[2 * lo]);
+      };
+      for (int s = g * group; s < std::min(ns, (g + 1) * group); ++s) {
+        const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
+        int len[64] = {0};
+        for (int r = r0; r < r1; ++r) {
+          len[r - r0] = A.i[perm[r] + 1] - A.i[perm[r]];
+          rowlen[r] = len[r - r0];
+        }
+        size_t pos = (size_t)slice_ptr[s];
+        for (int k = 0; k < len[0]; ++k) {
+          int cnt = 0;
+          while (cnt < r1 - r0 && len[cnt] > k) ++cnt;  // lanes sorted by descending length
+          for (int l = 0; l < cnt; ++l) {
+            const int src = perm[r0 + l];
+            const int c = A.j[A.i[src] + k];
+            col16[pos + l] = (unsigned short)local(c);
+            val[pos + l] = A.a[A.i[src] + k];
+          }
+          pos += cnt;
+        }
       }
     }
   }
   return true;
+}
+
+// Packed SELL-64 entries (k_sell_code PK): code = ((col - base[slice]) << vbits)
+// | value index, base = the slice's smallest column, padding 0xFFFFFFFF.  false
+// when some slice's column span does not fit 32 - vbits bits (all-ones span
+// reserved, so no entry equals the padding code).
+bool pack_sell_codes(const std::vector<int>& sp, const hvec<int>& col,
+                            const hvec<unsigned short>& vi, int nv, hvec<unsigned>& code,
+                            std::vector<int>& base, int& vbits) {
+  int vb = 1;
+  while ((1 << vb) < nv) ++vb;
+  const int ns = (int)sp.size() - 1;
+  const int64_t lim = (int64_t(1) << (32 - vb)) - 1;
+  base.assign(ns + 1, 0);  // one past the last: the kernel's scalar load may run ahead
+  code.clear();
+  code.resize(col.size());
+  int ok = 1;
+#pragma omp parallel for schedule(static) reduction(min : ok)
+  for (int s = 0; s < ns; ++s) {
+    std::fill(code.begin() + sp[s], code.begin() + sp[s + 1], 0xFFFFFFFFu);
+    int lo = INT32_MAX, hi = -1;
+    for (int q = sp[s]; q < sp[s + 1]; ++q)
+      if (col[q] >= 0) { lo = std::min(lo, col[q]); hi = std::max(hi, col[q]); }
+    if (hi < 0) continue;
+    if ((int64_t)hi - lo >= lim) { ok = 0; continue; }
+    base[s] = lo;
+    for (int q = sp[s]; q < sp[s + 1]; ++q)
+      if (col[q] >= 0) code[q] = ((unsigned)(col[q] - lo) << vb) | vi[q];
+  }
+  if (!ok) return false;
+  vbits = vb;
+  return true;
+}
+
+int csr_max_col(const CSR& A) {
+  int mx = -1;
+  const int64_t nnz = A.nnz();
+#pragma omp parallel for schedule(static) reduction(max : mx)
+  for (int64_t k = 0; k < nnz; ++k) mx = std::max(mx, A.j[k]);
+  return mx;
+}
+
+bool l1_rows_match(const CSR& A, const std::vector<int>& map, const std::vector<double>& l1) {
+  int ok = 1;
+#pragma omp parallel for schedule(static) reduction(min : ok)
+  for (int i = 0; i < A.nrows; ++i) {
+    double s = 0.0;
+    for (int q = A.i[i]; q < A.i[i + 1]; ++q) s += std::fabs(A.a[q]);
+    if (A.i[i + 1] > A.i[i] && A.a[A.i[i]] < 0.0) s = -s;
+    const int g = map.empty() ? i : map[i];
+    if (g < 0 || g >= (int)l1.size() || std::memcmp(&s, &l1[g], sizeof(double)) != 0) ok = 0;
+  }
+  return ok != 0;
 }
 
 std::vector<int> hypre_block_starts(int n, int nb) {

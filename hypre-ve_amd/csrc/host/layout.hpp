@@ -1,5 +1,6 @@
 #pragma once
 #include <cstdint>
+#include <utility>
 #include <string>
 #include <vector>
 
@@ -12,14 +13,14 @@ namespace hve {
 // receives the CSR row stored at position i; sigma == 0 keeps the row order
 // and leaves perm empty.
 void build_sell_host(const CSR& A, int sigma, std::vector<int>& perm, std::vector<int>& slice_ptr,
-                     std::vector<int>& col, std::vector<double>& val);
+                     hvec<int>& col, hvec<double>& val);
 // SELL-64 with 16-bit column deltas (row order and entry order kept; padded
 // slots may sit between a row's entries): entry k of the slice's lane r at
 // slice_ptr[s] + 64k + r holds col - row - slot_base[slice_ptr[s]/64 + k], or
 // kDeltaPad for padding.  false when some row does not fit (no layout built).
 constexpr short kDeltaPad = -32768;
 bool build_sell_delta_host(const CSR& A, std::vector<int>& slice_ptr, std::vector<int>& slot_base,
-                           std::vector<short>& dcol, std::vector<double>& val);
+                           hvec<short>& dcol, hvec<double>& val);
 // Slot-uniform SELL-64 for constant-coefficient stencils: no per-entry data.
 // Slices with identical slot sequences share a pattern: slice s uses pattern
 // slice_pat[s], whose `width` slots k (index pattern * width + k) hold column
@@ -33,10 +34,9 @@ bool build_sell_stencil_host(const CSR& A, int max_width, int& width, std::vecto
 // Lossless value table: idx[i] indexes tab (ascending by bit pattern) with
 // tab[idx[i]] bitwise equal to val[i]; false when more than maxv (<= 256)
 // distinct values occur.
-bool build_value_table(const std::vector<double>& val, int maxv, std::vector<unsigned char>& idx,
-                       std::vector<double>& tab);
+bool build_value_table(const double* val, size_t n, int maxv, hvec<unsigned char>& idx, std::vector<double>& tab);
 // The same with 16-bit indices (maxv <= 65536).
-bool build_value_table16(const std::vector<double>& val, int maxv, std::vector<unsigned short>& idx,
+bool build_value_table16(const double* val, size_t n, int maxv, hvec<unsigned short>& idx,
                          std::vector<double>& tab);
 // Offset-coded SELL-64 (P and R between two levels of a grid hierarchy).  Row
 // i of A (local row g = rowmap[i], identity when empty) has the anchor
@@ -50,14 +50,14 @@ bool build_value_table16(const std::vector<double>& val, int maxv, std::vector<u
 // not recovered exactly.
 bool build_sell_coded_host(const CSR& A, const std::vector<int>& rowmap, const std::vector<int>& anc,
                            const std::vector<int>& colpos, const std::vector<int>& cmap, std::vector<int>& slice_ptr,
-                           std::vector<unsigned short>& code, std::vector<int>& otab, std::vector<double>& vtab,
+                           hvec<unsigned short>& code, std::vector<int>& otab, std::vector<double>& vtab,
                            int& vbits);
 // Jagged SELL-64 (no stored padding): perm[i] = CSR row at stored position i
 // (rows sorted by descending length inside each slice), rowlen[i] its length
 // (nslices*64 entries, 0 past the last row), entry k of the slice's lane r at
 // slice_ptr[s] + sum_{k'<k} #{lanes with rowlen > k'} + r.
 void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<int>& slice_ptr,
-                            std::vector<int>& rowlen, std::vector<int>& col, std::vector<double>& val);
+                            std::vector<int>& rowlen, hvec<int>& col, hvec<double>& val);
 // Jagged SELL-64 with a per-slice column dictionary (16-bit local column
 // indices into the slice's ascending list of distinct columns).  false when
 // a slice has more than dmax distinct columns; max_distinct is set either way.
@@ -72,10 +72,24 @@ void build_sell_jagged_host(const CSR& A, std::vector<int>& perm, std::vector<in
 // position in the concatenated ranges.  false when a group covers more than
 // dmax columns or the covered columns exceed max_cover x its distinct ones;
 // max_distinct is then the largest covered count.
+// Rows 0..n-1 ordered by ascending key, ties by row (a stable sort by key).
+void sort_rows_by_key(const std::vector<int64_t>& key, std::vector<int>& order);
 bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& perm, std::vector<int>& slice_ptr,
-                          std::vector<int>& rowlen, std::vector<unsigned short>& col16, std::vector<double>& val,
+                          std::vector<int>& rowlen, hvec<unsigned short>& col16, hvec<double>& val,
                           std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct,
                           int max_ranges = 0, double max_cover = 1.5, const std::vector<int>* pre = nullptr);
+// Packed SELL-64 entries (k_sell_code PK) from a padded layout (col, 16-bit
+// value indices vi into nv values): code = ((col - base[slice]) << vbits) |
+// value index, base = the slice's smallest column, padding 0xFFFFFFFF.  false
+// when some slice's column span does not fit 32 - vbits bits.
+bool pack_sell_codes(const std::vector<int>& sp, const hvec<int>& col, const hvec<unsigned short>& vi, int nv,
+                     hvec<unsigned>& code, std::vector<int>& base, int& vbits);
+// Largest column index of A (-1 when empty).
+int csr_max_col(const CSR& A);
+// True when every row's l1[map[i]] (map empty: i) equals, bit for bit, the sum
+// of |a_ij| over its stored entries in order, negated for a negative first
+// entry (the on-the-fly l1 norms of the device kernels).
+bool l1_rows_match(const CSR& A, const std::vector<int>& map, const std::vector<double>& l1);
 // Padded entry count of the SELL-64 layout for a given sigma (0 = no sort).
 int64_t sell_padded_nnz(const CSR& A, int sigma);
 // Packed, step-ordered schedule of one hybrid Gauss-Seidel sweep (par_relax.c

@@ -497,7 +497,7 @@ struct W {
     const char* p = (const char*)&v;
     b.insert(b.end(), p, p + sizeof(T));
   }
-  template <typename T> void vec(const std::vector<T>& v) {
+  template <typename T, typename Al> void vec(const std::vector<T, Al>& v) {
     pod<int64_t>((int64_t)v.size());
     const char* p = (const char*)v.data();
     b.insert(b.end(), p, p + v.size() * sizeof(T));
@@ -516,7 +516,7 @@ struct Rd {
     std::memcpy(&v, b.data() + o, sizeof(T));
     o += sizeof(T);
   }
-  template <typename T> void vec(std::vector<T>& v) {
+  template <typename T, typename Al> void vec(std::vector<T, Al>& v) {
     int64_t n;
     pod(n);
     if (n < 0 || o + (size_t)n * sizeof(T) > b.size()) throw std::runtime_error("deserialize: bad length");

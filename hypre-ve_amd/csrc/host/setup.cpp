@@ -791,8 +791,8 @@ void truncate_rows(CSR& P, double tol, int max_elmts) {
   }
   std::vector<int> ni(n + 1, 0);
   for (int r = 0; r < n; ++r) ni[r + 1] = ni[r] + newlen[r];
-  std::vector<int> nj(ni[n]);
-  std::vector<double> na(ni[n]);
+  hvec<int> nj(ni[n]);
+  hvec<double> na(ni[n]);
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < n; ++r) {
     std::copy(P.j.begin() + P.i[r], P.j.begin() + P.i[r] + newlen[r], nj.begin() + ni[r]);
@@ -1309,7 +1309,7 @@ void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Patte
   std::vector<int> frow, ffrow;
   fffc(A, cf, S, false, FF, FC, frow, ffrow);
   const int nF = (int)frow.size();
-  const std::vector<double> orig = FF.a;
+  const hvec<double> orig = FF.a;
   std::vector<double> dq(nF, 0.0), dw(nF, 0.0), dth(nF, 0.0);
 #pragma omp parallel for schedule(static)
   for (int r = 0; r < nF; ++r)
@@ -2194,7 +2194,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         CSR S2A;  // hypre passes S2 as the matrix too (only its row lengths, for cut_factor)
         S2A.resize_rows(S2.n, S2.n);
         S2A.i = S2.i;
-        S2A.j = S2.j;
+        S2A.j.assign(S2.j.begin(), S2.j.end());
         S2A.a.assign(S2.j.size(), 1.0);
         coarsen_hmis(S2, &S2A, prm.measure_type + 3, prm.coarsen_cut_factor, cfn, rsc);
       } else {
