@@ -1192,9 +1192,13 @@ HYPRE_Int HYPRE_BoomerAMGSetup(HYPRE_Solver s, HYPRE_ParCSRMatrix A, HYPRE_ParVe
   if (lent) give_back_single_rank(s->H, s->RH);
   s->dev->set_use_graph(s->use_graph);
   const double t3 = now();
-  char tb[160];
-  snprintf(tb, sizeof tb, "setup: hierarchy %.3fs, rank partition %.3fs, device layouts and upload %.3fs\n", t1 - t0,
-           t2 - t1, t3 - t2);
+  char tb[224];
+  double rss_c, rss_p;
+  host_rss_gb(&rss_c, &rss_p);
+  snprintf(tb, sizeof tb,
+           "setup: hierarchy %.3fs, rank partition %.3fs, device layouts and upload %.3fs (host RSS %.1f GB, peak "
+           "%.1f GB)\n",
+           t1 - t0, t2 - t1, t3 - t2, rss_c, rss_p);
   s->H.log += tb;
   if (s->prm.print_level > 0) fputs(tb, stderr);
   API_END

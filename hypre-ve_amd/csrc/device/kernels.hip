@@ -1561,13 +1561,19 @@ static constexpr int kGsWaves = 4;           // teams per workgroup
 static constexpr int kGsProd = 512;          // LDS products per wave and chunk
 static constexpr int kGsPer = kGsProd / 64;  // entries per lane and chunk
 int gs_chunk_entries() { return kGsProd; }
-// The pipelined sweep (k_hybrid_gs_pipe): HVE_GS_PIPE 1 (default) = every
-// schedule, 2 = only where every step fits one chunk, 0 = k_hybrid_gs
-// (except schedules stored with 8-bit value indices, which only it reads).
+// The pipelined sweep (k_hybrid_gs_pipe): HVE_GS_PIPE 2 (default) = where
+// every step fits one chunk, 1 = every schedule, 0 = k_hybrid_gs (except
+// schedules stored with 8-bit value indices, which only it reads).  Measured
+// at 512^3 (relax 13/14, profiles/r05/08_gs_variants): 49.8 ms a cycle with
+// 2, 52.2 with 1 (the Galerkin levels' steps of 4 rows gain nothing from the
+// prefetch).  Two variants measured slower and not kept: loading only a
+// unit's used 64-entry groups (level 0 3.42 vs 3.15 ms a sweep), and skipping
+// the U fences in teams that read no U (4.49 ms: the fence's drain every 4
+// steps keeps the sweep faster).
 bool gs_uses_pipe(bool one_chunk) {
   static const int pipe_env = [] {
     const char* e = getenv("HVE_GS_PIPE");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 2;
   }();
   return pipe_env == 1 || (pipe_env == 2 && one_chunk);
 }

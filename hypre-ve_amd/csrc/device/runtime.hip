@@ -762,6 +762,9 @@ void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forw
   entries = (int64_t)S.code.size();
   nnz = S.nnz;
   team_step = dupload(S.team_step.data(), S.team_step.size());
+  if (getenv("HVE_LAYOUT_LOG"))
+    fprintf(stderr, "[layout] gs %s rows=%d teams=%d steps=%d one_chunk=%d\n", forward ? "fwd" : "bwd", A.nrows,
+            S.nteams, S.team_step.empty() ? 0 : S.team_step.back(), (int)one_chunk);
   step = dupload(S.step.data(), std::max<size_t>(4, S.step.size()));
   code = dupload(S.code.data(), std::max<size_t>(1, S.code.size()));
   // At most 256 distinct values (level 0 of a constant-coefficient stencil):
@@ -1273,7 +1276,12 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
       D.cheby_o = dalloc<double>(D.n);
       HVE_HIP(hipMemset(D.cheby_t, 0, sizeof(double) * std::max(1, D.n + D.hu.n_halo)));
     }
-    if (tlog) fprintf(stderr, "[build] level %d: %.3fs (A %s)\n", l, now() - tl0, D.A.in.slot_mask ? "stencil" : "");
+    if (tlog) {
+      double rc, rp;
+      host_rss_gb(&rc, &rp);
+      fprintf(stderr, "[build] level %d: %.3fs (A %s) host RSS %.1f GB, peak %.1f GB\n", l, now() - tl0,
+              D.A.in.slot_mask ? "stencil" : "", rc, rp);
+    }
   }
   // Hybrid Gauss-Seidel schedules for the relax types the cycle uses
   // (num_blocks = hypre's thread count: row blocks of each level).

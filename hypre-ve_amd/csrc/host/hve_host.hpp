@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <memory>
 #include <new>
@@ -77,6 +78,21 @@ void par_assign(hvec<T>& v, size_t n, T x) {
   for (int64_t i = 0; i < (int64_t)n; ++i) p[i] = x;
 }
 
+
+// Resident and peak host memory of this process in GB (/proc/self/status
+// VmRSS / VmHWM; 0 where unavailable): the setup's stage logs.
+inline void host_rss_gb(double* cur, double* peak) {
+  *cur = *peak = 0.0;
+  if (FILE* f = fopen("/proc/self/status", "r")) {
+    char line[256];
+    while (fgets(line, sizeof line, f)) {
+      long long kb = 0;
+      if (sscanf(line, "VmRSS: %lld kB", &kb) == 1) *cur = kb / 1048576.0;
+      if (sscanf(line, "VmHWM: %lld kB", &kb) == 1) *peak = kb / 1048576.0;
+    }
+    fclose(f);
+  }
+}
 
 // CSR matrix, 0-based, hypre convention: in square operators the diagonal
 // entry is stored first in its row (parcsr_mv relies on A_diag_i[i] == diag).

@@ -885,9 +885,9 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
   S.team_step.assign(nt + 1, 0);
   for (int t = 0; t <= nt; ++t) S.team_step[t] = (int)t_steps[t];
   S.step.assign((size_t)nsteps * 4, 0);
-  S.code.assign((size_t)nent, -1);
-  S.val.assign((size_t)nent, 0.0);
-  if (with_tcol) S.tcol.assign((size_t)nent, -1);
+  par_assign(S.code, (size_t)nent, -1);
+  par_assign(S.val, (size_t)nent, 0.0);
+  if (with_tcol) par_assign(S.tcol, (size_t)nent, -1);
   S.rowmap.assign(n, 0);
   // per row: its position, step and lane
   std::vector<int> pos(n, 0), st_of(n, 0), ln_of(n, 0), blk_of(n, 0);

@@ -143,9 +143,9 @@ struct GsSchedule {
   std::vector<int> block_start;  // nb + 1 row boundaries (hypre's ns / ne)
   std::vector<int> team_step;    // nteams + 1: step range of each team
   std::vector<int> step;         // 4 per step: entry offset (unsigned), position offset, rows, width
-  std::vector<int> code;         // per entry (see above)
-  std::vector<double> val;       // per entry, 0 for padding
-  std::vector<int> tcol;         // with_tcol: in-block entries' T offset in G (the weighted forms' Vtemp), else -1
+  hvec<int> code;                // per entry (see above)
+  hvec<double> val;              // per entry, 0 for padding
+  hvec<int> tcol;                // with_tcol: in-block entries' T offset in G (the weighted forms' Vtemp), else -1
   std::vector<int> rowmap;       // nrows: row of each position
   std::vector<double> l1;        // l1 norms by position (when given)
   std::vector<int> cf;           // CF marker by position (when given)

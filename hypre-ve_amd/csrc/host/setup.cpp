@@ -2357,8 +2357,12 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     }
     if (level == prm.max_levels - 1 || coarse_size <= prm.max_coarse_size) finished = true;
   }
-  snprintf(buf, sizeof buf, "setup phases: strength %.3fs coarsen %.3fs interp %.3fs rap %.3fs transpose %.3fs\n",
-           t_s, t_c, t_i, t_r, t_t);
+  double rss_c, rss_p;
+  host_rss_gb(&rss_c, &rss_p);
+  snprintf(buf, sizeof buf,
+           "setup phases: strength %.3fs coarsen %.3fs interp %.3fs rap %.3fs transpose %.3fs (host RSS %.1f GB, "
+           "peak %.1f GB)\n",
+           t_s, t_c, t_i, t_r, t_t, rss_c, rss_p);
   H.log += buf;
   const double t_l1 = now();
   const int nl = (int)H.lev.size();
