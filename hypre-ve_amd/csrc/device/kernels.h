@@ -125,7 +125,8 @@ int gs_chunk_entries();
 // whether launch_hybrid_gs takes the pipelined sweep for a schedule
 bool gs_uses_pipe(bool one_chunk);
 // The sweep's vectors in its order (layout.hpp GsSchedule): G[k] = tmp[rowmap[k]]
-// (T; u when tmp is null), G[n + k] = u[rowmap[k]] (C), F[k] = f[rowmap[k]],
+// (T; not written when tmp is null: the sweep then reads T from C, t_is_c),
+// G[n + k] = u[rowmap[k]] (C), F[k] = f[rowmap[k]],
 // and the off-rank halo of u, u[n .. n + nhalo), into G[3n ..).
 hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp, const double* f, int nhalo,
                             double* G, double* F, hipStream_t st);
@@ -133,7 +134,7 @@ hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp,
 // writes G's U part, then scatters it into u (natural rows).  G (3n + nhalo
 // doubles) must stay below 4 GiB.
 hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, int nhalo,
-                            const double* F, double* u, double w, double omega, hipStream_t st);
+                            const double* F, double* u, double w, double omega, bool t_is_c, hipStream_t st);
 int sell_batch_override();
 // Tuning knobs read at launch (0 = default): 0 offset-coded row blocks per
 // step (1, 2, 4), 1 its codes per batch (4, 8, 16), 2 its workgroups per CU,

@@ -1556,7 +1556,17 @@ struct GsArgs {
   int n, nteams, relax_points;
   unsigned gbytes;  // G's size in bytes (< 4 GiB: 32-bit buffer offsets)
   double w, omega;
+  int exp;  // HVE_GS_EXP (timing experiments, wrong results): 1 no value loads, 2 no source gathers
+  // n when T is u itself (no pre-sweep copy of another vector): T codes read
+  // C, so an off-block value shares the L2 lines its own team reads, and the
+  // gather writes one copy instead of two
+  unsigned tshift;
 };
+// G byte offset of an entry's source (ring and padding codes read G[0])
+__device__ __forceinline__ int gs_src_off(int c, unsigned n, unsigned tshift) {
+  const unsigned u = c > 0 ? (unsigned)c : 0u;
+  return (int)((u < n ? u + tshift : u) * 8u);
+}
 static constexpr int kGsWaves = 4;           // teams per workgroup
 static constexpr int kGsProd = 512;          // LDS products per wave and chunk
 static constexpr int kGsPer = kGsProd / 64;  // entries per lane and chunk
@@ -1650,15 +1660,15 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
         const int e = lane + 64 * t;
         const int o = base + (e < E ? e : 0);
         c[t] = gs_ld32(rc, o * 4);
-        a[t] = gs_ld64(rv8, o * 8);
+        a[t] = (p.exp & 1) ? 1.0 : gs_ld64(rv8, o * 8);
         tc[t] = WGT ? gs_ld32(rt, o * 4) : -1;
       }
 #pragma unroll
       for (int t = 0; t < kGsPer; ++t) {
         if (64 * t >= E) break;
         // unsigned byte offsets: G may exceed 2 GiB (< 4 GiB)
-        x[t] = gs_ld64(rG, (int)((unsigned)(c[t] > 0 ? c[t] : 0) * 8u));
-        if (WGT) t2[t] = gs_ld64(rG, (int)((unsigned)(tc[t] > 0 ? tc[t] : 0) * 8u));
+        x[t] = (p.exp & 2) ? 1.0 : gs_ld64(rG, gs_src_off(c[t], (unsigned)p.n, p.tshift));
+        if (WGT) t2[t] = gs_ld64(rG, gs_src_off(tc[t], (unsigned)p.n, p.tshift));
       }
 #pragma unroll
       for (int t = 0; t < kGsPer; ++t) {
@@ -1837,8 +1847,8 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
   auto load_b = [&](const GsStage<VT>& S, double (&x)[kGsPer], double (&t2)[kGsPer]) {
 #pragma unroll
     for (int t = 0; t < kGsPer; ++t) {
-      x[t] = gs_ld64(rG, (int)((unsigned)(S.c[t] > 0 ? S.c[t] : 0) * 8u));
-      t2[t] = WGT ? gs_ld64(rG, (int)((unsigned)(S.tc[t] > 0 ? S.tc[t] : 0) * 8u)) : 0.0;
+      x[t] = gs_ld64(rG, gs_src_off(S.c[t], (unsigned)p.n, p.tshift));
+      t2[t] = WGT ? gs_ld64(rG, gs_src_off(S.tc[t], (unsigned)p.n, p.tshift)) : 0.0;
     }
   };
   GsStage<VT> S0, S1, S2;
@@ -1974,17 +1984,26 @@ template <bool NAT>
 __global__ void __launch_bounds__(256) k_gs_gather(int n, int nhalo, const int* __restrict__ map,
                                                    const double* __restrict__ u, const double* __restrict__ tmp,
                                                    const double* __restrict__ f, double* __restrict__ G,
-                                                   double* __restrict__ F) {
+                                                   double* __restrict__ F, bool writeT) {
   int q0, q1;
   gs_perm_range(n, q0, q1);
   for (int q = q0 + threadIdx.x; q < q1; q += 256) {
     const int i = NAT ? q : map[q], k = NAT ? map[q] : q;
     const double v = u[i];
-    G[k] = tmp ? tmp[i] : v;
+    if (tmp || writeT) G[k] = tmp ? tmp[i] : v;  // else the sweep reads T from C
     G[n + k] = v;
     F[k] = f[i];
   }
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nhalo; k += gridDim.x * blockDim.x) G[3 * n + k] = u[n + k];
+}
+
+// HVE_GS_TC=0: the gather writes T = u as its own copy and T codes read it
+static bool gs_t_from_c() {
+  static const bool v = [] {
+    const char* e = getenv("HVE_GS_TC");
+    return e ? atoi(e) != 0 : true;
+  }();
+  return v;
 }
 
 static int gs_natural_order() {
@@ -2000,20 +2019,25 @@ hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp,
   if (S.nrows <= 0) return hipSuccess;
   const int grid = std::min((S.nrows + 255) / 256 + 7, 256 * 16) & ~7;
   if (gs_natural_order() & 1)
-    hipLaunchKernelGGL(k_gs_gather<true>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.pos, u, tmp, f, G, F);
+    hipLaunchKernelGGL(k_gs_gather<true>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.pos, u, tmp, f, G, F,
+                       !gs_t_from_c());
   else
-    hipLaunchKernelGGL(k_gs_gather<false>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.rowmap, u, tmp, f, G, F);
+    hipLaunchKernelGGL(k_gs_gather<false>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.rowmap, u, tmp, f, G, F,
+                       !gs_t_from_c());
   return hipGetLastError();
 }
 
 hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_points, double* G, int nhalo,
-                            const double* F, double* u, double w, double omega, hipStream_t st) {
+                            const double* F, double* u, double w, double omega, bool t_is_c, hipStream_t st) {
   if (S.nteams <= 0) return hipSuccess;
   GsArgs a;
   a.team_step = S.team_step; a.step = S.step; a.code = S.code; a.val = S.val; a.tcol = S.tcol; a.rowmap = S.rowmap;
   a.vidx = S.vidx8; a.vtab = S.vtab; a.nvtab = S.nvtab;
   a.l1 = S.l1; a.cf = S.cf; a.G = G; a.F = F; a.u = u;
   a.n = S.nrows; a.nteams = S.nteams; a.relax_points = relax_points; a.w = w; a.omega = omega;
+  a.tshift = (t_is_c && gs_t_from_c()) ? (unsigned)S.nrows : 0u;
+  static const int gs_exp = getenv("HVE_GS_EXP") ? atoi(getenv("HVE_GS_EXP")) : 0;
+  a.exp = gs_exp;
   const uint64_t gbytes = (3 * (uint64_t)S.nrows + (uint64_t)nhalo) * sizeof(double);
   if (gbytes > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit buffer offsets (about 178M rows a GPU)
   a.gbytes = (unsigned)gbytes;

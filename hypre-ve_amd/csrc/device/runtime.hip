@@ -1592,12 +1592,12 @@ void DevAMG::relax(int level, int relax_type, int relax_points, const double* f,
       if (fw) {
         HVE_HIP(launch_gs_gather(L.gs_fwd.view(), u_cur, nullptr, f, L.hu.n_halo, L.gs_G, L.gs_F, s));
         HVE_HIP(launch_hybrid_gs(L.gs_fwd.view(), use_l1, cfsel, relax_points, L.gs_G, L.hu.n_halo, L.gs_F, u_cur, w, omega,
-                                         s));
+                                 true, s));
       }
       if (bw) {
         HVE_HIP(launch_gs_gather(L.gs_bwd.view(), u_cur, fw ? L.gs_tmp : nullptr, f, L.hu.n_halo, L.gs_G, L.gs_F, s));
         HVE_HIP(launch_hybrid_gs(L.gs_bwd.view(), use_l1, cfsel, relax_points, L.gs_G, L.hu.n_halo, L.gs_F, u_cur, w, omega,
-                                         s));
+                                 !fw, s));
       }
       break;
     }
