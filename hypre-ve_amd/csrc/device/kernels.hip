@@ -1125,40 +1125,97 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
     pre[r] = act[r] ? row_preload<OP, true>(p, g[r]) : RowPre{};
     t[r] = act[r] ? row_init<OP, true>(p, g[r]) : 0.0;
   }
-  unsigned c[NR][B];
-#pragma unroll
-  for (int r = 0; r < NR; ++r)
-#pragma unroll
-    for (int q = 0; q < B; ++q) c[r][q] = q < width[r] ? (unsigned)__builtin_nontemporal_load(cp[r] + q * kWave) : PAD;
-  for (int k = 0; k < wmax; k += B) {
-    double xv[NR][B];
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-      for (int q = 0; q < B; ++q) {
-        const int pos = c[r][q] != PAD ? a[r] + (PK ? (int)(c[r][q] >> vb) : ot[c[r][q] >> vb]) : 0;
-        const int col = c[r][q] == PAD ? -1 : (MAP && !PK) ? p.cmap[pos] : pos;
-        xv[r][q] = col >= 0 ? p.x[col] : 0.0;
-      }
-    unsigned cn[NR][B];
+  if constexpr (!PK && !MAP) {
+    // R_0: every lane issues every load (codes of slot min(k, wmax - 1), the
+    // gather of a left-out entry at the row's anchor), so a batch is a fixed
+    // count of loads and the waits are exact counters instead of a drain at
+    // each lane-masked branch; the offset and value tables are read for every
+    // entry before the sums (slot 0 for a left-out one).  An entry past the
+    // lane's width, a padding code or an inactive lane is selected out of the
+    // sum (t unchanged).  1.62 -> 1.44 ms at 512^3 (scripts/code_knobs.py).
+    const int wl = max(wmax - 1, 0);
+    unsigned c[NR][B];
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
-      for (int q = 0; q < B; ++q)
-        cn[r][q] = (k + B + q) < width[r] ? (unsigned)__builtin_nontemporal_load(cp[r] + (k + B + q) * kWave) : PAD;
+      for (int q = 0; q < B; ++q) c[r][q] = (unsigned)__builtin_nontemporal_load(cp[r] + min(q, wl) * kWave);
+    for (int k = 0; k < wmax; k += B) {
+      bool ok[NR][B];
+      double xv[NR][B];
 #pragma unroll
-    for (int r = 0; r < NR; ++r)
+      for (int r = 0; r < NR; ++r)
 #pragma unroll
-      for (int q = 0; q < B; ++q) {
-        if (c[r][q] != PAD) {
-          const double pr = vt[c[r][q] & vm] * xv[r][q];
-          t[r] = sub ? t[r] - pr : t[r] + pr;
+        for (int q = 0; q < B; ++q) {
+          ok[r][q] = (k + q) < width[r] && c[r][q] != PAD;
+          const int off = ot[ok[r][q] ? (c[r][q] >> vb) : 0u];
+          xv[r][q] = p.x[a[r] + (ok[r][q] ? off : 0)];
         }
-      }
+      unsigned cn[NR][B];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          // (none past the last batch: a wave-uniform test)
+          cn[r][q] = k + B < wmax ? (unsigned)__builtin_nontemporal_load(cp[r] + min(k + B + q, wl) * kWave) : PAD;
+        }
+      asm volatile("" ::: "memory");  // the next codes go out before the sums
+      double av[NR][B];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) av[r][q] = vt[ok[r][q] ? (c[r][q] & vm) : 0u];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const double pr = av[r][q] * xv[r][q];
+          const double tn = sub ? t[r] - pr : t[r] + pr;
+          t[r] = ok[r][q] ? tn : t[r];
+        }
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) c[r][q] = cn[r][q];
+    }
+  } else {
+    // P_0: lane-masked code loads and gathers (its rows are short and
+    // half its slots padding, so all-lane loads cost more than the
+    // exact waits gain: 0.99 -> 1.61 ms at 512^3)
+    unsigned c[NR][B];
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
-      for (int q = 0; q < B; ++q) c[r][q] = cn[r][q];
+      for (int q = 0; q < B; ++q) c[r][q] = q < width[r] ? (unsigned)__builtin_nontemporal_load(cp[r] + q * kWave) : PAD;
+    for (int k = 0; k < wmax; k += B) {
+      double xv[NR][B];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const int pos = c[r][q] != PAD ? a[r] + (PK ? (int)(c[r][q] >> vb) : ot[c[r][q] >> vb]) : 0;
+          const int col = c[r][q] == PAD ? -1 : (MAP && !PK) ? p.cmap[pos] : pos;
+          xv[r][q] = col >= 0 ? p.x[col] : 0.0;
+        }
+      unsigned cn[NR][B];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q)
+          cn[r][q] = (k + B + q) < width[r] ? (unsigned)__builtin_nontemporal_load(cp[r] + (k + B + q) * kWave) : PAD;
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          if (c[r][q] != PAD) {
+            const double pr = vt[c[r][q] & vm] * xv[r][q];
+            t[r] = sub ? t[r] - pr : t[r] + pr;
+          }
+        }
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) c[r][q] = cn[r][q];
+    }
   }
 #pragma unroll
   for (int r = 0; r < NR; ++r)
@@ -1346,22 +1403,75 @@ __global__ void __launch_bounds__(256) k_sell_pw(SpArgs p) {
 // reads 2-byte local columns and takes x from LDS.  Same entries, same order,
 // same rounding as every other loop: bitwise the same.
 // ---------------------------------------------------------------------------
+// Experiment switches (compile time): clamped all-lane loads in the
+// dictionary loop, two register sets there, lane-masked gathers in the coded
+// loop
+#ifndef HVE_DICT_CLAMP
+#define HVE_DICT_CLAMP 0
+#endif
+#ifndef HVE_DICT_DB
+#define HVE_DICT_DB 1
+#endif
+
+// A batch's loads.  Every lane issues every load, so the batch is a fixed
+// count of loads and the loop waits on exact counters (a lane-masked load sits
+// behind an exec branch, and the compiler then drains every load at each
+// use).  A lane past its row end (slot k + q holds entries for lanes
+// [0, cnt) only: rows are sorted by descending length) reads the last active
+// lane's entry instead, a line the wave fetches anyway; its words are never
+// used (dict_sum selects them out).  cp and vl point at the slice's first
+// entry; P is the offset of slot k.
 template <int B, bool NT, class V>
 __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp, const V& vl, int& P, int k, int blen,
-                                          int llen, int (&c)[B], typename V::raw (&a)[B], int dexp = 0) {
+                                          int (&c)[B], typename V::raw (&a)[B], int dexp = 0) {
+  const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int q = 0; q < B; ++q) {
+    const int cnt = __popcll(__builtin_amdgcn_ballot_w64((k + q) < blen));
+#if HVE_DICT_CLAMP
+    const int e = P + min(lane, max(cnt - 1, 0));
+#else
+    const int e = P + lane;
+    if ((k + q) >= blen) {  // lane-masked loads (exec branches)
+      c[q] = -1;
+      a[q] = V::none();
+      P += cnt;
+      continue;
+    }
+#endif
+#ifdef HVE_DICT_EXP
+    // timing only: 2 leaves out the column loads, 4 the value loads
+    c[q] = (dexp & 2) ? (int)((threadIdx.x + q) & 255) : (int)mload<NT>(cp + e);
+    a[q] = (dexp & 4) ? typename V::raw(1) : vl.template load<NT>(e);
+#else
+    (void)dexp;
+    c[q] = (int)mload<NT>(cp + e);
+    a[q] = vl.template load<NT>(e);
+#endif
+    P += cnt;
+  }
+}
+
+// A batch's sums: every x (and table value) is read from LDS first, all B
+// reads in flight at once (an entry past the lane's row end, or a skipped
+// row, reads slot 0), then the products are added in stored order; those
+// entries leave t unchanged by a select, so the active entries see exactly
+// the sequential sum.
+template <int B, class V>
+__device__ __forceinline__ void dict_sum(const double* xl, const V& vl, const int (&c)[B],
+                                         const typename V::raw (&a)[B], int k, int llen, bool sub, double& t) {
+  double xv[B], av[B];
 #pragma unroll
   for (int q = 0; q < B; ++q) {
     const bool in = (k + q) < llen;
-#ifdef HVE_DICT_EXP
-    // timing only: 2 leaves out the column loads, 4 the value loads
-    c[q] = in ? ((dexp & 2) ? (int)((threadIdx.x + q) & 255) : (int)mload<NT>(cp + P)) : -1;
-    a[q] = in ? ((dexp & 4) ? typename V::raw(1) : vl.template load<NT>(P)) : V::none();
-#else
-    (void)dexp;
-    c[q] = in ? (int)mload<NT>(cp + P) : -1;
-    a[q] = in ? vl.template load<NT>(P) : V::none();
-#endif
-    P += __popcll(__ballot((k + q) < blen));
+    xv[q] = xl[in ? c[q] : 0];
+    av[q] = vl.value((sizeof(typename V::raw) == 8 || in) ? a[q] : V::none());  // a table index must be valid
+  }
+#pragma unroll
+  for (int q = 0; q < B; ++q) {
+    const double pr = av[q] * xv[q];
+    const double tn = sub ? t - pr : t + pr;
+    t = (k + q) < llen ? tn : t;
   }
 }
 
@@ -1408,20 +1518,20 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
     t = row_init<OP, NT>(p, g);
     if (!skip) pre = row_preload<OP, NT>(p, g);
   }
-  const V vl = V::make(p, vt, beg + lane);
+  const V vl = V::make(p, vt, beg);
   typename V::raw draw = V::none();  // diagonal stored first; its value is read after the table is staged
   if (own && OP == OP_JAC) {
     uo = p.x[g];
-    if (blen > 0) draw = vl.template load<false>(0);
+    if (blen > 0) draw = vl.template load<false>(lane);
   }
   const int llen = skip ? 0 : blen;
   const int k0 = (OP == OP_JAC) ? 1 : 0;
-  const unsigned short* __restrict__ cp = p.col16 + beg + lane;
+  const unsigned short* __restrict__ cp = p.col16 + beg;
   int P = 0;
   for (int k = 0; k < k0; ++k) P += __popcll(__ballot(k < blen));
   int c[B];
   typename V::raw a[B];
-  dict_load<B, NT>(cp, vl, P, k0, blen, llen, c, a, p.dexp);
+  dict_load<B, NT>(cp, vl, P, k0, blen, c, a, p.dexp);
   // 1. x-tile -> LDS, TG loads in flight per thread
   constexpr int TG = HVE_DICT_TG;
   constexpr int NT_ = 64 * G;
@@ -1489,22 +1599,32 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   __syncthreads();
   if (!wave_live) return;
   if (OP == OP_JAC && own) d = blen > 0 ? vl.value(draw) : 0.0;
-  // 2. jagged row loop over local columns
-  for (int k = k0; k < width; k += B) {
-    int cn[B];
-    typename V::raw an[B];
-    dict_load<B, NT>(cp, vl, P, k + B, blen, llen, cn, an, p.dexp);
-#pragma unroll
-    for (int q = 0; q < B; ++q) {
-      if (c[q] >= 0) {
-        const double pr = vl.value(a[q]) * xl[c[q]];
-        if (sub) t -= pr;
-        else t += pr;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < B; ++q) { c[q] = cn[q]; a[q] = an[q]; }
+  // 2. jagged row loop over local columns, two register sets in turn (no
+  // copies between batches, so a batch's loads stay in flight while the other
+  // set is summed); the sums read x from LDS branch-free (dict_sum)
+  int c2[B];
+  typename V::raw a2[B];
+  // (the empty asm keeps each batch's loads ahead of the other set's sums:
+  // without it the compiler sinks them past the exit test, next to their use)
+#if HVE_DICT_DB
+  for (int k = k0; k < width; k += 2 * B) {
+    dict_load<B, NT>(cp, vl, P, k + B, blen, c2, a2, p.dexp);
+    asm volatile("" ::: "memory");
+    dict_sum<B>(xl, vl, c, a, k, llen, sub, t);
+    if (k + B >= width) break;
+    dict_load<B, NT>(cp, vl, P, k + 2 * B, blen, c, a, p.dexp);
+    asm volatile("" ::: "memory");
+    dict_sum<B>(xl, vl, c2, a2, k + B, llen, sub, t);
   }
+#else
+  for (int k = k0; k < width; k += B) {
+    dict_load<B, NT>(cp, vl, P, k + B, blen, c2, a2, p.dexp);
+    asm volatile("" ::: "memory");
+    dict_sum<B>(xl, vl, c, a, k, llen, sub, t);
+#pragma unroll
+    for (int q = 0; q < B; ++q) { c[q] = c2[q]; a[q] = a2[q]; }
+  }
+#endif
   if (own) row_store_pre<OP, NT>(p, g, skip, t, uo, d, pre);
 }
 

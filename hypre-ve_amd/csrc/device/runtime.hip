@@ -29,7 +29,9 @@ template <typename T>
 static T* dalloc(size_t n) {
   T* p = nullptr;
   if (n == 0) n = 1;
-  HVE_HIP(hipMalloc((void**)&p, n * sizeof(T)));
+  // 256 B of slack past the end: the dictionary loop's clamped loads may read
+  // one element past a stream's last slice (the value is never used)
+  HVE_HIP(hipMalloc((void**)&p, n * sizeof(T) + 256));
   return p;
 }
 template <typename T>
