@@ -356,6 +356,10 @@ void build_modext_interp(const CSR& A, const std::vector<int>& cf, const Pattern
 void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                                 int max_elmts, bool pe, CSR& P, const std::vector<int>* emul = nullptr,
                                 int mm_square = -1);
+// partial ext+i / ext (agg_interp_type 1, 6 / 3): rows = the first stage's C
+// points, columns = the second's; resets markers below -1 to -1
+void build_partial_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                                int max_elmts, bool plus_i, CSR& P);
 void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P, int mm_square = -1);
 void build_multipass_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                             int max_elmts, CSR& P);

@@ -1429,6 +1429,59 @@ void build_modpartialext_interp(const CSR& A, const std::vector<int>& cf, const 
   if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
 }
 
+// Second stage of the classical 2-stage aggressive interpolations:
+// agg_interp_type 1 / 6 (partial.c:16 hypre_BoomerAMGBuildPartialExtPIInterp)
+// and 3 (partial.c:1855 hypre_BoomerAMGBuildPartialExtInterp, plus_i false).
+// Rows are the first stage's C points in order (cf 1: the identity to the
+// second stage's C point, cf -2: an interpolated row), columns the second
+// stage's C points.  An interpolated row is extpi_row_fill's over the combined
+// marker: C neighbours are cf >= 0, strong F neighbours any other point but
+// an SF one (-3), the weight loop the same (partial.c:590-700 / :2360-2430).
+// Truncated with the P12 parameters inside (partial.c:797 / :2552); then
+// every marker below -1 becomes -1 (partial.c:818 / :2573).
+void build_partial_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S, double trunc_factor,
+                                int max_elmts, bool plus_i, CSR& P) {
+  const int n = A.nrows;
+  std::vector<int> fine_to_coarse(n, -1), old;
+  int nc = 0;
+  for (int i = 0; i < n; ++i) {
+    if (cf[i] == 1) fine_to_coarse[i] = nc++;
+    if (cf[i] == 1 || cf[i] == -2) old.push_back(i);
+  }
+  const int no = (int)old.size();
+  CSR Pf;  // fine-row indexed: only the first stage's C points hold entries
+  Pf.resize_rows(n, nc);
+  std::vector<int> rowcnt(n, 0);
+#pragma omp parallel
+  {
+    RowMap M;
+#pragma omp for schedule(static)
+    for (int k = 0; k < no; ++k) rowcnt[old[k]] = extpi_row_count(S, cf, old[k], M);
+  }
+  for (int i = 0; i < n; ++i) Pf.i[i + 1] = Pf.i[i] + rowcnt[i];
+  Pf.j.assign(Pf.i[n], 0);
+  Pf.a.assign(Pf.i[n], 0.0);
+#pragma omp parallel
+  {
+    RowMap M;
+#pragma omp for schedule(static)
+    for (int k = 0; k < no; ++k) extpi_row_fill(A, S, cf, fine_to_coarse, old[k], M, Pf, plus_i);
+  }
+  P.resize_rows(no, nc);
+  for (int k = 0; k < no; ++k) P.i[k + 1] = P.i[k] + rowcnt[old[k]];
+  P.j.assign(P.i[no], 0);
+  P.a.assign(P.i[no], 0.0);
+#pragma omp parallel for schedule(static)
+  for (int k = 0; k < no; ++k) {
+    const int i = old[k];
+    std::copy(Pf.j.begin() + Pf.i[i], Pf.j.begin() + Pf.i[i + 1], P.j.begin() + P.i[k]);
+    std::copy(Pf.a.begin() + Pf.i[i], Pf.a.begin() + Pf.i[i + 1], P.a.begin() + P.i[k]);
+  }
+  if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+  for (int& v : cf)
+    if (v < -1) v = -1;
+}
+
 // P = P1 P2 (par_amg_setup.c:1681 hypre_ParMatmul), then the aggressive
 // truncation (:1685)
 void multiply_interp(const CSR& P1, const CSR& P2, double trunc_factor, int max_elmts, CSR& P, int mm_square) {
@@ -2123,9 +2176,11 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
-  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4 && prm.agg_interp_type != 5 && prm.agg_interp_type != 7)
-    throw std::runtime_error("aggressive coarsening: agg_interp_type " + std::to_string(prm.agg_interp_type) +
-                             " is not available in this build (4 multipass, 5 / 7 2-stage extended / ext+e MM)");
+  const int at = prm.agg_interp_type;
+  if (prm.agg_num_levels > 0 && at != 1 && at != 3 && at != 4 && at != 5 && at != 6 && at != 7)
+    throw std::runtime_error("aggressive coarsening: agg_interp_type " + std::to_string(at) +
+                             " is not available in this build (1 / 3 2-stage extended+i / extended, 4 multipass,"
+                             " 5 / 6 / 7 2-stage extended / ext+i / ext+e MM)");
   if (prm.num_paths < 1) throw std::runtime_error("num_paths must be >= 1");
   int coarsen_type = prm.coarsen_type;
   H.lev.emplace_back();
@@ -2204,6 +2259,12 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         correct_cf_marker(cf, cfn);  // agg_interp_type 4: par_amg_setup.c:1590
       } else {
         cf1 = cf;  // the first stage's markers, for P1
+        // P1 of types 1 / 3 (the classical ext+i / ext builders) turns the SF
+        // markers into F ones before the markers are combined
+        // (par_lr_interp.c:1890 / :5414, then par_amg_setup.c:1600)
+        if (at == 1 || at == 3)
+          for (int& v : cf)
+            if (v == SF_PT) v = F_PT;
         correct_cf_marker2(cf, cfn);  // par_amg_setup.c:1600 (par_strength.c:2978)
       }
     }
@@ -2222,10 +2283,22 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       // 2-stage: P1 to the first stage's C points, P2 from them to the
       // second's (par_amg_setup.c:1575-1689)
       CSR P1, P2;
-      const bool pe = prm.agg_interp_type == 7;
+      const bool pe = at == 7;
+      // P1 (par_amg_setup.c:1553-1596): 1 ext+i, 3 ext, 5 MM ext, 6 MM ext+i,
+      // 7 MM ext+e; P2 (:1620-1672): 1 / 6 partial ext+i, 3 partial ext,
+      // 5 / 7 the MM partial forms
+      auto stage1 = [&](double tf, int mx, const std::vector<int>* em) {
+        if (at == 1 || at == 3) build_extpi_interp(L.A, cf1, S, tf, mx, P1, at == 1);
+        else if (at == 6) build_modextpi_interp(L.A, cf1, S, tf, mx, P1, em);
+        else build_modext_interp(L.A, cf1, S, tf, mx, pe, P1, em);
+      };
+      auto stage2 = [&](double tf, int mx, const std::vector<int>* em) {
+        if (at == 1 || at == 3 || at == 6) build_partial_extpi_interp(L.A, cf, S, tf, mx, at != 3, P2);
+        else build_modpartialext_interp(L.A, cf, S, tf, mx, pe, P2, em);
+      };
       if (emul.empty()) {
-        build_modext_interp(L.A, cf1, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P1);
-        build_modpartialext_interp(L.A, cf, S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P2);
+        stage1(prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, nullptr);
+        stage2(prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, nullptr);
         multiply_interp(P1, P2, prm.agg_trunc_factor, prm.agg_P_max_elmts, P);
       } else {
         // emulated ranks: every product in hypre_ParMatmul's np > 1 order and
@@ -2243,9 +2316,9 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
           if (tf != 0.0 || mx > 0) truncate_rows(M, tf, mx);
           rank_order_rows(M, rs, cs);
         };
-        build_modext_interp(L.A, cf1, S, 0.0, 0, pe, P1, &emul);
+        stage1(0.0, 0, &emul);
         trunc(P1, emul, cs1, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts);
-        build_modpartialext_interp(L.A, cf, S, 0.0, 0, pe, P2, &emul);
+        stage2(0.0, 0, &emul);
         trunc(P2, cs1, cs2, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts);
         MatmulRanks rk;
         rk.nranks = (int)emul.size() - 1;

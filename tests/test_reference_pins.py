@@ -26,6 +26,15 @@ agg_interp_type 5 / 7 with interp_type 18 (agg_interp.out.14/15/19).
 agg_interp.out.20 (10 aggressive levels of type 7, agg_P12_mx 4) reaches the
 saved 11 iterations but a final residual of 1.647026e-09 against 1.654514e-09:
 test_agg_interp_out20_band keeps it as a band until that is found.
+Round 5 adds the classical 2-stage interpolations agg_interp_type 1 (ext+i,
+then partial ext+i, partial.c:16) and 3 (ext, then partial ext, partial.c:1855):
+agg_interp.out.1/3/5/7/9 match every printed digit (1 and 10 aggressive
+levels, agg_Pmx 4, agg_tr 0.3 / agg_P12_tr 0.2, agg_P12_mx 3).  Type 6 (MM
+ext+i, then partial ext+i) reaches agg_interp.out.16's 9 iterations with
+5.533979e-09 against 6.146679e-09 (test_agg_interp_out16_band).  The two open
+cases share one thing no exact case has: agg_P12_mx truncating a first stage
+built in matrix-matrix form (types 6 / 7), so the entry order that truncation's
+tie-breaking sees there is the suspect.
 """
 import json
 import os
@@ -140,3 +149,18 @@ def test_agg_interp_out20_band(hv, orc):
     it, rr = orc.OracleAMG(amg).pcg(b, np.zeros(A.n), 1e-8, 1000, 1)
     assert it == 11
     assert abs(rr - 1.654514e-09) < 0.01 * 1.654514e-09
+
+
+def test_agg_interp_out16_band(hv, orc):
+    """agg_interp.out.16 (mpirun -np 8 ./ij -rhsrand -n 30 29 31 -P 2 2 2
+    -agg_nl 1 -agg_interp 6 -agg_Pmx 4 -agg_P12_mx 4 -solver 1 -rlx 6):
+    saved 9 iterations, 6.146679e-09; not yet digit-exact (module docstring)."""
+    base = next(c for c in CASES if c["name"] == "agg_interp.out.4")
+    case = dict(base)
+    case["settings"] = {"agg_num_levels": 1, "agg_interp_type": 6, "agg_P_max_elmts": 4, "agg_P12_max_elmts": 4,
+                        "relax_type": 6}
+    A, amg, b, _ = build(hv, case)
+    amg.setup_host(A)
+    it, rr = orc.OracleAMG(amg).pcg(b, np.zeros(A.n), 1e-8, 1000, 1)
+    assert it == 9
+    assert abs(rr - 6.146679e-09) < 0.15 * 6.146679e-09
