@@ -712,10 +712,11 @@ AMG_SET(ChebyEigEst, cheby_eig_est, HYPRE_Int)
 // par_amg.c SetRelaxWt / SetOuterWt overwrite every level's weight;
 // SetLevelRelaxWt / SetLevelOuterWt (par_amg.c:2368) set one level.  A
 // negative weight -k asks for the CG estimate with at most k steps at Setup
-// (par_cg_relax_wt.c); 0 (the scaled-norm weight of relax 0/7) is not restated.
+// (par_cg_relax_wt.c); a relax weight of 0 asks for 4/3 over the scaled norm
+// of the level's matrix at Setup (par_amg_setup.c:3184); an outer weight of 0
+// is not restated.
 HYPRE_Int HYPRE_BoomerAMGSetRelaxWt(HYPRE_Solver s, HYPRE_Real w) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  if (!(w != 0.0)) return set_err(HYPRE_ERROR_ARG, "relax weight 0 (scaled-norm weight) is not available");
   s->prm.relax_weight = w;
   s->prm.lev_relax_wt_set = 0;
   return 0;
@@ -730,7 +731,6 @@ HYPRE_Int HYPRE_BoomerAMGSetOuterWt(HYPRE_Solver s, HYPRE_Real w) {
 HYPRE_Int HYPRE_BoomerAMGSetLevelRelaxWt(HYPRE_Solver s, HYPRE_Real w, HYPRE_Int level) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(level >= 0 && level < AMGParams::kWeightLevels && level < s->prm.max_levels, 3);
-  if (!(w != 0.0)) return set_err(HYPRE_ERROR_ARG, "relax weight 0 (scaled-norm weight) is not available");
   s->prm.lev_relax_wt[level] = w;
   s->prm.lev_relax_wt_set |= (uint64_t)1 << level;
   return 0;

@@ -2512,6 +2512,26 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       prm.lev_outer_wt_set |= (uint64_t)1 << j;
     }
   }
+  // par_amg_setup.c:3184: a relax weight of 0 on level j becomes 4/3 over the
+  // scaled norm max_i sum_j |a_ij| d_i d_j, d = 1/sqrt(|a_ii|)
+  // (par_scaled_matnorm.c:21; each row summed in stored order, diagonal part
+  // first, then the max over all rows); a zero norm leaves the weight 0
+  for (int j = 0; j < nl; ++j) {
+    if (prm.wt(j) != 0.0) continue;
+    if (j >= AMGParams::kWeightLevels) throw std::runtime_error("relax weight 0 beyond level 63");
+    const CSR& M = H.lev[j].A;
+    std::vector<double> dis(M.nrows);
+    for (int i = 0; i < M.nrows; ++i) dis[i] = 1.0 / sqrt(fabs(M.a[M.i[i]]));
+    double mx = 0.0;
+#pragma omp parallel for reduction(max : mx) schedule(static)
+    for (int i = 0; i < M.nrows; ++i) {
+      double sum = 0.0;
+      for (int q = M.i[i]; q < M.i[i + 1]; ++q) sum += fabs(M.a[q]) * dis[i] * dis[M.j[q]];
+      if (mx < sum) mx = sum;
+    }
+    prm.lev_relax_wt[j] = mx != 0.0 ? 4.0 / 3.0 / mx : 0.0;
+    prm.lev_relax_wt_set |= (uint64_t)1 << j;
+  }
   // coarsest-level direct solve
   if (nl > 1 && (prm.relax_type[3] == 9 || prm.relax_type[3] == 99 || prm.relax_type[3] == 19 ||
                  prm.relax_type[3] == 98)) {

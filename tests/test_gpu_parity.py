@@ -61,12 +61,13 @@ def test_single_cycle_bitwise(gpu, orc, n3, relax, coarsen):
 
 
 @pytest.mark.parametrize("relax,coarsen,wt", [(18, 8, 1.0), (0, 8, 1.0), (18, 10, 1.0), (7, 10, 1.0),
-                                              (18, 8, 0.8), (7, 8, 1.0)])
+                                              (18, 8, 0.8), (7, 8, 1.0), (0, 8, 0.0), (18, 10, 0.0)])
 def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen, wt):
     """relax_order 1 (C points, then F points on the way down; F then C up).
     relax 18: hypre_ParCSRRelax_L1_Jacobi per point class with the C/F-restricted
     l1 norms (par_cycle.c:398-415, par_relax_more.c:991); relax 7: two full
     sweeps (RelaxIF, par_relax.c:3463 ignores relax_points); relax 0: C/F Jacobi.
+    wt 0: every level's weight is 4/3 over its scaled norm (par_amg_setup.c:3184).
     The oracle's C/F sweep is itself checked against the formula in
     tests/test_oracle_relax.py.  Control: the same hierarchy with relax_order 0
     gives different bits, so the C/F path is really taken."""

@@ -387,3 +387,29 @@ def test_distributed_chebyshev_matches_one_process(hv, size, coarsen, order, sca
     amg.set(coarsen_type=coarsen, interp_type=6, relax_type=16, P_max_elmts=4, cheby_order=order,
             cheby_scale=scale, cheby_variant=variant, cheby_eig_est=eig)
     amg.dist_setup_check(A, size)
+
+
+@pytest.mark.parametrize("relax", [0, 18])
+def test_scaled_norm_relax_weight(hv, relax):
+    """relax_wt 0 (par_amg_setup.c:3184): every level's weight is 4/3 over
+    max_i sum_j |a_ij| / sqrt(|a_ii|) / sqrt(|a_jj|) (par_scaled_matnorm.c:21,
+    each row summed in stored order), recomputed here entry by entry."""
+    A = hv.ParCSRMatrix.laplacian(14, 12, 10, cx=0.3)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, relax_type=relax, relax_wt=0.0)
+    amg = hv.BoomerAMG(**kw)
+    amg.setup_host(A)
+    for l in range(amg.num_levels()):
+        ip, jj, vv, (nr, _) = amg.level_matrix(l, 0)
+        ip, jj, vv = np.asarray(ip), np.asarray(jj), np.asarray(vv)
+        dis = 1.0 / np.sqrt(np.abs(vv[ip[:-1]]))
+        mx = 0.0
+        for i in range(nr):
+            s = 0.0
+            for q in range(ip[i], ip[i + 1]):
+                s += abs(vv[q]) * dis[i] * dis[jj[q]]
+            mx = max(mx, s)
+        w, _ = amg.level_weights(l)
+        assert w == 4.0 / 3.0 / mx
+    amg.destroy()
+    A.destroy()
