@@ -195,7 +195,8 @@ struct AMGParams {
   int coarsen_type = 10;          // 8 PMIS, 9 PMIS(seq rand), 10 HMIS
   int measure_type = 0;
   int coarsen_cut_factor = 0;
-  int interp_type = 6;            // 6 ext+i, 14 ext, 16/17/18 ext / ext+i / ext+e (MM), 3 direct
+  int interp_type = 6;            // 6 ext+i, 14 ext, 16/17/18 ext / ext+i / ext+e (MM), 3 direct, 8 standard
+  int sep_weight = 0;             // standard interpolation: separate factors for positive / negative weights
   int P_max_elmts = 4;
   double trunc_factor = 0.0;
   // grid_relax_type (par_amg.c:218-220, 339-341: [0] keeps the 3 of the
@@ -332,6 +333,9 @@ void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_fact
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P, bool plus_i = true);
 // extended+i in matrix-matrix form (interp_type 17, par_mod_lr_interp.c:474)
+// standard interpolation (interp_type 8; 9 = 8 with sep_weight 1); rs: emulated rank starts
+void build_std_interp(const CSR& A, std::vector<int>& cf, const Pattern& S, double trunc_factor, int max_elmts,
+                      int sep_weight, CSR& P, const std::vector<int>* rs = nullptr, bool partial = false);
 void build_modextpi_interp(const CSR& A, const std::vector<int>& cf, const Pattern& S, double trunc_factor,
                            int max_elmts, CSR& P, const std::vector<int>* emul = nullptr, int mm_square = -1);
 // extended+e in matrix-matrix form (interp_type 18, par_mod_lr_interp.c:1040)

@@ -919,6 +919,207 @@ void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, 
   }
 }
 
+// Standard interpolation (interp_type 8, 9 = 8 with sep_weight 1;
+// par_lr_interp.c:22 hypre_BoomerAMGBuildStdInterp, weight loop :600-910).
+// The interpolatory set and its order are ext+i's (extpi_row_fill's first
+// half).  The row of A is then "hatted": every strong F neighbour i1 is
+// eliminated through its own equation (a_{i,i1} / a_{i1,i1} times row i1
+// subtracted), the others added as they stand; each point met gets a slot in
+// order of discovery (C-hat points: C slots; i itself first among the F
+// slots; any other point an F slot, weak SF neighbours of i left out).  With
+// sep_weight 0, alfa = (sum of all slots but the diagonal) / (sum of the C
+// slots) / diagonal and w_ij = -alfa * ahat_j; with 1, positive and negative
+// slots get their own factor (beta, alfa).  Under rank emulation the slots
+// of other-rank points are summed after the own ones (the reference's
+// ahat_offd), each group in discovery order.  A row whose factor cannot be
+// formed (sum_C * diagonal == 0) keeps the previous row's, as the reference's
+// function-scope alfa / beta do (per rank).  Rows of SF points stay empty;
+// SF markers become F after (par_lr_interp.c:996).
+namespace {
+struct StdRow {  // one row's pre-scale data
+  double alfa = 0, beta = 0;
+  bool has_a = false, has_b = false;
+};
+}
+void build_std_interp(const CSR& A, std::vector<int>& cf, const Pattern& S, double trunc_factor, int max_elmts,
+                      int sep_weight, CSR& P, const std::vector<int>* rs, bool partial) {
+  const int n = A.nrows;
+  std::vector<int> f2c(n, -1);
+  int nc = 0;
+  for (int i = 0; i < n; ++i)
+    if (partial ? cf[i] == 1 : cf[i] >= 0) f2c[i] = nc++;
+  // the rows built: every point, or (partial) the first stage's C points
+  auto built = [&](int i) { return !partial || cf[i] == 1 || cf[i] == -2; };
+  auto rank_of = [&](int p) -> int {
+    if (!rs) return 0;
+    return (int)(std::upper_bound(rs->begin(), rs->end(), p) - rs->begin()) - 1;
+  };
+  P.resize_rows(n, nc);
+  std::vector<int> rowcnt(n, 0);
+#pragma omp parallel
+  {
+    RowMap M;
+#pragma omp for schedule(static)
+    for (int i = 0; i < n; ++i) rowcnt[i] = built(i) ? extpi_row_count(S, cf, i, M) : 0;
+  }
+  for (int i = 0; i < n; ++i) P.i[i + 1] = P.i[i] + rowcnt[i];
+  P.j.assign(P.i[n], 0);
+  P.a.assign(P.i[n], 0.0);
+  std::vector<StdRow> rw(n);
+  std::vector<int> pt(P.i[n], 0);  // interpolatory points (fine indices) of each row, in order
+#pragma omp parallel
+  {
+    RowMap M, H;
+    std::vector<int> spt;      // slot -> point
+    std::vector<double> sv;    // slot values
+    std::vector<char> sc, so;  // slot is a C-hat point / an own-rank point
+#pragma omp for schedule(dynamic, 64)
+    for (int i = 0; i < n; ++i) {
+      if (!built(i)) continue;
+      const int jb = P.i[i];
+      if (cf[i] >= 0) {
+        pt[jb] = i;
+        P.a[jb] = 1.0;
+        continue;
+      }
+      if (cf[i] == SF_PT) continue;
+      constexpr int kNone = -1, kStrongF = -2;
+      M.begin(extpi_bound(S, i));
+      int jc = jb;
+      bool fresh;
+      for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+        const int i1 = S.j[jj];
+        if (cf[i1] >= 0) {
+          M.find_or_insert(i1, jc, &fresh);
+          if (fresh) pt[jc++] = i1;
+        } else if (cf[i1] != SF_PT) {
+          *M.find_or_insert(i1, kStrongF, &fresh) = kStrongF;
+          for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+            const int k1 = S.j[kk];
+            if (cf[k1] >= 0) {
+              M.find_or_insert(k1, jc, &fresh);
+              if (fresh) pt[jc++] = k1;
+            }
+          }
+        }
+      }
+      // the hatted row
+      int64_t hb = 1 + (A.i[i + 1] - A.i[i]);
+      for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) hb += A.i[A.j[jj] + 1] - A.i[A.j[jj]];
+      H.begin(hb);
+      spt.clear(); sv.clear(); sc.clear(); so.clear();
+      const int ri = rank_of(i);
+      auto slot = [&](int p, bool isc) -> int {
+        int* v = H.find_or_insert(p, (int)spt.size(), &fresh);
+        if (fresh) {
+          spt.push_back(p);
+          sv.push_back(0.0);
+          sc.push_back(isc ? 1 : 0);
+          so.push_back(rank_of(p) == ri ? 1 : 0);
+        }
+        return *v;
+      };
+      const int dslot = slot(i, false);
+      sv[dslot] = A.a[A.i[i]];
+      for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
+        const int i1 = A.j[jj];
+        const int m1 = M.get(i1, kNone);
+        if (m1 != kStrongF) {
+          const int h = H.get(i1, -1);
+          if (h >= 0) sv[h] += A.a[jj];
+          else if (m1 >= 0) { const int q = slot(i1, true); sv[q] += A.a[jj]; }
+          else if (cf[i1] != SF_PT) { const int q = slot(i1, false); sv[q] += A.a[jj]; }
+        } else {
+          const double distribute = A.a[jj] / A.a[A.i[i1]];
+          for (int kk = A.i[i1] + 1; kk < A.i[i1 + 1]; ++kk) {
+            const int k1 = A.j[kk];
+            int h = H.get(k1, -1);
+            if (h < 0) h = slot(k1, M.get(k1, kNone) >= 0);
+            sv[h] -= A.a[kk] * distribute;
+          }
+        }
+      }
+      const double diagonal = sv[dslot];
+      StdRow& r = rw[i];
+      if (sep_weight == 1) {
+        double spc = 0, snc = 0;
+        for (int pass = 1; pass >= 0; --pass)  // own-rank slots, then the others
+          for (size_t q = 0; q < spt.size(); ++q)
+            if (sc[q] && so[q] == pass) {
+              if (sv[q] > 0) spc += sv[q];
+              else snc += sv[q];
+            }
+        double sp = spc, sn = snc;
+        for (int pass = 1; pass >= 0; --pass)
+          for (size_t q = 0; q < spt.size(); ++q)
+            if (!sc[q] && so[q] == pass && (int)q != dslot) {
+              if (sv[q] > 0) sp += sv[q];
+              else sn += sv[q];
+            }
+        if (snc * diagonal != 0) { r.alfa = sn / snc / diagonal; r.has_a = true; }
+        if (spc * diagonal != 0) { r.beta = sp / spc / diagonal; r.has_b = true; }
+      } else {
+        double sum_c = 0;
+        for (int pass = 1; pass >= 0; --pass)
+          for (size_t q = 0; q < spt.size(); ++q)
+            if (sc[q] && so[q] == pass) sum_c += sv[q];
+        double sum = sum_c;
+        for (int pass = 1; pass >= 0; --pass)
+          for (size_t q = 0; q < spt.size(); ++q)
+            if (!sc[q] && so[q] == pass && (int)q != dslot) sum += sv[q];
+        if (sum_c * diagonal != 0) { r.alfa = sum / sum_c / diagonal; r.has_a = true; }
+      }
+      for (int jj = jb; jj < jc; ++jj) P.a[jj] = sv[H.get(pt[jj], -1)];  // ahat, scaled below
+    }
+  }
+  // the factors carried from row to row (per rank, in row order), then the weights
+  {
+    const int nr = rs ? (int)rs->size() - 1 : 1;
+    for (int k = 0; k < nr; ++k) {
+      const int r0 = rs ? (*rs)[k] : 0, r1 = rs ? (*rs)[k + 1] : n;
+      double alfa = 1.0, beta = 1.0;
+      for (int i = r0; i < r1; ++i) {
+        if (!built(i) || cf[i] >= 0 || cf[i] == SF_PT) continue;
+        if (rw[i].has_a) alfa = rw[i].alfa;
+        if (rw[i].has_b) beta = rw[i].beta;
+        rw[i].alfa = alfa;
+        rw[i].beta = beta;
+      }
+    }
+  }
+#pragma omp parallel for schedule(static)
+  for (int i = 0; i < n; ++i) {
+    for (int jj = P.i[i]; jj < P.i[i + 1]; ++jj) {
+      if (cf[i] < 0) {
+        const double ah = P.a[jj];
+        P.a[jj] = (sep_weight == 1 && ah > 0) ? -rw[i].beta * ah : -rw[i].alfa * ah;
+      }
+      P.j[jj] = f2c[pt[jj]];
+    }
+  }
+  if (partial) {  // rows of the first stage's C points only, in order
+    CSR Pc;
+    std::vector<int> old;
+    for (int i = 0; i < n; ++i)
+      if (built(i)) old.push_back(i);
+    const int no = (int)old.size();
+    Pc.resize_rows(no, nc);
+    for (int k = 0; k < no; ++k) Pc.i[k + 1] = Pc.i[k] + rowcnt[old[k]];
+    Pc.j.assign(Pc.i[no], 0);
+    Pc.a.assign(Pc.i[no], 0.0);
+#pragma omp parallel for schedule(static)
+    for (int k = 0; k < no; ++k) {
+      const int i = old[k];
+      std::copy(P.j.begin() + P.i[i], P.j.begin() + P.i[i + 1], Pc.j.begin() + Pc.i[k]);
+      std::copy(P.a.begin() + P.i[i], P.a.begin() + P.i[i + 1], Pc.a.begin() + Pc.i[k]);
+    }
+    P = std::move(Pc);
+  }
+  if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+  for (int& v : cf)  // par_lr_interp.c:996; the partial form: partial.c:1812
+    if (partial ? v < -1 : v == SF_PT) v = F_PT;
+}
+
 // Row lists for the device setup's host fallback and its table bounds
 // (OpenMP here; setup_dev.hip is compiled without it).
 int64_t extpi_bound_max(const Pattern& S) {
@@ -2176,11 +2377,16 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
+  // par_amg_setup.c:319: interp_type 9 is standard interpolation with separated weights
+  if (prm.interp_type == 9) {
+    prm.interp_type = 8;
+    prm.sep_weight = 1;
+  }
   const int at = prm.agg_interp_type;
-  if (prm.agg_num_levels > 0 && at != 1 && at != 3 && at != 4 && at != 5 && at != 6 && at != 7)
+  if (prm.agg_num_levels > 0 && (at < 1 || at > 7))
     throw std::runtime_error("aggressive coarsening: agg_interp_type " + std::to_string(at) +
-                             " is not available in this build (1 / 3 2-stage extended+i / extended, 4 multipass,"
-                             " 5 / 6 / 7 2-stage extended / ext+i / ext+e MM)");
+                             " is not available in this build (1 / 2 / 3 2-stage extended+i / standard / extended,"
+                             " 4 multipass, 5 / 6 / 7 2-stage extended / ext+i / ext+e MM)");
   if (prm.num_paths < 1) throw std::runtime_error("num_paths must be >= 1");
   int coarsen_type = prm.coarsen_type;
   H.lev.emplace_back();
@@ -2191,7 +2397,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   if (rank_starts && rank_starts->size() > 2) {
     emul = *rank_starts;
     if (emul.front() != 0 || emul.back() != A0.nrows) throw std::runtime_error("rank emulation: row starts do not cover A");
-    if (prm.interp_type != 6 && prm.interp_type != 14 && (prm.interp_type < 16 || prm.interp_type > 18))
+    if (prm.interp_type != 6 && prm.interp_type != 8 && prm.interp_type != 14 &&
+        (prm.interp_type < 16 || prm.interp_type > 18))
       throw std::runtime_error("rank emulation: interp_type " + std::to_string(prm.interp_type) + " is not restated");
     rank_order_rows(H.lev[0].A, emul, emul);
   }
@@ -2262,7 +2469,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         // P1 of types 1 / 3 (the classical ext+i / ext builders) turns the SF
         // markers into F ones before the markers are combined
         // (par_lr_interp.c:1890 / :5414, then par_amg_setup.c:1600)
-        if (at == 1 || at == 3)
+        if (at == 1 || at == 2 || at == 3)
           for (int& v : cf)
             if (v == SF_PT) v = F_PT;
         correct_cf_marker2(cf, cfn);  // par_amg_setup.c:1600 (par_strength.c:2978)
@@ -2289,11 +2496,13 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       // 5 / 7 the MM partial forms
       auto stage1 = [&](double tf, int mx, const std::vector<int>* em) {
         if (at == 1 || at == 3) build_extpi_interp(L.A, cf1, S, tf, mx, P1, at == 1);
+        else if (at == 2) build_std_interp(L.A, cf1, S, tf, mx, 0, P1, em);  // sep_weight 0 here (par_amg_setup.c:1562)
         else if (at == 6) build_modextpi_interp(L.A, cf1, S, tf, mx, P1, em);
         else build_modext_interp(L.A, cf1, S, tf, mx, pe, P1, em);
       };
       auto stage2 = [&](double tf, int mx, const std::vector<int>* em) {
         if (at == 1 || at == 3 || at == 6) build_partial_extpi_interp(L.A, cf, S, tf, mx, at != 3, P2);
+        else if (at == 2) build_std_interp(L.A, cf, S, tf, mx, prm.sep_weight, P2, em, true);
         else build_modpartialext_interp(L.A, cf, S, tf, mx, pe, P2, em);
       };
       if (emul.empty()) {
@@ -2341,7 +2550,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         rank_order_rows(P, emul, cs);
       }
     }
-    else if ((prm.interp_type == 6 || prm.interp_type == 14 || (prm.interp_type >= 16 && prm.interp_type <= 18)) &&
+    else if ((prm.interp_type == 6 || prm.interp_type == 8 || prm.interp_type == 14 ||
+              (prm.interp_type >= 16 && prm.interp_type <= 18)) &&
              !emul.empty()) {
       // par_csr_matrix.c:2671 truncates the row [P_diag | P_offd] and splits
       // the kept entries back into the two parts in their sorted order
@@ -2354,6 +2564,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       if (prm.interp_type == 16) build_modext_interp(L.A, cf, S, 0.0, 0, false, P, &emul);
       else if (prm.interp_type == 17) build_modextpi_interp(L.A, cf, S, 0.0, 0, P, &emul);
       else if (prm.interp_type == 18) build_modextpe_interp(L.A, cf, S, 0.0, 0, P, &emul);
+      else if (prm.interp_type == 8) build_std_interp(L.A, cf, S, 0.0, 0, prm.sep_weight, P, &emul);
       else build_extpi_interp(L.A, cf, S, 0.0, 0, P, prm.interp_type == 6);
       rank_order_rows(P, emul, cs);
       if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
@@ -2379,6 +2590,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       build_modext_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, false, P);
     else if (prm.interp_type == 14) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P, false);
     else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
+    else if (prm.interp_type == 8) build_std_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, prm.sep_weight, P);
     else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));
     double t3 = now();
     t_i += t3 - t2;

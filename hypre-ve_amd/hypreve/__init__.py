@@ -124,6 +124,7 @@ SIGNATURES = [
     ("HYPRE_BoomerAMGSetAggPMaxElmts", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetAggP12MaxElmts", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetInterpType", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetSepWeight", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetTruncFactor", _i, [_p, _d]),
     ("HYPRE_BoomerAMGSetPMaxElmts", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetCycleType", _i, [_p, _i]),
@@ -406,6 +407,7 @@ class BoomerAMG:
         "max_row_sum": ("HYPRE_BoomerAMGSetMaxRowSum", float),
         "coarsen_type": ("HYPRE_BoomerAMGSetCoarsenType", int),
         "interp_type": ("HYPRE_BoomerAMGSetInterpType", int),
+        "sep_weight": ("HYPRE_BoomerAMGSetSepWeight", int),
         "trunc_factor": ("HYPRE_BoomerAMGSetTruncFactor", float),
         "P_max_elmts": ("HYPRE_BoomerAMGSetPMaxElmts", int),
         "cycle_type": ("HYPRE_BoomerAMGSetCycleType", int),

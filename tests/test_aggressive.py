@@ -96,6 +96,6 @@ def test_multipass_structure(hv, orc):
 def test_unsupported_agg_interp_refused(hv):
     A = hv.ParCSRMatrix.laplacian(10, 10, 10)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
-    amg.set(agg_num_levels=1, agg_interp_type=2)  # 2-stage standard: not restated
+    amg.set(agg_num_levels=1, agg_interp_type=8)  # not a reference type
     with pytest.raises(hv.HypreError):
         amg.setup_host(A)

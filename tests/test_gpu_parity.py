@@ -374,14 +374,15 @@ def test_aggressive_coarsening_bitwise(gpu, orc, agg, coarsen, relax, coef):
 
 
 @pytest.mark.parametrize("interp,agg,agg_interp", [(14, 0, 4), (16, 0, 4), (17, 0, 4), (18, 0, 4), (6, 1, 5), (6, 2, 5), (18, 1, 5), (6, 1, 7),
-                                                     (6, 1, 1), (6, 2, 3), (6, 1, 6)])
+                                                     (6, 1, 1), (6, 2, 3), (6, 1, 6), (8, 0, 4), (6, 1, 2)])
 @pytest.mark.parametrize("order", [0, 1])
 def test_interp_types_bitwise(gpu, orc, interp, agg, agg_interp, order):
     """Extended (14), ext / ext+i / ext+e MM (16 / 17 / 18) and the 2-stage extended / ext+e MM
     aggressive interpolations (agg_interp_type 5 / 7, whose levels keep -2
     markers that C/F relaxation skips), and the classical 2-stage ext+i / ext
-    and MM ext+i ones (agg_interp_type 1 / 3 / 6, partial.c): one V-cycle and a
-    solve equal the oracle's bits."""
+    and MM ext+i ones (agg_interp_type 1 / 3 / 6, partial.c), standard
+    interpolation (8) and its 2-stage form (agg_interp_type 2): one V-cycle and
+    a solve equal the oracle's bits."""
     hv = gpu
     A = hv.ParCSRMatrix.laplacian(28, 26, 24, cx=0.01)
     kw = hv.ij_amg_defaults(0)

@@ -35,6 +35,10 @@ ext+i, then partial ext+i) reaches agg_interp.out.16's 9 iterations with
 cases share one thing no exact case has: agg_P12_mx truncating a first stage
 built in matrix-matrix form (types 6 / 7), so the entry order that truncation's
 tie-breaking sees there is the suspect.
+Standard interpolation (interp_type 8, par_lr_interp.c:22) matches
+interp.out.2 (Pmx 0) in every printed digit; interp.out.5 (Pmx 4) has both
+complexities exact and the convergence factor 0.203484 against 0.203482
+(test_interp_out5_band).
 """
 import json
 import os
@@ -164,3 +168,18 @@ def test_agg_interp_out16_band(hv, orc):
     it, rr = orc.OracleAMG(amg).pcg(b, np.zeros(A.n), 1e-8, 1000, 1)
     assert it == 9
     assert abs(rr - 6.146679e-09) < 0.15 * 6.146679e-09
+
+
+def test_interp_out5_band(hv, orc):
+    """interp.out.5 (mpirun -np 4 ./ij -rhsrand -n 15 15 10 -P 2 2 1
+    -interptype 8): complexities to every printed digit, convergence factor
+    within 1e-5 of the saved 0.203482 (module docstring)."""
+    base = next(c for c in CASES if c["name"] == "interp.out.2")
+    case = dict(base)
+    case["settings"] = {"interp_type": 8}
+    A, amg, b, _ = build(hv, case)
+    amg.setup_host(A)
+    g, o, _ = amg.complexities()
+    assert f"{g:f}" == "1.582667" and f"{o:f}" == "2.662245"
+    st = orc.OracleAMG(amg).solve(b, np.zeros(A.n), 1e-8, 100)
+    assert abs(st["conv_factor"] - 0.203482) < 1e-5
