@@ -698,6 +698,8 @@ AMG_SET(AggP12MaxElmts, agg_P12_max_elmts, HYPRE_Int)
 AMG_SET(NumPaths, num_paths, HYPRE_Int)
 AMG_SET(InterpType, interp_type, HYPRE_Int)
 AMG_SET(SepWeight, sep_weight, HYPRE_Int)
+AMG_SET(SeqThreshold, seq_threshold, HYPRE_Int)
+AMG_SET(Redundant, redundant, HYPRE_Int)
 AMG_SET(TruncFactor, trunc_factor, HYPRE_Real)
 AMG_SET(PMaxElmts, P_max_elmts, HYPRE_Int)
 AMG_SET(CycleType, cycle_type, HYPRE_Int)

@@ -257,6 +257,12 @@ struct AMGParams {
   // agg_num_levels levels coarsen twice (second pass on S*S + 2S over the C
   // points, num_paths paths needed) and interpolate with agg_interp_type 4
   // (multipass), truncated by agg_trunc_factor / agg_P_max_elmts.
+  // Redundant coarse-grid AMG (par_amg_setup.c:2880-2897, gen_redcs_mat.c:18):
+  // with more than one process the hierarchy stops at seq_threshold global
+  // rows and a one-process BoomerAMG on that level does the coarse solve
+  // (one V-cycle); redundant: every process solves it (same numbers)
+  int seq_threshold = 0;
+  int redundant = 0;
   int agg_num_levels = 0;
   int agg_interp_type = 4;
   double agg_trunc_factor = 0.0;
@@ -304,6 +310,10 @@ struct Hierarchy {
   std::vector<double> coarse_dense;
   double grid_complexity = 0, operator_complexity = 0;
   std::string log;
+  // first level of a redundant coarse-grid AMG (seq_threshold under rank
+  // emulation, gen_redcs_mat.c): from here on one process's hierarchy, whose
+  // levels every rank holds whole; -1: none
+  int seq_level = -1;
 };
 
 // ---- generators (parcsr_ls/par_laplace.c:15, par_laplace_27pt.c) ----

@@ -100,7 +100,9 @@ static std::vector<std::vector<int>> level_starts(const Hierarchy& H, const std:
 static int hierarchy_agg_level(const Hierarchy& H, int size) {
   std::vector<int64_t> grows(H.lev.size());
   for (size_t l = 0; l < H.lev.size(); ++l) grows[l] = H.lev[l].A.nrows;
-  return agglomeration_level(H.prm, grows, size);
+  int a = agglomeration_level(H.prm, grows, size);
+  if (H.seq_level >= 0 && (a < 0 || H.seq_level < a)) a = H.seq_level;  // a redundant coarse-grid AMG
+  return a;
 }
 
 static bool uses_hybrid_gs(const AMGParams& prm) {

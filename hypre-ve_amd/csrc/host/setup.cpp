@@ -2640,7 +2640,74 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       // par_amg_setup.c:2858 switches to CLJP; not available in this build.
       throw std::runtime_error("slow coarsening (coarse >= 0.75 fine) would switch to CLJP: unsupported");
     }
-    if (level == prm.max_levels - 1 || coarse_size <= prm.max_coarse_size) finished = true;
+    // par_amg_setup.c:2880: the redundant coarse grid's threshold stops the
+    // coarsening too (num_procs > 1 only: par_amg_setup.c:294)
+    const int max_thresh = std::max(prm.max_coarse_size, rs ? prm.seq_threshold : 0);
+    if (level == prm.max_levels - 1 || coarse_size <= max_thresh) finished = true;
+  }
+  // par_amg_setup.c:2893: the redundant coarse-grid AMG (gen_redcs_mat.c:18
+  // hypre_seqAMGSetup): a one-process BoomerAMG on the last level, created with
+  // the defaults plus the parameters hypre_seqAMGSetup copies, whose single
+  // V-cycle (max_iter 1, tol 0, from the zero coarse-level guess) is the
+  // coarse solve.  That cycle is the combined hierarchy's V-cycle below the
+  // level, so its levels are appended; from the level on every rank holds the
+  // rows whole and relaxes them in one process's blocks.
+  if (rs && prm.seq_threshold > 0 && prm.seq_threshold >= prm.max_coarse_size &&
+      H.lev.back().A.nrows > prm.max_coarse_size && level != prm.max_levels - 1) {
+    AMGParams sub;  // HYPRE_BoomerAMGCreate defaults
+    sub.max_row_sum = prm.max_row_sum;
+    sub.strong_threshold = prm.strong_threshold;
+    sub.coarsen_type = prm.coarsen_type;
+    sub.interp_type = prm.interp_type;
+    sub.sep_weight = prm.sep_weight;
+    sub.trunc_factor = prm.trunc_factor;
+    sub.P_max_elmts = prm.P_max_elmts;
+    if (prm.user_relax_type > -1) {  // HYPRE_BoomerAMGSetRelaxType (par_amg.c:2100)
+      for (int c = 0; c < 3; ++c) sub.relax_type[c] = prm.user_relax_type;
+      sub.relax_type[3] = 9;
+      sub.user_relax_type = prm.user_relax_type;
+    }
+    sub.relax_order = prm.relax_order;
+    sub.relax_weight = prm.relax_weight;
+    for (int c = 0; c < 4; ++c) sub.num_sweeps[c] = prm.num_sweeps[c];
+    sub.num_blocks = prm.num_blocks;
+    sub.auto_block_rows = prm.auto_block_rows;
+    sub.auto_block_min = prm.auto_block_min;
+    sub.max_iter = 1;
+    sub.tol = 0.0;
+    // the combined cycle relaxes every level alike: refuse what would differ
+    for (int c = 0; c < 4; ++c)
+      if (sub.relax_type[c] != prm.relax_type[c] || sub.num_sweeps[c] != prm.num_sweeps[c])
+        throw std::runtime_error("seq_threshold: the coarse-grid AMG would relax otherwise than the hierarchy "
+                                 "(set the relax type with SetRelaxType)");
+    if (prm.lev_relax_wt_set || prm.lev_outer_wt_set || prm.outer_weight != 1.0)
+      throw std::runtime_error("seq_threshold with per-level or outer weights");
+    Hierarchy Hs;
+    const int Lq = (int)H.lev.size() - 1;
+    amg_setup(H.lev[Lq].A, sub, Hs, nullptr, nullptr);
+    if (Hs.lev.size() > 1) {
+      Level& Lv = H.lev[Lq];
+      Lv.cf.swap(Hs.lev[0].cf);
+      Lv.P.swap(Hs.lev[0].P);
+      Lv.R.swap(Hs.lev[0].R);
+      for (size_t k = 1; k < Hs.lev.size(); ++k) {
+        H.lev.emplace_back();
+        Level& D = H.lev.back();
+        D.A.swap(Hs.lev[k].A);
+        D.P.swap(Hs.lev[k].P);
+        D.R.swap(Hs.lev[k].R);
+        D.cf.swap(Hs.lev[k].cf);
+      }
+      H.seq_level = Lq;
+      for (int l = Lq; l < (int)H.lev.size(); ++l) {
+        const std::vector<int> one = {0, H.lev[l].A.nrows};
+        if (l < (int)lev_starts.size()) lev_starts[l] = one;
+        else lev_starts.push_back(one);
+      }
+      snprintf(buf, sizeof buf, "seq_threshold: a one-process coarse-grid AMG from level %d (%d rows): %d levels\n", Lq,
+               H.lev[Lq].A.nrows, (int)Hs.lev.size());
+      H.log += buf;
+    }
   }
   double rss_c, rss_p;
   host_rss_gb(&rss_c, &rss_p);
@@ -2756,7 +2823,8 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   H.log += buf;
   if (prm.print_level > 0) fputs(H.log.c_str(), stderr);
   double tot_rows = 0, tot_nnz = 0;
-  for (auto& L : H.lev) { tot_rows += L.A.nrows; tot_nnz += (double)L.A.nnz(); }
+  const int ncx = H.seq_level >= 0 ? H.seq_level + 1 : (int)H.lev.size();  // the outer AMG's levels
+  for (int l = 0; l < ncx; ++l) { tot_rows += H.lev[l].A.nrows; tot_nnz += (double)H.lev[l].A.nnz(); }
   H.grid_complexity = tot_rows / H.lev[0].A.nrows;
   H.operator_complexity = tot_nnz / (double)H.lev[0].A.nnz();
   return 0;

@@ -125,6 +125,8 @@ SIGNATURES = [
     ("HYPRE_BoomerAMGSetAggP12MaxElmts", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetInterpType", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetSepWeight", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetSeqThreshold", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetRedundant", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetTruncFactor", _i, [_p, _d]),
     ("HYPRE_BoomerAMGSetPMaxElmts", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetCycleType", _i, [_p, _i]),
@@ -408,6 +410,8 @@ class BoomerAMG:
         "coarsen_type": ("HYPRE_BoomerAMGSetCoarsenType", int),
         "interp_type": ("HYPRE_BoomerAMGSetInterpType", int),
         "sep_weight": ("HYPRE_BoomerAMGSetSepWeight", int),
+        "seq_threshold": ("HYPRE_BoomerAMGSetSeqThreshold", int),
+        "redundant": ("HYPRE_BoomerAMGSetRedundant", int),
         "trunc_factor": ("HYPRE_BoomerAMGSetTruncFactor", float),
         "P_max_elmts": ("HYPRE_BoomerAMGSetPMaxElmts", int),
         "cycle_type": ("HYPRE_BoomerAMGSetCycleType", int),

@@ -160,6 +160,11 @@ HYPRE_Int HYPRE_BoomerAMGSetAggP12MaxElmts(HYPRE_Solver solver, HYPRE_Int agg_P1
 /* interp_type 6 ext+i, 14 ext, 16 / 17 / 18 ext / ext+i / ext+e (matrix-matrix form), 3 direct */
 HYPRE_Int HYPRE_BoomerAMGSetInterpType(HYPRE_Solver solver, HYPRE_Int interp_type); /* :442 */
 HYPRE_Int HYPRE_BoomerAMGSetSepWeight(HYPRE_Solver solver, HYPRE_Int sep_weight); /* :464 (standard interpolation) */
+/* :667 / :673: redundant coarse-grid AMG below seq_threshold global rows; it
+ * acts only with more than one rank, as in the reference (par_amg_setup.c:294):
+ * under hypreve_BoomerAMGSetRankEmulation; the distributed setup gathers for it */
+HYPRE_Int HYPRE_BoomerAMGSetSeqThreshold(HYPRE_Solver solver, HYPRE_Int seq_threshold);
+HYPRE_Int HYPRE_BoomerAMGSetRedundant(HYPRE_Solver solver, HYPRE_Int redundant);
 HYPRE_Int HYPRE_BoomerAMGSetTruncFactor(HYPRE_Solver solver, HYPRE_Real trunc_factor); /* :448 */
 HYPRE_Int HYPRE_BoomerAMGSetPMaxElmts(HYPRE_Solver solver, HYPRE_Int P_max_elmts); /* :455 */
 HYPRE_Int HYPRE_BoomerAMGSetCycleType(HYPRE_Solver solver, HYPRE_Int cycle_type); /* :572 */

@@ -35,6 +35,10 @@ ext+i, then partial ext+i) reaches agg_interp.out.16's 9 iterations with
 cases share one thing no exact case has: agg_P12_mx truncating a first stage
 built in matrix-matrix form (types 6 / 7), so the entry order that truncation's
 tie-breaking sees there is the suspect.
+The redundant coarse-grid AMG (seq_threshold, par_amg_setup.c:2880-2897,
+gen_redcs_mat.c:18) reproduces solvers.out.105/106 (80^3 on 8 ranks, a
+one-process BoomerAMG below 100 rows) to every printed digit;
+test_seq_threshold_has_teeth shows the number moves without it.
 Standard interpolation (interp_type 8, par_lr_interp.c:22) matches
 interp.out.2 (Pmx 0) in every printed digit; interp.out.5 (Pmx 4) has both
 complexities exact and the convergence factor 0.203484 against 0.203482
@@ -183,3 +187,14 @@ def test_interp_out5_band(hv, orc):
     assert f"{g:f}" == "1.582667" and f"{o:f}" == "2.662245"
     st = orc.OracleAMG(amg).solve(b, np.zeros(A.n), 1e-8, 100)
     assert abs(st["conv_factor"] - 0.203482) < 1e-5
+
+
+def test_seq_threshold_has_teeth(hv, orc):
+    """Without seq_threshold the same 8-rank run ends at 3.104551e-09, not the
+    saved 3.104258e-09: the pin depends on the redundant coarse-grid AMG."""
+    case = dict(next(c for c in CASES if c["name"] == "solvers.out.105"))
+    case["settings"] = {k: v for k, v in case["settings"].items() if k != "seq_threshold"}
+    A, amg, b, _ = build(hv, case)
+    amg.setup_host(A)
+    it, rr = orc.OracleAMG(amg).pcg(b, np.zeros(A.n), 1e-8, 1000, 1)
+    assert f"{rr:e}" != "3.104258e-09"
