@@ -699,6 +699,7 @@ AMG_SET(NumPaths, num_paths, HYPRE_Int)
 AMG_SET(InterpType, interp_type, HYPRE_Int)
 AMG_SET(SepWeight, sep_weight, HYPRE_Int)
 AMG_SET(SeqThreshold, seq_threshold, HYPRE_Int)
+AMG_SET(NumFunctions, num_functions, HYPRE_Int)
 AMG_SET(Redundant, redundant, HYPRE_Int)
 AMG_SET(TruncFactor, trunc_factor, HYPRE_Real)
 AMG_SET(PMaxElmts, P_max_elmts, HYPRE_Int)

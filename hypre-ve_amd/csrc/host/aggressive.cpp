@@ -234,7 +234,7 @@ void build_multipass_interp(const CSR& A, const std::vector<int>& cf, const Patt
     int c = Pi[i1];
     for (int k = A.i[i1] + 1; k < A.i[i1 + 1]; ++k) {
       const int j1 = A.j[k];
-      if (cf[j1] != -3) sum_N += A.a[k];
+      if (cf[j1] != -3 && (!hve_setup_dof || hve_setup_dof[i1] == hve_setup_dof[j1])) sum_N += A.a[k];
       if (j1 != -1 && tmp_marker[j1] == i1) {
         P.a[c] = A.a[k];
         P.j[c++] = fine_to_coarse[j1];
@@ -273,7 +273,7 @@ void build_multipass_interp(const CSR& A, const std::vector<int>& cf, const Patt
             sum_N += alfa;
           }
         } else {
-          if (cf[j1] != -3) sum_N += A.a[k];
+          if (cf[j1] != -3 && (!hve_setup_dof || hve_setup_dof[i1] == hve_setup_dof[j1])) sum_N += A.a[k];
         }
       }
       const double diagonal = A.a[A.i[i1]];

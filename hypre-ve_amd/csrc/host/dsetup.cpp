@@ -1149,6 +1149,7 @@ bool dist_setup_supported(const AMGParams& prm, std::string* why) {
     return no("interp_type not 6, 14, 16, 17 or 18");
   if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4 && prm.agg_interp_type != 5 && prm.agg_interp_type != 7)
     return no("aggressive coarsening with agg_interp_type not 4, 5 or 7");
+  if (prm.num_functions > 1) return no("num_functions > 1 (systems AMG is set up in one process)");
   if (prm.seq_threshold > 0) return no("seq_threshold (the redundant coarse-grid AMG is set up in one process)");
   for (int j = 0; j < std::min(prm.max_levels, (int)AMGParams::kWeightLevels); ++j)
     if (prm.wt(j) == 0.0) return no("relax weight 0 (the scaled-norm weight of the one-process setup)");

@@ -261,6 +261,7 @@ struct AMGParams {
   // with more than one process the hierarchy stops at seq_threshold global
   // rows and a one-process BoomerAMG on that level does the coarse solve
   // (one V-cycle); redundant: every process solves it (same numbers)
+  int num_functions = 1;          // systems AMG: functions per point, interleaved (dof = row % num_functions)
   int seq_threshold = 0;
   int redundant = 0;
   int agg_num_levels = 0;
@@ -329,6 +330,12 @@ void generate_laplacian_7pt_block(int nx, int ny, int nz, int P, int Q, int R, i
 
 // ---- setup building blocks ----
 void create_strength(const CSR& A, double thr, double max_row_sum, Pattern& S);
+// Systems AMG ("unknown" approach, num_functions > 1, nodal 0): the function
+// of every row of the level being set up (dof_func_array[level]), read by the
+// strength, ext(+i), partial ext(+i) and multipass builders; null for one
+// function.  Set by amg_setup for the duration of a level (not re-entrant
+// across threads; the setup runs one hierarchy at a time).
+extern const int* hve_setup_dof;
 // rs (optional): emulate the coarsening of an N-rank run, rank r owning rows
 // [rs[r], rs[r+1]) (per-rank random streams and first passes, hypre's
 // CF_marker_offd semantics).
@@ -433,8 +440,10 @@ int l1_option_for_level(const AMGParams& prm, int j, int nl, bool* cf_restricted
 // owning the C points of its rows on the next level; nothing else changes
 // (entry order, interpolation, RAP stay the one-process ones).  This is what
 // the distributed setup computes (dsetup.cpp hmis_dist); PMIS ignores it.
+// dof0 (num_functions > 1): the level-0 functions when given (the redundant
+// coarse grid's gathered ones), else row % num_functions.
 int amg_setup(const CSR& A, const AMGParams& prm, Hierarchy& H, const std::vector<int>* rank_starts = nullptr,
-              const std::vector<int>* coarsen_starts = nullptr);
+              const std::vector<int>* coarsen_starts = nullptr, const std::vector<int>* dof0 = nullptr);
 
 
 }  // namespace hve

@@ -253,7 +253,47 @@ double hypre_rand_at(int64_t k, int seed) {
 // num_functions == 1, no offd part.  The first stored entry of each row is
 // the diagonal and is never in S.
 // ---------------------------------------------------------------------------
+const int* hve_setup_dof = nullptr;
+
+// num_functions > 1 (par_strength.c:254-294, :347-396): the row's scale and
+// sum take the entries of its own function only, and only those can be strong
 void create_strength(const CSR& A, double thr, double max_row_sum, Pattern& S) {
+  const int* dof = hve_setup_dof;
+  if (dof) {
+    const int n = A.nrows;
+    S.n = n;
+    S.i.assign(n + 1, 0);
+    std::vector<unsigned char> keep(A.nnz(), 0);
+    std::vector<int> cnt(n, 0);
+#pragma omp parallel for schedule(static)
+    for (int r = 0; r < n; ++r) {
+      const int b = A.i[r], e = A.i[r + 1];
+      const double diag = A.a[b];
+      double row_scale = 0.0, row_sum = diag;
+      for (int k = b + 1; k < e; ++k) {
+        if (dof[r] != dof[A.j[k]]) continue;
+        row_scale = diag < 0 ? std::max(row_scale, A.a[k]) : std::min(row_scale, A.a[k]);
+        row_sum += A.a[k];
+      }
+      int c = 0;
+      if (!((std::fabs(row_sum) > std::fabs(diag) * max_row_sum) && (max_row_sum < 1.0))) {
+        for (int k = b + 1; k < e; ++k) {
+          if (dof[r] != dof[A.j[k]]) continue;
+          if (diag < 0 ? !(A.a[k] <= thr * row_scale) : !(A.a[k] >= thr * row_scale)) { keep[k] = 1; ++c; }
+        }
+      }
+      cnt[r] = c;
+    }
+    for (int r = 0; r < n; ++r) S.i[r + 1] = S.i[r] + cnt[r];
+    S.j.resize(S.i[n]);
+#pragma omp parallel for schedule(static)
+    for (int r = 0; r < n; ++r) {
+      int o = S.i[r];
+      for (int k = A.i[r] + 1; k < A.i[r + 1]; ++k)
+        if (keep[k]) S.j[o++] = A.j[k];
+    }
+    return;
+  }
   const int n = A.nrows;
   S.n = n;
   S.i.assign(n + 1, 0);
@@ -910,8 +950,8 @@ void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, 
       } else {
         diagonal += A.a[jj];
       }
-    } else if (cf[i1] != SF_PT) {
-      diagonal += A.a[jj];
+    } else if (cf[i1] != SF_PT && (!hve_setup_dof || hve_setup_dof[i] == hve_setup_dof[i1])) {
+      diagonal += A.a[jj];  // a weak neighbour of another function is dropped (par_lr_interp.c:1727)
     }
   }
   if (diagonal) {
@@ -2373,7 +2413,7 @@ static void rank_order_rows(CSR& M, const std::vector<int>& rs, const std::vecto
 }
 
 int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::vector<int>* rank_starts,
-              const std::vector<int>* coarsen_starts) {
+              const std::vector<int>* coarsen_starts, const std::vector<int>* dof0) {
   H = Hierarchy();
   H.prm = prm_in;
   AMGParams& prm = H.prm;
@@ -2383,6 +2423,30 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     prm.sep_weight = 1;
   }
   const int at = prm.agg_interp_type;
+  // systems AMG, unknown approach (par_amg_setup.c:668-689: function j of the
+  // interleaved unknowns, dof = global row % num_functions; coarse levels keep
+  // the functions of their C points, par_coarse_parms.c)
+  std::vector<int> dof;
+  struct DofGuard {
+    const int* saved = hve_setup_dof;
+    ~DofGuard() { hve_setup_dof = saved; }
+  } dof_guard;
+  hve_setup_dof = nullptr;
+  if (prm.num_functions > 1) {
+    if (prm.interp_type != 6 && prm.interp_type != 14)
+      throw std::runtime_error("num_functions > 1: interp_type " + std::to_string(prm.interp_type) +
+                               " is not restated for systems (6, 14)");
+    if (prm.agg_num_levels > 0 && at != 1 && at != 3 && at != 4)
+      throw std::runtime_error("num_functions > 1: agg_interp_type " + std::to_string(at) +
+                               " is not restated for systems (1, 3, 4)");
+    if (dof0) {
+      if ((int)dof0->size() != A0.nrows) throw std::runtime_error("dof_func: one function per row");
+      dof = *dof0;
+    } else {
+      dof.resize(A0.nrows);
+      for (int i = 0; i < A0.nrows; ++i) dof[i] = i % prm.num_functions;
+    }
+  }
   if (prm.agg_num_levels > 0 && (at < 1 || at > 7))
     throw std::runtime_error("aggressive coarsening: agg_interp_type " + std::to_string(at) +
                              " is not available in this build (1 / 2 / 3 2-stage extended+i / standard / extended,"
@@ -2422,6 +2486,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     const int fine_size = L.A.nrows;
     Pattern S;
     double t0 = now();
+    hve_setup_dof = dof.empty() ? nullptr : dof.data();
     create_strength(L.A, prm.strong_threshold, prm.max_row_sum, S);
     double t1 = now();
     t_s += t1 - t0;
@@ -2570,7 +2635,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
       rank_order_rows(P, emul, cs);
     }
-    else if (prm.interp_type == 6 && prm.device_setup) {
+    else if (prm.interp_type == 6 && prm.device_setup && dof.empty()) {
       std::vector<int> f2c(cf.size(), -1);
       int nc = 0;
       for (size_t i = 0; i < cf.size(); ++i)
@@ -2629,6 +2694,13 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       for (size_t i = 0; i < L.cf.size(); ++i) pref[i + 1] = pref[i] + (L.cf[i] == 1);
       for (int& v : crs) v = pref[v];
     }
+    if (!dof.empty()) {  // the next level's functions: those of the C points, in order
+      std::vector<int> cdof;
+      cdof.reserve(coarse_size);
+      for (size_t i = 0; i < L.cf.size(); ++i)
+        if (L.cf[i] == 1) cdof.push_back(dof[i]);
+      dof.swap(cdof);
+    }
     H.lev.emplace_back();
     H.lev[level + 1].A.swap(Ac);
     if (!emul.empty()) {
@@ -2675,6 +2747,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     sub.auto_block_min = prm.auto_block_min;
     sub.max_iter = 1;
     sub.tol = 0.0;
+    sub.num_functions = prm.num_functions;  // and the gathered functions (gen_redcs_mat.c:212)
     // the combined cycle relaxes every level alike: refuse what would differ
     for (int c = 0; c < 4; ++c)
       if (sub.relax_type[c] != prm.relax_type[c] || sub.num_sweeps[c] != prm.num_sweeps[c])
@@ -2684,7 +2757,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       throw std::runtime_error("seq_threshold with per-level or outer weights");
     Hierarchy Hs;
     const int Lq = (int)H.lev.size() - 1;
-    amg_setup(H.lev[Lq].A, sub, Hs, nullptr, nullptr);
+    amg_setup(H.lev[Lq].A, sub, Hs, nullptr, nullptr, dof.empty() ? nullptr : &dof);
     if (Hs.lev.size() > 1) {
       Level& Lv = H.lev[Lq];
       Lv.cf.swap(Hs.lev[0].cf);

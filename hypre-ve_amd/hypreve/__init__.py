@@ -126,6 +126,7 @@ SIGNATURES = [
     ("HYPRE_BoomerAMGSetInterpType", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetSepWeight", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetSeqThreshold", _i, [_p, _i]),
+    ("HYPRE_BoomerAMGSetNumFunctions", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetRedundant", _i, [_p, _i]),
     ("HYPRE_BoomerAMGSetTruncFactor", _i, [_p, _d]),
     ("HYPRE_BoomerAMGSetPMaxElmts", _i, [_p, _i]),
@@ -411,6 +412,7 @@ class BoomerAMG:
         "interp_type": ("HYPRE_BoomerAMGSetInterpType", int),
         "sep_weight": ("HYPRE_BoomerAMGSetSepWeight", int),
         "seq_threshold": ("HYPRE_BoomerAMGSetSeqThreshold", int),
+        "num_functions": ("HYPRE_BoomerAMGSetNumFunctions", int),
         "redundant": ("HYPRE_BoomerAMGSetRedundant", int),
         "trunc_factor": ("HYPRE_BoomerAMGSetTruncFactor", float),
         "P_max_elmts": ("HYPRE_BoomerAMGSetPMaxElmts", int),

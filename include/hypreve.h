@@ -164,6 +164,10 @@ HYPRE_Int HYPRE_BoomerAMGSetSepWeight(HYPRE_Solver solver, HYPRE_Int sep_weight)
  * acts only with more than one rank, as in the reference (par_amg_setup.c:294):
  * under hypreve_BoomerAMGSetRankEmulation; the distributed setup gathers for it */
 HYPRE_Int HYPRE_BoomerAMGSetSeqThreshold(HYPRE_Solver solver, HYPRE_Int seq_threshold);
+/* :168: systems AMG, unknown approach (interleaved functions, dof = row %
+ * num_functions; strength and weak lumping within a function); with
+ * interp_type 6 / 14 and agg_interp_type 1 / 3 / 4, one-process setup */
+HYPRE_Int HYPRE_BoomerAMGSetNumFunctions(HYPRE_Solver solver, HYPRE_Int num_functions);
 HYPRE_Int HYPRE_BoomerAMGSetRedundant(HYPRE_Solver solver, HYPRE_Int redundant);
 HYPRE_Int HYPRE_BoomerAMGSetTruncFactor(HYPRE_Solver solver, HYPRE_Real trunc_factor); /* :448 */
 HYPRE_Int HYPRE_BoomerAMGSetPMaxElmts(HYPRE_Solver solver, HYPRE_Int P_max_elmts); /* :455 */

@@ -70,6 +70,63 @@ def laplacian_ranks(nx, ny, nz, P, Q, R, c=(1.0, 1.0, 1.0), pt27=False):
     return A, starts
 
 
+def sys_laplacian_ranks(nx, ny, nz, P, Q, R, nf=3, mtrx=None):
+    """(scipy CSR, level-0 rank starts) of ij -sysL nf (BuildParSysLaplacian,
+    sys_opt 0; par_laplace.c:394 GenerateSysLaplacian) on a P x Q x R process
+    grid: nf interleaved unknowns a grid point, row (point, f) holding the
+    blocks own, z-1, y-1, x-1, x+1, y+1, z+1 of nf entries each (value[k] *
+    mtrx[f][j], zeros stored), the own block's entries 0 and f swapped so the
+    diagonal comes first (par_laplace.c:846-860)."""
+    if mtrx is None:
+        mtrx = {3: [2.0, 1.0, 0.0, 1.0, 2.0, 1.0, 0.0, 1.0, 2.0]}[nf]
+    xp, yp, zp = partition(nx, P), partition(ny, Q), partition(nz, R)
+    own_x = np.searchsorted(xp, np.arange(nx), side="right") - 1
+    own_y = np.searchsorted(yp, np.arange(ny), side="right") - 1
+    own_z = np.searchsorted(zp, np.arange(nz), side="right") - 1
+    offs = {}
+    o = 0
+    for r in range(R):
+        for q in range(Q):
+            for p in range(P):
+                offs[p + P * q + P * Q * r] = o
+                o += (xp[p + 1] - xp[p]) * (yp[q + 1] - yp[q]) * (zp[r + 1] - zp[r])
+
+    def gidx(ix, iy, iz):
+        p, q, r = own_x[ix], own_y[iy], own_z[iz]
+        nxl, nyl = xp[p + 1] - xp[p], yp[q + 1] - yp[q]
+        return offs[p + P * q + P * Q * r] + (ix - xp[p]) + nxl * ((iy - yp[q]) + nyl * (iz - zp[r]))
+
+    value = [0.0, -1.0, -1.0, -1.0]
+    for dim in (nx, ny, nz):
+        if dim > 1:
+            value[0] += 2.0
+    ip, jj, vv, starts = [0], [], [], [0]
+    for rk in range(P * Q * R):
+        p, q, r = rk % P, (rk // P) % Q, rk // (P * Q)
+        for iz in range(zp[r], zp[r + 1]):
+            for iy in range(yp[q], yp[q + 1]):
+                for ix in range(xp[p], xp[p + 1]):
+                    blocks = [(gidx(ix, iy, iz), 0)]
+                    for jx, jy, jz, k in ((ix, iy, iz - 1, 3), (ix, iy - 1, iz, 2), (ix - 1, iy, iz, 1),
+                                          (ix + 1, iy, iz, 1), (ix, iy + 1, iz, 2), (ix, iy, iz + 1, 3)):
+                        if 0 <= jx < nx and 0 <= jy < ny and 0 <= jz < nz:
+                            blocks.append((gidx(jx, jy, jz), k))
+                    for f in range(nf):
+                        ent = []
+                        for g, k in blocks:
+                            for j in range(nf):
+                                ent.append((nf * g + j, value[k] * mtrx[f * nf + j]))
+                        ent[0], ent[f] = ent[f], ent[0]
+                        for col, v in ent:
+                            jj.append(col)
+                            vv.append(v)
+                        ip.append(len(jj))
+        starts.append(len(ip) - 1)
+    n = nf * nx * ny * nz
+    A = sp.csr_matrix((np.array(vv), np.array(jj, dtype=np.int32), np.array(ip, dtype=np.int32)), shape=(n, n))
+    return A, starts
+
+
 def rand_stream(n, seed):
     """n draws of hypre_Rand() after hypre_SeedRand(seed) (utilities/random.c)."""
     a, m = 16807, 2147483647

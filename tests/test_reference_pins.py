@@ -39,6 +39,13 @@ The redundant coarse-grid AMG (seq_threshold, par_amg_setup.c:2880-2897,
 gen_redcs_mat.c:18) reproduces solvers.out.105/106 (80^3 on 8 ranks, a
 one-process BoomerAMG below 100 rows) to every printed digit;
 test_seq_threshold_has_teeth shows the number moves without it.
+Systems AMG, unknown approach (-sysL 3 -nf 3: par_laplace.c:394's
+interleaved 3-function Laplacian, strength and weak lumping within a
+function, par_strength.c:254 / par_lr_interp.c:1727 / par_multi_interp.c:1229,
+coarse functions from the C points) reproduces agg_interp.out.10 (multipass,
+10 aggressive levels), agg_interp.out.11 (2-stage ext+i) and
+solvers.out.107/108 (with the redundant coarse grid) to every printed digit;
+test_systems_amg_has_teeth shows num_functions 1 gives other numbers.
 Standard interpolation (interp_type 8, par_lr_interp.c:22) matches
 interp.out.2 (Pmx 0) in every printed digit; interp.out.5 (Pmx 4) has both
 complexities exact and the convergence factor 0.203484 against 0.203482
@@ -58,8 +65,11 @@ CASES = json.load(open(os.path.join(HERE, "golden", "ij_rank_fixtures.json")))["
 
 def build(hv, case):
     prob = case["problem"]
-    A_s, starts = ij_emul.laplacian_ranks(*prob["n"], *prob["P"], c=tuple(prob.get("c", (1.0, 1.0, 1.0))),
-                                          pt27=prob["stencil"] == 27)
+    if prob.get("sysL"):
+        A_s, starts = ij_emul.sys_laplacian_ranks(*prob["n"], *prob["P"], nf=prob["sysL"])
+    else:
+        A_s, starts = ij_emul.laplacian_ranks(*prob["n"], *prob["P"], c=tuple(prob.get("c", (1.0, 1.0, 1.0))),
+                                              pt27=prob["stencil"] == 27)
     A = hv.ParCSRMatrix.from_scipy(A_s)
     kw = hv.ij_amg_defaults(0 if case["solver"] == "amg" else 1)
     kw.update(num_blocks=1)
@@ -198,3 +208,14 @@ def test_seq_threshold_has_teeth(hv, orc):
     amg.setup_host(A)
     it, rr = orc.OracleAMG(amg).pcg(b, np.zeros(A.n), 1e-8, 1000, 1)
     assert f"{rr:e}" != "3.104258e-09"
+
+
+def test_systems_amg_has_teeth(hv, orc):
+    """agg_interp.out.10's system with num_functions 1 (strength across
+    functions) ends elsewhere than the saved 22 iterations / 8.737365e-09."""
+    case = dict(next(c for c in CASES if c["name"] == "agg_interp.out.10"))
+    case["settings"] = {k: v for k, v in case["settings"].items() if k != "num_functions"}
+    A, amg, b, _ = build(hv, case)
+    amg.setup_host(A)
+    it, rr = orc.OracleAMG(amg).pcg(b, np.zeros(A.n), 1e-8, 1000, 1)
+    assert (it, f"{rr:e}") != (22, "8.737365e-09")
