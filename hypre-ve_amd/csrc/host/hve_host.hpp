@@ -350,6 +350,9 @@ void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_fact
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P, bool plus_i = true);
 // extended+i in matrix-matrix form (interp_type 17, par_mod_lr_interp.c:474)
+// extended+i where no common C point (interp_type 7)
+void build_extpicc_interp(const CSR& A, std::vector<int>& cf, const Pattern& S, double trunc_factor, int max_elmts,
+                          CSR& P);
 // standard interpolation (interp_type 8; 9 = 8 with sep_weight 1); rs: emulated rank starts
 void build_std_interp(const CSR& A, std::vector<int>& cf, const Pattern& S, double trunc_factor, int max_elmts,
                       int sep_weight, CSR& P, const std::vector<int>* rs = nullptr, bool partial = false);

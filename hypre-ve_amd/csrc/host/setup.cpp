@@ -959,6 +959,124 @@ void extpi_row_fill(const CSR& A, const Pattern& S, const std::vector<int>& cf, 
   }
 }
 
+// Extended+i where no common C point (interp_type 7; par_lr_interp.c:1932
+// hypre_BoomerAMGBuildExtPICCInterp): the interpolatory set is i's strong C
+// neighbours, then, for every strong F neighbour i1 (marker -1) that shares
+// no strong C neighbour with i, the strong C neighbours of i1; the weights
+// are ext+i's (extpi_row_fill's second half, distribution over that set).
+static void extpicc_chat(const Pattern& S, const std::vector<int>& cf, int i, RowMap& M, std::vector<int>& out) {
+  out.clear();
+  constexpr int kStrongF = -2;
+  M.begin(extpi_bound(S, i));
+  bool fresh;
+  for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {  // the C neighbours first
+    const int i1 = S.j[jj];
+    if (cf[i1] > 0) {
+      M.find_or_insert(i1, (int)out.size(), &fresh);
+      if (fresh) out.push_back(i1);
+    }
+  }
+  const int ndirect = (int)out.size();
+  for (int jj = S.i[i]; jj < S.i[i + 1]; ++jj) {
+    const int i1 = S.j[jj];
+    if (cf[i1] != -1) continue;
+    *M.find_or_insert(i1, kStrongF, &fresh) = kStrongF;
+    bool common = false;
+    for (int kk = S.i[i1]; kk < S.i[i1 + 1] && !common; ++kk) {
+      const int m = M.get(S.j[kk], -1);
+      common = m >= 0 && m < ndirect;  // a strong C neighbour of i itself
+    }
+    if (common) continue;
+    for (int kk = S.i[i1]; kk < S.i[i1 + 1]; ++kk) {
+      const int k1 = S.j[kk];
+      if (cf[k1] > 0) {
+        M.find_or_insert(k1, (int)out.size(), &fresh);
+        if (fresh) out.push_back(k1);
+      }
+    }
+  }
+}
+
+void build_extpicc_interp(const CSR& A, std::vector<int>& cf, const Pattern& S, double trunc_factor, int max_elmts,
+                          CSR& P) {
+  const int n = A.nrows;
+  std::vector<int> f2c(n, -1);
+  int nc = 0;
+  for (int i = 0; i < n; ++i)
+    if (cf[i] >= 0) f2c[i] = nc++;
+  P.resize_rows(n, nc);
+  std::vector<int> rowcnt(n, 0);
+#pragma omp parallel
+  {
+    RowMap M;
+    std::vector<int> ch;
+#pragma omp for schedule(static)
+    for (int i = 0; i < n; ++i) {
+      if (cf[i] >= 0) rowcnt[i] = 1;
+      else if (cf[i] != SF_PT) {
+        extpicc_chat(S, cf, i, M, ch);
+        rowcnt[i] = (int)ch.size();
+      }
+    }
+  }
+  for (int i = 0; i < n; ++i) P.i[i + 1] = P.i[i] + rowcnt[i];
+  P.j.assign(P.i[n], 0);
+  P.a.assign(P.i[n], 0.0);
+#pragma omp parallel
+  {
+    RowMap M;
+    std::vector<int> ch;
+#pragma omp for schedule(static)
+    for (int i = 0; i < n; ++i) {
+      const int jb = P.i[i];
+      if (cf[i] >= 0) {
+        P.j[jb] = f2c[i];
+        P.a[jb] = 1.0;
+        continue;
+      }
+      if (cf[i] == SF_PT) continue;
+      constexpr int kNone = -1, kStrongF = -2;
+      extpicc_chat(S, cf, i, M, ch);  // M: C-hat point -> index, strong F (-1) -> kStrongF
+      const int jc = jb + (int)ch.size();
+      for (int k = 0; k < (int)ch.size(); ++k) { P.j[jb + k] = f2c[ch[k]]; P.a[jb + k] = 0.0; }
+      auto pos = [&](int p) -> int { const int m = M.get(p, kNone); return m >= 0 ? jb + m : m; };
+      double diagonal = A.a[A.i[i]];
+      for (int jj = A.i[i] + 1; jj < A.i[i + 1]; ++jj) {
+        const int i1 = A.j[jj];
+        const int m1 = pos(i1);
+        if (m1 >= jb) {
+          P.a[m1] += A.a[jj];
+        } else if (m1 == kStrongF) {
+          double sum = 0.0;
+          const int sgn = A.a[A.i[i1]] < 0 ? -1 : 1;
+          for (int jj1 = A.i[i1] + 1; jj1 < A.i[i1 + 1]; ++jj1) {
+            const int i2 = A.j[jj1];
+            if ((pos(i2) >= jb || i2 == i) && (sgn * A.a[jj1]) < 0) sum += A.a[jj1];
+          }
+          if (sum != 0) {
+            const double distribute = A.a[jj] / sum;
+            for (int jj1 = A.i[i1]; jj1 < A.i[i1 + 1]; ++jj1) {
+              const int i2 = A.j[jj1];
+              const int m2 = pos(i2);
+              if (m2 >= jb && (sgn * A.a[jj1]) < 0) P.a[m2] += distribute * A.a[jj1];
+              if (i2 == i && (sgn * A.a[jj1]) < 0) diagonal += distribute * A.a[jj1];
+            }
+          } else {
+            diagonal += A.a[jj];
+          }
+        } else if (cf[i1] != SF_PT && (!hve_setup_dof || hve_setup_dof[i] == hve_setup_dof[i1])) {
+          diagonal += A.a[jj];
+        }
+      }
+      if (diagonal)
+        for (int jj = jb; jj < jc; ++jj) P.a[jj] /= -diagonal;
+    }
+  }
+  if (trunc_factor != 0.0 || max_elmts > 0) truncate_rows(P, trunc_factor, max_elmts);
+  for (int& v : cf)
+    if (v == SF_PT) v = F_PT;
+}
+
 // Standard interpolation (interp_type 8, 9 = 8 with sep_weight 1;
 // par_lr_interp.c:22 hypre_BoomerAMGBuildStdInterp, weight loop :600-910).
 // The interpolatory set and its order are ext+i's (extpi_row_fill's first
@@ -2461,7 +2579,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   if (rank_starts && rank_starts->size() > 2) {
     emul = *rank_starts;
     if (emul.front() != 0 || emul.back() != A0.nrows) throw std::runtime_error("rank emulation: row starts do not cover A");
-    if (prm.interp_type != 6 && prm.interp_type != 8 && prm.interp_type != 14 &&
+    if (prm.interp_type != 6 && prm.interp_type != 7 && prm.interp_type != 8 && prm.interp_type != 14 &&
         (prm.interp_type < 16 || prm.interp_type > 18))
       throw std::runtime_error("rank emulation: interp_type " + std::to_string(prm.interp_type) + " is not restated");
     rank_order_rows(H.lev[0].A, emul, emul);
@@ -2615,7 +2733,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
         rank_order_rows(P, emul, cs);
       }
     }
-    else if ((prm.interp_type == 6 || prm.interp_type == 8 || prm.interp_type == 14 ||
+    else if ((prm.interp_type == 6 || prm.interp_type == 7 || prm.interp_type == 8 || prm.interp_type == 14 ||
               (prm.interp_type >= 16 && prm.interp_type <= 18)) &&
              !emul.empty()) {
       // par_csr_matrix.c:2671 truncates the row [P_diag | P_offd] and splits
@@ -2630,6 +2748,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
       else if (prm.interp_type == 17) build_modextpi_interp(L.A, cf, S, 0.0, 0, P, &emul);
       else if (prm.interp_type == 18) build_modextpe_interp(L.A, cf, S, 0.0, 0, P, &emul);
       else if (prm.interp_type == 8) build_std_interp(L.A, cf, S, 0.0, 0, prm.sep_weight, P, &emul);
+      else if (prm.interp_type == 7) build_extpicc_interp(L.A, cf, S, 0.0, 0, P);
       else build_extpi_interp(L.A, cf, S, 0.0, 0, P, prm.interp_type == 6);
       rank_order_rows(P, emul, cs);
       if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
@@ -2656,6 +2775,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     else if (prm.interp_type == 14) build_extpi_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P, false);
     else if (prm.interp_type == 3) build_direct_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else if (prm.interp_type == 8) build_std_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, prm.sep_weight, P);
+    else if (prm.interp_type == 7) build_extpicc_interp(L.A, cf, S, prm.trunc_factor, prm.P_max_elmts, P);
     else throw std::runtime_error("unsupported interp_type " + std::to_string(prm.interp_type));
     double t3 = now();
     t_i += t3 - t2;

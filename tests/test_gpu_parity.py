@@ -374,7 +374,8 @@ def test_aggressive_coarsening_bitwise(gpu, orc, agg, coarsen, relax, coef):
 
 
 @pytest.mark.parametrize("interp,agg,agg_interp", [(14, 0, 4), (16, 0, 4), (17, 0, 4), (18, 0, 4), (6, 1, 5), (6, 2, 5), (18, 1, 5), (6, 1, 7),
-                                                     (6, 1, 1), (6, 2, 3), (6, 1, 6), (8, 0, 4), (6, 1, 2)])
+                                                     (6, 1, 1), (6, 2, 3), (6, 1, 6), (8, 0, 4), (6, 1, 2),
+                                                     (7, 0, 4)])
 @pytest.mark.parametrize("order", [0, 1])
 def test_interp_types_bitwise(gpu, orc, interp, agg, agg_interp, order):
     """Extended (14), ext / ext+i / ext+e MM (16 / 17 / 18) and the 2-stage extended / ext+e MM

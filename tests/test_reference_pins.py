@@ -46,6 +46,8 @@ coarse functions from the C points) reproduces agg_interp.out.10 (multipass,
 10 aggressive levels), agg_interp.out.11 (2-stage ext+i) and
 solvers.out.107/108 (with the redundant coarse grid) to every printed digit;
 test_systems_amg_has_teeth shows num_functions 1 gives other numbers.
+Extended+i where no common C point (interp_type 7, par_lr_interp.c:1932)
+matches interp.out.1/4 (Pmx 0 and 4) to every printed digit.
 Standard interpolation (interp_type 8, par_lr_interp.c:22) matches
 interp.out.2 (Pmx 0) in every printed digit; interp.out.5 (Pmx 4) has both
 complexities exact and the convergence factor 0.203484 against 0.203482
