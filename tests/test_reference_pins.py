@@ -82,7 +82,12 @@ def build(hv, case):
     kw.update(st)
     amg = hv.BoomerAMG(**kw)
     amg.set_rank_emulation(starts)
-    b = ij_emul.rhsrand(starts) if case["rhs"] == "rhsrand" else np.ones(A.n)
+    if case["rhs"] == "rhsrand":
+        b = ij_emul.rhsrand(starts)
+    elif case["rhs"] == "xisone":  # ij -xisone: b = A * ones (ij.c:629)
+        b = A_s @ np.ones(A.n)
+    else:
+        b = np.ones(A.n)
     return A, amg, b, starts
 
 
