@@ -85,6 +85,7 @@ struct hypre_Solver_struct {
   bool device_setup = true;
   std::vector<int> gs_rank_starts;  // one GPU emulating the GS blocks of an N-rank run
   std::vector<int> rank_emul;       // one process emulating a reference N-rank setup (SetRankEmulation)
+  const HYPRE_Int* dof_user = nullptr;  // SetDofFunc: the caller's array, read at Setup (hypre keeps the pointer)
   std::vector<int> coarsen_starts;  // one process coarsening HMIS as N ranks do (SetCoarsenRankStarts)
   // per level: those blocks and their l1 norms (host copies for the introspection calls)
   std::vector<std::vector<int>> gs_blocks_host;
@@ -700,6 +701,13 @@ AMG_SET(InterpType, interp_type, HYPRE_Int)
 AMG_SET(SepWeight, sep_weight, HYPRE_Int)
 AMG_SET(SeqThreshold, seq_threshold, HYPRE_Int)
 AMG_SET(NumFunctions, num_functions, HYPRE_Int)
+// HYPRE_parcsr_ls.h:176: the function of every local row; the array is read at
+// Setup (one process, or under the rank emulation: every row)
+HYPRE_Int HYPRE_BoomerAMGSetDofFunc(HYPRE_Solver s, HYPRE_Int* dof_func) {
+  CHECK_ARG(s && s->kind == KIND_AMG, 1);
+  s->dof_user = dof_func;
+  return 0;
+}
 AMG_SET(Redundant, redundant, HYPRE_Int)
 AMG_SET(TruncFactor, trunc_factor, HYPRE_Real)
 AMG_SET(PMaxElmts, P_max_elmts, HYPRE_Int)
@@ -1000,6 +1008,8 @@ static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
       }
       for (int q = 0; q < (int)all[3 * r]; ++q) G.i[starts0[r] + q + 1] = (int)(nnzoff[r] + li[q + 1]);
     }
+    if (s->dof_user && s->prm.num_functions > 1)
+      throw std::runtime_error("HYPRE_BoomerAMGSetDofFunc with more than one rank is not available");
     amg_setup(G, s->prm, s->H, nullptr, &starts0);  // HMIS per rank, as the distributed setup
     { CSR().swap(G); }  // the gathered matrix is level 0 of H now
     bufs.resize(size);
@@ -1145,11 +1155,16 @@ static void setup_dist(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
 
 static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
   if (s->rank_emul.empty()) {
-    amg_setup(A->diag, s->prm, s->H, nullptr, s->coarsen_starts.empty() ? nullptr : &s->coarsen_starts);
+    std::vector<int> dof;
+    if (s->dof_user && s->prm.num_functions > 1) dof.assign(s->dof_user, s->dof_user + A->diag.nrows);
+    amg_setup(A->diag, s->prm, s->H, nullptr, s->coarsen_starts.empty() ? nullptr : &s->coarsen_starts,
+              dof.empty() ? nullptr : &dof);
   } else {
     AMGParams prm = s->prm;
     prm.agglo_rows = 0;
-    amg_setup(A->diag, prm, s->H, &s->rank_emul);
+    std::vector<int> dof;
+    if (s->dof_user && s->prm.num_functions > 1) dof.assign(s->dof_user, s->dof_user + A->diag.nrows);
+    amg_setup(A->diag, prm, s->H, &s->rank_emul, nullptr, dof.empty() ? nullptr : &dof);
   }
   gs_rank_blocks_host(s->H, s->gs_rank_starts, s->gs_blocks_host, s->gs_l1_host);
   if (s->gs_blocks_host.empty() && s->prm.auto_block_rows > 0) {

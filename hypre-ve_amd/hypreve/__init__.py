@@ -194,6 +194,7 @@ SIGNATURES = [
     ("hypreve_BoomerAMGGetLevelLayout", _i, [_p, _i, _i, _pi]),
     ("hypreve_BoomerAMGSetGsRankStarts", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGSetRankEmulation", _i, [_p, _i, _pi]),
+    ("HYPRE_BoomerAMGSetDofFunc", _i, [_p, _pi]),
     ("hypreve_BoomerAMGSetCoarsenRankStarts", _i, [_p, _i, _pi]),
     ("hypreve_BoomerAMGGsScheduleCheck", _i, [_p, _i]),
     ("hypreve_BoomerAMGGsScheduleStats", _i, [_p, _i, _i, _i, _pi64]),
@@ -640,6 +641,16 @@ class BoomerAMG:
             return
         arr = (C.c_int * len(starts))(*[int(v) for v in starts])
         check(lib().hypreve_BoomerAMGSetGsRankStarts(self.h, len(starts) - 1, arr), "SetGsRankStarts")
+
+    def set_dof_func(self, dof):
+        """The function of every row (HYPRE_BoomerAMGSetDofFunc); the array is
+        kept alive here and read at Setup.  None clears it."""
+        if dof is None:
+            self._dof = None
+            check(lib().HYPRE_BoomerAMGSetDofFunc(self.h, None), "SetDofFunc")
+            return
+        self._dof = (C.c_int * len(dof))(*[int(v) for v in dof])
+        check(lib().HYPRE_BoomerAMGSetDofFunc(self.h, self._dof), "SetDofFunc")
 
     def set_rank_emulation(self, starts):
         """Reproduce a reference N-rank setup in one process (level-0 row starts,

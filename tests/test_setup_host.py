@@ -413,3 +413,31 @@ def test_scaled_norm_relax_weight(hv, relax):
         assert w == 4.0 / 3.0 / mx
     amg.destroy()
     A.destroy()
+
+
+def test_dof_func_matches_interleaved_default(hv):
+    """HYPRE_BoomerAMGSetDofFunc with the interleaved map (0, 1, 2, 0, ...) gives
+    the hierarchy num_functions alone builds, and another partition of the rows
+    into functions another one."""
+    import scipy.sparse as sp  # noqa: F401
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__)))
+    import ij_emul
+    A_s, _ = ij_emul.sys_laplacian_ranks(8, 7, 6, 1, 1, 1, nf=3)
+    A = hv.ParCSRMatrix.from_scipy(A_s)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, num_functions=3)
+    digests = []
+    for dof in (None, [i % 3 for i in range(A.n)], [(i // 3) % 3 for i in range(A.n)]):
+        amg = hv.BoomerAMG(**kw)
+        amg.set_dof_func(dof)
+        amg.setup_host(A)
+        h = hashlib.sha256()
+        for l in range(amg.num_levels()):
+            ip, jj, vv, _ = amg.level_matrix(l, 0)
+            h.update(np.asarray(jj).tobytes())
+            h.update(np.asarray(vv).tobytes())
+        digests.append(h.hexdigest())
+        amg.destroy()
+    assert digests[0] == digests[1]
+    assert digests[0] != digests[2]
+    A.destroy()
