@@ -2551,12 +2551,14 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   } dof_guard;
   hve_setup_dof = nullptr;
   if (prm.num_functions > 1) {
-    if (prm.interp_type != 6 && prm.interp_type != 14)
+    // the matrix-matrix builders (16-18, agg 5 / 7) take no functions: only
+    // their strength matrix is per function (par_mod_lr_interp.c, par_2s_interp.c)
+    if (prm.interp_type != 6 && prm.interp_type != 14 && (prm.interp_type < 16 || prm.interp_type > 18))
       throw std::runtime_error("num_functions > 1: interp_type " + std::to_string(prm.interp_type) +
-                               " is not restated for systems (6, 14)");
-    if (prm.agg_num_levels > 0 && at != 1 && at != 3 && at != 4)
+                               " is not restated for systems (6, 14, 16-18)");
+    if (prm.agg_num_levels > 0 && at != 1 && at != 3 && at != 4 && at != 5 && at != 7)
       throw std::runtime_error("num_functions > 1: agg_interp_type " + std::to_string(at) +
-                               " is not restated for systems (1, 3, 4)");
+                               " is not restated for systems (1, 3, 4, 5, 7)");
     if (dof0) {
       if ((int)dof0->size() != A0.nrows) throw std::runtime_error("dof_func: one function per row");
       dof = *dof0;
