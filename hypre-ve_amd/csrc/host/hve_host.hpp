@@ -341,11 +341,14 @@ extern const int* hve_setup_dof;
 // CF_marker_offd semantics).
 void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf, const std::vector<int>* rs = nullptr);
 // full_row_len (optional): strong connections of each row including those the
-// pattern omits (another rank's columns), for the empty-row test.
+// pattern omits (another rank's columns), for the empty-row test.  f_pnt: the
+// marker of measure-0 points (Z_PT under HMIS, F_PT for coarsen_type 11).
 void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, int cut_factor,
-                             std::vector<int>& cf, const int* full_row_len = nullptr);
+                             std::vector<int>& cf, const int* full_row_len = nullptr, int f_pnt = Z_PT);
 void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
                   const std::vector<int>* rs = nullptr);
+void coarsen_ruge1p(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
+                    const std::vector<int>* rs = nullptr);
 // plus_i false: extended interpolation (interp_type 14) instead of ext+i
 void build_extpi_interp(const CSR& A, std::vector<int>& cf, const Pattern& S,
                         double trunc_factor, int max_elmts, CSR& P, bool plus_i = true);

@@ -604,14 +604,15 @@ struct MeasureLists {
 };
 }  // namespace
 
-// coarsen_type 10 -> first pass only with Z_PT for measure-0 points
-// (par_coarsen.c:1082-1086, 1347-1354).
+// The first pass of par_coarsen.c:940 hypre_BoomerAMGCoarsenRuge, which is
+// all of coarsen_type 11 (:1347-1354) and HMIS's first stage (coarsen_type 10
+// -> 11 with f_pnt = Z_PT for measure-0 points, :1082-1086); coarsen_type 11
+// itself leaves f_pnt = F_PT.
 void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, int cut_factor,
-                             std::vector<int>& cf, const int* full_row_len) {
+                             std::vector<int>& cf, const int* full_row_len, int f_pnt) {
   constexpr int UNDECIDED = 0, SC_PT = 3;
   const int n = S.n;
   const bool agg_2 = (measure_type == 3 || measure_type == 4);
-  const int f_pnt = Z_PT;
   // ST = transpose of S (par_coarsen.c:1032-1057), counting sort
   std::vector<int> ST_i(n + 1, 0), ST_j(S.j.size());
   for (size_t k = 0; k < S.j.size(); ++k) ST_i[S.j[k] + 1]++;
@@ -728,6 +729,33 @@ void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, i
 // Emulated ranks (rs): every rank runs the first pass on its own rows with the
 // strong connections it owns (S_diag, local measures, measure_type 0), then
 // PMIS runs over the whole graph.
+// Emulated ranks (rs): every rank runs the Ruge first pass on its own rows
+// with the strong connections it owns (S_diag, local measures:
+// par_coarsen.c:1088 builds no S_ext for measure_type 0), counting the whole
+// row (diag and offd) for the isolated-point test.
+static void ruge_first_pass_ranks(const Pattern& S, int measure_type, int f_pnt, std::vector<int>& cf,
+                                  const std::vector<int>* rs) {
+  const int nr = (int)rs->size() - 1;
+  cf.assign(S.n, 0);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int r = 0; r < nr; ++r) {
+    const int a = (*rs)[r], b = (*rs)[r + 1];
+    Pattern Sl;
+    Sl.n = b - a;
+    Sl.i.assign(Sl.n + 1, 0);
+    std::vector<int> full(Sl.n);
+    for (int i = a; i < b; ++i) {
+      full[i - a] = S.i[i + 1] - S.i[i];
+      for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+        if (S.j[k] >= a && S.j[k] < b) Sl.j.push_back(S.j[k] - a);
+      Sl.i[i - a + 1] = (int)Sl.j.size();
+    }
+    std::vector<int> cl;
+    coarsen_ruge_first_pass(Sl, nullptr, measure_type, 0, cl, full.data(), f_pnt);
+    std::copy(cl.begin(), cl.end(), cf.begin() + a);
+  }
+}
+
 void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
                   const std::vector<int>* rs) {
   if (!rs) {
@@ -737,27 +765,23 @@ void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_fact
     // local measures: 0, or 3 (the aggressive second pass: local, agg_2)
     if (measure_type != 0 && measure_type != 3)
       throw std::runtime_error("rank emulation: HMIS needs local measures (measure_type 0 or 3)");
-    const int nr = (int)rs->size() - 1;
-    cf.assign(S.n, 0);
-#pragma omp parallel for schedule(dynamic, 1)
-    for (int r = 0; r < nr; ++r) {
-      const int a = (*rs)[r], b = (*rs)[r + 1];
-      Pattern Sl;
-      Sl.n = b - a;
-      Sl.i.assign(Sl.n + 1, 0);
-      std::vector<int> full(Sl.n);
-      for (int i = a; i < b; ++i) {
-        full[i - a] = S.i[i + 1] - S.i[i];
-        for (int k = S.i[i]; k < S.i[i + 1]; ++k)
-          if (S.j[k] >= a && S.j[k] < b) Sl.j.push_back(S.j[k] - a);
-        Sl.i[i - a + 1] = (int)Sl.j.size();
-      }
-      std::vector<int> cl;
-      coarsen_ruge_first_pass(Sl, nullptr, measure_type, 0, cl, full.data());
-      std::copy(cl.begin(), cl.end(), cf.begin() + a);
-    }
+    ruge_first_pass_ranks(S, measure_type, Z_PT, cf, rs);
   }
   coarsen_pmis(S, 1, cf, rs);
+}
+
+// coarsen_type 11 (ij -ruge1p): the Ruge first pass alone, measure-0 points F
+// (par_coarsen.c:1347).  With emulated ranks only local measures are restated
+// (measure_type 1 builds S_ext and a global first pass).
+void coarsen_ruge1p(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
+                    const std::vector<int>* rs) {
+  if (!rs) {
+    coarsen_ruge_first_pass(S, A, measure_type, cut_factor, cf, nullptr, F_PT);
+    return;
+  }
+  if (cut_factor > 0 || measure_type != 0)
+    throw std::runtime_error("rank emulation: coarsen_type 11 needs local measures and no cut factor");
+  ruge_first_pass_ranks(S, measure_type, F_PT, cf, rs);
 }
 
 // ---------------------------------------------------------------------------
@@ -2615,6 +2639,7 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     else if (coarsen_type == 9) coarsen_pmis(S, 2, cf, rs);
     else if (coarsen_type == 10)
       coarsen_hmis(S, &L.A, prm.measure_type, prm.coarsen_cut_factor, cf, rs ? rs : (crs.empty() ? nullptr : &crs));
+    else if (coarsen_type == 11) coarsen_ruge1p(S, &L.A, prm.measure_type, prm.coarsen_cut_factor, cf, rs);
     else throw std::runtime_error("unsupported coarsen_type " + std::to_string(coarsen_type));
     double t2 = now();
     t_c += t2 - t1;

@@ -78,7 +78,7 @@ def sys_laplacian_ranks(nx, ny, nz, P, Q, R, nf=3, mtrx=None):
     mtrx[f][j], zeros stored), the own block's entries 0 and f swapped so the
     diagonal comes first (par_laplace.c:846-860)."""
     if mtrx is None:
-        mtrx = {3: [2.0, 1.0, 0.0, 1.0, 2.0, 1.0, 0.0, 1.0, 2.0]}[nf]
+        mtrx = {2: [2.0, 1.0, 1.0, 2.0], 3: [2.0, 1.0, 0.0, 1.0, 2.0, 1.0, 0.0, 1.0, 2.0]}[nf]
     xp, yp, zp = partition(nx, P), partition(ny, Q), partition(nz, R)
     own_x = np.searchsorted(xp, np.arange(nx), side="right") - 1
     own_y = np.searchsorted(yp, np.arange(ny), side="right") - 1

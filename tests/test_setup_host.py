@@ -33,13 +33,13 @@ def _digest(threads, coarsen_type):
     return out.stdout.strip()
 
 
-@pytest.mark.parametrize("coarsen_type", [8, 10])
+@pytest.mark.parametrize("coarsen_type", [8, 10, 11])
 def test_setup_bitwise_independent_of_threads(coarsen_type):
     d1 = _digest(1, coarsen_type)
     assert d1 == _digest(3, coarsen_type) == _digest(8, coarsen_type)
 
 
-@pytest.mark.parametrize("coarsen_type", [8, 10])
+@pytest.mark.parametrize("coarsen_type", [8, 10, 11])
 def test_hierarchy_invariants(hv, coarsen_type):
     A = hv.ParCSRMatrix.laplacian(16, 16, 16)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
@@ -62,8 +62,9 @@ def test_hierarchy_invariants(hv, coarsen_type):
         assert np.allclose(P[c].toarray().max(axis=1), 1.0)
         assert set(np.unique(cf)) <= {1, -1, -3}
         # every F point with strong connections has a strong C neighbour
-        # (PMIS / HMIS second phase); on these M-matrices every off-diagonal
-        # entry is strong at threshold 0.25 unless the row sum test drops it
+        # (PMIS / HMIS second phase; the Ruge first pass on a symmetric S); on
+        # these M-matrices every off-diagonal entry is strong at threshold 0.25
+        # unless the row sum test drops it
         Aoff = Al.copy(); Aoff.setdiag(0); Aoff.eliminate_zeros()
         fpts = np.where(cf == -1)[0]
         hasC = (abs(Aoff[fpts]) @ (cf == 1).astype(float)) > 0
