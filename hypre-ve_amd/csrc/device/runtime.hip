@@ -1708,6 +1708,14 @@ void DevAMG::emit_cycle(const double* f0, double* u0, hipStream_t s, bool presmo
       if (relax_type == 9 || relax_type == 99 || relax_type == 19 || relax_type == 98) {
         coarse_solve(level, fl[level], ucur[level], s);
         zero[level] = 0;
+      } else if (relax_type == 17) {
+        // par_cycle.c:451 / par_relax_more.c:661 FCF-Jacobi: weighted Jacobi over
+        // the F, C, F points whatever relax_order; one full sweep on the coarsest level
+        const int pts[3] = {-1, 1, -1};
+        for (int q = 0; q < (level == nl - 1 ? 1 : 3); ++q) {
+          relax(level, 0, level == nl - 1 ? 0 : pts[q], fl[level], ucur[level], ualt[level], zero[level], s);
+          zero[level] = 0;
+        }
       } else if (relax_type == 18 && !(prm.relax_order == 1 && cycle_param < 3)) {
         relax(level, relax_type, 0, fl[level], ucur[level], ualt[level], zero[level], s);
         zero[level] = 0;

@@ -356,6 +356,15 @@ int orc_cycle(const orc_amg *amg, double **F, double **U, double *op_count) {
         /* par_cycle.c:445 scaled Chebyshev: Aux_F, Aux_U, Vtemp, Ztemp */
         err = orc_cheby(&amg->A[level], F[level], amg->cheby_ds[level], amg->cheby_coefs[level],
                         amg->cheby_order, amg->cheby_scale, U[level], vtemp, ztemp);
+      } else if (relax_type == 17) {
+        /* par_cycle.c:451 / par_relax_more.c:661 FCF-Jacobi: weighted Jacobi
+         * (relax 0) over the F, then C, then F points, whatever relax_order;
+         * one plain sweep on the coarsest level */
+        const int pts[3] = {-1, 1, -1};
+        relax_type = 0;
+        if (level == nl - 1) err = RELAX(0);
+        for (int q = 0; q < 3 && level != nl - 1 && !err; q++) err = RELAX(pts[q]);
+        relax_type = 17;
       } else if (relax_type == 18 && !(amg->relax_order == 1 && cycle_param < 3)) {
         err = RELAX(0);
       } else {

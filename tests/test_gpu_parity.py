@@ -43,10 +43,11 @@ def test_fixture_default_on_gpu(gpu, orc, relax):
 
 
 @pytest.mark.parametrize("n3,relax,coarsen", [((24, 20, 16), 18, 8), ((17, 13, 11), 0, 8), ((33, 33, 33), 18, 8),
-                                              ((24, 20, 16), 18, 10), ((31, 29, 27), 0, 10), ((23, 19, 17), 18, 11)])
+                                              ((24, 20, 16), 18, 10), ((31, 29, 27), 0, 10), ((23, 19, 17), 18, 11),
+                                              ((22, 18, 15), 17, 8)])
 def test_single_cycle_bitwise(gpu, orc, n3, relax, coarsen):
     """One V-cycle from a random iterate; coarsen 10 = HMIS (test/ij.c default),
-    11 = the Ruge first pass alone (ij -ruge1p)."""
+    11 = the Ruge first pass alone (ij -ruge1p); relax 17 = FCF-Jacobi."""
     hv = gpu
     A, amg, O = setup_pair(hv, orc, n3, coarsen_type=coarsen, relax_type=relax)
     n = A.n

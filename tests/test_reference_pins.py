@@ -49,7 +49,8 @@ test_systems_amg_has_teeth shows num_functions 1 gives other numbers.
 The Ruge first pass alone (coarsen_type 11, ij -ruge1p: par_coarsen.c:1347,
 measure-0 points F, local measures per rank) reproduces coarsening.out.9;
 default.out.0 (np 1, random PMIS) and solvers.out.sysu (-sysL 2 -nf 2, the
-default solver) match every printed digit.
+default solver) match every printed digit, and FCF-Jacobi (relax 17,
+par_relax_more.c:661) smoother.out.14.
 Extended+i where no common C point (interp_type 7, par_lr_interp.c:1932)
 matches interp.out.1/4 (Pmx 0 and 4) to every printed digit.
 Standard interpolation (interp_type 8, par_lr_interp.c:22) matches
