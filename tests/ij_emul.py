@@ -7,6 +7,8 @@ stacked rank by rank.  Rows are in rank order and each row keeps its
 generation order; hypreve_BoomerAMGSetRankEmulation puts every row into ParCSR
 order (own columns first) and emulates the per-rank coarsening.
 """
+import math
+
 import numpy as np
 import scipy.sparse as sp
 
@@ -123,6 +125,50 @@ def sys_laplacian_ranks(nx, ny, nz, P, Q, R, nf=3, mtrx=None):
                         ip.append(len(jj))
         starts.append(len(ip) - 1)
     n = nf * nx * ny * nz
+    A = sp.csr_matrix((np.array(vv), np.array(jj, dtype=np.int32), np.array(ip, dtype=np.int32)), shape=(n, n))
+    return A, starts
+
+
+def rotate_ranks(nx, ny, P, Q, alpha, eps):
+    """(scipy CSR, level-0 rank starts) of ij -rotate (BuildParRotate7pt,
+    parcsr_ls/par_rotate_7pt.c GenerateRotate7pt) on a P x Q process grid,
+    rank = p + P*q: the rotated anisotropic 2-D operator, each row centre,
+    (-1,-1), (0,-1), (-1,0), (+1,0), (0,+1), (+1,+1)."""
+    x = 4.0 * math.atan(1.0) * alpha / 180.0
+    s, c = math.sin(x), math.cos(x)
+    ac = -(c * c + eps * s * s)
+    bc = 2.0 * (1.0 - eps) * s * c
+    cc = -(s * s + eps * c * c)
+    v0, v1, v2, v3 = -2 * (2 * ac + bc + 2 * cc), 2 * ac + bc, bc + 2 * cc, -bc
+    xp, yp = partition(nx, P), partition(ny, Q)
+    own_x = np.searchsorted(xp, np.arange(nx), side="right") - 1
+    own_y = np.searchsorted(yp, np.arange(ny), side="right") - 1
+    offs, o = {}, 0
+    for q in range(Q):
+        for p in range(P):
+            offs[p + P * q] = o
+            o += (xp[p + 1] - xp[p]) * (yp[q + 1] - yp[q])
+
+    def gidx(ix, iy):
+        p, q = own_x[ix], own_y[iy]
+        return offs[p + P * q] + (ix - xp[p]) + (xp[p + 1] - xp[p]) * (iy - yp[q])
+
+    ip, jj, vv, starts = [0], [], [], [0]
+    for rk in range(P * Q):
+        p, q = rk % P, rk // P
+        for iy in range(yp[q], yp[q + 1]):
+            for ix in range(xp[p], xp[p + 1]):
+                ent = [(gidx(ix, iy), v0)]
+                for jx, jy, v in ((ix - 1, iy - 1, v3), (ix, iy - 1, v2), (ix - 1, iy, v1), (ix + 1, iy, v1),
+                                  (ix, iy + 1, v2), (ix + 1, iy + 1, v3)):
+                    if 0 <= jx < nx and 0 <= jy < ny:
+                        ent.append((gidx(jx, jy), v))
+                for col, v in ent:
+                    jj.append(col)
+                    vv.append(v)
+                ip.append(len(jj))
+        starts.append(len(ip) - 1)
+    n = nx * ny
     A = sp.csr_matrix((np.array(vv), np.array(jj, dtype=np.int32), np.array(ip, dtype=np.int32)), shape=(n, n))
     return A, starts
 

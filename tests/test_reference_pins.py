@@ -50,7 +50,8 @@ The Ruge first pass alone (coarsen_type 11, ij -ruge1p: par_coarsen.c:1347,
 measure-0 points F, local measures per rank) reproduces coarsening.out.9;
 default.out.0 (np 1, random PMIS) and solvers.out.sysu (-sysL 2 -nf 2, the
 default solver) match every printed digit, and FCF-Jacobi (relax 17,
-par_relax_more.c:661) smoother.out.14.
+par_relax_more.c:661) smoother.out.14; ij -rotate's 2-D operator
+(par_rotate_7pt.c, tests/ij_emul.py) under Chebyshev smoother.out.19.
 Extended+i where no common C point (interp_type 7, par_lr_interp.c:1932)
 matches interp.out.1/4 (Pmx 0 and 4) to every printed digit.
 Standard interpolation (interp_type 8, par_lr_interp.c:22) matches
@@ -72,7 +73,9 @@ CASES = json.load(open(os.path.join(HERE, "golden", "ij_rank_fixtures.json")))["
 
 def build(hv, case):
     prob = case["problem"]
-    if prob.get("sysL"):
+    if prob.get("rotate"):
+        A_s, starts = ij_emul.rotate_ranks(*prob["n"], *prob["P"], *prob["rotate"])
+    elif prob.get("sysL"):
         A_s, starts = ij_emul.sys_laplacian_ranks(*prob["n"], *prob["P"], nf=prob["sysL"])
     else:
         A_s, starts = ij_emul.laplacian_ranks(*prob["n"], *prob["P"], c=tuple(prob.get("c", (1.0, 1.0, 1.0))),
