@@ -173,6 +173,87 @@ def rotate_ranks(nx, ny, P, Q, alpha, eps):
     return A, starts
 
 
+def _vdc_coef(xx, yy, zz):
+    """afun = bfun = cfun of par_vardifconv.c:397-483: 0.01 in the eight corner
+    cubes, 1000 in the inner cube, 1 elsewhere."""
+    lo = lambda v: v < 0.1
+    hi = lambda v: v > 0.9
+    if ((lo(xx) and lo(yy) and lo(zz)) or (lo(xx) and lo(yy) and hi(zz)) or (lo(xx) and hi(yy) and lo(zz))
+            or (hi(xx) and lo(yy) and lo(zz)) or (hi(xx) and hi(yy) and lo(zz)) or (hi(xx) and lo(yy) and hi(zz))
+            or (lo(xx) and hi(yy) and hi(zz)) or (hi(xx) and hi(yy) and hi(zz))):
+        return 0.01
+    if 0.1 <= xx <= 0.9 and 0.1 <= yy <= 0.9 and 0.1 <= zz <= 0.9:
+        return 1000.0
+    return 1.0
+
+
+def vardifconv_ranks(nx, ny, nz, P, Q, R, eps):
+    """(scipy CSR, level-0 rank starts, rhs) of ij -vardifconv (type 0,
+    parcsr_ls/par_vardifconv.c:15 GenerateVarDifConv) on a P x Q x R process
+    grid: the variable-coefficient diffusion with d = e = f = g = 0, r = 1 and
+    zero boundary values, each row centre, z-1, y-1, x-1, x+1, y+1, z+1."""
+    xp, yp, zp = partition(nx, P), partition(ny, Q), partition(nz, R)
+    own_x = np.searchsorted(xp, np.arange(nx), side="right") - 1
+    own_y = np.searchsorted(yp, np.arange(ny), side="right") - 1
+    own_z = np.searchsorted(zp, np.arange(nz), side="right") - 1
+    offs, o = {}, 0
+    for r in range(R):
+        for q in range(Q):
+            for p in range(P):
+                offs[p + P * q + P * Q * r] = o
+                o += (xp[p + 1] - xp[p]) * (yp[q + 1] - yp[q]) * (zp[r + 1] - zp[r])
+
+    def gidx(ix, iy, iz):
+        p, q, r = own_x[ix], own_y[iy], own_z[iz]
+        nxl, nyl = xp[p + 1] - xp[p], yp[q + 1] - yp[q]
+        return offs[p + P * q + P * Q * r] + (ix - xp[p]) + nxl * ((iy - yp[q]) + nyl * (iz - zp[r]))
+
+    hhx, hhy, hhz = 1.0 / (nx + 1), 1.0 / (ny + 1), 1.0 / (nz + 1)
+    ip, jj, vv, rhs, starts = [0], [], [], [], [0]
+    for rk in range(P * Q * R):
+        p, q, r = rk % P, (rk // P) % Q, rk // (P * Q)
+        for iz in range(zp[r], zp[r + 1]):
+            zz = (iz + 1) * hhz
+            for iy in range(yp[q], yp[q + 1]):
+                yy = (iy + 1) * hhy
+                for ix in range(xp[p], xp[p + 1]):
+                    xx = (ix + 1) * hhx
+                    afp = eps * _vdc_coef(xx + 0.5 * hhx, yy, zz) / hhx / hhx
+                    afm = eps * _vdc_coef(xx - 0.5 * hhx, yy, zz) / hhx / hhx
+                    bfp = eps * _vdc_coef(xx, yy + 0.5 * hhy, zz) / hhy / hhy
+                    bfm = eps * _vdc_coef(xx, yy - 0.5 * hhy, zz) / hhy / hhy
+                    cfp = eps * _vdc_coef(xx, yy, zz + 0.5 * hhz) / hhz / hhz
+                    cfm = eps * _vdc_coef(xx, yy, zz - 0.5 * hhz) / hhz / hhz
+                    df = ef = ff = gf = 0.0
+                    ent = [(gidx(ix, iy, iz), afp + afm + bfp + bfm + cfp + cfm + gf - df - ef - ff)]
+                    # rfun = 1; the boundary terms add coefficient * bndfun = 0
+                    b = 1.0
+                    for cond, coef in ((ix == 0, afm), (iy == 0, bfm), (iz == 0, cfm), (ix + 1 == nx, afp - df),
+                                       (iy + 1 == ny, bfp - ef), (iz + 1 == nz, cfp - ff)):
+                        if cond:
+                            b += coef * 0.0
+                    rhs.append(b)
+                    for jx, jy, jz, v in ((ix, iy, iz - 1, -cfm), (ix, iy - 1, iz, -bfm), (ix - 1, iy, iz, -afm),
+                                          (ix + 1, iy, iz, -afp + df), (ix, iy + 1, iz, -bfp + ef),
+                                          (ix, iy, iz + 1, -cfp + ff)):
+                        if 0 <= jx < nx and 0 <= jy < ny and 0 <= jz < nz:
+                            ent.append((gidx(jx, jy, jz), v))
+                    for col, v in ent:
+                        jj.append(col)
+                        vv.append(v)
+                    ip.append(len(jj))
+        starts.append(len(ip) - 1)
+    n = nx * ny * nz
+    A = sp.csr_matrix((np.array(vv), np.array(jj, dtype=np.int32), np.array(ip, dtype=np.int32)), shape=(n, n))
+    return A, starts, np.array(rhs)
+
+
+def rand_guess(starts):
+    """ij's random initial guess (build_src_type 5, ij.c:3046): every rank
+    hypre_SeedRand(myid), then hypre_Rand() per entry."""
+    return np.concatenate([rand_stream(starts[k + 1] - starts[k], k) for k in range(len(starts) - 1)])
+
+
 def rand_stream(n, seed):
     """n draws of hypre_Rand() after hypre_SeedRand(seed) (utilities/random.c)."""
     a, m = 16807, 2147483647

@@ -13,7 +13,7 @@ relative).
 import numpy as np
 import pytest
 
-from test_reference_pins import CASES, build, check_stats
+from test_reference_pins import CASES, build, check_stats, initial_guess
 
 pytestmark = pytest.mark.gpu
 
@@ -21,15 +21,16 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_gpu_rank_fixture(gpu, orc, case):
     hv = gpu
-    A, amg, b_h, _ = build(hv, case)
+    A, amg, b_h, starts = build(hv, case)
     n = A.n
     b = hv.ParVector(n, b_h)
-    x = hv.ParVector(n, np.zeros(n))
+    x0 = initial_guess(case, starts, n)
+    x = hv.ParVector(n, x0)
     if case["solver"] == "amg":
         amg.setup(A)
         it, rr = amg.solve(A, b, x)
         O = orc.OracleAMG(amg)
-        u = np.zeros(n)
+        u = x0.copy()
         st = O.solve(b_h, u, 1e-8, 100)
         assert it == st["iterations"]
         assert np.array_equal(x.get(), u), "GPU iterate differs from the oracle"

@@ -51,7 +51,10 @@ measure-0 points F, local measures per rank) reproduces coarsening.out.9;
 default.out.0 (np 1, random PMIS) and solvers.out.sysu (-sysL 2 -nf 2, the
 default solver) match every printed digit, and FCF-Jacobi (relax 17,
 par_relax_more.c:661) smoother.out.14; ij -rotate's 2-D operator
-(par_rotate_7pt.c, tests/ij_emul.py) under Chebyshev smoother.out.19.
+(par_rotate_7pt.c, tests/ij_emul.py) under Chebyshev smoother.out.19, and
+ij -vardifconv's jumping coefficients (par_vardifconv.c, its own right-hand
+side, ij's random initial guess) with a 5-step CG eigenvalue estimate
+smoother.out.20.
 Extended+i where no common C point (interp_type 7, par_lr_interp.c:1932)
 matches interp.out.1/4 (Pmx 0 and 4) to every printed digit.
 Standard interpolation (interp_type 8, par_lr_interp.c:22) matches
@@ -73,8 +76,11 @@ CASES = json.load(open(os.path.join(HERE, "golden", "ij_rank_fixtures.json")))["
 
 def build(hv, case):
     prob = case["problem"]
+    b_gen = None
     if prob.get("rotate"):
         A_s, starts = ij_emul.rotate_ranks(*prob["n"], *prob["P"], *prob["rotate"])
+    elif prob.get("vardifconv"):
+        A_s, starts, b_gen = ij_emul.vardifconv_ranks(*prob["n"], *prob["P"], prob["vardifconv"])
     elif prob.get("sysL"):
         A_s, starts = ij_emul.sys_laplacian_ranks(*prob["n"], *prob["P"], nf=prob["sysL"])
     else:
@@ -90,13 +96,20 @@ def build(hv, case):
     kw.update(st)
     amg = hv.BoomerAMG(**kw)
     amg.set_rank_emulation(starts)
-    if case["rhs"] == "rhsrand":
+    if case["rhs"] == "generated":  # the generator's own right-hand side (ij build_rhs_type 6)
+        b = b_gen
+    elif case["rhs"] == "rhsrand":
         b = ij_emul.rhsrand(starts)
     elif case["rhs"] == "xisone":  # ij -xisone: b = A * ones (ij.c:629)
         b = A_s @ np.ones(A.n)
     else:
         b = np.ones(A.n)
     return A, amg, b, starts
+
+
+def initial_guess(case, starts, n):
+    """x0: zero, or ij's per-rank random guess (build_src_type 5)."""
+    return ij_emul.rand_guess(starts) if case.get("x0") == "rand" else np.zeros(n)
 
 
 def check_stats(case, amg, st=None, it=None, rr=None):
@@ -115,10 +128,10 @@ def check_stats(case, amg, st=None, it=None, rr=None):
 
 @pytest.mark.parametrize("case", CASES, ids=[c["name"] for c in CASES])
 def test_rank_fixture(hv, orc, case):
-    A, amg, b, _ = build(hv, case)
+    A, amg, b, starts = build(hv, case)
     amg.setup_host(A)
     O = orc.OracleAMG(amg)
-    x = np.zeros(A.n)
+    x = initial_guess(case, starts, A.n)
     if case["solver"] == "amg":
         st = O.solve(b, x, 1e-8, 100)
         check_stats(case, amg, st, st["iterations"], st["rel_res"])
