@@ -342,9 +342,11 @@ extern const int* hve_setup_dof;
 void coarsen_pmis(const Pattern& S, int cf_init, std::vector<int>& cf, const std::vector<int>* rs = nullptr);
 // full_row_len (optional): strong connections of each row including those the
 // pattern omits (another rank's columns), for the empty-row test.  f_pnt: the
-// marker of measure-0 points (Z_PT under HMIS, F_PT for coarsen_type 11).
+// marker of measure-0 points (Z_PT under HMIS, F_PT for coarsen_type 11);
+// meas_add (optional): measure counted from other ranks' rows (global measures).
 void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, int cut_factor,
-                             std::vector<int>& cf, const int* full_row_len = nullptr, int f_pnt = Z_PT);
+                             std::vector<int>& cf, const int* full_row_len = nullptr, int f_pnt = Z_PT,
+                             const int* meas_add = nullptr);
 void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
                   const std::vector<int>* rs = nullptr);
 void coarsen_ruge1p(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,

@@ -609,7 +609,7 @@ struct MeasureLists {
 // -> 11 with f_pnt = Z_PT for measure-0 points, :1082-1086); coarsen_type 11
 // itself leaves f_pnt = F_PT.
 void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, int cut_factor,
-                             std::vector<int>& cf, const int* full_row_len, int f_pnt) {
+                             std::vector<int>& cf, const int* full_row_len, int f_pnt, const int* meas_add) {
   constexpr int UNDECIDED = 0, SC_PT = 3;
   const int n = S.n;
   const bool agg_2 = (measure_type == 3 || measure_type == 4);
@@ -623,7 +623,7 @@ void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, i
       for (int k = S.i[i]; k < S.i[i + 1]; ++k) ST_j[pos[S.j[k]]++] = i;
   }
   std::vector<int> measure(n);
-  for (int i = 0; i < n; ++i) measure[i] = ST_i[i + 1] - ST_i[i];
+  for (int i = 0; i < n; ++i) measure[i] = ST_i[i + 1] - ST_i[i] + (meas_add ? meas_add[i] : 0);
 
   cf.assign(n, 0);  // CF_marker allocated by the coarsening (all UNDECIDED)
   int num_left = 0;
@@ -733,9 +733,20 @@ void coarsen_ruge_first_pass(const Pattern& S, const CSR* A, int measure_type, i
 // with the strong connections it owns (S_diag, local measures:
 // par_coarsen.c:1088 builds no S_ext for measure_type 0), counting the whole
 // row (diag and offd) for the isolated-point test.
+// measure_type 1 (global measures, par_coarsen.c:1088-1108): a point's
+// measure also counts the other ranks' points that strongly depend on it
+// (S_ext); the pass itself still follows the rank's own connections.
 static void ruge_first_pass_ranks(const Pattern& S, int measure_type, int f_pnt, std::vector<int>& cf,
                                   const std::vector<int>* rs) {
   const int nr = (int)rs->size() - 1;
+  std::vector<int> ext;
+  if (measure_type == 1) {
+    auto owner = [&](int i) { return (int)(std::upper_bound(rs->begin(), rs->end(), i) - rs->begin()) - 1; };
+    ext.assign(S.n, 0);
+    for (int i = 0; i < S.n; ++i)
+      for (int k = S.i[i]; k < S.i[i + 1]; ++k)
+        if (owner(S.j[k]) != owner(i)) ext[S.j[k]]++;
+  }
   cf.assign(S.n, 0);
 #pragma omp parallel for schedule(dynamic, 1)
   for (int r = 0; r < nr; ++r) {
@@ -751,7 +762,7 @@ static void ruge_first_pass_ranks(const Pattern& S, int measure_type, int f_pnt,
       Sl.i[i - a + 1] = (int)Sl.j.size();
     }
     std::vector<int> cl;
-    coarsen_ruge_first_pass(Sl, nullptr, measure_type, 0, cl, full.data(), f_pnt);
+    coarsen_ruge_first_pass(Sl, nullptr, measure_type, 0, cl, full.data(), f_pnt, ext.empty() ? nullptr : ext.data() + a);
     std::copy(cl.begin(), cl.end(), cf.begin() + a);
   }
 }
@@ -771,16 +782,15 @@ void coarsen_hmis(const Pattern& S, const CSR* A, int measure_type, int cut_fact
 }
 
 // coarsen_type 11 (ij -ruge1p): the Ruge first pass alone, measure-0 points F
-// (par_coarsen.c:1347).  With emulated ranks only local measures are restated
-// (measure_type 1 builds S_ext and a global first pass).
+// (par_coarsen.c:1347); with emulated ranks, local (0) or global (1) measures.
 void coarsen_ruge1p(const Pattern& S, const CSR* A, int measure_type, int cut_factor, std::vector<int>& cf,
                     const std::vector<int>* rs) {
   if (!rs) {
     coarsen_ruge_first_pass(S, A, measure_type, cut_factor, cf, nullptr, F_PT);
     return;
   }
-  if (cut_factor > 0 || measure_type != 0)
-    throw std::runtime_error("rank emulation: coarsen_type 11 needs local measures and no cut factor");
+  if (cut_factor > 0 || (measure_type != 0 && measure_type != 1))
+    throw std::runtime_error("rank emulation: coarsen_type 11 needs measure_type 0 or 1 and no cut factor");
   ruge_first_pass_ranks(S, measure_type, F_PT, cf, rs);
 }
 

@@ -47,7 +47,9 @@ coarse functions from the C points) reproduces agg_interp.out.10 (multipass,
 solvers.out.107/108 (with the redundant coarse grid) to every printed digit;
 test_systems_amg_has_teeth shows num_functions 1 gives other numbers.
 The Ruge first pass alone (coarsen_type 11, ij -ruge1p: par_coarsen.c:1347,
-measure-0 points F, local measures per rank) reproduces coarsening.out.9;
+measure-0 points F) reproduces coarsening.out.9 (local measures per rank) and
+coarsening.out.8 (-gm: global measures, other ranks' dependents counted,
+par_coarsen.c:1088-1108);
 default.out.0 (np 1, random PMIS) and solvers.out.sysu (-sysL 2 -nf 2, the
 default solver) match every printed digit, and FCF-Jacobi (relax 17,
 par_relax_more.c:661) smoother.out.14; ij -rotate's 2-D operator
@@ -247,3 +249,14 @@ def test_systems_amg_has_teeth(hv, orc):
     amg.setup_host(A)
     it, rr = orc.OracleAMG(amg).pcg(b, np.zeros(A.n), 1e-8, 1000, 1)
     assert (it, f"{rr:e}") != (22, "8.737365e-09")
+
+
+def test_global_measures_have_teeth(hv, orc):
+    """coarsening.out.8 with local measures (measure_type 0) misses the saved
+    13 iterations / 3.043813e-09: the other ranks' dependents matter."""
+    case = dict(next(c for c in CASES if c["name"] == "coarsening.out.8"))
+    case["settings"] = {"coarsen_type": 11, "measure_type": 0}
+    A, amg, b, _ = build(hv, case)
+    amg.setup_host(A)
+    st = orc.OracleAMG(amg).solve(b, np.zeros(A.n), 1e-8, 100)
+    assert (st["iterations"], f"{st['rel_res']:e}") != (13, "3.043813e-09")
