@@ -56,7 +56,9 @@ par_relax_more.c:661) smoother.out.14; ij -rotate's 2-D operator
 (par_rotate_7pt.c, tests/ij_emul.py) under Chebyshev smoother.out.19, and
 ij -vardifconv's jumping coefficients (par_vardifconv.c, its own right-hand
 side, ij's random initial guess) with a 5-step CG eigenvalue estimate
-smoother.out.20.
+smoother.out.20; the reference's own 2-rank elasticity matrix (TEST_ij/A.0000*,
+kept as tests/golden/ij_elast_A.npz by scripts/make_file_fixtures.py) under
+2-function systems AMG and PCG: elast.out.7.
 Extended+i where no common C point (interp_type 7, par_lr_interp.c:1932)
 matches interp.out.1/4 (Pmx 0 and 4) to every printed digit.
 Standard interpolation (interp_type 8, par_lr_interp.c:22) matches
@@ -69,6 +71,7 @@ import os
 
 import numpy as np
 import pytest
+import scipy.sparse as sp
 
 import ij_emul
 
@@ -79,7 +82,12 @@ CASES = json.load(open(os.path.join(HERE, "golden", "ij_rank_fixtures.json")))["
 def build(hv, case):
     prob = case["problem"]
     b_gen = None
-    if prob.get("rotate"):
+    if prob.get("file"):  # a matrix the reference's tests read with ij -fromfile (scripts/make_file_fixtures.py)
+        z = np.load(os.path.join(HERE, "golden", prob["file"]))
+        n = len(z["indptr"]) - 1
+        A_s = sp.csr_matrix((z["data"], z["indices"], z["indptr"]), shape=(n, n))
+        starts = [int(v) for v in z["starts"]]
+    elif prob.get("rotate"):
         A_s, starts = ij_emul.rotate_ranks(*prob["n"], *prob["P"], *prob["rotate"])
     elif prob.get("vardifconv"):
         A_s, starts, b_gen = ij_emul.vardifconv_ranks(*prob["n"], *prob["P"], prob["vardifconv"])
