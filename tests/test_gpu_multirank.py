@@ -69,7 +69,7 @@ def _solve_nranks(hv, nx, ny, nz, kw, nranks, timeout=300, stencil=7):
 
 @pytest.mark.parametrize("nranks,nx,nz", [(2, 16, 16), (3, 14, 20), (4, 12, 13)])
 @pytest.mark.parametrize("agglo", [0, 2000])
-@pytest.mark.parametrize("relax", [18, 0])
+@pytest.mark.parametrize("relax", [18, 0, 17])
 def test_loopback_partitioned_solve_bitwise(hv, nranks, nx, nz, relax, agglo):
     """agglo 0: every level distributed; 2000: the coarse levels from the first
     one under 2000 rows are replicated on every rank (one all-gather down)."""
