@@ -1403,24 +1403,12 @@ __global__ void __launch_bounds__(256) k_sell_pw(SpArgs p) {
 // reads 2-byte local columns and takes x from LDS.  Same entries, same order,
 // same rounding as every other loop: bitwise the same.
 // ---------------------------------------------------------------------------
-// Experiment switches (compile time): clamped all-lane loads in the
-// dictionary loop, two register sets there, lane-masked gathers in the coded
-// loop
-#ifndef HVE_DICT_CLAMP
-#define HVE_DICT_CLAMP 0
-#endif
-#ifndef HVE_DICT_DB
-#define HVE_DICT_DB 1
-#endif
-
-// A batch's loads.  Every lane issues every load, so the batch is a fixed
-// count of loads and the loop waits on exact counters (a lane-masked load sits
-// behind an exec branch, and the compiler then drains every load at each
-// use).  A lane past its row end (slot k + q holds entries for lanes
-// [0, cnt) only: rows are sorted by descending length) reads the last active
-// lane's entry instead, a line the wave fetches anyway; its words are never
-// used (dict_sum selects them out).  cp and vl point at the slice's first
-// entry; P is the offset of slot k.
+// A batch's loads, lane-masked: slot k + q holds entries for lanes [0, cnt)
+// only (rows are sorted by descending length), so a lane past its row end
+// loads nothing and its words are never used (dict_sum selects them out).
+// (Clamped all-lane loads, exact waits instead of the drain at each masked
+// branch, measured 12 % slower on A1: profiles/r05/13_loops/README.txt.)
+// cp and vl point at the slice's first entry; P is the offset of slot k.
 template <int B, bool NT, class V>
 __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp, const V& vl, int& P, int k, int blen,
                                           int (&c)[B], typename V::raw (&a)[B], int dexp = 0) {
@@ -1428,9 +1416,6 @@ __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp,
 #pragma unroll
   for (int q = 0; q < B; ++q) {
     const int cnt = __popcll(__builtin_amdgcn_ballot_w64((k + q) < blen));
-#if HVE_DICT_CLAMP
-    const int e = P + min(lane, max(cnt - 1, 0));
-#else
     const int e = P + lane;
     if ((k + q) >= blen) {  // lane-masked loads (exec branches)
       c[q] = -1;
@@ -1438,7 +1423,6 @@ __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp,
       P += cnt;
       continue;
     }
-#endif
 #ifdef HVE_DICT_EXP
     // timing only: 2 leaves out the column loads, 4 the value loads
     c[q] = (dexp & 2) ? (int)((threadIdx.x + q) & 255) : (int)mload<NT>(cp + e);
@@ -1606,7 +1590,6 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   typename V::raw a2[B];
   // (the empty asm keeps each batch's loads ahead of the other set's sums:
   // without it the compiler sinks them past the exit test, next to their use)
-#if HVE_DICT_DB
   for (int k = k0; k < width; k += 2 * B) {
     dict_load<B, NT>(cp, vl, P, k + B, blen, c2, a2, p.dexp);
     asm volatile("" ::: "memory");
@@ -1616,15 +1599,6 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
     asm volatile("" ::: "memory");
     dict_sum<B>(xl, vl, c2, a2, k + B, llen, sub, t);
   }
-#else
-  for (int k = k0; k < width; k += B) {
-    dict_load<B, NT>(cp, vl, P, k + B, blen, c2, a2, p.dexp);
-    asm volatile("" ::: "memory");
-    dict_sum<B>(xl, vl, c, a, k, llen, sub, t);
-#pragma unroll
-    for (int q = 0; q < B; ++q) { c[q] = c2[q]; a[q] = a2[q]; }
-  }
-#endif
   if (own) row_store_pre<OP, NT>(p, g, skip, t, uo, d, pre);
 }
 
