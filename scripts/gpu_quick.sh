@@ -15,8 +15,3 @@ step() {
 step tests 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_scale.py tests/test_gpu_multirank.py -m gpu -x -q --timeout 300 --timeout-method thread
 step ops512 500 python scripts/ops_time.py ${N:-512}
 echo "=== done"
-if [[ ${GRIDSWEEP:-0} == 1 ]]; then
-  for G in 0 4096 1024; do
-    HVE_STENCIL_GRID=$G step ops512_grid$G 500 python scripts/ops_time.py ${N:-512}
-  done
-fi

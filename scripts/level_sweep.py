@@ -30,7 +30,7 @@ def main():
     import hypreve as hv
 
     hv.init()
-    variant = {k: os.environ.get(k, "") for k in ("HVE_SELL_BATCH", "HVE_SELL_SIGMA", "HVE_SELL_PIPE", "HVE_SELL_NT", "HVE_SELL_JAG", "HVE_SELL_JAG_SORT")}
+    variant = {k: os.environ.get(k, "") for k in ("HVE_SELL_BATCH", "HVE_SELL_SIGMA", "HVE_SELL_PIPE", "HVE_SELL_NT", "HVE_SELL_JAG")}
     print(f"variant {variant}", flush=True)
     rows = []
     for eb in (4, 8, 16):
