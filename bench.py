@@ -48,6 +48,8 @@ KERNEL_OF_LAYOUT = {
     "delta": ("k_sell_delta<0, false, |, true, 0>(hve::SpArgs)", "SELL-64 with 16-bit column deltas"),
     "dict": ("k_sell_dict<0, false, |, true, ", "jagged SELL-64 with an LDS x-tile dictionary"),
     "dict-ranges": ("k_sell_dict<0, false, |, true, ", "jagged SELL-64 with an LDS x-tile of column ranges"),
+    "dict-wide": ("k_sell_dictw<0, false, true, ", "jagged SELL-64 with an LDS x-tile dictionary, lane-packed "
+                  "value / column streams"),
     "padded": ("k_sell<0, false, |, ", "padded SELL-64"),
     "jagged": ("k_sell<0, false, |, ", "jagged SELL-64"),
     "wide": ("k_sell_wide<0, false, |", "padded SELL-64, one workgroup per slice"),
@@ -129,9 +131,7 @@ def sha256_f64(v):
 
 def slab_digests_of(x, nx, ny, nz, worlds=(2, 4, 8)):
     """sha256 of the whole iterate and of its z-slabs as an N-rank run would
-    own them, for each N in worlds: an N-rank line's per-rank digests must
-    equal the N-column here (the N-rank iterate equals the 1-rank iterate bit
-    for bit)."""
+    own them, for each N in worlds."""
     out = {"1": [sha256_f64(x)]}
     for w in worlds:
         if w <= nz:
@@ -139,7 +139,22 @@ def slab_digests_of(x, nx, ny, nz, worlds=(2, 4, 8)):
     return out
 
 
+def slab_starts(nx, ny, nz, world):
+    """Level-0 row starts of the world-rank z-slab run (slab_rows)."""
+    cuts = slab_rows(nx, ny, nz, world)
+    return [f for f, _ in cuts] + [nx * ny * nz]
+
+
 GOLDEN_DIGESTS = os.path.join(ROOT, "tests", "golden", "slab_digests.json")
+# Workloads no single process can hold, so no one-GPU reference exists (the
+# N-rank line then reports "equal": null with this reason)
+NO_REFERENCE = {
+    "512x512x512 stencil27": (
+        "no one-process reference exists: GenerateLaplacian27pt at 512^3 has 3.62e9 nonzeros, past the 2^31 - 1 "
+        "entries a 32-bit CSR row pointer addresses (the reference's default 32-bit HYPRE_Int build has the same "
+        "bound for one process); the 8-rank run holds 4.5e8 a rank.  The same code is pinned at 256^3 "
+        "(tests/golden/slab_digests.json, 256x256x256 stencil27, columns 2 / 4 / 8)"),
+}
 
 
 def digest_key(args, nx, ny, nz, iters):
@@ -150,9 +165,13 @@ def digest_key(args, nx, ny, nz, iters):
 
 
 def golden_slab_digests(key):
-    """The committed one-GPU digests of workload `key` (tests/golden/
-    slab_digests.json: N = 1 bench lines, the iterate bitwise equal to the C
-    oracle's), or None."""
+    """The committed digests of workload `key` (tests/golden/slab_digests.json,
+    merged by scripts/golden_digests.py from one-GPU lines whose iterate was
+    bitwise equal to the C oracle's): column "1" the whole iterate of the
+    one-process setup, column "N" the slabs of the N-rank setup's iterate (a
+    one-GPU run under the rank emulation of N z-slab ranks, bench.py
+    --emulate N: hypre's N-process rules, the contract of every N-rank run),
+    or None."""
     try:
         with open(GOLDEN_DIGESTS) as f:
             return json.load(f).get(key)
@@ -247,6 +266,46 @@ def pcg_parity(hv, amg, A, b, x, O, nrows, iters):
     return {"kind": "rtol 1e-9 (PCG reductions reorder)", "equal": ok, "iterations": int(it_g),
             "oracle_iterations": int(it_o), "rows": int(nrows), "rel_diff": rel,
             "final_rel_res": rr_g, "oracle_final_rel_res": rr_o}
+
+
+def tol_key(tol):
+    """JSON key of the time-to-solution entry: iters_to_1e-8 for 1e-8."""
+    return "iters_to_" + f"{tol:g}".replace("e-0", "e-")
+
+
+def iters_to_tol(hv, amg, A, b, x, n, tol=1e-8, oracle=None):
+    """Time to solution, the number a hypre user sees: BoomerAMG as the solver
+    (ij -solver 0) and as PCG's preconditioner (ij -solver 1, one V-cycle an
+    iteration) from x = 0 with rhs = ones, each to the relative residual tol,
+    on the GPU; oracle (an OracleAMG of the same hierarchy): the C oracle's
+    counts beside them."""
+    out = {"tol": tol}
+    amg.set(tol=tol, max_iter=1000, min_iter=0)
+    x.fill(0.0)
+    t0 = time.perf_counter()
+    it, rr = amg.solve(A, b, x)
+    out["vcycle"] = {"iterations": int(it), "rel_res": rr, "seconds": round(time.perf_counter() - t0, 3)}
+    amg.set(tol=0.0, max_iter=1)  # the preconditioner: one cycle
+    kr = hv.PCG(tol=tol, max_iter=1000, two_norm=1)
+    kr.set_precond_amg(amg, setup=False)
+    kr.setup(A, b, x)
+    x.fill(0.0)
+    t0 = time.perf_counter()
+    it, rr = kr.solve(A, b, x)
+    out["pcg"] = {"iterations": int(it), "rel_res": rr, "seconds": round(time.perf_counter() - t0, 3)}
+    kr.destroy()
+    if oracle is not None:
+        u = np.zeros(n)
+        st = oracle.solve(np.ones(n), u, tol, 1000)
+        out["vcycle"]["oracle_iterations"] = st["iterations"]
+        u[:] = 0.0
+        ito, _ = oracle.pcg(np.ones(n), u, tol, 1000, 1)
+        out["pcg"]["oracle_iterations"] = int(ito)
+    log(f"[bench] iterations to {tol:g}: V-cycle {out['vcycle']['iterations']}"
+        f"{' (oracle ' + str(out['vcycle'].get('oracle_iterations')) + ')' if oracle is not None else ''}, "
+        f"PCG {out['pcg']['iterations']}"
+        f"{' (oracle ' + str(out['pcg'].get('oracle_iterations')) + ')' if oracle is not None else ''}")
+    return out
 
 
 def hierarchy_digest(amg):
@@ -478,26 +537,37 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
         log(f"[bench] fine SpMV {spmv_ms:.4f} ms, {stored_bytes/1e9:.3f} GB stored -> {achieved:.1f} GB/s "
             f"(CSR-equivalent {csr_gbs:.1f} GB/s); host peak RSS {peak_rss_gb():.1f} GB")
 
-    cpu, parity, parity_detail, parity_pcg, slab = None, None, None, None, None
+    cpu, parity, parity_detail, parity_pcg, slab, to_tol = None, None, None, None, None, None
+    if world == 1 and comm is None and args.iters_tol > 0 and not pcg:
+        O_tol = None
+        if light and args.cpu_cycles > 0:  # the secondary size: the C oracle's counts beside the GPU's
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle_py
+            O_tol = oracle_py.OracleAMG(amg)
+        to_tol = iters_to_tol(hv, amg, A, b, x, nrows, args.iters_tol, O_tol)
+        del O_tol
+        amg.set(tol=1e-300, min_iter=0)
     if rank == 0 and not light and args.cpu_cycles > 0 and world == 1 and comm is None:
         cpu, u_orc, iters, O = oracle_cpu_baseline(amg, nrows, f"{nx}x{ny}x{nz}", pcg, args)
         parity, parity_detail = gpu_parity(hv, amg, krylov, A, b, x, u_orc, iters, pcg)
         if not pcg:
-            # the oracle-equal iterate, cut where an N-rank run's slabs end
+            # the oracle-equal iterate of the one-process setup (the N-rank
+            # references come from --emulate N lines)
             key = digest_key(args, nx, ny, nz, iters)
             slab = {"iterations": iters, "key": key, "equal_to_oracle": parity_detail["equal"],
-                    "digests": slab_digests_of(u_orc, nx, ny, nz)}
+                    "digests": {"1": [sha256_f64(u_orc)]}}
             log(f"[bench] slab digests ({key}): whole {slab['digests']['1'][0][:16]}...")
         del u_orc
         if not pcg and args.pcg_iters > 0:
             parity_pcg = pcg_parity(hv, amg, A, b, x, O, nrows, args.pcg_iters)
         del O
     if not light and world > 1 and args.parity_iters > 0 and not pcg:
-        # bench contract: the CPU baseline is timed at N = 1 only.  Under strong
-        # scaling the N = 1 line runs this same global problem and prints the
-        # digests of its oracle-equal iterate cut at the N-rank slab
-        # boundaries; here every rank solves the same iterations from x = 0 and
-        # rank 0 compares the gathered 32-byte digests of the rank iterates
+        # bench contract: the CPU baseline is timed at N = 1 only.  An N-rank
+        # run follows hypre's N-process setup rules, which one GPU reproduces
+        # under the rank emulation (bench.py --emulate N: the same iterate bit
+        # for bit, checked there against the C oracle); here every rank solves
+        # the same iterations from x = 0 and rank 0 compares the gathered
+        # 32-byte digests of the rank iterates with that reference's slabs
         # (the halo exchange of par_csr_communication.c:298 is on this path)
         x.fill(0.0)
         amg.set(max_iter=args.parity_iters)
@@ -510,18 +580,18 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
             cuts = slab_rows(nx, ny, nz, world)
             dig = [d for _, d in got]
             same_cut = [f for f, _ in got] == [f for f, _ in cuts]
-            # hybrid GS blocks follow the ranks (par_relax.c: each process's
-            # threads sweep its own rows), so its N-rank iterate is not the
-            # 1-rank one and has no N = 1 reference
-            want = (ref or {}).get(str(world)) if args.relax >= 0 else None
+            want = (ref or {}).get(str(world))
             equal = (dig == want and same_cut) if want is not None else None
-            parity = {"kind": "slab sha256 vs N=1", "equal": equal, "iterations": args.parity_iters,
-                      "key": key, "rank_digests": dig, "rank_first_rows": [f for f, _ in got],
-                      "reference": ("tests/golden/slab_digests.json (N = 1 bench line; its iterate is bitwise "
-                                    "equal to the C oracle's)") if want is not None else
-                      "no committed N = 1 digests for this workload: compare rank_digests with the N = 1 line's "
-                      "slab_digests"}
-            log(f"[bench] slab parity vs N=1 after {args.parity_iters} iterations: "
+            parity = {"kind": f"slab sha256 vs the one-GPU rank emulation of {world} ranks", "equal": equal,
+                      "iterations": args.parity_iters, "key": key, "rank_digests": dig,
+                      "rank_first_rows": [f for f, _ in got],
+                      "reference": (f"tests/golden/slab_digests.json column {world} (bench.py --emulate {world} "
+                                    "line: one GPU, hypreve_BoomerAMGSetRankEmulation, its iterate bitwise equal "
+                                    "to the C oracle's on that hierarchy)") if want is not None else
+                      NO_REFERENCE.get(key.split()[0] + " " + key.split()[1],
+                                       f"no committed {world}-rank digests for this workload: run bench.py "
+                                       f"--emulate {world} on one GPU and compare rank_digests with its digests")}
+            log(f"[bench] slab parity vs the {world}-rank emulation after {args.parity_iters} iterations: "
                 f"{'bitwise' if equal else ('MISMATCH' if equal is False else 'no reference')}")
     comm_stats = None
     if world > 1:
@@ -574,6 +644,8 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
     }
     if parity_detail is not None:
         out["parity_detail"] = parity_detail
+    if to_tol is not None:
+        out[tol_key(args.iters_tol)] = to_tol
     if parity_pcg is not None:
         out["parity_pcg"] = parity_pcg
     if slab is not None:
@@ -582,6 +654,112 @@ def run_rank(hv, args, comm, rank, world, barrier, max_over_ranks, gather, n=Non
         out["cpu_baseline_note"] = ("timed at N = 1 only (bench contract); strong scaling: the N = 1 line runs "
                                     "the same global problem") if strong else "timed at N = 1 only (bench contract)"
     return out
+
+
+def gs_leg(hv, args, n):
+    """BoomerAMG's default smoothers (l1 hybrid Gauss-Seidel 13 down / 14 up,
+    par_relax.c:4340 / :4732, automatic blocks) on the n^3 7-point Laplacian,
+    the bench's other settings unchanged: args.steps solve iterations timed as
+    the headline is, then args.parity_iters iterations from x = 0 compared
+    bit for bit with the C oracle on the same hierarchy."""
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+
+    t0 = time.time()
+    A = hv.ParCSRMatrix.laplacian(n, n, n)
+    kw = amg_settings(hv, False, 0, -1, args.coarsen)
+    kw.update(tol=1e-300, max_iter=args.warmup, min_iter=0)
+    amg = hv.BoomerAMG(**kw)
+    with heartbeat("hybrid GS setup"):
+        amg.setup(A)
+    t_setup = time.time() - t0
+    b = hv.ParVector(A.n, np.ones(A.n))
+    x = hv.ParVector(A.n, np.zeros(A.n))
+    if args.warmup > 0:
+        amg.solve(A, b, x)
+    x.fill(0.0)
+    amg.set(max_iter=args.steps)
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    it, rr = amg.solve(A, b, x)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - ts
+    assert it == args.steps, (it, args.steps)
+    iters = args.parity_iters
+    x.fill(0.0)
+    amg.set(max_iter=iters)
+    amg.solve(A, b, x)
+    xg = x.get()
+    O = oracle_py.OracleAMG(amg)
+    u = np.zeros(A.n)
+    O.solve(np.ones(A.n), u, 1e-300, iters)
+    same = bool(np.array_equal(xg, u))
+    out = {"config": f"3D 7-point Laplacian {n}^3, BoomerAMG V-cycle, PMIS + ext+i (Pmx 4), l1 hybrid Gauss-Seidel "
+                     f"13 down / 14 up (BoomerAMG's default smoothers, automatic blocks), Gaussian elimination coarsest",
+           "value": round(A.n * args.steps / el, 1), "unit": "DOF/s", "ms_per_step": round(el / args.steps * 1e3, 4),
+           "steps": args.steps, "levels": amg.num_levels(), "setup_s": round(t_setup, 1),
+           "parity": {"kind": "bitwise", "equal": same, "iterations": iters, "rows": A.n}}
+    log(f"[bench] hybrid GS {n}^3: {out['ms_per_step']:.3f} ms/step, setup {t_setup:.1f}s, parity vs oracle after "
+        f"{iters} iterations: {'bitwise' if same else 'MISMATCH'}")
+    for o in (amg, A, b, x):
+        o.destroy()
+    return out
+
+
+def emulated_reference(hv, args, world):
+    """The reference of a world-rank line, made on one GPU: the global problem
+    set up under the rank emulation of world z-slab ranks
+    (hypreve_BoomerAMGSetRankEmulation: hypre's N-process setup rules, which
+    every N-rank setup of the library follows), solved args.parity_iters
+    iterations from x = 0, and checked bit for bit against the C oracle run on
+    the same hierarchy.  Prints one JSON line whose slab_digests (column
+    `world`: the iterate cut at the ranks' slabs) scripts/golden_digests.py
+    merges into tests/golden/slab_digests.json."""
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+
+    torch.cuda.set_device(0)
+    hv.init()
+    cx, cy, cz = (float(v) for v in args.coef.split(","))
+    nx, ny, nz = global_grid(args, 1)
+    if world > nz:
+        raise SystemExit(f"--emulate {world}: fewer planes ({nz}) than ranks")
+    t0 = time.time()
+    A = (hv.ParCSRMatrix.laplacian27(nx, ny, nz) if args.stencil == 27
+         else hv.ParCSRMatrix.laplacian(nx, ny, nz, cx=cx, cy=cy, cz=cz))
+    n = A.n
+    iters = args.parity_iters
+    kw = amg_settings(hv, False, args.agg, args.relax, args.coarsen)
+    kw.update(tol=1e-300, max_iter=iters, min_iter=0)
+    amg = hv.BoomerAMG(**kw)
+    amg.set_rank_emulation(slab_starts(nx, ny, nz, world))
+    with heartbeat(f"setup under the {world}-rank emulation"):
+        amg.setup(A)
+    t_setup = time.time() - t0
+    b = hv.ParVector(n, np.ones(n))
+    x = hv.ParVector(n, np.zeros(n))
+    it, rr = amg.solve(A, b, x)
+    xg = x.get()
+    with heartbeat("oracle"):
+        O = oracle_py.OracleAMG(amg)
+        u = np.zeros(n)
+        st = O.solve(np.ones(n), u, 1e-300, iters)
+    same = bool(np.array_equal(xg, u)) and st["iterations"] == it == iters
+    key = digest_key(args, nx, ny, nz, iters)
+    dig = {str(world): [sha256_f64(u[f:f + c]) for f, c in slab_rows(nx, ny, nz, world)]}
+    g, o, c = amg.complexities()
+    log(f"[bench] --emulate {world}: {nx}x{ny}x{nz}, {amg.num_levels()} levels, setup {t_setup:.1f}s, "
+        f"GPU vs oracle after {iters} iterations: {'bitwise' if same else 'MISMATCH'}")
+    out = {"kind": f"one-GPU reference of the {world}-rank run (rank emulation)", "n_gpus": 1,
+           "emulated_ranks": world, "setup_path": amg.setup_path(), "levels": amg.num_levels(),
+           "grid_complexity": round(g, 6), "operator_complexity": round(o, 6), "setup_s": round(t_setup, 1),
+           "rel_res": rr, "slab_digests": {"iterations": iters, "key": key, "equal_to_oracle": same, "digests": dig}}
+    print(json.dumps(out), flush=True)
+    return 0 if same else 1
 
 
 def visible_gpus():
@@ -669,7 +847,20 @@ def main():
                          "launch on a one-GPU box: a 1-rank RCCL communicator, partitioned solve path)")
     ap.add_argument("--loopback", type=int, default=0,
                     help="rehearsal only: N virtual ranks (threads) sharing this process's GPU")
+    ap.add_argument("--iters-tol", type=float, default=1e-8,
+                    help="one GPU: iterations to this relative residual from x = 0 (V-cycle and PCG), with the C "
+                         "oracle's counts at the secondary size (0 = skip)")
+    ap.add_argument("--gs-n", type=int, default=256,
+                    help="one GPU: also time BoomerAMG's default smoothers (hybrid GS 13 down / 14 up) at this "
+                         "size, bitwise against the C oracle (secondary_gs; 0 = skip)")
+    ap.add_argument("--emulate", type=int, default=0,
+                    help="one GPU: the reference of an N-rank line (the N-rank setup under the rank emulation, "
+                         "the iterate checked against the C oracle, its slab digests); no timing")
     args = ap.parse_args()
+    if args.emulate > 1:
+        rank_threads()
+        import hypreve as hv
+        sys.exit(emulated_reference(hv, args, args.emulate))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ and args.loopback <= 1:
         # one process per GPU: start the ranks under torch.distributed.run as a
         # child process (nothing here has touched the GPU) and exit with its code
@@ -782,12 +973,15 @@ def main():
     if out is not None and world == 1 and comm is None and args.secondary_n > 0 and args.secondary_n != args.n \
             and not args.grid:
         sec = run_rank(hv, args, None, 0, 1, barrier, max_over_ranks, gather, n=args.secondary_n, light=True)
-        out["secondary"] = {k: sec[k] for k in ("value", "unit", "ms_per_step", "steps")}
+        out["secondary"] = {k: sec[k] for k in ("value", "unit", "ms_per_step", "steps", tol_key(args.iters_tol))
+                            if k in sec}
         out["secondary"]["config"] = sec["config"]
         out["secondary"]["roofline"] = {k: sec["roofline"][k] for k in ("achieved", "frac", "avg_ms", "kernel",
                                                                         "bytes_per_launch", "per_kernel")}
         if args.setup_parity:
             out["setup_parity"] = setup_parity(hv, args, args.secondary_n)
+    if out is not None and world == 1 and comm is None and args.gs_n > 0 and not args.grid and args.relax >= 0:
+        out["secondary_gs"] = gs_leg(hv, args, args.gs_n)
     if out is not None:
         print(json.dumps(out), flush=True)
     if dist:

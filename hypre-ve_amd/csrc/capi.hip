@@ -87,6 +87,10 @@ struct hypre_Solver_struct {
   std::vector<int> rank_emul;       // one process emulating a reference N-rank setup (SetRankEmulation)
   const HYPRE_Int* dof_user = nullptr;  // SetDofFunc: the caller's array, read at Setup (hypre keeps the pointer)
   std::vector<int> coarsen_starts;  // one process coarsening HMIS as N ranks do (SetCoarsenRankStarts)
+  // the last Setup's path (hypreve_BoomerAMGGetSetupPath): 0 one process, 1 one
+  // process under the rank emulation, 2 distributed (dsetup.cpp), 3 gathered on
+  // rank 0 under the rank emulation, 4 gathered one-process (direct interpolation)
+  int setup_path = -1;
   // per level: those blocks and their l1 norms (host copies for the introspection calls)
   std::vector<std::vector<int>> gs_blocks_host;
   std::vector<std::vector<double>> gs_l1_host;
@@ -108,15 +112,8 @@ static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A);
 // MI355X (256^3, relax 13/14): blocks of 4096 rows on every level 45.6 ms a
 // cycle, 1024 rows 38.5 (the coarse Galerkin levels' long in-block dependency
 // chains on few blocks), the level-0 count everywhere (round 2) 11.5.
-// HVE_AUTO_BLOCK_ROWS overrides the level-0 block size (tuning).
-static int auto_block_rows() {
-  static const int v = [] {
-    const char* e = getenv("HVE_AUTO_BLOCK_ROWS");
-    const int r = e ? atoi(e) : 0;
-    return r > 0 ? r : 4096;
-  }();
-  return v;
-}
+// The level-0 block size of the automatic hybrid-GS blocks: 4096 rows.
+static int auto_block_rows() { return 4096; }
 static void resolve_blocks(hypre_Solver_struct* s, int local_rows) {
   s->prm.auto_block_rows = s->auto_blocks ? auto_block_rows() : 0;
   if (s->auto_blocks) s->prm.num_blocks = std::max(1, (local_rows + auto_block_rows() - 1) / auto_block_rows());
@@ -820,10 +817,9 @@ HYPRE_Int hypreve_BoomerAMGSetGsRankStarts(HYPRE_Solver s, HYPRE_Int nranks, con
   }
   return 0;
 }
-// HMIS on one process as the distributed setup of an N-rank run coarsens it
-// (each rank's Ruge first pass, per-rank random streams; dsetup.cpp
-// hmis_dist), everything else the one-process setup: with
-// SetGsRankStarts-free relax types the iterates then equal the N-rank ones.
+// HMIS on one process as an N-rank run coarsens it (each rank's Ruge first
+// pass, per-rank random streams; dsetup.cpp hmis_dist), everything else the
+// one-process setup: a partial rank emulation (SetRankEmulation is the whole).
 HYPRE_Int hypreve_BoomerAMGSetCoarsenRankStarts(HYPRE_Solver s, HYPRE_Int nranks, const HYPRE_Int* starts) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
   CHECK_ARG(nranks <= 1 || starts, 3);
@@ -848,7 +844,7 @@ HYPRE_Int hypreve_BoomerAMGSetRankEmulation(HYPRE_Solver s, HYPRE_Int nranks, co
 }
 // Tuning: re-key the row-block traversal of the built device hierarchy with
 // nbands bands of the grid's y extent (0: natural order; default at Setup:
-// HVE_BLOCK_ORDER, 8).  Only the visiting order of row blocks changes.
+// 8 bands).  Only the visiting order of row blocks changes.
 HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands, HYPRE_Int which_mask) {
   CHECK_ARG(s && s->kind == KIND_AMG && s->dev && s->dev->built(), 1);
   CHECK_ARG(nbands >= 0, 2);
@@ -869,7 +865,7 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands, HYPRE
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  CHECK_ARG(policy >= 0 && policy <= 13, 2);
+  CHECK_ARG(policy >= 0 && policy <= 14, 2);
   s->prm.sell_policy = policy;
   return 0;
 }
@@ -918,6 +914,12 @@ HYPRE_Int hypreve_BoomerAMGSetDeviceSetup(HYPRE_Solver s, HYPRE_Int on) {
   return 0;
 }
 
+HYPRE_Int hypreve_BoomerAMGGetSetupPath(HYPRE_Solver s, HYPRE_Int* path) {
+  CHECK_ARG(s && s->kind == KIND_AMG && path, 1);
+  *path = s->setup_path;
+  return 0;
+}
+
 HYPRE_Int hypreve_BoomerAMGGetSetupLog(HYPRE_Solver s, char* buf, HYPRE_Int len) {
   CHECK_ARG(s && s->kind == KIND_AMG && buf && len > 0, 1);
   snprintf(buf, (size_t)len, "%s", s->H.log.c_str());
@@ -927,10 +929,13 @@ HYPRE_Int hypreve_BoomerAMGGetSetupLog(HYPRE_Solver s, char* buf, HYPRE_Int len)
 }  // extern "C"
 
 // ---------------------------------------------------------------------------
-// Multi-rank setup.  hypre's BoomerAMGSetup is itself distributed; this build
-// runs the (bit-identical) single-process setup on rank 0 over the gathered
-// global matrix and ships every rank its part of each level (RCCL, device
-// staging), so an N-GPU solve reproduces the 1-GPU iterates exactly.
+// Multi-rank setup, gathered: for the options the distributed setup
+// (dsetup.cpp) does not take, rank 0 gathers the global matrix, runs the
+// N-rank emulation of hypre's setup over it (setup.cpp amg_setup with the
+// ranks' row starts) and ships every rank its part of each level (RCCL,
+// device staging).  An N-GPU solve then reproduces hypre's N-process run,
+// and a one-GPU run under hypreve_BoomerAMGSetRankEmulation with the same
+// starts bit for bit.
 // ---------------------------------------------------------------------------
 template <typename T>
 static T* dev_copy(const T* h, size_t n) {
@@ -1010,7 +1015,16 @@ static void setup_multi(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
     }
     if (s->dof_user && s->prm.num_functions > 1)
       throw std::runtime_error("HYPRE_BoomerAMGSetDofFunc with more than one rank is not available");
-    amg_setup(G, s->prm, s->H, nullptr, &starts0);  // HMIS per rank, as the distributed setup
+    // One contract for every N-rank setup: hypre's own setup on `size`
+    // processes, as the rank emulation restates it (pinned to the reference's
+    // np > 1 runs; dsetup.cpp follows the same rules distributed).  The
+    // direct interpolation (3), which the emulation does not restate, keeps
+    // the one-process hierarchy with HMIS coarsened per rank.
+    const int it = s->prm.interp_type;
+    const bool emulated = size > 1 && (it == 6 || it == 7 || it == 8 || it == 9 || it == 14 || (it >= 16 && it <= 18));
+    if (emulated) amg_setup(G, s->prm, s->H, &starts0, nullptr);
+    else amg_setup(G, s->prm, s->H, nullptr, &starts0);
+    s->setup_path = emulated ? 3 : 4;
     { CSR().swap(G); }  // the gathered matrix is level 0 of H now
     bufs.resize(size);
     std::vector<RankHierarchy> parts;
@@ -1151,9 +1165,12 @@ static void setup_dist(hypre_Solver_struct* s, HYPRE_ParCSRMatrix A) {
   if (amg_setup_dist(A->diag, A->first_row, s->prm, hc, s->RH, &log) != 0)
     throw std::runtime_error("distributed setup refused its parameters");
   if (s->prm.print_level > 0) fputs(log.c_str(), stderr);
+  s->H.log = log;
+  s->setup_path = 2;
 }
 
 static void setup_one_process(HYPRE_Solver s, HYPRE_ParCSRMatrix A) {
+  s->setup_path = s->rank_emul.empty() ? 0 : 1;
   if (s->rank_emul.empty()) {
     std::vector<int> dof;
     if (s->dof_user && s->prm.num_functions > 1) dof.assign(s->dof_user, s->dof_user + A->diag.nrows);
@@ -1420,7 +1437,8 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver s, HYPRE_Real* bytes) {
 // 4 dictionary (LDS x-tile), 5 16-bit column deltas, 6 deltas + 8-bit value
 // table, 7 deltas + 16-bit value table, 8 padded + 16-bit value table,
 // 9 jagged + 16-bit value table, 10 range dictionary, 11 slot-uniform stencil
-// (no per-entry data).
+// (no per-entry data), 12 offset-coded, 13 packed codes, 14 the stencil's grid
+// form, 15 dictionary with lane-packed streams (k_sell_dictw).
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which, HYPRE_Int* kind) {
   CHECK_ARG(s && s->dev && s->dev->built() && kind, 1);
   CHECK_ARG(level >= 0 && level < s->dev->num_levels(), 2);
@@ -1430,7 +1448,7 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE
   const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
   *kind = M.code32 ? 13 : M.code16 ? 12 : M.slot_mask ? (grid_stencil_on(M.view()) ? 14 : 11)
          : M.dcol ? (M.vidx16 ? 7 : M.vidx ? 6 : 5)
-                 : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? (M.dict_ranges ? 10 : 4) : M.pw ? 3 : M.rowlen ? 1
+                 : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? (M.dict_ranges ? 10 : M.wptr ? 15 : 4) : M.pw ? 3 : M.rowlen ? 1
                  : M.wide ? 2 : 0;
   API_END
 }

@@ -29,6 +29,10 @@
 namespace hve {
 
 static constexpr int kWave = 64;
+// 16- and 8-byte lane loads of the lane-packed streams
+typedef double dv2_t __attribute__((ext_vector_type(2)));
+typedef unsigned uv4_t __attribute__((ext_vector_type(4)));
+typedef unsigned uv2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int xcd_logical_block(int b, int nblocks_pad) {
   // nblocks_pad is a multiple of 8; block b runs on XCD b%8; give each XCD a
@@ -102,7 +106,7 @@ struct SpArgs {
   int relax_points;
   const GSlot* __restrict__ gslot;           // grid stencil (k_grid_stencil)
   int gnx, gny, gnz, gzc, gz0, gz1;
-  int dexp;  // timing-only builds (-DHVE_DICT_EXP): phases of k_sell_dict left out (knob 12)
+  const int* __restrict__ wptr;              // dictionary layout, lane-packed streams: slice offsets
 };
 
 // Logical workgroup block -> stored row block (SpArgs::blk_map): the
@@ -1089,14 +1093,22 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
 // entry, ((column - slice base) << vbits) | value index, the base per slice in
 // slot_base: 4 B an entry and the column without a second gather (P_0, whose
 // offset-coded form needs cmap).
-template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK>
+// CPK > 1 (R_0, host: pack_codes_lanes): a lane's CPK consecutive codes are
+// stored together, so one 8- or 16-byte load brings CPK entries of its row
+// (slice widths padded to a multiple of CPK with 0xFFFF).
+template <int CPK>
+struct CodePack {
+  using type = typename std::conditional<CPK == 8, uv4_t, uv2_t>::type;
+};
+template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK, int CPK>
 __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, const int* ot, int rb0, int rb1) {
   using CT = typename std::conditional<PK, unsigned, unsigned short>::type;
   constexpr unsigned PAD = PK ? 0xFFFFFFFFu : 0xFFFFu;
+  static_assert(CPK == 1 || (!PK && !MAP && B % CPK == 0), "lane-packed codes: R_0's loop, whole loads a batch");
   const int vb = p.vbits;
   const unsigned vm = (1u << vb) - 1u;
   const bool sub = op_subtracts<OP>() || (OP == OP_GENERAL && p.w == -1.0);
-  int g[NR], a[NR], width[NR];
+  int g[NR], a[NR], width[NR], ws[NR];
   bool act[NR];
   const CT* cp[NR];
   RowPre pre[NR];
@@ -1110,11 +1122,13 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
     act[r] = row < p.nrows;
     const int slice = __builtin_amdgcn_readfirstlane(act[r] ? row >> 6 : 0);
     const int beg = p.slice_ptr[slice];
-    width[r] = act[r] ? __builtin_amdgcn_readfirstlane((p.slice_ptr[slice + 1] - beg) >> 6) : 0;
+    ws[r] = __builtin_amdgcn_readfirstlane(act[r] ? (p.slice_ptr[slice + 1] - beg) >> 6 : 0);
+    width[r] = act[r] ? ws[r] : 0;
     g[r] = act[r] ? (p.rowmap ? mload<true>(p.rowmap + row) : row) : 0;
     if constexpr (PK) cp[r] = p.code32 + beg + (threadIdx.x & (kWave - 1));
+    else if constexpr (CPK > 1) cp[r] = p.code16 + beg + (threadIdx.x & (kWave - 1)) * CPK;
     else cp[r] = p.code16 + beg + (threadIdx.x & (kWave - 1));
-    wmax = max(wmax, width[r]);  // the slice's width: wave-uniform
+    wmax = max(wmax, ws[r]);  // the widest of the NR slices: wave-uniform
     if (CFSEL && act[r] && p.cf[g[r]] != p.relax_points) {
       if (OP == OP_L1JAC || OP == OP_L1JAC_W || OP == OP_JAC) sstore<true>(p.y + g[r], p.x[g[r]]);
       act[r] = false;
@@ -1125,20 +1139,76 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
     pre[r] = act[r] ? row_preload<OP, true>(p, g[r]) : RowPre{};
     t[r] = act[r] ? row_init<OP, true>(p, g[r]) : 0.0;
   }
-  if constexpr (!PK && !MAP) {
-    // R_0: every lane issues every load (codes of slot min(k, wmax - 1), the
-    // gather of a left-out entry at the row's anchor), so a batch is a fixed
-    // count of loads and the waits are exact counters instead of a drain at
-    // each lane-masked branch; the offset and value tables are read for every
-    // entry before the sums (slot 0 for a left-out one).  An entry past the
-    // lane's width, a padding code or an inactive lane is selected out of the
-    // sum (t unchanged).  1.62 -> 1.44 ms at 512^3 (scripts/code_knobs.py).
-    const int wl = max(wmax - 1, 0);
+  if constexpr (!PK && !MAP && CPK > 1) {
+    // R_0, lane-packed codes: B / CPK loads a batch bring a lane B codes
+    // (slots k .. k + B - 1 of its row), every lane issuing every load
+    // (groups past a slice's width re-read its last group: selected out), so
+    // the waits are exact counters; the gathers and table reads as below.
+    using PT = typename CodePack<CPK>::type;
+    constexpr int NL = B / CPK;
+    int gl[NR];  // each slice's last group (its width is a multiple of CPK)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) gl[r] = max(ws[r] / CPK - 1, 0);
+    PT c[NR][NL];
+#pragma unroll
+    for (int r = 0; r < NR; ++r)
+#pragma unroll
+      for (int i = 0; i < NL; ++i)
+        c[r][i] = __builtin_nontemporal_load(reinterpret_cast<const PT*>(cp[r] + min(i, gl[r]) * kWave * CPK));
+    for (int k = 0; k < wmax; k += B) {
+      bool ok[NR][B];
+      unsigned cq[NR][B];
+      double xv[NR][B];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const unsigned w = c[r][q / CPK][(q % CPK) >> 1];
+          cq[r][q] = (q & 1) ? (w >> 16) : (w & 0xffffu);
+          ok[r][q] = (k + q) < width[r] && cq[r][q] != PAD;
+          const int off = ot[ok[r][q] ? (cq[r][q] >> vb) : 0u];
+          xv[r][q] = p.x[a[r] + (ok[r][q] ? off : 0)];
+        }
+      if (k + B < wmax) {  // wave-uniform
+#pragma unroll
+        for (int r = 0; r < NR; ++r)
+#pragma unroll
+          for (int i = 0; i < NL; ++i)
+            c[r][i] = __builtin_nontemporal_load(
+                reinterpret_cast<const PT*>(cp[r] + min((k + B) / CPK + i, gl[r]) * kWave * CPK));
+      }
+      asm volatile("" ::: "memory");  // the next codes go out before the sums
+      double av[NR][B];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) av[r][q] = vt[ok[r][q] ? (cq[r][q] & vm) : 0u];
+#pragma unroll
+      for (int r = 0; r < NR; ++r)
+#pragma unroll
+        for (int q = 0; q < B; ++q) {
+          const double pr = av[r][q] * xv[r][q];
+          const double tn = sub ? t[r] - pr : t[r] + pr;
+          t[r] = ok[r][q] ? tn : t[r];
+        }
+    }
+  } else if constexpr (!PK && !MAP) {
+    // R_0: every lane issues every load (codes of slot min(k, width - 1) of
+    // its slice, the gather of a left-out entry at the row's anchor), so a
+    // batch is a fixed count of loads and the waits are exact counters
+    // instead of a drain at each lane-masked branch; the offset and value
+    // tables are read for every entry before the sums (slot 0 for a left-out
+    // one).  An entry past the lane's width, a padding code or an inactive
+    // lane is selected out of the sum (t unchanged).  1.62 -> 1.44 ms at
+    // 512^3 (scripts/code_knobs.py).
+    int wl[NR];  // each slice's own last slot (NR > 1: slices of other widths)
+#pragma unroll
+    for (int r = 0; r < NR; ++r) wl[r] = max(ws[r] - 1, 0);
     unsigned c[NR][B];
 #pragma unroll
     for (int r = 0; r < NR; ++r)
 #pragma unroll
-      for (int q = 0; q < B; ++q) c[r][q] = (unsigned)__builtin_nontemporal_load(cp[r] + min(q, wl) * kWave);
+      for (int q = 0; q < B; ++q) c[r][q] = (unsigned)__builtin_nontemporal_load(cp[r] + min(q, wl[r]) * kWave);
     for (int k = 0; k < wmax; k += B) {
       bool ok[NR][B];
       double xv[NR][B];
@@ -1156,7 +1226,7 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
 #pragma unroll
         for (int q = 0; q < B; ++q) {
           // (none past the last batch: a wave-uniform test)
-          cn[r][q] = k + B < wmax ? (unsigned)__builtin_nontemporal_load(cp[r] + min(k + B + q, wl) * kWave) : PAD;
+          cn[r][q] = k + B < wmax ? (unsigned)__builtin_nontemporal_load(cp[r] + min(k + B + q, wl[r]) * kWave) : PAD;
         }
       asm volatile("" ::: "memory");  // the next codes go out before the sums
       double av[NR][B];
@@ -1225,7 +1295,7 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
 // Persistent grid (the tables are staged once per workgroup); each XCD's
 // workgroups walk its contiguous share of the row blocks, NR consecutive
 // blocks at a time.
-template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK>
+template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK, int CPK = 1>
 __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
   extern __shared__ double vt[];  // nvtab doubles, then notab ints
   int* ot = reinterpret_cast<int*>(vt + p.nvtab);
@@ -1237,7 +1307,7 @@ __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
   const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
   const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
   for (int rb = r0 + (int)(blockIdx.x >> 3) * NR; rb < r1; rb += per_wg * NR)
-    code_rows_op<OP, CFSEL, B, MAP, NR, PK>(p, vt, ot, rb, r1);
+    code_rows_op<OP, CFSEL, B, MAP, NR, PK, CPK>(p, vt, ot, rb, r1);
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -1411,7 +1481,7 @@ __global__ void __launch_bounds__(256) k_sell_pw(SpArgs p) {
 // cp and vl point at the slice's first entry; P is the offset of slot k.
 template <int B, bool NT, class V>
 __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp, const V& vl, int& P, int k, int blen,
-                                          int (&c)[B], typename V::raw (&a)[B], int dexp = 0) {
+                                          int (&c)[B], typename V::raw (&a)[B]) {
   const int lane = threadIdx.x & (kWave - 1);
 #pragma unroll
   for (int q = 0; q < B; ++q) {
@@ -1423,16 +1493,34 @@ __device__ __forceinline__ void dict_load(const unsigned short* __restrict__ cp,
       P += cnt;
       continue;
     }
-#ifdef HVE_DICT_EXP
-    // timing only: 2 leaves out the column loads, 4 the value loads
-    c[q] = (dexp & 2) ? (int)((threadIdx.x + q) & 255) : (int)mload<NT>(cp + e);
-    a[q] = (dexp & 4) ? typename V::raw(1) : vl.template load<NT>(e);
-#else
-    (void)dexp;
     c[q] = (int)mload<NT>(cp + e);
     a[q] = vl.template load<NT>(e);
-#endif
     P += cnt;
+  }
+}
+
+// Phase 1 of the dictionary loops: x[dict[d0 .. d1)] of the workgroup's
+// group (the ascending distinct columns of its G slices) gathered into the
+// LDS x-tile, TG loads in flight per thread.
+template <int G, bool NT, int TG>
+__device__ __forceinline__ void dict_gather_tile(const SpArgs& p, int group, double* xl) {
+  constexpr int NT_ = 64 * G;
+  const int d0 = p.dict_ptr[group], m = p.dict_ptr[group + 1] - d0;
+  for (int j0 = 0; j0 < m; j0 += TG * NT_) {
+    int idx[TG];
+#pragma unroll
+    for (int i = 0; i < TG; ++i) {
+      const int j = j0 + i * NT_ + (int)threadIdx.x;
+      idx[i] = j < m ? mload<NT>(p.dict + d0 + j) : -1;
+    }
+    double v[TG];
+#pragma unroll
+    for (int i = 0; i < TG; ++i) v[i] = idx[i] >= 0 ? p.x[idx[i]] : 0.0;
+#pragma unroll
+    for (int i = 0; i < TG; ++i) {
+      const int j = j0 + i * NT_ + (int)threadIdx.x;
+      if (j < m) xl[j] = v[i];
+    }
   }
 }
 
@@ -1515,14 +1603,10 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   for (int k = 0; k < k0; ++k) P += __popcll(__ballot(k < blen));
   int c[B];
   typename V::raw a[B];
-  dict_load<B, NT>(cp, vl, P, k0, blen, c, a, p.dexp);
+  dict_load<B, NT>(cp, vl, P, k0, blen, c, a);
   // 1. x-tile -> LDS, TG loads in flight per thread
   constexpr int TG = HVE_DICT_TG;
   constexpr int NT_ = 64 * G;
-#ifdef HVE_DICT_EXP
-  if (p.dexp & 1) {  // timing only: no x-tile gather
-  } else
-#endif
   if (p.dict_ranges) {
     // Range dictionary: the tile is the concatenation of at most 63 column
     // ranges; lane k of every wave holds pair k (start, offset; the terminal
@@ -1561,24 +1645,7 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
       }
     }
   } else {
-    // x[dict[d0 .. d1)]: the ascending distinct columns, gathered
-    const int d0 = p.dict_ptr[group], m = p.dict_ptr[group + 1] - d0;
-    for (int j0 = 0; j0 < m; j0 += TG * NT_) {
-      int idx[TG];
-#pragma unroll
-      for (int i = 0; i < TG; ++i) {
-        const int j = j0 + i * NT_ + (int)threadIdx.x;
-        idx[i] = j < m ? mload<NT>(p.dict + d0 + j) : -1;
-      }
-      double v[TG];
-#pragma unroll
-      for (int i = 0; i < TG; ++i) v[i] = idx[i] >= 0 ? p.x[idx[i]] : 0.0;
-#pragma unroll
-      for (int i = 0; i < TG; ++i) {
-        const int j = j0 + i * NT_ + (int)threadIdx.x;
-        if (j < m) xl[j] = v[i];
-      }
-    }
+    dict_gather_tile<G, NT, TG>(p, group, xl);
   }
   __syncthreads();
   if (!wave_live) return;
@@ -1591,13 +1658,125 @@ __global__ void __launch_bounds__(64 * G) k_sell_dict(SpArgs p) {
   // (the empty asm keeps each batch's loads ahead of the other set's sums:
   // without it the compiler sinks them past the exit test, next to their use)
   for (int k = k0; k < width; k += 2 * B) {
-    dict_load<B, NT>(cp, vl, P, k + B, blen, c2, a2, p.dexp);
+    dict_load<B, NT>(cp, vl, P, k + B, blen, c2, a2);
     asm volatile("" ::: "memory");
     dict_sum<B>(xl, vl, c, a, k, llen, sub, t);
     if (k + B >= width) break;
-    dict_load<B, NT>(cp, vl, P, k + 2 * B, blen, c, a, p.dexp);
+    dict_load<B, NT>(cp, vl, P, k + 2 * B, blen, c, a);
     asm volatile("" ::: "memory");
     dict_sum<B>(xl, vl, c2, a2, k + B, llen, sub, t);
+  }
+  if (own) row_store_pre<OP, NT>(p, g, skip, t, uo, d, pre);
+}
+
+// ---------------------------------------------------------------------------
+// The dictionary loop over lane-packed streams (host: pack_dict_wide).  The
+// same slices, sorted rows, dictionaries and x-tile as k_sell_dict, but a lane
+// fetches two consecutive values of its row with one 16-B load and eight
+// consecutive local columns with another: per 16 entries 8 + 2 vector loads
+// instead of 32, each wave-instruction a contiguous run of 16 B per active
+// lane.  The per-entry loop is address-bound (A_1 at 512^3: TA busy 84 %,
+// traffic 1.06x its bytes, profiles/r05/02_opprof), so the lever is the count
+// of load instructions, not bytes.  Every row is still summed by its own lane
+// over its entries in stored order: the same bits (csr_matvec.c:207-327).
+// ---------------------------------------------------------------------------
+struct DictWBatch {  // 16 consecutive entries of a lane's row
+  uv4_t cw[2];       // two column octets
+  dv2_t av[8];       // eight value pairs
+};
+// Batch k's loads (k a multiple of 16).  Octet o / pair j of the slice is
+// stored for the lanes whose row reaches its first entry (rows sorted by
+// descending length), so its offset advances by a ballot count, wave-uniform.
+template <bool NT>
+__device__ __forceinline__ void dictw_load(const uv4_t* __restrict__ cb, const dv2_t* __restrict__ vb, int& Pc,
+                                           int& Pv, int k, int blen, DictWBatch& b) {
+  const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const bool in = k + 8 * o < blen;
+    const int cnt = __popcll(__builtin_amdgcn_ballot_w64(in));
+    b.cw[o] = in ? mload<NT>(cb + Pc + lane) : uv4_t(0u);
+    Pc += cnt;
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const bool in = k + 2 * j < blen;
+    const int cnt = __popcll(__builtin_amdgcn_ballot_w64(in));
+    b.av[j] = in ? mload<NT>(vb + Pv + lane) : dv2_t(0.0);
+    Pv += cnt;
+  }
+}
+// Batch k's sums: the 16 x-tile reads first (a left-out entry reads slot 0),
+// then the products added in stored order; entries before k0 (the diagonal
+// of OP_JAC) or past the row's end leave t unchanged by a select.
+__device__ __forceinline__ void dictw_sum(const double* xl, const DictWBatch& b, int k, int k0, int llen, bool sub,
+                                          double& t) {
+  double xv[16];
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const unsigned w = b.cw[e >> 3][(e & 7) >> 1];
+    const unsigned c = (e & 1) ? (w >> 16) : (w & 0xffffu);
+    const bool in = (k + e) < llen && (k + e) >= k0;
+    xv[e] = xl[in ? c : 0u];
+  }
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool in = (k + e) < llen && (k + e) >= k0;
+    const double pr = b.av[e >> 1][e & 1] * xv[e];
+    const double tn = sub ? t - pr : t + pr;
+    t = in ? tn : t;
+  }
+}
+template <int OP, bool CFSEL, bool NT, int G>
+__global__ void __launch_bounds__(64 * G) k_sell_dictw(SpArgs p) {
+  extern __shared__ double xl[];
+  const int group = map_block(p, xcd_logical_block(blockIdx.x, p.nblocks_pad));
+  if (group * G * kWave >= p.nrows) return;  // the whole workgroup is past the end
+  const int lane = threadIdx.x & (kWave - 1);
+  const int slice = group * G + (threadIdx.x >> 6);
+  const bool wave_live = slice * kWave < p.nrows;  // uniform per wave
+  const int row = slice * kWave + lane;
+  const int blen = wave_live ? mload<NT>(p.rowlen + row) : 0;  // 0 past the last row
+  const int width = __builtin_amdgcn_readfirstlane(blen);       // sorted: lane 0 is the longest
+  const int ns = (p.nrows + kWave - 1) / kWave;
+  const int sl = wave_live ? slice : 0;
+  const dv2_t* __restrict__ vb = reinterpret_cast<const dv2_t*>(p.val + p.wptr[sl]);
+  const uv4_t* __restrict__ cb = reinterpret_cast<const uv4_t*>(p.col16 + p.wptr[ns + 1 + sl]);
+  const bool own = wave_live && row < p.nrows;
+  const bool sub = op_subtracts<OP>() || (OP == OP_GENERAL && p.w == -1.0);
+  int g = 0;
+  bool skip = false;
+  double t = 0.0, uo = 0.0, d = 0.0, draw = 0.0;
+  RowPre pre;
+  if (own) {
+    g = p.rowmap ? mload<NT>(p.rowmap + row) : row;
+    if (CFSEL) skip = p.cf[g] != p.relax_points;
+    t = row_init<OP, NT>(p, g);
+    if (!skip) pre = row_preload<OP, NT>(p, g);
+    if (OP == OP_JAC) {
+      uo = p.x[g];
+      if (blen > 0) draw = vb[lane][0];  // the diagonal, stored first
+    }
+  }
+  const int llen = skip ? 0 : blen;
+  constexpr int k0 = (OP == OP_JAC) ? 1 : 0;
+  int Pc = 0, Pv = 0;
+  DictWBatch b0, b1;
+  // the first batch's loads go out before the x-tile gather and overlap it
+  dictw_load<NT>(cb, vb, Pc, Pv, 0, blen, b0);
+  dict_gather_tile<G, NT, HVE_DICT_TG>(p, group, xl);
+  __syncthreads();
+  if (!wave_live) return;
+  if (OP == OP_JAC && own) d = blen > 0 ? draw : 0.0;
+  // two register sets in turn, as in k_sell_dict
+  for (int k = 0; k < width; k += 32) {
+    dictw_load<NT>(cb, vb, Pc, Pv, k + 16, blen, b1);
+    asm volatile("" ::: "memory");
+    dictw_sum(xl, b0, k, k0, llen, sub, t);
+    if (k + 16 >= width) break;
+    dictw_load<NT>(cb, vb, Pc, Pv, k + 32, blen, b0);
+    asm volatile("" ::: "memory");
+    dictw_sum(xl, b1, k + 16, k0, llen, sub, t);
   }
   if (own) row_store_pre<OP, NT>(p, g, skip, t, uo, d, pre);
 }
@@ -1650,7 +1829,6 @@ struct GsArgs {
   int n, nteams, relax_points;
   unsigned gbytes;  // G's size in bytes (< 4 GiB: 32-bit buffer offsets)
   double w, omega;
-  int exp;  // HVE_GS_EXP (timing experiments, wrong results): 1 no value loads, 2 no source gathers
   // n when T is u itself (no pre-sweep copy of another vector): T codes read
   // C, so an off-block value shares the L2 lines its own team reads, and the
   // gather writes one copy instead of two
@@ -1754,14 +1932,14 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
         const int e = lane + 64 * t;
         const int o = base + (e < E ? e : 0);
         c[t] = gs_ld32(rc, o * 4);
-        a[t] = (p.exp & 1) ? 1.0 : gs_ld64(rv8, o * 8);
+        a[t] = gs_ld64(rv8, o * 8);
         tc[t] = WGT ? gs_ld32(rt, o * 4) : -1;
       }
 #pragma unroll
       for (int t = 0; t < kGsPer; ++t) {
         if (64 * t >= E) break;
         // unsigned byte offsets: G may exceed 2 GiB (< 4 GiB)
-        x[t] = (p.exp & 2) ? 1.0 : gs_ld64(rG, gs_src_off(c[t], (unsigned)p.n, p.tshift));
+        x[t] = gs_ld64(rG, gs_src_off(c[t], (unsigned)p.n, p.tshift));
         if (WGT) t2[t] = gs_ld64(rG, gs_src_off(tc[t], (unsigned)p.n, p.tshift));
       }
 #pragma unroll
@@ -2059,65 +2237,40 @@ __device__ __forceinline__ void gs_perm_range(int n, int& q0, int& q1) {
   q1 = (int)min<int64_t>((int64_t)q0 + per, n);
 }
 
-// u[rowmap[k]] = U[k]: the sweep's result back in natural row order (NAT:
-// u[i] = U[pos[i]], rows in order).
-template <bool NAT>
+// u[rowmap[k]] = U[k]: the sweep's result back in natural row order.  (Reading
+// the gathers in natural order and writing them permuted measured 0.9 ms slower
+// a cycle at 256^3, profiles/r04/gs_tune.)
 __global__ void __launch_bounds__(256) k_gs_scatter(int n, const int* __restrict__ map, const double* __restrict__ U,
                                                     double* __restrict__ u) {
   int q0, q1;
   gs_perm_range(n, q0, q1);
-  for (int q = q0 + threadIdx.x; q < q1; q += 256) {
-    if (NAT) u[q] = U[map[q]];
-    else u[map[q]] = U[q];
-  }
+  for (int q = q0 + threadIdx.x; q < q1; q += 256) u[map[q]] = U[q];
 }
 
-// NAT = false: positions in order, rows gathered (rowmap); NAT = true: rows in
-// natural order (coalesced reads), positions scattered (pos = rowmap^-1).
-template <bool NAT>
+// The sweep's vectors in its order: positions in order, rows gathered through
+// rowmap.  T (the pre-sweep copy) is written only for a symmetric sweep's
+// second half (tmp); otherwise the sweep's T codes read C (GsArgs::tshift).
 __global__ void __launch_bounds__(256) k_gs_gather(int n, int nhalo, const int* __restrict__ map,
                                                    const double* __restrict__ u, const double* __restrict__ tmp,
                                                    const double* __restrict__ f, double* __restrict__ G,
-                                                   double* __restrict__ F, bool writeT) {
+                                                   double* __restrict__ F) {
   int q0, q1;
   gs_perm_range(n, q0, q1);
   for (int q = q0 + threadIdx.x; q < q1; q += 256) {
-    const int i = NAT ? q : map[q], k = NAT ? map[q] : q;
+    const int i = map[q];
     const double v = u[i];
-    if (tmp || writeT) G[k] = tmp ? tmp[i] : v;  // else the sweep reads T from C
-    G[n + k] = v;
-    F[k] = f[i];
+    if (tmp) G[q] = tmp[i];
+    G[n + q] = v;
+    F[q] = f[i];
   }
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < nhalo; k += gridDim.x * blockDim.x) G[3 * n + k] = u[n + k];
-}
-
-// HVE_GS_TC=0: the gather writes T = u as its own copy and T codes read it
-static bool gs_t_from_c() {
-  static const bool v = [] {
-    const char* e = getenv("HVE_GS_TC");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
-static int gs_natural_order() {
-  static const int v = [] {
-    const char* e = getenv("HVE_GS_NAT");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
 }
 
 hipError_t launch_gs_gather(const GsView& S, const double* u, const double* tmp, const double* f, int nhalo,
                             double* G, double* F, hipStream_t st) {
   if (S.nrows <= 0) return hipSuccess;
   const int grid = std::min((S.nrows + 255) / 256 + 7, 256 * 16) & ~7;
-  if (gs_natural_order() & 1)
-    hipLaunchKernelGGL(k_gs_gather<true>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.pos, u, tmp, f, G, F,
-                       !gs_t_from_c());
-  else
-    hipLaunchKernelGGL(k_gs_gather<false>, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.rowmap, u, tmp, f, G, F,
-                       !gs_t_from_c());
+  hipLaunchKernelGGL(k_gs_gather, dim3(grid), dim3(256), 0, st, S.nrows, nhalo, S.rowmap, u, tmp, f, G, F);
   return hipGetLastError();
 }
 
@@ -2129,9 +2282,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   a.vidx = S.vidx8; a.vtab = S.vtab; a.nvtab = S.nvtab;
   a.l1 = S.l1; a.cf = S.cf; a.G = G; a.F = F; a.u = u;
   a.n = S.nrows; a.nteams = S.nteams; a.relax_points = relax_points; a.w = w; a.omega = omega;
-  a.tshift = (t_is_c && gs_t_from_c()) ? (unsigned)S.nrows : 0u;
-  static const int gs_exp = getenv("HVE_GS_EXP") ? atoi(getenv("HVE_GS_EXP")) : 0;
-  a.exp = gs_exp;
+  a.tshift = t_is_c ? (unsigned)S.nrows : 0u;
   const uint64_t gbytes = (3 * (uint64_t)S.nrows + (uint64_t)nhalo) * sizeof(double);
   if (gbytes > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit buffer offsets (about 178M rows a GPU)
   a.gbytes = (unsigned)gbytes;
@@ -2156,11 +2307,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
 #undef HVE_GW
 #undef HVE_G
   const int sgrid = std::min((S.nrows + 255) / 256 + 7, 256 * 16) & ~7;
-  if (gs_natural_order() & 2)
-    hipLaunchKernelGGL(k_gs_scatter<true>, dim3(sgrid), dim3(256), 0, st, S.nrows, S.pos, G + 2 * (size_t)S.nrows, u);
-  else
-    hipLaunchKernelGGL(k_gs_scatter<false>, dim3(sgrid), dim3(256), 0, st, S.nrows, S.rowmap, G + 2 * (size_t)S.nrows,
-                       u);
+  hipLaunchKernelGGL(k_gs_scatter, dim3(sgrid), dim3(256), 0, st, S.nrows, S.rowmap, G + 2 * (size_t)S.nrows, u);
   return hipGetLastError();
 }
 
@@ -2387,13 +2534,37 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
   const bool pipe = sell_pipe_override() >= 0 ? sell_pipe_override() == 1 : M.pipe != 0;
   const bool nt = sell_nt();
   const bool jag = M.rowlen != nullptr;
-  a.dexp = knob(12);
   if (M.col16) {  // dictionary layout: G waves per workgroup share an x-tile in LDS
     const int G = M.dict_group;
     const int ngroups = ((M.nrows + 63) / 64 + G - 1) / G;
     a.nblocks_pad = (ngroups + 7) / 8 * 8;
     a.dmax = M.dmax;
+    a.wptr = M.wptr;
     const dim3 dgrid(a.nblocks_pad), dblock(64 * G);
+    if (M.wptr) {  // lane-packed streams (k_sell_dictw), G = 1 or 4
+      if (G != 1 && G != 4) return hipErrorInvalidValue;
+      const size_t lds = (size_t)M.dmax * sizeof(double);
+#define HVE_DW(OPV, CF)                                                                              \
+  if (G == 4) {                                                                                      \
+    if (nt) hipLaunchKernelGGL((k_sell_dictw<OPV, CF, true, 4>), dgrid, dblock, lds, s, a);          \
+    else hipLaunchKernelGGL((k_sell_dictw<OPV, CF, false, 4>), dgrid, dblock, lds, s, a);            \
+  } else {                                                                                           \
+    if (nt) hipLaunchKernelGGL((k_sell_dictw<OPV, CF, true, 1>), dgrid, dblock, lds, s, a);          \
+    else hipLaunchKernelGGL((k_sell_dictw<OPV, CF, false, 1>), dgrid, dblock, lds, s, a);            \
+  }
+#define HVE_DWL(OPV)                                                  \
+  case OPV:                                                           \
+    if (cfsel) { HVE_DW(OPV, true) } else { HVE_DW(OPV, false) }     \
+    break;
+      switch (op) {
+        HVE_DWL(OP_RESID) HVE_DWL(OP_MATVEC) HVE_DWL(OP_L1JAC) HVE_DWL(OP_L1JAC_W) HVE_DWL(OP_JAC)
+        HVE_DWL(OP_PROLONG) HVE_DWL(OP_RESTRICT) HVE_DWL(OP_GENERAL) HVE_DWL(OP_RESID_L1JAC) HVE_DWL(OP_RESTRICT_ZG)
+        default: return hipErrorInvalidValue;
+      }
+#undef HVE_DWL
+#undef HVE_DW
+      return hipGetLastError();
+    }
     if (M.vidx16) {  // 16-bit value indices: the table staged after the x-tile (one slice per workgroup)
       if (G != 1) return hipErrorInvalidValue;
       const size_t ldsv = (size_t)(M.dmax + M.nvtab) * sizeof(double);
@@ -2564,9 +2735,15 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     const bool map = M.cmap != nullptr;
     const int nr = knob(0) > 0 ? knob(0) : 1;   // row blocks per workgroup step
     const int cb = knob(1) > 0 ? knob(1) : 8;   // codes per batch
+    const int cpk = (M.code16 && !map) ? M.code_pack : 1;
+    if (cpk != 1 && cpk != 4 && cpk != 8) return hipErrorInvalidValue;
+#define HVE_CP(OPV, CF, BB, NRV)                                                                             \
+  if (cpk == 8) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, false, 8>), cgrid, block, lds, s, a); \
+  else hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, false, 4>), cgrid, block, lds, s, a);
 #define HVE_C2(OPV, CF, BB, NRV)                                                                  \
   if (M.code32) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, true>), cgrid, block, lds, s, a); \
   else if (map) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, true, NRV, false>), cgrid, block, lds, s, a); \
+  else if (cpk > 1) { HVE_CP(OPV, CF, (BB < 8 ? 8 : BB), NRV) } \
   else hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, false>), cgrid, block, lds, s, a);
 #define HVE_C(OPV, CF)                                                    \
   if (CF) { HVE_C2(OPV, CF, 8, 1) }                                        \
@@ -2587,6 +2764,7 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_CL
 #undef HVE_C
 #undef HVE_C2
+#undef HVE_CP
     return hipGetLastError();
   }
   if (M.vidx16) {  // 32-bit columns, 16-bit value indices (padded or jagged)
@@ -2686,15 +2864,9 @@ bool sell_nt() {
   }();
   return v;
 }
-// Jagged operators: per-wave product-parallel loop (k_sell_pw) instead of the
-// lane-per-row loop; HVE_SELL_PW=0|1.
-bool sell_pw() {
-  static const bool v = [] {
-    const char* e = getenv("HVE_SELL_PW");
-    return e ? atoi(e) != 0 : false;
-  }();
-  return v;
-}
+// Jagged operators: the lane-per-row loop; the per-wave product-parallel loop
+// (k_sell_pw, 5-8 % slower on R_0 / A_1) only under policy 4 (tests).
+bool sell_pw() { return false; }
 int sell_pipe_override() {
   static const int p = [] {
     const char* e = getenv("HVE_SELL_PIPE");
@@ -2858,31 +3030,17 @@ int dot_num_parts(int n) {
   int b = blocks_for(n);
   return b < 1024 ? (b < 1 ? 1 : b) : 1024;
 }
-// Slices per wave of the stencil loop (k_sell_stencil): HVE_STENCIL_R=1|2|4.
-// Measured on MI355X (256^3 A0): 1 / 2 / 4 slices 0.105 / 0.107 / 0.113 ms;
-// 512^3 with slot patterns: 0.877 / 0.897 / 0.898 ms, 15.6 / 17.0 / 17.9 ms
-// per solve iteration.
-int stencil_slices_per_wave() {
-  static const int r = [] {
-    const char* e = getenv("HVE_STENCIL_R");
-    const int v = e ? atoi(e) : 1;
-    return (v == 1 || v == 2 || v == 4) ? v : 1;
-  }();
-  return r;
-}
+// Slices per wave of the stencil loop (k_sell_stencil): 1.  Measured on
+// MI355X (256^3 A0): 1 / 2 / 4 slices 0.105 / 0.107 / 0.113 ms; 512^3 with
+// slot patterns: 0.877 / 0.897 / 0.898 ms, 15.6 / 17.0 / 17.9 ms per solve
+// iteration.  (The kernel keeps R as a template parameter.)
+int stencil_slices_per_wave() { return 1; }
 // Grid of the stencil loop: one workgroup per block of 4R slices, whole XCD
 // rounds.  (A persistent grid that fetched each next block's traversal entry
 // and patterns ahead measured slower: 512^3 A0 1.60-1.68 ms against 0.87.)
 // One scalar load of {slice, pattern} per wave (SellView::wave_map) instead of
-// the traversal map and then the slice's pattern; HVE_STENCIL_WMAP=0 keeps the
-// two dependent loads.
-bool stencil_wave_map() {
-  static const bool v = [] {
-    const char* e = getenv("HVE_STENCIL_WMAP");
-    return e ? atoi(e) != 0 : true;
-  }();
-  return v;
-}
+// the traversal map and then the slice's pattern.
+bool stencil_wave_map() { return true; }
 int stencil_grid(int nrows) {
   const int R = stencil_slices_per_wave();
   const int nlb = ((std::max(nrows, 1) + 63) / 64 + 4 * R - 1) / (4 * R);

@@ -217,6 +217,16 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       nnz_pad = (int64_t)sp.back();
       batch = 8;
       pipe = 1;
+      // Lane-packed codes (R_0: anchors, no position map): a lane's CPK
+      // consecutive codes in one 8- / 16-byte load instead of one 2-byte load
+      // per entry (its loop is address-bound: TA busy 90 %, 2878 vector reads
+      // a wave, profiles/r05/02_opprof).  HVE_CODE_PACK=1|4|8 (default 8).
+      static const int cpk_env = [] {
+        const char* e = getenv("HVE_CODE_PACK");
+        return e ? atoi(e) : 8;
+      }();
+      code_pack = (!coded->cmap || coded->cmap->empty()) && (cpk_env == 4 || cpk_env == 8) ? cpk_env : 1;
+      if (code_pack > 1) pack_codes_lanes(sp, cd, code_pack);
       slice_ptr = dupload(sp.data(), sp.size());
       code16 = dupload(cd.data(), cd.size());
       otab = dupload(ot.data(), ot.size());
@@ -233,8 +243,9 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
         cmap_n = (int64_t)coded->cmap->size();
       }
       if (getenv("HVE_LAYOUT_LOG"))
-        fprintf(stderr, "[layout] coded rows=%d offsets=%d values=%d vbits=%d pad=%.2f\n", A.nrows, notab, nvtab, vbits,
-                (double)nnz_pad / std::max<int64_t>(1, nnz));
+        fprintf(stderr, "[layout] coded rows=%d offsets=%d values=%d vbits=%d pad=%.2f (%.2f packed by %d)\n", A.nrows,
+                notab, nvtab, vbits, (double)nnz_pad / std::max<int64_t>(1, nnz),
+                (double)sp.back() / std::max<int64_t>(1, nnz), code_pack);
       if (!rowmap_h.empty()) {
         bool ident = true;
         for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
@@ -253,12 +264,9 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
   // finest 7-point operator is nearly uniform and keeps contiguous rows.
   // Measured on MI355X (256^3 Poisson, PMIS/ext+i): sorting a 1024-row window
   // cut level-1 padding from 1.40x to 1.03x but slowed its SpMV 745 -> 1073 us,
-  // because a wave's 64 rows then gather x from a 16x wider range.  Off by
-  // default; HVE_SELL_SIGMA=<rows> re-enables it for experiments.
-  static const int sigma_env = [] {
-    const char* e = getenv("HVE_SELL_SIGMA");
-    return e ? atoi(e) : 0;
-  }();
+  // because a wave's 64 rows then gather x from a 16x wider range, so it is
+  // off (build_sell_host keeps the sigma parameter).
+  constexpr int sigma_env = 0;
   // Jagged layout (no stored padding) for large operators with long rows and
   // more than 10% padding: level-1/2 Galerkin A and R = P^T.  Measured on
   // MI355X (256^3, PMIS/ext+i): R_0 -16%, A_1 -15%, R_1 -14%, A_2 -4%; but
@@ -315,7 +323,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
     wide = policy == 3 ? 1 : 0;
     jag = (policy == 2 || policy == 4 || policy == 9) && A.nnz() > 0;
     pw = policy == 4 && jag;
-    use_dict = (policy == 5 || policy == 10) && A.nnz() > 0;
+    use_dict = (policy == 5 || policy == 10 || policy == 14) && A.nnz() > 0;
   }
   // 16-bit column deltas against per-(slice, slot) bases where the padded
   // layout stays and rows are stencil-long (the finest A): 10 B an entry
@@ -485,13 +493,8 @@ dict:
     // ranges, copied instead of gathered through a 4-byte index list) where
     // the ranges cover at most 1.5x the distinct columns.  Measured on MI355X:
     // A_1 at 256^3 411 vs 412 us, at 512^3 4.31 vs 3.66 ms (the larger tiles
-    // cost occupancy), so it is off by default: HVE_DICT_RANGES=1 turns it on,
-    // policy 10 forces it (tests).
-    static const int ranges_env = [] {
-      const char* e = getenv("HVE_DICT_RANGES");
-      return e ? atoi(e) : 0;
-    }();
-    const bool try_ranges = policy == 10 || (policy == 0 && ranges_env != 0 && A.nrows == A.ncols);
+    // cost occupancy), so only policy 10 takes it (tests).
+    const bool try_ranges = policy == 10;
     bool built = false, ranges = false;
     if (try_ranges) {
       built = build_sell_dict_host(A, group > 1 ? 8192 : 4096, group, perm, sp, rl2, c16, val, dp, dc, mxd, 63,
@@ -532,17 +535,13 @@ dict:
                 (double)dc.size() / std::max<size_t>(1, dp.size() - 1));
       rowlen = dupload(rl2.data(), rl2.size());
       slice_ptr = dupload(sp.data(), sp.size());
-      col16 = dupload(c16.data(), c16.size());
       // one-slice dictionaries (restrictions) whose values take at most 4096
       // bit patterns: 16-bit indices into a table staged in LDS after the
       // x-tile, 4 B an entry instead of 10.  Measured on R_0 at 512^3 (its
       // 64-row slices hold 573 distinct fine columns, 9 a row): 3.73 ms
       // against 1.59 for the offset-coded layout, so it is taken only under
-      // the forced dictionary policy (5, tested bitwise) or HVE_DICT_VT=1.
-      static const int dict_vt_env = [] {
-        const char* e = getenv("HVE_DICT_VT");
-        return e ? atoi(e) : 0;
-      }();
+      // the forced dictionary policy (5, tested bitwise).
+      constexpr int dict_vt_env = 0;
       hvec<unsigned short> vi16;
       std::vector<double> tab;
       if (group == 1 && !ranges && !relax_ops && (dict_vt_env != 0 || policy == 5) && sell_valtab_env() != 0 &&
@@ -550,8 +549,32 @@ dict:
         vidx16 = dupload(vi16.data(), vi16.size());
         vtab = dupload(tab.data(), tab.size());
         nvtab = (int)tab.size();
+        col16 = dupload(c16.data(), c16.size());
       } else {
-        this->val = dupload(val.data(), val.size());
+        // Lane-packed streams (k_sell_dictw): one 16-B load brings a lane two
+        // values or eight columns of its row, instead of one 8-B value load and
+        // one 2-B column load per entry (the per-entry loop is address-bound:
+        // TA busy 84 % on A_1, profiles/r05/02_opprof).  HVE_DICT_WIDE=0 keeps
+        // the per-entry streams; range dictionaries keep them, and policy 14
+        // forces them (tests).
+        static const int wide_env = [] {
+          const char* e = getenv("HVE_DICT_WIDE");
+          return e ? atoi(e) : 1;
+        }();
+        std::vector<int> wp;
+        hvec<unsigned short> cw;
+        hvec<double> vw;
+        if (!ranges && (group == 1 || group == 4) && wide_env != 0 && policy != 14 && pack_dict_wide(sp, rl2, c16, val, wp, cw, vw)) {
+          wptr = dupload(wp.data(), wp.size());
+          col16 = dupload(cw.data(), cw.size());
+          this->val = dupload(vw.data(), vw.size());
+          wval_n = (int64_t)vw.size();
+          wcol_n = (int64_t)cw.size();
+          lap("dict lane packing");
+        } else {
+          col16 = dupload(c16.data(), c16.size());
+          this->val = dupload(val.data(), val.size());
+        }
       }
       dict_ptr = dupload(dp.data(), dp.size());
       dict = dupload(dc.data(), std::max<size_t>(1, dc.size()));
@@ -719,7 +742,10 @@ void DevSell::release() {
   for (void* q : {(void*)code16, (void*)otab, (void*)anc, (void*)cmap})
     if (q) (void)hipFree(q);
   code16 = nullptr; otab = nullptr; anc = nullptr; cmap = nullptr;
-  notab = vbits = 0; anc_n = cmap_n = 0;
+  notab = vbits = 0; anc_n = cmap_n = 0; code_pack = 1;
+  if (wptr) (void)hipFree(wptr);
+  wptr = nullptr;
+  wval_n = wcol_n = 0;
   if (gslot) (void)hipFree(gslot);
   gslot = nullptr;
   gnx = gny = gnz = gzc = gz0 = gz1 = 0;
@@ -731,19 +757,9 @@ void DevSell::release() {
 // one LDS chunk.  Measured at 256^3 (relax 13/14): level 0 (7 entries a row)
 // 0.70 ms a sweep with 64 rows against 1.01 with 16; level 1 (29 a row) 1.12
 // ms with 16 against 2.34 with 64; the cycle 8.03 / 8.35 / 9.11 ms with wide
-// teams of 4 / 8 / 16 rows (profiles/r04/gs_tune).  HVE_GS_TEAM_ROWS /
-// HVE_GS_TEAM_ROWS_WIDE override (tuning).
+// teams of 4 / 8 / 16 rows (profiles/r04/gs_tune).
 static int gs_team_rows(const CSR& A) {
-  static const int narrow = [] {
-    const char* e = getenv("HVE_GS_TEAM_ROWS");
-    const int r = e ? atoi(e) : 0;
-    return r > 0 ? r : 64;
-  }();
-  static const int wide = [] {
-    const char* e = getenv("HVE_GS_TEAM_ROWS_WIDE");
-    const int r = e ? atoi(e) : 0;
-    return r > 0 ? r : 4;
-  }();
+  constexpr int narrow = 64, wide = 4;
   int w = 0;
   for (int i = 0; i < A.nrows; ++i) w = std::max(w, A.i[i + 1] - A.i[i]);
   return w > 8 ? wide : narrow;
@@ -771,11 +787,8 @@ void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forw
   code = dupload(S.code.data(), std::max<size_t>(1, S.code.size()));
   // At most 256 distinct values (level 0 of a constant-coefficient stencil):
   // 8-bit indices into a table, 1 B an entry instead of 8, read only by the
-  // pipelined sweep.  HVE_GS_VT=0 keeps the values.
-  static const int vt_env = [] {
-    const char* e = getenv("HVE_GS_VT");
-    return e ? atoi(e) : 1;
-  }();
+  // pipelined sweep.
+  constexpr int vt_env = 1;
   {
     hvec<unsigned char> vi;
     std::vector<double> tab;
@@ -970,7 +983,7 @@ static bool grid_strides(const CSR& A, const std::vector<int>& map, int n_loc, i
 // keyed as (XCD band of f's y coordinate, f).  Each XCD then streams one band
 // of the grid through all its planes, so the x window that the neighbouring
 // planes share stays in its 4 MiB L2 even when a whole plane does not (512^3:
-// 2 MiB of x per plane).  HVE_BLOCK_ORDER=0 keeps the natural order.
+// 2 MiB of x per plane).
 static void locality_keys(const RankHierarchy& R, int agg_level, int nbands, std::vector<std::vector<int64_t>>& keys) {
   keys.assign(R.lev.size(), {});
   if (nbands <= 0 || R.lev.empty()) return;
@@ -1008,14 +1021,10 @@ static void locality_keys(const RankHierarchy& R, int agg_level, int nbands, std
 // row is taken from its level-0 grid point f, with sides of about the cube
 // root of the fine points 256 of the level's rows cover (powers of two), and
 // rows are keyed (tile, f).  Only the row order of the layout changes, not any
-// row's sum.  HVE_DICT_TILES=0 keeps the natural order.
+// row's sum.
 static void tile_keys(const RankHierarchy& R, int agg_level, std::vector<std::vector<int64_t>>& keys) {
   keys.assign(R.lev.size(), {});
-  static const int on = [] {
-    const char* e = getenv("HVE_DICT_TILES");
-    return e ? atoi(e) : 1;
-  }();
-  if (!on || R.lev.empty()) return;
+  if (R.lev.empty()) return;
   const RankLevel& L0 = R.lev[0];
   int64_t plane = 0, line = 0;
   if (!grid_strides(L0.A.interior, L0.A.map_int, L0.n_loc, &plane, &line)) return;
@@ -1049,18 +1058,6 @@ static void tile_keys(const RankHierarchy& R, int agg_level, std::vector<std::ve
         tx = std::min<int64_t>(nx, 64);
         ty = std::min<int64_t>(ny, 4);
         tz = std::min<int64_t>(nz, 4);
-      }
-      // "tx,ty,tz" in fine points (tuning): HVE_DICT_TILE for level 1, HVE_DICT_TILE2 beyond
-      static const char* shape1 = getenv("HVE_DICT_TILE");
-      static const char* shape2 = getenv("HVE_DICT_TILE2");
-      const char* shape = l == 1 ? shape1 : shape2;
-      if (shape) {
-        long long a = 0, b = 0, c = 0;
-        if (sscanf(shape, "%lld,%lld,%lld", &a, &b, &c) == 3 && a > 0 && b > 0 && c > 0) {
-          tx = std::min<int64_t>(nx, a);
-          ty = std::min<int64_t>(ny, b);
-          tz = std::min<int64_t>(nz, c);
-        }
       }
       const int64_t ntx = (nx + tx - 1) / tx, nty = (ny + ty - 1) / ty;
       std::vector<int64_t>& k = keys[l];
@@ -1179,20 +1176,14 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
   agg_level_ = comm_ ? R.agg_level : -1;
   agg_starts_ = R.agg_starts;
   std::vector<std::vector<int64_t>> keys;
-  static const int nbands_env = [] {
-    const char* e = getenv("HVE_BLOCK_ORDER");
-    return e ? atoi(e) : 8;  // bands of the grid's y extent; 0 = natural order
-  }();
+  constexpr int nbands_env = 8;  // bands of the grid's y extent (0 would be natural order)
   locality_keys(R, agg_level_, nbands_env, keys);
   // Restrictions gather from a window of ~10 fine planes per in-flight coarse
   // row range (R_0: the fine residual), wider than A's 3 planes, so they keep
   // it in L2 with narrower bands.  Measured on MI355X (512^3, R_0 alone):
   // 0 / 8 / 16 / 32 / 64 / 128 / 256 bands 1.92 / 1.81 / 1.67 / 1.63 / 1.61 /
-  // 1.62 / 1.78 ms; A_0 and P_0 are best at 8.  HVE_BLOCK_ORDER_R overrides.
-  static const int nbands_r_env = [] {
-    const char* e = getenv("HVE_BLOCK_ORDER_R");
-    return e ? atoi(e) : 32;
-  }();
+  // 1.62 / 1.78 ms; A_0 and P_0 are best at 8.
+  constexpr int nbands_r_env = 32;
   std::vector<std::vector<int64_t>> keys_r;
   if (nbands_r_env != nbands_env) locality_keys(R, agg_level_, nbands_r_env, keys_r);
   const std::vector<std::vector<int64_t>>& kr = nbands_r_env != nbands_env ? keys_r : keys;
@@ -1212,12 +1203,8 @@ void DevAMG::build(const RankHierarchy& R, DevComm* comm) {
     const std::vector<int64_t>* kc = (l + 1 < nl && !kr[l + 1].empty()) ? &kr[l + 1] : nullptr;
     // A on level 1 and the restrictions (measured at 512^3: A_1 3.42 -> 3.24 ms,
     // R_1 0.582 -> 0.560; A_2 0.873 -> 0.936, so A_2 keeps the natural order)
-    // HVE_DICT_TILES_A2=1 tiles A_2 too (64x4x4: 0.872 -> 0.932 ms at 512^3)
-    static const int a2_tiles = [] {
-      const char* e = getenv("HVE_DICT_TILES_A2");
-      return e ? atoi(e) : 0;
-    }();
-    const std::vector<int64_t>* tl = ((l == 1 || (l >= 2 && a2_tiles)) && !tiles[l].empty()) ? &tiles[l] : nullptr;
+    // (tiling A_2 too, 64x4x4: 0.872 -> 0.932 ms at 512^3)
+    const std::vector<int64_t>* tl = (l == 1 && !tiles[l].empty()) ? &tiles[l] : nullptr;
     const std::vector<int64_t>* tc = (l + 1 < nl && !tiles[l + 1].empty()) ? &tiles[l + 1] : nullptr;
     D.A.relax_ops = true;
     D.A.upload(L.A, prm.sell_policy, kl, nullptr, tl);

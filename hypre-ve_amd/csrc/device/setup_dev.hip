@@ -837,8 +837,7 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   const size_t lds = (size_t)3 * cap * sizeof(int) + (size_t)(cap / 2) * sizeof(double);
   DBuf<int> cnt(n);
   const int grid = grid_rows(n, 32);
-  // HVE_DSETUP_PCOUNT=0: the one-lane count passes
-  static const int pcount = getenv("HVE_DSETUP_PCOUNT") ? atoi(getenv("HVE_DSETUP_PCOUNT")) : 1;
+  constexpr int pcount = 1;  // the wave-parallel count (one lane a row: level-1 ext+i count 1.7 s against 0.3 at 512^3)
   if (pcount)
     hipLaunchKernelGGL(k_extpi_count_w, dim3(grid), dim3(64), (size_t)cap * 8, 0, dS, dcf.p, n, cap, lg, cnt.p);
   else
@@ -865,13 +864,10 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   DBuf<double> Pa((size_t)t);
   Pi.up(hp);
   // the count buffer keeps -1 on overflow rows: the fill pass skips them.
-  // HVE_EXTPI_SERIAL=1 / 0 forces the one-lane fill (k_extpi<true>) / the
-  // wave-shared one.
   // Rows with few candidates (the finest 7-point level: at most 43) run the
   // one-lane fill; the wave-shared one pays its synchronisation only on the
   // long Galerkin rows (512^3, level 0: 0.89 vs 4.3 s; level 1: 6.9 vs 1.6 s).
-  static const int serial_env = getenv("HVE_EXTPI_SERIAL") ? atoi(getenv("HVE_EXTPI_SERIAL")) : -1;
-  const bool serial_fill = serial_env >= 0 ? serial_env != 0 : bmax <= 64;
+  const bool serial_fill = bmax <= 64;
   if (serial_fill)
     hipLaunchKernelGGL((k_extpi<true>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
                        Pi.p, Pj.p, Pa.p);
@@ -1008,7 +1004,7 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   const DCsr dR{Ri.p, Rj.p, Ra.p, nc};
   DBuf<int> len((size_t)nc);
   const int grid = grid_rows(nc, 32);
-  static const int pcount = getenv("HVE_DSETUP_PCOUNT") ? atoi(getenv("HVE_DSETUP_PCOUNT")) : 1;
+  constexpr int pcount = 1;  // the wave-parallel count
   if (pcount)
     hipLaunchKernelGGL(k_rap_count_w, dim3(grid), dim3(64), (size_t)(cap1 + cap2) * 8 + (size_t)(cap1 / 2) * 4, 0, dR,
                        dA.view(), dP.view(), cap1, lg1, cap2, lg2, len.p);

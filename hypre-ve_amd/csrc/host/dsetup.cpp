@@ -142,11 +142,16 @@ void map_cols(CSR& M, const Universe& U) {
 }
 
 // ---------------------------------------------------------------------------
-// PMIS (coarsen_type 8), setup.cpp coarsen_pmis with cf_init 0, distributed.
+// PMIS (coarsen_type 8, cf_init 0; 9, cf_init 2), distributed as hypre runs
+// it on N processes (setup.cpp coarsen_pmis with rank starts, the N-rank
+// emulation pinned to the reference's np > 1 runs): the random measures from
+// one stream per rank, seed 2747 + rank from the rank's first row
+// (par_indepset.c:45, seq_rand 0), or the global stream for coarsen_type 9.
 // ---------------------------------------------------------------------------
-// cf_init 3 (the aggressive second pass, setup.cpp coarsen_pmis(S2, 3)):
-// rows without strong connections become C points, and the first pass skips
-// the independent-set selection (only F points are decided there: order-free).
+// cf_init 3 / 4 (the aggressive second pass of type 8 / 9, setup.cpp
+// coarsen_pmis(S2, 3 | 4)): rows without strong connections become C points,
+// and the first pass skips the independent-set selection; its F decisions
+// read own-rank markers only (CF_marker_offd is 0 there).
 // cf_init 1 (HMIS's second stage, hmis_dist): cf holds this rank's Ruge first
 // pass; the random measures come from one stream per rank (seed 2747 + rank
 // from the rank's first row, par_indepset.c:25 as hypre runs it on N
@@ -167,10 +172,14 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
   for (int p = 0; p < size; ++p)
     for (int g : got[p]) mcount[g - first]++;
   std::vector<double> measure(n);
+  // par_indepset.c:45-57: seed 2747 + my_id, one hypre_Rand() per local row
+  // from the rank's first row; seq_rand (CF_init 2 / 4: coarsen_type 9) seeds
+  // 2747 and skips the rows of the ranks before, i.e. the global stream
+  const bool seq_rand = cf_init == 2 || cf_init == 4;
   for (int r = 0; r < n; ++r) {
     measure[r] = (double)mcount[r];
-    if (cf_init == 1) measure[r] += hypre_rand_at(r, 2747 + rank);  // the rank's own stream
-    else measure[r] += hypre_rand_at((int64_t)first + r, 2747);  // par_indepset.c:25 at the global row
+    if (seq_rand) measure[r] += hypre_rand_at((int64_t)first + r, 2747);
+    else measure[r] += hypre_rand_at(r, 2747 + rank);  // the rank's own stream
   }
   std::vector<int> off;
   for (int c : S.j)
@@ -205,7 +214,7 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
     cf.assign(n, 0);
     for (int r = 0; r < n; ++r) {
       if (S.i[r + 1] - S.i[r] == 0) {
-        cf[r] = cf_init == 3 ? C_PT : SF_PT;
+        cf[r] = (cf_init == 3 || cf_init == 4) ? C_PT : SF_PT;
         measure[r] = 0;
       } else {
         graph.push_back(r);
@@ -252,9 +261,10 @@ void pmis_dist(const Pattern& S, int first, int n, const std::vector<int>& start
     }
     gp.push(gdem, cf.data(), [](int cur, int flag) { return flag ? 0 : cur; }, comm);
     gp.pull(cf.data(), gcf, comm);
-    if (cf_init == 1 && iter == 1) {
-      // the seeded sweep: row order, own-rank markers only (a neighbour j < i
-      // already holds its new marker)
+    if (cf_init != 0 && iter == 1) {
+      // the first sweep of a seeded / CF_init run (no selection before it):
+      // row order, own-rank markers only, CF_marker_offd still 0
+      // (par_coarsen.c:2348; a neighbour j < i already holds its new marker)
       for (int ig = 0; ig < gs; ++ig) {
         const int i = graph[ig];
         if (measure[i] < 1) cf[i] = F_PT;
@@ -683,34 +693,6 @@ void build_ghost_universe(const CSR& A, const Pattern& S, int first, int n, cons
   }
 }
 
-// Global index of each owned point of class `sel` (cf > 0 by default) from
-// `cstart` on; -1 elsewhere.
-std::vector<int> class_index(const std::vector<int>& cf, int cstart, bool (*sel)(int)) {
-  std::vector<int> f2c(cf.size(), -1);
-  int cc = cstart;
-  for (size_t i = 0; i < cf.size(); ++i)
-    if (sel(cf[i])) f2c[i] = cc++;
-  return f2c;
-}
-bool is_c(int v) { return v > 0; }
-
-// Rows [0, nrows) of a universe product P (columns: the universe's points of
-// the column class in universe order, as fffc / extpi number them) with
-// global column indices: gidxU holds every universe point's global index in
-// that class (-1 outside it).
-CSR owned_rows_global_cols(const CSR& Pu, int nrows, const std::vector<int>& gidxU, int ncols_glob) {
-  std::vector<int> uc2g;
-  for (int v : gidxU)
-    if (v >= 0) uc2g.push_back(v);
-  CSR P;
-  P.resize_rows(nrows, ncols_glob);
-  for (int r = 0; r < nrows; ++r) P.i[r + 1] = Pu.i[r + 1];
-  P.j.assign(Pu.j.begin(), Pu.j.begin() + Pu.i[nrows]);
-  P.a.assign(Pu.a.begin(), Pu.a.begin() + Pu.i[nrows]);
-  for (int& c : P.j) c = uc2g.at(c);
-  return P;
-}
-
 // ---------------------------------------------------------------------------
 // Ext+i (plus_i) or ext (interp_type 14, par_lr_interp.c:4686) rows of the
 // owned fine points (extpi_core over the ghost universe).
@@ -727,96 +709,6 @@ void extpi_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, int 
   build_ghost_universe(A, S, first, n, starts, strong_threshold, max_row_sum, comm, G);
   const std::vector<int> cfU = G.extend(cf, comm), f2cU = G.extend(f2c, comm);
   extpi_core(G.A, G.S, cfU, f2cU, n, (int)cstarts[size], G.U.size(), P, plus_i);
-}
-
-// ---------------------------------------------------------------------------
-// The matrix-matrix interpolations over the ghost universe (setup.cpp:
-// par_mod_lr_interp.c's ModExt 16 / ModExtPI 17 / ModExtPE 18, and the
-// 2-stage agg_interp_type 5 / 7 of par_amg_setup.c:1575-1689): the one-process
-// builders run on the universe, and the owned rows are kept.  Every owned row
-// reads only owned and G1 rows (its F neighbours' As_FF / As_FC rows and their
-// scalings), so it is the one-process row.  hypre_ParMatmul's allsquare is
-// decided by the global sizes; a square product (a zero diagonal at the
-// row's own index) is refused.
-// ---------------------------------------------------------------------------
-int64_t L0_rows_glob(HostComm& comm, int n) { return comm.allreduce_sum((int64_t)n); }
-
-int mm_square_global(int64_t rows_glob, int64_t cols_glob) {
-  if (rows_glob == cols_glob)
-    throw std::runtime_error("distributed setup: square interpolation product (hypre_ParMatmul allsquare)");
-  return 0;
-}
-
-void mm_interp_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf, int first, int n,
-                    const std::vector<int>& starts, const std::vector<int>& cstarts, const AMGParams& prm,
-                    HostComm& comm, CSR& P) {
-  const int rank = comm.rank(), size = comm.size();
-  GhostUniverse G;
-  build_ghost_universe(A, S, first, n, starts, prm.strong_threshold, prm.max_row_sum, comm, G, true);
-  const std::vector<int> cfU = G.extend(cf, comm);
-  const std::vector<int> gcU = G.extend(class_index(cf, cstarts[rank], is_c), comm);
-  int64_t nf = 0;
-  for (int v : cf) nf += v < 0;
-  const int sq = mm_square_global(comm.allreduce_sum(nf), cstarts[size]);
-  CSR Pu;
-  if (prm.interp_type == 16) build_modext_interp(G.A, cfU, G.S, prm.trunc_factor, prm.P_max_elmts, false, Pu, nullptr, sq);
-  else if (prm.interp_type == 17) build_modextpi_interp(G.A, cfU, G.S, prm.trunc_factor, prm.P_max_elmts, Pu, nullptr, sq);
-  else build_modextpe_interp(G.A, cfU, G.S, prm.trunc_factor, prm.P_max_elmts, Pu, nullptr, sq);
-  P = owned_rows_global_cols(Pu, n, gcU, cstarts[size]);
-}
-
-// 2-stage aggressive interpolation: cf1 the first stage's markers (> 0: its C
-// points, numbered by c1starts), cf the corrected ones (1: C of both stages,
-// -2: C of the first only).  P1 (fine -> first-stage C) and P2 (first-stage C
-// -> C) over the universe, each truncated by the P12 limits; P = P1 P2 with
-// the P2 rows of off-rank first-stage C points fetched, then the aggressive
-// truncation.
-void twostage_dist(const CSR& A, const Pattern& S, const std::vector<int>& cf1, const std::vector<int>& cf, int first,
-                   int n, const std::vector<int>& starts, const std::vector<int>& c1starts,
-                   const std::vector<int>& cstarts, const AMGParams& prm, HostComm& comm, CSR& P) {
-  const int rank = comm.rank(), size = comm.size();
-  const bool pe = prm.agg_interp_type == 7;
-  GhostUniverse G;
-  build_ghost_universe(A, S, first, n, starts, prm.strong_threshold, prm.max_row_sum, comm, G, true);
-  const std::vector<int> cf1U = G.extend(cf1, comm), cfU = G.extend(cf, comm);
-  const std::vector<int> g1U = G.extend(class_index(cf1, c1starts[rank], is_c), comm);
-  const std::vector<int> g2U = G.extend(class_index(cf, cstarts[rank], is_c), comm);
-  int64_t nf1 = 0, nc1 = 0;
-  for (int v : cf1) { nf1 += v < 0; nc1 += v > 0; }
-  CSR P1u, P2u;
-  build_modext_interp(G.A, cf1U, G.S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P1u, nullptr,
-                      mm_square_global(comm.allreduce_sum(nf1), c1starts[size]));
-  int64_t nf2 = 0;  // As_FF's rows in the partial form: the first stage's C points only (-2)
-  for (int v : cf) nf2 += v == -2;
-  build_modpartialext_interp(G.A, cfU, G.S, prm.agg_P12_trunc_factor, prm.agg_P12_max_elmts, pe, P2u, nullptr,
-                             mm_square_global(comm.allreduce_sum(nf2), cstarts[size]));
-  const CSR P1 = owned_rows_global_cols(P1u, n, g1U, c1starts[size]);
-  // P2's rows are the universe's first-stage C points in universe order: the owned ones first
-  const CSR P2 = owned_rows_global_cols(P2u, (int)nc1, g2U, cstarts[size]);
-  // P1's columns -> rows of [owned P2 rows | fetched P2 rows]
-  const int c1first = c1starts[rank];
-  std::vector<int> want;
-  for (int c : P1.j)
-    if (c < c1first || c >= c1first + (int)nc1) want.push_back(c);
-  sort_unique(want);
-  const CSR P2g = fetch_rows(P2, c1first, c1starts, want, comm);
-  CSR Y;
-  Y.resize_rows((int)nc1 + P2g.nrows, cstarts[size]);
-  for (int r = 0; r < (int)nc1; ++r) Y.i[r + 1] = P2.i[r + 1];
-  for (int r = 0; r < P2g.nrows; ++r) Y.i[nc1 + r + 1] = P2.i[nc1] + P2g.i[r + 1];
-  Y.j = P2.j;
-  Y.a = P2.a;
-  Y.j.insert(Y.j.end(), P2g.j.begin(), P2g.j.end());
-  Y.a.insert(Y.a.end(), P2g.a.begin(), P2g.a.end());
-  CSR X = P1;
-  X.ncols = Y.nrows;
-  for (int& c : X.j) {
-    if (c >= c1first && c < c1first + (int)nc1) c -= c1first;
-    else c = (int)nc1 + (int)(std::lower_bound(want.begin(), want.end(), c) - want.begin());
-  }
-  multiply_interp(X, Y, prm.agg_trunc_factor, prm.agg_P_max_elmts, P,
-                  mm_square_global(L0_rows_glob(comm, n), cstarts[size]));
-  P.ncols = cstarts[size];
 }
 
 // ---------------------------------------------------------------------------
@@ -976,14 +868,15 @@ void l1_dist(const CSR& A, int first, int nglob, int option, const std::vector<i
 }
 
 // ---------------------------------------------------------------------------
-// Chebyshev smoother data (relax 16) with the one-process result, distributed:
-// par_relax_more.c:115 hypre_ParCSRMaxEigEstimateCG's start vector takes
-// hypre_Rand at the global row (the one-process stream), the matvec reads the
-// ghost values of its vector, and every inner product is formed as the
-// one-process loop forms it: a running sum handed from rank to rank in rank
-// order, each rank adding its rows to it.  The Lanczos tridiagonal, its
-// eigenvalues and the coefficients (par_cheby.c:36) are then the one-process
-// ones bit for bit.  par_relax_more.c:25's inf-norm bound is a max over rows.
+// Chebyshev smoother data (relax 16), distributed as the N-rank emulation
+// (setup.cpp max_eig_estimate_cg with rank starts) states it:
+// par_relax_more.c:115 hypre_ParCSRMaxEigEstimateCG's start vector takes each
+// rank's own random stream (seed my_id + 1, par_vector.c:337), the matvec
+// reads the ghost values of its vector, and every inner product is formed as
+// that loop forms it: a running sum handed from rank to rank in rank order,
+// each rank adding its rows to it.  The Lanczos tridiagonal, its eigenvalues
+// and the coefficients (par_cheby.c:36) are then the emulation's bit for bit.
+// par_relax_more.c:25's inf-norm bound is a max over rows.
 // ---------------------------------------------------------------------------
 double chain_dot(const std::vector<double>& x, const std::vector<double>& y, HostComm& comm) {
   const int size = comm.size(), rank = comm.rank();
@@ -1016,7 +909,9 @@ void max_eig_cg_dist(const CSR& A, int first, int n, const std::vector<int>& sta
   }
   std::vector<double> r(n), p(n, 0.0), s(n, 0.0), ds(n), u(n, 0.0), xg, xfull;
   std::vector<double> tridiag(max_iter + 1, 0.0), trioffd(max_iter + 1, 0.0);
-  for (int i = 0; i < n; ++i) r[i] = 2.0 * hypre_rand_at((int64_t)first + i, 1) - 1.0;
+  // hypre_ParVectorSetRandomValues(r, 1) (par_vector.c:337): seed 1 * (my_id + 1),
+  // every rank from its own first row
+  for (int i = 0; i < n; ++i) r[i] = 2.0 * hypre_rand_at(i, comm.rank() + 1) - 1.0;
   for (int i = 0; i < n; ++i) ds[i] = scale ? 1 / std::sqrt(A.a[A.i[i]]) : 1.0;
   auto matvec = [&](const std::vector<double>& x, std::vector<double>& y) {
     gp.pull(x.data(), xg, comm);
@@ -1133,6 +1028,27 @@ RankHalo make_halo(const std::vector<int>& halo, int first, int nloc, const std:
   return h;
 }
 
+// Rows of a rank in hypre's ParCSR order (diag, then offd, each in its own
+// entry order): a stable partition of every row by whether its column lies in
+// the rank's own column range [c0, c1) (setup.cpp rank_order_rows for one rank).
+void rank_order_local(CSR& M, int c0, int c1) {
+#pragma omp parallel
+  {
+    std::vector<int> tj;
+    std::vector<double> ta;
+#pragma omp for schedule(static)
+    for (int r = 0; r < M.nrows; ++r) {
+      tj.clear();
+      ta.clear();
+      for (int pass = 0; pass < 2; ++pass)
+        for (int k = M.i[r]; k < M.i[r + 1]; ++k)
+          if ((M.j[k] >= c0 && M.j[k] < c1) == (pass == 0)) { tj.push_back(M.j[k]); ta.push_back(M.a[k]); }
+      std::copy(tj.begin(), tj.end(), M.j.begin() + M.i[r]);
+      std::copy(ta.begin(), ta.end(), M.a.begin() + M.i[r]);
+    }
+  }
+}
+
 void offrank_cols(const CSR& M, int a, int b, std::vector<int>& out) {
   for (int c : M.j)
     if (c < a || c >= b) out.push_back(c);
@@ -1142,13 +1058,16 @@ void offrank_cols(const CSR& M, int a, int b, std::vector<int>& out) {
 
 bool dist_setup_supported(const AMGParams& prm, std::string* why) {
   auto no = [&](const char* w) { if (why) *why = w; return false; };
-  if (prm.coarsen_type != 8 && prm.coarsen_type != 10) return no("coarsen_type not 8 (PMIS) or 10 (HMIS)");
+  if (prm.coarsen_type != 8 && prm.coarsen_type != 9 && prm.coarsen_type != 10)
+    return no("coarsen_type not 8 / 9 (PMIS) or 10 (HMIS)");
   if (prm.coarsen_type == 10 && (prm.measure_type != 0 || prm.coarsen_cut_factor != 0))
     return no("HMIS with global measures or a cut factor");
-  if (prm.interp_type != 6 && prm.interp_type != 14 && (prm.interp_type < 16 || prm.interp_type > 18))
-    return no("interp_type not 6, 14, 16, 17 or 18");
-  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4 && prm.agg_interp_type != 5 && prm.agg_interp_type != 7)
-    return no("aggressive coarsening with agg_interp_type not 4, 5 or 7");
+  if (prm.interp_type != 6 && prm.interp_type != 14)
+    return no("interp_type not 6 or 14 (the matrix-matrix forms follow hypre_ParMatmul's N-rank order: "
+              "set up on rank 0 under the rank emulation)");
+  if (prm.agg_num_levels > 0 && prm.agg_interp_type != 4)
+    return no("aggressive coarsening with agg_interp_type not 4 (the 2-stage forms are set up on rank 0 under "
+              "the rank emulation)");
   if (prm.num_functions > 1) return no("num_functions > 1 (systems AMG is set up in one process)");
   if (prm.seq_threshold > 0) return no("seq_threshold (the redundant coarse-grid AMG is set up in one process)");
   for (int j = 0; j < std::min(prm.max_levels, (int)AMGParams::kWeightLevels); ++j)
@@ -1172,6 +1091,10 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     L[0].nloc = A0.nrows;
     L[0].nglob = L[0].starts[size];
   }
+  // hypre's ParCSR rows: the diagonal block's entries, then the off-diagonal
+  // block's (every operator of the hierarchy keeps that order: the input here,
+  // P around its truncation and every Galerkin product below)
+  rank_order_local(L[0].A, L[0].starts[rank], L[0].starts[rank + 1]);
   int level = 0;
   bool finished = prm.max_levels <= 1;
   char buf[256];
@@ -1181,7 +1104,7 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     create_strength(L[level].A, prm.strong_threshold, prm.max_row_sum, S);
     std::vector<int> cf;
     if (prm.coarsen_type == 10) hmis_dist(S, first, n, L[level].starts, comm, prm.measure_type, cf);
-    else pmis_dist(S, first, n, L[level].starts, comm, cf);
+    else pmis_dist(S, first, n, L[level].starts, comm, cf, prm.coarsen_type == 9 ? 2 : 0);
     // aggressive level: PMIS again on S*S + 2S of the C points, and the second
     // marker refines the first (setup.cpp amg_setup, par_amg_setup.c:1239)
     const bool agg_lvl = level < prm.agg_num_levels;
@@ -1191,7 +1114,7 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
       std::vector<int> cfn;
       second_strength_dist(S, cf, first, n, L[level].starts, prm.num_paths, comm, c1starts, S2);
       if (prm.coarsen_type == 10) hmis_dist(S2, c1starts[rank], S2.n, c1starts, comm, prm.measure_type + 3, cfn);
-      else pmis_dist(S2, c1starts[rank], S2.n, c1starts, comm, cfn, 3);
+      else pmis_dist(S2, c1starts[rank], S2.n, c1starts, comm, cfn, prm.coarsen_type == 9 ? 4 : 3);
       if (prm.agg_interp_type == 4) {
         correct_cf_marker(cf, cfn);
       } else {
@@ -1215,17 +1138,20 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     std::vector<int> cstarts(size + 1, 0);
     for (int p = 0; p < size; ++p) cstarts[p + 1] = cstarts[p] + (int)ncs[p];
     CSR P;
-    if (agg_lvl && prm.agg_interp_type != 4) {
-      twostage_dist(L[level].A, S, cf1, cf, first, n, L[level].starts, c1starts, cstarts, prm, comm, P);
-    } else if (agg_lvl) {
+    const int cc0 = cstarts[rank], cc1 = cstarts[rank + 1];  // this rank's coarse columns
+    if (agg_lvl) {
+      // multipass rows as P_diag | P_offd (setup.cpp amg_setup, emulated ranks)
       multipass_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm.agg_trunc_factor, prm.agg_P_max_elmts,
                      comm, P);
-    } else if (prm.interp_type >= 16 && prm.interp_type <= 18) {
-      mm_interp_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm, comm, P);
+      rank_order_local(P, cc0, cc1);
     } else {
       extpi_dist(L[level].A, S, cf, first, n, L[level].starts, cstarts, prm.strong_threshold, prm.max_row_sum, comm,
                  P, prm.interp_type == 6);
+      // par_csr_matrix.c:2671 truncates the row [P_diag | P_offd] and splits the
+      // kept entries back into the two parts in their sorted order
+      rank_order_local(P, cc0, cc1);
       if (prm.trunc_factor != 0.0 || prm.P_max_elmts > 0) truncate_rows(P, prm.trunc_factor, prm.P_max_elmts);
+      rank_order_local(P, cc0, cc1);
       for (int i = 0; i < n; ++i)
         if (cf[i] == SF_PT) cf[i] = F_PT;
     }
@@ -1233,6 +1159,7 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     transpose_dist(P, first, fine_size, cstarts, comm, R);
     CSR Ac;
     rap_dist(R, L[level].A, P, first, L[level].starts, cstarts, comm, Ac);
+    rank_order_local(Ac, cc0, cc1);  // hypre's RAP keeps each coarse row as diag then offd (par_rap.c)
     snprintf(buf, sizeof buf, "rank %d level %d: rows %d/%d -> coarse %d/%lld\n", rank, level, n, fine_size,
              (int)ncs[rank], (long long)coarse_size);
     if (log) *log += buf;
@@ -1326,6 +1253,18 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
   std::vector<int64_t> grows(nl);
   for (int l = 0; l < nl; ++l) grows[l] = L[l].nglob;
   const int agg = agglomeration_level(prm, grows, size);
+  // the hybrid-GS blocks of a level over all its rows: num_blocks blocks of
+  // every rank's rows (D.starts: the distributed owners)
+  auto owner_blocks = [&](const DLevel& D) {
+    std::vector<int> b(1, 0);
+    for (int r = 0; r < size; ++r) {
+      const int a0 = D.starts[r], n0 = D.starts[r + 1] - a0;
+      const int nb = prm.blocks_for(n0);
+      const std::vector<int> loc = hypre_block_starts(n0, nb);
+      for (int k = 1; k <= nb; ++k) b.push_back(a0 + loc[k]);
+    }
+    return b;
+  };
   int agg_share = 0;  // this rank's rows of level agg (the restriction's output)
   out.agg_level = agg;
   if (agg >= 0) {
@@ -1341,12 +1280,11 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
       D.cf = comm.allgatherv(D.cf);
       D.l1 = comm.allgatherv(D.l1);
       D.cheby_ds = comm.allgatherv(D.cheby_ds);
-      // a replicated level is swept as one rank's rows: its hybrid-GS l1
-      // norms over num_blocks blocks of the whole level
+      // a replicated level is swept by every rank whole, in its owners'
+      // blocks (partition.cpp rank_gs_blocks): its hybrid-GS l1 norms over them
       bool cfr = false;
       if (!D.l1.empty() && l1_option_for_level(prm, l, nl, &cfr) == 4)
-        compute_l1_norms_blocks(D.A, 4, (cfr && !D.cf.empty()) ? D.cf.data() : nullptr,
-                                hypre_block_starts(D.nglob, prm.blocks_for(D.nglob)), D.l1);
+        compute_l1_norms_blocks(D.A, 4, (cfr && !D.cf.empty()) ? D.cf.data() : nullptr, owner_blocks(D), D.l1);
     }
     for (int l = agg; l < nl; ++l) {
       DLevel& D = L[l];
@@ -1397,7 +1335,8 @@ int amg_setup_dist(const CSR& A0, int first_row, const AMGParams& prm_in, HostCo
     RL.cf = D.cf;
     RL.cheby_ds = D.cheby_ds;
     RL.cheby_coefs = D.cheby_coefs;
-    if (size > 1 && uses_hybrid_gs_any(prm)) RL.gs_blocks = hypre_block_starts(D.nloc, prm.blocks_for(D.nloc));
+    if (size > 1 && uses_hybrid_gs_any(prm))
+      RL.gs_blocks = (agg >= 0 && l >= agg) ? owner_blocks(D) : hypre_block_starts(D.nloc, prm.blocks_for(D.nloc));
     if (agg >= 0 && l >= agg) {
       RL.hu.n_loc = D.nloc;
       if (l + 1 < nl) RL.hv.n_loc = D.nloc;
@@ -1414,8 +1353,8 @@ int dist_setup_self_check(const CSR& A, const AMGParams& prm, int size, std::str
   const int n0 = A.nrows;
   std::vector<int> s0(size + 1);
   for (int r = 0; r <= size; ++r) s0[r] = (int)((int64_t)n0 * r / size);
-  // HMIS: its first pass per rank (the one-process statement: coarsen_starts)
-  amg_setup(A, prm, H, nullptr, &s0);
+  // the one-process statement of the same N-rank setup: the rank emulation
+  amg_setup(A, prm, H, size > 1 ? &s0 : nullptr, nullptr);
   std::vector<RankHierarchy> ref;
   partition_hierarchy_all(H, s0, size, ref);
   auto comms = make_thread_host_comms(size);

@@ -702,6 +702,96 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
   return true;
 }
 
+bool pack_dict_wide(const std::vector<int>& slice_ptr, const std::vector<int>& rowlen,
+                    const hvec<unsigned short>& col16, const hvec<double>& val, std::vector<int>& wptr,
+                    hvec<unsigned short>& colw, hvec<double>& valw) {
+  const int ns = (int)slice_ptr.size() - 1;
+  std::vector<int64_t> vs(ns + 1, 0), cs(ns + 1, 0);
+  // cnt(k) of a slice: lanes are sorted by descending length
+  auto cnt_at = [&](int s, int k) {
+    int c = 0;
+    while (c < 64 && rowlen[(size_t)s * 64 + c] > k) ++c;
+    return c;
+  };
+#pragma omp parallel for schedule(static)
+  for (int s = 0; s < ns; ++s) {
+    const int w = rowlen[(size_t)s * 64];
+    int64_t v = 0, c = 0;
+    for (int k = 0; k < w; k += 2) v += 2 * cnt_at(s, k);
+    for (int k = 0; k < w; k += 8) c += 8 * cnt_at(s, k);
+    vs[s + 1] = v;
+    cs[s + 1] = c;
+  }
+  for (int s = 0; s < ns; ++s) {
+    vs[s + 1] += vs[s];
+    cs[s + 1] += cs[s];
+  }
+  if (vs[ns] > 0x7fffffffLL || cs[ns] > 0x7fffffffLL) return false;
+  wptr.assign(2 * (size_t)(ns + 1), 0);
+  for (int s = 0; s <= ns; ++s) {
+    wptr[s] = (int)vs[s];
+    wptr[ns + 1 + s] = (int)cs[s];
+  }
+  valw.clear();
+  colw.clear();
+  valw.resize((size_t)vs[ns]);
+  colw.resize((size_t)cs[ns]);
+#pragma omp parallel for schedule(static)
+  for (int s = 0; s < ns; ++s) {
+    const int w = rowlen[(size_t)s * 64];
+    // jagged offset of entry k's first lane
+    std::vector<int64_t> off(w + 1, slice_ptr[s]);
+    std::vector<int> cnt(w + 1, 0);
+    for (int k = 0; k < w; ++k) {
+      cnt[k] = cnt_at(s, k);
+      off[k + 1] = off[k] + cnt[k];
+    }
+    const int* len = &rowlen[(size_t)s * 64];
+    int64_t pv = vs[s], pc = cs[s];
+    for (int j = 0; 2 * j < w; ++j) {
+      const int k = 2 * j, cl = cnt[k];
+      for (int l = 0; l < cl; ++l) {
+        valw[pv + 2 * l] = val[off[k] + l];
+        valw[pv + 2 * l + 1] = len[l] > k + 1 ? val[off[k + 1] + l] : 0.0;
+      }
+      pv += 2 * cl;
+    }
+    for (int o = 0; 8 * o < w; ++o) {
+      const int k0 = 8 * o, cl = cnt[k0];
+      for (int l = 0; l < cl; ++l)
+        for (int e = 0; e < 8; ++e) {
+          const int k = k0 + e;
+          colw[pc + 8 * l + e] = len[l] > k ? col16[off[k] + l] : (unsigned short)0;
+        }
+      pc += 8 * cl;
+    }
+  }
+  return true;
+}
+
+void pack_codes_lanes(std::vector<int>& slice_ptr, hvec<unsigned short>& code, int cpk) {
+  const int ns = (int)slice_ptr.size() - 1;
+  std::vector<int64_t> sp(ns + 1, 0);
+  for (int s = 0; s < ns; ++s) {
+    const int w = (slice_ptr[s + 1] - slice_ptr[s]) / 64;
+    sp[s + 1] = sp[s] + (int64_t)((w + cpk - 1) / cpk * cpk) * 64;
+  }
+  if (sp[ns] > 0x7fffffffLL) throw std::runtime_error("coded layout exceeds 2^31 slots");
+  hvec<unsigned short> out;
+  out.resize((size_t)sp[ns]);
+#pragma omp parallel for schedule(static)
+  for (int s = 0; s < ns; ++s) {
+    const int w = (slice_ptr[s + 1] - slice_ptr[s]) / 64;
+    const int wp = (w + cpk - 1) / cpk * cpk;
+    for (int k = 0; k < wp; ++k)
+      for (int l = 0; l < 64; ++l)
+        out[(size_t)sp[s] + (size_t)(k / cpk) * 64 * cpk + (size_t)l * cpk + k % cpk] =
+            k < w ? code[(size_t)slice_ptr[s] + (size_t)k * 64 + l] : (unsigned short)0xFFFF;
+  }
+  for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
+  code.swap(out);
+}
+
 // Packed SELL-64 entries (k_sell_code PK): code = ((col - base[slice]) << vbits)
 // | value index, base = the slice's smallest column, padding 0xFFFFFFFF.  false
 // when some slice's column span does not fit 32 - vbits bits (all-ones span

@@ -78,6 +78,24 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
                           std::vector<int>& rowlen, hvec<unsigned short>& col16, hvec<double>& val,
                           std::vector<int>& dict_ptr, std::vector<int>& dict, int& max_distinct,
                           int max_ranges = 0, double max_cover = 1.5, const std::vector<int>* pre = nullptr);
+// Lane-packed streams of a jagged dictionary layout (k_sell_dictw): the same
+// slices, rows and entry order, stored so that one 16-byte load of a lane
+// fetches two consecutive values of its row, and one 16-byte load eight
+// consecutive 16-bit local columns.  Per slice s, with cnt(k) = #{lanes whose
+// row is longer than k}:
+//   values: pair j (entries 2j, 2j+1) of lane l < cnt(2j) at
+//           wptr[s] + 2 (cnt(0) + cnt(2) + ... + cnt(2j - 2)) + 2l (doubles);
+//   columns: octet o (entries 8o .. 8o+7) of lane l < cnt(8o) at
+//           wptr[ns + 1 + s] + 8 (cnt(0) + cnt(8) + ... + cnt(8o - 8)) + 8l;
+// entries past a row's end are 0 (never summed).  wptr has 2 (ns + 1) ints;
+// false when a stream exceeds 2^31 elements.
+bool pack_dict_wide(const std::vector<int>& slice_ptr, const std::vector<int>& rowlen,
+                    const hvec<unsigned short>& col16, const hvec<double>& val, std::vector<int>& wptr,
+                    hvec<unsigned short>& colw, hvec<double>& valw);
+// R_0's offset-coded codes, lane-packed (k_sell_code with CPK codes a load):
+// a slice of padded width w (a multiple of CPK) stores slot k of lane l at
+// slice_ptr[s] + (k / CPK) * 64 CPK + l CPK + k % CPK; padding 0xFFFF.
+void pack_codes_lanes(std::vector<int>& slice_ptr, hvec<unsigned short>& code, int cpk);
 // Packed SELL-64 entries (k_sell_code PK) from a padded layout (col, 16-bit
 // value indices vi into nv values): code = ((col - base[slice]) << vbits) |
 // value index, base = the slice's smallest column, padding 0xFFFFFFFF.  false

@@ -113,14 +113,18 @@ static bool uses_hybrid_gs(const AMGParams& prm) {
   return false;
 }
 
+// Hybrid-GS row blocks of every level in an N-rank run: each rank's rows in
+// num_blocks blocks (hypre's threads per process).  Agglomerated levels keep
+// them (every rank sweeps the whole level redundantly, in its owners' blocks,
+// which is hypre's per-process sweep); the levels of the redundant coarse-grid
+// AMG (seq_threshold) are one process's (gen_redcs_mat.c).
 std::vector<std::vector<int>> rank_gs_blocks(const Hierarchy& H, const std::vector<int>& starts0, int size) {
   const int nl = (int)H.lev.size();
   const auto starts = level_starts(H, starts0, size);
-  const int agg = hierarchy_agg_level(H, size);
   std::vector<std::vector<int>> out(nl);
   for (int l = 0; l < nl; ++l) {
     const int n = H.lev[l].A.nrows;
-    if (agg >= 0 && l >= agg) {
+    if (H.seq_level >= 0 && l >= H.seq_level) {
       out[l] = hypre_block_starts(n, H.prm.blocks_for(n));
       continue;
     }
@@ -162,7 +166,11 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
   // threads per process), and the option-4 l1 norms follow those blocks
   const bool gs_ranks = size > 1 && uses_hybrid_gs(H.prm);
   std::vector<std::vector<double>> l1_ranks;
-  if (gs_ranks) l1_ranks = l1_for_blocks(H, rank_gs_blocks(H, starts0, size));
+  std::vector<std::vector<int>> gs_blocks;
+  if (gs_ranks) {
+    gs_blocks = rank_gs_blocks(H, starts0, size);
+    l1_ranks = l1_for_blocks(H, gs_blocks);
+  }
   // rows of level l this rank holds: its block, or all of a replicated level
   auto lo = [&](int l, int r) { return (agg >= 0 && l >= agg) ? 0 : starts[l][r]; };
   auto hi = [&](int l, int r) { return (agg >= 0 && l >= agg) ? H.lev[l].A.nrows : starts[l][r + 1]; };
@@ -229,7 +237,8 @@ static void partition_all(const Hierarchy& H, const std::vector<int>& starts0, i
       }
       if (gs_ranks) {
         if (!l1_ranks[l].empty()) RL.l1.assign(l1_ranks[l].begin() + a, l1_ranks[l].begin() + b);
-        RL.gs_blocks = hypre_block_starts(b - a, H.prm.blocks_for(b - a));
+        // a replicated level: every rank sweeps it whole in its owners' blocks
+        RL.gs_blocks = (agg >= 0 && l >= agg) ? gs_blocks[l] : hypre_block_starts(b - a, H.prm.blocks_for(b - a));
       } else if (!L.l1.empty()) {
         RL.l1.assign(L.l1.begin() + a, L.l1.begin() + b);
       }

@@ -2550,17 +2550,22 @@ static void rank_order_rows(CSR& M, const std::vector<int>& rs, const std::vecto
   auto owner = [](const std::vector<int>& st, int i) {
     return (int)(std::upper_bound(st.begin(), st.end(), i) - st.begin()) - 1;
   };
-  std::vector<int> tj;
-  std::vector<double> ta;
-  for (int r = 0; r < M.nrows; ++r) {
-    const int o = owner(rs, r);
-    tj.clear();
-    ta.clear();
-    for (int pass = 0; pass < 2; ++pass)
-      for (int k = M.i[r]; k < M.i[r + 1]; ++k)
-        if ((owner(cs, M.j[k]) == o) == (pass == 0)) { tj.push_back(M.j[k]); ta.push_back(M.a[k]); }
-    std::copy(tj.begin(), tj.end(), M.j.begin() + M.i[r]);
-    std::copy(ta.begin(), ta.end(), M.a.begin() + M.i[r]);
+#pragma omp parallel
+  {
+    std::vector<int> tj;
+    std::vector<double> ta;
+#pragma omp for schedule(static)
+    for (int r = 0; r < M.nrows; ++r) {
+      const int o = owner(rs, r);
+      const int c0 = cs[o], c1 = cs[o + 1];  // the owner's columns
+      tj.clear();
+      ta.clear();
+      for (int pass = 0; pass < 2; ++pass)
+        for (int k = M.i[r]; k < M.i[r + 1]; ++k)
+          if ((M.j[k] >= c0 && M.j[k] < c1) == (pass == 0)) { tj.push_back(M.j[k]); ta.push_back(M.a[k]); }
+      std::copy(tj.begin(), tj.end(), M.j.begin() + M.i[r]);
+      std::copy(ta.begin(), ta.end(), M.a.begin() + M.i[r]);
+    }
   }
 }
 

@@ -205,6 +205,7 @@ SIGNATURES = [
     ("hypreve_SetKnob", _i, [_i, _i]),
     ("hypreve_BoomerAMGSetDeviceSetup", _i, [_p, _i]),
     ("hypreve_BoomerAMGGetSetupLog", _i, [_p, C.c_char_p, _i]),
+    ("hypreve_BoomerAMGGetSetupPath", _i, [_p, C.POINTER(C.c_int)]),
     ("hypreve_BenchLevelOp", _i, [_p, _i, _i, _i, _pd, _pd, _pd]),
     ("hypreve_BenchLevelOpStoredBytes", _i, [_p, _i, _i, _pd]),
     ("hypreve_BenchOperator", _i, [_p, _i, _i, _i, _i, _pd, _pd, C.c_char_p, _i]),
@@ -594,6 +595,15 @@ class BoomerAMG:
         check(lib().hypreve_BoomerAMGStencilLayoutCheck(self.h, level, C.byref(w), C.byref(npat)), "StencilLayoutCheck")
         return w.value, npat.value
 
+    SETUP_PATHS = ("one process", "one process, rank emulation", "distributed", "gathered, rank emulation",
+                   "gathered, one process")
+
+    def setup_path(self):
+        """The path the last setup took (hypreve_BoomerAMGGetSetupPath), by name."""
+        v = C.c_int()
+        check(lib().hypreve_BoomerAMGGetSetupPath(self.h, C.byref(v)), "GetSetupPath")
+        return self.SETUP_PATHS[v.value] if v.value >= 0 else None
+
     def setup_log(self):
         """The setup's log: levels, phase times, rows the device setup left to the host."""
         buf = C.create_string_buffer(1 << 16)
@@ -672,7 +682,7 @@ class BoomerAMG:
         check(lib().hypreve_BoomerAMGSetCoarsenRankStarts(self.h, len(starts) - 1, arr), "SetCoarsenRankStarts")
 
     LAYOUTS = ("padded", "jagged", "wide", "jag-pw", "dict", "delta", "delta+vt8", "delta+vt16", "padded+vt16",
-               "jagged+vt16", "dict-ranges", "stencil", "coded", "packed", "grid-stencil")
+               "jagged+vt16", "dict-ranges", "stencil", "coded", "packed", "grid-stencil", "dict-wide")
 
     def level_layout(self, level, which=0):
         """Device layout name of A_l (0), P_l (1) or R_l (2) (interior rows)."""

@@ -149,20 +149,24 @@ HYPRE_Int HYPRE_BoomerAMGSetMeasureType(HYPRE_Solver solver, HYPRE_Int measure_t
 HYPRE_Int HYPRE_BoomerAMGSetAggNumLevels(HYPRE_Solver solver, HYPRE_Int agg_num_levels); /* :369 */
 HYPRE_Int HYPRE_BoomerAMGSetNumPaths(HYPRE_Solver solver, HYPRE_Int num_paths); /* :377 */
 /* Aggressive-level interpolation: 4 (multipass, the default), 5 (2-stage
- * extended, matrix-matrix form: par_mod_lr_interp.c:16 then par_2s_interp.c:15)
- * and 7 (2-stage extended+e: par_mod_lr_interp.c:1040 then par_2s_interp.c:564);
- * Setup fails with HYPRE_ERROR_ARG for 1-3, 6 and 8. */
+ * extended, matrix-matrix form: par_mod_lr_interp.c:16 then par_2s_interp.c:15),
+ * 7 (2-stage extended+e: par_mod_lr_interp.c:1040 then par_2s_interp.c:564),
+ * 1 / 3 (2-stage extended+i / extended, then partial.c:16 / :1855), 2 (standard,
+ * then partial standard, partial.c:859) and 6 (MM extended+i, then partial
+ * extended+i); Setup fails with HYPRE_ERROR_ARG for 8. */
 HYPRE_Int HYPRE_BoomerAMGSetAggInterpType(HYPRE_Solver solver, HYPRE_Int agg_interp_type); /* :480 */
 HYPRE_Int HYPRE_BoomerAMGSetAggTruncFactor(HYPRE_Solver solver, HYPRE_Real agg_trunc_factor); /* :488 */
 HYPRE_Int HYPRE_BoomerAMGSetAggP12TruncFactor(HYPRE_Solver solver, HYPRE_Real agg_P12_trunc_factor); /* :496 */
 HYPRE_Int HYPRE_BoomerAMGSetAggPMaxElmts(HYPRE_Solver solver, HYPRE_Int agg_P_max_elmts); /* :504 */
 HYPRE_Int HYPRE_BoomerAMGSetAggP12MaxElmts(HYPRE_Solver solver, HYPRE_Int agg_P12_max_elmts); /* :512 */
-/* interp_type 6 ext+i, 14 ext, 16 / 17 / 18 ext / ext+i / ext+e (matrix-matrix form), 3 direct */
+/* interp_type 6 ext+i, 14 ext, 16 / 17 / 18 ext / ext+i / ext+e (matrix-matrix form), 3 direct,
+ * 7 ext+i where no common C point, 8 / 9 standard (9: separated weights) */
 HYPRE_Int HYPRE_BoomerAMGSetInterpType(HYPRE_Solver solver, HYPRE_Int interp_type); /* :442 */
 HYPRE_Int HYPRE_BoomerAMGSetSepWeight(HYPRE_Solver solver, HYPRE_Int sep_weight); /* :464 (standard interpolation) */
 /* :667 / :673: redundant coarse-grid AMG below seq_threshold global rows; it
  * acts only with more than one rank, as in the reference (par_amg_setup.c:294):
- * under hypreve_BoomerAMGSetRankEmulation; the distributed setup gathers for it */
+ * under hypreve_BoomerAMGSetRankEmulation, and on N ranks (the rank-0
+ * gathered setup runs that emulation) */
 HYPRE_Int HYPRE_BoomerAMGSetSeqThreshold(HYPRE_Solver solver, HYPRE_Int seq_threshold);
 /* :168: systems AMG, unknown approach (interleaved functions, dof = row %
  * num_functions; strength and weak lumping within a function); with
@@ -273,7 +277,10 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands,
  * stencil, else as 7, 12 offset-coded P and R (one 16-bit code per entry:
  * offset from the row's grid point and value index) where they build, else
  * padded, 13 packed P and R (one 32-bit code per entry: column less the
- * slice's smallest column, and value index) where they fit, else as 8.  All give identical bits; the forced settings exist for parity tests
+ * slice's smallest column, and value index) where they fit, else as 8,
+ * 14 as 5 with the per-entry streams (5 and the automatic choice store the
+ * dictionary layout's values and columns lane-packed, 16 B a lane load).
+ * All give identical bits; the forced settings exist for parity tests
  * and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
 /* One GPU runs the hybrid Gauss-Seidel smoothers with the row blocks of an
@@ -290,8 +297,9 @@ HYPRE_Int hypreve_BoomerAMGGetLevelWeights(HYPRE_Solver solver, HYPRE_Int level,
  * random stream per rank in the PMIS stage (par_coarsen.c:2774 on N
  * processes), rank r owning level-0 rows starts[r] .. starts[r+1]-1 and the
  * C points of its rows below.  The rest of the setup stays the one-process
- * one, so the iterates equal those of the distributed setup on N ranks.
- * nranks <= 1 clears it; other coarsenings ignore it.  Takes effect at Setup. */
+ * one (a partial emulation, for experiments; an N-rank setup follows the
+ * whole of hypreve_BoomerAMGSetRankEmulation).  nranks <= 1 clears it; other
+ * coarsenings ignore it.  Takes effect at Setup. */
 HYPRE_Int hypreve_BoomerAMGSetCoarsenRankStarts(HYPRE_Solver solver, HYPRE_Int nranks, const HYPRE_Int *starts);
 /* One process reproduces the setup and smoothing of a reference N-rank run
  * (mpirun -np N) whose level-0 rows start at starts[0..nranks]: every row in
@@ -305,7 +313,11 @@ HYPRE_Int hypreve_BoomerAMGSetCoarsenRankStarts(HYPRE_Solver solver, HYPRE_Int n
  * Interpolation: ext+i (6) and ext (14) per rank, the matrix-matrix forms
  * (16 / 17 / 18) with hypre_ParMatmul's np > 1 entry order; aggressive levels:
  * the second pass per rank as well, multipass rows in P_diag | P_offd order,
- * and the 2-stage types 5 / 7.  Takes effect at Setup. */
+ * and the 2-stage types.  These are the rules of every N-rank setup of this
+ * library too (the distributed one, dsetup.cpp, and the rank-0 gathered one),
+ * so an N-GPU run equals a one-GPU run given the same starts here bit for
+ * bit, and both reproduce the reference's N-process run.  Takes effect at
+ * Setup. */
 HYPRE_Int hypreve_BoomerAMGSetRankEmulation(HYPRE_Solver solver, HYPRE_Int nranks, const HYPRE_Int *starts);
 /* Multi-rank: coarse levels with at most `rows` global rows (from the first
  * such level down) are held whole by every rank and cycled redundantly, with
@@ -365,7 +377,8 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver solver, HYPRE_Real *byte
  * 7 deltas + 16-bit value table, 8 padded + 16-bit value table, 9 jagged +
  * 16-bit value table, 10 range dictionary, 11 slot-uniform stencil,
  * 12 offset-coded (P, R), 13 packed 32-bit codes (P, R), 14 slot-uniform
- * stencil over a grid in natural order (k_grid_stencil: LDS x-tile). */
+ * stencil over a grid in natural order (k_grid_stencil: LDS x-tile),
+ * 15 dictionary with lane-packed value / column streams (k_sell_dictw). */
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int *kind);
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */
@@ -397,6 +410,13 @@ HYPRE_Int hypreve_BoomerAMGSetDeviceSetup(HYPRE_Solver solver, HYPRE_Int on);
 /* The setup's log (levels, phase times, rows the device setup left to the
  * host) into buf[0..len). */
 HYPRE_Int hypreve_BoomerAMGGetSetupLog(HYPRE_Solver solver, char *buf, HYPRE_Int len);
+/* The path the last Setup took: 0 one process, 1 one process under
+ * hypreve_BoomerAMGSetRankEmulation, 2 distributed (every rank its own rows,
+ * hypre's N-process rules), 3 gathered on rank 0 under the rank emulation of
+ * the same N-process rules (the options the distributed setup does not take),
+ * 4 gathered one-process (direct interpolation, which the emulation does not
+ * restate); -1 before the first Setup. */
+HYPRE_Int hypreve_BoomerAMGGetSetupPath(HYPRE_Solver solver, HYPRE_Int *path);
 /* Host check of the offset-coded layout of level's P (which 1) or R (which 2)
  * (after hypreve_BoomerAMGSetupHost or Setup): every row decoded from its
  * 16-bit codes equals the CSR row entry for entry, values bitwise.

@@ -5,7 +5,7 @@ PMIS + ext+i Pmx 4, relax 18) and read-only stream references.
 
 Prints one line per (level, operator): rows, nnz, SELL padding, avg us,
 algorithmic GB/s.  Kernel variants are chosen by environment variables read
-by the library (HVE_SELL_BATCH, HVE_SELL_SIGMA), so run one process per variant.
+by the library (HVE_SELL_BATCH, HVE_SELL_PIPE), so run one process per variant.
 """
 import argparse
 import json
@@ -30,7 +30,7 @@ def main():
     import hypreve as hv
 
     hv.init()
-    variant = {k: os.environ.get(k, "") for k in ("HVE_SELL_BATCH", "HVE_SELL_SIGMA", "HVE_SELL_PIPE", "HVE_SELL_NT", "HVE_SELL_JAG")}
+    variant = {k: os.environ.get(k, "") for k in ("HVE_SELL_BATCH", "HVE_SELL_PIPE", "HVE_SELL_NT", "HVE_SELL_JAG")}
     print(f"variant {variant}", flush=True)
     rows = []
     for eb in (4, 8, 16):

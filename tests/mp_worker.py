@@ -9,8 +9,10 @@ the box's single GPU, which RCCL refuses, so the communicator is the
 host-staged shared-memory transport (hypreve_CommCreateShm); every other line
 of the data path -- operator split, halo exchange on the side stream,
 agglomerated coarse levels, coarse solve, the distributed setup's all-to-alls
--- is the production code.  Rank 0 then solves the same problem on one rank
-without a communicator and compares the gathered iterate bit for bit.
+-- is the production code.  Rank 0 then solves the same problem on one GPU
+without a communicator under the rank emulation of the same N-rank setup
+(hypreve_BoomerAMGSetRankEmulation: hypre's N-process rules, the contract of
+every N-rank run) and compares the gathered iterate bit for bit.
 Prints one JSON line on rank 0; exits nonzero on any mismatch.
 """
 import json
@@ -80,16 +82,15 @@ def main():
             xN = np.concatenate([o[1] for o in gathered])
             A1 = gen(hv, stencil, nx, ny, nz)
             a1 = hv.BoomerAMG(**kw)
-            if relax in (3, 4, 6, 8, 13, 14):
-                a1.set_gs_rank_starts(starts)  # hybrid GS: the N-rank row blocks on one GPU
+            a1.set_rank_emulation(starts)  # the N-rank setup (and hybrid-GS row blocks) on one GPU
             a1.setup(A1)
             b1 = hv.ParVector(N, b_glob)
             x1 = hv.ParVector(N, np.zeros(N))
             it1, rr1 = a1.solve(A1, b1, x1)
             x1h = x1.get()
             same = bool(np.array_equal(x1h, xN))
-            # bench.py's N-rank parity: each rank's sha256 against the 1-rank
-            # iterate cut at GenerateLaplacian's slab boundaries
+            # bench.py's N-rank parity: each rank's sha256 against the emulated
+            # one-GPU iterate cut at GenerateLaplacian's slab boundaries
             cut = bench.slab_rows(nx, ny, nz, world)
             digests_ok = [o[0] for o in gathered] == [f for f, _ in cut] and \
                 [o[5] for o in gathered] == [bench.sha256_f64(x1h[f:f + c]) for f, c in cut]

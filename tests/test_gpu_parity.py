@@ -102,7 +102,7 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen, wt):
     assert np.array_equal(x.get(), xo)
 
 
-@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
 @pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
 def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
@@ -122,6 +122,10 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
         assert amg.level_layout(0, 1) == "coded" and amg.level_layout(0, 2) == "coded"
     if policy == 13:
         assert amg.level_layout(0, 1) == "packed" and amg.level_layout(0, 2) == "packed"
+    if policy == 5:  # the lane-packed dictionary streams (k_sell_dictw), A's 4-slice groups included
+        assert amg.level_layout(0, 0) == "dict-wide" and amg.level_layout(1, 0) == "dict-wide"
+    if policy == 14:  # the per-entry dictionary streams (k_sell_dict)
+        assert amg.level_layout(0, 0) == "dict" and amg.level_layout(1, 0) == "dict"
     rng = np.random.default_rng(23 + policy)
     f_h = rng.standard_normal(n)
     u0 = rng.standard_normal(n)

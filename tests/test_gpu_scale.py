@@ -65,7 +65,7 @@ def test_bench_size_256_bitwise(gpu, orc):
     layouts = {(l, w): amg.level_layout(l, w) for l in range(3) for w in range(3)}
     print("layouts", layouts)
     assert layouts[(0, 0)] == "grid-stencil"  # the stencil layout's grid form (64 | nx)
-    assert layouts[(1, 0)] == "dict"
+    assert layouts[(1, 0)] == "dict-wide"  # the dictionary layout, lane-packed streams
     cycle_and_solve_bitwise(hv, orc, A, amg, 101, 3)
 
 

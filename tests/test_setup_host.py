@@ -101,9 +101,12 @@ def test_distributed_setup_matches_one_process(hv, size, stencil, relax, order, 
     """Distributed setup (each rank builds its rows' levels from a ghost
     layer: PMIS passes exchanging measures / demotions / C-F state, ext+i over
     fetched neighbour rows, R from P entries sent to their coarse owner, RAP
-    over fetched A and P rows) on `size` host threads: every rank's part of
-    every level equals the one-process hierarchy partitioned the same way,
-    byte for byte (operators, C/F, l1 norms, halo plans, coarsest operator)."""
+    over fetched A and P rows) on `size` host threads, under hypre's N-process
+    rules (per-rank PMIS streams, rows in ParCSR order, truncation over
+    [P_diag | P_offd]): every rank's part of every level equals the rank
+    emulation's one-process hierarchy (SetRankEmulation, pinned to the
+    reference's np > 1 runs) partitioned the same way, byte for byte
+    (operators, C/F, l1 norms, hybrid-GS blocks, halo plans, coarsest operator)."""
     if stencil == 27:
         A = hv.ParCSRMatrix.laplacian27(17, 15, 19)
     else:
@@ -117,9 +120,10 @@ def test_distributed_setup_matches_one_process(hv, size, stencil, relax, order, 
 @pytest.mark.parametrize("agg,cx", [(1, 1.0), (2, 1.0), (1, 0.001), (10, 0.001)])
 def test_distributed_setup_aggressive(hv, size, agg, cx):
     """configs[4]: aggressive levels in the distributed setup (second strength
-    over the C points from fetched neighbour S rows, PMIS with CF_init 3,
-    CorrectCFMarker, multipass interpolation pass by pass with the previous
-    pass's ghost P rows fetched) equal the one-process hierarchy byte for byte."""
+    over the C points from fetched neighbour S rows, PMIS with CF_init 3 and
+    per-rank streams, CorrectCFMarker, multipass interpolation pass by pass
+    with the previous pass's ghost P rows fetched, rows as P_diag | P_offd)
+    equal the rank emulation's hierarchy byte for byte."""
     A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=cx)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
     amg.set(coarsen_type=8, interp_type=6, relax_type=18, P_max_elmts=4, agg_num_levels=agg)
@@ -129,7 +133,7 @@ def test_distributed_setup_aggressive(hv, size, agg, cx):
 @pytest.mark.parametrize("size", [2, 4, 7])
 def test_distributed_setup_anisotropic(hv, size):
     """configs[4]'s operator family (anisotropic diffusion, strong couplings in
-    one direction only): the distributed setup still equals the one-process one."""
+    one direction only): the distributed setup still equals the rank emulation."""
     A = hv.ParCSRMatrix.laplacian(21, 19, 25, cx=0.001, cy=1.0, cz=1.0)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
     amg.set(coarsen_type=8, interp_type=6, relax_type=18, P_max_elmts=4)
@@ -326,9 +330,8 @@ def test_distributed_hmis_matches_rank_coarsening(hv, size, stencil, relax, inte
     in the distributed setup: each rank's Ruge first pass over the strong
     connections it owns, then PMIS seeded with its C points with one random
     stream per rank (par_coarsen.c:2774 on N processes; dsetup.cpp hmis_dist).
-    Every rank's part of every level equals the one-process setup that
-    coarsens HMIS with the same rank starts (amg_setup's coarsen_starts) byte
-    for byte, with aggressive levels (the second pass per rank too)."""
+    Every rank's part of every level equals the rank emulation's hierarchy
+    byte for byte, with aggressive levels (the second pass per rank too)."""
     if stencil == 27:
         A = hv.ParCSRMatrix.laplacian27(17, 15, 19)
     else:
@@ -340,7 +343,8 @@ def test_distributed_hmis_matches_rank_coarsening(hv, size, stencil, relax, inte
 
 def test_hmis_rank_coarsening_has_teeth(hv):
     """The per-rank HMIS differs from the one-process HMIS (first pass over the
-    whole graph), so the check above compares against the right hierarchy."""
+    whole graph), so the checks above compare against another hierarchy than
+    the one-process setup's."""
     A = hv.ParCSRMatrix.laplacian(19, 17, 23)
     sizes = []
     for starts in (None, [0, A.n // 3, 2 * A.n // 3, A.n]):
@@ -355,23 +359,22 @@ def test_hmis_rank_coarsening_has_teeth(hv):
     assert sizes[0] != sizes[1]
 
 
-@pytest.mark.parametrize("size", [2, 3, 5, 8])
-@pytest.mark.parametrize("coarsen,interp,agg,agg_interp,pmx", [(8, 16, 0, 4, 4), (8, 17, 0, 4, 4), (8, 18, 0, 4, 0),
-                                                                (10, 17, 0, 4, 4), (8, 6, 1, 5, 4), (8, 6, 1, 7, 4),
-                                                                (10, 6, 2, 5, 4), (10, 18, 1, 7, 0)])
-def test_distributed_mm_interp_matches_one_process(hv, size, coarsen, interp, agg, agg_interp, pmx):
-    """The matrix-matrix interpolations (16 ext, 17 ext+i, 18 ext+e:
-    par_mod_lr_interp.c) and the 2-stage aggressive ones (agg_interp_type 5 /
-    7: par_2s_interp.c, P = P1 P2) in the distributed setup: each rank runs the
-    one-process builders over its ghost universe (owned points, off-rank
-    neighbours with fetched A rows, the points those reach) and keeps its
-    rows; P2's off-rank rows are fetched for the product.  Every rank's part
-    equals the one-process hierarchy byte for byte (HMIS: coarsened per rank)."""
-    A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=1.0, cy=0.8, cz=1.0)
+@pytest.mark.parametrize("coarsen,interp,agg,agg_interp", [(8, 16, 0, 4), (8, 17, 0, 4), (10, 18, 0, 4),
+                                                            (8, 6, 1, 5), (8, 6, 1, 7), (10, 6, 1, 1), (8, 3, 0, 4)])
+def test_distributed_setup_refuses_to_the_gathered_emulation(hv, coarsen, interp, agg, agg_interp):
+    """The matrix-matrix interpolations (16-18), the 2-stage aggressive ones
+    and the direct one (3) are not set up distributed: their products follow
+    hypre_ParMatmul's N-rank entry order, which the rank emulation restates in
+    one process, so an N-rank setup gathers the matrix on rank 0 and runs that
+    emulation there (capi.hip setup_multi, GetSetupPath 3; the direct
+    interpolation, which the emulation does not restate, path 4).  The
+    distributed setup refuses them and says why."""
+    A = hv.ParCSRMatrix.laplacian(11, 10, 12)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
-    amg.set(coarsen_type=coarsen, interp_type=interp, relax_type=18, P_max_elmts=pmx, agg_num_levels=agg,
-            agg_interp_type=agg_interp, agg_P12_max_elmts=4 if agg_interp == 7 else 0, agg_P_max_elmts=4)
-    amg.dist_setup_check(A, size)
+    amg.set(coarsen_type=coarsen, interp_type=interp, relax_type=18, P_max_elmts=4, agg_num_levels=agg,
+            agg_interp_type=agg_interp)
+    with pytest.raises(hv.HypreError, match="distributed setup: (interp_type|aggressive)"):
+        amg.dist_setup_check(A, 2)
 
 
 @pytest.mark.parametrize("size", [2, 3, 5, 8])
@@ -379,10 +382,11 @@ def test_distributed_mm_interp_matches_one_process(hv, size, coarsen, interp, ag
                                                              (8, 2, 1, 0, 0)])
 def test_distributed_chebyshev_matches_one_process(hv, size, coarsen, order, scale, variant, eig):
     """Chebyshev (relax 16) in the distributed setup: the eigenvalue estimate's
-    CG (par_relax_more.c:115) draws its start vector at the global rows, and
-    every inner product is a running sum handed from rank to rank in rank
-    order, so the coefficients and the scaling equal the one-process ones
-    byte for byte; eig 0: the inf-norm bound (par_relax_more.c:25)."""
+    CG (par_relax_more.c:115) draws its start vector from every rank's own
+    stream (seed my_id + 1, par_vector.c:337), and every inner product is a
+    running sum handed from rank to rank in rank order, so the coefficients
+    and the scaling equal the rank emulation's byte for byte; eig 0: the
+    inf-norm bound (par_relax_more.c:25)."""
     A = hv.ParCSRMatrix.laplacian(19, 17, 23, cx=1.0, cy=0.5, cz=1.0)
     amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
     amg.set(coarsen_type=coarsen, interp_type=6, relax_type=16, P_max_elmts=4, cheby_order=order,
