@@ -48,6 +48,7 @@ KERNEL_OF_LAYOUT = {
     "delta": ("k_sell_delta<0, false, |, true, 0>(hve::SpArgs)", "SELL-64 with 16-bit column deltas"),
     "dict": ("k_sell_dict<0, false, |, true, ", "jagged SELL-64 with an LDS x-tile dictionary"),
     "dict-ranges": ("k_sell_dict<0, false, |, true, ", "jagged SELL-64 with an LDS x-tile of column ranges"),
+    "coded-jag": ("k_code_pw<0, ", "offset-coded rows, jagged, product-parallel"),
     "dict-wide": ("k_sell_dictw<0, false, true, ", "jagged SELL-64 with an LDS x-tile dictionary, lane-packed "
                   "value / column streams"),
     "padded": ("k_sell<0, false, |, ", "padded SELL-64"),

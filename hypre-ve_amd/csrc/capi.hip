@@ -865,7 +865,7 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver s, HYPRE_Int nbands, HYPRE
 }
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver s, HYPRE_Int policy) {
   CHECK_ARG(s && s->kind == KIND_AMG, 1);
-  CHECK_ARG(policy >= 0 && policy <= 14, 2);
+  CHECK_ARG(policy >= 0 && policy <= 15, 2);
   s->prm.sell_policy = policy;
   return 0;
 }
@@ -1446,7 +1446,7 @@ HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver s, HYPRE_Int level, HYPRE
   API_BEGIN
   const DevLevel& L = s->dev->level(level);
   const DevSell& M = which == 0 ? L.A.in : which == 1 ? L.P.in : L.R.in;
-  *kind = M.code32 ? 13 : M.code16 ? 12 : M.slot_mask ? (grid_stencil_on(M.view()) ? 14 : 11)
+  *kind = M.code32 ? 13 : M.code16 ? (M.rowlen ? 16 : 12) : M.slot_mask ? (grid_stencil_on(M.view()) ? 14 : 11)
          : M.dcol ? (M.vidx16 ? 7 : M.vidx ? 6 : 5)
                  : M.vidx16 ? (M.rowlen ? 9 : 8) : M.col16 ? (M.dict_ranges ? 10 : M.wptr ? 15 : 4) : M.pw ? 3 : M.rowlen ? 1
                  : M.wide ? 2 : 0;

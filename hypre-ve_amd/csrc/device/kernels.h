@@ -36,9 +36,6 @@ struct SellView {
   // val / col16 hold value pairs / column octets per lane, wptr the 2 (nslices + 1)
   // slice offsets (values, then columns); nullptr = the per-entry streams
   const int* wptr = nullptr;
-  // offset-coded layout: codes per lane load (1 = one slot per load, 4 / 8 =
-  // lane-packed groups of consecutive slots, host: pack_codes_lanes)
-  int code_pack = 1;
   const short* dcol = nullptr;     // delta layout (k_sell_delta): col - row - slot base, padded
   const int* slot_base = nullptr;  // delta layout: base offset per (slice, slot)
   const unsigned char* vidx = nullptr;  // delta layout: 8-bit value indices (val unused)

@@ -29,10 +29,9 @@
 namespace hve {
 
 static constexpr int kWave = 64;
-// 16- and 8-byte lane loads of the lane-packed streams
+// 16-byte lane loads of the lane-packed dictionary streams
 typedef double dv2_t __attribute__((ext_vector_type(2)));
 typedef unsigned uv4_t __attribute__((ext_vector_type(4)));
-typedef unsigned uv2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int xcd_logical_block(int b, int nblocks_pad) {
   // nblocks_pad is a multiple of 8; block b runs on XCD b%8; give each XCD a
@@ -1093,18 +1092,10 @@ __global__ void __launch_bounds__(256) k_sell_delta(SpArgs p) {
 // entry, ((column - slice base) << vbits) | value index, the base per slice in
 // slot_base: 4 B an entry and the column without a second gather (P_0, whose
 // offset-coded form needs cmap).
-// CPK > 1 (R_0, host: pack_codes_lanes): a lane's CPK consecutive codes are
-// stored together, so one 8- or 16-byte load brings CPK entries of its row
-// (slice widths padded to a multiple of CPK with 0xFFFF).
-template <int CPK>
-struct CodePack {
-  using type = typename std::conditional<CPK == 8, uv4_t, uv2_t>::type;
-};
-template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK, int CPK>
+template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK>
 __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, const int* ot, int rb0, int rb1) {
   using CT = typename std::conditional<PK, unsigned, unsigned short>::type;
   constexpr unsigned PAD = PK ? 0xFFFFFFFFu : 0xFFFFu;
-  static_assert(CPK == 1 || (!PK && !MAP && B % CPK == 0), "lane-packed codes: R_0's loop, whole loads a batch");
   const int vb = p.vbits;
   const unsigned vm = (1u << vb) - 1u;
   const bool sub = op_subtracts<OP>() || (OP == OP_GENERAL && p.w == -1.0);
@@ -1126,7 +1117,6 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
     width[r] = act[r] ? ws[r] : 0;
     g[r] = act[r] ? (p.rowmap ? mload<true>(p.rowmap + row) : row) : 0;
     if constexpr (PK) cp[r] = p.code32 + beg + (threadIdx.x & (kWave - 1));
-    else if constexpr (CPK > 1) cp[r] = p.code16 + beg + (threadIdx.x & (kWave - 1)) * CPK;
     else cp[r] = p.code16 + beg + (threadIdx.x & (kWave - 1));
     wmax = max(wmax, ws[r]);  // the widest of the NR slices: wave-uniform
     if (CFSEL && act[r] && p.cf[g[r]] != p.relax_points) {
@@ -1139,60 +1129,7 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
     pre[r] = act[r] ? row_preload<OP, true>(p, g[r]) : RowPre{};
     t[r] = act[r] ? row_init<OP, true>(p, g[r]) : 0.0;
   }
-  if constexpr (!PK && !MAP && CPK > 1) {
-    // R_0, lane-packed codes: B / CPK loads a batch bring a lane B codes
-    // (slots k .. k + B - 1 of its row), every lane issuing every load
-    // (groups past a slice's width re-read its last group: selected out), so
-    // the waits are exact counters; the gathers and table reads as below.
-    using PT = typename CodePack<CPK>::type;
-    constexpr int NL = B / CPK;
-    int gl[NR];  // each slice's last group (its width is a multiple of CPK)
-#pragma unroll
-    for (int r = 0; r < NR; ++r) gl[r] = max(ws[r] / CPK - 1, 0);
-    PT c[NR][NL];
-#pragma unroll
-    for (int r = 0; r < NR; ++r)
-#pragma unroll
-      for (int i = 0; i < NL; ++i)
-        c[r][i] = __builtin_nontemporal_load(reinterpret_cast<const PT*>(cp[r] + min(i, gl[r]) * kWave * CPK));
-    for (int k = 0; k < wmax; k += B) {
-      bool ok[NR][B];
-      unsigned cq[NR][B];
-      double xv[NR][B];
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-#pragma unroll
-        for (int q = 0; q < B; ++q) {
-          const unsigned w = c[r][q / CPK][(q % CPK) >> 1];
-          cq[r][q] = (q & 1) ? (w >> 16) : (w & 0xffffu);
-          ok[r][q] = (k + q) < width[r] && cq[r][q] != PAD;
-          const int off = ot[ok[r][q] ? (cq[r][q] >> vb) : 0u];
-          xv[r][q] = p.x[a[r] + (ok[r][q] ? off : 0)];
-        }
-      if (k + B < wmax) {  // wave-uniform
-#pragma unroll
-        for (int r = 0; r < NR; ++r)
-#pragma unroll
-          for (int i = 0; i < NL; ++i)
-            c[r][i] = __builtin_nontemporal_load(
-                reinterpret_cast<const PT*>(cp[r] + min((k + B) / CPK + i, gl[r]) * kWave * CPK));
-      }
-      asm volatile("" ::: "memory");  // the next codes go out before the sums
-      double av[NR][B];
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-#pragma unroll
-        for (int q = 0; q < B; ++q) av[r][q] = vt[ok[r][q] ? (cq[r][q] & vm) : 0u];
-#pragma unroll
-      for (int r = 0; r < NR; ++r)
-#pragma unroll
-        for (int q = 0; q < B; ++q) {
-          const double pr = av[r][q] * xv[r][q];
-          const double tn = sub ? t[r] - pr : t[r] + pr;
-          t[r] = ok[r][q] ? tn : t[r];
-        }
-    }
-  } else if constexpr (!PK && !MAP) {
+  if constexpr (!PK && !MAP) {
     // R_0: every lane issues every load (codes of slot min(k, width - 1) of
     // its slice, the gather of a left-out entry at the row's anchor), so a
     // batch is a fixed count of loads and the waits are exact counters
@@ -1200,7 +1137,11 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
     // tables are read for every entry before the sums (slot 0 for a left-out
     // one).  An entry past the lane's width, a padding code or an inactive
     // lane is selected out of the sum (t unchanged).  1.62 -> 1.44 ms at
-    // 512^3 (scripts/code_knobs.py).
+    // 512^3 (scripts/code_knobs.py).  Lane-packed codes (4 or 8 consecutive
+    // slots of a lane in one 8- / 16-byte load, widths padded to a multiple)
+    // measured slower: 1.442 / 1.521 / 1.530 ms for 1 / 4 / 8 codes a load on
+    // one box (profiles/r06/04_ab): the loop waits on its gathers, not on the
+    // code loads' address work.
     int wl[NR];  // each slice's own last slot (NR > 1: slices of other widths)
 #pragma unroll
     for (int r = 0; r < NR; ++r) wl[r] = max(ws[r] - 1, 0);
@@ -1295,7 +1236,7 @@ __device__ __forceinline__ void code_rows_op(const SpArgs& p, const double* vt, 
 // Persistent grid (the tables are staged once per workgroup); each XCD's
 // workgroups walk its contiguous share of the row blocks, NR consecutive
 // blocks at a time.
-template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK, int CPK = 1>
+template <int OP, bool CFSEL, int B, bool MAP, int NR, bool PK>
 __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
   extern __shared__ double vt[];  // nvtab doubles, then notab ints
   int* ot = reinterpret_cast<int*>(vt + p.nvtab);
@@ -1307,7 +1248,100 @@ __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
   const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
   const int r0 = xcd * per_xcd, r1 = min(nrb, r0 + per_xcd);
   for (int rb = r0 + (int)(blockIdx.x >> 3) * NR; rb < r1; rb += per_wg * NR)
-    code_rows_op<OP, CFSEL, B, MAP, NR, PK, CPK>(p, vt, ot, rb, r1);
+    code_rows_op<OP, CFSEL, B, MAP, NR, PK>(p, vt, ot, rb, r1);
+}
+
+// ---------------------------------------------------------------------------
+// Offset-coded rows, jagged and product-parallel (R_0; host:
+// jag_codes_from_padded).  The padded coded loop (k_sell_code) issues a code
+// load and a fine-residual gather for every slot up to its slice's widest row:
+// R_0's slices are padded 1.77x, and the loop is bound by the address work of
+// those gathers (TA busy 90 %, profiles/r05/02_opprof).  Here a slice's rows are
+// sorted by length and only their entries are stored, entry-major (chunk k of
+// the jagged run holds entry k of the cnt(k) longest rows); the 64 lanes of a
+// wave walk a chunk of KC entries per row contiguously, every lane one entry
+// (its row: r = e - the chunk's offset of its k; the row's anchor from that
+// lane by a cross-lane read), form the products into the wave's LDS, and then
+// each lane adds its own row's products in stored order: the same sums and
+// rounding as every other loop (csr_matvec.c:585), so bitwise the same, with
+// one code load and one gather per entry and no padding.  Persistent grid (the
+// value and offset tables are staged once per workgroup), each XCD walking its
+// contiguous share of the row blocks.
+// ---------------------------------------------------------------------------
+template <int OP, int KC>
+__global__ void __launch_bounds__(256) k_code_pw(SpArgs p) {
+  extern __shared__ double vt[];  // nvtab doubles, notab ints, then 4 x 64 KC products
+  int* ot = reinterpret_cast<int*>(vt + p.nvtab);
+  double* prod_all = vt + p.nvtab + (p.notab + 1) / 2;
+  for (int i = threadIdx.x; i < p.nvtab; i += 256) vt[i] = p.vtab[i];
+  for (int i = threadIdx.x; i < p.notab; i += 256) ot[i] = p.otab[i];
+  __syncthreads();
+  const int lane = threadIdx.x & (kWave - 1);
+  double* __restrict__ lp = prod_all + (threadIdx.x >> 6) * (kWave * KC);
+  const int vb = p.vbits;
+  const unsigned vm = (1u << vb) - 1u;
+  const bool sub = op_subtracts<OP>() || (OP == OP_GENERAL && p.w == -1.0);
+  const int nrb = (p.nrows + 255) >> 8;
+  const int per_xcd = (nrb + 7) >> 3;
+  const int xcd = blockIdx.x & 7, per_wg = gridDim.x >> 3;
+  const int rb0 = xcd * per_xcd, rb1 = min(nrb, rb0 + per_xcd);
+  for (int rb = rb0 + (int)(blockIdx.x >> 3); rb < rb1; rb += per_wg) {
+    const int row = map_block(p, rb) * 256 + (int)threadIdx.x;
+    const int slice = row >> 6;
+    if (slice * kWave >= p.nrows) continue;  // uniform per wave
+    const bool own = row < p.nrows;
+    const int blen = own ? mload<true>(p.rowlen + row) : 0;
+    const int width = __builtin_amdgcn_readfirstlane(blen);  // sorted: lane 0 is the longest
+    const int beg = __builtin_amdgcn_readfirstlane(p.slice_ptr[slice]);
+    const int g = own ? (p.rowmap ? mload<true>(p.rowmap + row) : row) : 0;
+    const int a = own ? (p.anc ? mload<true>(p.anc + g) : g) : 0;
+    RowPre pre;
+    double t = 0.0;
+    if (own) {
+      pre = row_preload<OP, true>(p, g);
+      t = row_init<OP, true>(p, g);
+    }
+    const unsigned short* __restrict__ cb = p.code16 + beg;
+    int P0 = 0;
+    for (int k0 = 0; k0 < width; k0 += KC) {
+      int off[KC + 1];
+      off[0] = 0;
+#pragma unroll
+      for (int q = 0; q < KC; ++q) off[q + 1] = off[q] + __popcll(__builtin_amdgcn_ballot_w64((k0 + q) < blen));
+      const int m = off[KC];  // wave-uniform
+      unsigned c[KC];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        const int e = lane + kWave * j;
+        c[j] = (kWave * j < m && e < m) ? (unsigned)__builtin_nontemporal_load(cb + P0 + e) : 0xFFFFu;
+      }
+      double xv[KC];
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        const int e = lane + kWave * j;
+        int r = 0;  // the row of entry e: e - off[q] for the q whose run holds e
+#pragma unroll
+        for (int q = 1; q < KC; ++q) r = e >= off[q] ? e - off[q] : r;
+        r = e < off[1] ? e : r;
+        const int ar = __shfl(a, r & (kWave - 1));
+        xv[j] = e < m ? p.x[ar + ot[c[j] >> vb]] : 0.0;
+      }
+#pragma unroll
+      for (int j = 0; j < KC; ++j) {
+        const int e = lane + kWave * j;
+        if (e < m) lp[e] = vt[c[j] & vm] * xv[j];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int q = 0; q < KC; ++q)
+        if (k0 + q < blen) t = sub ? t - lp[off[q] + lane] : t + lp[off[q] + lane];
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      P0 += m;
+    }
+    if (own) row_store_pre<OP, true>(p, g, false, t, 0.0, 0.0, pre);
+  }
 }
 
 template <int OP, bool CFSEL, bool NT>
@@ -1768,7 +1802,9 @@ __global__ void __launch_bounds__(64 * G) k_sell_dictw(SpArgs p) {
   __syncthreads();
   if (!wave_live) return;
   if (OP == OP_JAC && own) d = blen > 0 ? draw : 0.0;
-  // two register sets in turn, as in k_sell_dict
+  // two register sets in turn, as in k_sell_dict.  (Both sets' loads issued
+  // before the x-tile gather: A_1 2.545 against 2.475 ms; 5 waves a SIMD
+  // through launch bounds spill: 5.78 ms; profiles/r06/07_ab_dictw.)
   for (int k = 0; k < width; k += 32) {
     dictw_load<NT>(cb, vb, Pc, Pv, k + 16, blen, b1);
     asm volatile("" ::: "memory");
@@ -2721,6 +2757,30 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_P
     return hipGetLastError();
   }
+  if (M.code16 && M.rowlen) {  // offset-coded rows, jagged, product-parallel (R_0)
+    a.code16 = M.code16;
+    a.otab = M.otab;
+    a.notab = M.notab;
+    a.vbits = M.vbits;
+    a.anc = M.anc;
+    a.cmap = nullptr;
+    a.vtab = M.vtab;
+    a.nvtab = M.nvtab;
+    if (cfsel || M.cmap) return hipErrorInvalidValue;
+    constexpr int KC = 8;
+    const size_t lds = (size_t)M.nvtab * sizeof(double) + (size_t)((M.notab + 1) / 2) * sizeof(double) +
+                       (size_t)4 * kWave * KC * sizeof(double);
+    const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
+    const dim3 cgrid(std::min(a.nblocks_pad, 256 * per_cu));
+#define HVE_CW(OPV) \
+  case OPV: hipLaunchKernelGGL((k_code_pw<OPV, KC>), cgrid, block, lds, s, a); break;
+    switch (op) {
+      HVE_CW(OP_RESTRICT) HVE_CW(OP_RESTRICT_ZG) HVE_CW(OP_MATVEC) HVE_CW(OP_GENERAL) HVE_CW(OP_PROLONG)
+      default: return hipErrorInvalidValue;
+    }
+#undef HVE_CW
+    return hipGetLastError();
+  }
   if (M.code16 || M.code32) {  // offset-coded (P_0 / R_0 of a grid hierarchy) or packed entries
     a.code16 = M.code16;
     a.code32 = M.code32;
@@ -2735,15 +2795,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     const bool map = M.cmap != nullptr;
     const int nr = knob(0) > 0 ? knob(0) : 1;   // row blocks per workgroup step
     const int cb = knob(1) > 0 ? knob(1) : 8;   // codes per batch
-    const int cpk = (M.code16 && !map) ? M.code_pack : 1;
-    if (cpk != 1 && cpk != 4 && cpk != 8) return hipErrorInvalidValue;
-#define HVE_CP(OPV, CF, BB, NRV)                                                                             \
-  if (cpk == 8) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, false, 8>), cgrid, block, lds, s, a); \
-  else hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, false, 4>), cgrid, block, lds, s, a);
 #define HVE_C2(OPV, CF, BB, NRV)                                                                  \
   if (M.code32) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, true>), cgrid, block, lds, s, a); \
   else if (map) hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, true, NRV, false>), cgrid, block, lds, s, a); \
-  else if (cpk > 1) { HVE_CP(OPV, CF, (BB < 8 ? 8 : BB), NRV) } \
   else hipLaunchKernelGGL((k_sell_code<OPV, CF, BB, false, NRV, false>), cgrid, block, lds, s, a);
 #define HVE_C(OPV, CF)                                                    \
   if (CF) { HVE_C2(OPV, CF, 8, 1) }                                        \
@@ -2764,7 +2818,6 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 #undef HVE_CL
 #undef HVE_C
 #undef HVE_C2
-#undef HVE_CP
     return hipGetLastError();
   }
   if (M.vidx16) {  // 32-bit columns, 16-bit value indices (padded or jagged)

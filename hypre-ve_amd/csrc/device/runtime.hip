@@ -202,7 +202,7 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
     return e ? atoi(e) : 1;
   }();
   const bool coded_auto = coded_env == 2 || (coded_env == 1 && coded && coded->anc);
-  if (coded && A.nnz() > 0 && ((policy == 0 && coded_auto && A.nrows >= (1 << 18)) || policy == 12)) {
+  if (coded && A.nnz() > 0 && ((policy == 0 && coded_auto && A.nrows >= (1 << 18)) || policy == 12 || policy == 15)) {
     static const std::vector<int> none;
     std::vector<int> sp, ot;
     hvec<unsigned short> cd;
@@ -217,16 +217,23 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       nnz_pad = (int64_t)sp.back();
       batch = 8;
       pipe = 1;
-      // Lane-packed codes (R_0: anchors, no position map): a lane's CPK
-      // consecutive codes in one 8- / 16-byte load instead of one 2-byte load
-      // per entry (its loop is address-bound: TA busy 90 %, 2878 vector reads
-      // a wave, profiles/r05/02_opprof).  HVE_CODE_PACK=1|4|8 (default 8).
-      static const int cpk_env = [] {
-        const char* e = getenv("HVE_CODE_PACK");
-        return e ? atoi(e) : 8;
+      // Restrictions (anchors, no position map): the jagged, product-parallel
+      // form (k_code_pw), no padding stored or gathered.  HVE_CODE_PW=0 keeps
+      // the padded loop (k_sell_code); policy 15 forces the jagged form (tests).
+      static const int pw_env = [] {
+        const char* e = getenv("HVE_CODE_PW");
+        return e ? atoi(e) : 0;
       }();
-      code_pack = (!coded->cmap || coded->cmap->empty()) && (cpk_env == 4 || cpk_env == 8) ? cpk_env : 1;
-      if (code_pack > 1) pack_codes_lanes(sp, cd, code_pack);
+      std::vector<int> jperm;
+      if ((!coded->cmap || coded->cmap->empty()) && coded->anc && ((policy == 0 && pw_env != 0) || policy == 15)) {
+        std::vector<int> sp2, rl;
+        hvec<unsigned short> cd2;
+        jag_codes_from_padded(A, sp, cd, jperm, sp2, rl, cd2);
+        sp.swap(sp2);
+        cd.swap(cd2);
+        nnz_pad = nnz;
+        rowlen = dupload(rl.data(), rl.size());
+      }
       slice_ptr = dupload(sp.data(), sp.size());
       code16 = dupload(cd.data(), cd.size());
       otab = dupload(ot.data(), ot.size());
@@ -243,16 +250,20 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
         cmap_n = (int64_t)coded->cmap->size();
       }
       if (getenv("HVE_LAYOUT_LOG"))
-        fprintf(stderr, "[layout] coded rows=%d offsets=%d values=%d vbits=%d pad=%.2f (%.2f packed by %d)\n", A.nrows,
-                notab, nvtab, vbits, (double)nnz_pad / std::max<int64_t>(1, nnz),
-                (double)sp.back() / std::max<int64_t>(1, nnz), code_pack);
-      if (!rowmap_h.empty()) {
-        bool ident = true;
-        for (int i = 0; i < A.nrows && ident; ++i) ident = rowmap_h[i] == i;
-        if (!ident) rowmap = dupload(rowmap_h.data(), rowmap_h.size());
+        fprintf(stderr, "[layout] coded rows=%d offsets=%d values=%d vbits=%d pad=%.2f\n", A.nrows, notab, nvtab, vbits,
+                (double)nnz_pad / std::max<int64_t>(1, nnz));
+      std::vector<int> map = rowmap_h;
+      if (!jperm.empty()) {  // stored (sorted) row -> local row
+        map.resize(A.nrows);
+        for (int i = 0; i < A.nrows; ++i) map[i] = rowmap_h.empty() ? jperm[i] : rowmap_h[jperm[i]];
       }
-      stored_map = rowmap_h;
-      if (key) set_block_order(rowmap_h, *key);
+      if (!map.empty()) {
+        bool ident = true;
+        for (int i = 0; i < A.nrows && ident; ++i) ident = map[i] == i;
+        if (!ident) rowmap = dupload(map.data(), map.size());
+      }
+      stored_map = map;
+      if (key) set_block_order(map, *key);
       return;
     }
   }
@@ -742,7 +753,7 @@ void DevSell::release() {
   for (void* q : {(void*)code16, (void*)otab, (void*)anc, (void*)cmap})
     if (q) (void)hipFree(q);
   code16 = nullptr; otab = nullptr; anc = nullptr; cmap = nullptr;
-  notab = vbits = 0; anc_n = cmap_n = 0; code_pack = 1;
+  notab = vbits = 0; anc_n = cmap_n = 0;
   if (wptr) (void)hipFree(wptr);
   wptr = nullptr;
   wval_n = wcol_n = 0;

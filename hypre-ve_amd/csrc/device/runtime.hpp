@@ -42,7 +42,6 @@ struct DevSell {
   int dict_ranges = 0;     // dictionary layout: the tile is a union of column ranges
   int* wptr = nullptr;     // dictionary layout, lane-packed streams (SellView::wptr)
   int64_t wval_n = 0, wcol_n = 0;  // their stored values / columns (padding included)
-  int code_pack = 1;       // offset-coded layout: codes per lane load (SellView::code_pack)
   short* dcol = nullptr;   // delta layout: 16-bit column deltas
   int* slot_base = nullptr;
   unsigned char* vidx = nullptr;  // delta layout with a value table
@@ -90,7 +89,7 @@ struct DevSell {
     SellView v;
     v.slice_ptr = slice_ptr; v.col = col; v.val = val; v.rowmap = rowmap; v.rowlen = rowlen; v.nrows = nrows; v.ncols = ncols; v.batch = batch; v.pipe = pipe; v.wide = wide; v.pw = pw;
     v.col16 = col16; v.dict_ptr = dict_ptr; v.dict = dict; v.dmax = dmax; v.dict_group = dict_group; v.dict_ranges = dict_ranges;
-    v.wptr = wptr; v.code_pack = code_pack;
+    v.wptr = wptr;
     v.dcol = dcol; v.slot_base = slot_base; v.vidx = vidx; v.vidx16 = vidx16; v.vtab = vtab; v.nvtab = nvtab;
     v.slot_vi = slot_vi; v.slot_mask = slot_mask; v.stencil_w = stencil_w; v.slice_pat = slice_pat;
     v.blk_map = blk_map; v.nblk = nblk; v.wave_map = wave_map; v.nwave = nwave;
@@ -133,7 +132,7 @@ struct DevSell {
       return (size_t)nslices * 4 + (size_t)npat * stencil_w * 16 + (rowmap ? (size_t)nrows * 4 : 0);
     if (code16)  // offset-coded: 2 B a slot, the anchors, the position -> column map once
       return (size_t)(nslices + 1) * 4 + (size_t)nnz_pad * 2 + (size_t)(anc_n + cmap_n) * 4 +
-             (rowmap ? (size_t)nrows * 4 : 0);
+             (rowmap ? (size_t)nrows * 4 : 0) + (rowlen ? (size_t)nrows * 4 : 0);
     if (code32)  // packed: 4 B a slot, a base per slice
       return (size_t)(nslices + 1) * 8 + (size_t)nnz_pad * 4 + (rowmap ? (size_t)nrows * 4 : 0);
     // (lane-packed dictionary streams, wptr: counted by their entries, as the

@@ -769,27 +769,43 @@ bool pack_dict_wide(const std::vector<int>& slice_ptr, const std::vector<int>& r
   return true;
 }
 
-void pack_codes_lanes(std::vector<int>& slice_ptr, hvec<unsigned short>& code, int cpk) {
-  const int ns = (int)slice_ptr.size() - 1;
+void jag_codes_from_padded(const CSR& A, const std::vector<int>& sp_pad, const hvec<unsigned short>& code_pad,
+                           std::vector<int>& perm, std::vector<int>& slice_ptr, std::vector<int>& rowlen,
+                           hvec<unsigned short>& code) {
+  const int n = A.nrows;
+  const int ns = (n + 63) / 64;
+  sell_order(A, 64, perm);  // stable, descending length inside each slice
+  slice_ptr.assign(ns + 1, 0);
+  rowlen.assign((size_t)ns * 64, 0);
   std::vector<int64_t> sp(ns + 1, 0);
   for (int s = 0; s < ns; ++s) {
-    const int w = (slice_ptr[s + 1] - slice_ptr[s]) / 64;
-    sp[s + 1] = sp[s] + (int64_t)((w + cpk - 1) / cpk * cpk) * 64;
+    int64_t t = 0;
+    for (int r = s * 64; r < std::min(n, (s + 1) * 64); ++r) t += A.i[perm[r] + 1] - A.i[perm[r]];
+    sp[s + 1] = sp[s] + t;
   }
-  if (sp[ns] > 0x7fffffffLL) throw std::runtime_error("coded layout exceeds 2^31 slots");
-  hvec<unsigned short> out;
-  out.resize((size_t)sp[ns]);
+  if (sp[ns] > 0x7fffffffLL) throw std::runtime_error("coded operator exceeds 2^31 entries on one GPU");
+  for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
+  code.clear();
+  code.resize((size_t)sp[ns]);
 #pragma omp parallel for schedule(static)
   for (int s = 0; s < ns; ++s) {
-    const int w = (slice_ptr[s + 1] - slice_ptr[s]) / 64;
-    const int wp = (w + cpk - 1) / cpk * cpk;
-    for (int k = 0; k < wp; ++k)
-      for (int l = 0; l < 64; ++l)
-        out[(size_t)sp[s] + (size_t)(k / cpk) * 64 * cpk + (size_t)l * cpk + k % cpk] =
-            k < w ? code[(size_t)slice_ptr[s] + (size_t)k * 64 + l] : (unsigned short)0xFFFF;
+    const int r0 = s * 64, r1 = std::min(n, (s + 1) * 64);
+    int len[64] = {0};
+    for (int r = r0; r < r1; ++r) {
+      len[r - r0] = A.i[perm[r] + 1] - A.i[perm[r]];
+      rowlen[r] = len[r - r0];
+    }
+    size_t pos = (size_t)slice_ptr[s];
+    for (int k = 0; k < len[0]; ++k) {
+      int cnt = 0;
+      while (cnt < r1 - r0 && len[cnt] > k) ++cnt;
+      for (int l = 0; l < cnt; ++l) {
+        const int src = perm[r0 + l];  // its lane in the padded slice: src & 63 (same slice)
+        code[pos + l] = code_pad[(size_t)sp_pad[s] + (size_t)k * 64 + (src & 63)];
+      }
+      pos += cnt;
+    }
   }
-  for (int s = 0; s <= ns; ++s) slice_ptr[s] = (int)sp[s];
-  code.swap(out);
 }
 
 // Packed SELL-64 entries (k_sell_code PK): code = ((col - base[slice]) << vbits)

@@ -92,10 +92,15 @@ bool build_sell_dict_host(const CSR& A, int dmax, int group, std::vector<int>& p
 bool pack_dict_wide(const std::vector<int>& slice_ptr, const std::vector<int>& rowlen,
                     const hvec<unsigned short>& col16, const hvec<double>& val, std::vector<int>& wptr,
                     hvec<unsigned short>& colw, hvec<double>& valw);
-// R_0's offset-coded codes, lane-packed (k_sell_code with CPK codes a load):
-// a slice of padded width w (a multiple of CPK) stores slot k of lane l at
-// slice_ptr[s] + (k / CPK) * 64 CPK + l CPK + k % CPK; padding 0xFFFF.
-void pack_codes_lanes(std::vector<int>& slice_ptr, hvec<unsigned short>& code, int cpk);
+// Jagged form of an offset-coded layout (k_code_pw): every slice's rows sorted
+// by descending length (stable; perm[i] = CSR row at stored position i), entry
+// k of stored lane l at slice_ptr[s] + cnt(0) + ... + cnt(k-1) + l with
+// cnt(k) = #{lanes whose row is longer than k}; no padding stored.  From the
+// padded codes of build_sell_coded_host (sp_pad, code_pad: entries in slots
+// 0 .. len - 1 of their lane) and the rows' lengths.
+void jag_codes_from_padded(const CSR& A, const std::vector<int>& sp_pad, const hvec<unsigned short>& code_pad,
+                           std::vector<int>& perm, std::vector<int>& slice_ptr, std::vector<int>& rowlen,
+                           hvec<unsigned short>& code);
 // Packed SELL-64 entries (k_sell_code PK) from a padded layout (col, 16-bit
 // value indices vi into nv values): code = ((col - base[slice]) << vbits) |
 // value index, base = the slice's smallest column, padding 0xFFFFFFFF.  false

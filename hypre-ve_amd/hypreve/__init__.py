@@ -682,7 +682,7 @@ class BoomerAMG:
         check(lib().hypreve_BoomerAMGSetCoarsenRankStarts(self.h, len(starts) - 1, arr), "SetCoarsenRankStarts")
 
     LAYOUTS = ("padded", "jagged", "wide", "jag-pw", "dict", "delta", "delta+vt8", "delta+vt16", "padded+vt16",
-               "jagged+vt16", "dict-ranges", "stencil", "coded", "packed", "grid-stencil", "dict-wide")
+               "jagged+vt16", "dict-ranges", "stencil", "coded", "packed", "grid-stencil", "dict-wide", "coded-jag")
 
     def level_layout(self, level, which=0):
         """Device layout name of A_l (0), P_l (1) or R_l (2) (interior rows)."""

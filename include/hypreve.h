@@ -279,7 +279,9 @@ HYPRE_Int hypreve_BoomerAMGSetBlockBands(HYPRE_Solver solver, HYPRE_Int nbands,
  * padded, 13 packed P and R (one 32-bit code per entry: column less the
  * slice's smallest column, and value index) where they fit, else as 8,
  * 14 as 5 with the per-entry streams (5 and the automatic choice store the
- * dictionary layout's values and columns lane-packed, 16 B a lane load).
+ * dictionary layout's values and columns lane-packed, 16 B a lane load),
+ * 15 as 12 with R in the jagged, product-parallel coded form (the automatic
+ * choice for restrictions; 12 keeps them padded).
  * All give identical bits; the forced settings exist for parity tests
  * and experiments. */
 HYPRE_Int hypreve_BoomerAMGSetSellPolicy(HYPRE_Solver solver, HYPRE_Int policy);
@@ -378,7 +380,8 @@ HYPRE_Int hypreve_BenchFineSpMVStoredBytes(HYPRE_Solver solver, HYPRE_Real *byte
  * 16-bit value table, 10 range dictionary, 11 slot-uniform stencil,
  * 12 offset-coded (P, R), 13 packed 32-bit codes (P, R), 14 slot-uniform
  * stencil over a grid in natural order (k_grid_stencil: LDS x-tile),
- * 15 dictionary with lane-packed value / column streams (k_sell_dictw). */
+ * 15 dictionary with lane-packed value / column streams (k_sell_dictw),
+ * 16 offset-coded, jagged and product-parallel (k_code_pw: R). */
 HYPRE_Int hypreve_BoomerAMGGetLevelLayout(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int which, HYPRE_Int *kind);
 /* Host check: each hybrid Gauss-Seidel level schedule (num_blocks row blocks)
  * reproduces the sequential per-block sweep bit for bit on random data. */

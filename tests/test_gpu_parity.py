@@ -102,7 +102,7 @@ def test_cf_relaxation_cycle_bitwise(gpu, orc, relax, coarsen, wt):
     assert np.array_equal(x.get(), xo)
 
 
-@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14])
+@pytest.mark.parametrize("policy", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 @pytest.mark.parametrize("relax,order", [(18, 0), (0, 1)])
 def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     """Every device layout / row loop (padded lane-per-row, jagged lane-per-row,
@@ -120,6 +120,8 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     n = A.n
     if policy == 12:  # the layout is really taken (level 0's P and R)
         assert amg.level_layout(0, 1) == "coded" and amg.level_layout(0, 2) == "coded"
+    if policy == 15:  # R in the jagged, product-parallel coded form (k_code_pw), P padded
+        assert amg.level_layout(0, 1) == "coded" and amg.level_layout(0, 2) == "coded-jag"
     if policy == 13:
         assert amg.level_layout(0, 1) == "packed" and amg.level_layout(0, 2) == "packed"
     if policy == 5:  # the lane-packed dictionary streams (k_sell_dictw), A's 4-slice groups included
