@@ -1268,7 +1268,20 @@ __global__ void __launch_bounds__(256) k_sell_code(SpArgs p) {
 // value and offset tables are staged once per workgroup), each XCD walking its
 // contiguous share of the row blocks.
 // ---------------------------------------------------------------------------
-template <int OP, int KC>
+template <int KC>
+__device__ __forceinline__ void code_pw_load(const unsigned short* __restrict__ cb, int P0, int blen, int k0,
+                                             int lane, unsigned (&c)[KC]) {
+  int m = 0;
+#pragma unroll
+  for (int q = 0; q < KC; ++q) m += __popcll(__builtin_amdgcn_ballot_w64((k0 + q) < blen));
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    const int e = lane + kWave * j;
+    c[j] = (kWave * j < m && e < m) ? (unsigned)__builtin_nontemporal_load(cb + P0 + e) : 0xFFFFu;
+  }
+}
+
+template <int OP, int KC, bool PF>
 __global__ void __launch_bounds__(256) k_code_pw(SpArgs p) {
   extern __shared__ double vt[];  // nvtab doubles, notab ints, then 4 x 64 KC products
   int* ot = reinterpret_cast<int*>(vt + p.nvtab);
@@ -1303,17 +1316,19 @@ __global__ void __launch_bounds__(256) k_code_pw(SpArgs p) {
     }
     const unsigned short* __restrict__ cb = p.code16 + beg;
     int P0 = 0;
+    unsigned c[KC];
+    if (PF) code_pw_load<KC>(cb, 0, blen, 0, lane, c);
     for (int k0 = 0; k0 < width; k0 += KC) {
       int off[KC + 1];
       off[0] = 0;
 #pragma unroll
       for (int q = 0; q < KC; ++q) off[q + 1] = off[q] + __popcll(__builtin_amdgcn_ballot_w64((k0 + q) < blen));
       const int m = off[KC];  // wave-uniform
-      unsigned c[KC];
-#pragma unroll
-      for (int j = 0; j < KC; ++j) {
-        const int e = lane + kWave * j;
-        c[j] = (kWave * j < m && e < m) ? (unsigned)__builtin_nontemporal_load(cb + P0 + e) : 0xFFFFu;
+      unsigned cn[KC];
+      if (PF) {  // the next chunk's codes in flight during this chunk's gathers
+        if (k0 + KC < width) code_pw_load<KC>(cb, P0 + m, blen, k0 + KC, lane, cn);
+      } else {
+        code_pw_load<KC>(cb, P0, blen, k0, lane, c);
       }
       double xv[KC];
 #pragma unroll
@@ -1339,6 +1354,10 @@ __global__ void __launch_bounds__(256) k_code_pw(SpArgs p) {
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
       __builtin_amdgcn_wave_barrier();
       P0 += m;
+      if (PF) {
+#pragma unroll
+        for (int j = 0; j < KC; ++j) c[j] = cn[j];
+      }
     }
     if (own) row_store_pre<OP, true>(p, g, false, t, 0.0, 0.0, pre);
   }
@@ -2767,18 +2786,27 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     a.vtab = M.vtab;
     a.nvtab = M.nvtab;
     if (cfsel || M.cmap) return hipErrorInvalidValue;
-    constexpr int KC = 8;
+    // knob 4: entries per row and chunk (4 | 8 | 16), knob 5: 1 = no code prefetch
+    const int kc = (knob(4) == 4 || knob(4) == 16) ? knob(4) : 8;
+    const bool pf = knob(5) != 1;
     const size_t lds = (size_t)M.nvtab * sizeof(double) + (size_t)((M.notab + 1) / 2) * sizeof(double) +
-                       (size_t)4 * kWave * KC * sizeof(double);
-    const int per_cu = std::max(1, std::min(8, (int)((160 * 1024) / lds)));
+                       (size_t)4 * kWave * kc * sizeof(double);
+    const int per_cu = std::max(1, std::min(knob(2) > 0 ? knob(2) : 8, (int)((160 * 1024) / lds)));
     const dim3 cgrid(std::min(a.nblocks_pad, 256 * per_cu));
-#define HVE_CW(OPV) \
-  case OPV: hipLaunchKernelGGL((k_code_pw<OPV, KC>), cgrid, block, lds, s, a); break;
+#define HVE_CW3(OPV, KCV, PFV) hipLaunchKernelGGL((k_code_pw<OPV, KCV, PFV>), cgrid, block, lds, s, a)
+#define HVE_CW(OPV)                        \
+  case OPV:                                \
+    if (kc == 4) HVE_CW3(OPV, 4, true);    \
+    else if (kc == 16) HVE_CW3(OPV, 16, true); \
+    else if (pf) HVE_CW3(OPV, 8, true);    \
+    else HVE_CW3(OPV, 8, false);           \
+    break;
     switch (op) {
       HVE_CW(OP_RESTRICT) HVE_CW(OP_RESTRICT_ZG) HVE_CW(OP_MATVEC) HVE_CW(OP_GENERAL) HVE_CW(OP_PROLONG)
       default: return hipErrorInvalidValue;
     }
 #undef HVE_CW
+#undef HVE_CW3
     return hipGetLastError();
   }
   if (M.code16 || M.code32) {  // offset-coded (P_0 / R_0 of a grid hierarchy) or packed entries

@@ -18,6 +18,8 @@ A = hv.ParCSRMatrix.laplacian(n, n, n)
 kw = hv.ij_amg_defaults(0)
 kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18, tol=1e-300, max_iter=1, min_iter=0)
 kw.update({k: type(kw.get(k, 0))(float(v)) if k in kw else int(v) for k, v in extra.items()})
+if kw["relax_type"] < 0:  # relax_type=-1: BoomerAMG's default smoothers (hybrid GS 13 / 14)
+    del kw["relax_type"]
 amg = hv.BoomerAMG(**kw)
 t = time.time()
 amg.setup(A)

@@ -147,6 +147,32 @@ def test_sell_policy_cycle_bitwise(gpu, orc, policy, relax, order):
     assert np.array_equal(x.get(), xo)
 
 
+@pytest.mark.parametrize("kc,nopf", [(4, 0), (8, 1), (16, 0)])
+def test_code_pw_chunk_variants_bitwise(gpu, orc, kc, nopf):
+    """The jagged coded loop's launch variants (knob 4: entries per row and
+    chunk, knob 5: no code prefetch) give the same bits: R_0 and the cycle."""
+    hv = gpu
+    A, amg, O = setup_pair(hv, orc, (30, 27, 25), coarsen_type=8, interp_type=6, P_max_elmts=4,
+                           relax_type=18, sell_policy=15)
+    assert amg.level_layout(0, 2) == "coded-jag"
+    n = A.n
+    rng = np.random.default_rng(5 + kc)
+    f_h = rng.standard_normal(n)
+    u0 = rng.standard_normal(n)
+    f = hv.ParVector(n, f_h)
+    u = hv.ParVector(n, u0)
+    hv.set_knob(4, kc)
+    hv.set_knob(5, nopf)
+    try:
+        amg.cycle(f, u)
+    finally:
+        hv.set_knob(4, 0)
+        hv.set_knob(5, 0)
+    uo = u0.copy()
+    O.cycle(f_h, uo)
+    assert np.array_equal(u.get(), uo)
+
+
 @pytest.mark.parametrize("policy", [6, 7, 11])
 def test_delta_layout_wide_stride_bitwise(gpu, orc, policy):
     """16-bit column deltas where the z-neighbour is 36000 rows away: the
