@@ -123,6 +123,7 @@ struct GsView {
   const int* cf = nullptr;         // CF marker by position
   int nteams = 0, nrows = 0, max_width = 0;
   bool one_chunk = false;  // every step's rows x width fits one product chunk (k_hybrid_gs_pipe)
+  int cap = 512;           // entries a unit of the pipelined sweep holds at most (128 | 256 | 512)
 };
 // entries of one product chunk of the hybrid-GS kernels (LDS per wave)
 int gs_chunk_entries();

@@ -1888,6 +1888,7 @@ struct GsArgs {
   // C, so an off-block value shares the L2 lines its own team reads, and the
   // gather writes one copy instead of two
   unsigned tshift;
+  int ustore;  // the sweep stores its rows into u too (no k_gs_scatter)
 };
 // G byte offset of an entry's source (ring and padding codes read G[0])
 __device__ __forceinline__ int gs_src_off(int c, unsigned n, unsigned tshift) {
@@ -1930,12 +1931,103 @@ __device__ __forceinline__ void gs_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <bool L1, bool CFSEL, bool WGT>
+// Entries of a chunk per row (even, so that every unit starts on an even
+// entry: the schedule pads each step's entries to an even count, host
+// build_gs_schedule).  The sums do not depend on the chunking.
+__device__ __forceinline__ int gs_kc(int R, int cap = kGsProd) { return (cap / R) & ~1; }
+
+// Slot t of a lane.  PR (paired): slots 2m and 2m + 1 are entries
+// 128 m + 2 lane and + 1, loaded by one 8-byte code load, one 16-byte value
+// load (2-byte for 8-bit value indices) and one 8-byte tcol load, a third of
+// the vector-memory instructions of one entry a slot (lane + 64 t).  The
+// gathers through the codes stay one a slot.
+template <bool PR>
+__device__ __forceinline__ int gs_slot_entry(int t, int lane) {
+  return PR ? 128 * (t >> 1) + 2 * lane + (t & 1) : lane + 64 * t;
+}
+template <bool PR>
+__device__ __forceinline__ int gs_slot_first(int t) {  // the first entry of slot t's load
+  return PR ? 128 * (t >> 1) : 64 * t;
+}
+// The codes, values (8-bit indices when VT) and tcol of a unit's slots:
+// entries [base, base + E) of the step's stream; slots past E read the unit's
+// entry 0 (ALL: every slot is loaded; else loads stop at the first slot past E)
+template <bool PR, bool VT, bool WGT, bool ALL, int NSL, typename AT>
+__device__ __forceinline__ void gs_load_unit(__amdgpu_buffer_rsrc_t rc, __amdgpu_buffer_rsrc_t rv,
+                                             __amdgpu_buffer_rsrc_t rt, int base, int E, int lane,
+                                             int (&c)[NSL], AT (&a)[NSL], int (&tc)[NSL]) {
+  if (PR) {
+#pragma unroll
+    for (int m = 0; m < NSL / 2; ++m) {
+      if (!ALL && 128 * m >= E) break;
+      const int e0 = 128 * m + 2 * lane;
+      const int o = base + (e0 < E ? e0 : 0);  // even: 8- / 16-byte aligned
+      const auto cw = __builtin_amdgcn_raw_buffer_load_b64(rc, o * 4, 0, 0);
+      c[2 * m] = (int)cw[0];
+      c[2 * m + 1] = (int)cw[1];
+      if (VT) {
+        const unsigned v2 = __builtin_amdgcn_raw_buffer_load_b16(rv, o, 0, 0);
+        a[2 * m] = (AT)(v2 & 0xffu);
+        a[2 * m + 1] = (AT)(v2 >> 8);
+      } else {
+        const auto aw = __builtin_amdgcn_raw_buffer_load_b128(rv, o * 8, 0, 0);
+        a[2 * m] = (AT)__builtin_bit_cast(double, ((unsigned long long)aw[1] << 32) | aw[0]);
+        a[2 * m + 1] = (AT)__builtin_bit_cast(double, ((unsigned long long)aw[3] << 32) | aw[2]);
+      }
+      if (WGT) {
+        const auto tw = __builtin_amdgcn_raw_buffer_load_b64(rt, o * 4, 0, 0);
+        tc[2 * m] = (int)tw[0];
+        tc[2 * m + 1] = (int)tw[1];
+      } else {
+        tc[2 * m] = tc[2 * m + 1] = -1;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < NSL; ++t) {
+      if (!ALL && 64 * t >= E) break;
+      const int e = lane + 64 * t;
+      const int o = base + (e < E ? e : 0);
+      c[t] = gs_ld32(rc, o * 4);
+      if (VT) a[t] = (AT)gs_ld8(rv, o);
+      else a[t] = (AT)gs_ld64(rv, o * 8);
+      tc[t] = WGT ? gs_ld32(rt, o * 4) : -1;
+    }
+  }
+}
+
+// A batch of steps leaves the ring: into U (the sweep's later U reads) and,
+// with ustore, into u at the rows' natural positions, so that no scatter
+// pass follows the sweep (nothing in the sweep reads u: T, C and the halo
+// come from G).  Steps j - j % kGsBatch .. j; rgq[d]: lane r's row in step
+// j - j % kGsBatch + d.
+template <typename CI>
+__device__ __forceinline__ void gs_batch_store(const GsArgs& p, CI* steps, const double* ring, double* Ub,
+                                               const int (&rgq)[kGsBatch], int j, int lane) {
+  const int q0 = j - j % kGsBatch;
+#pragma unroll
+  for (int d = 0; d < kGsBatch; ++d) {
+    const int q = q0 + d;
+    if (q > j) break;
+    const int rq = steps[4 * q + 2];
+    const double v = ring[(q % kGsRing) * kWave + lane];
+    if (lane < rq) {
+      Ub[steps[4 * q + 1] + lane] = v;
+      if (p.ustore) p.u[rgq[d]] = v;
+    }
+  }
+}
+
+// CAP: products a chunk holds (LDS a workgroup: 4 x (8 KiB ring + CAP x 8 B),
+// 48 KiB at 512; 40 KiB at 256 fits four workgroups a CU instead of three but
+// measured slower, see launch_hybrid_gs)
+template <bool L1, bool CFSEL, bool WGT, bool PR, int CAP>
 __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
+  constexpr int NSL = CAP / 64;
   __shared__ double ring_all[kGsWaves][kGsRingSlots];
-  __shared__ double prod_all[kGsWaves][kGsProd];
-  __shared__ double prod2_all[kGsWaves][WGT ? kGsProd : 1];
-  __shared__ unsigned char cls_all[kGsWaves][WGT ? kGsProd : 1];
+  __shared__ double prod_all[kGsWaves][CAP];
+  __shared__ double prod2_all[kGsWaves][WGT ? CAP : 1];
+  __shared__ unsigned char cls_all[kGsWaves][WGT ? CAP : 1];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & (kWave - 1);
   // consecutive teams (adjacent rows of the grid, which read each other's T
@@ -1958,6 +2050,10 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
   const auto rF = gs_rsrc(p.F, (unsigned)p.n * 8u);
   const auto rL = gs_rsrc(L1 ? p.l1 : p.F, (unsigned)p.n * 8u);
   const auto rCF = gs_rsrc(CFSEL ? (const void*)p.cf : (const void*)p.F, (unsigned)p.n * 4u);
+  const auto rRM = gs_rsrc(p.rowmap, (unsigned)p.n * 4u);
+  int rgq[kGsBatch];  // ustore: the rows of the batch's steps (lane r: row r of each)
+#pragma unroll
+  for (int d = 0; d < kGsBatch; ++d) rgq[d] = 0;
   for (int j = 0; j < ns; ++j) {
     const unsigned ent = (unsigned)steps[4 * j];
     const int roff = steps[4 * j + 1], R = steps[4 * j + 2], W = steps[4 * j + 3];
@@ -1971,41 +2067,34 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
     const double fv = gs_ld64(rF, (int)((unsigned)kp * 8u));
     const double sc = L1 ? gs_ld64(rL, (int)((unsigned)kp * 8u)) : gs_ld64(rv8, r * 8);
     const int cfv = CFSEL ? gs_ld32(rCF, kp * 4) : 0;
+    const int rg = p.ustore ? gs_ld32(rRM, kp * 4) : 0;
     double res = fv, res0 = 0.0, res2 = 0.0;
-    const int KC = kGsProd / R;
+    const int KC = gs_kc(R, CAP);
     // one chunk of entries [kc, kc + KC) of every row of the step; the first
     // chunk runs straight after the row loads (the loop is for wide rows only,
     // so no loop merge makes the compiler wait for the row loads first)
     auto chunk = [&](int kc) {
       const int kw = min(KC, W - kc), E = kw * R;
       const int base = kc * R;
-      int c[kGsPer], tc[kGsPer];
-      double a[kGsPer], x[kGsPer], rv[kGsPer], t2[kGsPer];
+      int c[NSL], tc[NSL];
+      double a[NSL], x[NSL], rv[NSL], t2[NSL];
+      gs_load_unit<PR, false, WGT, false>(rc, rv8, rt, base, E, lane, c, a, tc);
 #pragma unroll
-      for (int t = 0; t < kGsPer; ++t) {
-        if (64 * t >= E) break;
-        const int e = lane + 64 * t;
-        const int o = base + (e < E ? e : 0);
-        c[t] = gs_ld32(rc, o * 4);
-        a[t] = gs_ld64(rv8, o * 8);
-        tc[t] = WGT ? gs_ld32(rt, o * 4) : -1;
-      }
-#pragma unroll
-      for (int t = 0; t < kGsPer; ++t) {
-        if (64 * t >= E) break;
+      for (int t = 0; t < NSL; ++t) {
+        if (gs_slot_first<PR>(t) >= E) break;
         // unsigned byte offsets: G may exceed 2 GiB (< 4 GiB)
         x[t] = gs_ld64(rG, gs_src_off(c[t], (unsigned)p.n, p.tshift));
         if (WGT) t2[t] = gs_ld64(rG, gs_src_off(tc[t], (unsigned)p.n, p.tshift));
       }
 #pragma unroll
-      for (int t = 0; t < kGsPer; ++t) {
-        if (64 * t >= E) break;
+      for (int t = 0; t < NSL; ++t) {
+        if (gs_slot_first<PR>(t) >= E) break;
         rv[t] = ring[c[t] < -1 ? -2 - c[t] : 0];
       }
 #pragma unroll
-      for (int t = 0; t < kGsPer; ++t) {
-        if (64 * t >= E) break;
-        const int e = lane + 64 * t;
+      for (int t = 0; t < NSL; ++t) {
+        if (gs_slot_first<PR>(t) >= E) break;
+        const int e = gs_slot_entry<PR>(t, lane);
         const int cc = c[t];
         const double xv = cc < -1 ? rv[t] : x[t];
         const double pv = cc == -1 ? 0.0 : a[t] * xv;
@@ -2045,16 +2134,16 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
       un = run ? v : un;
     }
     ring[(j % kGsRing) * kWave + lane] = un;
+#pragma unroll
+    for (int d = 0; d < kGsBatch; ++d)
+      if (j % kGsBatch == d) rgq[d] = rg;
     gs_wave_sync();  // the next steps' lanes read the ring slot
     if (j % kGsBatch == kGsBatch - 1 || j == ns - 1) {
       // the previous batch is complete (issued kGsBatch steps ago) and
       // visible to this wave's later U loads; then this batch leaves the ring
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      for (int q = j - j % kGsBatch; q <= j; ++q) {
-        const int rq = steps[4 * q + 2];
-        if (lane < rq) Ub[steps[4 * q + 1] + lane] = ring[(q % kGsRing) * kWave + lane];
-      }
+      gs_batch_store(p, steps, ring, Ub, rgq, j, lane);
     }
   }
 }
@@ -2079,22 +2168,26 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
 // VT: the values as 8-bit indices into the operator's table of distinct
 // values (level 0 of a constant-coefficient stencil: 2), staged in LDS; a
 // stage keeps the raw index and the table is read when the unit is summed.
-template <bool VT>
+template <bool VT, int NSL>
 struct GsStage {
   using A = typename std::conditional<VT, int, double>::type;
-  int c[kGsPer], tc[kGsPer];
-  A a[kGsPer];  // VT: the index
+  int c[NSL], tc[NSL];
+  A a[NSL];  // VT: the index
   double uo, fv, sc;
   int sci;      // VT and !L1: the diagonal's index (sc unused)
   int cfv, R, kc, kw, roff, j, first, last;
+  int rg;       // ustore: the lane's row (natural index)
 };
 
-template <bool L1, bool CFSEL, bool WGT, bool VT>
+template <bool L1, bool CFSEL, bool WGT, bool VT, bool PR, int CAP>
 __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
+  constexpr int NSL = CAP / 64;  // slots a lane loads per unit
+  // LDS a workgroup: 4 x (8 KiB ring + CAP products), 36 KiB at CAP 128: four
+  // workgroups a CU, the whole 4096-team grid of a 256^3 Galerkin level at once
   __shared__ double ring_all[kGsWaves][kGsRingSlots];
-  __shared__ double prod_all[kGsWaves][kGsProd];
-  __shared__ double prod2_all[kGsWaves][WGT ? kGsProd : 1];
-  __shared__ unsigned char cls_all[kGsWaves][WGT ? kGsProd : 1];
+  __shared__ double prod_all[kGsWaves][CAP];
+  __shared__ double prod2_all[kGsWaves][WGT ? CAP : 1];
+  __shared__ unsigned char cls_all[kGsWaves][WGT ? CAP : 1];
   __shared__ double vt_lds[VT ? 256 : 1];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & (kWave - 1);
@@ -2121,10 +2214,14 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
   const auto rF = gs_rsrc(p.F, (unsigned)p.n * 8u);
   const auto rL = gs_rsrc(L1 ? p.l1 : p.F, (unsigned)p.n * 8u);
   const auto rCF = gs_rsrc(CFSEL ? (const void*)p.cf : (const void*)p.F, (unsigned)p.n * 4u);
+  const auto rRM = gs_rsrc(p.rowmap, (unsigned)p.n * 4u);
+  int rgq[kGsBatch];
+#pragma unroll
+  for (int d = 0; d < kGsBatch; ++d) rgq[d] = 0;
   // unit (j, c): chunk c of step j; the next one, j = ns at the end
   auto next_unit = [&](int& j, int& c) {
     const int R = steps[4 * j + 2], W = steps[4 * j + 3];
-    const int KC = kGsProd / R;
+    const int KC = gs_kc(R, CAP);
     if ((c + 1) * KC < W) {
       ++c;
     } else {
@@ -2133,14 +2230,14 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
     }
   };
   // the unit's codes, values (never written during the sweep) and, for a
-  // step's first unit, its row data; every lane loads kGsPer entries (those
+  // step's first unit, its row data; every lane loads NSL entries (those
   // past the unit read its entry 0)
-  auto load_a = [&](int j, int c, GsStage<VT>& S) {
+  auto load_a = [&](int j, int c, GsStage<VT, NSL>& S) {
     const unsigned ent = (unsigned)steps[4 * j];
     S.roff = steps[4 * j + 1];
     S.R = steps[4 * j + 2];
     const int W = steps[4 * j + 3];
-    const int KC = kGsProd / S.R;
+    const int KC = gs_kc(S.R, CAP);
     S.j = j;
     S.kc = c * KC;
     S.kw = min(KC, W - S.kc);
@@ -2158,28 +2255,21 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
       else if (VT) S.sci = gs_ld8(rv8, r);
       else S.sc = gs_ld64(rv8, r * 8);
       S.cfv = CFSEL ? gs_ld32(rCF, kp * 4) : 0;
+      S.rg = p.ustore ? gs_ld32(rRM, kp * 4) : 0;
     }
     const int E = S.kw * S.R, base = S.kc * S.R;
-#pragma unroll
-    for (int t = 0; t < kGsPer; ++t) {
-      const int e = lane + 64 * t;
-      const int o = base + (e < E ? e : 0);
-      S.c[t] = gs_ld32(rc, o * 4);
-      if (VT) S.a[t] = gs_ld8(rv8, o);
-      else S.a[t] = gs_ld64(rv8, o * 8);
-      S.tc[t] = WGT ? gs_ld32(rt, o * 4) : -1;
-    }
+    gs_load_unit<PR, VT, WGT, true>(rc, rv8, rt, base, E, lane, S.c, S.a, S.tc);
   };
   // the unit's source values from G (ring and padding codes read G[0], unused)
-  auto load_b = [&](const GsStage<VT>& S, double (&x)[kGsPer], double (&t2)[kGsPer]) {
+  auto load_b = [&](const GsStage<VT, NSL>& S, double (&x)[NSL], double (&t2)[NSL]) {
 #pragma unroll
-    for (int t = 0; t < kGsPer; ++t) {
+    for (int t = 0; t < NSL; ++t) {
       x[t] = gs_ld64(rG, gs_src_off(S.c[t], (unsigned)p.n, p.tshift));
       t2[t] = WGT ? gs_ld64(rG, gs_src_off(S.tc[t], (unsigned)p.n, p.tshift)) : 0.0;
     }
   };
-  GsStage<VT> S0, S1, S2;
-  double x0[kGsPer], x1[kGsPer], u0[kGsPer], u1[kGsPer];
+  GsStage<VT, NSL> S0, S1, S2;
+  double x0[NSL], x1[NSL], u0[NSL], u1[NSL];
   int j1 = 0, c1 = 0, j2 = 0, c2 = 0;
   if (ns > 0) {
     load_a(0, 0, S0);
@@ -2193,7 +2283,7 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
   }
   if (ns > 0) load_b(S0, x0, u0);
   double res = 0.0, res0 = 0.0, res2 = 0.0, uo = 0.0, sc = 0.0;
-  int cfv = 0;
+  int cfv = 0, rg = 0;
   bool more = ns > 0;
   while (more) {
     const bool have1 = j1 < ns, have2 = j2 < ns;
@@ -2208,16 +2298,17 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
       uo = S0.uo;
       sc = (VT && !L1) ? vt_lds[S0.sci] : S0.sc;
       cfv = S0.cfv;
+      rg = S0.rg;
     }
-    double rv[kGsPer], av[kGsPer];
+    double rv[NSL], av[NSL];
 #pragma unroll
-    for (int t = 0; t < kGsPer; ++t) {
+    for (int t = 0; t < NSL; ++t) {
       rv[t] = ring[S0.c[t] < -1 ? -2 - S0.c[t] : 0];
       av[t] = VT ? vt_lds[(int)S0.a[t]] : (double)S0.a[t];
     }
 #pragma unroll
-    for (int t = 0; t < kGsPer; ++t) {
-      const int e = lane + 64 * t;
+    for (int t = 0; t < NSL; ++t) {
+      const int e = gs_slot_entry<PR>(t, lane);
       const int cc = S0.c[t];
       const double xv = cc < -1 ? rv[t] : x0[t];
       const double pv = cc == -1 ? 0.0 : av[t] * xv;
@@ -2255,14 +2346,14 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
         un = run ? v : un;
       }
       ring[(j % kGsRing) * kWave + lane] = un;
+#pragma unroll
+      for (int d = 0; d < kGsBatch; ++d)
+        if (j % kGsBatch == d) rgq[d] = rg;
       gs_wave_sync();  // the next steps' lanes read the ring slot; the next products overwrite prod
       if (j % kGsBatch == kGsBatch - 1 || j == ns - 1) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-        for (int q = j - j % kGsBatch; q <= j; ++q) {
-          const int rq = steps[4 * q + 2];
-          if (lane < rq) Ub[steps[4 * q + 1] + lane] = ring[(q % kGsRing) * kWave + lane];
-        }
+        gs_batch_store(p, steps, ring, Ub, rgq, j, lane);
       }
     } else {
       gs_wave_sync();  // the next chunk overwrites the products
@@ -2271,7 +2362,7 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
     S0 = S1;
     S1 = S2;
 #pragma unroll
-    for (int t = 0; t < kGsPer; ++t) { x0[t] = x1[t]; u0[t] = u1[t]; }
+    for (int t = 0; t < NSL; ++t) { x0[t] = x1[t]; u0[t] = u1[t]; }
     j1 = j2;
     c1 = c2;
     if (have2) next_unit(j2, c2);
@@ -2338,6 +2429,7 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   a.l1 = S.l1; a.cf = S.cf; a.G = G; a.F = F; a.u = u;
   a.n = S.nrows; a.nteams = S.nteams; a.relax_points = relax_points; a.w = w; a.omega = omega;
   a.tshift = t_is_c ? (unsigned)S.nrows : 0u;
+  a.ustore = knob(13) == 1 ? 0 : 1;  // knob 13 = 1: the separate scatter pass (the A/B)
   const uint64_t gbytes = (3 * (uint64_t)S.nrows + (uint64_t)nhalo) * sizeof(double);
   if (gbytes > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit buffer offsets (about 178M rows a GPU)
   a.gbytes = (unsigned)gbytes;
@@ -2346,23 +2438,45 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   if (use_l1 && !S.l1) return hipErrorInvalidValue;
   if (cfsel && !S.cf) return hipErrorInvalidValue;
   const dim3 grid(((S.nteams + kGsWaves - 1) / kGsWaves + 7) & ~7), blk(kGsWaves * kWave);
-  const bool pipe = gs_uses_pipe(S.one_chunk) || S.vidx8;
+  // knob 8: 1 = the pipelined sweep on every schedule, 2 = on none (but 8-bit
+  // value indices, which only it reads); knob 10: its unit capacity (128 |
+  // 256 | 512 entries; default the schedule's, GsView::cap)
+  const int pmode = knob(8);
+  const bool pipe = S.vidx8 || pmode == 1 || (pmode == 0 && gs_uses_pipe(S.one_chunk));
+  const int cap = S.vidx8 ? 512 : (knob(10) == 128 || knob(10) == 256 || knob(10) == 512) ? knob(10) : S.cap;
+  // k_hybrid_gs's chunk: 512 products; knob 12 = 256 takes 256 (four
+  // workgroups a CU instead of three, but wide steps in more chunks: the
+  // cycle 7.08 against 6.87-6.91 ms at 256^3, 48.3 against 44.9 ms at 512^3,
+  // profiles/r06/15_gschunk)
+  const int ncap = knob(12) == 256 ? 256 : 512;
   if (!S.vidx8 && !S.val) return hipErrorInvalidValue;
-#define HVE_G(L1V, CFV, WV)                                                                           \
-  if (S.vidx8) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, true>), grid, blk, 0, st, a);        \
-  else if (pipe) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false>), grid, blk, 0, st, a);    \
-  else hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV>), grid, blk, 0, st, a);
+  // knob 6 = 1: one entry a slot (the unpaired loads), l1 sweeps without C/F
+  // selection or weights only (the A/B against the paired loads)
+  const bool unpaired = knob(6) == 1 && use_l1 && !cfsel && !wgt;
+#define HVE_GP(L1V, CFV, WV, PRV)                                                                          \
+  if (S.vidx8) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, true, PRV, 512>), grid, blk, 0, st, a);   \
+  else if (!pipe && ncap == 512) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, PRV, 512>), grid, blk, 0, st, a); \
+  else if (!pipe) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, PRV, 256>), grid, blk, 0, st, a);           \
+  else if (cap == 128) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 128>), grid, blk, 0, st, a); \
+  else if (cap == 256) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 256>), grid, blk, 0, st, a); \
+  else hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 512>), grid, blk, 0, st, a);
+#define HVE_G(L1V, CFV, WV) HVE_GP(L1V, CFV, WV, true)
 #define HVE_GW(L1V, CFV) \
   if (wgt) { HVE_G(L1V, CFV, true) } else { HVE_G(L1V, CFV, false) }
-  if (use_l1) {
+  if (unpaired) {
+    HVE_GP(true, false, false, false)
+  } else if (use_l1) {
     if (cfsel) { HVE_GW(true, true) } else { HVE_GW(true, false) }
   } else {
     if (cfsel) { HVE_GW(false, true) } else { HVE_GW(false, false) }
   }
 #undef HVE_GW
 #undef HVE_G
-  const int sgrid = std::min((S.nrows + 255) / 256 + 7, 256 * 16) & ~7;
-  hipLaunchKernelGGL(k_gs_scatter, dim3(sgrid), dim3(256), 0, st, S.nrows, S.rowmap, G + 2 * (size_t)S.nrows, u);
+#undef HVE_GP
+  if (!a.ustore) {
+    const int sgrid = std::min((S.nrows + 255) / 256 + 7, 256 * 16) & ~7;
+    hipLaunchKernelGGL(k_gs_scatter, dim3(sgrid), dim3(256), 0, st, S.nrows, S.rowmap, G + 2 * (size_t)S.nrows, u);
+  }
   return hipGetLastError();
 }
 
@@ -2791,7 +2905,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     const bool pf = knob(5) != 1;
     const size_t lds = (size_t)M.nvtab * sizeof(double) + (size_t)((M.notab + 1) / 2) * sizeof(double) +
                        (size_t)4 * kWave * kc * sizeof(double);
-    const int per_cu = std::max(1, std::min(knob(2) > 0 ? knob(2) : 8, (int)((160 * 1024) / lds)));
+    // 4 workgroups a CU: 1.45 ms for R_0 at 512^3 against 1.60 with 6 (the LDS
+    // limit) and 1.63 / 2.20 with 3 / 2 (profiles/r06/11_r0wpc)
+    const int per_cu = std::max(1, std::min(knob(2) > 0 ? knob(2) : 4, (int)((160 * 1024) / lds)));
     const dim3 cgrid(std::min(a.nblocks_pad, 256 * per_cu));
 #define HVE_CW3(OPV, KCV, PFV) hipLaunchKernelGGL((k_code_pw<OPV, KCV, PFV>), cgrid, block, lds, s, a)
 #define HVE_CW(OPV)                        \

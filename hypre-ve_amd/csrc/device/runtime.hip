@@ -217,15 +217,12 @@ void DevSell::upload(const CSR& A, const std::vector<int>& rowmap_h, int policy,
       nnz_pad = (int64_t)sp.back();
       batch = 8;
       pipe = 1;
-      // Restrictions (anchors, no position map): the jagged, product-parallel
-      // form (k_code_pw), no padding stored or gathered.  HVE_CODE_PW=0 keeps
-      // the padded loop (k_sell_code); policy 15 forces the jagged form (tests).
-      static const int pw_env = [] {
-        const char* e = getenv("HVE_CODE_PW");
-        return e ? atoi(e) : 0;
-      }();
+      // Policy 15: restrictions (anchors, no position map) in the jagged,
+      // product-parallel form (k_code_pw), no padding stored or gathered.  Not
+      // the default: R_0 at 512^3 took 1.434-1.603 ms over its launch variants
+      // against 1.405 ms for the padded loop on one box (profiles/r06/11_r0wpc).
       std::vector<int> jperm;
-      if ((!coded->cmap || coded->cmap->empty()) && coded->anc && ((policy == 0 && pw_env != 0) || policy == 15)) {
+      if ((!coded->cmap || coded->cmap->empty()) && coded->anc && policy == 15) {
         std::vector<int> sp2, rl;
         hvec<unsigned short> cd2;
         jag_codes_from_padded(A, sp, cd, jperm, sp2, rl, cd2);
@@ -787,7 +784,15 @@ void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forw
   max_width = S.max_width;
   one_chunk = true;  // k_hybrid_gs_pipe: every step's entries in one product chunk
   for (size_t q = 0; q + 3 < S.step.size() && one_chunk; q += 4)
-    one_chunk = (int64_t)S.step[q + 2] * S.step[q + 3] <= gs_chunk_entries();
+    one_chunk = S.step[q + 3] <= ((gs_chunk_entries() / S.step[q + 2]) & ~1);  // kernels.hip gs_kc
+  // the pipelined sweep's unit capacity: the power of two (128 to 512) at or
+  // above the mean entries a step, so that a lane loads no more slots than a
+  // typical step fills
+  {
+    const int64_t nst = (int64_t)S.step.size() / 4;
+    const double mean = nst ? (double)S.code.size() / (double)nst : 0.0;
+    cap = mean <= 128 ? 128 : mean <= 256 ? 256 : 512;
+  }
   entries = (int64_t)S.code.size();
   nnz = S.nnz;
   team_step = dupload(S.team_step.data(), S.team_step.size());
@@ -832,6 +837,7 @@ void DevGs::release() {
   nvtab = 0;
   nrows = nteams = nblocks = max_steps = max_width = 0;
   one_chunk = false;
+  cap = 512;
   entries = nnz = 0;
 }
 

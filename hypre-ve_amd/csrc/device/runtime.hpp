@@ -179,6 +179,7 @@ struct DevGs {
   int* cf = nullptr;     // by position
   int nrows = 0, nteams = 0, nblocks = 0, max_steps = 0, max_width = 0;
   bool one_chunk = false;
+  int cap = 512;  // unit capacity of the pipelined sweep (GsView::cap)
   int64_t entries = 0, nnz = 0;
   bool built() const { return nblocks > 0; }
   GsView view() const {
@@ -186,6 +187,7 @@ struct DevGs {
     v.team_step = team_step; v.step = step; v.code = code; v.val = val; v.tcol = tcol; v.rowmap = rowmap;
     v.pos = pos; v.l1 = l1; v.cf = cf; v.nteams = nteams; v.nrows = nrows; v.max_width = max_width;
     v.one_chunk = one_chunk;
+    v.cap = cap;
     v.vidx8 = vidx8; v.vtab = vtab; v.nvtab = nvtab;
     return v;
   }

@@ -917,6 +917,11 @@ void gs_levels(const CSR& A, const std::vector<int>& block_start, bool forward, 
 
 int knob(int id);  // kernels.hip (tests' knobs)
 
+// A step's stored entries: rows x width, padded to an even count so that every
+// step (and every chunk of one, kernels.hip gs_kc) starts on an even entry,
+// where the sweep's paired 8- / 16-byte loads are aligned
+static int64_t gs_step_entries(int width, int rows) { return ((int64_t)width * rows + 1) & ~(int64_t)1; }
+
 void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool forward, GsSchedule& S,
                        int team_rows, bool with_tcol, const std::vector<double>* l1, const std::vector<int>* cf) {
   const int n = A.nrows, nb = (int)block_start.size() - 1;
@@ -975,7 +980,7 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
     int64_t ns = 0, ne = 0;
     for_each_step(t, [&](const int* rows, int cnt) {
       ++ns;
-      ne += (int64_t)width_of(rows, cnt) * cnt;
+      ne += gs_step_entries(width_of(rows, cnt), cnt);
     });
     t_steps[t + 1] = ns;
     t_ent[t + 1] = ne;
@@ -1018,7 +1023,7 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
       }
       ++s;
       r += cnt;
-      e += (int64_t)w * cnt;
+      e += gs_step_entries(w, cnt);
     });
   }
 #pragma omp parallel for schedule(dynamic, 4)
@@ -1140,6 +1145,7 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
       const size_t base = (uint32_t)m[0];
       const int cnt = m[2], width = m[3], j = s - s0;
       if (cnt < 1 || cnt > 64) { msg = "step rows out of range"; return 1; }
+      if (base & 1) { msg = "step entries not on an even offset (paired loads)"; return 1; }
       std::vector<double> out(cnt);
       for (int q = 0; q < cnt; ++q) {
         const int kpos = m[1] + q, i = S.rowmap[kpos];

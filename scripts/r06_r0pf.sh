@@ -5,6 +5,6 @@ set -o pipefail
 OUT=gpurun_out/r06/${1:-11_r0wpc}
 mkdir -p $OUT
 true && \
-HVE_CODE_PW=0 timeout -k 10 200 python -u scripts/r0_pw_knobs.py 512 > $OUT/pw0.txt 2>&1 && \
-HVE_CODE_PW=1 timeout -k 10 200 python -u scripts/r0_pw_knobs.py 512 > $OUT/pw1.txt 2>&1
+timeout -k 10 200 python -u scripts/r0_pw_knobs.py 512 > $OUT/pw0.txt 2>&1 && \
+timeout -k 10 200 python -u scripts/r0_pw_knobs.py 512 jag > $OUT/pw1.txt 2>&1
 echo "exit $?"

@@ -1,11 +1,10 @@
-"""R_0 on the jagged product-parallel coded loop (HVE_CODE_PW=1 at upload):
+"""R_0 on the jagged product-parallel coded loop (sell policy 15 at upload):
 knob 4 = entries per row and chunk (4 | 8 | 16), knob 5 = 1 turns the code
 prefetch off, knob 2 caps workgroups per CU; each variant timed alone on the
-bench hierarchy at N^3 (HIP events, bench_level_op).  With HVE_CODE_PW=0 the
-padded coded loop's time is printed once for comparison.
-python scripts/r0_pw_knobs.py N"""
+bench hierarchy at N^3 (HIP events, bench_level_op).  Without "jag" the
+padded coded loop's time is printed for comparison.
+python scripts/r0_pw_knobs.py N [jag]"""
 import json
-import os
 import sys
 
 sys.path.insert(0, "hypre-ve_amd")
@@ -16,11 +15,14 @@ hv.init()
 A = hv.ParCSRMatrix.laplacian(n, n, n)
 kw = hv.ij_amg_defaults(0)
 kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
+jag = "jag" in sys.argv[2:]
+if jag:
+    kw.update(sell_policy=15)
 amg = hv.BoomerAMG(**kw)
 amg.setup(A)
 layout = amg.level_layout(0, 2)
 variants = [(8, 0, 4), (8, 1, 4), (8, 0, 3), (8, 1, 3), (8, 0, 2), (8, 1, 2), (4, 0, 4), (4, 0, 2), (8, 0, 6), (8, 0, 4)]
-if os.environ.get("HVE_CODE_PW", "0") == "0":
+if not jag:
     variants = [(0, 0, 0), (0, 0, 6), (0, 0, 4), (0, 0, 3), (0, 0, 0)]
 for kc, nopf, wpc in variants:
     hv.set_knob(4, kc)
