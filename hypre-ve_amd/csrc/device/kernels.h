@@ -124,6 +124,7 @@ struct GsView {
   int nteams = 0, nrows = 0, max_width = 0;
   bool one_chunk = false;  // every step's rows x width fits one product chunk (k_hybrid_gs_pipe)
   int cap = 512;           // entries a unit of the pipelined sweep holds at most (128 | 256 | 512)
+  int ring_w = 64;         // lanes of an LDS ring slot = most rows a step (GsSchedule::ring_w)
 };
 // entries of one product chunk of the hybrid-GS kernels (LDS per wave)
 int gs_chunk_entries();

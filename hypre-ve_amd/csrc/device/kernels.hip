@@ -1889,6 +1889,7 @@ struct GsArgs {
   // gather writes one copy instead of two
   unsigned tshift;
   int ustore;  // the sweep stores its rows into u too (no k_gs_scatter)
+  int rw;      // ring width: lanes a ring slot holds, the schedule's most rows a step (16 | 64)
 };
 // G byte offset of an entry's source (ring and padding codes read G[0])
 __device__ __forceinline__ int gs_src_off(int c, unsigned n, unsigned tshift) {
@@ -2010,7 +2011,7 @@ __device__ __forceinline__ void gs_batch_store(const GsArgs& p, CI* steps, const
     const int q = q0 + d;
     if (q > j) break;
     const int rq = steps[4 * q + 2];
-    const double v = ring[(q % kGsRing) * kWave + lane];
+    const double v = ring[lane < rq ? (q % kGsRing) * p.rw + lane : 0];
     if (lane < rq) {
       Ub[steps[4 * q + 1] + lane] = v;
       if (p.ustore) p.u[rgq[d]] = v;
@@ -2024,7 +2025,7 @@ __device__ __forceinline__ void gs_batch_store(const GsArgs& p, CI* steps, const
 template <bool L1, bool CFSEL, bool WGT, bool PR, int CAP>
 __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
   constexpr int NSL = CAP / 64;
-  __shared__ double ring_all[kGsWaves][kGsRingSlots];
+  extern __shared__ double gs_ring_all[];  // kGsWaves x kGsRing x p.rw (dynamic: the schedule's ring width)
   __shared__ double prod_all[kGsWaves][CAP];
   __shared__ double prod2_all[kGsWaves][WGT ? CAP : 1];
   __shared__ unsigned char cls_all[kGsWaves][WGT ? CAP : 1];
@@ -2034,7 +2035,7 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
   // values) on one XCD: the grid is padded to a multiple of 8
   const int team = xcd_logical_block(blockIdx.x, gridDim.x) * kGsWaves + wave;
   if (team >= p.nteams) return;
-  double* ring = ring_all[wave];
+  double* ring = gs_ring_all + wave * kGsRing * p.rw;
   double* prod = prod_all[wave];
   double* prod2 = prod2_all[wave];
   unsigned char* cls = cls_all[wave];
@@ -2133,7 +2134,7 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs(GsArgs p) {
       const double v = L1 ? un + res / sc : res / sc;
       un = run ? v : un;
     }
-    ring[(j % kGsRing) * kWave + lane] = un;
+    if (lane < p.rw) ring[(j % kGsRing) * p.rw + lane] = un;
 #pragma unroll
     for (int d = 0; d < kGsBatch; ++d)
       if (j % kGsBatch == d) rgq[d] = rg;
@@ -2184,7 +2185,7 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
   constexpr int NSL = CAP / 64;  // slots a lane loads per unit
   // LDS a workgroup: 4 x (8 KiB ring + CAP products), 36 KiB at CAP 128: four
   // workgroups a CU, the whole 4096-team grid of a 256^3 Galerkin level at once
-  __shared__ double ring_all[kGsWaves][kGsRingSlots];
+  extern __shared__ double gs_ring_all[];  // kGsWaves x kGsRing x p.rw (dynamic: the schedule's ring width)
   __shared__ double prod_all[kGsWaves][CAP];
   __shared__ double prod2_all[kGsWaves][WGT ? CAP : 1];
   __shared__ unsigned char cls_all[kGsWaves][WGT ? CAP : 1];
@@ -2199,7 +2200,7 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
   // values) on one XCD: the grid is padded to a multiple of 8
   const int team = xcd_logical_block(blockIdx.x, gridDim.x) * kGsWaves + wave;
   if (team >= p.nteams) return;
-  double* ring = ring_all[wave];
+  double* ring = gs_ring_all + wave * kGsRing * p.rw;
   double* prod = prod_all[wave];
   double* prod2 = prod2_all[wave];
   unsigned char* cls = cls_all[wave];
@@ -2345,7 +2346,7 @@ __global__ void __launch_bounds__(kGsWaves * kWave) k_hybrid_gs_pipe(GsArgs p) {
         const double v = L1 ? un + res / sc : res / sc;
         un = run ? v : un;
       }
-      ring[(j % kGsRing) * kWave + lane] = un;
+      if (lane < p.rw) ring[(j % kGsRing) * p.rw + lane] = un;
 #pragma unroll
       for (int d = 0; d < kGsBatch; ++d)
         if (j % kGsBatch == d) rgq[d] = rg;
@@ -2430,6 +2431,9 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   a.n = S.nrows; a.nteams = S.nteams; a.relax_points = relax_points; a.w = w; a.omega = omega;
   a.tshift = t_is_c ? (unsigned)S.nrows : 0u;
   a.ustore = knob(13) == 1 ? 0 : 1;  // knob 13 = 1: the separate scatter pass (the A/B)
+  a.rw = S.ring_w;
+  if (a.rw != 16 && a.rw != 64) return hipErrorInvalidValue;
+  const size_t rlds = (size_t)kGsWaves * kGsRing * a.rw * sizeof(double);
   const uint64_t gbytes = (3 * (uint64_t)S.nrows + (uint64_t)nhalo) * sizeof(double);
   if (gbytes > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit buffer offsets (about 178M rows a GPU)
   a.gbytes = (unsigned)gbytes;
@@ -2454,12 +2458,12 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   // selection or weights only (the A/B against the paired loads)
   const bool unpaired = knob(6) == 1 && use_l1 && !cfsel && !wgt;
 #define HVE_GP(L1V, CFV, WV, PRV)                                                                          \
-  if (S.vidx8) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, true, PRV, 512>), grid, blk, 0, st, a);   \
-  else if (!pipe && ncap == 512) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, PRV, 512>), grid, blk, 0, st, a); \
-  else if (!pipe) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, PRV, 256>), grid, blk, 0, st, a);           \
-  else if (cap == 128) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 128>), grid, blk, 0, st, a); \
-  else if (cap == 256) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 256>), grid, blk, 0, st, a); \
-  else hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 512>), grid, blk, 0, st, a);
+  if (S.vidx8) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, true, PRV, 512>), grid, blk, rlds, st, a);   \
+  else if (!pipe && ncap == 512) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, PRV, 512>), grid, blk, rlds, st, a); \
+  else if (!pipe) hipLaunchKernelGGL((k_hybrid_gs<L1V, CFV, WV, PRV, 256>), grid, blk, rlds, st, a);           \
+  else if (cap == 128) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 128>), grid, blk, rlds, st, a); \
+  else if (cap == 256) hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 256>), grid, blk, rlds, st, a); \
+  else hipLaunchKernelGGL((k_hybrid_gs_pipe<L1V, CFV, WV, false, PRV, 512>), grid, blk, rlds, st, a);
 #define HVE_G(L1V, CFV, WV) HVE_GP(L1V, CFV, WV, true)
 #define HVE_GW(L1V, CFV) \
   if (wgt) { HVE_G(L1V, CFV, true) } else { HVE_G(L1V, CFV, false) }

@@ -782,6 +782,7 @@ void DevGs::upload(const CSR& A, const std::vector<int>& block_starts, bool forw
   nteams = S.nteams;
   max_steps = S.max_steps;
   max_width = S.max_width;
+  ring_w = S.ring_w;
   one_chunk = true;  // k_hybrid_gs_pipe: every step's entries in one product chunk
   for (size_t q = 0; q + 3 < S.step.size() && one_chunk; q += 4)
     one_chunk = S.step[q + 3] <= ((gs_chunk_entries() / S.step[q + 2]) & ~1);  // kernels.hip gs_kc
@@ -838,6 +839,7 @@ void DevGs::release() {
   nrows = nteams = nblocks = max_steps = max_width = 0;
   one_chunk = false;
   cap = 512;
+  ring_w = 64;
   entries = nnz = 0;
 }
 

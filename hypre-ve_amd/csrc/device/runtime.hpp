@@ -180,6 +180,7 @@ struct DevGs {
   int nrows = 0, nteams = 0, nblocks = 0, max_steps = 0, max_width = 0;
   bool one_chunk = false;
   int cap = 512;  // unit capacity of the pipelined sweep (GsView::cap)
+  int ring_w = 64;
   int64_t entries = 0, nnz = 0;
   bool built() const { return nblocks > 0; }
   GsView view() const {
@@ -188,6 +189,7 @@ struct DevGs {
     v.pos = pos; v.l1 = l1; v.cf = cf; v.nteams = nteams; v.nrows = nrows; v.max_width = max_width;
     v.one_chunk = one_chunk;
     v.cap = cap;
+    v.ring_w = ring_w;
     v.vidx8 = vidx8; v.vtab = vtab; v.nvtab = nvtab;
     return v;
   }

@@ -930,6 +930,12 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
   S = GsSchedule();
   S.block_start = block_start;
   team_rows = std::max(1, team_rows);
+  // rows a step, lanes a ring slot: 64.  Knob 14 = 16 takes 16 for the small
+  // teams of wide operators (a quarter of the LDS ring: six workgroups a CU
+  // instead of three, but steps of at most 16 rows): the cycle 6.99 against
+  // 7.06 ms at 256^3, 47.5 against 44.3 ms at 512^3 (profiles/r06/17_gsring)
+  const int rw = (team_rows <= 4 && knob(14) == 16) ? 16 : 64;
+  S.ring_w = rw;
   // ring reach: values computed up to kGsFence steps earlier come from the LDS
   // ring, older ones from U.  Knob 11 (tests only) shortens it, which hands U
   // values out before the kernel's fences publish them: gs_schedule_self_check
@@ -966,7 +972,7 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
         const int ns = block_start[b];
         for (int q = G.lptr[b][l]; q < G.lptr[b][l + 1]; ++q) rows.push_back(G.byl[ns + q]);
       }
-      for (size_t r0 = 0; r0 < rows.size(); r0 += 64) fn(rows.data() + r0, (int)std::min<size_t>(64, rows.size() - r0));
+      for (size_t r0 = 0; r0 < rows.size(); r0 += rw) fn(rows.data() + r0, (int)std::min<size_t>(rw, rows.size() - r0));
     }
   };
   auto width_of = [&](const int* rows, int cnt) {
@@ -1051,7 +1057,7 @@ void build_gs_schedule(const CSR& A, const std::vector<int>& block_start, bool f
           if (with_tcol) S.tcol[p] = pos[c];
           const int d = (int)sx - st_of[c];
           if (c == i || d < 1) S.code[p] = n + pos[c];  // C
-          else if (d <= reach) S.code[p] = -2 - (((st_of[c] - s0) % kGsRing) * 64 + ln_of[c]);
+          else if (d <= reach) S.code[p] = -2 - (((st_of[c] - s0) % kGsRing) * rw + ln_of[c]);
           else S.code[p] = 2 * n + pos[c];  // U
         }
       }
@@ -1138,13 +1144,15 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
   const int k0 = use_l1 && !weighted ? 0 : 1;
   for (int t = 0; t < S.nteams; ++t) {
     const int s0 = S.team_step[t];
-    std::vector<double> ring((size_t)kGsRingSlots, std::nan(""));
+    const int rw = S.ring_w;
+    if (rw != 16 && rw != 64) { msg = "ring width"; return 1; }
+    std::vector<double> ring((size_t)kGsRing * rw, std::nan(""));
     std::vector<std::pair<int, double>> batch, issued;  // this batch's values; stores issued, not fenced
     for (int s = s0; s < S.team_step[t + 1]; ++s) {
       const int* m = &S.step[(size_t)s * 4];
       const size_t base = (uint32_t)m[0];
       const int cnt = m[2], width = m[3], j = s - s0;
-      if (cnt < 1 || cnt > 64) { msg = "step rows out of range"; return 1; }
+      if (cnt < 1 || cnt > rw) { msg = "step rows out of range"; return 1; }
       if (base & 1) { msg = "step entries not on an even offset (paired loads)"; return 1; }
       std::vector<double> out(cnt);
       for (int q = 0; q < cnt; ++q) {
@@ -1168,7 +1176,7 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
           else if (code >= 0) c = S.rowmap[code], in = false;
           else if (code == -1) { msg = "padding inside a row"; return 1; }
           else {
-            const int slot = -2 - code, rs = slot / 64, rl = slot % 64;
+            const int slot = -2 - code, rs = slot / rw, rl = slot % rw;
             int js = -1;
             for (int d = 1; d <= kGsFence; ++d)
               if (j - d >= 0 && (j - d) % kGsRing == rs) js = j - d;
@@ -1215,7 +1223,7 @@ int gs_schedule_self_check(const CSR& A, int num_blocks, bool forward, bool use_
       for (int q = 0; q < cnt; ++q) {
         batch.push_back({m[1] + q, out[q]});
         u[S.rowmap[m[1] + q]] = out[q];
-        ring[(size_t)(j % kGsRing) * 64 + q] = out[q];
+        ring[(size_t)(j % kGsRing) * rw + q] = out[q];
       }
       if (j % kGsBatch == kGsBatch - 1 || s + 1 == S.team_step[t + 1]) {
         for (auto& pr : issued) {  // the fence completes the previous batch

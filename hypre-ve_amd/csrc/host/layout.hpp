@@ -126,7 +126,9 @@ int64_t sell_padded_nnz(const CSR& A, int sigma);
 //    consecutive blocks are swept together by one wavefront (a team): level l
 //    of the team is level l of each of its blocks.  A team takes blocks while
 //    its rows stay within team_rows x its level count.
-//  * Steps.  A team level is cut into steps of at most 64 rows.  Position k
+//  * Steps.  A team level is cut into steps of at most ring_w rows (64; a
+//    knob takes 16 for teams of at most 4 rows a level, whose kernel LDS ring
+//    is then a quarter as wide).  Position k
 //    of the sweep order (rowmap[k] = row) is step s's row offset + lane, and
 //    the sweep works on vectors permuted into that order, so a step reads and
 //    writes its rows contiguously.  They sit in one buffer G of 3n + nhalo
@@ -142,8 +144,9 @@ int64_t sell_padded_nnz(const CSR& A, int sigma);
 //                  (the kernel fences its U stores every kGsFence steps), or
 //                  the halo for an off-rank column
 //      -1          padding
-//      <= -2       the team's LDS ring, slot -2 - code: a value an in-block
-//                  row computed at most kGsFence steps earlier
+//      <= -2       the team's LDS ring, slot -2 - code = (step % kGsRing) x
+//                  ring_w + lane: a value an in-block row computed at most
+//                  kGsFence steps earlier
 //    Every row's products are summed in CSR order, so a sweep equals the
 //    sequential per-block sweep bit for bit.
 #ifndef HVE_GS_RING
@@ -151,7 +154,6 @@ int64_t sell_padded_nnz(const CSR& A, int sigma);
 #endif
 constexpr int kGsRing = HVE_GS_RING;
 constexpr int kGsFence = kGsRing - 1;
-constexpr int kGsRingSlots = kGsRing * 64;
 // U stores leave the ring in batches of kGsBatch steps (k_hybrid_gs): at the
 // end of a batch the wave fences, which completes the previous batch's stores,
 // then issues this batch's.  A value computed at step q is therefore visible
@@ -173,6 +175,7 @@ struct GsSchedule {
   std::vector<double> l1;        // l1 norms by position (when given)
   std::vector<int> cf;           // CF marker by position (when given)
   int nteams = 0, max_steps = 0, max_width = 0;
+  int ring_w = 64;               // rows a step holds at most = lanes of a ring slot (16 | 64)
   int64_t nnz = 0;               // the operator's entries (the stored ones minus padding)
   double rows_per_step = 0;
 };

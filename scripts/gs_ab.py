@@ -4,8 +4,10 @@ loads, knob 8 = 1 the pipelined sweep on every level (2: on none), knob 10 its
 unit capacity, knob 12 = 256 the unpipelined sweep's 256-entry chunks, knob
 13 = 1 the separate scatter pass after the sweep.  The
 iterates after 4 iterations from x = 0 must be bitwise equal across variants;
-then ms per solve iteration, each variant twice.
-python scripts/gs_ab.py N"""
+then ms per solve iteration, each variant twice.  "rw16": the wide
+operators' schedules built with 16-lane ring slots (knob 14 at setup); "quick":
+the default launch only.  python scripts/gs_ab.py N [rw16] [quick]"""
+import hashlib
 import json
 import sys
 import time
@@ -25,6 +27,8 @@ VARIANTS = {  # name: {knob: value}
     "scatter": {13: 1},
 }
 KNOBS = (6, 8, 10, 12, 13)
+if "quick" in sys.argv[2:]:  # the default launch only (the ring-width A/B)
+    VARIANTS = {"default": {}}
 
 
 def use(v):
@@ -33,13 +37,16 @@ def use(v):
 
 
 hv.init()
+rw16 = "rw16" in sys.argv[2:]
+hv.set_knob(14, 16 if rw16 else 0)
 A = hv.ParCSRMatrix.laplacian(n, n, n)
 kw = hv.ij_amg_defaults(0)
 kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, tol=1e-300, max_iter=4, min_iter=0)
 amg = hv.BoomerAMG(**kw)
 t = time.time()
 amg.setup(A)
-print(f"setup {time.time() - t:.1f}s levels {amg.num_levels()}", flush=True)
+hv.set_knob(14, 0)
+print(f"setup {time.time() - t:.1f}s levels {amg.num_levels()} ring16 {rw16}", flush=True)
 keep = []  # vectors stay alive: a freed buffer's address could bring back a captured graph
 ref = None
 for v in VARIANTS:
@@ -52,7 +59,8 @@ for v in VARIANTS:
     xv = x.get()
     if ref is None:
         ref = xv
-    print(json.dumps({"n": n, "variant": v, "bitwise_equal_default": bool(np.array_equal(xv, ref))}), flush=True)
+    print(json.dumps({"n": n, "variant": v, "rw16": rw16, "bitwise_equal_default": bool(np.array_equal(xv, ref)),
+                      "sha": hashlib.sha256(xv.tobytes()).hexdigest()[:16]}), flush=True)
 for rep in range(2):
     for v in VARIANTS:
         use(v)
@@ -67,5 +75,5 @@ for rep in range(2):
         amg.solve(A, b, x)
         hv.lib().hypreve_DeviceSynchronize()
         ms = (time.perf_counter() - t) / iters * 1e3
-        print(json.dumps({"n": n, "variant": v, "ms_per_iter": round(ms, 3)}), flush=True)
+        print(json.dumps({"n": n, "variant": v, "rw16": rw16, "ms_per_iter": round(ms, 3)}), flush=True)
 use("default")

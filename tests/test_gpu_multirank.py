@@ -331,6 +331,11 @@ LOOPBACK_PINS = ["coarsening.out.4", "coarsening.out.13", "default.out.1", "inte
                  "smoother.out.9", "smoother.out.10", "solvers.out.0", "smoother.out.11", "agg_interp.out.4"]
 
 
+# seq_threshold (the redundant coarse-grid AMG, gen_redcs_mat.c) takes the
+# gathered setup, which runs the rank emulation on rank 0
+GATHERED_PINS = ["solvers.out.105", "solvers.out.106"]
+
+
 @pytest.mark.parametrize("name", LOOPBACK_PINS)
 def test_loopback_reference_np_runs(hv, name):
     """A reference `mpirun -np N ./ij ...` run, N loopback ranks, no emulation:
@@ -341,6 +346,20 @@ def test_loopback_reference_np_runs(hv, name):
     partitioned cycle (halo exchange, agglomerated coarse levels).  The saved
     iteration count and final relative residual, or convergence factor and
     complexities, come out to every printed digit."""
+    _loopback_pin(hv, name, "distributed")
+
+
+@pytest.mark.parametrize("name", GATHERED_PINS)
+def test_loopback_reference_gathered_runs(hv, name):
+    """The same for 8-rank runs with seq_threshold 100 (solvers.out.105 / 106,
+    80^3, aggressive level, hybrid GS 6 under PCG): the ranks gather to rank 0,
+    whose setup is hypre's 8-process one (the rank emulation) with the
+    one-process BoomerAMG below 100 rows appended, and the partitioned cycle
+    reproduces the saved iterations and residual on every rank."""
+    _loopback_pin(hv, name, "gathered, rank emulation")
+
+
+def _loopback_pin(hv, name, path):
     case = next(c for c in CASES if c["name"] == name)
     prob = case["problem"]
     P, Q, R = prob["P"]
@@ -394,7 +413,8 @@ def test_loopback_reference_np_runs(hv, name):
     for e in errs:
         if e is not None:
             raise e
-    assert all(o[3] == "distributed" for o in out), [o[3] for o in out]
+    # the gathered setup records its path on rank 0 (the others receive levels)
+    assert out[0][3] == path and all(o[3] in (path, None) for o in out), [o[3] for o in out]
     it, rr, (g, o, cyc), _ = out[0]
     assert all(ob[0] == it for ob in out)
     exp = case["expect"]

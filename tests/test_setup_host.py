@@ -321,6 +321,23 @@ def test_gs_self_check_models_the_kernel_fences(hv):
     amg.gs_schedule_check(1)
 
 
+@pytest.mark.parametrize("nb", [1, 7])
+def test_gs_schedule_16_lane_ring(hv, nb):
+    """Knob 14 = 16: the small teams (team_rows 3 in the check) are cut into
+    steps of at most 16 rows with 16-lane ring slots (ring codes slot x 16 +
+    lane); every level, both directions, both scalings and the weighted form
+    still equal the sequential sweep bit for bit, and every step starts on an
+    even entry (the paired loads)."""
+    A = hv.ParCSRMatrix.laplacian(14, 12, 11)
+    amg = hv.BoomerAMG(**hv.ij_amg_defaults(0))
+    amg.set(coarsen_type=8, relax_type=13, P_max_elmts=4)
+    amg.setup_host(A)
+    hv.set_knob(14, 16)
+    try:
+        amg.gs_schedule_check(nb)
+    finally:
+        hv.set_knob(14, 0)
+
 
 @pytest.mark.parametrize("size", [2, 3, 5, 8])
 @pytest.mark.parametrize("stencil,relax,interp,agg", [(7, 18, 6, 0), (27, 13, 6, 0), (7, 13, 14, 0), (7, 18, 6, 1),
