@@ -807,9 +807,186 @@ void row_ptr(const DBuf<int>& cnt, int n, DBuf<int>& ptr, std::vector<int>& hptr
 
 int grid_rows(int n, int waves_per_cu) { return std::max(1, std::min(n, 256 * waves_per_cu)); }
 
+// ---------------------------------------------------------------------------
+// Strength of connection (setup.cpp create_strength, par_strength.c:80, one
+// function): one row per thread, the row's scale and sum over its entries in
+// stored order, the same comparisons.  FILL: the kept columns in order.
+// ---------------------------------------------------------------------------
+template <bool FILL>
+__global__ void __launch_bounds__(256) k_strength(DCsr A, double thr, double max_row_sum, int* __restrict__ cnt,
+                                                  const int* __restrict__ Si, int* __restrict__ Sj) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= A.n) return;
+  const int b = A.i[r], e = A.i[r + 1];
+  const double diag = A.a[b];
+  double row_scale = 0.0, row_sum = diag;
+  // std::max / std::min as on the host (the first argument on ties)
+  if (diag < 0) {
+    for (int k = b + 1; k < e; ++k) { const double v = A.a[k]; row_scale = row_scale < v ? v : row_scale; row_sum += v; }
+  } else {
+    for (int k = b + 1; k < e; ++k) { const double v = A.a[k]; row_scale = v < row_scale ? v : row_scale; row_sum += v; }
+  }
+  const bool weak = (fabs(row_sum) > fabs(diag) * max_row_sum) && (max_row_sum < 1.0);
+  int c = 0, o = FILL ? Si[r] : 0;
+  if (!weak) {
+    for (int k = b + 1; k < e; ++k) {
+      const double v = A.a[k];
+      const bool keep = diag < 0 ? !(v <= thr * row_scale) : !(v >= thr * row_scale);
+      if (keep) {
+        if (FILL) Sj[o++] = A.j[k];
+        ++c;
+      }
+    }
+  }
+  if (!FILL) cnt[r] = c;
+}
+
+// ---------------------------------------------------------------------------
+// PMIS (setup.cpp coarsen_pmis, par_coarsen.c:2031, one process, CF_init 0 /
+// 2: the one-process streams agree).  measure = column count of S + the
+// row's hypre_Rand draw (seed 2747, draw r + 1: A^(r+1) seed mod M), then the
+// host loop's passes as kernels over the rows still undecided (act), each
+// pass order-free as on the host (the independent-set pass only writes 0).
+// ---------------------------------------------------------------------------
+constexpr uint64_t kDRandA = 16807, kDRandM = 2147483647;  // setup.cpp hypre_Rand (utilities/random.c)
+__device__ uint64_t d_powmod(uint64_t b, uint64_t e, uint64_t m) {
+  uint64_t r = 1;
+  b %= m;
+  while (e) {
+    if (e & 1) r = (r * b) % m;
+    b = (b * b) % m;
+    e >>= 1;
+  }
+  return r;
+}
+__global__ void __launch_bounds__(256) k_pmis_init(int n, const int* __restrict__ Si, const int* __restrict__ mcount,
+                                                   double* __restrict__ measure, int* __restrict__ cf,
+                                                   unsigned char* __restrict__ act) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= n) return;
+  const uint64_t s = (d_powmod(kDRandA, (uint64_t)r + 1, kDRandM) * 2747ull) % kDRandM;
+  double m = (double)mcount[r];
+  m += (double)s / (double)kDRandM;
+  if (Si[r + 1] - Si[r] == 0) {
+    cf[r] = -3;  // SF_PT (par_coarsen.c:2320-2326)
+    m = 0;
+    act[r] = 0;
+  } else {
+    cf[r] = 0;
+    act[r] = 1;
+  }
+  measure[r] = m;
+}
+// pass 1: the initial independent set (measure > 1)
+__global__ void __launch_bounds__(256) k_pmis_mark(int n, const unsigned char* __restrict__ act,
+                                                   const double* __restrict__ measure, int* __restrict__ cf) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r < n && act[r] && measure[r] > 1) cf[r] = 1;
+}
+// pass 2: drop the smaller of two strongly connected candidates (writes 0 only)
+__global__ void __launch_bounds__(256) k_pmis_drop(int n, const unsigned char* __restrict__ act, const int* __restrict__ Si,
+                                                   const int* __restrict__ Sj, const double* __restrict__ measure,
+                                                   int* __restrict__ cf) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n || !act[i]) return;
+  const double mi = measure[i];
+  if (!(mi > 1)) return;
+  for (int k = Si[i]; k < Si[i + 1]; ++k) {
+    const int j = Sj[k];
+    const double mj = measure[j];
+    if (mj > 1) {
+      if (mi > mj) __hip_atomic_store(&cf[j], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else if (mj > mi) __hip_atomic_store(&cf[i], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+// pass 3: C and F points (a marker > 0 stays, so the reads are order-free)
+__global__ void __launch_bounds__(256) k_pmis_set(int n, const unsigned char* __restrict__ act, const int* __restrict__ Si,
+                                                  const int* __restrict__ Sj, const double* __restrict__ measure,
+                                                  int* __restrict__ cf) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n || !act[i]) return;
+  int v = cf[i];
+  if (measure[i] < 1) v = -1;  // F_PT
+  if (v > 0) {
+    v = 1;  // C_PT
+  } else {
+    for (int k = Si[i]; k < Si[i + 1]; ++k)
+      if (__hip_atomic_load(&cf[Sj[k]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > 0) { v = -1; break; }
+  }
+  if (v != cf[i]) __hip_atomic_store(&cf[i], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// pass 4: decided rows leave the graph (measure 0); the rest are counted
+__global__ void __launch_bounds__(256) k_pmis_next(int n, unsigned char* __restrict__ act, double* __restrict__ measure,
+                                                   const int* __restrict__ cf, int* __restrict__ left) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  int still = 0;
+  if (i < n && act[i]) {
+    if (cf[i] != 0) {
+      measure[i] = 0;
+      act[i] = 0;
+    } else {
+      still = 1;
+    }
+  }
+  const unsigned long long b = __ballot(still);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(left, __popcll(b));
+}
+
 }  // namespace
 
 long long dev_setup_host_rows() { return g_host_rows; }
+
+void dev_strength_pmis(const CSR& A, double thr, double max_row_sum, Pattern& S, std::vector<int>& cf,
+                       double* t_strength) {
+  const int n = A.nrows;
+  const auto t0 = STimer::now();
+  STimer T;
+  S.n = n;
+  S.i.assign((size_t)n + 1, 0);
+  S.j.clear();
+  cf.assign(n, 0);
+  if (n == 0) return;
+  const dim3 g((n + 255) / 256), b(256);
+  DBuf<int> Si, Sj;
+  {
+    DevCSR dA;
+    dA.up(A);
+    DBuf<int> cnt(n);
+    hipLaunchKernelGGL((k_strength<false>), g, b, 0, 0, dA.view(), thr, max_row_sum, cnt.p, nullptr, nullptr);
+    SDV(hipGetLastError());
+    row_ptr(cnt, n, Si, S.i);
+    Sj.alloc((size_t)S.i[n]);
+    hipLaunchKernelGGL((k_strength<true>), g, b, 0, 0, dA.view(), thr, max_row_sum, nullptr, Si.p, Sj.p);
+    SDV(hipGetLastError());
+    Sj.down(S.j, (size_t)S.i[n]);
+  }
+  T.lap("strength (upload, kernels, S down)");
+  if (t_strength) *t_strength = STimer::now() - t0;
+  const int64_t nnzs = S.i[n];
+  DBuf<int> mc(n), dcf(n), left(1);
+  DBuf<double> meas(n);
+  DBuf<unsigned char> act(n);
+  SDV(hipMemset(mc.p, 0, sizeof(int) * (size_t)n));
+  if (nnzs > 0)
+    hipLaunchKernelGGL(k_col_count, dim3((unsigned)((nnzs + 255) / 256)), b, 0, 0, nnzs, Sj.p, mc.p);
+  hipLaunchKernelGGL(k_pmis_init, g, b, 0, 0, n, Si.p, mc.p, meas.p, dcf.p, act.p);
+  SDV(hipGetLastError());
+  for (int iter = 0; iter < 1000; ++iter) {
+    hipLaunchKernelGGL(k_pmis_mark, g, b, 0, 0, n, act.p, meas.p, dcf.p);
+    hipLaunchKernelGGL(k_pmis_drop, g, b, 0, 0, n, act.p, Si.p, Sj.p, meas.p, dcf.p);
+    hipLaunchKernelGGL(k_pmis_set, g, b, 0, 0, n, act.p, Si.p, Sj.p, meas.p, dcf.p);
+    SDV(hipMemset(left.p, 0, sizeof(int)));
+    hipLaunchKernelGGL(k_pmis_next, g, b, 0, 0, n, act.p, meas.p, dcf.p, left.p);
+    SDV(hipGetLastError());
+    int h = 0;
+    SDV(hipMemcpy(&h, left.p, sizeof(int), hipMemcpyDeviceToHost));
+    if (h == 0) break;
+    if (iter == 999) throw std::runtime_error("device PMIS: no convergence after 1000 passes");
+  }
+  dcf.down(cf, n);
+  T.lap("PMIS kernels");
+}
 
 void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf,
                       const std::vector<int>& fine_to_coarse, int ncoarse, double trunc_factor, int max_elmts,

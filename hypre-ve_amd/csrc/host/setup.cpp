@@ -22,6 +22,8 @@
 #endif
 
 namespace hve {
+int knob(int id);  // kernels.hip (tests' knobs)
+
 
 // ---------------------------------------------------------------------------
 // Problem generators
@@ -2646,11 +2648,20 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
     Pattern S;
     double t0 = now();
     hve_setup_dof = dof.empty() ? nullptr : dof.data();
-    create_strength(L.A, prm.strong_threshold, prm.max_row_sum, S);
-    double t1 = now();
-    t_s += t1 - t0;
+    // one process, PMIS (the one-process streams of coarsen_type 8 and 9
+    // agree): strength and coarsening on the device, the same S and markers
+    // (levels of 2^16 rows and more; knob 15 sets the bound: tests take 1)
+    const bool dev_sc = prm.device_setup && dof.empty() && !rs && (coarsen_type == 8 || coarsen_type == 9) &&
+                        fine_size >= (knob(15) > 0 ? knob(15) : (1 << 16));
     std::vector<int> cf;
-    if (coarsen_type == 8) coarsen_pmis(S, 0, cf, rs);
+    double ts_dev = 0.0;
+    if (dev_sc) dev_strength_pmis(L.A, prm.strong_threshold, prm.max_row_sum, S, cf, &ts_dev);
+    else create_strength(L.A, prm.strong_threshold, prm.max_row_sum, S);
+    double t1 = dev_sc ? t0 + ts_dev : now();
+    t_s += t1 - t0;
+    if (dev_sc) {
+      // done above
+    } else if (coarsen_type == 8) coarsen_pmis(S, 0, cf, rs);
     else if (coarsen_type == 9) coarsen_pmis(S, 2, cf, rs);
     else if (coarsen_type == 10)
       coarsen_hmis(S, &L.A, prm.measure_type, prm.coarsen_cut_factor, cf, rs ? rs : (crs.empty() ? nullptr : &crs));

@@ -19,6 +19,11 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
 // Galerkin product C = P^T A P (rap_core with R = P^T, coarse_glob empty) and
 // R = P^T (transpose) itself.
 void dev_rap(const CSR& P, const CSR& A, CSR& R, CSR& C);
+// Strength (create_strength, one function) and PMIS (coarsen_pmis, CF_init 0
+// or 2, one process): S and the CF marker as the host functions give them;
+// *t_strength: the seconds of the strength part.
+void dev_strength_pmis(const CSR& A, double thr, double max_row_sum, Pattern& S, std::vector<int>& cf,
+                       double* t_strength);
 // Rows of the last dev_* call finished on the host (tables too large for LDS).
 long long dev_setup_host_rows();
 

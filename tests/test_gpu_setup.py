@@ -74,6 +74,45 @@ def test_device_setup_matches_host(gpu, gen, dims, extra):
     A.destroy()
 
 
+@pytest.mark.parametrize("gen,dims,extra", [
+    ("7", (30, 27, 25), {}),
+    ("7", (24, 22, 20), {"coarsen_type": 9}),
+    ("27", (20, 18, 16), {"max_row_sum": 0.9}),
+    ("aniso", (28, 26, 24), {"strong_threshold": 0.5}),
+    ("aniso", (30, 28, 26), {"agg_num_levels": 1}),
+    ("7", (48, 44, 40), {}),
+])
+def test_device_strength_pmis_matches_host(gpu, gen, dims, extra):
+    """Strength and PMIS on the device (dev_strength_pmis: one thread a row
+    for S, the PMIS passes as kernels over the undecided rows) on every level
+    (knob 15 = 1; by default levels of 2^16 rows and more, which the last case
+    reaches without it): the hierarchy equals the host setup's byte for byte,
+    CF markers included."""
+    hv = gpu
+    if gen == "27":
+        A = hv.ParCSRMatrix.laplacian27(*dims)
+    elif gen == "aniso":
+        A = hv.ParCSRMatrix.laplacian(*dims, cx=0.001, cy=1.0, cz=1.0)
+    else:
+        A = hv.ParCSRMatrix.laplacian(*dims)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
+    kw.update(extra)
+    host = hv.BoomerAMG(**kw)
+    host.setup_host(A)
+    big = dims[0] * dims[1] * dims[2] >= 1 << 16
+    hv.set_knob(15, 0 if big else 1)
+    try:
+        dev = hv.BoomerAMG(**kw)
+        dev.setup(A)
+    finally:
+        hv.set_knob(15, 0)
+    _same(_hier(hv, dev), _hier(hv, host))
+    for s in (dev, host):
+        s.destroy()
+    A.destroy()
+
+
 @pytest.mark.parametrize("lgcap", [5, 6])
 def test_device_setup_host_rows(gpu, lgcap):
     """Tables capped at 32 / 64 slots (knob 7): the interpolation and Galerkin
