@@ -439,11 +439,20 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver solver, HYPRE_Int level, HYPRE_Int w
 HYPRE_Int hypreve_BenchOperator(HYPRE_ParCSRMatrix A, HYPRE_Int op, HYPRE_Int policy, HYPRE_Int nbands,
                                 HYPRE_Int reps, HYPRE_Real *avg_ms, HYPRE_Real *stored_bytes, char *layout,
                                 HYPRE_Int len);
-/* Tuning knobs read at kernel launch (0 = built-in default): 0 row blocks per
- * step of the offset-coded loop (1, 2, 4), 1 its codes per batch (4, 8, 16),
- * 2 its persistent workgroups per CU, 3 the stream-mix access width (2: 16 B),
- * 7 the device setup's LDS table cap (2^v slots; rows beyond it are finished
- * on the host).  Results are unchanged. */
+/* Tuning knobs read at kernel launch or setup (0 = built-in default): 0 row
+ * blocks per step of the offset-coded loop (1, 2, 4), 1 its codes per batch
+ * (4, 8, 16), 2 its persistent workgroups per CU (also the jagged coded
+ * loop's), 3 the stream-mix access width (2: 16 B), 4 the jagged coded loop's
+ * entries per row and chunk (4, 8, 16), 5 = 1 its code prefetch off, 6 = 1
+ * the hybrid-GS sweep's unpaired entry loads, 7 the device setup's LDS table
+ * cap (2^v slots; rows beyond it are finished on the host), 8 the pipelined
+ * GS sweep on every schedule (1) or none (2), 9 the grid-stencil z-chunk,
+ * 10 the pipelined GS sweep's unit capacity (128, 256, 512), 11 (tests) the
+ * GS ring reach shortened, 12 = 256 the unpipelined GS sweep's chunk, 13 = 1
+ * the GS scatter pass after the sweep, 14 = 16 (setup) 16-lane GS ring slots
+ * for the wide operators, 15 (setup) the smallest level the device strength
+ * and PMIS take.  Results are unchanged, except knob 11's, which
+ * gs_schedule_self_check must refuse. */
 HYPRE_Int hypreve_SetKnob(HYPRE_Int id, HYPRE_Int value);
 /* Bytes the same launch streams in the operator's stored (compressed) layout,
  * vectors included. */
