@@ -1677,7 +1677,7 @@ HYPRE_Int hypreve_BenchLevelOp(HYPRE_Solver s, HYPRE_Int level, HYPRE_Int which,
 // Tuning knobs read by the launch code (kernels.h set_knob): variants compared
 // in one process on one hierarchy.
 HYPRE_Int hypreve_SetKnob(HYPRE_Int id, HYPRE_Int value) {
-  CHECK_ARG(id >= 0 && id < 16, 1);
+  CHECK_ARG(id >= 0 && id < 32, 1);
   set_knob(id, value);
   return 0;
 }

@@ -2433,7 +2433,13 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   a.ustore = knob(13) == 1 ? 0 : 1;  // knob 13 = 1: the separate scatter pass (the A/B)
   a.rw = S.ring_w;
   if (a.rw != 16 && a.rw != 64) return hipErrorInvalidValue;
-  const size_t rlds = (size_t)kGsWaves * kGsRing * a.rw * sizeof(double);
+  // 8 KiB of LDS a workgroup beyond what the sweep uses: two workgroups a CU
+  // instead of three (the teams' T / C / U lines stay in L2 longer): the
+  // cycle 6.91 -> 6.68 ms at 256^3, 43.7 -> 42.2 ms at 512^3; 32 KiB (one
+  // workgroup a CU for the level-0 sweep) 46.5 ms at 512^3
+  // (profiles/r06/22_gsocc).  Knob 16: other KiB (-1: none).
+  const int pad_kib = knob(16) > 0 ? knob(16) : knob(16) < 0 ? 0 : 8;
+  const size_t rlds = (size_t)kGsWaves * kGsRing * a.rw * sizeof(double) + (size_t)pad_kib * 1024;
   const uint64_t gbytes = (3 * (uint64_t)S.nrows + (uint64_t)nhalo) * sizeof(double);
   if (gbytes > 0xffffffffull) return hipErrorInvalidValue;  // 32-bit buffer offsets (about 178M rows a GPU)
   a.gbytes = (unsigned)gbytes;
@@ -2716,7 +2722,8 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     const dim3 dgrid(a.nblocks_pad), dblock(64 * G);
     if (M.wptr) {  // lane-packed streams (k_sell_dictw), G = 1 or 4
       if (G != 1 && G != 4) return hipErrorInvalidValue;
-      const size_t lds = (size_t)M.dmax * sizeof(double);
+      // knob 17: extra LDS a workgroup in KiB (fewer workgroups a CU: the A/B)
+      const size_t lds = (size_t)M.dmax * sizeof(double) + (size_t)std::max(0, knob(17)) * 1024;
 #define HVE_DW(OPV, CF)                                                                              \
   if (G == 4) {                                                                                      \
     if (nt) hipLaunchKernelGGL((k_sell_dictw<OPV, CF, true, 4>), dgrid, dblock, lds, s, a);          \
@@ -3038,11 +3045,11 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
 
 // Tuning knobs (hypreve_SetKnob): read at launch time, so variants can be
 // compared in one process on one hierarchy.  0 = the built-in default.
-static int g_knob[16];
+static int g_knob[32];
 void set_knob(int id, int v) {
-  if (id >= 0 && id < 16) g_knob[id] = v;
+  if (id >= 0 && id < 32) g_knob[id] = v;
 }
-int knob(int id) { return (id >= 0 && id < 16) ? g_knob[id] : 0; }
+int knob(int id) { return (id >= 0 && id < 32) ? g_knob[id] : 0; }
 
 // Entries per load batch in the SELL row loop: chosen per operator at upload
 // (SellView::batch); HVE_SELL_BATCH=8|16 overrides it and HVE_SELL_PIPE=1

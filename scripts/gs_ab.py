@@ -6,7 +6,8 @@ unit capacity, knob 12 = 256 the unpipelined sweep's 256-entry chunks, knob
 iterates after 4 iterations from x = 0 must be bitwise equal across variants;
 then ms per solve iteration, each variant twice.  "rw16": the wide
 operators' schedules built with 16-lane ring slots (knob 14 at setup); "quick":
-the default launch only.  python scripts/gs_ab.py N [rw16] [quick]"""
+the default launch only; "occ": extra LDS a workgroup (knob 16, fewer
+workgroups a CU).  python scripts/gs_ab.py N [rw16] [quick | occ]"""
 import hashlib
 import json
 import sys
@@ -26,9 +27,11 @@ VARIANTS = {  # name: {knob: value}
     "pipe_auto": {8: 1},
     "scatter": {13: 1},
 }
-KNOBS = (6, 8, 10, 12, 13)
+KNOBS = (6, 8, 10, 12, 13, 16)
 if "quick" in sys.argv[2:]:  # the default launch only (the ring-width A/B)
     VARIANTS = {"default": {}}
+if "occ" in sys.argv[2:]:  # fewer workgroups a CU through extra LDS (knob 16, KiB)
+    VARIANTS = {"default": {}, "nopad": {16: -1}, "lds+16": {16: 16}}
 
 
 def use(v):
