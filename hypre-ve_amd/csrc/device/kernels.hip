@@ -2438,6 +2438,8 @@ hipError_t launch_hybrid_gs(const GsView& S, bool use_l1, bool cfsel, int relax_
   // cycle 6.91 -> 6.68 ms at 256^3, 43.7 -> 42.2 ms at 512^3; 32 KiB (one
   // workgroup a CU for the level-0 sweep) 46.5 ms at 512^3
   // (profiles/r06/22_gsocc).  Knob 16: other KiB (-1: none).
+  // (the level-0 sweep alone without the pad, or with 16 KiB: the same times,
+  // profiles/r06/24_occ3: the gain is the Galerkin levels')
   const int pad_kib = knob(16) > 0 ? knob(16) : knob(16) < 0 ? 0 : 8;
   const size_t rlds = (size_t)kGsWaves * kGsRing * a.rw * sizeof(double) + (size_t)pad_kib * 1024;
   const uint64_t gbytes = (3 * (uint64_t)S.nrows + (uint64_t)nhalo) * sizeof(double);
