@@ -96,6 +96,70 @@ struct DevCSR {
 
 long long g_host_rows = 0;
 
+// Device copies of one setup level's matrices (A, S, P), so that strength /
+// PMIS, ext+i and RAP upload each once: keyed by the host arrays' addresses
+// and sizes, and emptied by amg_setup at the start of every level (within a
+// level the host A, S and P are not modified between the device calls).
+struct SetupCache {
+  const void *aj = nullptr, *aa = nullptr;
+  int64_t annz = -1;
+  int an = -1;
+  DevCSR A;
+  const void* sj = nullptr;
+  int64_t snnz = -1;
+  int sn = -1;
+  DBuf<int> Si, Sj;
+  const void *pj = nullptr, *pa = nullptr;
+  int64_t pnnz = -1;
+  int pn = -1;
+  DevCSR P;
+  void clear() {
+    A.i.free(); A.j.free(); A.a.free();
+    Si.free(); Sj.free();
+    P.i.free(); P.j.free(); P.a.free();
+    aj = aa = sj = pj = pa = nullptr;
+    annz = snnz = pnnz = -1;
+    an = sn = pn = -1;
+  }
+  const DevCSR& matA(const CSR& h) {
+    if (!(aj == (const void*)h.j.data() && aa == (const void*)h.a.data() && annz == (int64_t)h.nnz() && an == h.nrows)) {
+      A.up(h);
+      aj = h.j.data(); aa = h.a.data(); annz = h.nnz(); an = h.nrows;
+    }
+    return A;
+  }
+  DCsr patS(const Pattern& h) {
+    if (!(sj == (const void*)h.j.data() && snnz == (int64_t)h.j.size() && sn == h.n)) {
+      Si.up(h.i);
+      Sj.up(h.j);
+      sj = h.j.data(); snnz = (int64_t)h.j.size(); sn = h.n;
+    }
+    return DCsr{Si.p, Sj.p, nullptr, h.n};
+  }
+  void keepS(const Pattern& h) { sj = h.j.data(); snnz = (int64_t)h.j.size(); sn = h.n; }
+  const DevCSR& matP(const CSR& h) {
+    if (!(pj == (const void*)h.j.data() && pa == (const void*)h.a.data() && pnnz == (int64_t)h.nnz() && pn == h.nrows)) {
+      P.up(h);
+      pj = h.j.data(); pa = h.a.data(); pnnz = h.nnz(); pn = h.nrows;
+    }
+    return P;
+  }
+  void keepP(const CSR& h) { pj = h.j.data(); pa = h.a.data(); pnnz = h.nnz(); pn = h.nrows; P.n = h.nrows; P.ncols = h.ncols; }
+};
+// never destroyed: its buffers must not be freed after the HIP runtime is gone
+SetupCache& cache() {
+  static SetupCache* c = new SetupCache();
+  return *c;
+}
+template <typename T>
+void take(DBuf<T>& dst, DBuf<T>& src) {
+  dst.free();
+  dst.p = src.p;
+  dst.n = src.n;
+  src.p = nullptr;
+  src.n = 0;
+}
+
 // HVE_SETUP_T: stage times of the device setup on stderr
 struct STimer {
   bool on = getenv("HVE_SETUP_T") != nullptr;
@@ -937,6 +1001,8 @@ __global__ void __launch_bounds__(256) k_pmis_next(int n, unsigned char* __restr
 
 long long dev_setup_host_rows() { return g_host_rows; }
 
+void dev_setup_cache_clear() { cache().clear(); }
+
 void dev_strength_pmis(const CSR& A, double thr, double max_row_sum, Pattern& S, std::vector<int>& cf,
                        double* t_strength) {
   const int n = A.nrows;
@@ -948,10 +1014,11 @@ void dev_strength_pmis(const CSR& A, double thr, double max_row_sum, Pattern& S,
   cf.assign(n, 0);
   if (n == 0) return;
   const dim3 g((n + 255) / 256), b(256);
-  DBuf<int> Si, Sj;
+  SetupCache& C = cache();
+  DBuf<int>& Si = C.Si;
+  DBuf<int>& Sj = C.Sj;
   {
-    DevCSR dA;
-    dA.up(A);
+    const DevCSR& dA = C.matA(A);  // kept for ext+i and RAP
     DBuf<int> cnt(n);
     hipLaunchKernelGGL((k_strength<false>), g, b, 0, 0, dA.view(), thr, max_row_sum, cnt.p, nullptr, nullptr);
     SDV(hipGetLastError());
@@ -960,6 +1027,7 @@ void dev_strength_pmis(const CSR& A, double thr, double max_row_sum, Pattern& S,
     hipLaunchKernelGGL((k_strength<true>), g, b, 0, 0, dA.view(), thr, max_row_sum, nullptr, Si.p, Sj.p);
     SDV(hipGetLastError());
     Sj.down(S.j, (size_t)S.i[n]);
+    C.keepS(S);  // S stays on the device for ext+i
   }
   T.lap("strength (upload, kernels, S down)");
   if (t_strength) *t_strength = STimer::now() - t0;
@@ -996,14 +1064,12 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   P.resize_rows(n, ncoarse);
   if (n == 0) return;
   STimer T;
-  DevCSR dA;
-  dA.up(A);
-  DBuf<int> Si, Sj, dcf, df2c;
-  Si.up(S.i);
-  Sj.up(S.j);
+  SetupCache& C = cache();
+  const DevCSR& dA = C.matA(A);  // uploaded by the strength pass of this level, or now
+  const DCsr dS = C.patS(S);
+  DBuf<int> dcf, df2c;
   dcf.up(cf);
   df2c.up(fine_to_coarse);
-  const DCsr dS{Si.p, Sj.p, nullptr, S.n};
   T.lap("extpi upload");
   // table capacity from the largest candidate count of a row (capped; rows
   // beyond it overflow to the host)
@@ -1053,11 +1119,6 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
                        dS, dcf.p, df2c.p, n, cap, lg, cnt.p, Pi.p, Pj.p, Pa.p);
   SDV(hipGetLastError());
   T.lap("extpi fill kernel");
-  dA.i.free();
-  dA.j.free();
-  dA.a.free();
-  Si.free();
-  Sj.free();
   const bool trunc = trunc_factor != 0.0 || max_elmts > 0;
   if (!trunc) {
     P.i = hp;
@@ -1123,6 +1184,11 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   Na.down(P.a, (size_t)ni[n]);
   T.lap("P download");
   g_host_rows = (long long)(ovf.size() + longrows.size());
+  // the complete P (host-finished rows included) stays on the device for RAP
+  take(C.P.i, Ni);
+  take(C.P.j, Nj);
+  take(C.P.a, Na);
+  C.keepP(P);
 }
 
 void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
@@ -1130,9 +1196,9 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   const int nf = P.nrows, nc = P.ncols;
   const int64_t nnzp = P.nnz();
   STimer T;
-  DevCSR dP, dA;
-  dP.up(P);
-  dA.up(A);
+  SetupCache& Cc = cache();
+  const DevCSR& dP = Cc.matP(P);  // ext+i's device P, or uploaded now
+  const DevCSR& dA = Cc.matA(A);
   T.lap("rap upload");
   // R = P^T: a stable radix sort of the entries by column keeps every
   // column's rows ascending (transpose's counting sort)

@@ -2642,9 +2642,15 @@ int amg_setup(const CSR& A0, const AMGParams& prm_in, Hierarchy& H, const std::v
   bool finished = prm.max_levels <= 1;
   auto now = [] { return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
   double t_s = 0, t_c = 0, t_i = 0, t_r = 0, t_t = 0;
+  // the device calls of a level share its device A, S and P (setup_dev.hip)
+  struct CacheScope {
+    bool on;
+    ~CacheScope() { if (on) dev_setup_cache_clear(); }
+  } cache_scope{prm.device_setup};
   while (!finished) {
     Level& L = H.lev[level];
     const int fine_size = L.A.nrows;
+    if (prm.device_setup) dev_setup_cache_clear();
     Pattern S;
     double t0 = now();
     hve_setup_dof = dof.empty() ? nullptr : dof.data();

@@ -24,6 +24,9 @@ void dev_rap(const CSR& P, const CSR& A, CSR& R, CSR& C);
 // *t_strength: the seconds of the strength part.
 void dev_strength_pmis(const CSR& A, double thr, double max_row_sum, Pattern& S, std::vector<int>& cf,
                        double* t_strength);
+// Frees the device copies of the current level's A, S and P that the dev_*
+// calls share (amg_setup calls it at the start of every level and at the end).
+void dev_setup_cache_clear();
 // Rows of the last dev_* call finished on the host (tables too large for LDS).
 long long dev_setup_host_rows();
 
