@@ -405,10 +405,11 @@ HYPRE_Int hypreve_BoomerAMGStencilLayoutCheck(HYPRE_Solver solver, HYPRE_Int lev
  * can address an nx x ny x nz grid on one rank, else 0: a larger rank share
  * keeps the per-slice stencil loop (no GPU needed). */
 HYPRE_Int hypreve_GridStencilAddressable(HYPRE_BigInt nx, HYPRE_BigInt ny, HYPRE_BigInt nz);
-/* Setup's heavy row loops on the GPU (default 1): ext+i interpolation and its
- * truncation, R = P^T and the Galerkin product RAP, byte for byte the host
- * functions' result (device/setup_dev.hip); 0 runs them on the host.  The
- * distributed setup keeps the host. */
+/* Setup's heavy row loops on the GPU (default 1): strength and PMIS
+ * coarsening (one process, coarsen_type 8 / 9, levels of 2^16 rows and more),
+ * ext+i interpolation and its truncation, R = P^T and the Galerkin product
+ * RAP, byte for byte the host functions' result (device/setup_dev.hip); 0 runs
+ * them on the host.  The distributed setup keeps the host. */
 HYPRE_Int hypreve_BoomerAMGSetDeviceSetup(HYPRE_Solver solver, HYPRE_Int on);
 /* The setup's log (levels, phase times, rows the device setup left to the
  * host) into buf[0..len). */
