@@ -1019,17 +1019,20 @@ void dev_strength_pmis(const CSR& A, double thr, double max_row_sum, Pattern& S,
   DBuf<int>& Sj = C.Sj;
   {
     const DevCSR& dA = C.matA(A);  // kept for ext+i and RAP
+    T.lap("strength: A upload");
     DBuf<int> cnt(n);
     hipLaunchKernelGGL((k_strength<false>), g, b, 0, 0, dA.view(), thr, max_row_sum, cnt.p, nullptr, nullptr);
     SDV(hipGetLastError());
     row_ptr(cnt, n, Si, S.i);
+    T.lap("strength: count, row starts");
     Sj.alloc((size_t)S.i[n]);
     hipLaunchKernelGGL((k_strength<true>), g, b, 0, 0, dA.view(), thr, max_row_sum, nullptr, Si.p, Sj.p);
     SDV(hipGetLastError());
+    T.lap("strength: fill");
     Sj.down(S.j, (size_t)S.i[n]);
     C.keepS(S);  // S stays on the device for ext+i
   }
-  T.lap("strength (upload, kernels, S down)");
+  T.lap("strength: S download");
   if (t_strength) *t_strength = STimer::now() - t0;
   const int64_t nnzs = S.i[n];
   DBuf<int> mc(n), dcf(n), left(1);

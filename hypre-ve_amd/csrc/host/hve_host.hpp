@@ -112,7 +112,8 @@ struct CSR {
 // Strength pattern (hypre S): column indices only, no diagonal.
 struct Pattern {
   int n = 0;
-  std::vector<int> i, j;
+  std::vector<int> i;
+  hvec<int> j;  // no zero fill: the device strength downloads into it
 };
 
 // Per-row marker map: the reference's P_marker / A_marker arrays (one int per
