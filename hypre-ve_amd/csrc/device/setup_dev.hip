@@ -398,8 +398,10 @@ __device__ __forceinline__ int wave_sum(int v) {
 
 // ext+i count (k_extpi<false>): |C-hat_i|, strong F neighbours taking table
 // slots as in the fill pass.  LDS: cap 64-bit words.
+// rowkeys (optional): the row's table keys (C-hat plus strong F neighbours; 0
+// for C and SF rows), which size the fill pass's table (dev_extpi_interp)
 __global__ void __launch_bounds__(64) k_extpi_count_w(DCsr S, const int* __restrict__ cf, int n, int cap, int lg,
-                                                      int* __restrict__ rowcnt) {
+                                                      int* __restrict__ rowcnt, int* __restrict__ rowkeys) {
   extern __shared__ unsigned long long lds64[];
   for (int t = threadIdx.x; t < cap; t += 64) lds64[t] = 0ull;
   __syncthreads();
@@ -411,7 +413,10 @@ __global__ void __launch_bounds__(64) k_extpi_count_w(DCsr S, const int* __restr
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const int ci = cf[i];
     if (ci >= 0 || ci == kSF) {
-      if (lane == 0) rowcnt[i] = ci >= 0 ? 1 : 0;
+      if (lane == 0) {
+        rowcnt[i] = ci >= 0 ? 1 : 0;
+        if (rowkeys) rowkeys[i] = 0;
+      }
       continue;
     }
     ++cur;
@@ -440,14 +445,17 @@ __global__ void __launch_bounds__(64) k_extpi_count_w(DCsr S, const int* __restr
       }
     }
     const int tk = wave_sum(keys), tc = wave_sum(cntc), tb = wave_sum(bad);
-    if (lane == 0) rowcnt[i] = (tb || tk > limit) ? -1 : tc;
+    if (lane == 0) {
+      rowcnt[i] = (tb || tk > limit) ? -1 : tc;
+      if (rowkeys) rowkeys[i] = tk;
+    }
   }
 }
 
 // Galerkin count (k_rap<false>): distinct columns of C row q (q itself
 // first).  LDS: cap1 + cap2 64-bit words and the RA list (cap1 / 2 ints).
 __global__ void __launch_bounds__(64) k_rap_count_w(DCsr R, DCsr A, DCsr P, int cap1, int lg1, int cap2, int lg2,
-                                                    int* __restrict__ rowlen) {
+                                                    int* __restrict__ rowlen, int* __restrict__ rownra) {
   extern __shared__ unsigned long long lds64[];
   for (int t = threadIdx.x; t < cap1 + cap2; t += 64) lds64[t] = 0ull;
   int* ra = reinterpret_cast<int*>(lds64 + cap1 + cap2);
@@ -496,7 +504,10 @@ __global__ void __launch_bounds__(64) k_rap_count_w(DCsr R, DCsr A, DCsr P, int 
     } else {
       bad = 1;
     }
-    if (lane == 0) rowlen[q] = (bad || keys > lim2) ? -1 : keys;
+    if (lane == 0) {
+      rowlen[q] = (bad || keys > lim2) ? -1 : keys;
+      if (rownra) rownra[q] = nra;
+    }
     __syncthreads();
   }
 }
@@ -516,10 +527,13 @@ __device__ __forceinline__ void wsync() {
 // slot (a row holds a column once, so no two lanes meet), and the diagonal's
 // single contribution of row i1 is added by every lane's copy of the diagonal
 // in the same place as on the host.  Same operations, same order.
+// keys / (kmin, kmax]: only the rows whose table keys fall in the range (a
+// launch with a small table for the many short rows, another for the rest)
 __global__ void __launch_bounds__(64) k_extpi_fill_w(DCsr A, DCsr S, const int* __restrict__ cf,
                                                      const int* __restrict__ f2c, int n, int cap, int lg,
                                                      const int* __restrict__ rowcnt, const int* __restrict__ Pi,
-                                                     int* __restrict__ Pj, double* __restrict__ Pa) {
+                                                     int* __restrict__ Pj, double* __restrict__ Pa,
+                                                     const int* __restrict__ keys, int kmin, int kmax) {
   extern __shared__ int lds[];
   lds_zero(lds + 2 * cap, cap);  // generation stamps
   const int lane = threadIdx.x;
@@ -531,6 +545,7 @@ __global__ void __launch_bounds__(64) k_extpi_fill_w(DCsr A, DCsr S, const int* 
   constexpr int kNone = -1, kStrongF = -2;
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     if (rowcnt[i] < 0) continue;  // finished on the host
+    if (keys && (keys[i] <= kmin || keys[i] > kmax)) continue;  // the other launch's row
     const int ci = cf[i];
     const int jb = Pi[i];
     if (ci >= 0) {
@@ -769,9 +784,13 @@ __global__ void __launch_bounds__(256) k_transpose_fill(int64_t nnz, const int* 
 // doubles) + map2 (3 x cap2) + the row's values (cap2/2 doubles).
 // ---------------------------------------------------------------------------
 template <bool FILL>
+// mode 1: only the rows with at most lim1 RA keys (rownra) and lim2 C keys
+// (their length), mode 2: only the others, 0: every row (dev_rap's two
+// table sizes)
 __global__ void __launch_bounds__(64) k_rap(DCsr R, DCsr A, DCsr P, int cap1, int lg1, int cap2, int lg2,
                                             int* __restrict__ rowlen, const int* __restrict__ Ci,
-                                            int* __restrict__ Cj, double* __restrict__ Ca) {
+                                            int* __restrict__ Cj, double* __restrict__ Ca,
+                                            const int* __restrict__ rownra, int mode, int lim1, int lim2) {
   extern __shared__ int lds[];
   int* m1 = lds;
   int* m2 = m1 + 3 * cap1;
@@ -786,6 +805,10 @@ __global__ void __launch_bounds__(64) k_rap(DCsr R, DCsr A, DCsr P, int cap1, in
   M2.init(m2, cap2, lg2);
   for (int q = blockIdx.x; q < R.n; q += gridDim.x) {
     if (FILL && rowlen[q] < 0) continue;  // finished on the host
+    if (FILL && mode) {
+      const bool small = rownra[q] <= lim1 && rowlen[q] <= lim2;
+      if (small != (mode == 1)) continue;  // the other launch's row
+    }
     M1.begin();
     int nra = 0;
     bool fresh, ovf = false;
@@ -1083,9 +1106,15 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   const size_t lds = (size_t)3 * cap * sizeof(int) + (size_t)(cap / 2) * sizeof(double);
   DBuf<int> cnt(n);
   const int grid = grid_rows(n, 32);
+  // Rows with few candidates (the finest 7-point level: at most 43) run the
+  // one-lane fill; the wave-shared one pays its synchronisation only on the
+  // long Galerkin rows (512^3, level 0: 0.89 vs 4.3 s; level 1: 6.9 vs 1.6 s).
+  const bool serial_fill = bmax <= 64;
+  DBuf<int> keys(serial_fill ? 1 : (size_t)n);  // per-row table keys (the wave-shared fill's two launches)
   constexpr int pcount = 1;  // the wave-parallel count (one lane a row: level-1 ext+i count 1.7 s against 0.3 at 512^3)
   if (pcount)
-    hipLaunchKernelGGL(k_extpi_count_w, dim3(grid), dim3(64), (size_t)cap * 8, 0, dS, dcf.p, n, cap, lg, cnt.p);
+    hipLaunchKernelGGL(k_extpi_count_w, dim3(grid), dim3(64), (size_t)cap * 8, 0, dS, dcf.p, n, cap, lg, cnt.p,
+                       serial_fill ? nullptr : keys.p);
   else
     hipLaunchKernelGGL((k_extpi<false>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
                        nullptr, nullptr, nullptr);
@@ -1110,16 +1139,29 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
   DBuf<double> Pa((size_t)t);
   Pi.up(hp);
   // the count buffer keeps -1 on overflow rows: the fill pass skips them.
-  // Rows with few candidates (the finest 7-point level: at most 43) run the
-  // one-lane fill; the wave-shared one pays its synchronisation only on the
-  // long Galerkin rows (512^3, level 0: 0.89 vs 4.3 s; level 1: 6.9 vs 1.6 s).
-  const bool serial_fill = bmax <= 64;
-  if (serial_fill)
+  if (serial_fill) {
     hipLaunchKernelGGL((k_extpi<true>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
                        Pi.p, Pj.p, Pa.p);
-  else
-    hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), lds + 64 * (sizeof(double) + sizeof(int)), 0, dA.view(),
-                       dS, dcf.p, df2c.p, n, cap, lg, cnt.p, Pi.p, Pj.p, Pa.p);
+  } else {
+    // The wave-shared fill in two launches: rows of at most 128 table keys
+    // with a 256-slot table (5 KiB of LDS a wave: 32 waves a CU), the rest
+    // with the full one (up to 33 KiB: 4 waves a CU), so the many short rows
+    // do not run at the long rows' occupancy; the same entries either way.
+    // (knob 19: the small table's log2 size, tests: both launches populated)
+    const int lgs = knob(19) > 0 ? std::min(knob(19), 8) : 8, caps = 1 << lgs;
+    const int ks = std::min(caps / 2, cap / 2);
+    const size_t ldss = (size_t)3 * caps * sizeof(int) + (size_t)(caps / 2) * sizeof(double);
+    const size_t extra = 64 * (sizeof(double) + sizeof(int));
+    if (cap > caps) {
+      hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), ldss + extra, 0, dA.view(), dS, dcf.p, df2c.p, n, caps,
+                         lgs, cnt.p, Pi.p, Pj.p, Pa.p, keys.p, -1, ks);
+      hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), lds + extra, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg,
+                         cnt.p, Pi.p, Pj.p, Pa.p, keys.p, ks, 0x7fffffff);
+    } else {
+      hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), lds + extra, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg,
+                         cnt.p, Pi.p, Pj.p, Pa.p, nullptr, 0, 0);
+    }
+  }
   SDV(hipGetLastError());
   T.lap("extpi fill kernel");
   const bool trunc = trunc_factor != 0.0 || max_elmts > 0;
@@ -1248,15 +1290,15 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   const size_t lds = (size_t)3 * (cap1 + cap2) * sizeof(int) + (size_t)(cap1 / 2) * (sizeof(int) + sizeof(double)) +
                      (size_t)(cap2 / 2) * sizeof(double);
   const DCsr dR{Ri.p, Rj.p, Ra.p, nc};
-  DBuf<int> len((size_t)nc);
+  DBuf<int> len((size_t)nc), nra((size_t)nc);  // C row lengths, RA keys a row
   const int grid = grid_rows(nc, 32);
   constexpr int pcount = 1;  // the wave-parallel count
   if (pcount)
     hipLaunchKernelGGL(k_rap_count_w, dim3(grid), dim3(64), (size_t)(cap1 + cap2) * 8 + (size_t)(cap1 / 2) * 4, 0, dR,
-                       dA.view(), dP.view(), cap1, lg1, cap2, lg2, len.p);
+                       dA.view(), dP.view(), cap1, lg1, cap2, lg2, len.p, nra.p);
   else
     hipLaunchKernelGGL((k_rap<false>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
-                       len.p, nullptr, nullptr, nullptr);
+                       len.p, nullptr, nullptr, nullptr, nullptr, 0, 0, 0);
   SDV(hipGetLastError());
   T.lap("rap count kernel");
   std::vector<int> hl;
@@ -1276,8 +1318,23 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   DBuf<int> Ci, Cj((size_t)ci[nc]);
   DBuf<double> Ca((size_t)ci[nc]);
   Ci.up(ci);
-  hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
-                     len.p, Ci.p, Cj.p, Ca.p);
+  // two launches: rows of at most 128 RA keys and 128 C keys with 256-slot
+  // tables (8.5 KiB of LDS a wave), the rest with the full ones, so the short
+  // rows run at a higher occupancy; the same entries either way
+  const int lgs = knob(19) > 0 ? std::min(knob(19), 8) : 8, caps = 1 << lgs;  // knob 19 as in dev_extpi_interp
+  if (cap1 > caps || cap2 > caps) {
+    const int c1 = std::min(cap1, caps), c2 = std::min(cap2, caps);
+    const int l1 = std::min(lg1, lgs), l2 = std::min(lg2, lgs);
+    const size_t ldss = (size_t)3 * (c1 + c2) * sizeof(int) + (size_t)(c1 / 2) * (sizeof(int) + sizeof(double)) +
+                        (size_t)(c2 / 2) * sizeof(double);
+    hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), ldss, 0, dR, dA.view(), dP.view(), c1, l1, c2, l2, len.p,
+                       Ci.p, Cj.p, Ca.p, nra.p, 1, c1 / 2, c2 / 2);
+    hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
+                       len.p, Ci.p, Cj.p, Ca.p, nra.p, 2, c1 / 2, c2 / 2);
+  } else {
+    hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
+                       len.p, Ci.p, Cj.p, Ca.p, nullptr, 0, 0, 0);
+  }
   SDV(hipGetLastError());
   T.lap("rap fill kernel");
   C.resize_rows(nc, nc);

@@ -453,7 +453,8 @@ HYPRE_Int hypreve_BenchOperator(HYPRE_ParCSRMatrix A, HYPRE_Int op, HYPRE_Int po
  * the GS scatter pass after the sweep, 14 = 16 (setup) 16-lane GS ring slots
  * for the wide operators, 15 (setup) the smallest level the device strength
  * and PMIS take, 16 the GS sweeps' LDS pad a workgroup in KiB (-1: none), 17
- * extra LDS a workgroup of the dictionary loops in KiB.  Ids 0-31.  Results
+ * extra LDS a workgroup of the dictionary loops in KiB, 19 (setup) the log2
+ * size of the small tables of the ext+i and RAP fills.  Ids 0-31.  Results
  * are unchanged, except knob 11's, which gs_schedule_self_check must
  * refuse. */
 HYPRE_Int hypreve_SetKnob(HYPRE_Int id, HYPRE_Int value);

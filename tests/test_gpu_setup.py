@@ -113,6 +113,30 @@ def test_device_strength_pmis_matches_host(gpu, gen, dims, extra):
     A.destroy()
 
 
+@pytest.mark.parametrize("lgs", [3, 5])
+def test_device_setup_two_table_sizes(gpu, lgs):
+    """The wave-shared ext+i fill and the RAP fill run the rows that fit a
+    small table in one launch and the rest with the full table in another;
+    with the small table at 2^3 / 2^5 slots (knob 19) both launches get rows
+    on every Galerkin level, and every level still equals the host setup."""
+    hv = gpu
+    A = hv.ParCSRMatrix.laplacian27(20, 18, 16)
+    kw = hv.ij_amg_defaults(0)
+    kw.update(coarsen_type=8, interp_type=6, P_max_elmts=4, relax_type=18)
+    host = hv.BoomerAMG(**kw)
+    host.setup_host(A)
+    hv.set_knob(19, lgs)
+    try:
+        dev = hv.BoomerAMG(**kw)
+        dev.setup(A)
+    finally:
+        hv.set_knob(19, 0)
+    _same(_hier(hv, dev), _hier(hv, host))
+    for s in (dev, host):
+        s.destroy()
+    A.destroy()
+
+
 @pytest.mark.parametrize("lgcap", [5, 6])
 def test_device_setup_host_rows(gpu, lgcap):
     """Tables capped at 32 / 64 slots (knob 7): the interpolation and Galerkin
