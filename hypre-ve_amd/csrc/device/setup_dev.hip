@@ -784,13 +784,14 @@ __global__ void __launch_bounds__(256) k_transpose_fill(int64_t nnz, const int* 
 // doubles) + map2 (3 x cap2) + the row's values (cap2/2 doubles).
 // ---------------------------------------------------------------------------
 template <bool FILL>
-// mode 1: only the rows with at most lim1 RA keys (rownra) and lim2 C keys
-// (their length), mode 2: only the others, 0: every row (dev_rap's two
-// table sizes)
+// mode t > 0: only the rows of tier t, where tier 1 holds at most lim1a RA
+// keys (rownra) and lim2a C keys (their length), tier 2 at most lim1b /
+// lim2b, tier 3 the rest; mode 0: every row (dev_rap's table sizes)
 __global__ void __launch_bounds__(64) k_rap(DCsr R, DCsr A, DCsr P, int cap1, int lg1, int cap2, int lg2,
                                             int* __restrict__ rowlen, const int* __restrict__ Ci,
                                             int* __restrict__ Cj, double* __restrict__ Ca,
-                                            const int* __restrict__ rownra, int mode, int lim1, int lim2) {
+                                            const int* __restrict__ rownra, int mode, int lim1a, int lim2a,
+                                            int lim1b, int lim2b) {
   extern __shared__ int lds[];
   int* m1 = lds;
   int* m2 = m1 + 3 * cap1;
@@ -806,8 +807,9 @@ __global__ void __launch_bounds__(64) k_rap(DCsr R, DCsr A, DCsr P, int cap1, in
   for (int q = blockIdx.x; q < R.n; q += gridDim.x) {
     if (FILL && rowlen[q] < 0) continue;  // finished on the host
     if (FILL && mode) {
-      const bool small = rownra[q] <= lim1 && rowlen[q] <= lim2;
-      if (small != (mode == 1)) continue;  // the other launch's row
+      const int na = rownra[q], nl = rowlen[q];
+      const int tier = (na <= lim1a && nl <= lim2a) ? 1 : (na <= lim1b && nl <= lim2b) ? 2 : 3;
+      if (tier != mode) continue;  // another launch's row
     }
     M1.begin();
     int nra = 0;
@@ -1143,20 +1145,24 @@ void dev_extpi_interp(const CSR& A, const Pattern& S, const std::vector<int>& cf
     hipLaunchKernelGGL((k_extpi<true>), dim3(grid), dim3(64), lds, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg, cnt.p,
                        Pi.p, Pj.p, Pa.p);
   } else {
-    // The wave-shared fill in two launches: rows of at most 128 table keys
-    // with a 256-slot table (5 KiB of LDS a wave: 32 waves a CU), the rest
-    // with the full one (up to 33 KiB: 4 waves a CU), so the many short rows
-    // do not run at the long rows' occupancy; the same entries either way.
-    // (knob 19: the small table's log2 size, tests: both launches populated)
-    const int lgs = knob(19) > 0 ? std::min(knob(19), 8) : 8, caps = 1 << lgs;
-    const int ks = std::min(caps / 2, cap / 2);
-    const size_t ldss = (size_t)3 * caps * sizeof(int) + (size_t)(caps / 2) * sizeof(double);
+    // The wave-shared fill in tiers of table sizes: rows of at most 128
+    // table keys with a 256-slot table (5 KiB of LDS a wave: 32 waves a CU),
+    // at most 256 with 512 slots (9 KiB), the rest with the full table (up to
+    // 33 KiB: 4 waves a CU), so the many shorter rows do not run at the long
+    // rows' occupancy; the same entries in every tier.
+    // (knob 19: the small table's log2 size, tests: every tier populated)
+    const int lgs = knob(19) > 0 ? std::min(knob(19), 8) : 8;
     const size_t extra = 64 * (sizeof(double) + sizeof(int));
-    if (cap > caps) {
-      hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), ldss + extra, 0, dA.view(), dS, dcf.p, df2c.p, n, caps,
-                         lgs, cnt.p, Pi.p, Pj.p, Pa.p, keys.p, -1, ks);
-      hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), lds + extra, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg,
-                         cnt.p, Pi.p, Pj.p, Pa.p, keys.p, ks, 0x7fffffff);
+    auto ldsz = [](int c) { return (size_t)3 * c * sizeof(int) + (size_t)(c / 2) * sizeof(double); };
+    if (cap > (1 << lgs)) {
+      int lo = -1;
+      for (int lt = lgs; lt <= lg; ++lt) {
+        const int c = 1 << lt, hi = lt == lg ? 0x7fffffff : c / 2;
+        hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), ldsz(c) + extra, 0, dA.view(), dS, dcf.p, df2c.p, n,
+                           c, lt, cnt.p, Pi.p, Pj.p, Pa.p, keys.p, lo, hi);
+        lo = hi;
+        if (lt == lgs + 1 && lt < lg) lt = lg - 1;  // three tiers: small, twice small, full
+      }
     } else {
       hipLaunchKernelGGL(k_extpi_fill_w, dim3(grid), dim3(64), lds + extra, 0, dA.view(), dS, dcf.p, df2c.p, n, cap, lg,
                          cnt.p, Pi.p, Pj.p, Pa.p, nullptr, 0, 0);
@@ -1298,7 +1304,7 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
                        dA.view(), dP.view(), cap1, lg1, cap2, lg2, len.p, nra.p);
   else
     hipLaunchKernelGGL((k_rap<false>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
-                       len.p, nullptr, nullptr, nullptr, nullptr, 0, 0, 0);
+                       len.p, nullptr, nullptr, nullptr, nullptr, 0, 0, 0, 0, 0);
   SDV(hipGetLastError());
   T.lap("rap count kernel");
   std::vector<int> hl;
@@ -1318,22 +1324,29 @@ void dev_rap(const CSR& P, const CSR& A, CSR& Rh, CSR& C) {
   DBuf<int> Ci, Cj((size_t)ci[nc]);
   DBuf<double> Ca((size_t)ci[nc]);
   Ci.up(ci);
-  // two launches: rows of at most 128 RA keys and 128 C keys with 256-slot
-  // tables (8.5 KiB of LDS a wave), the rest with the full ones, so the short
-  // rows run at a higher occupancy; the same entries either way
-  const int lgs = knob(19) > 0 ? std::min(knob(19), 8) : 8, caps = 1 << lgs;  // knob 19 as in dev_extpi_interp
-  if (cap1 > caps || cap2 > caps) {
-    const int c1 = std::min(cap1, caps), c2 = std::min(cap2, caps);
-    const int l1 = std::min(lg1, lgs), l2 = std::min(lg2, lgs);
-    const size_t ldss = (size_t)3 * (c1 + c2) * sizeof(int) + (size_t)(c1 / 2) * (sizeof(int) + sizeof(double)) +
-                        (size_t)(c2 / 2) * sizeof(double);
-    hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), ldss, 0, dR, dA.view(), dP.view(), c1, l1, c2, l2, len.p,
-                       Ci.p, Cj.p, Ca.p, nra.p, 1, c1 / 2, c2 / 2);
-    hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
-                       len.p, Ci.p, Cj.p, Ca.p, nra.p, 2, c1 / 2, c2 / 2);
+  // Tiers of table sizes: rows of at most 128 RA keys and 128 C keys with
+  // 256-slot tables (8.5 KiB of LDS a wave), rows of at most 256 / 256 with
+  // 512-slot ones (17 KiB), the rest with the full ones (26 KiB at 1024 /
+  // 512), so the shorter rows run at a higher occupancy; the same entries in
+  // every tier
+  const int lgs = knob(19) > 0 ? std::min(knob(19), 8) : 8;  // knob 19 as in dev_extpi_interp
+  auto ldsz = [](int c1, int c2) {
+    return (size_t)3 * (c1 + c2) * sizeof(int) + (size_t)(c1 / 2) * (sizeof(int) + sizeof(double)) +
+           (size_t)(c2 / 2) * sizeof(double);
+  };
+  const int ca1 = std::min(cap1, 1 << lgs), ca2 = std::min(cap2, 1 << lgs);
+  const int cb1 = std::min(cap1, 2 << lgs), cb2 = std::min(cap2, 2 << lgs);
+  if (cap1 > ca1 || cap2 > ca2) {
+    const int la1 = std::min(lg1, lgs), la2 = std::min(lg2, lgs), lb1 = std::min(lg1, lgs + 1),
+              lb2 = std::min(lg2, lgs + 1);
+    const int tiers[3][4] = {{ca1, la1, ca2, la2}, {cb1, lb1, cb2, lb2}, {cap1, lg1, cap2, lg2}};
+    for (int t = 0; t < 3; ++t)
+      hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), ldsz(tiers[t][0], tiers[t][2]), 0, dR, dA.view(),
+                         dP.view(), tiers[t][0], tiers[t][1], tiers[t][2], tiers[t][3], len.p, Ci.p, Cj.p, Ca.p,
+                         nra.p, t + 1, ca1 / 2, ca2 / 2, cb1 / 2, cb2 / 2);
   } else {
     hipLaunchKernelGGL((k_rap<true>), dim3(grid), dim3(64), lds, 0, dR, dA.view(), dP.view(), cap1, lg1, cap2, lg2,
-                       len.p, Ci.p, Cj.p, Ca.p, nullptr, 0, 0, 0);
+                       len.p, Ci.p, Cj.p, Ca.p, nullptr, 0, 0, 0, 0, 0);
   }
   SDV(hipGetLastError());
   T.lap("rap fill kernel");
