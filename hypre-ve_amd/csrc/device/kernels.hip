@@ -2946,7 +2946,9 @@ hipError_t launch_sell(int op, const SellView& M, const double* x, const double*
     a.vbits = M.vbits;
     a.anc = M.anc;
     a.cmap = M.cmap;
-    const int wpc = knob(2) > 0 ? knob(2) : 8;  // persistent workgroups per CU
+    // persistent workgroups per CU: 16 (R_0 at 512^3 1.443 -> 1.403 ms against
+    // 8, P_0 the same; 12 / 20: 1.419 / 1.412; profiles/r06/33_wpc)
+    const int wpc = knob(2) > 0 ? knob(2) : 16;
     const dim3 cgrid(std::min(a.nblocks_pad, 256 * wpc));
     const size_t lds = (size_t)M.nvtab * sizeof(double) + (size_t)M.notab * sizeof(int);
     const bool map = M.cmap != nullptr;
